@@ -1,0 +1,386 @@
+// Memory-bound NN building blocks (NHWC bf16, leading client-group dim), all vectorised to
+// 16-byte accesses and grid-strided (cdna_hip_programming.md Guideline 11/13).
+//
+//   ddl_prep_images   : device-resident dataset gather (uint8 HWC) + normalise + optional stem
+//                       im2col into a 32-channel NHWC bf16 tensor (fuses the first conv's im2col
+//                       into the data loader so the stem runs as a K=32 GEMM on MFMA)
+//   ddl_nchw_to_nhwc  : fp32 NCHW -> NHWC bf16 (channel-padded) for the torch-compatible API
+//   ddl_maxpool2_*    : 2x2/2 max pool fwd + bwd (argmax recomputed, first-max like torch)
+//   ddl_avgpool_*     : global average pool fwd + bwd
+//   ddl_dropout       : Philox counter-based dropout, mask recomputed in backward
+//   ddl_act_*         : relu / leaky-relu fwd + masked bwd
+//   ddl_channel_sum   : per-channel sum (bias grads), fp32 atomics into the flat grad buffer
+//   ddl_cast_*        : fp32 <-> bf16
+//
+// Reference parity: F.relu / F.max_pool2d / nn.Dropout / torch.flatten of MnistCnn
+// (reference lab/tutorial_1a/hfl_complete.py:50-62) and transforms.Normalize (:19-24).
+#include "ddl_common.h"
+
+static int grid_for(long long work, int block) {
+  long long b = (work + block - 1) / block;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+#define GSTRIDE_LOOP(t, total) \
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < (total); \
+       t += (long long)gridDim.x * blockDim.x)
+
+// ---------------------------------------------------------------------------------------------
+// src: uint8 [num_samples][Hs][Ws][Cs]; idx: int32 [G*B] sample ids (row-major over g,b)
+// im2col=0: out [G*B][Hs][Ws][Cout], channel c<Cs normalised, c>=Cs zero
+// im2col=1: out [G*B][Ho][Wo][Cout] with Ho=Hs+2pad-2, channel j=(r*3+s)*Cs+c (<9*Cs), rest 0
+__global__ void prep_images_kernel(const uint8_t* __restrict__ src, const int* __restrict__ idx,
+                                   const float* __restrict__ mean, const float* __restrict__ inv_std,
+                                   bf16_t* __restrict__ out, int nimg, int Hs, int Ws, int Cs,
+                                   int Ho, int Wo, int Cout, int im2col, int pad) {
+  const long long total = (long long)nimg * Ho * Wo * (Cout / 8);
+  GSTRIDE_LOOP(t, total) {
+    const int cchunk = (int)(t % (Cout / 8));
+    long long pix = t / (Cout / 8);
+    const int w = (int)(pix % Wo);
+    pix /= Wo;
+    const int h = (int)(pix % Ho);
+    const int b = (int)(pix / Ho);
+    const long long sbase = (long long)idx[b] * Hs * Ws * Cs;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int ch = cchunk * 8 + k;
+      float val = 0.f;
+      if (!im2col) {
+        if (ch < Cs) val = ((float)src[sbase + ((long long)h * Ws + w) * Cs + ch] * (1.f / 255.f) - mean[ch]) * inv_std[ch];
+      } else if (ch < 9 * Cs) {
+        const int tap = ch / Cs, c = ch - tap * Cs;
+        const int r = tap / 3, s = tap - r * 3;
+        const int ih = h - pad + r, iw = w - pad + s;
+        if ((unsigned)ih < (unsigned)Hs && (unsigned)iw < (unsigned)Ws)
+          val = ((float)src[sbase + ((long long)ih * Ws + iw) * Cs + c] * (1.f / 255.f) - mean[c]) * inv_std[c];
+        // zero padding happens in normalised space (matches conv zero-padding)
+      }
+      v[k] = val;
+    }
+    *(i4v*)(out + t * 8) = pack8(v);
+  }
+}
+
+DDL_API int ddl_prep_images(const void* src, const int* idx, const float* mean, const float* inv_std,
+                            void* out, int nimg, int Hs, int Ws, int Cs, int Cout, int im2col,
+                            int pad, hipStream_t s) {
+  if (Cout % 8) return (int)hipErrorInvalidValue;
+  if (im2col && 9 * Cs > Cout) return (int)hipErrorInvalidValue;
+  const int Ho = im2col ? Hs + 2 * pad - 2 : Hs, Wo = im2col ? Ws + 2 * pad - 2 : Ws;
+  const long long total = (long long)nimg * Ho * Wo * (Cout / 8);
+  hipLaunchKernelGGL(prep_images_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s,
+                     (const uint8_t*)src, idx, mean, inv_std, (bf16_t*)out, nimg, Hs, Ws, Cs, Ho, Wo,
+                     Cout, im2col, pad);
+  return (int)hipGetLastError();
+}
+
+// fp32 NCHW (already normalised) -> NHWC bf16, optionally im2col 3x3 (same rules as above)
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, bf16_t* __restrict__ out, int N,
+                                    int Cs, int Hs, int Ws, int Ho, int Wo, int Cout, int im2col,
+                                    int pad) {
+  const long long total = (long long)N * Ho * Wo * (Cout / 8);
+  GSTRIDE_LOOP(t, total) {
+    const int cchunk = (int)(t % (Cout / 8));
+    long long pix = t / (Cout / 8);
+    const int w = (int)(pix % Wo);
+    pix /= Wo;
+    const int h = (int)(pix % Ho);
+    const int n = (int)(pix / Ho);
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int ch = cchunk * 8 + k;
+      float val = 0.f;
+      if (!im2col) {
+        if (ch < Cs) val = x[(((long long)n * Cs + ch) * Hs + h) * Ws + w];
+      } else if (ch < 9 * Cs) {
+        const int tap = ch / Cs, c = ch - tap * Cs;
+        const int r = tap / 3, s = tap - r * 3;
+        const int ih = h - pad + r, iw = w - pad + s;
+        if ((unsigned)ih < (unsigned)Hs && (unsigned)iw < (unsigned)Ws)
+          val = x[(((long long)n * Cs + c) * Hs + ih) * Ws + iw];
+      }
+      v[k] = val;
+    }
+    *(i4v*)(out + t * 8) = pack8(v);
+  }
+}
+
+DDL_API int ddl_nchw_to_nhwc(const float* x, void* out, int N, int Cs, int Hs, int Ws, int Cout,
+                             int im2col, int pad, hipStream_t s) {
+  if (Cout % 8) return (int)hipErrorInvalidValue;
+  if (im2col && 9 * Cs > Cout) return (int)hipErrorInvalidValue;
+  const int Ho = im2col ? Hs + 2 * pad - 2 : Hs, Wo = im2col ? Ws + 2 * pad - 2 : Ws;
+  const long long total = (long long)N * Ho * Wo * (Cout / 8);
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s, x,
+                     (bf16_t*)out, N, Cs, Hs, Ws, Ho, Wo, Cout, im2col, pad);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// 2x2 stride-2 max pool over NHWC (NB = G*N images)
+__global__ void maxpool2_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int NB,
+                                    int H, int W, int C) {
+  const int Ho = H / 2, Wo = W / 2, CC = C / 8;
+  const long long total = (long long)NB * Ho * Wo * CC;
+  GSTRIDE_LOOP(t, total) {
+    const int cc = (int)(t % CC);
+    long long p = t / CC;
+    const int wo = (int)(p % Wo);
+    p /= Wo;
+    const int ho = (int)(p % Ho);
+    const int n = (int)(p / Ho);
+    const bf16_t* b = x + (((long long)n * H + 2 * ho) * W + 2 * wo) * C + cc * 8;
+    float m[8], v[8];
+    unpack8(*(const i4v*)b, m);
+    unpack8(*(const i4v*)(b + C), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m[k] = (v[k] > m[k] || v[k] != v[k]) ? v[k] : m[k];
+    unpack8(*(const i4v*)(b + (long long)W * C), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m[k] = (v[k] > m[k] || v[k] != v[k]) ? v[k] : m[k];
+    unpack8(*(const i4v*)(b + (long long)W * C + C), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m[k] = (v[k] > m[k] || v[k] != v[k]) ? v[k] : m[k];
+    *(i4v*)(y + t * 8) = pack8(m);
+  }
+}
+
+__global__ void maxpool2_bwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                                    bf16_t* __restrict__ dx, int NB, int H, int W, int C) {
+  const int Ho = H / 2, Wo = W / 2, CC = C / 8;
+  const long long total = (long long)NB * Ho * Wo * CC;
+  GSTRIDE_LOOP(t, total) {
+    const int cc = (int)(t % CC);
+    long long p = t / CC;
+    const int wo = (int)(p % Wo);
+    p /= Wo;
+    const int ho = (int)(p % Ho);
+    const int n = (int)(p / Ho);
+    const long long o00 = (((long long)n * H + 2 * ho) * W + 2 * wo) * C + cc * 8;
+    const long long offs[4] = {o00, o00 + C, o00 + (long long)W * C, o00 + (long long)W * C + C};
+    float v[4][8], d[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) unpack8(*(const i4v*)(x + offs[j]), v[j]);
+    unpack8(*(const i4v*)(dy + t * 8), d);
+    float out[4][8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      int am = 0;
+      float m = v[0][k];
+#pragma unroll
+      for (int j = 1; j < 4; ++j)
+        if (v[j][k] > m || v[j][k] != v[j][k]) { m = v[j][k]; am = j; }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out[j][k] = (j == am) ? d[k] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *(i4v*)(dx + offs[j]) = pack8(out[j]);
+  }
+}
+
+DDL_API int ddl_maxpool2_fwd(const void* x, void* y, int NB, int H, int W, int C, hipStream_t s) {
+  if (C % 8 || H % 2 || W % 2) return (int)hipErrorInvalidValue;
+  const long long total = (long long)NB * (H / 2) * (W / 2) * (C / 8);
+  hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s,
+                     (const bf16_t*)x, (bf16_t*)y, NB, H, W, C);
+  return (int)hipGetLastError();
+}
+DDL_API int ddl_maxpool2_bwd(const void* x, const void* dy, void* dx, int NB, int H, int W, int C,
+                             hipStream_t s) {
+  if (C % 8 || H % 2 || W % 2) return (int)hipErrorInvalidValue;
+  const long long total = (long long)NB * (H / 2) * (W / 2) * (C / 8);
+  hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s,
+                     (const bf16_t*)x, (const bf16_t*)dy, (bf16_t*)dx, NB, H, W, C);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// global average pool: x [NB][HW][C] -> y [NB][C]; one thread per (image, 8-channel chunk)
+__global__ void avgpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int NB,
+                                   int HW, int C) {
+  const int CC = C / 8;
+  const long long total = (long long)NB * CC;
+  GSTRIDE_LOOP(t, total) {
+    const int cc = (int)(t % CC);
+    const long long n = t / CC;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int p = 0; p < HW; ++p) {
+      float v[8];
+      unpack8(*(const i4v*)(x + (n * HW + p) * C + cc * 8), v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += v[k];
+    }
+    const float inv = 1.f / HW;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] *= inv;
+    *(i4v*)(y + n * C + cc * 8) = pack8(acc);
+  }
+}
+__global__ void avgpool_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int NB,
+                                   int HW, int C) {
+  const int CC = C / 8;
+  const long long total = (long long)NB * HW * CC;
+  const float inv = 1.f / HW;
+  GSTRIDE_LOOP(t, total) {
+    const int cc = (int)(t % CC);
+    const long long n = t / CC / HW;
+    float v[8];
+    unpack8(*(const i4v*)(dy + n * C + cc * 8), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] *= inv;
+    *(i4v*)(dx + t * 8) = pack8(v);
+  }
+}
+DDL_API int ddl_avgpool_fwd(const void* x, void* y, int NB, int HW, int C, hipStream_t s) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(grid_for((long long)NB * C / 8, 256)), dim3(256), 0,
+                     s, (const bf16_t*)x, (bf16_t*)y, NB, HW, C);
+  return (int)hipGetLastError();
+}
+DDL_API int ddl_avgpool_bwd(const void* dy, void* dx, int NB, int HW, int C, hipStream_t s) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for((long long)NB * HW * C / 8, 256)), dim3(256),
+                     0, s, (const bf16_t*)dy, (bf16_t*)dx, NB, HW, C);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// dropout: keep iff philox(seed, element/4)[element%4] >= p ; scale 1/(1-p). Mask recomputed.
+__global__ void dropout_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n,
+                               float p, unsigned long long seed, unsigned long long offset) {
+  const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+  GSTRIDE_LOOP(t, n / 8) {
+    float v[8];
+    unpack8(*(const i4v*)(x + t * 8), v);
+    const unsigned long long ctr0 = offset + (unsigned long long)t * 2;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const unsigned long long c = ctr0 + h;
+      const uint4 r = philox4x32(make_uint4((uint32_t)c, (uint32_t)(c >> 32), 0x5bd1e995u, 0), key);
+      const uint32_t rr[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[h * 4 + k] = (u32_to_unit(rr[k]) > p) ? v[h * 4 + k] * scale : 0.f;
+    }
+    *(i4v*)(y + t * 8) = pack8(v);
+  }
+}
+DDL_API int ddl_dropout(const void* x, void* y, long long n, float p, unsigned long long seed,
+                        unsigned long long offset, hipStream_t s) {
+  if (n % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n / 8, 256)), dim3(256), 0, s, (const bf16_t*)x,
+                     (bf16_t*)y, n, p, seed, offset);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// act fwd: 1 relu, 2 leaky(slope); act bwd: dx = dy * act'(y) (y = fwd output; sign preserved)
+__global__ void act_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n,
+                               int act, float slope) {
+  GSTRIDE_LOOP(t, n / 8) {
+    float v[8];
+    unpack8(*(const i4v*)(x + t * 8), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : (act == 2 ? slope * v[k] : 0.f);
+    *(i4v*)(y + t * 8) = pack8(v);
+  }
+}
+__global__ void act_bwd_kernel(const bf16_t* __restrict__ y, const bf16_t* __restrict__ dy,
+                               bf16_t* __restrict__ dx, long long n, int act, float slope) {
+  GSTRIDE_LOOP(t, n / 8) {
+    float v[8], d[8];
+    unpack8(*(const i4v*)(y + t * 8), v);
+    unpack8(*(const i4v*)(dy + t * 8), d);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = v[k] > 0.f ? d[k] : (act == 2 ? slope * d[k] : 0.f);
+    *(i4v*)(dx + t * 8) = pack8(d);
+  }
+}
+DDL_API int ddl_act_fwd(const void* x, void* y, long long n, int act, float slope, hipStream_t s) {
+  if (n % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(act_fwd_kernel, dim3(grid_for(n / 8, 256)), dim3(256), 0, s, (const bf16_t*)x,
+                     (bf16_t*)y, n, act, slope);
+  return (int)hipGetLastError();
+}
+DDL_API int ddl_act_bwd(const void* y, const void* dy, void* dx, long long n, int act, float slope,
+                        hipStream_t s) {
+  if (n % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(act_bwd_kernel, dim3(grid_for(n / 8, 256)), dim3(256), 0, s, (const bf16_t*)y,
+                     (const bf16_t*)dy, (bf16_t*)dx, n, act, slope);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// per-channel sum of x [G][M][C] bf16 -> out [G] (+g*gs) fp32 accumulate
+__global__ __launch_bounds__(256) void channel_sum_kernel(const bf16_t* __restrict__ x,
+                                                          float* __restrict__ out, long long gs,
+                                                          long long M, int C) {
+  __shared__ float red[256 * 9];
+  const int g = blockIdx.y;
+  const int TPR = C / 8, RPI = 256 / TPR;
+  const int tid = threadIdx.x, cc = tid % TPR, row = tid / TPR;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (row < RPI) {
+    for (long long p = (long long)blockIdx.x * RPI + row; p < M; p += (long long)gridDim.x * RPI) {
+      float v[8];
+      unpack8(*(const i4v*)(x + ((long long)g * M + p) * C + cc * 8), v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[k] += v[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[tid * 9 + k] = s[k];
+  __syncthreads();
+  if (tid < TPR) {
+    float t8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int r = 0; r < RPI; ++r)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t8[k] += red[(r * TPR + tid) * 9 + k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) atomicAdd(out + (long long)g * gs + tid * 8 + k, t8[k]);
+  }
+}
+DDL_API int ddl_channel_sum(const void* x, float* out, long long gs, long long M, int C, int G,
+                            hipStream_t s) {
+  if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
+  const int RPI = 256 / (C / 8);
+  long long blocks = (M + (long long)RPI * 16 - 1) / ((long long)RPI * 16);
+  if (blocks > 512) blocks = 512;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(channel_sum_kernel, dim3((unsigned)blocks, G), dim3(256), 0, s,
+                     (const bf16_t*)x, out, gs, M, C);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long long n) {
+  GSTRIDE_LOOP(t, (n + 3) / 4) {
+    const long long e = t * 4;
+    if (e + 4 <= n) {
+      const float4 v = *(const float4*)(x + e);
+      i2v o;
+      o[0] = (int)pack_bf2(v.x, v.y);
+      o[1] = (int)pack_bf2(v.z, v.w);
+      *(i2v*)(y + e) = o;
+    } else {
+      for (long long k = e; k < n; ++k) y[k] = f2bf(x[k]);
+    }
+  }
+}
+__global__ void cast_bf16_f32_kernel(const bf16_t* __restrict__ x, float* __restrict__ y, long long n) {
+  GSTRIDE_LOOP(t, n) y[t] = bf2f(x[t]);
+}
+DDL_API int ddl_cast_f32_bf16(const float* x, void* y, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for((n + 3) / 4, 256)), dim3(256), 0, s, x,
+                     (bf16_t*)y, n);
+  return (int)hipGetLastError();
+}
+DDL_API int ddl_cast_bf16_f32(const void* x, float* y, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, (const bf16_t*)x,
+                     y, n);
+  return (int)hipGetLastError();
+}

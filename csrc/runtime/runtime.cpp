@@ -1,0 +1,273 @@
+// Host-side native runtime for ddl25spring_amd (g++, no GPU dependency), loaded through ctypes.
+//
+//  1. Pipeline schedule IR: builds per-stage action lists for the naive / GPipe / 1F1B schedules
+//     (reference lab/tutorial_1b/PP/1F1B/intro_PP_1F1B.py, intro_PP_1F1B_MB.py,
+//     intro_PP_1F1B_MP.py) and *verifies* them by simulating RCCL point-to-point semantics
+//     (blocking rendezvous, FIFO matching per directed pair, grouped send/recv completing
+//     together). The reference's 1F1B attempt deadlocks at iteration 0
+//     (lab/Abgabe/outputs/out_MP0.txt:11); schedules emitted here are checked deadlock-free and
+//     microbatch-consistent before any rank runs them.
+//  2. Epoch planner: per-client shuffled mini-batch index plans for the device-resident data
+//     loader (replaces the per-client DataLoader(shuffle=True, generator) of
+//     hfl_complete.py:146-151 with one int32 table uploaded once per round).
+//  3. Gradient bucket planner for the overlapped data-parallel all-reduce.
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <tuple>
+#include <vector>
+
+#define API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+enum Op : int32_t { FWD = 0, BWD = 1, SEND_ACT = 2, RECV_ACT = 3, SEND_GRAD = 4, RECV_GRAD = 5 };
+
+struct Action {
+  int32_t stage, op, mb, peer, group;  // group: actions with the same (stage, group>=0) are posted together
+};
+
+struct Builder {
+  std::vector<Action> out;
+  int next_group = 0;
+  void add(int s, int op, int mb, int peer, int group = -1) { out.push_back({s, op, mb, peer, group}); }
+};
+
+// naive / GPipe: all forwards (recv act -> fwd -> send act) then all backwards
+void build_gpipe(Builder& b, int S, int M) {
+  for (int s = 0; s < S; ++s) {
+    for (int m = 0; m < M; ++m) {
+      if (s > 0) b.add(s, RECV_ACT, m, s - 1);
+      b.add(s, FWD, m, -1);
+      if (s < S - 1) b.add(s, SEND_ACT, m, s + 1);
+    }
+    for (int m = 0; m < M; ++m) {
+      if (s < S - 1) b.add(s, RECV_GRAD, m, s + 1);
+      b.add(s, BWD, m, -1);
+      if (s > 0) b.add(s, SEND_GRAD, m, s - 1);
+    }
+  }
+}
+
+// 1F1B (PipeDream-Flush / DAPPLE): warmup forwards, steady F/B alternation, cooldown backwards.
+// In the steady state a stage's "send activation of mb i" and "receive gradient of mb j" are posted
+// as ONE group (like Megatron's send_forward_recv_backward), and symmetrically
+// "send gradient" + "receive activation": this is what removes the ordering deadlock.
+void build_1f1b(Builder& b, int S, int M) {
+  for (int s = 0; s < S; ++s) {
+    const int warm = std::min(S - s - 1, M);
+    const int steady = M - warm;
+    int f = 0, bw = 0;
+    // warmup
+    for (int i = 0; i < warm; ++i) {
+      if (s > 0) b.add(s, RECV_ACT, f, s - 1);
+      b.add(s, FWD, f, -1);
+      if (s < S - 1) b.add(s, SEND_ACT, f, s + 1);
+      ++f;
+    }
+    if (steady > 0 && s > 0) b.add(s, RECV_ACT, f, s - 1);
+    for (int i = 0; i < steady; ++i) {
+      b.add(s, FWD, f, -1);
+      // send act(f) + recv grad(bw) grouped
+      const int g1 = b.next_group++;
+      if (s < S - 1) {
+        b.add(s, SEND_ACT, f, s + 1, g1);
+        b.add(s, RECV_GRAD, bw, s + 1, g1);
+      }
+      ++f;
+      b.add(s, BWD, bw, -1);
+      // send grad(bw) + recv act(next f) grouped
+      const int g2 = b.next_group++;
+      const bool last = (i == steady - 1);
+      if (s > 0) {
+        b.add(s, SEND_GRAD, bw, s - 1, g2);
+        if (!last) b.add(s, RECV_ACT, f, s - 1, g2);
+      }
+      ++bw;
+    }
+    // cooldown
+    for (int i = 0; i < warm; ++i) {
+      if (s < S - 1) b.add(s, RECV_GRAD, bw, s + 1);
+      b.add(s, BWD, bw, -1);
+      if (s > 0) b.add(s, SEND_GRAD, bw, s - 1);
+      ++bw;
+    }
+  }
+}
+
+bool is_send(int op) { return op == SEND_ACT || op == SEND_GRAD; }
+bool is_comm(int op) { return op >= SEND_ACT; }
+int expected_recv(int send_op) { return send_op == SEND_ACT ? RECV_ACT : RECV_GRAD; }
+
+}  // namespace
+
+// kind: 0 naive (== gpipe with M micro-batches, M usually 1), 1 gpipe, 2 1f1b
+// out: int32[cap][5] (stage, op, mb, peer, group); returns #actions or -needed if cap too small
+API int ddl_sched_build(int kind, int n_stages, int n_micro, int32_t* out, int cap) {
+  if (n_stages < 1 || n_micro < 1) return 0;
+  Builder b;
+  if (kind == 2) build_1f1b(b, n_stages, n_micro);
+  else build_gpipe(b, n_stages, kind == 0 ? n_micro : n_micro);
+  // stable order by stage so each stage's program is contiguous
+  std::stable_sort(b.out.begin(), b.out.end(),
+                   [](const Action& x, const Action& y) { return x.stage < y.stage; });
+  const int n = (int)b.out.size();
+  if (n > cap) return -n;
+  for (int i = 0; i < n; ++i) {
+    out[5 * i + 0] = b.out[i].stage;
+    out[5 * i + 1] = b.out[i].op;
+    out[5 * i + 2] = b.out[i].mb;
+    out[5 * i + 3] = b.out[i].peer;
+    out[5 * i + 4] = b.out[i].group;
+  }
+  return n;
+}
+
+// Simulates the schedule. Returns 0 if every stage runs to completion with FIFO-consistent
+// matching; 1 + index of the first action of a blocked stage on deadlock; -(1+index) of the
+// receive whose FIFO-matched send carries a different (op, micro-batch) (silent data mix-up);
+// -1000000 on malformed input. Also checks every FWD precedes the BWD of the same micro-batch.
+API int ddl_sched_verify(const int32_t* acts, int n, int n_stages) {
+  std::vector<std::vector<int>> prog(n_stages);
+  for (int i = 0; i < n; ++i) {
+    const int s = acts[5 * i];
+    if (s < 0 || s >= n_stages) return -1000000;
+    prog[s].push_back(i);
+  }
+  // per-stage compute-order sanity
+  for (int s = 0; s < n_stages; ++s) {
+    std::map<int, int> fwd_done;
+    for (int i : prog[s]) {
+      const int op = acts[5 * i + 1], mb = acts[5 * i + 2];
+      if (op == FWD) fwd_done[mb] = 1;
+      if (op == BWD && !fwd_done.count(mb)) return 1 + i;
+    }
+  }
+  std::vector<size_t> pc(n_stages, 0);
+  // posted-but-unmatched sends / recvs per directed pair (src,dst), FIFO by issue order
+  std::map<std::pair<int, int>, std::deque<int>> sends, recvs;
+  std::vector<char> posted(n, 0), matched(n, 0);
+  auto try_match = [&](std::pair<int, int> key) -> int {
+    auto& sq = sends[key];
+    auto& rq = recvs[key];
+    while (!sq.empty() && !rq.empty()) {
+      const int si = sq.front(), ri = rq.front();
+      sq.pop_front();
+      rq.pop_front();
+      if (acts[5 * ri + 1] != expected_recv(acts[5 * si + 1]) || acts[5 * ri + 2] != acts[5 * si + 2])
+        return -(1 + ri);
+      matched[si] = matched[ri] = 1;
+    }
+    return 0;
+  };
+  bool progress = true;
+  while (progress) {
+    progress = false;
+    for (int s = 0; s < n_stages; ++s) {
+      while (pc[s] < prog[s].size()) {
+        const int i = prog[s][pc[s]];
+        const int op = acts[5 * i + 1];
+        if (!is_comm(op)) {
+          ++pc[s];
+          progress = true;
+          continue;
+        }
+        // collect the group [pc, end)
+        size_t end = pc[s] + 1;
+        const int grp = acts[5 * i + 4];
+        if (grp >= 0)
+          while (end < prog[s].size() && acts[5 * prog[s][end] + 4] == grp) ++end;
+        for (size_t k = pc[s]; k < end; ++k) {
+          const int j = prog[s][k];
+          if (posted[j]) continue;
+          posted[j] = 1;
+          progress = true;
+          const int peer = acts[5 * j + 3];
+          if (peer < 0 || peer >= n_stages) return -1000000;
+          if (is_send(acts[5 * j + 1])) {
+            auto key = std::make_pair(s, peer);
+            sends[key].push_back(j);
+            if (int e = try_match(key)) return e;
+          } else {
+            auto key = std::make_pair(peer, s);
+            recvs[key].push_back(j);
+            if (int e = try_match(key)) return e;
+          }
+        }
+        bool all = true;
+        for (size_t k = pc[s]; k < end; ++k) all = all && matched[prog[s][k]];
+        if (!all) break;
+        pc[s] = end;
+        progress = true;
+      }
+    }
+  }
+  for (int s = 0; s < n_stages; ++s)
+    if (pc[s] < prog[s].size()) return 1 + prog[s][pc[s]];
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+namespace {
+struct SplitMix {
+  uint64_t s;
+  uint64_t next() {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ULL);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+  }
+  uint64_t below(uint64_t n) {  // unbiased
+    uint64_t lim = UINT64_MAX - UINT64_MAX % n;
+    uint64_t v;
+    do v = next(); while (v >= lim);
+    return v % n;
+  }
+};
+}  // namespace
+
+// Per-client shuffled batch plan. idx: concatenation of the G clients' sample-id lists, each of
+// length `count` (equal sizes: the client-batched engine groups clients by size). Output int32
+// [steps][G][batch] with steps = ceil(count/batch) (last step's tail padded with -1), one
+// Fisher-Yates shuffle per client seeded with seeds[g]. Returns steps.
+API int ddl_plan_epoch(const int32_t* idx, int G, int count, int batch, const uint64_t* seeds,
+                       int shuffle, int32_t* out) {
+  if (G <= 0 || count <= 0 || batch <= 0) return 0;
+  const int steps = (count + batch - 1) / batch;
+  std::vector<int32_t> perm(count);
+  for (int g = 0; g < G; ++g) {
+    std::memcpy(perm.data(), idx + (size_t)g * count, sizeof(int32_t) * count);
+    if (shuffle) {
+      SplitMix rng{seeds[g]};
+      for (int i = count - 1; i > 0; --i) std::swap(perm[i], perm[rng.below((uint64_t)i + 1)]);
+    }
+    for (int st = 0; st < steps; ++st)
+      for (int b = 0; b < batch; ++b) {
+        const int k = st * batch + b;
+        out[((size_t)st * G + g) * batch + b] = k < count ? perm[k] : -1;
+      }
+  }
+  return steps;
+}
+
+// Greedy gradient buckets in gradient-ready order (reverse of parameter order): consecutive
+// tensors are packed until `cap_bytes`; a tensor larger than the cap gets its own bucket.
+// sizes: element counts in *ready* order; out: bucket id per tensor. Returns #buckets.
+API int ddl_bucket_plan(const int64_t* sizes, int n, int64_t cap_bytes, int elem_bytes, int32_t* out) {
+  int bucket = 0;
+  int64_t fill = 0;
+  for (int i = 0; i < n; ++i) {
+    const int64_t b = sizes[i] * elem_bytes;
+    if (fill > 0 && fill + b > cap_bytes) {
+      ++bucket;
+      fill = 0;
+    }
+    out[i] = bucket;
+    fill += b;
+  }
+  return n ? bucket + 1 : 0;
+}
+
+API int ddl_runtime_version() { return 1; }

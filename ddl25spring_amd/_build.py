@@ -1,0 +1,120 @@
+"""Native build for ddl25spring_amd: hipcc (gfx950) for the HIP kernels, g++ for the host runtime.
+
+No torch.utils.cpp_extension / hipify step is involved: the kernels are plain HIP C++ with an
+``extern "C"`` ABI (loaded through ctypes by :mod:`ddl25spring_amd.ops._lib`), built in-tree so the
+``.so`` files travel with the repository snapshot to the GPU box.
+
+    python -m ddl25spring_amd._build            # incremental
+    python -m ddl25spring_amd._build --clean    # from scratch
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "csrc"
+PKG = ROOT / "ddl25spring_amd"
+LIBDIR = PKG / "lib"
+OBJDIR = ROOT / "build" / "obj"
+ARCH = os.environ.get("DDL_OFFLOAD_ARCH", "gfx950")
+
+KERNEL_LIB = LIBDIR / "libddl_kernels.so"
+RUNTIME_LIB = LIBDIR / "libddl_runtime.so"
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build ddl25spring_amd kernels)")
+
+
+def _newest(paths) -> float:
+    return max((p.stat().st_mtime for p in paths), default=0.0)
+
+
+def _run(cmd: list[str]) -> None:
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        sys.stderr.write(res.stdout + res.stderr)
+        raise RuntimeError(f"build command failed: {' '.join(cmd[:6])} ...")
+
+
+def _jobs() -> int:
+    env = os.environ.get("MAX_JOBS")
+    if env and env.isdigit():
+        return max(1, min(16, int(env)))
+    return max(1, min(16, os.cpu_count() or 4))
+
+
+def build_kernels(force: bool = False, verbose: bool = False) -> Path:
+    srcs = sorted((CSRC / "kernels").glob("*.hip"))
+    headers = list((CSRC / "include").glob("*.h"))
+    hdr_time = _newest(headers)
+    OBJDIR.mkdir(parents=True, exist_ok=True)
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    hipcc = _hipcc()
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", f"-I{CSRC / 'include'}",
+             "-Wno-unused-result", "-Wno-unused-value", "-munsafe-fp-atomics"]
+
+    def compile_one(src: Path) -> Path:
+        obj = OBJDIR / (src.stem + ".o")
+        if force or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, hdr_time):
+            if verbose:
+                print(f"[build] hipcc {src.name}", flush=True)
+            _run([hipcc, *flags, "-c", str(src), "-o", str(obj)])
+        return obj
+
+    with ThreadPoolExecutor(_jobs()) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    if force or not KERNEL_LIB.exists() or KERNEL_LIB.stat().st_mtime < _newest(objs):
+        if verbose:
+            print(f"[build] link {KERNEL_LIB.name}", flush=True)
+        tmp = KERNEL_LIB.with_suffix(".so.tmp")
+        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)])
+        os.replace(tmp, KERNEL_LIB)
+    return KERNEL_LIB
+
+
+def build_runtime(force: bool = False, verbose: bool = False) -> Path:
+    srcs = sorted((CSRC / "runtime").glob("*.cpp"))
+    headers = list((CSRC / "runtime").glob("*.h"))
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    if not srcs:
+        return RUNTIME_LIB
+    newest = _newest([*srcs, *headers])
+    if force or not RUNTIME_LIB.exists() or RUNTIME_LIB.stat().st_mtime < newest:
+        cxx = os.environ.get("CXX", shutil.which("g++") or "g++")
+        if verbose:
+            print(f"[build] {Path(cxx).name} {RUNTIME_LIB.name}", flush=True)
+        tmp = RUNTIME_LIB.with_suffix(".so.tmp")
+        _run([cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall",
+              *map(str, srcs), "-o", str(tmp)])
+        os.replace(tmp, RUNTIME_LIB)
+    return RUNTIME_LIB
+
+
+def build_all(force: bool = False, verbose: bool = False) -> None:
+    build_runtime(force, verbose)
+    build_kernels(force, verbose)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clean", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    args = ap.parse_args()
+    if args.clean:
+        shutil.rmtree(OBJDIR, ignore_errors=True)
+    build_all(force=args.clean, verbose=True)
+    print(f"[build] ok: {KERNEL_LIB} {RUNTIME_LIB}")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,197 @@
+"""ctypes bindings to the in-tree native libraries.
+
+``libddl_kernels.so`` holds every HIP/CDNA4 kernel of the framework (built by
+:mod:`ddl25spring_amd._build` with ``hipcc --offload-arch=gfx950``); ``libddl_runtime.so`` the
+host-side C++ runtime (schedules, epoch planner, bucket planner).
+
+Policy: on a machine with a GPU the HIP library is *required* — every op raises if it is missing
+or fails to load, there is no silent fallback to PyTorch kernels. CPU tensors (unit tests, the
+gloo-only configs) go through the pure-PyTorch reference implementations in
+:mod:`ddl25spring_amd.ops.reference`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch
+
+LIBDIR = Path(__file__).resolve().parent.parent / "lib"
+KERNEL_LIB_PATH = LIBDIR / "libddl_kernels.so"
+RUNTIME_LIB_PATH = LIBDIR / "libddl_runtime.so"
+
+_kernels = None
+_runtime = None
+
+vp = ctypes.c_void_p
+i32 = ctypes.c_int
+i64 = ctypes.c_longlong
+u64 = ctypes.c_ulonglong
+f32 = ctypes.c_float
+fp = ctypes.POINTER(ctypes.c_float)
+
+
+class ConvArgs(ctypes.Structure):
+    _fields_ = [("x", vp), ("w", vp), ("dy", vp), ("out", vp), ("stats", vp), ("bias", vp),
+                ("residual", vp), ("mask", vp),
+                ("x_gs", i64), ("w_gs", i64), ("dy_gs", i64), ("out_gs", i64), ("bias_gs", i64),
+                ("stats_gs", i64),
+                ("G", i32), ("N", i32), ("H", i32), ("W", i32), ("C", i32), ("K", i32), ("R", i32),
+                ("S", i32), ("P", i32), ("Q", i32), ("stride", i32), ("pad", i32),
+                ("relu", i32), ("accumulate", i32), ("split_k", i32), ("reserved", i32)]
+
+
+class BNArgs(ctypes.Structure):
+    _fields_ = [("stats", vp), ("gamma", vp), ("beta", vp), ("running_mean", vp),
+                ("running_var", vp), ("scale", vp), ("shift", vp), ("mean", vp), ("rstd", vp),
+                ("gs_param", i64), ("gs_buf", i64), ("G", i32), ("C", i32), ("count", i64),
+                ("eps", f32), ("momentum", f32), ("training", i32), ("reserved", i32)]
+
+
+class SGDArgs(ctypes.Structure):
+    _fields_ = [("p", vp), ("g", vp), ("mom", vp), ("shadow", vp), ("n", i64), ("lr", f32),
+                ("wd", f32), ("momentum", f32), ("dampening", f32), ("grad_scale", f32),
+                ("nesterov", i32), ("first_step", i32)]
+
+
+class AdamArgs(ctypes.Structure):
+    _fields_ = [("p", vp), ("g", vp), ("m", vp), ("v", vp), ("shadow", vp), ("n", i64),
+                ("lr", f32), ("beta1", f32), ("beta2", f32), ("eps", f32), ("wd", f32),
+                ("grad_scale", f32), ("bc1", f32), ("bc2", f32), ("decoupled", i32),
+                ("amsgrad_unused", i32)]
+
+
+_SIGS = {
+    # conv_igemm.hip
+    "ddl_conv_fwd": [ctypes.POINTER(ConvArgs), i32, vp],
+    "ddl_conv_dgrad": [ctypes.POINTER(ConvArgs), i32, vp],
+    "ddl_conv_wgrad": [ctypes.POINTER(ConvArgs), i32, vp],
+    # batchnorm.hip
+    "ddl_bn_finalize": [ctypes.POINTER(BNArgs), vp],
+    "ddl_bn_apply": [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, vp],
+    "ddl_bn_bwd_reduce": [vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i32, i32, vp],
+    "ddl_bn_bwd_apply": [vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, i64, i32, i32, vp],
+    # nn_ops.hip
+    "ddl_prep_images": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp],
+    "ddl_nchw_to_nhwc": [vp, vp, i32, i32, i32, i32, i32, i32, i32, vp],
+    "ddl_maxpool2_fwd": [vp, vp, i32, i32, i32, i32, vp],
+    "ddl_maxpool2_bwd": [vp, vp, vp, i32, i32, i32, i32, vp],
+    "ddl_avgpool_fwd": [vp, vp, i32, i32, i32, vp],
+    "ddl_avgpool_bwd": [vp, vp, i32, i32, i32, vp],
+    "ddl_dropout": [vp, vp, i64, f32, u64, u64, vp],
+    "ddl_act_fwd": [vp, vp, i64, i32, f32, vp],
+    "ddl_act_bwd": [vp, vp, vp, i64, i32, f32, vp],
+    "ddl_channel_sum": [vp, vp, i64, i64, i32, i32, vp],
+    "ddl_cast_f32_bf16": [vp, vp, i64, vp],
+    "ddl_cast_bf16_f32": [vp, vp, i64, vp],
+    # loss.hip
+    "ddl_ce_fwd_bwd": [vp, vp, vp, i32, i32, i32, i32, f32, vp, vp, vp, vp],
+    "ddl_ce_vocab": [vp, vp, i32, i32, i32, f32, i32, vp, vp, vp],
+    "ddl_mse_kl": [vp, vp, i64, vp, vp, i64, f32, f32, vp, vp, vp, vp, vp],
+    # optim.hip
+    "ddl_sgd": [ctypes.POINTER(SGDArgs), vp],
+    "ddl_adam": [ctypes.POINTER(AdamArgs), vp],
+    # aggregate.hip
+    "ddl_weighted_sum": [vp, i64, vp, i32, i64, vp, i32, vp],
+    "ddl_broadcast_rows": [vp, vp, i64, i32, i64, vp, i64, vp],
+    "ddl_gram_f32": [vp, i64, vp, i32, i64, vp, vp],
+    "ddl_coord_select": [vp, i64, i32, i64, i32, i32, vp, vp],
+}
+
+_OPTIONAL_SIGS: dict[str, list] = {}
+
+
+def register_signatures(sigs: dict[str, list]) -> None:
+    """Other op modules (llama kernels, ...) add their launchers here."""
+    _OPTIONAL_SIGS.update(sigs)
+    if _kernels is not None:
+        _declare(_kernels, sigs)
+
+
+def _declare(lib, sigs) -> None:
+    for name, argt in sigs.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.argtypes = argt
+        fn.restype = ctypes.c_int
+
+
+def kernels_available() -> bool:
+    return KERNEL_LIB_PATH.exists()
+
+
+def kernels():
+    """The loaded HIP kernel library (raises if it is missing: no silent fallback)."""
+    global _kernels
+    if _kernels is None:
+        if not KERNEL_LIB_PATH.exists():
+            raise RuntimeError(
+                f"{KERNEL_LIB_PATH} is missing: build it with `python -m ddl25spring_amd._build` "
+                "(hipcc --offload-arch=gfx950)")
+        _ = torch.cuda.is_available()  # make sure torch's HIP runtime is the one we bind to
+        lib = ctypes.CDLL(str(KERNEL_LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+        _declare(lib, _SIGS)
+        _declare(lib, _OPTIONAL_SIGS)
+        for name, size_fn, cls in (("ConvArgs", "ddl_conv_args_size", ConvArgs),
+                                   ("BNArgs", "ddl_bn_args_size", BNArgs),
+                                   ("SGDArgs", "ddl_sgd_args_size", SGDArgs),
+                                   ("AdamArgs", "ddl_adam_args_size", AdamArgs)):
+            f = getattr(lib, size_fn)
+            f.restype = ctypes.c_int
+            if f() != ctypes.sizeof(cls):
+                raise RuntimeError(f"ABI mismatch for {name}: C {f()} vs ctypes {ctypes.sizeof(cls)}")
+        _kernels = lib
+    return _kernels
+
+
+def runtime():
+    """The host C++ runtime library (schedules / planners)."""
+    global _runtime
+    if _runtime is None:
+        if not RUNTIME_LIB_PATH.exists():
+            from .. import _build
+            _build.build_runtime()
+        lib = ctypes.CDLL(str(RUNTIME_LIB_PATH))
+        p32 = ctypes.POINTER(ctypes.c_int32)
+        lib.ddl_sched_build.argtypes = [i32, i32, i32, p32, i32]
+        lib.ddl_sched_verify.argtypes = [p32, i32, i32]
+        lib.ddl_plan_epoch.argtypes = [p32, i32, i32, i32, ctypes.POINTER(ctypes.c_uint64), i32, p32]
+        lib.ddl_bucket_plan.argtypes = [ctypes.POINTER(ctypes.c_int64), i32, ctypes.c_int64, i32, p32]
+        for f in ("ddl_sched_build", "ddl_sched_verify", "ddl_plan_epoch", "ddl_bucket_plan"):
+            getattr(lib, f).restype = ctypes.c_int
+        _runtime = lib
+    return _runtime
+
+
+class KernelError(RuntimeError):
+    pass
+
+
+def check(rc: int, name: str) -> None:
+    if rc != 0:
+        raise KernelError(f"{name} failed with hipError {rc}")
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def loaded_library_paths() -> list[str]:
+    """For diagnostics: which in-tree native libraries this process has mapped."""
+    out = []
+    try:
+        with open(f"/proc/{os.getpid()}/maps") as f:
+            for line in f:
+                if str(LIBDIR) in line:
+                    p = line.split()[-1]
+                    if p not in out:
+                        out.append(p)
+    except OSError:
+        pass
+    return out

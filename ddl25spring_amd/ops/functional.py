@@ -1,0 +1,401 @@
+"""Tensor-level op API over the HIP kernels (device tensors) and the PyTorch reference (CPU).
+
+Layout contract (see csrc/include/ddl_common.h):
+  * activations: bf16, NHWC, leading client-group dim  ``[G, N, H, W, C]`` (or ``[G, N, C]``)
+  * weights: bf16 shadow views ``[G, K, R, S, C]`` whose group stride may be the flat-buffer
+    stride (inner dims contiguous)
+  * grads / master params / optimizer state: fp32 views of the same flat buffers
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from . import reference as ref
+from ._lib import check, ptr, stream
+
+
+@dataclass(frozen=True)
+class ConvGeom:
+    G: int
+    N: int
+    H: int
+    W: int
+    C: int
+    K: int
+    R: int = 3
+    S: int = 3
+    stride: int = 1
+    pad: int = 0
+
+    @property
+    def P(self) -> int:
+        return (self.H + 2 * self.pad - self.R) // self.stride + 1
+
+    @property
+    def Q(self) -> int:
+        return (self.W + 2 * self.pad - self.S) // self.stride + 1
+
+    def flops(self) -> int:
+        return 2 * self.G * self.N * self.P * self.Q * self.K * self.R * self.S * self.C
+
+
+def _gs(t: torch.Tensor | None) -> int:
+    return 0 if t is None else t.stride(0)
+
+
+def _conv_args(geom: ConvGeom, **kw) -> _lib.ConvArgs:
+    a = _lib.ConvArgs()
+    for k, v in kw.items():
+        setattr(a, k, v)
+    a.G, a.N, a.H, a.W, a.C, a.K = geom.G, geom.N, geom.H, geom.W, geom.C, geom.K
+    a.R, a.S, a.P, a.Q, a.stride, a.pad = geom.R, geom.S, geom.P, geom.Q, geom.stride, geom.pad
+    return a
+
+
+def _check_inner(t: torch.Tensor, name: str) -> None:
+    inner = t[0] if t.dim() > 1 else t
+    if not inner.is_contiguous():
+        raise ValueError(f"{name}: per-group inner dims must be contiguous")
+
+
+def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out=None, cfg=0):
+    """y[G,N,P,Q,K] = conv(x[G,N,H,W,C], w[G,K,R,S,C]) (+bias)(relu); stats[G,2,K] += sum, sumsq."""
+    if not x.is_cuda:
+        y = ref.conv_fwd(x, w, geom, bias, relu, stats)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    _check_inner(x, "x"); _check_inner(w, "w")
+    y = out if out is not None else torch.empty(geom.G, geom.N, geom.P, geom.Q, geom.K,
+                                                dtype=torch.bfloat16, device=x.device)
+    a = _conv_args(geom, x=ptr(x), w=ptr(w), out=ptr(y), stats=ptr(stats), bias=ptr(bias),
+                   x_gs=_gs(x), w_gs=_gs(w), out_gs=_gs(y), bias_gs=_gs(bias),
+                   stats_gs=0 if stats is None else stats.stride(0), relu=int(relu))
+    check(_lib.kernels().ddl_conv_fwd(ctypes.byref(a), cfg, stream()), "conv_fwd")
+    return y
+
+
+def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0):
+    """dx[G,N,H,W,C] = conv_transpose(dy, w) (+residual) * (mask > 0)."""
+    if not dy.is_cuda:
+        dx = ref.conv_dgrad(dy, w, geom, residual, mask)
+        if out is not None:
+            out.copy_(dx)
+            return out
+        return dx
+    _check_inner(dy, "dy"); _check_inner(w, "w")
+    dx = out if out is not None else torch.empty(geom.G, geom.N, geom.H, geom.W, geom.C,
+                                                 dtype=torch.bfloat16, device=dy.device)
+    if residual is not None and residual.stride(0) != dx.stride(0):
+        residual = residual.contiguous()
+    if mask is not None and mask.stride(0) != dx.stride(0):
+        mask = mask.contiguous()
+    a = _conv_args(geom, w=ptr(w), dy=ptr(dy), out=ptr(dx), residual=ptr(residual),
+                   mask=ptr(mask), w_gs=_gs(w), dy_gs=_gs(dy), out_gs=_gs(dx))
+    check(_lib.kernels().ddl_conv_dgrad(ctypes.byref(a), cfg, stream()), "conv_dgrad")
+    return dx
+
+
+def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0):
+    """dw[G,K,R,S,C] (+)= sum over pixels dy (x) x  — fp32, split-K with atomics."""
+    if not dy.is_cuda:
+        ref.conv_wgrad(dy, x, geom, dw, accumulate)
+        return dw
+    _check_inner(dy, "dy"); _check_inner(x, "x"); _check_inner(dw, "dw")
+    a = _conv_args(geom, x=ptr(x), dy=ptr(dy), out=ptr(dw), x_gs=_gs(x), dy_gs=_gs(dy),
+                   out_gs=_gs(dw), accumulate=int(accumulate))
+    if not accumulate:
+        cfg = (cfg & 0x00FFFFFF) | (1 << 24)  # force a single split (plain stores)
+    check(_lib.kernels().ddl_conv_wgrad(ctypes.byref(a), cfg, stream()), "conv_wgrad")
+    return dw
+
+
+# ------------------------------------------------------------------------------------- BN
+def bn_finalize(stats, gamma, beta, running_mean, running_var, count, eps=1e-5, momentum=0.1,
+                training=True):
+    """-> (scale, shift, mean, rstd), each [G, C] fp32 contiguous."""
+    if not stats.is_cuda:
+        return ref.bn_finalize(stats, gamma, beta, running_mean, running_var, count, eps, momentum,
+                               training)
+    G, C = stats.shape[0], stats.shape[-1]
+    outs = torch.empty(4, G, C, dtype=torch.float32, device=stats.device)
+    a = _lib.BNArgs()
+    a.stats, a.gamma, a.beta = ptr(stats), ptr(gamma), ptr(beta)
+    a.running_mean, a.running_var = ptr(running_mean), ptr(running_var)
+    a.scale, a.shift, a.mean, a.rstd = (ptr(outs[i]) for i in range(4))
+    a.gs_param = _gs(gamma) if gamma is not None else _gs(beta)
+    a.gs_buf = _gs(running_mean)
+    a.G, a.C, a.count = G, C, int(count)
+    a.eps, a.momentum, a.training = float(eps), float(momentum), int(training)
+    check(_lib.kernels().ddl_bn_finalize(ctypes.byref(a), stream()), "bn_finalize")
+    return outs[0], outs[1], outs[2], outs[3]
+
+
+def bn_apply(x, scale, shift, r=None, rscale=None, rshift=None, act=0, out=None):
+    if not x.is_cuda:
+        y = ref.bn_apply(x, scale, shift, r, rscale, rshift, act)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    assert x.is_contiguous() and (r is None or r.is_contiguous())
+    y = out if out is not None else torch.empty_like(x)
+    G, C = x.shape[0], x.shape[-1]
+    check(_lib.kernels().ddl_bn_apply(ptr(x), ptr(scale), ptr(shift), ptr(r), ptr(rscale),
+                                      ptr(rshift), ptr(y), x[0].numel(), C, G, act, stream()),
+          "bn_apply")
+    return y
+
+
+def bn_bwd_reduce(dy, ymask, x, mean, rstd, dgamma=None, dbeta=None):
+    """-> sums [G, 2, C] = (sum dy_m, sum dy_m*xhat); also accumulates into dgamma/dbeta views."""
+    if not dy.is_cuda:
+        return ref.bn_bwd_reduce(dy, ymask, x, mean, rstd, dgamma, dbeta)
+    G, C = x.shape[0], x.shape[-1]
+    sums = torch.zeros(G, 2, C, dtype=torch.float32, device=x.device)
+    gs = _gs(dgamma) if dgamma is not None else _gs(dbeta)
+    check(_lib.kernels().ddl_bn_bwd_reduce(ptr(dy), ptr(ymask), ptr(x), ptr(mean), ptr(rstd),
+                                           ptr(sums), ptr(dgamma), ptr(dbeta), gs,
+                                           x[0].numel() // C, C, G, stream()), "bn_bwd_reduce")
+    return sums
+
+
+def bn_bwd_apply(dy, ymask, x, mean, rstd, gamma, sums, emit_dym=False):
+    if not dy.is_cuda:
+        return ref.bn_bwd_apply(dy, ymask, x, mean, rstd, gamma, sums, emit_dym)
+    G, C = x.shape[0], x.shape[-1]
+    dx = torch.empty_like(x)
+    dym = torch.empty_like(x) if emit_dym else None
+    check(_lib.kernels().ddl_bn_bwd_apply(ptr(dy), ptr(ymask), ptr(x), ptr(mean), ptr(rstd),
+                                          ptr(gamma), _gs(gamma), ptr(sums), ptr(dx), ptr(dym),
+                                          x[0].numel() // C, C, G, stream()), "bn_bwd_apply")
+    return (dx, dym) if emit_dym else dx
+
+
+# ----------------------------------------------------------------------------- elementwise
+def maxpool2_fwd(x):
+    if not x.is_cuda:
+        return ref.maxpool2_fwd(x)
+    G, N, H, W, C = x.shape
+    y = torch.empty(G, N, H // 2, W // 2, C, dtype=x.dtype, device=x.device)
+    check(_lib.kernels().ddl_maxpool2_fwd(ptr(x), ptr(y), G * N, H, W, C, stream()), "maxpool2_fwd")
+    return y
+
+
+def maxpool2_bwd(x, dy):
+    if not x.is_cuda:
+        return ref.maxpool2_bwd(x, dy)
+    G, N, H, W, C = x.shape
+    dx = torch.empty_like(x)
+    check(_lib.kernels().ddl_maxpool2_bwd(ptr(x), ptr(dy), ptr(dx), G * N, H, W, C, stream()),
+          "maxpool2_bwd")
+    return dx
+
+
+def avgpool_fwd(x):
+    if not x.is_cuda:
+        return ref.avgpool_fwd(x)
+    G, N, H, W, C = x.shape
+    y = torch.empty(G, N, C, dtype=x.dtype, device=x.device)
+    check(_lib.kernels().ddl_avgpool_fwd(ptr(x), ptr(y), G * N, H * W, C, stream()), "avgpool_fwd")
+    return y
+
+
+def avgpool_bwd(dy, H, W):
+    if not dy.is_cuda:
+        return ref.avgpool_bwd(dy, H, W)
+    G, N, C = dy.shape
+    dx = torch.empty(G, N, H, W, C, dtype=dy.dtype, device=dy.device)
+    check(_lib.kernels().ddl_avgpool_bwd(ptr(dy), ptr(dx), G * N, H * W, C, stream()), "avgpool_bwd")
+    return dx
+
+
+def dropout(x, p, seed, offset):
+    if p <= 0:
+        return x
+    if not x.is_cuda:
+        return ref.dropout(x, p, seed, offset)
+    y = torch.empty_like(x)
+    check(_lib.kernels().ddl_dropout(ptr(x), ptr(y), x.numel(), float(p), int(seed), int(offset),
+                                     stream()), "dropout")
+    return y
+
+
+ACT = {"none": 0, "relu": 1, "leaky_relu": 2}
+
+
+def act_fwd(x, act: int, slope=0.01):
+    if not x.is_cuda:
+        return ref.act_fwd(x, act, slope)
+    y = torch.empty_like(x)
+    check(_lib.kernels().ddl_act_fwd(ptr(x), ptr(y), x.numel(), act, float(slope), stream()), "act_fwd")
+    return y
+
+
+def act_bwd(y, dy, act: int, slope=0.01):
+    if not y.is_cuda:
+        return ref.act_bwd(y, dy, act, slope)
+    dx = torch.empty_like(dy)
+    check(_lib.kernels().ddl_act_bwd(ptr(y), ptr(dy), ptr(dx), y.numel(), act, float(slope),
+                                     stream()), "act_bwd")
+    return dx
+
+
+def channel_sum(x, out):
+    """out[G, C] (view, fp32) += sum over all but first/last dims of x."""
+    if not x.is_cuda:
+        ref.channel_sum(x, out)
+        return out
+    G, C = x.shape[0], x.shape[-1]
+    check(_lib.kernels().ddl_channel_sum(ptr(x), ptr(out), _gs(out), x[0].numel() // C, C, G,
+                                         stream()), "channel_sum")
+    return out
+
+
+def to_bf16(x32: torch.Tensor, out=None):
+    out = out if out is not None else torch.empty(x32.shape, dtype=torch.bfloat16, device=x32.device)
+    if not x32.is_cuda:
+        out.copy_(x32)
+        return out
+    assert x32.is_contiguous() and out.is_contiguous()
+    check(_lib.kernels().ddl_cast_f32_bf16(ptr(x32), ptr(out), x32.numel(), stream()), "cast")
+    return out
+
+
+def nchw_to_nhwc(x: torch.Tensor, cpad: int, im2col: bool = False, pad: int = 0):
+    """fp32 NCHW -> bf16 NHWC [1, N, H', W', cpad] (optionally 3x3 im2col for the stem conv)."""
+    N, C, H, W = x.shape
+    Ho, Wo = (H + 2 * pad - 2, W + 2 * pad - 2) if im2col else (H, W)
+    if not x.is_cuda:
+        xf = x.float()
+        if im2col:
+            cols = torch.nn.functional.unfold(xf, 3, padding=pad)  # [N, C*9, L] ordered (c, r, s)
+            cols = cols.reshape(N, C, 9, Ho * Wo).permute(0, 3, 2, 1).reshape(N, Ho, Wo, 9 * C)
+        else:
+            cols = xf.permute(0, 2, 3, 1)
+        out = torch.zeros(1, N, Ho, Wo, cpad, dtype=torch.bfloat16)
+        out[0, ..., :cols.shape[-1]] = cols.to(torch.bfloat16)
+        return out
+    xc = x.float().contiguous()
+    out = torch.empty(1, N, Ho, Wo, cpad, dtype=torch.bfloat16, device=x.device)
+    check(_lib.kernels().ddl_nchw_to_nhwc(ptr(xc), ptr(out), N, C, H, W, cpad, int(im2col), pad,
+                                          stream()), "nchw_to_nhwc")
+    return out
+
+
+def prep_images(src_u8, idx, mean, inv_std, cpad, im2col=False, pad=0, out=None):
+    """Gather uint8 HWC samples by id, normalise, NHWC bf16 (channel-padded / stem-im2col)."""
+    n = idx.numel()
+    Hs, Ws, Cs = src_u8.shape[1:]
+    Ho, Wo = (Hs + 2 * pad - 2, Ws + 2 * pad - 2) if im2col else (Hs, Ws)
+    if out is None:
+        out = torch.empty(n, Ho, Wo, cpad, dtype=torch.bfloat16, device=src_u8.device)
+    if not src_u8.is_cuda:
+        x = src_u8[idx.long().reshape(-1)].float() / 255.0
+        x = (x - mean) * inv_std
+        x = x.permute(0, 3, 1, 2)
+        out.copy_(nchw_to_nhwc(x, cpad, im2col, pad)[0].reshape(out.shape))
+        return out
+    check(_lib.kernels().ddl_prep_images(ptr(src_u8), ptr(idx), ptr(mean), ptr(inv_std), ptr(out),
+                                         n, Hs, Ws, Cs, cpad, int(im2col), pad, stream()),
+          "prep_images")
+    return out
+
+
+# ------------------------------------------------------------------------------------- loss
+def cross_entropy(logits, labels=None, targets=None, ncls=None, scale=1.0, want_grad=True,
+                  with_correct=False):
+    """Fused softmax-CE over logits [G, N, ld] -> (loss[G] fp32, dlogits bf16|None, correct[G]|None)."""
+    G, N, ld = logits.shape
+    ncls = ncls or ld
+    dev = logits.device
+    loss = torch.zeros(G, dtype=torch.float32, device=dev)
+    correct = torch.zeros(G, dtype=torch.int32, device=dev) if with_correct else None
+    if not logits.is_cuda:
+        d = ref.ce_fwd_bwd(logits, labels, targets, ncls, scale, loss, correct, want_grad)
+        return loss, d, correct
+    d = torch.empty_like(logits) if want_grad else None
+    lab = labels.to(torch.int32).contiguous() if labels is not None else None
+    tgt = targets.float().contiguous() if targets is not None else None
+    check(_lib.kernels().ddl_ce_fwd_bwd(ptr(logits), ptr(lab), ptr(tgt), G * N, N, ncls, ld,
+                                        float(scale), ptr(loss), ptr(d), ptr(correct), stream()),
+          "ce_fwd_bwd")
+    return loss, d, correct
+
+
+# --------------------------------------------------------------------------------- optimizers
+def sgd_step(p, g, mom, shadow, lr, wd=0.0, momentum=0.0, dampening=0.0, nesterov=False,
+             first_step=False, grad_scale=1.0):
+    if not p.is_cuda:
+        ref.sgd(p, g, mom, shadow, lr, wd, momentum, dampening, nesterov, first_step, grad_scale)
+        return
+    a = _lib.SGDArgs()
+    a.p, a.g, a.mom, a.shadow = ptr(p), ptr(g), ptr(mom), ptr(shadow)
+    a.n = p.numel()
+    a.lr, a.wd, a.momentum, a.dampening, a.grad_scale = lr, wd, momentum, dampening, grad_scale
+    a.nesterov, a.first_step = int(nesterov), int(first_step)
+    check(_lib.kernels().ddl_sgd(ctypes.byref(a), stream()), "sgd")
+
+
+def adam_step(p, g, m, v, shadow, lr, beta1, beta2, eps, wd, step, decoupled, grad_scale=1.0):
+    if not p.is_cuda:
+        ref.adam(p, g, m, v, shadow, lr, beta1, beta2, eps, wd, step, decoupled, grad_scale)
+        return
+    a = _lib.AdamArgs()
+    a.p, a.g, a.m, a.v, a.shadow = ptr(p), ptr(g), ptr(m), ptr(v), ptr(shadow)
+    a.n = p.numel()
+    a.lr, a.beta1, a.beta2, a.eps, a.wd, a.grad_scale = lr, beta1, beta2, eps, wd, grad_scale
+    a.bc1, a.bc2 = 1 - beta1 ** step, 1 - beta2 ** step
+    a.decoupled = int(decoupled)
+    check(_lib.kernels().ddl_adam(ctypes.byref(a), stream()), "adam")
+
+
+# ------------------------------------------------------------------------------- aggregation
+def weighted_sum(src, coeff, out, accumulate=False):
+    """out[P] (+)= sum_g coeff[g] * src[g, :P] (src rows may be strided views of a [G, *] buffer)."""
+    if not src.is_cuda:
+        ref.weighted_sum(src, coeff, out, accumulate)
+        return out
+    assert src.stride(1) == 1 and out.is_contiguous()
+    check(_lib.kernels().ddl_weighted_sum(ptr(src), src.stride(0), ptr(coeff.float().contiguous()),
+                                          src.shape[0], out.numel(), ptr(out), int(accumulate),
+                                          stream()), "weighted_sum")
+    return out
+
+
+def broadcast_rows(src, dst, shadow=None):
+    if not src.is_cuda:
+        ref.broadcast_rows(src, dst, shadow)
+        return
+    assert dst.stride(1) == 1
+    check(_lib.kernels().ddl_broadcast_rows(ptr(src), ptr(dst), dst.stride(0), dst.shape[0],
+                                            src.numel(), ptr(shadow),
+                                            0 if shadow is None else shadow.stride(0), stream()),
+          "broadcast_rows")
+
+
+def gram(X, center=None):
+    """(X - c)(X - c)^T for X [K, n] fp32 on the exact-fp32 MFMA (K <= 64)."""
+    if not X.is_cuda:
+        return ref.gram(X, center)
+    K = X.shape[0]
+    out = torch.zeros(K, K, dtype=torch.float32, device=X.device)
+    check(_lib.kernels().ddl_gram_f32(ptr(X), X.stride(0), ptr(center), K, X.shape[1], ptr(out),
+                                      stream()), "gram_f32")
+    return out
+
+
+def coord_select(X, mode: str, trim: int = 0):
+    """Coordinate-wise median ('median') or trimmed mean ('trimmed') over K rows of X [K, n]."""
+    m = 0 if mode == "median" else 1
+    if not X.is_cuda or X.shape[0] > 64:
+        return ref.coord_select(X, m, trim)
+    out = torch.empty(X.shape[1], dtype=torch.float32, device=X.device)
+    check(_lib.kernels().ddl_coord_select(ptr(X), X.stride(0), X.shape[0], X.shape[1], m, trim,
+                                          ptr(out), stream()), "coord_select")
+    return out

@@ -1,0 +1,229 @@
+"""Numerics of every HIP kernel against the plain-PyTorch fp32 reference of the same op."""
+import pytest
+import torch
+
+from ddl25spring_amd.ops import functional as Fn
+from ddl25spring_amd.ops import reference as ref
+from ddl25spring_amd.ops.functional import ConvGeom
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, rel=2e-2, abs_=1e-3):
+    a = a.float().cpu()
+    b = b.float().cpu()
+    scale = b.abs().max().item() + 1e-6
+    err = (a - b).abs().max().item()
+    assert err <= rel * scale + abs_, f"max err {err} vs scale {scale}"
+
+
+def _rand(*shape, dev="cpu", scale=1.0):
+    return (torch.randn(*shape) * scale).to(torch.bfloat16).to(dev)
+
+
+GEOMS = [
+    ConvGeom(G=2, N=3, H=8, W=8, C=32, K=64, R=3, S=3, stride=1, pad=1),
+    ConvGeom(G=1, N=2, H=9, W=9, C=64, K=128, R=3, S=3, stride=2, pad=1),
+    ConvGeom(G=3, N=4, H=4, W=4, C=128, K=64, R=1, S=1, stride=2, pad=0),
+    ConvGeom(G=2, N=37, H=1, W=1, C=96, K=32, R=1, S=1, stride=1, pad=0),
+    ConvGeom(G=1, N=2, H=26, W=26, C=32, K=64, R=3, S=3, stride=1, pad=0),
+    ConvGeom(G=2, N=4, H=8, W=8, C=256, K=256, R=3, S=3, stride=1, pad=1),
+]
+
+
+def _weights(geom, dev, strided=True):
+    # strided group view into a flat [G, P] buffer, like the flat parameter store
+    inner = geom.K * geom.R * geom.S * geom.C
+    pad = 96 if strided else 0
+    flat = _rand(geom.G, inner + pad, dev=dev, scale=0.1)
+    return flat[:, :inner].view(geom.G, geom.K, geom.R, geom.S, geom.C) if not strided else \
+        flat[:, 16:16 + inner].unflatten(1, (geom.K, geom.R, geom.S, geom.C))
+
+
+@pytest.mark.parametrize("geom", GEOMS, ids=lambda g: f"{g.C}x{g.K}_{g.H}_{g.R}s{g.stride}p{g.pad}")
+def test_conv_fwd(cuda, geom):
+    x = _rand(geom.G, geom.N, geom.H, geom.W, geom.C, dev=cuda)
+    w = _weights(geom, cuda)
+    bias = torch.randn(geom.G, geom.K, device=cuda)
+    stats = torch.zeros(geom.G, 2, geom.K, device=cuda)
+    y = Fn.conv_fwd(x, w, geom, stats=stats)
+    stats_ref = torch.zeros(geom.G, 2, geom.K)
+    y_ref = ref.conv_fwd(x.cpu(), w.cpu(), geom, stats=stats_ref)
+    _close(y, y_ref)
+    _close(stats, stats_ref, rel=1e-3)
+    y2 = Fn.conv_fwd(x, w, geom, bias=bias, relu=True)
+    _close(y2, ref.conv_fwd(x.cpu(), w.cpu(), geom, bias=bias.cpu(), relu=True))
+
+
+@pytest.mark.parametrize("geom", GEOMS, ids=lambda g: f"{g.C}x{g.K}_{g.H}_{g.R}s{g.stride}p{g.pad}")
+def test_conv_dgrad(cuda, geom):
+    dy = _rand(geom.G, geom.N, geom.P, geom.Q, geom.K, dev=cuda)
+    w = _weights(geom, cuda)
+    dx = Fn.conv_dgrad(dy, w, geom)
+    _close(dx, ref.conv_dgrad(dy.cpu(), w.cpu(), geom))
+    res = _rand(geom.G, geom.N, geom.H, geom.W, geom.C, dev=cuda)
+    mask = _rand(geom.G, geom.N, geom.H, geom.W, geom.C, dev=cuda)
+    dx2 = Fn.conv_dgrad(dy, w, geom, residual=res, mask=mask)
+    _close(dx2, ref.conv_dgrad(dy.cpu(), w.cpu(), geom, residual=res.cpu(), mask=mask.cpu()))
+
+
+@pytest.mark.parametrize("geom", GEOMS, ids=lambda g: f"{g.C}x{g.K}_{g.H}_{g.R}s{g.stride}p{g.pad}")
+def test_conv_wgrad(cuda, geom):
+    x = _rand(geom.G, geom.N, geom.H, geom.W, geom.C, dev=cuda)
+    dy = _rand(geom.G, geom.N, geom.P, geom.Q, geom.K, dev=cuda)
+    inner = geom.K * geom.R * geom.S * geom.C
+    flat = torch.zeros(geom.G, inner + 64, device=cuda)
+    dw = flat[:, 32:32 + inner].unflatten(1, (geom.K, geom.R, geom.S, geom.C))
+    Fn.conv_wgrad(dy, x, geom, dw, accumulate=True)
+    dw_ref = torch.zeros(geom.G, geom.K, geom.R, geom.S, geom.C)
+    ref.conv_wgrad(dy.cpu(), x.cpu(), geom, dw_ref)
+    _close(dw, dw_ref, rel=2e-3)
+    assert flat[:, :32].abs().max().item() == 0 and flat[:, 32 + inner:].abs().max().item() == 0
+
+
+def test_conv_tile_configs(cuda):
+    geom = ConvGeom(G=2, N=3, H=8, W=8, C=128, K=128, R=3, S=3, stride=1, pad=1)
+    x = _rand(geom.G, geom.N, geom.H, geom.W, geom.C, dev=cuda)
+    w = _weights(geom, cuda)
+    dy = _rand(geom.G, geom.N, geom.P, geom.Q, geom.K, dev=cuda)
+    y_ref = ref.conv_fwd(x.cpu(), w.cpu(), geom)
+    dx_ref = ref.conv_dgrad(dy.cpu(), w.cpu(), geom)
+    dw_ref = torch.zeros(geom.G, geom.K, geom.R, geom.S, geom.C)
+    ref.conv_wgrad(dy.cpu(), x.cpu(), geom, dw_ref)
+    for bp in (64, 128):
+        for bq in (64, 128):
+            for bk in (32, 64):
+                cfg = bp | (bq << 8) | (bk << 16)
+                _close(Fn.conv_fwd(x, w, geom, cfg=cfg), y_ref)
+                _close(Fn.conv_dgrad(dy, w, geom, cfg=cfg), dx_ref)
+                for splits in (1, 3):
+                    dw = torch.zeros(geom.G, geom.K, geom.R, geom.S, geom.C, device=cuda)
+                    Fn.conv_wgrad(dy, x, geom, dw, cfg=cfg | (splits << 24))
+                    _close(dw, dw_ref, rel=2e-3)
+
+
+def test_batchnorm(cuda):
+    G, N, H, W, C = 2, 5, 6, 6, 64
+    x = _rand(G, N, H, W, C, dev=cuda, scale=2.0) + 0.5
+    stats = torch.stack([x.float().reshape(G, -1, C).sum(1), (x.float() ** 2).reshape(G, -1, C).sum(1)], 1)
+    gamma = torch.rand(G, C, device=cuda) + 0.5
+    beta = torch.randn(G, C, device=cuda)
+    rm, rv = torch.zeros(G, C, device=cuda), torch.ones(G, C, device=cuda)
+    rm_r, rv_r = rm.cpu().clone(), rv.cpu().clone()
+    M = N * H * W
+    sc, sh, mu, rs = Fn.bn_finalize(stats, gamma, beta, rm, rv, M)
+    sc_r, sh_r, mu_r, rs_r = ref.bn_finalize(stats.cpu(), gamma.cpu(), beta.cpu(), rm_r, rv_r, M, 1e-5, 0.1, True)
+    _close(sc, sc_r, rel=1e-4); _close(sh, sh_r, rel=1e-4); _close(rm, rm_r, rel=1e-4); _close(rv, rv_r, rel=1e-4)
+    r = _rand(G, N, H, W, C, dev=cuda)
+    for act in (0, 1, 2):
+        _close(Fn.bn_apply(x, sc, sh, r=r, rscale=sc, rshift=sh, act=act),
+               ref.bn_apply(x.cpu(), sc_r, sh_r, r.cpu(), sc_r, sh_r, act))
+    y = Fn.bn_apply(x, sc, sh, act=1)
+    dy = _rand(G, N, H, W, C, dev=cuda)
+    dg = torch.zeros(G, C, device=cuda); db = torch.zeros(G, C, device=cuda)
+    sums = Fn.bn_bwd_reduce(dy, y, x, mu, rs, dg, db)
+    dg_r = torch.zeros(G, C); db_r = torch.zeros(G, C)
+    sums_r = ref.bn_bwd_reduce(dy.cpu(), y.cpu(), x.cpu(), mu_r, rs_r, dg_r, db_r)
+    _close(sums, sums_r, rel=2e-3); _close(dg, dg_r, rel=2e-3); _close(db, db_r, rel=2e-3)
+    dx, dym = Fn.bn_bwd_apply(dy, y, x, mu, rs, gamma, sums, emit_dym=True)
+    dx_r, dym_r = ref.bn_bwd_apply(dy.cpu(), y.cpu(), x.cpu(), mu_r, rs_r, gamma.cpu(), sums_r, True)
+    _close(dx, dx_r); _close(dym, dym_r)
+
+
+def test_pools_act_dropout(cuda):
+    x = _rand(2, 3, 8, 6, 64, dev=cuda)
+    _close(Fn.maxpool2_fwd(x), ref.maxpool2_fwd(x.cpu()), rel=0, abs_=0)
+    dy = _rand(2, 3, 4, 3, 64, dev=cuda)
+    _close(Fn.maxpool2_bwd(x, dy), ref.maxpool2_bwd(x.cpu(), dy.cpu()), rel=0, abs_=0)
+    _close(Fn.avgpool_fwd(x), ref.avgpool_fwd(x.cpu()))
+    d2 = _rand(2, 3, 64, dev=cuda)
+    _close(Fn.avgpool_bwd(d2, 8, 6), ref.avgpool_bwd(d2.cpu(), 8, 6))
+    for act in (1, 2):
+        y = Fn.act_fwd(x, act)
+        _close(y, ref.act_fwd(x.cpu(), act))
+        _close(Fn.act_bwd(y, x, act), ref.act_bwd(y.cpu(), x.cpu(), act))
+    ones = torch.ones(64, 1024, dtype=torch.bfloat16, device=cuda)
+    d = Fn.dropout(ones, 0.25, seed=7, offset=0)
+    keep = (d.float() > 0).float().mean().item()
+    assert abs(keep - 0.75) < 0.01
+    assert torch.allclose(d.float()[d.float() > 0], torch.full_like(d.float()[d.float() > 0], 1 / 0.75), rtol=1e-2)
+    d_again = Fn.dropout(ones, 0.25, seed=7, offset=0)
+    assert torch.equal(d, d_again)
+    out = torch.zeros(2, 64, device=cuda)
+    Fn.channel_sum(x, out)
+    _close(out, x.cpu().float().reshape(2, -1, 64).sum(1), rel=1e-3)
+
+
+def test_cross_entropy(cuda):
+    G, N, ld, ncls = 3, 50, 32, 10
+    logits = _rand(G, N, ld, dev=cuda, scale=3)
+    labels = torch.randint(0, ncls, (G, N), device=cuda)
+    loss, d, corr = Fn.cross_entropy(logits, labels, ncls=ncls, scale=1 / N, with_correct=True)
+    loss_r = torch.zeros(G); corr_r = torch.zeros(G, dtype=torch.int32)
+    d_r = ref.ce_fwd_bwd(logits.cpu(), labels.cpu(), None, ncls, 1 / N, loss_r, corr_r)
+    _close(loss, loss_r, rel=1e-4); _close(d, d_r); assert torch.equal(corr.cpu(), corr_r)
+    # torch oracle
+    lt = torch.stack([torch.nn.functional.cross_entropy(logits[g, :, :ncls].float().cpu(), labels[g].cpu()) for g in range(G)])
+    _close(loss, lt, rel=1e-4)
+    targets = torch.softmax(torch.randn(G, N, ncls), -1).to(cuda)
+    loss2, d2, _ = Fn.cross_entropy(logits, targets=targets, ncls=ncls, scale=1 / N)
+    loss2_r = torch.zeros(G)
+    d2_r = ref.ce_fwd_bwd(logits.cpu(), None, targets.cpu(), ncls, 1 / N, loss2_r)
+    _close(loss2, loss2_r, rel=1e-4); _close(d2, d2_r)
+
+
+def test_optimizers(cuda):
+    n = 1000 * 4 + 3
+    p = torch.randn(n, device=cuda); g = torch.randn(n, device=cuda)
+    for momentum, nest in ((0.0, False), (0.9, False), (0.9, True)):
+        pc, mc = p.cpu().clone(), torch.zeros(n)
+        pg, mg = p.clone(), torch.zeros(n, device=cuda)
+        sh = torch.empty(n, dtype=torch.bfloat16, device=cuda)
+        for step in range(3):
+            Fn.sgd_step(pg, g, mg, sh, 0.1, 1e-4, momentum, 0.0, nest, step == 0)
+            ref.sgd(pc, g.cpu(), mc, None, 0.1, 1e-4, momentum, 0.0, nest, step == 0)
+        _close(pg, pc, rel=1e-5, abs_=1e-6)
+        _close(sh, pc)
+    # adam / adamw vs torch.optim
+    for decoupled in (False, True):
+        w = torch.nn.Parameter(p.cpu().clone())
+        opt = (torch.optim.AdamW if decoupled else torch.optim.Adam)([w], lr=1e-2, weight_decay=0.01)
+        pg = p.clone(); m = torch.zeros(n, device=cuda); v = torch.zeros(n, device=cuda)
+        for step in range(1, 4):
+            w.grad = g.cpu().clone(); opt.step()
+            Fn.adam_step(pg, g, m, v, None, 1e-2, 0.9, 0.999, 1e-8, 0.01, step, decoupled)
+        _close(pg, w.detach(), rel=1e-5, abs_=1e-6)
+
+
+def test_aggregation(cuda):
+    G, P = 5, 12345
+    buf = torch.randn(G, P + 7, device=cuda)
+    src = buf[:, :P]
+    coeff = torch.rand(G, device=cuda)
+    out = torch.empty(P, device=cuda)
+    Fn.weighted_sum(src, coeff, out)
+    _close(out, (coeff.cpu()[:, None] * src.cpu()).sum(0), rel=1e-5)
+    dst = torch.zeros(G, P + 7, device=cuda)
+    sh = torch.zeros(G, P + 7, dtype=torch.bfloat16, device=cuda)
+    Fn.broadcast_rows(out, dst[:, :P], sh[:, :P])
+    assert torch.equal(dst[:, :P], out.expand(G, P)) and dst[:, P:].abs().max() == 0
+    for K in (3, 8, 20, 33, 64):
+        X = torch.randn(K, 20000, device=cuda)
+        c = torch.randn(20000, device=cuda)
+        _close(Fn.gram(X, c), ref.gram(X.cpu().double(), c.cpu().double()).float(), rel=1e-5)
+        for mode, trim in (("median", 0), ("trimmed", K // 4)):
+            if mode == "trimmed" and K - 2 * trim < 1:
+                continue
+            _close(Fn.coord_select(X, mode, trim), ref.coord_select(X.cpu(), 0 if mode == "median" else 1, trim), rel=1e-6)
+
+
+def test_prep_images(cuda):
+    src = torch.randint(0, 256, (50, 32, 32, 3), dtype=torch.uint8)
+    idx = torch.randint(0, 50, (2, 7), dtype=torch.int32)
+    mean = torch.tensor([0.4914, 0.4822, 0.4465]); inv = 1 / torch.tensor([0.247, 0.243, 0.261])
+    for im2col, pad in ((False, 0), (True, 1)):
+        a = Fn.prep_images(src.to(cuda), idx.to(cuda), mean.to(cuda), inv.to(cuda), 32, im2col, pad)
+        b = Fn.prep_images(src, idx, mean, inv, 32, im2col, pad)
+        _close(a, b, rel=1e-2)
+    x = torch.randn(4, 1, 28, 28)
+    _close(Fn.nchw_to_nhwc(x.to(cuda), 32, True, 0), Fn.nchw_to_nhwc(x, 32, True, 0))
