@@ -29,11 +29,12 @@ static int grid_for(long long work, int block) {
 // ---------------------------------------------------------------------------------------------
 // src: uint8 [num_samples][Hs][Ws][Cs]; idx: int32 [G*B] sample ids (row-major over g,b)
 // im2col=0: out [G*B][Hs][Ws][Cout], channel c<Cs normalised, c>=Cs zero
-// im2col=1: out [G*B][Ho][Wo][Cout] with Ho=Hs+2pad-2, channel j=(r*3+s)*Cs+c (<9*Cs), rest 0
+// im2col=k>0: out [G*B][Ho][Wo][Cout] with Ho=(Hs+2pad-k)/stride+1, channel j=(r*k+s)*Cs+c
+// (< k*k*Cs), rest 0 — the stem conv then runs as a 1x1 GEMM on MFMA.
 __global__ void prep_images_kernel(const uint8_t* __restrict__ src, const int* __restrict__ idx,
                                    const float* __restrict__ mean, const float* __restrict__ inv_std,
                                    bf16_t* __restrict__ out, int nimg, int Hs, int Ws, int Cs,
-                                   int Ho, int Wo, int Cout, int im2col, int pad) {
+                                   int Ho, int Wo, int Cout, int im2col, int pad, int stride) {
   const long long total = (long long)nimg * Ho * Wo * (Cout / 8);
   GSTRIDE_LOOP(t, total) {
     const int cchunk = (int)(t % (Cout / 8));
@@ -50,10 +51,10 @@ __global__ void prep_images_kernel(const uint8_t* __restrict__ src, const int* _
       float val = 0.f;
       if (!im2col) {
         if (ch < Cs) val = ((float)src[sbase + ((long long)h * Ws + w) * Cs + ch] * (1.f / 255.f) - mean[ch]) * inv_std[ch];
-      } else if (ch < 9 * Cs) {
+      } else if (ch < im2col * im2col * Cs) {
         const int tap = ch / Cs, c = ch - tap * Cs;
-        const int r = tap / 3, s = tap - r * 3;
-        const int ih = h - pad + r, iw = w - pad + s;
+        const int r = tap / im2col, s = tap - r * im2col;
+        const int ih = h * stride - pad + r, iw = w * stride - pad + s;
         if ((unsigned)ih < (unsigned)Hs && (unsigned)iw < (unsigned)Ws)
           val = ((float)src[sbase + ((long long)ih * Ws + iw) * Cs + c] * (1.f / 255.f) - mean[c]) * inv_std[c];
         // zero padding happens in normalised space (matches conv zero-padding)
@@ -66,21 +67,22 @@ __global__ void prep_images_kernel(const uint8_t* __restrict__ src, const int* _
 
 DDL_API int ddl_prep_images(const void* src, const int* idx, const float* mean, const float* inv_std,
                             void* out, int nimg, int Hs, int Ws, int Cs, int Cout, int im2col,
-                            int pad, hipStream_t s) {
-  if (Cout % 8) return (int)hipErrorInvalidValue;
-  if (im2col && 9 * Cs > Cout) return (int)hipErrorInvalidValue;
-  const int Ho = im2col ? Hs + 2 * pad - 2 : Hs, Wo = im2col ? Ws + 2 * pad - 2 : Ws;
+                            int pad, int stride, hipStream_t s) {
+  if (Cout % 8 || stride < 1) return (int)hipErrorInvalidValue;
+  if (im2col && im2col * im2col * Cs > Cout) return (int)hipErrorInvalidValue;
+  const int Ho = im2col ? (Hs + 2 * pad - im2col) / stride + 1 : Hs;
+  const int Wo = im2col ? (Ws + 2 * pad - im2col) / stride + 1 : Ws;
   const long long total = (long long)nimg * Ho * Wo * (Cout / 8);
   hipLaunchKernelGGL(prep_images_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s,
                      (const uint8_t*)src, idx, mean, inv_std, (bf16_t*)out, nimg, Hs, Ws, Cs, Ho, Wo,
-                     Cout, im2col, pad);
+                     Cout, im2col, pad, stride);
   return (int)hipGetLastError();
 }
 
 // fp32 NCHW (already normalised) -> NHWC bf16, optionally im2col 3x3 (same rules as above)
 __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, bf16_t* __restrict__ out, int N,
                                     int Cs, int Hs, int Ws, int Ho, int Wo, int Cout, int im2col,
-                                    int pad) {
+                                    int pad, int stride) {
   const long long total = (long long)N * Ho * Wo * (Cout / 8);
   GSTRIDE_LOOP(t, total) {
     const int cchunk = (int)(t % (Cout / 8));
@@ -96,10 +98,10 @@ __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, bf16_t* __restr
       float val = 0.f;
       if (!im2col) {
         if (ch < Cs) val = x[(((long long)n * Cs + ch) * Hs + h) * Ws + w];
-      } else if (ch < 9 * Cs) {
+      } else if (ch < im2col * im2col * Cs) {
         const int tap = ch / Cs, c = ch - tap * Cs;
-        const int r = tap / 3, s = tap - r * 3;
-        const int ih = h - pad + r, iw = w - pad + s;
+        const int r = tap / im2col, s = tap - r * im2col;
+        const int ih = h * stride - pad + r, iw = w * stride - pad + s;
         if ((unsigned)ih < (unsigned)Hs && (unsigned)iw < (unsigned)Ws)
           val = x[(((long long)n * Cs + c) * Hs + ih) * Ws + iw];
       }
@@ -110,13 +112,14 @@ __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, bf16_t* __restr
 }
 
 DDL_API int ddl_nchw_to_nhwc(const float* x, void* out, int N, int Cs, int Hs, int Ws, int Cout,
-                             int im2col, int pad, hipStream_t s) {
-  if (Cout % 8) return (int)hipErrorInvalidValue;
-  if (im2col && 9 * Cs > Cout) return (int)hipErrorInvalidValue;
-  const int Ho = im2col ? Hs + 2 * pad - 2 : Hs, Wo = im2col ? Ws + 2 * pad - 2 : Ws;
+                             int im2col, int pad, int stride, hipStream_t s) {
+  if (Cout % 8 || stride < 1) return (int)hipErrorInvalidValue;
+  if (im2col && im2col * im2col * Cs > Cout) return (int)hipErrorInvalidValue;
+  const int Ho = im2col ? (Hs + 2 * pad - im2col) / stride + 1 : Hs;
+  const int Wo = im2col ? (Ws + 2 * pad - im2col) / stride + 1 : Ws;
   const long long total = (long long)N * Ho * Wo * (Cout / 8);
   hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s, x,
-                     (bf16_t*)out, N, Cs, Hs, Ws, Ho, Wo, Cout, im2col, pad);
+                     (bf16_t*)out, N, Cs, Hs, Ws, Ho, Wo, Cout, im2col, pad, stride);
   return (int)hipGetLastError();
 }
 
@@ -382,5 +385,100 @@ DDL_API int ddl_cast_f32_bf16(const float* x, void* y, long long n, hipStream_t 
 DDL_API int ddl_cast_bf16_f32(const void* x, float* y, long long n, hipStream_t s) {
   hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, (const bf16_t*)x,
                      y, n);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// general k x k / stride / pad max pool (ImageNet stem 3x3/2 p1); -inf padding like torch
+__global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int NB,
+                                   int H, int W, int C, int k, int st, int pd, int Ho, int Wo) {
+  const int CC = C / 8;
+  const long long total = (long long)NB * Ho * Wo * CC;
+  GSTRIDE_LOOP(t, total) {
+    const int cc = (int)(t % CC);
+    long long p = t / CC;
+    const int wo = (int)(p % Wo);
+    p /= Wo;
+    const int ho = (int)(p % Ho);
+    const int n = (int)(p / Ho);
+    float m[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
+    for (int r = 0; r < k; ++r) {
+      const int ih = ho * st - pd + r;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int s2 = 0; s2 < k; ++s2) {
+        const int iw = wo * st - pd + s2;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        float v[8];
+        unpack8(*(const i4v*)(x + (((long long)n * H + ih) * W + iw) * C + cc * 8), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m[e] = (v[e] > m[e] || v[e] != v[e]) ? v[e] : m[e];
+      }
+    }
+    *(i4v*)(y + t * 8) = pack8(m);
+  }
+}
+// backward as a gather over the windows that contain each input pixel (no atomics): an input
+// element receives dy of every window whose (first) argmax it is.
+__global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                                   bf16_t* __restrict__ dx, int NB, int H, int W, int C, int k,
+                                   int st, int pd, int Ho, int Wo) {
+  const int CC = C / 8;
+  const long long total = (long long)NB * H * W * CC;
+  GSTRIDE_LOOP(t, total) {
+    const int cc = (int)(t % CC);
+    long long p = t / CC;
+    const int iw0 = (int)(p % W);
+    p /= W;
+    const int ih0 = (int)(p % H);
+    const int n = (int)(p / H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int ho_lo = max(0, (ih0 + pd - k + st) / st), ho_hi = min(Ho - 1, (ih0 + pd) / st);
+    const int wo_lo = max(0, (iw0 + pd - k + st) / st), wo_hi = min(Wo - 1, (iw0 + pd) / st);
+    for (int ho = ho_lo; ho <= ho_hi; ++ho)
+      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+        float m[8];
+        int am[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { m[e] = -INFINITY; am[e] = -1; }
+        for (int r = 0; r < k; ++r) {
+          const int ih = ho * st - pd + r;
+          if ((unsigned)ih >= (unsigned)H) continue;
+          for (int s2 = 0; s2 < k; ++s2) {
+            const int iw = wo * st - pd + s2;
+            if ((unsigned)iw >= (unsigned)W) continue;
+            float v[8];
+            unpack8(*(const i4v*)(x + (((long long)n * H + ih) * W + iw) * C + cc * 8), v);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (v[e] > m[e] || (v[e] != v[e] && m[e] == m[e])) { m[e] = v[e]; am[e] = ih * W + iw; }
+          }
+        }
+        float d[8];
+        unpack8(*(const i4v*)(dy + (((long long)n * Ho + ho) * Wo + wo) * C + cc * 8), d);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (am[e] == ih0 * W + iw0) acc[e] += d[e];
+      }
+    *(i4v*)(dx + t * 8) = pack8(acc);
+  }
+}
+DDL_API int ddl_maxpool_fwd(const void* x, void* y, int NB, int H, int W, int C, int k, int st,
+                            int pd, hipStream_t s) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const int Ho = (H + 2 * pd - k) / st + 1, Wo = (W + 2 * pd - k) / st + 1;
+  const long long total = (long long)NB * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s,
+                     (const bf16_t*)x, (bf16_t*)y, NB, H, W, C, k, st, pd, Ho, Wo);
+  return (int)hipGetLastError();
+}
+DDL_API int ddl_maxpool_bwd(const void* x, const void* dy, void* dx, int NB, int H, int W, int C,
+                            int k, int st, int pd, hipStream_t s) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const int Ho = (H + 2 * pd - k) / st + 1, Wo = (W + 2 * pd - k) / st + 1;
+  const long long total = (long long)NB * H * W * (C / 8);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s,
+                     (const bf16_t*)x, (const bf16_t*)dy, (bf16_t*)dx, NB, H, W, C, k, st, pd, Ho, Wo);
   return (int)hipGetLastError();
 }

@@ -1,0 +1,178 @@
+"""Net: a sequential container of explicit fwd/bwd layers over one flat ParamStore.
+
+* ``forward_train(x)`` / ``backward(dlogits)`` — the native training path used by the FL engine,
+  DP trainer and benchmark (no autograd, graph-capturable).
+* ``__call__`` — torch-compatible: with grad enabled the whole net is ONE autograd node, so
+  reference-style code (``output = model(data); F.nll_loss(output, target).backward()``) works and
+  the backward pass still runs our kernels.
+* ``train_step(x, labels)`` — forward + fused CE + backward in one call (client-batched).
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops import functional as Fn
+from .layers import RELU, ConvUnit, Layer
+from .params import ParamStore
+
+
+class Net:
+    def __init__(self, layers: list[Layer], groups: int = 1, num_classes: int | None = None,
+                 input_spec: dict | None = None, name: str = "net"):
+        self.layers = layers
+        self.G = groups
+        self.num_classes = num_classes
+        self.input_spec = input_spec or {}
+        self.name = name
+        self.store = ParamStore(groups)
+        for i, layer in enumerate(layers):
+            layer.declare(self.store, getattr(layer, "pname", f"{i}.{layer.name}"))
+        self._plan_fusions()
+        self.training = True
+        self.device = torch.device("cpu")
+
+    def _plan_fusions(self):
+        # a conv/linear whose producer ends in a plain ReLU fuses that ReLU's backward mask into
+        # its dgrad epilogue (dx *= x > 0), the producer then skips its own mask pass.
+        for prev, cur in zip(self.layers[:-1], self.layers[1:]):
+            if isinstance(cur, ConvUnit) and prev.out_act == RELU and not getattr(prev, "bn", False) \
+                    and not getattr(prev, "residual_out", False):
+                cur.mask_input = True
+                prev.grad_premasked = True
+        if self.layers:
+            self.layers[0].needs_input_grad = False
+
+    # ------------------------------------------------------------------ setup
+    def to(self, device, seed: int = 0, generator=None):
+        self.device = torch.device(device)
+        self.store.materialize(self.device, seed=seed, generator=generator)
+        for layer in self.layers:
+            layer.bind(self.store)
+        return self
+
+    def train(self, mode: bool = True):
+        self.training = mode
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    # ------------------------------------------------------------------ native path
+    def forward_native(self, x, train: bool | None = None):
+        train = self.training if train is None else train
+        self.store.ensure_shadow()
+        ctxs = []
+        for layer in self.layers:
+            x, c = layer.forward(x, train)
+            ctxs.append(c)
+        return x, ctxs
+
+    def backward_native(self, dy, ctxs):
+        for layer, c in zip(reversed(self.layers), reversed(ctxs)):
+            dy = layer.backward(dy, c)
+            if dy is None:
+                break
+        return dy
+
+    def train_step(self, x, labels, ncls=None, scale=None, targets=None, with_correct=False):
+        """forward + fused softmax-CE (mean over each client's batch) + backward.
+        Grads ACCUMULATE into store.grad (zero them per optimizer step). Returns (loss[G], correct)."""
+        logits, ctxs = self.forward_native(x, True)
+        N = logits.shape[1]
+        loss, dlogits, correct = Fn.cross_entropy(
+            logits, labels, targets, ncls=ncls or self.num_classes, scale=(1.0 / N) if scale is None else scale,
+            with_correct=with_correct)
+        self.backward_native(dlogits, ctxs)
+        return loss, correct
+
+    @torch.no_grad()
+    def predict(self, x):
+        logits, _ = self.forward_native(x, False)
+        return logits
+
+    # ------------------------------------------------------------------ torch-compatible path
+    def prepare_input(self, x: torch.Tensor) -> torch.Tensor:
+        """Accepts the native layout [G,N,...] bf16, or a torch-style fp32 batch (NCHW image /
+        [N, F] table) for G == 1, converting it with the kernels' input rules."""
+        if x.dtype == torch.bfloat16 and x.dim() >= 3 and x.shape[0] == self.G:
+            return x
+        spec = self.input_spec
+        if spec.get("flat") and x.dim() > 2:
+            x = x.reshape(x.shape[0], -1)
+        if x.dim() == 4:  # NCHW images
+            return Fn.nchw_to_nhwc(x.to(self.device), spec.get("cpad", 32),
+                                   spec.get("stem_k", 0) if spec.get("im2col") else 0,
+                                   spec.get("pad", 0), spec.get("stem_stride", 1))
+        if x.dim() == 2:  # [N, F]
+            F_ = x.shape[1]
+            cp = spec.get("cpad", (F_ + 31) // 32 * 32)
+            out = torch.zeros(1, x.shape[0], cp, dtype=torch.bfloat16, device=self.device)
+            out[0, :, :F_] = x.to(self.device, torch.bfloat16)
+            return out
+        raise ValueError(f"unsupported input shape {tuple(x.shape)}")
+
+    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        xin = self.prepare_input(x)
+        if torch.is_grad_enabled() and self.training:
+            return _NetFunction.apply(self, xin, self._token())
+        logits, _ = self.forward_native(xin, self.training)
+        return self._logits_out(logits)
+
+    forward = __call__
+
+    def _logits_out(self, logits):
+        ncls = self.num_classes or logits.shape[-1]
+        out = logits[..., :ncls].float()
+        if self.G == 1:
+            out = out[0]
+        return self.output_transform(out)
+
+    def output_transform(self, logits):
+        return logits
+
+    def output_transform_backward(self, out, grad):
+        return grad
+
+    def _token(self):
+        if not hasattr(self, "_tok"):
+            self._tok = torch.zeros((), requires_grad=True)
+        return self._tok
+
+    # torch.nn.Module-ish conveniences
+    def parameters(self):
+        return [self.store.data]
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.store.zero_grad()
+
+    def state_dict(self, group: int = 0):
+        return self.store.state_dict(group)
+
+    def load_state_dict(self, sd, group=None):
+        self.store.load_state_dict(sd, group)
+
+    def num_params(self) -> int:
+        return self.store.num_params()
+
+
+class _NetFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, net: Net, xin, token):
+        logits, ctxs = net.forward_native(xin, True)
+        out = net._logits_out(logits)
+        ctx.net, ctx.ctxs, ctx.lshape = net, ctxs, logits.shape
+        ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        net = ctx.net
+        (out,) = ctx.saved_tensors
+        g = net.output_transform_backward(out, grad.float())
+        G, N, ld = ctx.lshape
+        full = torch.zeros(G, N, ld, dtype=torch.bfloat16, device=g.device)
+        ncls = net.num_classes or ld
+        full[..., :ncls] = g.reshape(G, N, ncls).to(torch.bfloat16)
+        net.backward_native(full, ctx.ctxs)
+        ctx.ctxs = None
+        return None, None, None

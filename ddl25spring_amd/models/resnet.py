@@ -1,0 +1,266 @@
+"""ResNet-18 / ResNet-50 (He et al. 2016) on the fused conv/BN kernels, client-batched.
+
+North-star configs (BASELINE.json): "Horizontal FedAvg ResNet-18, CIFAR-10-shape" and
+"Data-parallel all-reduce SGD, ResNet-50 ImageNet-shape". Absent from the reference.
+
+MI355X-first choices:
+  * the stem's im2col is fused into the device data loader (``ops.prep_images``), so the CIFAR
+    stem (3x3, 3->64) and the ImageNet stem (7x7/2, 3->64) run as K=32 / K=160 GEMMs on MFMA
+    instead of 3-channel convolutions;
+  * BatchNorm statistics come out of the conv epilogue; BN-apply fuses the residual join (identity
+    or projected shortcut, whose own BN is folded into the same pass) and the ReLU;
+  * backward of the residual join: the shortcut gradient is added inside the dgrad epilogue of
+    the block's first conv.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops import functional as Fn
+from .layers import RELU, ConvUnit, GlobalAvgPool, Layer, Linear, pad32
+from .net import Net
+
+
+class _BNConv(ConvUnit):
+    """conv + BN statistics only (activation handled by the enclosing block)."""
+
+    def __init__(self, cin, cout, k, stride, pad):
+        super().__init__(cin, cout, k=k, stride=stride, pad=pad, bias=False, bn=True, act=None)
+
+    def conv_stats(self, x, train):
+        st = self.store
+        g = self.geom(x)
+        stats = torch.zeros(g.G, 2, self.cout, dtype=torch.float32, device=x.device) if train else None
+        c = Fn.conv_fwd(x, st.shadow_of(self.w), g, stats=stats)
+        if not train:
+            stats = torch.zeros(g.G, 2, self.cout, dtype=torch.float32, device=x.device)
+        sc, sh, mu, rs = Fn.bn_finalize(stats, st.param(self.gamma), st.param(self.beta),
+                                        st.buffer(self.rm), st.buffer(self.rv), g.N * g.P * g.Q,
+                                        self.eps, self.momentum, training=train)
+        return c, sc, sh, mu, rs, g
+
+    def bn_backward(self, dy, ymask, c, mu, rs, emit_dym=False):
+        st = self.store
+        sums = Fn.bn_bwd_reduce(dy, ymask, c, mu, rs, st.grad_of(self.gamma), st.grad_of(self.beta))
+        return Fn.bn_bwd_apply(dy, ymask, c, mu, rs, st.param(self.gamma), sums, emit_dym=emit_dym)
+
+
+class BasicBlock(Layer):
+    name = "basic"
+    residual_out = True
+    expansion = 1
+
+    def __init__(self, cin, planes, stride=1):
+        self.cin, self.cout, self.stride = cin, planes, stride
+        self.conv1 = _BNConv(cin, planes, 3, stride, 1)
+        self.conv2 = _BNConv(planes, planes, 3, 1, 1)
+        self.down = _BNConv(cin, planes, 1, stride, 0) if (stride != 1 or cin != planes) else None
+
+    @property
+    def out_act(self):
+        return RELU
+
+    def declare(self, store, prefix):
+        super().declare(store, prefix)
+        self.conv1.declare(store, prefix + ".conv1")
+        self.conv2.declare(store, prefix + ".conv2")
+        if self.down is not None:
+            self.down.declare(store, prefix + ".downsample")
+
+    def bind(self, store):
+        super().bind(store)
+        for c in (self.conv1, self.conv2, self.down):
+            if c is not None:
+                c.bind(store)
+
+    def forward(self, x, train):
+        c1, sc1, sh1, mu1, rs1, g1 = self.conv1.conv_stats(x, train)
+        a1 = Fn.bn_apply(c1, sc1, sh1, act=RELU)
+        c2, sc2, sh2, mu2, rs2, g2 = self.conv2.conv_stats(a1, train)
+        if self.down is not None:
+            cs, scs, shs, mus, rss, gs = self.down.conv_stats(x, train)
+            out = Fn.bn_apply(c2, sc2, sh2, r=cs, rscale=scs, rshift=shs, act=RELU)
+            dctx = (cs, mus, rss, gs)
+        else:
+            out = Fn.bn_apply(c2, sc2, sh2, r=x, act=RELU)
+            dctx = None
+        return out, (x, c1, a1, mu1, rs1, g1, c2, mu2, rs2, g2, out, dctx)
+
+    def backward(self, dout, ctx):
+        x, c1, a1, mu1, rs1, g1, c2, mu2, rs2, g2, out, dctx = ctx
+        st = self.store
+        dc2, dym = self.conv2.bn_backward(dout, out, c2, mu2, rs2, emit_dym=True)
+        if dctx is not None:
+            cs, mus, rss, gs = dctx
+            dcs = self.down.bn_backward(dym, None, cs, mus, rss)
+            Fn.conv_wgrad(dcs, x, gs, st.grad_of(self.down.w))
+            dres = Fn.conv_dgrad(dcs, st.shadow_of(self.down.w), gs) if self.needs_input_grad else None
+        else:
+            dres = dym
+        Fn.conv_wgrad(dc2, a1, g2, st.grad_of(self.conv2.w))
+        da1 = Fn.conv_dgrad(dc2, st.shadow_of(self.conv2.w), g2)
+        dc1 = self.conv1.bn_backward(da1, a1, c1, mu1, rs1)
+        Fn.conv_wgrad(dc1, x, g1, st.grad_of(self.conv1.w))
+        if not self.needs_input_grad:
+            return None
+        return Fn.conv_dgrad(dc1, st.shadow_of(self.conv1.w), g1, residual=dres)
+
+    def flops(self, s):
+        G, N, H, W, _ = s
+        Ho, Wo = (H + 2 - 3) // self.stride + 1, (W + 2 - 3) // self.stride + 1
+        f = 2 * G * N * Ho * Wo * self.cout * 9 * (self.cin + self.cout)
+        if self.down is not None:
+            f += 2 * G * N * Ho * Wo * self.cout * self.cin
+        return f
+
+    def out_shape(self, s):
+        G, N, H, W, _ = s
+        return (G, N, (H + 2 - 3) // self.stride + 1, (W + 2 - 3) // self.stride + 1, self.cout)
+
+
+class Bottleneck(Layer):
+    name = "bottleneck"
+    residual_out = True
+    expansion = 4
+
+    def __init__(self, cin, planes, stride=1):
+        self.cin, self.cout, self.stride = cin, planes * 4, stride
+        self.conv1 = _BNConv(cin, planes, 1, 1, 0)
+        self.conv2 = _BNConv(planes, planes, 3, stride, 1)
+        self.conv3 = _BNConv(planes, planes * 4, 1, 1, 0)
+        self.down = _BNConv(cin, planes * 4, 1, stride, 0) if (stride != 1 or cin != planes * 4) else None
+        self.planes = planes
+
+    @property
+    def out_act(self):
+        return RELU
+
+    def declare(self, store, prefix):
+        super().declare(store, prefix)
+        for n in ("conv1", "conv2", "conv3"):
+            getattr(self, n).declare(store, f"{prefix}.{n}")
+        if self.down is not None:
+            self.down.declare(store, prefix + ".downsample")
+
+    def bind(self, store):
+        super().bind(store)
+        for c in (self.conv1, self.conv2, self.conv3, self.down):
+            if c is not None:
+                c.bind(store)
+
+    def forward(self, x, train):
+        c1, sc1, sh1, mu1, rs1, g1 = self.conv1.conv_stats(x, train)
+        a1 = Fn.bn_apply(c1, sc1, sh1, act=RELU)
+        c2, sc2, sh2, mu2, rs2, g2 = self.conv2.conv_stats(a1, train)
+        a2 = Fn.bn_apply(c2, sc2, sh2, act=RELU)
+        c3, sc3, sh3, mu3, rs3, g3 = self.conv3.conv_stats(a2, train)
+        if self.down is not None:
+            cs, scs, shs, mus, rss, gs = self.down.conv_stats(x, train)
+            out = Fn.bn_apply(c3, sc3, sh3, r=cs, rscale=scs, rshift=shs, act=RELU)
+            dctx = (cs, mus, rss, gs)
+        else:
+            out = Fn.bn_apply(c3, sc3, sh3, r=x, act=RELU)
+            dctx = None
+        return out, (x, (c1, a1, mu1, rs1, g1), (c2, a2, mu2, rs2, g2), (c3, mu3, rs3, g3), out, dctx)
+
+    def backward(self, dout, ctx):
+        x, (c1, a1, mu1, rs1, g1), (c2, a2, mu2, rs2, g2), (c3, mu3, rs3, g3), out, dctx = ctx
+        st = self.store
+        dc3, dym = self.conv3.bn_backward(dout, out, c3, mu3, rs3, emit_dym=True)
+        if dctx is not None:
+            cs, mus, rss, gs = dctx
+            dcs = self.down.bn_backward(dym, None, cs, mus, rss)
+            Fn.conv_wgrad(dcs, x, gs, st.grad_of(self.down.w))
+            dres = Fn.conv_dgrad(dcs, st.shadow_of(self.down.w), gs) if self.needs_input_grad else None
+        else:
+            dres = dym
+        Fn.conv_wgrad(dc3, a2, g3, st.grad_of(self.conv3.w))
+        da2 = Fn.conv_dgrad(dc3, st.shadow_of(self.conv3.w), g3)
+        dc2 = self.conv2.bn_backward(da2, a2, c2, mu2, rs2)
+        Fn.conv_wgrad(dc2, a1, g2, st.grad_of(self.conv2.w))
+        da1 = Fn.conv_dgrad(dc2, st.shadow_of(self.conv2.w), g2)
+        dc1 = self.conv1.bn_backward(da1, a1, c1, mu1, rs1)
+        Fn.conv_wgrad(dc1, x, g1, st.grad_of(self.conv1.w))
+        if not self.needs_input_grad:
+            return None
+        return Fn.conv_dgrad(dc1, st.shadow_of(self.conv1.w), g1, residual=dres)
+
+    def flops(self, s):
+        G, N, H, W, _ = s
+        Ho, Wo = (H + 2 - 3) // self.stride + 1, (W + 2 - 3) // self.stride + 1
+        p = self.planes
+        f = 2 * G * N * (H * W * p * self.cin + Ho * Wo * p * 9 * p + Ho * Wo * self.cout * p)
+        if self.down is not None:
+            f += 2 * G * N * Ho * Wo * self.cout * self.cin
+        return f
+
+    def out_shape(self, s):
+        G, N, H, W, _ = s
+        return (G, N, (H + 2 - 3) // self.stride + 1, (W + 2 - 3) // self.stride + 1, self.cout)
+
+
+class MaxPool3s2(Layer):
+    """3x3/2 pad-1 max pool of the ImageNet stem (via two 2x2 reductions is NOT equivalent, so it
+    runs as its own kernel)."""
+    name = "maxpool3"
+
+    def forward(self, x, train):
+        return Fn.maxpool_fwd(x, 3, 2, 1), x
+
+    def backward(self, dy, x):
+        return Fn.maxpool_bwd(x, dy, 3, 2, 1)
+
+    def out_shape(self, s):
+        G, N, H, W, C = s
+        return (G, N, (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1, C)
+
+
+def _resnet(block, layers, num_classes, groups, stem: str, in_ch=3) -> Net:
+    mods: list[Layer] = []
+    if stem == "cifar":
+        # im2col'd 3x3 stem: channel j = (r*3+s)*3 + c (27 real of 32), 1x1 conv on MFMA
+        stem_conv = ConvUnit(32, 64, k=1, stride=1, pad=0, bn=True, act="relu",
+                             cin_true=9 * in_ch, fan_in=9 * in_ch)
+        input_spec = {"cpad": 32, "im2col": True, "pad": 1, "stem_k": 3}
+    else:
+        cpad = pad32(49 * in_ch)
+        stem_conv = ConvUnit(cpad, 64, k=1, stride=1, pad=0, bn=True, act="relu",
+                             cin_true=49 * in_ch, fan_in=49 * in_ch)
+        input_spec = {"cpad": cpad, "im2col": True, "pad": 3, "stem_k": 7, "stem_stride": 2}
+    stem_conv.pname = "conv1"
+    mods.append(stem_conv)
+    if stem != "cifar":
+        mp = MaxPool3s2()
+        mp.pname = "maxpool"
+        mods.append(mp)
+    cin = 64
+    for li, (planes, n) in enumerate(zip((64, 128, 256, 512), layers)):
+        for bi in range(n):
+            stride = 2 if (bi == 0 and li > 0) else 1
+            b = block(cin, planes, stride)
+            b.pname = f"layer{li + 1}.{bi}"
+            mods.append(b)
+            cin = planes * block.expansion
+    gp = GlobalAvgPool()
+    gp.pname = "avgpool"
+    mods.append(gp)
+    fc = Linear(cin, num_classes, bias=True, fout_true=num_classes)
+    fc.pname = "fc"
+    mods.append(fc)
+    net = Net(mods, groups=groups, num_classes=num_classes, input_spec=input_spec,
+              name=f"resnet{sum(layers) * (2 if block is BasicBlock else 3) + 2}")
+    return net
+
+
+def resnet18_cifar(num_classes=10, groups=1) -> Net:
+    """ResNet-18, CIFAR variant (3x3 stem, no max-pool), 11.17M params."""
+    return _resnet(BasicBlock, (2, 2, 2, 2), num_classes, groups, "cifar")
+
+
+def resnet50_imagenet(num_classes=1000, groups=1) -> Net:
+    """ResNet-50, ImageNet variant (7x7/2 stem + 3x3/2 max-pool), 25.6M params."""
+    return _resnet(Bottleneck, (3, 4, 6, 3), num_classes, groups, "imagenet")
+
+
+def resnet18_imagenet(num_classes=1000, groups=1) -> Net:
+    return _resnet(BasicBlock, (2, 2, 2, 2), num_classes, groups, "imagenet")

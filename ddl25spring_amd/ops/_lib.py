@@ -73,8 +73,10 @@ _SIGS = {
     "ddl_bn_bwd_reduce": [vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i32, i32, vp],
     "ddl_bn_bwd_apply": [vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, i64, i32, i32, vp],
     # nn_ops.hip
-    "ddl_prep_images": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp],
-    "ddl_nchw_to_nhwc": [vp, vp, i32, i32, i32, i32, i32, i32, i32, vp],
+    "ddl_prep_images": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
+    "ddl_nchw_to_nhwc": [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
+    "ddl_maxpool_fwd": [vp, vp, i32, i32, i32, i32, i32, i32, i32, vp],
+    "ddl_maxpool_bwd": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp],
     "ddl_maxpool2_fwd": [vp, vp, i32, i32, i32, i32, vp],
     "ddl_maxpool2_bwd": [vp, vp, vp, i32, i32, i32, i32, vp],
     "ddl_avgpool_fwd": [vp, vp, i32, i32, i32, vp],

@@ -267,44 +267,89 @@ def to_bf16(x32: torch.Tensor, out=None):
     return out
 
 
-def nchw_to_nhwc(x: torch.Tensor, cpad: int, im2col: bool = False, pad: int = 0):
-    """fp32 NCHW -> bf16 NHWC [1, N, H', W', cpad] (optionally 3x3 im2col for the stem conv)."""
+def _im2col_k(im2col) -> int:
+    return 3 if im2col is True else int(im2col or 0)
+
+
+def _stem_out(H, W, k, pad, stride):
+    if not k:
+        return H, W
+    return (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+
+
+def _im2col_cpu(xf, k, pad, stride, cpad):
+    N, C, H, W = xf.shape
+    Ho, Wo = _stem_out(H, W, k, pad, stride)
+    if k:
+        cols = torch.nn.functional.unfold(xf, k, padding=pad, stride=stride)  # [N, C*k*k, L]
+        cols = cols.reshape(N, C, k * k, Ho * Wo).permute(0, 3, 2, 1).reshape(N, Ho, Wo, k * k * C)
+    else:
+        cols = xf.permute(0, 2, 3, 1)
+    out = torch.zeros(1, N, Ho, Wo, cpad, dtype=torch.float32)
+    out[0, ..., :cols.shape[-1]] = cols
+    return ref._bf(out)
+
+
+def nchw_to_nhwc(x: torch.Tensor, cpad: int, im2col=0, pad: int = 0, stride: int = 1):
+    """fp32 NCHW -> bf16 NHWC [1, N, H', W', cpad]; ``im2col=k`` lays out the k x k / stride
+    patches of the stem conv as channels ((r*k+s)*C + c), so the stem runs as a 1x1 GEMM."""
+    k = _im2col_k(im2col)
     N, C, H, W = x.shape
-    Ho, Wo = (H + 2 * pad - 2, W + 2 * pad - 2) if im2col else (H, W)
+    Ho, Wo = _stem_out(H, W, k, pad, stride)
     if not x.is_cuda:
-        xf = x.float()
-        if im2col:
-            cols = torch.nn.functional.unfold(xf, 3, padding=pad)  # [N, C*9, L] ordered (c, r, s)
-            cols = cols.reshape(N, C, 9, Ho * Wo).permute(0, 3, 2, 1).reshape(N, Ho, Wo, 9 * C)
-        else:
-            cols = xf.permute(0, 2, 3, 1)
-        out = torch.zeros(1, N, Ho, Wo, cpad, dtype=torch.bfloat16)
-        out[0, ..., :cols.shape[-1]] = cols.to(torch.bfloat16)
-        return out
+        return _im2col_cpu(x.float(), k, pad, stride, cpad)
     xc = x.float().contiguous()
     out = torch.empty(1, N, Ho, Wo, cpad, dtype=torch.bfloat16, device=x.device)
-    check(_lib.kernels().ddl_nchw_to_nhwc(ptr(xc), ptr(out), N, C, H, W, cpad, int(im2col), pad,
+    check(_lib.kernels().ddl_nchw_to_nhwc(ptr(xc), ptr(out), N, C, H, W, cpad, k, pad, stride,
                                           stream()), "nchw_to_nhwc")
     return out
 
 
-def prep_images(src_u8, idx, mean, inv_std, cpad, im2col=False, pad=0, out=None):
+def prep_images(src_u8, idx, mean, inv_std, cpad, im2col=0, pad=0, stride=1, out=None):
     """Gather uint8 HWC samples by id, normalise, NHWC bf16 (channel-padded / stem-im2col)."""
+    k = _im2col_k(im2col)
     n = idx.numel()
     Hs, Ws, Cs = src_u8.shape[1:]
-    Ho, Wo = (Hs + 2 * pad - 2, Ws + 2 * pad - 2) if im2col else (Hs, Ws)
+    Ho, Wo = _stem_out(Hs, Ws, k, pad, stride)
     if out is None:
         out = torch.empty(n, Ho, Wo, cpad, dtype=torch.bfloat16, device=src_u8.device)
     if not src_u8.is_cuda:
         x = src_u8[idx.long().reshape(-1)].float() / 255.0
         x = (x - mean) * inv_std
-        x = x.permute(0, 3, 1, 2)
-        out.copy_(nchw_to_nhwc(x, cpad, im2col, pad)[0].reshape(out.shape))
+        out.copy_(_im2col_cpu(x.permute(0, 3, 1, 2), k, pad, stride, cpad)[0].reshape(out.shape))
         return out
     check(_lib.kernels().ddl_prep_images(ptr(src_u8), ptr(idx), ptr(mean), ptr(inv_std), ptr(out),
-                                         n, Hs, Ws, Cs, cpad, int(im2col), pad, stream()),
+                                         n, Hs, Ws, Cs, cpad, k, pad, stride, stream()),
           "prep_images")
     return out
+
+
+def maxpool_fwd(x, k, stride, pad):
+    G, N, H, W, C = x.shape
+    Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    if not x.is_cuda:
+        xi = x.float().reshape(G * N, H, W, C).permute(0, 3, 1, 2)
+        y = torch.nn.functional.max_pool2d(xi, k, stride, pad)
+        return y.permute(0, 2, 3, 1).reshape(G, N, Ho, Wo, C).to(torch.bfloat16).contiguous()
+    y = torch.empty(G, N, Ho, Wo, C, dtype=x.dtype, device=x.device)
+    check(_lib.kernels().ddl_maxpool_fwd(ptr(x), ptr(y), G * N, H, W, C, k, stride, pad, stream()),
+          "maxpool_fwd")
+    return y
+
+
+def maxpool_bwd(x, dy, k, stride, pad):
+    G, N, H, W, C = x.shape
+    if not x.is_cuda:
+        with torch.enable_grad():
+            xi = x.float().reshape(G * N, H, W, C).permute(0, 3, 1, 2).detach().requires_grad_(True)
+            y = torch.nn.functional.max_pool2d(xi, k, stride, pad)
+            g = dy.float().reshape(G * N, *dy.shape[2:]).permute(0, 3, 1, 2)
+            (dx,) = torch.autograd.grad(y, xi, g)
+        return dx.permute(0, 2, 3, 1).reshape(G, N, H, W, C).to(torch.bfloat16).contiguous()
+    dx = torch.empty_like(x)
+    check(_lib.kernels().ddl_maxpool_bwd(ptr(x), ptr(dy), ptr(dx), G * N, H, W, C, k, stride, pad,
+                                         stream()), "maxpool_bwd")
+    return dx
 
 
 # ------------------------------------------------------------------------------------- loss

@@ -153,10 +153,11 @@ def maxpool2_fwd(x):
 
 def maxpool2_bwd(x, dy):
     G, N, H, W, C = x.shape
-    xi = x.float().reshape(G * N, H, W, C).permute(0, 3, 1, 2).detach().requires_grad_(True)
-    y = F.max_pool2d(xi, 2)
-    g = dy.float().reshape(G * N, H // 2, W // 2, C).permute(0, 3, 1, 2)
-    (dx,) = torch.autograd.grad(y, xi, g)
+    with torch.enable_grad():  # may be called from inside an autograd backward
+        xi = x.float().reshape(G * N, H, W, C).permute(0, 3, 1, 2).detach().requires_grad_(True)
+        y = F.max_pool2d(xi, 2)
+        g = dy.float().reshape(G * N, H // 2, W // 2, C).permute(0, 3, 1, 2)
+        (dx,) = torch.autograd.grad(y, xi, g)
     return _bf(dx.permute(0, 2, 3, 1).reshape(G, N, H, W, C)).contiguous()
 
 
