@@ -1,0 +1,110 @@
+"""Headline benchmark: FedAvg rounds/s + local samples/s, ResNet-18, CIFAR-10 shape, 8 clients.
+
+BASELINE.json config #2 ("Horizontal FedAvg ResNet-18, CIFAR-10-shape, 8 IID clients = 8 x
+MI355X"). One *step* = one full FedAvg round: every one of the 8 clients runs E=1 local epoch of
+mini-batch SGD (B=100, lr=0.01 — the reference's FedAvg defaults, homework-1.ipynb:50-59) over its
+IID shard of the 50,000-image CIFAR-10-shaped training set (6,250 images each), then the server
+takes the n_k-weighted average (RCCL all-reduce across GPUs). Total work is fixed (8 clients) and
+spread over N GPUs, i.e. strong scaling: at N=1 the 8 clients run client-batched on one GPU, at N=8
+each GPU is one client.
+
+Data: synthetic CIFAR-10-shaped uint8 images (learnable class templates), random-init weights.
+Compute dtype bf16 (MFMA), fp32 master weights / grads / BN statistics / aggregation.
+
+    python bench.py --gpus 1 --steps 3 --warmup 1
+    torchrun --nproc-per-node 8 bench.py --gpus 8 ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+METRIC = "FedAvg rounds/sec + local samples/sec, ResNet-18 CIFAR-10-shape, 8 clients"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3, help="timed FedAvg rounds")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed FedAvg rounds")
+    ap.add_argument("--clients", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=100)
+    ap.add_argument("--epochs", type=int, default=1)
+    ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--train-size", type=int, default=50000)
+    ap.add_argument("--model", default="resnet18")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--eval", action="store_true", help="also report test accuracy (untimed)")
+    args = ap.parse_args()
+
+    from ddl25spring_amd.runtime import dist as rdist
+    ctx = rdist.init()
+    if ctx.device.type != "cuda":
+        print("bench.py needs a GPU", file=sys.stderr)
+    from ddl25spring_amd.data.images import DeviceImageDataset, synthetic_images
+    from ddl25spring_amd.data.split import split
+    from ddl25spring_amd.fl.algorithms import FedAvg
+    from ddl25spring_amd.models import resnet18_cifar
+
+    train = synthetic_images("cifar10", args.train_size, seed=0)
+    test = synthetic_images("cifar10", 2000, seed=1) if args.eval else None
+    dtrain = DeviceImageDataset(train, ctx.device)
+    dtest = DeviceImageDataset(test, ctx.device) if test is not None else None
+    parts = split(args.clients, True, 10, labels=train.labels)
+    model_fn = {"resnet18": resnet18_cifar}[args.model]
+    fl = FedAvg(model_fn, dtrain, parts, lr=args.lr, batch_size=args.batch,
+                local_epochs=args.epochs, client_fraction=1.0, seed=10, test_data=dtest,
+                use_graph=not args.no_graph, eval_every=0)
+
+    for _ in range(args.warmup):
+        fl.round()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    samples = 0
+    for _ in range(args.steps):
+        _, s = fl.round()
+        samples += s
+    ctx.barrier()
+    torch.cuda.synchronize()
+    elapsed = ctx.max_scalar(time.perf_counter() - t0)
+    ms_per_round = 1000.0 * elapsed / args.steps
+    samples_per_s = samples / elapsed
+    rounds_per_s = args.steps / elapsed
+    acc = fl.test() if args.eval else None
+    if ctx.is_main:
+        out = {
+            "metric": METRIC,
+            "value": round(samples_per_s, 1),
+            "unit": "samples/s",
+            "n_gpus": ctx.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_round, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic",
+            "rounds_per_sec": round(rounds_per_s, 4),
+            "local_samples_per_round": samples // max(args.steps, 1),
+            "config": {"model": "resnet18-cifar10", "global_batch": args.batch * args.clients,
+                       "seq_len": None, "parallelism": f"fedavg-{args.clients}clients-dp{ctx.world}",
+                       "clients": args.clients, "local_batch": args.batch,
+                       "local_epochs": args.epochs, "lr": args.lr,
+                       "samples_per_client": args.train_size // args.clients,
+                       "client_slots_per_gpu": fl.slots, "hip_graphs": not args.no_graph},
+        }
+        if acc is not None:
+            out["test_accuracy"] = acc
+        print(json.dumps(out), flush=True)
+    rdist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,87 @@
+"""Simulated Byzantine clients [north-star: the course's announced Part 3 "Attacks & Defenses",
+reference README.md:89-92 / lab/README.md:13-16, has no code].
+
+* ``LabelFlip``     — data poisoning: y -> (C - 1 - y) on the malicious clients' batches.
+* ``SignFlip``      — model poisoning: the malicious update is negated and scaled,
+                      w_k <- w_g - s * (w_k - w_g).
+* ``GaussianNoise`` — the malicious update is replaced by N(0, sigma^2) noise.
+* ``FreeRider``     — sends back the server weights unchanged (no local work).
+"""
+from __future__ import annotations
+
+import torch
+
+
+class Attack:
+    def __init__(self, malicious: list[int] | set[int]):
+        self.malicious = set(int(m) for m in malicious)
+
+    def label_transform_for(self, slot_clients: list[int], num_classes: int):
+        return None
+
+    def poison_updates(self, rows: torch.Tensor, w_global: torch.Tensor, slot_clients: list[int]):
+        pass
+
+    def skip_training(self, client: int) -> bool:
+        return False
+
+
+class LabelFlip(Attack):
+    def label_transform_for(self, slot_clients, num_classes):
+        bad = [i for i, c in enumerate(slot_clients) if c in self.malicious]
+        if not bad:
+            return None
+        mask_cpu = torch.zeros(len(slot_clients), dtype=torch.bool)
+        mask_cpu[bad] = True
+        cache = {}
+
+        def f(y, g0, g1):
+            key = (y.device, g0, g1)
+            if key not in cache:
+                cache[key] = mask_cpu[g0:g1].to(y.device).reshape(-1, *([1] * (y.dim() - 1)))
+            return torch.where(cache[key], (num_classes - 1) - y, y)
+        return f
+
+
+class SignFlip(Attack):
+    def __init__(self, malicious, scale: float = 1.0):
+        super().__init__(malicious)
+        self.scale = scale
+
+    def poison_updates(self, rows, w_global, slot_clients):
+        for i, c in enumerate(slot_clients):
+            if c in self.malicious:
+                rows[i].sub_(w_global).mul_(-self.scale).add_(w_global)
+
+
+class GaussianNoise(Attack):
+    def __init__(self, malicious, sigma: float = 1.0, seed: int = 0):
+        super().__init__(malicious)
+        self.sigma = sigma
+        self.gen = None
+        self.seed = seed
+
+    def poison_updates(self, rows, w_global, slot_clients):
+        for i, c in enumerate(slot_clients):
+            if c in self.malicious:
+                if self.gen is None:
+                    self.gen = torch.Generator(device=rows.device).manual_seed(self.seed)
+                noise = torch.randn(rows.shape[1], generator=self.gen, device=rows.device)
+                rows[i].copy_(w_global + self.sigma * noise)
+
+
+class FreeRider(Attack):
+    def skip_training(self, client):
+        return client in self.malicious
+
+    def poison_updates(self, rows, w_global, slot_clients):
+        for i, c in enumerate(slot_clients):
+            if c in self.malicious:
+                rows[i].copy_(w_global)
+
+
+def make_attack(name: str | None, malicious, **kw):
+    if not name or name == "none":
+        return None
+    return {"label_flip": LabelFlip, "sign_flip": SignFlip, "gaussian": GaussianNoise,
+            "free_rider": FreeRider}[name](malicious, **kw)

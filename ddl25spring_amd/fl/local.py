@@ -1,0 +1,147 @@
+"""Client-batched local training: E epochs of mini-batch SGD for all G client slots of this GPU
+in ONE stream of kernel launches (every launch covers all clients through the group dimension).
+
+Replaces the reference's sequential per-client loop (hfl_complete.py:360-373 calls
+``WeightClient.update`` client after client, each one an ``nn.Module`` replica fed by a CPU
+DataLoader and copied host<->device every round). Here:
+  * weights of all clients live in one flat [G, P] buffer, already on the device;
+  * the round's batch plan (which sample ids each client sees at each step) is computed once on
+    the host (native planner or torch.randperm for DataLoader-identical order) and uploaded once;
+  * the steady-state step (gather+normalise -> fwd -> fused CE -> bwd -> fused SGD) is captured in
+    a HIP graph and replayed, so the inner loop costs one graph launch per step.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .. import optim
+from ..data.split import plan_epoch
+
+
+class LocalTrainer:
+    def __init__(self, net, data, lr: float, batch_size: int, momentum: float = 0.0,
+                 weight_decay: float = 0.0, planner: str = "native", use_graph: bool | None = None,
+                 label_transform=None):
+        self.net, self.data = net, data
+        self.B = batch_size
+        self.opt = optim.SGD(net, lr=lr, momentum=momentum, weight_decay=weight_decay)
+        self.planner = planner
+        dev = net.device
+        self.use_graph = (dev.type == "cuda") if use_graph is None else (use_graph and dev.type == "cuda")
+        self.label_transform = label_transform  # callable(y [G,B]) -> y (attacks)
+        self._graphs: dict = {}
+        self.last_loss = None
+
+    # ---------------------------------------------------------------- one step (eager)
+    def _step(self, idx, g0: int, g1: int):
+        net, st = self.net, self.net.store
+        x, y = self.data.batch(idx)
+        if self.label_transform is not None:
+            y = self.label_transform(y, g0, g1)
+        with st.select(g0, g1):
+            st.grad[g0:g1].zero_()
+            loss, _ = net.train_step(x, y)
+            self.opt.select(g0, g1).step()
+        return loss
+
+    # ---------------------------------------------------------------- graph-captured step
+    def _graph_step(self, idx_host_row: torch.Tensor, G: int):
+        key = (G, self.B)
+        ent = self._graphs.get(key)
+        if ent is None:
+            ent = self._capture(idx_host_row, G)
+            self._graphs[key] = ent
+        graph, static_idx, loss = ent
+        static_idx.copy_(idx_host_row, non_blocking=True)
+        graph.replay()
+        self.last_loss = loss
+
+    def _capture(self, idx_row: torch.Tensor, G: int):
+        st, opt = self.net.store, self.opt
+        # the warm-up steps really train: snapshot and restore so the first graph step is exact
+        snap = (st.data[:G].clone(), st.buffers[:G].clone(),
+                None if opt.mom is None else opt.mom[:G].clone(), opt.steps)
+        static_idx = torch.empty(G, self.B, dtype=torch.int32, device=self.net.device)
+        static_idx.copy_(idx_row)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._step(static_idx, 0, G)
+        torch.cuda.current_stream().wait_stream(s)
+        # zero-initialised momentum == torch's "buffer = first grad" when dampening == 0, so the
+        # frozen first_step=False inside the graph is exact for every step of a round
+        assert opt.dampening == 0.0
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            loss = self._step(static_idx, 0, G)
+        st.data[:G].copy_(snap[0])
+        st.buffers[:G].copy_(snap[1])
+        if snap[2] is not None:
+            opt.mom[:G].copy_(snap[2])
+        opt.steps = snap[3]
+        st.sync_shadow()
+        return graph, static_idx, loss
+
+    # ---------------------------------------------------------------- public
+    def run(self, slot_indices: list[np.ndarray], seeds, epochs: int = 1, generators=None) -> int:
+        """Train slots [0, len(slot_indices)) for `epochs` local epochs; returns #samples seen."""
+        G = len(slot_indices)
+        if G == 0:
+            return 0
+        self.opt.reset_state()
+        sizes = {len(s) for s in slot_indices}
+        samples = 0
+        for ep in range(epochs):
+            if len(sizes) == 1:
+                groups = [(0, G, slot_indices)]
+            else:  # unequal client sizes: run each slot on its own (group-sliced views)
+                groups = [(g, g + 1, [slot_indices[g]]) for g in range(G)]
+            for g0, g1, idxs in groups:
+                sd = seeds[g0:g1]
+                if self.planner == "torch" and generators is not None:
+                    plan = self._torch_plan(idxs, generators[g0:g1])
+                else:
+                    plan = plan_epoch(idxs, self.B, [int(s) + 7919 * ep for s in sd], True, "native")
+                samples += self._run_plan(plan, g0, g1)
+        return samples
+
+    def _torch_plan(self, idxs, gens):
+        count = len(idxs[0])
+        steps = (count + self.B - 1) // self.B
+        out = -np.ones((steps, len(idxs), self.B), dtype=np.int32)
+        for g, (ci, gen) in enumerate(zip(idxs, gens)):
+            perm = torch.randperm(count, generator=gen).numpy()
+            seq = np.asarray(ci)[perm]
+            for s in range(steps):
+                chunk = seq[s * self.B:(s + 1) * self.B]
+                out[s, g, :len(chunk)] = chunk
+        return out
+
+    def _run_plan(self, plan: np.ndarray, g0: int, g1: int) -> int:
+        dev = self.net.device
+        steps = plan.shape[0]
+        full = (plan >= 0).all(axis=(1, 2))
+        plan_dev = torch.from_numpy(plan).to(dev, non_blocking=True)
+        samples = 0
+        G = g1 - g0
+        for s in range(steps):
+            if full[s]:
+                if self.use_graph and g0 == 0:
+                    self._graph_step(plan_dev[s], G)
+                else:
+                    self.last_loss = self._step(plan_dev[s], g0, g1)
+                samples += G * self.B
+            else:
+                n = int((plan[s, 0] >= 0).sum())
+                if (plan[s] >= 0).sum(1).min() == n and (plan[s] >= 0).sum(1).max() == n:
+                    self.last_loss = self._step(plan_dev[s, :, :n].contiguous(), g0, g1)
+                    samples += G * n
+                else:
+                    for g in range(G):
+                        m = int((plan[s, g] >= 0).sum())
+                        if m:
+                            self.last_loss = self._step(plan_dev[s, g:g + 1, :m].contiguous(), g0 + g, g0 + g + 1)
+                            samples += m
+        return samples

@@ -140,7 +140,8 @@ class Net:
 
     # torch.nn.Module-ish conveniences
     def parameters(self):
-        return [self.store.data]
+        """Flat master buffer (a list carrying ``.store`` so ``optim.SGD(net.parameters())`` works)."""
+        return _StoreParams([self.store.data], self.store)
 
     def zero_grad(self, set_to_none: bool = False):
         self.store.zero_grad()
@@ -153,6 +154,12 @@ class Net:
 
     def num_params(self) -> int:
         return self.store.num_params()
+
+
+class _StoreParams(list):
+    def __init__(self, items, store):
+        super().__init__(items)
+        self.store = store
 
 
 class _NetFunction(torch.autograd.Function):

@@ -128,8 +128,26 @@ class ParamStore:
             self.sync_shadow()
 
     # ---------------------------------------------------------------- views
+    _gsl = slice(None)
+
     def _view(self, flat: torch.Tensor, s: Spec) -> torch.Tensor:
-        return flat[:, s.offset:s.offset + s.numel].unflatten(1, s.shape)
+        return flat[self._gsl, s.offset:s.offset + s.numel].unflatten(1, s.shape)
+
+    class _Select:
+        def __init__(self, store, g0, g1):
+            self.store, self.sl = store, slice(g0, g1)
+
+        def __enter__(self):
+            self.prev = self.store._gsl
+            self.store._gsl = self.sl
+            return self.store
+
+        def __exit__(self, *a):
+            self.store._gsl = self.prev
+
+    def select(self, g0: int, g1: int):
+        """Context: layer views cover only client slots [g0, g1) (ragged tail steps)."""
+        return ParamStore._Select(self, g0, g1)
 
     def param(self, name):
         return self._view(self.data, self.specs[name])

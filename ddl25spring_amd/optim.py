@@ -1,0 +1,101 @@
+"""Fused optimizers over a model's flat ParamStore (one kernel for all params of all clients).
+
+Drop-in for the reference's ``torch.optim.SGD`` (hfl_complete.py:196,319), ``Adam`` (intro.py:22,
+generative-modeling.py:154) and ``AdamW`` (vfl.py:50): same hyper-parameters and update rules,
+but one launch over ``G*P`` floats that also refreshes the bf16 weight shadow.
+"""
+from __future__ import annotations
+
+import torch
+
+from .ops import functional as Fn
+
+
+def _store_of(params):
+    from .models.net import Net
+    from .models.params import ParamStore
+    if isinstance(params, Net):
+        return params.store
+    if isinstance(params, ParamStore):
+        return params
+    store = getattr(params, "store", None)
+    if store is None:
+        raise TypeError("ddl25spring_amd optimizers take a native Net / ParamStore "
+                        "(use torch.optim for plain torch modules)")
+    return store
+
+
+class _Base:
+    def __init__(self, params):
+        self.store = _store_of(params)
+        self._g = (0, self.store.G)
+
+    def zero_grad(self, set_to_none: bool = False):
+        g0, g1 = self._g
+        self.store.grad[g0:g1].zero_()
+
+    def select(self, g0: int, g1: int):
+        """Restrict the next steps to client slots [g0, g1)."""
+        self._g = (g0, g1)
+        return self
+
+    def _rows(self, t):
+        g0, g1 = self._g
+        return t[g0:g1]
+
+
+class SGD(_Base):
+    def __init__(self, params, lr: float, momentum: float = 0.0, dampening: float = 0.0,
+                 weight_decay: float = 0.0, nesterov: bool = False):
+        super().__init__(params)
+        self.lr, self.momentum, self.dampening = lr, momentum, dampening
+        self.weight_decay, self.nesterov = weight_decay, nesterov
+        self.mom = torch.zeros_like(self.store.data) if momentum else None
+        self.steps = 0
+
+    def step(self, grad_scale: float = 1.0):
+        st = self.store
+        Fn.sgd_step(self._rows(st.data), self._rows(st.grad),
+                    None if self.mom is None else self._rows(self.mom), self._rows(st.shadow),
+                    self.lr, self.weight_decay, self.momentum, self.dampening, self.nesterov,
+                    first_step=(self.steps == 0), grad_scale=grad_scale)
+        st._shadow_version = st.data._version
+        self.steps += 1
+
+    def reset_state(self):
+        self.steps = 0
+        if self.mom is not None:
+            self.mom.zero_()
+
+
+class Adam(_Base):
+    decoupled = False
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0):
+        super().__init__(params)
+        self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
+        self.m = torch.zeros_like(self.store.data)
+        self.v = torch.zeros_like(self.store.data)
+        self.t = 0
+
+    def step(self, grad_scale: float = 1.0):
+        self.t += 1
+        st = self.store
+        Fn.adam_step(self._rows(st.data), self._rows(st.grad), self._rows(self.m), self._rows(self.v),
+                     self._rows(st.shadow), self.lr, self.betas[0], self.betas[1], self.eps,
+                     self.weight_decay, self.t, self.decoupled, grad_scale)
+        st._shadow_version = st.data._version
+
+    def reset_state(self):
+        self.t = 0
+        self.m.zero_()
+        self.v.zero_()
+
+
+class AdamW(Adam):
+    decoupled = True
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.01):
+        super().__init__(params, lr, betas, eps, weight_decay)

@@ -1,0 +1,145 @@
+"""Process / device / communicator bootstrap.
+
+One process per GPU; ``torch.distributed`` with backend ``nccl`` (= RCCL on ROCm, over xGMI) for
+device tensors, ``gloo`` for CPU runs and tests. Rendezvous follows the torchrun / reference env
+contract (``MASTER_ADDR``/``MASTER_PORT``/``RANK``/``WORLD_SIZE``; reference
+lab/tutorial_1b/DP/gradient_aggr/intro_DP_GA.py:11-15 reads the rank from argv and hard-codes
+localhost:29500 — both spellings are accepted here).
+
+Sub-communicators are created *collectively* (every rank calls ``new_group`` for every group in
+the same order) which fixes the reference's non-collective group creation
+(intro_PP_1F1B_MP.py:31-36).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass, field
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    device: torch.device = field(default_factory=lambda: torch.device("cpu"))
+    backend: str = "none"
+    groups: dict = field(default_factory=dict)
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world > 1 and dist.is_initialized()
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    # ------------------------------------------------------------- collectives (no-ops at world 1)
+    def all_reduce(self, t: torch.Tensor, op=None, group=None):
+        if self.is_distributed:
+            dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=group)
+        return t
+
+    def broadcast(self, t: torch.Tensor, src: int = 0, group=None):
+        if self.is_distributed:
+            dist.broadcast(t, src, group=group)
+        return t
+
+    def all_gather_into(self, out: torch.Tensor, t: torch.Tensor, group=None):
+        if self.is_distributed:
+            dist.all_gather_into_tensor(out, t, group=group)
+        else:
+            out.copy_(t.reshape(out.shape))
+        return out
+
+    def all_to_all_single(self, out: torch.Tensor, t: torch.Tensor, group=None):
+        if self.is_distributed:
+            dist.all_to_all_single(out, t, group=group)
+        else:
+            out.copy_(t)
+        return out
+
+    def barrier(self):
+        if self.is_distributed:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+    def max_scalar(self, v: float) -> float:
+        if not self.is_distributed:
+            return v
+        t = torch.tensor([v], dtype=torch.float64,
+                         device=self.device if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_scalar(self, v: float) -> float:
+        if not self.is_distributed:
+            return v
+        t = torch.tensor([v], dtype=torch.float64,
+                         device=self.device if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def new_groups(self, name: str, partition: list[list[int]]):
+        """Collective creation of a partition of the ranks into sub-groups; returns my group."""
+        mine = None
+        for ranks in partition:
+            g = dist.new_group(ranks=ranks) if self.is_distributed else None
+            if self.rank in ranks:
+                mine = g
+        self.groups[name] = mine
+        return mine
+
+
+_CTX: DistContext | None = None
+
+
+def init(backend: str | None = None, device: str | None = None, rank: int | None = None,
+         world_size: int | None = None, timeout_s: int = 600) -> DistContext:
+    """Initialise from env (torchrun) or explicit args. Safe to call once per process."""
+    global _CTX
+    if _CTX is not None:
+        return _CTX
+    rank = int(os.environ.get("RANK", rank if rank is not None else 0))
+    world = int(os.environ.get("WORLD_SIZE", world_size if world_size is not None else 1))
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    want_gpu = device != "cpu" and (device is not None and device.startswith("cuda") or
+                                    (device is None and torch.cuda.is_available()))
+    if want_gpu:
+        ndev = torch.cuda.device_count()
+        dev = torch.device("cuda", local % max(ndev, 1))
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
+    backend = backend or ("nccl" if dev.type == "cuda" else "gloo")
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = dev
+        dist.init_process_group(backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    _CTX = DistContext(rank, world, local, dev, backend if world > 1 else "none")
+    return _CTX
+
+
+def context() -> DistContext:
+    return _CTX if _CTX is not None else init()
+
+
+def shutdown():
+    global _CTX
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    _CTX = None
+
+
+def set_context(ctx: DistContext | None):
+    global _CTX
+    _CTX = ctx
