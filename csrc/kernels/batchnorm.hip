@@ -5,10 +5,15 @@
 //   bn_finalize : stats -> (scale, shift, mean, rstd) + running-stat update   (G*C threads)
 //   bn_apply    : y = act(x*scale + shift [+ r*rscale + rshift | + r])       (one HBM pass)
 // which also fuses the ResNet residual join (identity or projected shortcut) and the ReLU.
-// Backward is two passes:
-//   bn_bwd_reduce : sum(dy_m), sum(dy_m * xhat)   with dy_m = dy * (y > 0) recomputed in-register
-//   bn_bwd_apply  : dx = gamma*rstd*(dy_m - sum_dy/M - xhat*sum_dyx/M)   (+ emits dy_m if asked)
+// Backward is three launches:
+//   bn_bwd_reduce : s0 = sum(dy_m), s1 = sum(dy_m * xhat)  (dy_m = dy * (y > 0) recomputed)
+//   bn_bwd_coef   : per channel  dx = A*dy_m + B*x + Cc     (folds gamma, rstd, mean, s0, s1)
+//   bn_bwd_apply  : one HBM pass  (+ emits dy_m for the residual branch if asked)
 // The reduce pass accumulates d(gamma), d(beta) directly into the fp32 flat grad buffer.
+//
+// Streaming layout shared by all passes: a 256-thread block covers RPI = 256/(C/8) pixel rows, each
+// thread owns one fixed 8-channel chunk (its per-channel coefficients stay in registers, no index
+// division inside the loop), blockIdx.y = client group.
 //
 // Reference parity: nn.BatchNorm1d/2d semantics (momentum 0.1, eps 1e-5, unbiased running var)
 // used by the VAE models (reference lab/tutorial_2a/generative-modeling.py:21-45,
@@ -71,22 +76,42 @@ DDL_API int ddl_bn_finalize(const BNArgs* a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+__device__ __forceinline__ void load8f(const float* p, float* v) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// blocks per group for a streaming pass over M rows with RPI rows per block-iteration
+static unsigned stream_blocks(long long M, int RPI, int G, int rows_per_thread) {
+  long long want = (M + (long long)RPI * rows_per_thread - 1) / ((long long)RPI * rows_per_thread);
+  long long cap = (2048 + G - 1) / G;
+  if (cap < 8) cap = 8;
+  if (want > cap) want = cap;
+  if (want < 1) want = 1;
+  return (unsigned)want;
+}
+
 // ---------------------------------------------------------------------------------------------
 // y = act(x*scale[c] + shift[c] + residual_term)     residual_term = r*rs[c]+rb[c] | r | 0
 // act: 0 none, 1 relu, 2 leaky(0.01)
-__global__ void bn_apply_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
-                                const float* __restrict__ shift, const bf16_t* __restrict__ r,
-                                const float* __restrict__ rscale, const float* __restrict__ rshift,
-                                bf16_t* __restrict__ y, long long per_group, int C, int G, int act) {
-  const long long chunks_pg = per_group / 8;
-  const long long total = chunks_pg * G;
-  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
-       t += (long long)gridDim.x * blockDim.x) {
-    const int g = (int)(t / chunks_pg);
-    const long long e = t * 8;
-    const int c0 = (int)((e - (long long)g * per_group) % C);
-    const float* sc = scale + (long long)g * C + c0;
-    const float* sh = shift + (long long)g * C + c0;
+__global__ __launch_bounds__(256) void bn_apply_kernel(
+    const bf16_t* __restrict__ x, const float* __restrict__ scale, const float* __restrict__ shift,
+    const bf16_t* __restrict__ r, const float* __restrict__ rscale, const float* __restrict__ rshift,
+    bf16_t* __restrict__ y, long long M, int C, int act) {
+  const int g = blockIdx.y;
+  const int TPR = C >> 3, RPI = 256 / TPR;
+  const int cc = threadIdx.x % TPR, row = threadIdx.x / TPR;
+  if (row >= RPI) return;
+  float sc[8], sh[8], rsc[8], rsh[8];
+  load8f(scale + (long long)g * C + cc * 8, sc);
+  load8f(shift + (long long)g * C + cc * 8, sh);
+  if (rscale) {
+    load8f(rscale + (long long)g * C + cc * 8, rsc);
+    load8f(rshift + (long long)g * C + cc * 8, rsh);
+  }
+  const long long base = (long long)g * M * C + cc * 8;
+  for (long long p = (long long)blockIdx.x * RPI + row; p < M; p += (long long)gridDim.x * RPI) {
+    const long long e = base + p * C;
     float v[8];
     unpack8(*(const i4v*)(x + e), v);
 #pragma unroll
@@ -95,8 +120,6 @@ __global__ void bn_apply_kernel(const bf16_t* __restrict__ x, const float* __res
       float rv[8];
       unpack8(*(const i4v*)(r + e), rv);
       if (rscale) {
-        const float* rsc = rscale + (long long)g * C + c0;
-        const float* rsh = rshift + (long long)g * C + c0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] += rv[k] * rsc[k] + rsh[k];
       } else {
@@ -115,28 +138,20 @@ __global__ void bn_apply_kernel(const bf16_t* __restrict__ x, const float* __res
   }
 }
 
-static int grid_for(long long work, int block) {
-  long long b = (work + block - 1) / block;
-  if (b > 4096) b = 4096;
-  if (b < 1) b = 1;
-  return (int)b;
-}
-
 DDL_API int ddl_bn_apply(const void* x, const float* scale, const float* shift, const void* r,
                          const float* rscale, const float* rshift, void* y, long long per_group,
                          int C, int G, int act, hipStream_t s) {
-  if (C % 8 || per_group % C) return (int)hipErrorInvalidValue;
-  const long long chunks = per_group / 8 * G;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(chunks, 256)), dim3(256), 0, s,
+  if (C % 8 || C / 8 > 256 || per_group % C) return (int)hipErrorInvalidValue;
+  const long long M = per_group / C;
+  const int RPI = 256 / (C / 8);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(stream_blocks(M, RPI, G, 4), G), dim3(256), 0, s,
                      (const bf16_t*)x, scale, shift, (const bf16_t*)r, rscale, rshift, (bf16_t*)y,
-                     per_group, C, G, act);
+                     M, C, act);
   return (int)hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
 // Backward reduce: per (g, c): s0 = sum dy_m, s1 = sum dy_m * xhat ; dy_m = dy * (ymask > 0)
-// Thread layout: TPR = C/8 threads per pixel row (one 16-B chunk each), RPI = 256/TPR rows per
-// iteration; partial sums folded through LDS, one atomic pair per (block, channel).
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ ymask, const bf16_t* __restrict__ x,
     const float* __restrict__ mean, const float* __restrict__ rstd, float* __restrict__ sums,
@@ -150,15 +165,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
   float s0[8], s1[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) s0[k] = s1[k] = 0.f;
-  const long long base = (long long)g * M * C;
-  const float* mu = mean + (long long)g * C + cc * 8;
-  const float* rs = rstd + (long long)g * C + cc * 8;
   float m8[8], r8[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) { m8[k] = mu[k]; r8[k] = rs[k]; }
+  load8f(mean + (long long)g * C + cc * 8, m8);
+  load8f(rstd + (long long)g * C + cc * 8, r8);
+  const long long base = (long long)g * M * C + cc * 8;
   if (active) {
     for (long long p = (long long)blockIdx.x * RPI + row; p < M; p += (long long)gridDim.x * RPI) {
-      const long long e = base + p * C + cc * 8;
+      const long long e = base + p * C;
       float d[8], xv[8];
       unpack8(*(const i4v*)(dy + e), d);
       unpack8(*(const i4v*)(x + e), xv);
@@ -210,32 +223,47 @@ DDL_API int ddl_bn_bwd_reduce(const void* dy, const void* ymask, const void* x, 
                               long long gs_param, long long M, int C, int G, hipStream_t s) {
   if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
   const int RPI = 256 / (C / 8);
-  long long want = (M + (long long)RPI * 16 - 1) / ((long long)RPI * 16);  // >=16 rows/thread
-  long long cap = (1024 + G - 1) / G;
-  if (cap < 4) cap = 4;
-  if (want > cap) want = cap;
-  if (want < 1) want = 1;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((unsigned)want, G), dim3(256), 0, s,
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(stream_blocks(M, RPI, G, 16), G), dim3(256), 0, s,
                      (const bf16_t*)dy, (const bf16_t*)ymask, (const bf16_t*)x, mean, rstd, sums,
                      dgamma, dbeta, gs_param, M, C);
   return (int)hipGetLastError();
 }
 
-__global__ void bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ ymask,
-                                    const bf16_t* __restrict__ x, const float* __restrict__ mean,
-                                    const float* __restrict__ rstd, const float* __restrict__ gamma,
-                                    long long gs_param, const float* __restrict__ sums,
-                                    bf16_t* __restrict__ dx, bf16_t* __restrict__ dym_out,
-                                    long long M, int C, int G) {
-  const long long per_group = M * C;
-  const long long chunks_pg = per_group / 8;
-  const long long total = chunks_pg * G;
+// dx = gamma*rstd*(dy_m - s0/M - xhat*s1/M) = A*dy_m + B*x + Cc
+__global__ void bn_bwd_coef_kernel(const float* __restrict__ mean, const float* __restrict__ rstd,
+                                   const float* __restrict__ gamma, long long gs_param,
+                                   const float* __restrict__ sums, float* __restrict__ coef,
+                                   long long M, int C, int G) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= G * C) return;
+  const int g = i / C, c = i - g * C;
   const float invM = 1.f / (float)M;
-  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
-       t += (long long)gridDim.x * blockDim.x) {
-    const int g = (int)(t / chunks_pg);
-    const long long e = t * 8;
-    const int c0 = (int)((e - (long long)g * per_group) % C);
+  const float mu = mean[i], rs = rstd[i];
+  const float ga = gamma ? gamma[(long long)g * gs_param + c] : 1.f;
+  const float s0 = sums[(long long)g * 2 * C + c], s1 = sums[(long long)g * 2 * C + C + c];
+  const float A = ga * rs;
+  const float B = -A * rs * s1 * invM;
+  coef[(long long)g * 3 * C + c] = A;
+  coef[(long long)g * 3 * C + C + c] = B;
+  coef[(long long)g * 3 * C + 2 * C + c] = -A * s0 * invM - B * mu;
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ ymask, const bf16_t* __restrict__ x,
+    const float* __restrict__ coef, bf16_t* __restrict__ dx, bf16_t* __restrict__ dym_out,
+    long long M, int C) {
+  const int g = blockIdx.y;
+  const int TPR = C >> 3, RPI = 256 / TPR;
+  const int cc = threadIdx.x % TPR, row = threadIdx.x / TPR;
+  if (row >= RPI) return;
+  float A[8], B[8], Cc[8];
+  const float* cg = coef + (long long)g * 3 * C + cc * 8;
+  load8f(cg, A);
+  load8f(cg + C, B);
+  load8f(cg + 2 * C, Cc);
+  const long long base = (long long)g * M * C + cc * 8;
+  for (long long p = (long long)blockIdx.x * RPI + row; p < M; p += (long long)gridDim.x * RPI) {
+    const long long e = base + p * C;
     float d[8], xv[8];
     unpack8(*(const i4v*)(dy + e), d);
     unpack8(*(const i4v*)(x + e), xv);
@@ -246,29 +274,24 @@ __global__ void bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t*
       for (int k = 0; k < 8; ++k) if (!(yv[k] > 0.f)) d[k] = 0.f;
     }
     if (dym_out) *(i4v*)(dym_out + e) = pack8(d);
-    const float* sg = sums + (long long)g * 2 * C;
     float o[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int c = c0 + k;
-      const float mu = mean[(long long)g * C + c], rs = rstd[(long long)g * C + c];
-      const float ga = gamma ? gamma[(long long)g * gs_param + c] : 1.f;
-      const float xh = (xv[k] - mu) * rs;
-      o[k] = ga * rs * (d[k] - sg[c] * invM - xh * sg[C + c] * invM);
-    }
+    for (int k = 0; k < 8; ++k) o[k] = A[k] * d[k] + B[k] * xv[k] + Cc[k];
     *(i4v*)(dx + e) = pack8(o);
   }
 }
 
 DDL_API int ddl_bn_bwd_apply(const void* dy, const void* ymask, const void* x, const float* mean,
                              const float* rstd, const float* gamma, long long gs_param,
-                             const float* sums, void* dx, void* dym_out, long long M, int C, int G,
-                             hipStream_t s) {
-  if (C % 8) return (int)hipErrorInvalidValue;
-  const long long chunks = M * C / 8 * G;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(chunks, 256)), dim3(256), 0, s,
-                     (const bf16_t*)dy, (const bf16_t*)ymask, (const bf16_t*)x, mean, rstd, gamma,
-                     gs_param, sums, (bf16_t*)dx, (bf16_t*)dym_out, M, C, G);
+                             const float* sums, float* coef_ws, void* dx, void* dym_out,
+                             long long M, int C, int G, hipStream_t s) {
+  if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((G * C + 255) / 256), dim3(256), 0, s, mean, rstd,
+                     gamma, gs_param, sums, coef_ws, M, C, G);
+  const int RPI = 256 / (C / 8);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_blocks(M, RPI, G, 4), G), dim3(256), 0, s,
+                     (const bf16_t*)dy, (const bf16_t*)ymask, (const bf16_t*)x, coef_ws,
+                     (bf16_t*)dx, (bf16_t*)dym_out, M, C);
   return (int)hipGetLastError();
 }
 

@@ -7,27 +7,28 @@
 //   DGRAD : dx[q=(n,h,w)][p=c]         = sum_{(r,s,k)}  W[k][(r,s,c)]     * dY[pix'(q,r,s)][k]
 //   WGRAD : dW[p=k][q=(r,s,c)]        += sum_{(n,p,q)}  dY[(n,p,q)][k]    * X[pix(n,p,q,r,s)][c]
 //
-// Every mode is written as D[p][q] = sum_k Pop[p][k] * Qop[q][k] with the MFMA A operand = Pop,
-// B operand = Qop, so the accumulator lane layout (lane holds 4 consecutive p for one q) gives
-// 8-byte contiguous NHWC stores in FWD/DGRAD and 64-byte row segments for the fp32 WGRAD atomics.
+// Every mode is D[p][q] = sum_k Pop[p][k] * Qop[q][k] with the MFMA A operand = Pop, B = Qop, so
+// the accumulator layout (lane holds 4 consecutive p for one q) gives 8-byte contiguous NHWC
+// stores in FWD/DGRAD and 64-byte row segments for the fp32 WGRAD atomics.
 //
-// Operands are staged global -> registers -> LDS (register staging: the implicit-GEMM gathers
-// are predicated / zero-filled per 16-byte chunk, which an LDS-DMA cannot express) into a
-// double-buffered LDS ring with one barrier per K-step. Two LDS images are used:
-//   * K-major  ([BK/32][rows][32] bf16, 16-B chunk XOR swizzle, fragment = one ds_read_b128)
-//     for operands whose reduction index is memory-contiguous (weights / activations in FWD,
-//     dY in DGRAD);
-//   * MN-major ([BK][cols] bf16, 16-B chunk XOR swizzle, fragment = two ds_read_b64_tr_b16)
-//     for operands whose *output* index is contiguous (W in DGRAD, dY and X in WGRAD). The
-//     gfx950 transpose read turns them into K-contiguous MFMA fragments with no extra pass.
-// Both swizzles are conflict-free for the fragment reads (derivation in docs/KERNELS.md).
+// Operand staging: LDS-DMA (`global_load_lds_dwordx4`, 1 KiB per wave-instruction) into an
+// NSTAGE-deep LDS ring, one raw s_barrier per K-step and COUNTED `s_waitcnt vmcnt(N)` so the next
+// NSTAGE-2 stages stay in flight across the barrier (cdna_hip_programming.md §5 "Pipelining across
+// barriers"). The implicit-GEMM gather is expressed purely through the per-lane SOURCE address:
+// padding / out-of-range taps point at a zero page, and the LDS swizzles are applied by
+// permuting which logical 16-byte chunk each lane fetches (the DMA destination is lane-linear).
+// Two LDS images:
+//   * K-major  [BK/32][rows][32] bf16, 16-B chunk XOR swizzle -> one ds_read_b128 per fragment,
+//     for operands whose reduction index is contiguous (W and X in FWD, dY in DGRAD);
+//   * MN-major [BK][cols] bf16, 16-B chunk XOR swizzle -> two ds_read_b64_tr_b16 per fragment
+//     (gfx950 transpose read), for operands whose output index is contiguous (W in DGRAD, dY and
+//     X in WGRAD).
+// Both swizzles are bank-conflict-free for the fragment reads.
+// Workgroup = 4 waves (2x2) on a BP x BQ tile; blockIdx.z = client group, blockIdx.y = split-K
+// slice (WGRAD), blockIdx.x = tile id remapped XCD-aware.
 //
-// Each workgroup is 4 waves (2x2) computing a BP x BQ tile; blockIdx.z = client group,
-// blockIdx.y = split-K slice (WGRAD), blockIdx.x = tile id remapped XCD-aware.
-//
-// Reference parity: replaces the stock nn.Conv2d / nn.Linear calls of MnistCnn
-// (reference lab/tutorial_1a/hfl_complete.py:43-61) and the ResNet convs of the
-// north-star configs.
+// Reference parity: replaces the stock nn.Conv2d / nn.Linear of MnistCnn
+// (reference lab/tutorial_1a/hfl_complete.py:43-61) and the ResNets of the north-star configs.
 #include "ddl_common.h"
 
 struct ConvArgs {
@@ -39,6 +40,7 @@ struct ConvArgs {
   const float* bias;     // FWD: [K] fp32 (optional)
   const void* residual;  // DGRAD: bf16 added to dx (optional), same layout as out
   const void* mask;      // DGRAD: dx *= (mask > 0) (optional), same layout as out
+  const void* zero;      // >= 64 zero bytes in global memory (DMA source for padding)
   long long x_gs, w_gs, dy_gs, out_gs, bias_gs, stats_gs;
   int G, N, H, W, C, K, R, S, P, Q, stride, pad;
   int relu, accumulate, split_k, reserved;
@@ -54,16 +56,27 @@ __device__ __forceinline__ int mn_swz(int k) {
   else
     return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
 }
-template <int ROWS>
-__device__ __forceinline__ int km_off(int row, int kc) {
-  return (kc >> 2) * ROWS * 64 + row * 64 + (((kc & 3) ^ km_swz(row)) << 4);
-}
-template <int COLS>
-__device__ __forceinline__ int mn_off(int krow, int cc) {
-  return krow * COLS * 2 + ((cc ^ mn_swz<COLS>(krow)) << 4);
-}
 
 typedef __attribute__((address_space(3))) s4v lds_s4v;
+
+// x / d for 0 <= x < 2^31 via a multiply-high (round-up method); built once per block.
+struct FastDiv {
+  uint32_t m;
+  int s;  // 0 => d == 1
+};
+__device__ __forceinline__ FastDiv make_fdiv(uint32_t d) {
+  FastDiv f;
+  if (d <= 1) { f.m = 0; f.s = 0; return f; }
+  const int l = 32 - __clz(d - 1);
+  f.m = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+  f.s = l;
+  return f;
+}
+__device__ __forceinline__ int fdiv(int x, FastDiv f) {
+  if (f.s == 0) return x;
+  const uint32_t t = __umulhi((uint32_t)x, f.m);
+  return (int)((t + (((uint32_t)x - t) >> 1)) >> (f.s - 1));
+}
 
 template <int ROWS>
 __device__ __forceinline__ s8v km_frag(const char* lds, int rb, int u, int lane) {
@@ -87,23 +100,39 @@ __device__ __forceinline__ s8v mn_frag(const char* lds, int cb, int u, int lane)
   return r;
 }
 
-__device__ __forceinline__ i4v ld16(const bf16_t* p) { return *(const i4v*)p; }
-__device__ __forceinline__ i4v zero16() { i4v z = {0, 0, 0, 0}; return z; }
+// one LDS-DMA wave-instruction: lane L's 16 source bytes land at lds_base + 16*L
+__device__ __forceinline__ void dma16(const void* src, char* lds_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
 
-template <int MODE, int BP, int BQ, int BK>
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void cta_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Wave-instruction geometry of one operand tile image (per K-step):
+//   K-major  ROWS x BK : NI = ROWS*BK/512 instructions, instr j -> sub-tile u = j/(ROWS/16),
+//                        rows 16*(j%(ROWS/16)) .. +15 ; lane L -> row +L/4, phys chunk L%4
+//   MN-major BK x COLS : NI = BK*COLS/512, instr j -> k-rows (512/COLS)*j .. ; lane L ->
+//                        k-row + L/(COLS/8), phys chunk L%(COLS/8)
+template <int MODE, int BP, int BQ, int BK, int NS>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   constexpr int P_BYTES = BP * BK * 2, Q_BYTES = BQ * BK * 2, STAGE = P_BYTES + Q_BYTES;
   constexpr int WP = BP / 2, WQ = BQ / 2, TP = WP / 16, TQ = WQ / 16;
-  // operand image kinds
   constexpr bool P_KMAJOR = (MODE == MODE_FWD);
   constexpr bool Q_KMAJOR = (MODE != MODE_WGRAD);
-  // load partitioning
-  constexpr int KCPR = BK / 8;                        // 16B chunks per K-major row
-  constexpr int P_NL = P_KMAJOR ? BP * KCPR / 256 : BK * (BP / 8) / 256;
-  constexpr int Q_NL = Q_KMAJOR ? BQ * KCPR / 256 : BK * (BQ / 8) / 256;
-  static_assert(P_NL >= 1 && Q_NL >= 1, "tile too small for 256 threads");
+  constexpr int P_NI = BP * BK / 512, Q_NI = BQ * BK / 512;  // wave-instructions per tile
+  constexpr int P_PW = P_NI / 4, Q_PW = Q_NI / 4;            // per wave
+  constexpr int LPS = P_PW + Q_PW;                           // DMA instructions per wave per stage
+  static_assert(P_PW >= 1 && Q_PW >= 1, "tile too small");
 
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wp = wid >> 1, wq = wid & 1;
@@ -112,164 +141,167 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   const int st = a.stride, pd = a.pad;
   const int RSC = R * S * C;
 
-  int Pd, Qd;
-  long long Kr;
+  int Pd, Qd, Kr;
   if constexpr (MODE == MODE_FWD) { Pd = K; Qd = a.N * P * Q; Kr = RSC; }
-  else if constexpr (MODE == MODE_DGRAD) { Pd = C; Qd = a.N * H * W; Kr = (long long)R * S * K; }
-  else { Pd = K; Qd = RSC; Kr = (long long)a.N * P * Q; }
+  else if constexpr (MODE == MODE_DGRAD) { Pd = C; Qd = a.N * H * W; Kr = R * S * K; }
+  else { Pd = K; Qd = RSC; Kr = a.N * P * Q; }
+  const FastDiv div_pq = make_fdiv(P * Q), div_q = make_fdiv(Q);
 
   const int ntp = (Pd + BP - 1) / BP;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int p0 = (tile % ntp) * BP, q0 = (tile / ntp) * BQ;
-  const int nk_total = (int)((Kr + BK - 1) / BK);
+  const int nk_total = (Kr + BK - 1) / BK;
   const int per = (nk_total + gridDim.y - 1) / gridDim.y;
   const int kt0 = blockIdx.y * per;
   const int kt1 = min(nk_total, kt0 + per);
   if (kt0 >= kt1) return;
+  const int nk = kt1 - kt0;
 
   const bf16_t* X = (const bf16_t*)a.x + (long long)g * a.x_gs;
   const bf16_t* Wt = (const bf16_t*)a.w + (long long)g * a.w_gs;
   const bf16_t* DY = (const bf16_t*)a.dy + (long long)g * a.dy_gs;
+  const bf16_t* ZERO = (const bf16_t*)a.zero;
 
-  // ---------------- per-thread loader state ----------------
-  // K-major loaders: fixed chunk column kc, rows r_i = tid/KCPR + i*(256/KCPR)
-  const int kc = tid % KCPR;
-  const int krow0 = tid / KCPR;
-  constexpr int KRSTEP = 256 / KCPR;
-  // Q K-major gather precompute (FWD: X rows = output pixels; DGRAD: dY rows = input pixels)
-  int qb[Q_KMAJOR ? Q_NL : 1], qh[Q_KMAJOR ? Q_NL : 1], qw[Q_KMAJOR ? Q_NL : 1];
-  // MN-major loaders: fixed column chunk cc, rows k_i = tid/CPR + i*(256/CPR)
-  constexpr int P_CPR = BP / 8, Q_CPR = BQ / 8;
-  const int p_cc = tid % P_CPR, p_kr0 = tid / P_CPR;
-  const int q_cc = tid % Q_CPR, q_kr0 = tid / Q_CPR;
-  // WGRAD X-gather column precompute
-  int wg_r = 0, wg_s = 0, wg_c = 0;
-  bool wg_cvalid = false;
-
-  if constexpr (Q_KMAJOR) {
+  // ---------------- per-lane DMA source precompute ----------------
+  // P operand
+  int pr_row[P_PW], pr_col[P_PW];  // K-major: (row, k-offset within stage) | MN-major: (k-row, col)
 #pragma unroll
-    for (int i = 0; i < Q_NL; ++i) {
-      const int qq = q0 + krow0 + i * KRSTEP;
+  for (int i = 0; i < P_PW; ++i) {
+    const int j = wid + 4 * i;
+    if constexpr (P_KMAJOR) {
+      const int u = j / (BP / 16), rb = 16 * (j % (BP / 16));
+      const int row = rb + lane / 4;
+      pr_row[i] = row;
+      pr_col[i] = u * 32 + (((lane & 3) ^ km_swz(row)) << 3);
+    } else {
+      constexpr int CPR = BP / 8, RPIN = 512 / BP;
+      const int kr = RPIN * j + lane / CPR;
+      pr_row[i] = kr;
+      pr_col[i] = ((lane % CPR) ^ mn_swz<BP>(kr)) << 3;
+    }
+  }
+  // Q operand
+  int qa[Q_PW], qb[Q_PW], qc[Q_PW], qd[Q_PW];
+#pragma unroll
+  for (int i = 0; i < Q_PW; ++i) {
+    const int j = wid + 4 * i;
+    if constexpr (Q_KMAJOR) {
+      const int u = j / (BQ / 16), rb = 16 * (j % (BQ / 16));
+      const int row = rb + lane / 4;
+      qd[i] = u * 32 + (((lane & 3) ^ km_swz(row)) << 3);  // k offset within stage
+      const int qq = q0 + row;
       if (qq < Qd) {
         if constexpr (MODE == MODE_FWD) {
           const int n = qq / (P * Q), rem = qq - n * (P * Q);
           const int op = rem / Q, oq = rem - op * Q;
-          qb[i] = n * H * W;
-          qh[i] = op * st - pd;
-          qw[i] = oq * st - pd;
+          qa[i] = n * H * W;
+          qb[i] = op * st - pd;
+          qc[i] = oq * st - pd;
         } else {
           const int n = qq / (H * W), rem = qq - n * (H * W);
           const int h = rem / W, w = rem - h * W;
-          qb[i] = n * P * Q;
-          qh[i] = h + pd;
-          qw[i] = w + pd;
+          qa[i] = n * P * Q;
+          qb[i] = h + pd;
+          qc[i] = w + pd;
         }
       } else {
+        qa[i] = 0;
+        qb[i] = -(1 << 28);
+        qc[i] = -(1 << 28);
+      }
+    } else {  // WGRAD X gather MN-major: k-row = pixel, col chunk = (r,s,c)
+      constexpr int CPR = BQ / 8, RPIN = 512 / BQ;
+      const int kr = RPIN * j + lane / CPR;
+      const int col = q0 + (((lane % CPR) ^ mn_swz<BQ>(kr)) << 3);
+      qd[i] = kr;
+      if (col < Qd) {
+        const int rs = col / C;
+        qc[i] = col - rs * C;
+        qa[i] = rs / S;
+        qb[i] = rs - qa[i] * S;
+      } else {
+        qa[i] = -(1 << 28);
         qb[i] = 0;
-        qh[i] = -(1 << 28);
-        qw[i] = -(1 << 28);
+        qc[i] = 0;
       }
     }
   }
-  if constexpr (MODE == MODE_WGRAD) {
-    const int col = q0 + q_cc * 8;
-    wg_cvalid = col < Qd;
-    const int rs = col / C;
-    wg_c = col - rs * C;
-    wg_r = rs / S;
-    wg_s = rs - wg_r * S;
+
+  // running (r, s, channel-offset) of the reduction index for FWD/DGRAD: issue() is called for
+  // consecutive K-steps, so the tap decomposition advances incrementally (no divisions in-loop)
+  const int CR = (MODE == MODE_FWD) ? C : K;  // contiguous reduction run per tap
+  int kg_run = kt0 * BK, t_r = 0, t_s = 0, t_c = 0;
+  if constexpr (MODE != MODE_WGRAD) {
+    const int rs = kg_run / CR;
+    t_c = kg_run - rs * CR;
+    t_r = rs / S;
+    t_s = rs - t_r * S;
   }
 
-  i4v rp[P_NL], rq[Q_NL];
-
-  auto load_tiles = [&](int kt) {
-    const long long kg = (long long)kt * BK;
-    // ---- P operand ----
-    if constexpr (MODE == MODE_FWD) {  // W K-major rows = out channels
+  auto issue = [&](int slot) {
+    char* Ps = smem + slot * STAGE;
+    char* Qs = Ps + P_BYTES;
+    const int kg = kg_run;
+    // ---- P ----
 #pragma unroll
-      for (int i = 0; i < P_NL; ++i) {
-        const int kk = p0 + krow0 + i * KRSTEP;
-        rp[i] = (kk < K) ? ld16(Wt + (long long)kk * RSC + kg + kc * 8) : zero16();
+    for (int i = 0; i < P_PW; ++i) {
+      const int j = wid + 4 * i;
+      const bf16_t* src = ZERO;
+      if constexpr (MODE == MODE_FWD) {
+        const int kk = p0 + pr_row[i];
+        if (kk < K) src = Wt + (long long)kk * RSC + kg + pr_col[i];
+      } else if constexpr (MODE == MODE_DGRAD) {
+        const int c = p0 + pr_col[i];
+        if (c < C) src = Wt + (long long)(t_c + pr_row[i]) * RSC + (t_r * S + t_s) * C + c;
+      } else {
+        const int pix = kg + pr_row[i];
+        const int kch = p0 + pr_col[i];
+        if (pix < Kr && kch < K) src = DY + (long long)pix * K + kch;
       }
-    } else if constexpr (MODE == MODE_DGRAD) {  // W MN-major: rows = reduction (k), cols = c
-      const int rs = (int)(kg / K);
-      const int k0 = (int)(kg - (long long)rs * K);
-      const int c = p0 + p_cc * 8;
-#pragma unroll
-      for (int i = 0; i < P_NL; ++i) {
-        const int kr = p_kr0 + i * (256 / P_CPR);
-        rp[i] = (c < C) ? ld16(Wt + (long long)(k0 + kr) * RSC + rs * C + c) : zero16();
-      }
-    } else {  // WGRAD: dY MN-major rows = pixels, cols = out channels
-      const int kch = p0 + p_cc * 8;
-#pragma unroll
-      for (int i = 0; i < P_NL; ++i) {
-        const long long pix = kg + p_kr0 + i * (256 / P_CPR);
-        rp[i] = (pix < Kr && kch < K) ? ld16(DY + pix * K + kch) : zero16();
-      }
+      dma16(src, Ps + j * 1024);
     }
-    // ---- Q operand ----
-    if constexpr (MODE == MODE_FWD) {  // X gather K-major
-      const int rs = (int)(kg / C);
-      const int c = (int)(kg - (long long)rs * C) + kc * 8;
-      const int r = rs / S, s = rs - r * S;
+    // ---- Q ----
 #pragma unroll
-      for (int i = 0; i < Q_NL; ++i) {
-        const int ih = qh[i] + r, iw = qw[i] + s;
-        const bool ok = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-        rq[i] = ok ? ld16(X + ((long long)(qb[i] + ih * W + iw)) * C + c) : zero16();
-      }
-    } else if constexpr (MODE == MODE_DGRAD) {  // dY gather K-major
-      const int rs = (int)(kg / K);
-      const int k0 = (int)(kg - (long long)rs * K) + kc * 8;
-      const int r = rs / S, s = rs - r * S;
-#pragma unroll
-      for (int i = 0; i < Q_NL; ++i) {
-        int ph = qh[i] - r, pw = qw[i] - s;
+    for (int i = 0; i < Q_PW; ++i) {
+      const int j = wid + 4 * i;
+      const bf16_t* src = ZERO;
+      if constexpr (MODE == MODE_FWD) {
+        const int ih = qb[i] + t_r, iw = qc[i] + t_s;
+        if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+          src = X + (long long)(qa[i] + ih * W + iw) * C + t_c + qd[i];
+      } else if constexpr (MODE == MODE_DGRAD) {
+        int ph = qb[i] - t_r, pw = qc[i] - t_s;
         bool ok = ph >= 0 && pw >= 0;
-        if (st > 1) {
+        if (st == 2) {
+          ok = ok && (((ph | pw) & 1) == 0);
+          ph >>= 1;
+          pw >>= 1;
+        } else if (st > 2) {
           ok = ok && (ph % st == 0) && (pw % st == 0);
           ph /= st;
           pw /= st;
         }
-        ok = ok && ph < P && pw < Q;
-        rq[i] = ok ? ld16(DY + ((long long)(qb[i] + ph * Q + pw)) * K + k0) : zero16();
-      }
-    } else {  // WGRAD: X gather MN-major rows = pixels (n,p,q), cols = (r,s,c)
-#pragma unroll
-      for (int i = 0; i < Q_NL; ++i) {
-        const long long pix = kg + q_kr0 + i * (256 / Q_CPR);
-        bool ok = wg_cvalid && pix < Kr;
-        i4v v = zero16();
-        if (ok) {
-          const int pi = (int)pix;
-          const int n = pi / (P * Q), rem = pi - n * (P * Q);
-          const int op = rem / Q, oq = rem - op * Q;
-          const int ih = op * st - pd + wg_r, iw = oq * st - pd + wg_s;
+        if (ok && ph < P && pw < Q) src = DY + (long long)(qa[i] + ph * Q + pw) * K + t_c + qd[i];
+      } else {
+        const int pix = kg + qd[i];
+        if (qa[i] >= 0 && pix < Kr) {
+          const int n = fdiv(pix, div_pq), rem = pix - n * (P * Q);
+          const int op = fdiv(rem, div_q), oq = rem - op * Q;
+          const int ih = op * st - pd + qa[i], iw = oq * st - pd + qb[i];
           if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
-            v = ld16(X + ((long long)(n * H + ih) * W + iw) * C + wg_c);
+            src = X + ((long long)(n * H + ih) * W + iw) * C + qc[i];
         }
-        rq[i] = v;
       }
+      dma16(src, Qs + j * 1024);
     }
-  };
-
-  auto store_tiles = [&](int buf) {
-    char* Ps = smem + buf * STAGE;
-    char* Qs = Ps + P_BYTES;
-    if constexpr (P_KMAJOR) {
-#pragma unroll
-      for (int i = 0; i < P_NL; ++i) *(i4v*)(Ps + km_off<BP>(krow0 + i * KRSTEP, kc)) = rp[i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < P_NL; ++i) *(i4v*)(Ps + mn_off<BP>(p_kr0 + i * (256 / P_CPR), p_cc)) = rp[i];
-    }
-    if constexpr (Q_KMAJOR) {
-#pragma unroll
-      for (int i = 0; i < Q_NL; ++i) *(i4v*)(Qs + km_off<BQ>(krow0 + i * KRSTEP, kc)) = rq[i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < Q_NL; ++i) *(i4v*)(Qs + mn_off<BQ>(q_kr0 + i * (256 / Q_CPR), q_cc)) = rq[i];
+    // advance the reduction cursor by one K-step
+    kg_run += BK;
+    if constexpr (MODE != MODE_WGRAD) {
+      t_c += BK;
+      if (t_c >= CR) {
+        t_c = 0;
+        if (++t_s == S) { t_s = 0; ++t_r; }
+      }
     }
   };
 
@@ -279,37 +311,43 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < TQ; ++j) acc[i][j] = (f4v){0.f, 0.f, 0.f, 0.f};
 
-  load_tiles(kt0);
-  store_tiles(0);
-  __syncthreads();
+  // prologue: stages 0 .. NS-2 in flight
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(s);
 
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const int cur = (kt - kt0) & 1;
-    const bool more = kt + 1 < kt1;
-    if (more) load_tiles(kt + 1);  // issue next tile's global loads before the MFMAs
-    const char* Ps = smem + cur * STAGE;
+  for (int i = 0; i < nk; ++i) {
+    // retire stage i: at most (stages issued after it) * LPS DMA ops may stay outstanding
+    if constexpr (NS >= 3) {
+      if (i + NS - 2 < nk) wait_vm<(NS - 2) * LPS>();
+      else if (NS >= 4 && i + NS - 3 < nk) wait_vm<(NS >= 4 ? (NS - 3) * LPS : 0)>();
+      else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    cta_barrier();  // stage i visible to all waves; slot of stage i-1 free for reuse
+    if (i + NS - 1 < nk) issue((i + NS - 1) % NS);
+    const char* Ps = smem + (i % NS) * STAGE;
     const char* Qs = Ps + P_BYTES;
 #pragma unroll
     for (int u = 0; u < BK / 32; ++u) {
       s8v pf[TP], qf[TQ];
 #pragma unroll
-      for (int i = 0; i < TP; ++i) {
-        if constexpr (P_KMAJOR) pf[i] = km_frag<BP>(Ps, wp * WP + i * 16, u, lane);
-        else pf[i] = mn_frag<BP>(Ps, wp * WP + i * 16, u, lane);
+      for (int t = 0; t < TP; ++t) {
+        if constexpr (P_KMAJOR) pf[t] = km_frag<BP>(Ps, wp * WP + t * 16, u, lane);
+        else pf[t] = mn_frag<BP>(Ps, wp * WP + t * 16, u, lane);
       }
 #pragma unroll
-      for (int j = 0; j < TQ; ++j) {
-        if constexpr (Q_KMAJOR) qf[j] = km_frag<BQ>(Qs, wq * WQ + j * 16, u, lane);
-        else qf[j] = mn_frag<BQ>(Qs, wq * WQ + j * 16, u, lane);
+      for (int t = 0; t < TQ; ++t) {
+        if constexpr (Q_KMAJOR) qf[t] = km_frag<BQ>(Qs, wq * WQ + t * 16, u, lane);
+        else qf[t] = mn_frag<BQ>(Qs, wq * WQ + t * 16, u, lane);
       }
 #pragma unroll
-      for (int i = 0; i < TP; ++i)
+      for (int ti = 0; ti < TP; ++ti)
 #pragma unroll
-        for (int j = 0; j < TQ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[i], qf[j], acc[i][j], 0, 0, 0);
+        for (int tj = 0; tj < TQ; ++tj)
+          acc[ti][tj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[ti], qf[tj], acc[ti][tj], 0, 0, 0);
     }
-    if (more) store_tiles(cur ^ 1);
-    __syncthreads();
   }
 
   // ---------------- epilogue ----------------
@@ -322,8 +360,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     const bf16_t* msk = a.mask ? (const bf16_t*)a.mask + (long long)g * a.out_gs : nullptr;
     float* stats = a.stats ? a.stats + (long long)g * a.stats_gs : nullptr;
 #pragma unroll
-    for (int i = 0; i < TP; ++i) {
-      const int p = p0 + wp * WP + i * 16 + lp;
+    for (int ti = 0; ti < TP; ++ti) {
+      const int p = p0 + wp * WP + ti * 16 + lp;
       float bsum[4] = {0.f, 0.f, 0.f, 0.f}, bsq[4] = {0.f, 0.f, 0.f, 0.f};
       float bv[4] = {0.f, 0.f, 0.f, 0.f};
       if (bias && p < Pd) {
@@ -331,12 +369,12 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         for (int e = 0; e < 4; ++e) bv[e] = bias[p + e];
       }
 #pragma unroll
-      for (int j = 0; j < TQ; ++j) {
-        const int q = q0 + wq * WQ + j * 16 + lq;
+      for (int tj = 0; tj < TQ; ++tj) {
+        const int q = q0 + wq * WQ + tj * 16 + lq;
         if (p < Pd && q < Qd) {
           float v[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bv[e];
+          for (int e = 0; e < 4; ++e) v[e] = acc[ti][tj][e] + bv[e];
           const long long o = (long long)q * ldo + p;
           if (res) {
             const i2v rv = *(const i2v*)(res + o);
@@ -390,17 +428,17 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     float* O = (float*)a.out + (long long)g * a.out_gs;
     const bool atomic = a.accumulate || gridDim.y > 1;
 #pragma unroll
-    for (int i = 0; i < TP; ++i) {
+    for (int ti = 0; ti < TP; ++ti) {
 #pragma unroll
-      for (int j = 0; j < TQ; ++j) {
-        const int q = q0 + wq * WQ + j * 16 + lq;
+      for (int tj = 0; tj < TQ; ++tj) {
+        const int q = q0 + wq * WQ + tj * 16 + lq;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int p = p0 + wp * WP + i * 16 + lp + e;
+          const int p = p0 + wp * WP + ti * 16 + lp + e;
           if (p < Pd && q < Qd) {
             float* dst = O + (long long)p * Qd + q;
-            if (atomic) atomicAdd(dst, acc[i][j][e]);
-            else *dst = acc[i][j][e];
+            if (atomic) atomicAdd(dst, acc[ti][tj][e]);
+            else *dst = acc[ti][tj][e];
           }
         }
       }
@@ -408,21 +446,22 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   }
 }
 
-template <int MODE, int BP, int BQ, int BK>
+template <int MODE, int BP, int BQ, int BK, int NS>
 static hipError_t launch_cfg(const ConvArgs& a, int Pd, int Qd, int splits, hipStream_t stream) {
   const int ntp = (Pd + BP - 1) / BP, ntq = (Qd + BQ - 1) / BQ;
   dim3 grid(ntp * ntq, splits, a.G);
-  hipLaunchKernelGGL((conv_igemm_kernel<MODE, BP, BQ, BK>), grid, dim3(256), 0, stream, a);
+  hipLaunchKernelGGL((conv_igemm_kernel<MODE, BP, BQ, BK, NS>), grid, dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 
+// LDS per stage = (BP+BQ)*BK*2: 3 stages for the big tiles (1-2 blocks/CU), 4 for small ones
 template <int MODE>
 static hipError_t dispatch(const ConvArgs& a, int Pd, int Qd, int bp, int bq, int bk, int splits,
                            hipStream_t s) {
-#define DDL_CFG(BP_, BQ_, BK_) \
-  if (bp == BP_ && bq == BQ_ && bk == BK_) return launch_cfg<MODE, BP_, BQ_, BK_>(a, Pd, Qd, splits, s);
-  DDL_CFG(64, 64, 32) DDL_CFG(64, 64, 64) DDL_CFG(64, 128, 32) DDL_CFG(64, 128, 64)
-  DDL_CFG(128, 64, 32) DDL_CFG(128, 64, 64) DDL_CFG(128, 128, 32) DDL_CFG(128, 128, 64)
+#define DDL_CFG(BP_, BQ_, BK_, NS_) \
+  if (bp == BP_ && bq == BQ_ && bk == BK_) return launch_cfg<MODE, BP_, BQ_, BK_, NS_>(a, Pd, Qd, splits, s);
+  DDL_CFG(64, 64, 32, 4) DDL_CFG(64, 64, 64, 3) DDL_CFG(64, 128, 32, 4) DDL_CFG(64, 128, 64, 3)
+  DDL_CFG(128, 64, 32, 4) DDL_CFG(128, 64, 64, 3) DDL_CFG(128, 128, 32, 4) DDL_CFG(128, 128, 64, 3)
 #undef DDL_CFG
   return hipErrorInvalidValue;
 }
@@ -441,7 +480,7 @@ static int num_cus() {
 // Validates the layout contract shared by all three modes.
 static bool conv_shapes_ok(const ConvArgs& a) {
   if (a.G <= 0 || a.N <= 0 || a.C % 32 || a.K % 32 || a.R <= 0 || a.S <= 0) return false;
-  if (a.stride <= 0 || a.pad < 0) return false;
+  if (a.stride <= 0 || a.pad < 0 || !a.zero) return false;
   if (a.P != (a.H + 2 * a.pad - a.R) / a.stride + 1) return false;
   if (a.Q != (a.W + 2 * a.pad - a.S) / a.stride + 1) return false;
   return a.P > 0 && a.Q > 0;
@@ -454,6 +493,7 @@ DDL_API int ddl_conv_fwd(const ConvArgs* ap, int cfg, hipStream_t stream) {
   const int Pd = a.K, Qd = a.N * a.P * a.Q;
   int bp = a.K >= 128 ? 128 : 64, bq = 128, bk = (a.C % 64 == 0) ? 64 : 32;
   if (cfg) { bp = cfg & 0xff; bq = (cfg >> 8) & 0xff; bk = (cfg >> 16) & 0xff; }
+  if (a.C % bk) return (int)hipErrorInvalidValue;
   return (int)dispatch<MODE_FWD>(a, Pd, Qd, bp, bq, bk, 1, stream);
 }
 
@@ -463,7 +503,7 @@ DDL_API int ddl_conv_dgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
   const int Pd = a.C, Qd = a.N * a.H * a.W;
   int bp = a.C >= 128 ? 128 : 64, bq = 128, bk = (a.K % 64 == 0) ? 64 : 32;
   if (cfg) { bp = cfg & 0xff; bq = (cfg >> 8) & 0xff; bk = (cfg >> 16) & 0xff; }
-  if (bk > 32 && (a.K % bk)) return (int)hipErrorInvalidValue;
+  if (a.K % bk) return (int)hipErrorInvalidValue;
   return (int)dispatch<MODE_DGRAD>(a, Pd, Qd, bp, bq, bk, 1, stream);
 }
 
@@ -472,10 +512,9 @@ DDL_API int ddl_conv_wgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
   if (!conv_shapes_ok(a)) return (int)hipErrorInvalidValue;
   const int Pd = a.K, Qd = a.R * a.S * a.C;
   const long long Kr = (long long)a.N * a.P * a.Q;
+  if (Kr >= (1LL << 31)) return (int)hipErrorInvalidValue;
   int bp = a.K >= 128 ? 128 : 64, bq = Qd >= 128 ? 128 : 64, bk = 64;
   if (cfg) { bp = cfg & 0xff; bq = (cfg >> 8) & 0xff; bk = (cfg >> 16) & 0xff; }
-  // wgrad gathers X by 8-channel chunks inside one (r,s) tap
-  if (a.C % 8) return (int)hipErrorInvalidValue;
   const long long tiles = (long long)((Pd + bp - 1) / bp) * ((Qd + bq - 1) / bq) * a.G;
   const long long nk = (Kr + bk - 1) / bk;
   int splits = (cfg >> 24) & 0xff;

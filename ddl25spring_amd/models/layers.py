@@ -17,6 +17,7 @@ import math
 import torch
 
 from ..ops import functional as Fn
+from ..ops import workspace as ws
 from ..ops.functional import ConvGeom
 from .params import ParamStore, const_, kaiming_uniform_, uniform_bias_
 
@@ -132,10 +133,10 @@ class ConvUnit(Layer):
         g = self.geom(x4)
         w = st.shadow_of(self.w)
         if self.bn:
-            stats = torch.zeros(g.G, 2, self.cout, dtype=torch.float32, device=x.device) if train else None
+            stats = ws.zeros((g.G, 2, self.cout), x.device) if train else None
             c = Fn.conv_fwd(x4, w, g, stats=stats)
             count = g.N * g.P * g.Q
-            sc, sh, mu, rs = Fn.bn_finalize(stats if train else torch.zeros(g.G, 2, self.cout, device=x.device),
+            sc, sh, mu, rs = Fn.bn_finalize(stats if train else ws.zeros((g.G, 2, self.cout), x.device),
                                             st.param(self.gamma), st.param(self.beta),
                                             st.buffer(self.rm), st.buffer(self.rv), count,
                                             self.eps, self.momentum, training=train)

@@ -12,6 +12,7 @@ from __future__ import annotations
 import torch
 
 from ..ops import functional as Fn
+from ..ops.workspace import Workspace
 from .layers import RELU, ConvUnit, Layer
 from .params import ParamStore
 
@@ -76,13 +77,20 @@ class Net:
 
     def train_step(self, x, labels, ncls=None, scale=None, targets=None, with_correct=False):
         """forward + fused softmax-CE (mean over each client's batch) + backward.
-        Grads ACCUMULATE into store.grad (zero them per optimizer step). Returns (loss[G], correct)."""
-        logits, ctxs = self.forward_native(x, True)
-        N = logits.shape[1]
-        loss, dlogits, correct = Fn.cross_entropy(
-            logits, labels, targets, ncls=ncls or self.num_classes, scale=(1.0 / N) if scale is None else scale,
-            with_correct=with_correct)
-        self.backward_native(dlogits, ctxs)
+        Grads ACCUMULATE into store.grad (zero them per optimizer step). Returns (loss[G], correct).
+        The returned loss lives in the step's scratch arena: read it before the next step."""
+        if not hasattr(self, "_ws"):
+            self._ws = Workspace()
+        self._ws.begin(self.device)
+        try:
+            logits, ctxs = self.forward_native(x, True)
+            N = logits.shape[1]
+            loss, dlogits, correct = Fn.cross_entropy(
+                logits, labels, targets, ncls=ncls or self.num_classes,
+                scale=(1.0 / N) if scale is None else scale, with_correct=with_correct)
+            self.backward_native(dlogits, ctxs)
+        finally:
+            self._ws.end()
         return loss, correct
 
     @torch.no_grad()

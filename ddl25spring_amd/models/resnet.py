@@ -17,6 +17,7 @@ from __future__ import annotations
 import torch
 
 from ..ops import functional as Fn
+from ..ops import workspace as ws
 from .layers import RELU, ConvUnit, GlobalAvgPool, Layer, Linear, pad32
 from .net import Net
 
@@ -33,7 +34,7 @@ class _BNConv(ConvUnit):
         stats = torch.zeros(g.G, 2, self.cout, dtype=torch.float32, device=x.device) if train else None
         c = Fn.conv_fwd(x, st.shadow_of(self.w), g, stats=stats)
         if not train:
-            stats = torch.zeros(g.G, 2, self.cout, dtype=torch.float32, device=x.device)
+            stats = ws.zeros((g.G, 2, self.cout), x.device)
         sc, sh, mu, rs = Fn.bn_finalize(stats, st.param(self.gamma), st.param(self.beta),
                                         st.buffer(self.rm), st.buffer(self.rv), g.N * g.P * g.Q,
                                         self.eps, self.momentum, training=train)

@@ -34,7 +34,7 @@ fp = ctypes.POINTER(ctypes.c_float)
 
 class ConvArgs(ctypes.Structure):
     _fields_ = [("x", vp), ("w", vp), ("dy", vp), ("out", vp), ("stats", vp), ("bias", vp),
-                ("residual", vp), ("mask", vp),
+                ("residual", vp), ("mask", vp), ("zero", vp),
                 ("x_gs", i64), ("w_gs", i64), ("dy_gs", i64), ("out_gs", i64), ("bias_gs", i64),
                 ("stats_gs", i64),
                 ("G", i32), ("N", i32), ("H", i32), ("W", i32), ("C", i32), ("K", i32), ("R", i32),
@@ -71,7 +71,7 @@ _SIGS = {
     "ddl_bn_finalize": [ctypes.POINTER(BNArgs), vp],
     "ddl_bn_apply": [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, vp],
     "ddl_bn_bwd_reduce": [vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i32, i32, vp],
-    "ddl_bn_bwd_apply": [vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, i64, i32, i32, vp],
+    "ddl_bn_bwd_apply": [vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, i64, i32, i32, vp],
     # nn_ops.hip
     "ddl_prep_images": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
     "ddl_nchw_to_nhwc": [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],

@@ -15,6 +15,7 @@ import torch
 
 from . import _lib
 from . import reference as ref
+from . import workspace as ws
 from ._lib import check, ptr, stream
 
 
@@ -47,8 +48,23 @@ def _gs(t: torch.Tensor | None) -> int:
     return 0 if t is None else t.stride(0)
 
 
-def _conv_args(geom: ConvGeom, **kw) -> _lib.ConvArgs:
+_ZERO_PAGES: dict = {}
+
+
+def zero_page(device) -> torch.Tensor:
+    """A small zeroed device buffer: DMA source for the implicit-GEMM padding taps."""
+    key = str(device)
+    z = _ZERO_PAGES.get(key)
+    if z is None:
+        z = torch.zeros(256, dtype=torch.float32, device=device)
+        _ZERO_PAGES[key] = z
+    return z
+
+
+def _conv_args(geom: ConvGeom, device=None, **kw) -> _lib.ConvArgs:
     a = _lib.ConvArgs()
+    if device is not None:
+        a.zero = zero_page(device).data_ptr()
     for k, v in kw.items():
         setattr(a, k, v)
     a.G, a.N, a.H, a.W, a.C, a.K = geom.G, geom.N, geom.H, geom.W, geom.C, geom.K
@@ -73,7 +89,7 @@ def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out=None, 
     _check_inner(x, "x"); _check_inner(w, "w")
     y = out if out is not None else torch.empty(geom.G, geom.N, geom.P, geom.Q, geom.K,
                                                 dtype=torch.bfloat16, device=x.device)
-    a = _conv_args(geom, x=ptr(x), w=ptr(w), out=ptr(y), stats=ptr(stats), bias=ptr(bias),
+    a = _conv_args(geom, x.device, x=ptr(x), w=ptr(w), out=ptr(y), stats=ptr(stats), bias=ptr(bias),
                    x_gs=_gs(x), w_gs=_gs(w), out_gs=_gs(y), bias_gs=_gs(bias),
                    stats_gs=0 if stats is None else stats.stride(0), relu=int(relu))
     check(_lib.kernels().ddl_conv_fwd(ctypes.byref(a), cfg, stream()), "conv_fwd")
@@ -95,7 +111,7 @@ def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0)
         residual = residual.contiguous()
     if mask is not None and mask.stride(0) != dx.stride(0):
         mask = mask.contiguous()
-    a = _conv_args(geom, w=ptr(w), dy=ptr(dy), out=ptr(dx), residual=ptr(residual),
+    a = _conv_args(geom, dy.device, w=ptr(w), dy=ptr(dy), out=ptr(dx), residual=ptr(residual),
                    mask=ptr(mask), w_gs=_gs(w), dy_gs=_gs(dy), out_gs=_gs(dx))
     check(_lib.kernels().ddl_conv_dgrad(ctypes.byref(a), cfg, stream()), "conv_dgrad")
     return dx
@@ -107,7 +123,7 @@ def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0):
         ref.conv_wgrad(dy, x, geom, dw, accumulate)
         return dw
     _check_inner(dy, "dy"); _check_inner(x, "x"); _check_inner(dw, "dw")
-    a = _conv_args(geom, x=ptr(x), dy=ptr(dy), out=ptr(dw), x_gs=_gs(x), dy_gs=_gs(dy),
+    a = _conv_args(geom, dy.device, x=ptr(x), dy=ptr(dy), out=ptr(dw), x_gs=_gs(x), dy_gs=_gs(dy),
                    out_gs=_gs(dw), accumulate=int(accumulate))
     if not accumulate:
         cfg = (cfg & 0x00FFFFFF) | (1 << 24)  # force a single split (plain stores)
@@ -157,7 +173,7 @@ def bn_bwd_reduce(dy, ymask, x, mean, rstd, dgamma=None, dbeta=None):
     if not dy.is_cuda:
         return ref.bn_bwd_reduce(dy, ymask, x, mean, rstd, dgamma, dbeta)
     G, C = x.shape[0], x.shape[-1]
-    sums = torch.zeros(G, 2, C, dtype=torch.float32, device=x.device)
+    sums = ws.zeros((G, 2, C), x.device)
     gs = _gs(dgamma) if dgamma is not None else _gs(dbeta)
     check(_lib.kernels().ddl_bn_bwd_reduce(ptr(dy), ptr(ymask), ptr(x), ptr(mean), ptr(rstd),
                                            ptr(sums), ptr(dgamma), ptr(dbeta), gs,
@@ -171,9 +187,11 @@ def bn_bwd_apply(dy, ymask, x, mean, rstd, gamma, sums, emit_dym=False):
     G, C = x.shape[0], x.shape[-1]
     dx = torch.empty_like(x)
     dym = torch.empty_like(x) if emit_dym else None
+    coef = ws.scratch((G, 3, C), x.device)
     check(_lib.kernels().ddl_bn_bwd_apply(ptr(dy), ptr(ymask), ptr(x), ptr(mean), ptr(rstd),
-                                          ptr(gamma), _gs(gamma), ptr(sums), ptr(dx), ptr(dym),
-                                          x[0].numel() // C, C, G, stream()), "bn_bwd_apply")
+                                          ptr(gamma), _gs(gamma), ptr(sums), ptr(coef), ptr(dx),
+                                          ptr(dym), x[0].numel() // C, C, G, stream()),
+          "bn_bwd_apply")
     return (dx, dym) if emit_dym else dx
 
 
@@ -359,7 +377,7 @@ def cross_entropy(logits, labels=None, targets=None, ncls=None, scale=1.0, want_
     G, N, ld = logits.shape
     ncls = ncls or ld
     dev = logits.device
-    loss = torch.zeros(G, dtype=torch.float32, device=dev)
+    loss = ws.zeros((G,), dev)
     correct = torch.zeros(G, dtype=torch.int32, device=dev) if with_correct else None
     if not logits.is_cuda:
         d = ref.ce_fwd_bwd(logits, labels, targets, ncls, scale, loss, correct, want_grad)
