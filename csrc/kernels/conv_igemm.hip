@@ -147,15 +147,37 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   else { Pd = K; Qd = RSC; Kr = a.N * P * Q; }
   const FastDiv div_pq = make_fdiv(P * Q), div_q = make_fdiv(Q);
 
+  // DGRAD at stride 2: sub-pixel phase decomposition. blockIdx.y = phase (a, b); the phase's
+  // input pixels (2i+a, 2j+b) only receive taps r = r0 (mod 2), s = s0 (mod 2), so no MFMA or
+  // DMA is spent on the 3/4 of (pixel, tap) pairs that hit no output position.
+  int ph_a = 0, ph_b = 0, Hs = H, Ws = W, r0 = 0, s0 = 0, tstep = 1, Rn = R, Sn = S;
+  constexpr bool PHASED_MODE = (MODE == MODE_DGRAD);
+  const bool phased = PHASED_MODE && st == 2;
+  if (phased) {
+    ph_a = blockIdx.y >> 1;
+    ph_b = blockIdx.y & 1;
+    Hs = (H - ph_a + 1) >> 1;
+    Ws = (W - ph_b + 1) >> 1;
+    r0 = (ph_a + pd) & 1;
+    s0 = (ph_b + pd) & 1;
+    Rn = (R - r0 + 1) >> 1;
+    Sn = (S - s0 + 1) >> 1;
+    tstep = 2;
+    Qd = a.N * Hs * Ws;
+    Kr = Rn * Sn * K;
+  }
+
   const int ntp = (Pd + BP - 1) / BP;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int p0 = (tile % ntp) * BP, q0 = (tile / ntp) * BQ;
+  if (q0 >= Qd) return;  // smaller phases of a phased launch
+  const int nsplit = PHASED_MODE ? 1 : gridDim.y, split = PHASED_MODE ? 0 : blockIdx.y;
   const int nk_total = (Kr + BK - 1) / BK;
-  const int per = (nk_total + gridDim.y - 1) / gridDim.y;
-  const int kt0 = blockIdx.y * per;
+  const int per = (nk_total + nsplit - 1) / nsplit;
+  const int kt0 = split * per;
   const int kt1 = min(nk_total, kt0 + per);
-  if (kt0 >= kt1) return;
-  const int nk = kt1 - kt0;
+  if (kt0 >= kt1 && MODE == MODE_WGRAD) return;  // empty split-K slice (atomics: nothing to add)
+  const int nk = max(0, kt1 - kt0);  // FWD/DGRAD with no taps still write (zero) outputs
 
   const bf16_t* X = (const bf16_t*)a.x + (long long)g * a.x_gs;
   const bf16_t* Wt = (const bf16_t*)a.w + (long long)g * a.w_gs;
@@ -198,11 +220,11 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
           qb[i] = op * st - pd;
           qc[i] = oq * st - pd;
         } else {
-          const int n = qq / (H * W), rem = qq - n * (H * W);
-          const int h = rem / W, w = rem - h * W;
+          const int n = qq / (Hs * Ws), rem = qq - n * (Hs * Ws);
+          const int hi = rem / Ws, wi = rem - hi * Ws;
           qa[i] = n * P * Q;
-          qb[i] = h + pd;
-          qc[i] = w + pd;
+          qb[i] = hi * tstep + ph_a + pd;
+          qc[i] = wi * tstep + ph_b + pd;
         }
       } else {
         qa[i] = 0;
@@ -232,10 +254,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   const int CR = (MODE == MODE_FWD) ? C : K;  // contiguous reduction run per tap
   int kg_run = kt0 * BK, t_r = 0, t_s = 0, t_c = 0;
   if constexpr (MODE != MODE_WGRAD) {
-    const int rs = kg_run / CR;
-    t_c = kg_run - rs * CR;
-    t_r = rs / S;
-    t_s = rs - t_r * S;
+    const int ti = kg_run / CR;  // tap index among the (phase's) valid taps
+    t_c = kg_run - ti * CR;
+    t_r = r0 + tstep * (ti / Sn);
+    t_s = s0 + tstep * (ti % Sn);
   }
 
   auto issue = [&](int slot) {
@@ -300,7 +322,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       t_c += BK;
       if (t_c >= CR) {
         t_c = 0;
-        if (++t_s == S) { t_s = 0; ++t_r; }
+        t_s += tstep;
+        if (t_s >= S) { t_s = s0; t_r += tstep; }
       }
     }
   };
@@ -375,7 +398,12 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
           float v[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = acc[ti][tj][e] + bv[e];
-          const long long o = (long long)q * ldo + p;
+          long long o = (long long)q * ldo + p;
+          if (phased) {  // phase-local pixel (n, i, j) -> NHWC offset of (n, 2i+a, 2j+b)
+            const int n = q / (Hs * Ws), rem = q - n * (Hs * Ws);
+            const int hi = rem / Ws, wi = rem - hi * Ws;
+            o = ((long long)(n * H + 2 * hi + ph_a) * W + 2 * wi + ph_b) * ldo + p;
+          }
           if (res) {
             const i2v rv = *(const i2v*)(res + o);
             v[0] += lo_bf((uint32_t)rv[0]); v[1] += hi_bf((uint32_t)rv[0]);
@@ -447,21 +475,25 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 }
 
 template <int MODE, int BP, int BQ, int BK, int NS>
-static hipError_t launch_cfg(const ConvArgs& a, int Pd, int Qd, int splits, hipStream_t stream) {
+static hipError_t launch_cfg(const ConvArgs& a, int Pd, int Qd, int gy, hipStream_t stream) {
   const int ntp = (Pd + BP - 1) / BP, ntq = (Qd + BQ - 1) / BQ;
-  dim3 grid(ntp * ntq, splits, a.G);
+  dim3 grid(ntp * ntq, gy, a.G);
   hipLaunchKernelGGL((conv_igemm_kernel<MODE, BP, BQ, BK, NS>), grid, dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 
-// LDS per stage = (BP+BQ)*BK*2: 3 stages for the big tiles (1-2 blocks/CU), 4 for small ones
+// Instantiated (tile, K-step, LDS stages). LDS = NS*(BP+BQ)*BK*2 bytes: the 4-stage BK=32 tiles
+// (<= 64 KB) keep 2 workgroups per CU, which the per-layer sweep (scripts/conv_bench.py --sweep,
+// profiles/conv_sweep_*.log) found fastest for every ResNet-18 shape.
 template <int MODE>
-static hipError_t dispatch(const ConvArgs& a, int Pd, int Qd, int bp, int bq, int bk, int splits,
+static hipError_t dispatch(const ConvArgs& a, int Pd, int Qd, int bp, int bq, int bk, int ns, int gy,
                            hipStream_t s) {
 #define DDL_CFG(BP_, BQ_, BK_, NS_) \
-  if (bp == BP_ && bq == BQ_ && bk == BK_) return launch_cfg<MODE, BP_, BQ_, BK_, NS_>(a, Pd, Qd, splits, s);
-  DDL_CFG(64, 64, 32, 4) DDL_CFG(64, 64, 64, 3) DDL_CFG(64, 128, 32, 4) DDL_CFG(64, 128, 64, 3)
-  DDL_CFG(128, 64, 32, 4) DDL_CFG(128, 64, 64, 3) DDL_CFG(128, 128, 32, 4) DDL_CFG(128, 128, 64, 3)
+  if (bp == BP_ && bq == BQ_ && bk == BK_ && ns == NS_) \
+    return launch_cfg<MODE, BP_, BQ_, BK_, NS_>(a, Pd, Qd, gy, s);
+  DDL_CFG(64, 64, 32, 4) DDL_CFG(64, 128, 32, 4) DDL_CFG(128, 64, 32, 4) DDL_CFG(128, 128, 32, 4)
+  DDL_CFG(128, 128, 32, 3) DDL_CFG(64, 128, 64, 3) DDL_CFG(128, 128, 64, 3) DDL_CFG(128, 128, 64, 2)
+  DDL_CFG(64, 64, 64, 3) DDL_CFG(128, 64, 64, 3)
 #undef DDL_CFG
   return hipErrorInvalidValue;
 }
@@ -483,28 +515,41 @@ static bool conv_shapes_ok(const ConvArgs& a) {
   if (a.stride <= 0 || a.pad < 0 || !a.zero) return false;
   if (a.P != (a.H + 2 * a.pad - a.R) / a.stride + 1) return false;
   if (a.Q != (a.W + 2 * a.pad - a.S) / a.stride + 1) return false;
+  if ((long long)a.N * a.H * a.W * (a.C > a.K ? a.C : a.K) >= (1LL << 31)) return false;
   return a.P > 0 && a.Q > 0;
 }
 
-// tile override: cfg = bp | bq<<8 | bk<<16 | splits<<24 (0 = heuristic); used by the autotuner.
+// cfg = bp | bq<<8 | bk<<16 | ns<<24 (0 = heuristic); WGRAD split-K count in a.split_k (0 = auto)
+static void decode_cfg(int cfg, int& bp, int& bq, int& bk, int& ns) {
+  if (!cfg) return;
+  bp = cfg & 0xff;
+  bq = (cfg >> 8) & 0xff;
+  bk = (cfg >> 16) & 0xff;
+  ns = (cfg >> 24) & 0xff;
+  if (!ns) ns = bk == 32 ? 4 : 3;
+}
+
 DDL_API int ddl_conv_fwd(const ConvArgs* ap, int cfg, hipStream_t stream) {
   const ConvArgs& a = *ap;
   if (!conv_shapes_ok(a)) return (int)hipErrorInvalidValue;
   const int Pd = a.K, Qd = a.N * a.P * a.Q;
-  int bp = a.K >= 128 ? 128 : 64, bq = 128, bk = (a.C % 64 == 0) ? 64 : 32;
-  if (cfg) { bp = cfg & 0xff; bq = (cfg >> 8) & 0xff; bk = (cfg >> 16) & 0xff; }
+  int bp = a.K >= 128 ? 128 : 64, bq = 128, bk = 32, ns = 4;
+  decode_cfg(cfg, bp, bq, bk, ns);
   if (a.C % bk) return (int)hipErrorInvalidValue;
-  return (int)dispatch<MODE_FWD>(a, Pd, Qd, bp, bq, bk, 1, stream);
+  return (int)dispatch<MODE_FWD>(a, Pd, Qd, bp, bq, bk, ns, 1, stream);
 }
 
 DDL_API int ddl_conv_dgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
   const ConvArgs& a = *ap;
   if (!conv_shapes_ok(a)) return (int)hipErrorInvalidValue;
-  const int Pd = a.C, Qd = a.N * a.H * a.W;
-  int bp = a.C >= 128 ? 128 : 64, bq = 128, bk = (a.K % 64 == 0) ? 64 : 32;
-  if (cfg) { bp = cfg & 0xff; bq = (cfg >> 8) & 0xff; bk = (cfg >> 16) & 0xff; }
+  // stride 2 runs as 4 sub-pixel phases (blockIdx.y); grid sized for the largest (phase 0,0)
+  const bool phased = a.stride == 2;
+  const int Pd = a.C;
+  const int Qd = phased ? a.N * ((a.H + 1) / 2) * ((a.W + 1) / 2) : a.N * a.H * a.W;
+  int bp = a.C >= 128 ? 128 : 64, bq = 128, bk = 32, ns = 4;
+  decode_cfg(cfg, bp, bq, bk, ns);
   if (a.K % bk) return (int)hipErrorInvalidValue;
-  return (int)dispatch<MODE_DGRAD>(a, Pd, Qd, bp, bq, bk, 1, stream);
+  return (int)dispatch<MODE_DGRAD>(a, Pd, Qd, bp, bq, bk, ns, phased ? 4 : 1, stream);
 }
 
 DDL_API int ddl_conv_wgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
@@ -512,22 +557,21 @@ DDL_API int ddl_conv_wgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
   if (!conv_shapes_ok(a)) return (int)hipErrorInvalidValue;
   const int Pd = a.K, Qd = a.R * a.S * a.C;
   const long long Kr = (long long)a.N * a.P * a.Q;
-  if (Kr >= (1LL << 31)) return (int)hipErrorInvalidValue;
-  int bp = a.K >= 128 ? 128 : 64, bq = Qd >= 128 ? 128 : 64, bk = 64;
-  if (cfg) { bp = cfg & 0xff; bq = (cfg >> 8) & 0xff; bk = (cfg >> 16) & 0xff; }
+  int bp = a.K >= 128 ? 128 : 64, bq = Qd >= 128 ? 128 : 64, bk = 32, ns = 4;
+  decode_cfg(cfg, bp, bq, bk, ns);
   const long long tiles = (long long)((Pd + bp - 1) / bp) * ((Qd + bq - 1) / bq) * a.G;
   const long long nk = (Kr + bk - 1) / bk;
-  int splits = (cfg >> 24) & 0xff;
+  int splits = a.split_k;
   if (!splits) {
-    // aim for ~2 waves of workgroups over the CUs, keep >= 8 K-steps per split
+    // aim for ~2 waves of workgroups over the CUs, keep >= 16 K-steps per split
     long long want = (2LL * num_cus() + tiles - 1) / tiles;
-    long long maxs = nk / 8 > 0 ? nk / 8 : 1;
+    long long maxs = nk / 16 > 0 ? nk / 16 : 1;
     splits = (int)(want < maxs ? want : maxs);
     if (splits < 1) splits = 1;
-    if (splits > 255) splits = 255;
+    if (splits > 1024) splits = 1024;
   }
   if (splits > 1 && !a.accumulate) return (int)hipErrorInvalidValue;  // needs zeroed fp32 output
-  return (int)dispatch<MODE_WGRAD>(a, Pd, Qd, bp, bq, bk, splits, stream);
+  return (int)dispatch<MODE_WGRAD>(a, Pd, Qd, bp, bq, bk, ns, splits, stream);
 }
 
 DDL_API int ddl_conv_args_size() { return (int)sizeof(ConvArgs); }

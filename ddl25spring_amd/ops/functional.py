@@ -117,16 +117,16 @@ def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0)
     return dx
 
 
-def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0):
-    """dw[G,K,R,S,C] (+)= sum over pixels dy (x) x  — fp32, split-K with atomics."""
+def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0):
+    """dw[G,K,R,S,C] (+)= sum over pixels dy (x) x  — fp32, split-K with atomics.
+    cfg = bp | bq<<8 | bk<<16 | stages<<24 (0: tuned default); splits = split-K slices (0: auto)."""
     if not dy.is_cuda:
         ref.conv_wgrad(dy, x, geom, dw, accumulate)
         return dw
     _check_inner(dy, "dy"); _check_inner(x, "x"); _check_inner(dw, "dw")
     a = _conv_args(geom, dy.device, x=ptr(x), dy=ptr(dy), out=ptr(dw), x_gs=_gs(x), dy_gs=_gs(dy),
-                   out_gs=_gs(dw), accumulate=int(accumulate))
-    if not accumulate:
-        cfg = (cfg & 0x00FFFFFF) | (1 << 24)  # force a single split (plain stores)
+                   out_gs=_gs(dw), accumulate=int(accumulate),
+                   split_k=1 if not accumulate else int(splits))
     check(_lib.kernels().ddl_conv_wgrad(ctypes.byref(a), cfg, stream()), "conv_wgrad")
     return dw
 

@@ -1,0 +1,127 @@
+"""Per-layer conv kernel timing (fwd / dgrad / wgrad) for the client-batched ResNet-18 shapes,
+optionally sweeping tile configs and comparing against PyTorch/MIOpen on the same shapes.
+
+    python scripts/conv_bench.py [--sweep] [--miopen] [--G 8 --N 100]
+Timing: HIP events around R back-to-back launches, median of 5 repeats, random bf16 data.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import statistics
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+from ddl25spring_amd.ops import functional as Fn  # noqa: E402
+from ddl25spring_amd.ops.functional import ConvGeom  # noqa: E402
+
+
+def resnet18_shapes(G, N):
+    out = [("stem", ConvGeom(G, N, 32, 32, 32, 64, 1, 1, 1, 0))]
+    spec = [(64, 32, 1), (128, 16, 2), (256, 8, 2), (512, 4, 2)]
+    cin, h = 64, 32
+    for planes, hw, stride in spec:
+        if stride == 2:
+            out.append((f"c{planes}s2", ConvGeom(G, N, h, h, cin, planes, 3, 3, 2, 1)))
+            out.append((f"sc{planes}", ConvGeom(G, N, h, h, cin, planes, 1, 1, 2, 0)))
+        out.append((f"c{planes}", ConvGeom(G, N, hw, hw, planes, planes, 3, 3, 1, 1)))
+        cin, h = planes, hw
+    return out
+
+
+def timeit(fn, reps=10, rounds=5):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(rounds):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b) / reps)
+    return statistics.median(ts)
+
+
+CFGS = [(64, 64, 32, 4), (64, 128, 32, 4), (128, 64, 32, 4), (128, 128, 32, 4), (128, 128, 32, 3),
+        (64, 128, 64, 3), (128, 128, 64, 3), (128, 128, 64, 2), (64, 64, 64, 3), (128, 64, 64, 3)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--G", type=int, default=8)
+    ap.add_argument("--N", type=int, default=100)
+    ap.add_argument("--sweep", action="store_true")
+    ap.add_argument("--miopen", action="store_true")
+    ap.add_argument("--json", default=None)
+    args = ap.parse_args()
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    results = []
+    tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0, "miopen": 0.0}
+    for name, g in resnet18_shapes(args.G, args.N):
+        x = torch.randn(g.G, g.N, g.H, g.W, g.C, device=dev).to(torch.bfloat16)
+        w = (torch.randn(g.G, g.K, g.R, g.S, g.C, device=dev) * 0.05).to(torch.bfloat16)
+        dy = torch.randn(g.G, g.N, g.P, g.Q, g.K, device=dev).to(torch.bfloat16)
+        dw = torch.zeros(g.G, g.K, g.R, g.S, g.C, device=dev)
+        fl = g.flops()
+        row = {"layer": name, "geom": str(g), "gflop": fl / 1e9}
+        modes = {
+            "fwd": lambda cfg: Fn.conv_fwd(x, w, g, cfg=cfg),
+            "dgrad": lambda cfg: Fn.conv_dgrad(dy, w, g, cfg=cfg),
+            "wgrad": lambda cfg: Fn.conv_wgrad(dy, x, g, dw, cfg=cfg),
+        }
+        for mode, f in modes.items():
+            if mode == "dgrad" and name == "stem":
+                continue
+            t = timeit(lambda: f(0))
+            row[mode] = {"ms": t, "tflops": fl / t / 1e9}
+            tot[mode] += t
+            if args.sweep:
+                best = (t, 0)
+                for bp, bq, bk, ns in CFGS:
+                    if mode == "fwd" and g.C % bk:
+                        continue
+                    if mode == "dgrad" and g.K % bk:
+                        continue
+                    cfg = bp | (bq << 8) | (bk << 16) | (ns << 24)
+                    try:
+                        tc = timeit(lambda: f(cfg), reps=5, rounds=3)
+                    except Exception:
+                        continue
+                    row.setdefault(mode + "_sweep", {})[f"{bp}x{bq}x{bk}s{ns}"] = round(fl / tc / 1e9, 1)
+                    if tc < best[0]:
+                        best = (tc, cfg)
+                row[mode]["best_cfg"] = best[1]
+                row[mode]["best_tflops"] = fl / best[0] / 1e9
+        if args.miopen:
+            xc = x[0].permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
+            wc = w[0].permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
+
+            def mi():
+                for _ in range(g.G):
+                    torch.nn.functional.conv2d(xc, wc, None, g.stride, g.pad)
+            t = timeit(mi)
+            row["miopen_fwd"] = {"ms": t, "tflops": fl / t / 1e9}
+            tot["miopen"] += t
+        results.append(row)
+        msg = f"{name:8s} {fl / 1e9:7.1f} GF"
+        for mode in ("fwd", "dgrad", "wgrad"):
+            if mode in row:
+                msg += f" | {mode} {row[mode]['ms'] * 1e3:7.1f}us {row[mode]['tflops']:6.0f}TF"
+                if "best_cfg" in row[mode]:
+                    msg += f" (best {row[mode]['best_tflops']:.0f} @{row[mode]['best_cfg']:#x})"
+        if "miopen_fwd" in row:
+            msg += f" | miopen fwd {row['miopen_fwd']['tflops']:6.0f}TF"
+        print(msg, flush=True)
+    print("totals (ms, one instance of each layer):", {k: round(v, 3) for k, v in tot.items()})
+    if args.json:
+        Path(args.json).write_text(json.dumps(results, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -28,6 +28,10 @@ GEOMS = [
     ConvGeom(G=2, N=37, H=1, W=1, C=96, K=32, R=1, S=1, stride=1, pad=0),
     ConvGeom(G=1, N=2, H=26, W=26, C=32, K=64, R=3, S=3, stride=1, pad=0),
     ConvGeom(G=2, N=4, H=8, W=8, C=256, K=256, R=3, S=3, stride=1, pad=1),
+    ConvGeom(G=2, N=3, H=7, W=5, C=64, K=64, R=3, S=3, stride=2, pad=1),   # odd sizes, phased dgrad
+    ConvGeom(G=1, N=2, H=5, W=6, C=32, K=64, R=1, S=1, stride=2, pad=0),   # 1x1/2: empty phases
+    ConvGeom(G=1, N=2, H=9, W=9, C=32, K=32, R=3, S=3, stride=3, pad=1),   # stride 3 (unphased)
+    ConvGeom(G=1, N=2, H=16, W=16, C=32, K=64, R=7, S=7, stride=2, pad=3), # 7x7/2 stem shape
 ]
 
 
@@ -90,16 +94,16 @@ def test_conv_tile_configs(cuda):
     dx_ref = ref.conv_dgrad(dy.cpu(), w.cpu(), geom)
     dw_ref = torch.zeros(geom.G, geom.K, geom.R, geom.S, geom.C)
     ref.conv_wgrad(dy.cpu(), x.cpu(), geom, dw_ref)
-    for bp in (64, 128):
-        for bq in (64, 128):
-            for bk in (32, 64):
-                cfg = bp | (bq << 8) | (bk << 16)
-                _close(Fn.conv_fwd(x, w, geom, cfg=cfg), y_ref)
-                _close(Fn.conv_dgrad(dy, w, geom, cfg=cfg), dx_ref)
-                for splits in (1, 3):
-                    dw = torch.zeros(geom.G, geom.K, geom.R, geom.S, geom.C, device=cuda)
-                    Fn.conv_wgrad(dy, x, geom, dw, cfg=cfg | (splits << 24))
-                    _close(dw, dw_ref, rel=2e-3)
+    cfgs = [(64, 64, 32, 4), (64, 128, 32, 4), (128, 64, 32, 4), (128, 128, 32, 4), (128, 128, 32, 3),
+            (64, 128, 64, 3), (128, 128, 64, 3), (128, 128, 64, 2), (64, 64, 64, 3), (128, 64, 64, 3)]
+    for bp, bq, bk, ns in cfgs:
+        cfg = bp | (bq << 8) | (bk << 16) | (ns << 24)
+        _close(Fn.conv_fwd(x, w, geom, cfg=cfg), y_ref)
+        _close(Fn.conv_dgrad(dy, w, geom, cfg=cfg), dx_ref)
+        for splits in (1, 3):
+            dw = torch.zeros(geom.G, geom.K, geom.R, geom.S, geom.C, device=cuda)
+            Fn.conv_wgrad(dy, x, geom, dw, cfg=cfg, splits=splits)
+            _close(dw, dw_ref, rel=2e-3)
 
 
 def test_batchnorm(cuda):
