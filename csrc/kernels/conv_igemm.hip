@@ -533,7 +533,9 @@ DDL_API int ddl_conv_fwd(const ConvArgs* ap, int cfg, hipStream_t stream) {
   const ConvArgs& a = *ap;
   if (!conv_shapes_ok(a)) return (int)hipErrorInvalidValue;
   const int Pd = a.K, Qd = a.N * a.P * a.Q;
-  int bp = a.K >= 128 ? 128 : 64, bq = 128, bk = 32, ns = 4;
+  // sweep-tuned (profiles/conv_sweep_r1.log): 128x128x64 / 2 stages for >=128 output channels
+  int bp = 64, bq = 128, bk = 32, ns = 4;
+  if (a.K >= 128 && a.C % 64 == 0) { bp = 128; bk = 64; ns = 2; }
   decode_cfg(cfg, bp, bq, bk, ns);
   if (a.C % bk) return (int)hipErrorInvalidValue;
   return (int)dispatch<MODE_FWD>(a, Pd, Qd, bp, bq, bk, ns, 1, stream);
@@ -546,7 +548,8 @@ DDL_API int ddl_conv_dgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
   const bool phased = a.stride == 2;
   const int Pd = a.C;
   const int Qd = phased ? a.N * ((a.H + 1) / 2) * ((a.W + 1) / 2) : a.N * a.H * a.W;
-  int bp = a.C >= 128 ? 128 : 64, bq = 128, bk = 32, ns = 4;
+  int bp = 64, bq = 128, bk = 32, ns = 4;
+  if (a.C >= 128 && a.K % 64 == 0) { bp = 128; bk = 64; ns = 2; }
   decode_cfg(cfg, bp, bq, bk, ns);
   if (a.K % bk) return (int)hipErrorInvalidValue;
   return (int)dispatch<MODE_DGRAD>(a, Pd, Qd, bp, bq, bk, ns, phased ? 4 : 1, stream);
@@ -558,6 +561,8 @@ DDL_API int ddl_conv_wgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
   const int Pd = a.K, Qd = a.R * a.S * a.C;
   const long long Kr = (long long)a.N * a.P * a.Q;
   int bp = a.K >= 128 ? 128 : 64, bq = Qd >= 128 ? 128 : 64, bk = 32, ns = 4;
+  if (a.K >= 128 && Qd >= 128) ns = 3;
+  if (Qd < 128) { bp = 64; bq = 64; bk = 64; ns = 3; }
   decode_cfg(cfg, bp, bq, bk, ns);
   const long long tiles = (long long)((Pd + bp - 1) / bp) * ((Qd + bq - 1) / bq) * a.G;
   const long long nk = (Kr + bk - 1) / bk;
