@@ -63,9 +63,9 @@ def synthetic_images(kind: str, n: int, seed: int = 0, learnable: bool = True,
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
         base = templ[labels[s:e]]
-        shift = rng.integers(-2, 3, 2)
-        base = np.roll(base, tuple(shift), axis=(1, 2))
-        x = 128 + 48 * base + rng.normal(0, 40, base.shape)
+        # per-sample contrast jitter + pixel noise (no shared shifts: train/test stay aligned)
+        gain = rng.uniform(0.7, 1.3, (e - s, 1, 1, 1))
+        x = 128 + 48 * gain * base + rng.normal(0, 36, base.shape)
         imgs[s:e] = np.clip(x, 0, 255).astype(np.uint8)
     return ImageArrays(imgs, labels, kind, True)
 

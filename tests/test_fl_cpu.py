@@ -1,0 +1,161 @@
+"""Horizontal-FL behaviour on the CPU reference path (+ gloo multi-process for the distributed
+aggregation). Mirrors the reference's algorithmic invariants."""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import ddl25spring_amd.ops.reference as R
+from ddl25spring_amd.data.images import DeviceImageDataset, synthetic_images
+from ddl25spring_amd.data.split import plan_epoch, split
+from ddl25spring_amd.fl import aggregate as A
+from ddl25spring_amd.fl.algorithms import FedAvg, FedSGD, FedSgdWeight
+from ddl25spring_amd.fl.attacks import LabelFlip, SignFlip
+from ddl25spring_amd.models import mnist_mlp
+from ddl25spring_amd.models import params as P
+from ddl25spring_amd.runtime.dist import DistContext
+
+
+@pytest.fixture
+def fp32(monkeypatch):
+    monkeypatch.setattr(R, "_bf", lambda t: t.float())
+    monkeypatch.setattr(P, "CPU_SHADOW_DTYPE", torch.float32)
+
+
+def _data(n=600, seed=0):
+    arr = synthetic_images("mnist", n, seed=seed)
+    return arr, DeviceImageDataset(arr, "cpu")
+
+
+def test_split_matches_reference_semantics():
+    labels = np.random.default_rng(0).integers(0, 10, 1000)
+    iid = split(7, True, 10, labels=labels)
+    rng = np.random.default_rng(10)
+    ref = np.array_split(rng.permutation(1000), 7)
+    assert all(np.array_equal(a, b) for a, b in zip(iid, ref))
+    non = split(5, False, 3, labels=labels)
+    rng = np.random.default_rng(3)
+    shards = np.array_split(np.argsort(labels), 10)
+    order = rng.permutation(10).reshape(5, 2)
+    for got, pair in zip(non, order):
+        assert np.array_equal(got, np.concatenate([shards[i] for i in pair]))
+    assert sorted(np.concatenate(non).tolist()) == list(range(1000))
+
+
+def test_native_epoch_planner():
+    idx = [np.arange(10) + 100 * g for g in range(3)]
+    plan = plan_epoch(idx, 4, [1, 2, 3])
+    assert plan.shape == (3, 3, 4)
+    for g in range(3):
+        seen = plan[:, g][plan[:, g] >= 0]
+        assert sorted(seen.tolist()) == idx[g].tolist()
+    assert (plan[-1, :, 2:] == -1).all()
+
+
+def test_mean_aggregator_equals_weighted_mean():
+    ctx = DistContext()
+    rows = torch.randn(5, 33)
+    coeffs = torch.tensor([0.1, 0.2, 0.3, 0.25, 0.15])
+    out = torch.empty(33)
+    A.MeanAggregator()(ctx, rows, coeffs, out)
+    assert torch.allclose(out, (coeffs[:, None] * rows).sum(0), atol=1e-6)
+    A.MeanAggregator()(ctx, rows, torch.full((5,), 0.2), out)
+    assert torch.allclose(out, rows.mean(0), atol=1e-6)
+
+
+@pytest.mark.parametrize("agg", ["median", "trimmed_mean", "krum"])
+def test_robust_aggregators_resist_sign_flip(agg):
+    torch.manual_seed(0)
+    ctx = DistContext()
+    honest = torch.randn(1, 200) * 0.1 + 1.0 + 0.05 * torch.randn(7, 200)
+    bad = -10.0 * torch.ones(2, 200)
+    rows = torch.cat([honest, bad])
+    a = A.make_aggregator(agg, trim=2, f=2)
+    out = a(ctx, rows, [9], 200)
+    assert (out - honest.mean(0)).abs().max() < 0.3, agg
+    mean = rows.mean(0)
+    assert (mean - honest.mean(0)).abs().max() > 2.0  # the plain mean is wrecked
+    if agg == "krum":
+        assert all(i < 7 for i in a.last_selected)
+
+
+def test_fedavg_learns_and_reports(fp32):
+    arr, data = _data(600)
+    tarr, tdata = _data(300, seed=1)
+    parts = split(6, True, 10, labels=arr.labels)
+    fa = FedAvg(mnist_mlp, data, parts, lr=0.1, batch_size=50, local_epochs=1, client_fraction=0.5,
+                seed=10, test_data=tdata)
+    res = fa.run(4)
+    assert res.message_count == [6, 12, 18, 24]
+    assert res.test_accuracy[-1] > 40.0, res.test_accuracy
+    df = res.as_df()
+    assert list(df.columns) == ["Round", "Algorithm", "N", "C", "B", "E", "η", "Seed",
+                                "Message count", "Test accuracy"]
+
+
+def test_fedsgd_gradient_equals_fedsgd_weight(fp32):
+    """sum_k p_k (w - lr g_k) = w - lr sum_k p_k g_k : the exchanged quantity does not matter."""
+    arr, data = _data(400)
+    parts = split(4, True, 1, labels=arr.labels)
+    kw = dict(lr=0.05, client_fraction=0.5, seed=3)
+    g = FedSGD(mnist_mlp, data, parts, **kw)
+    w = FedSgdWeight(mnist_mlp, data, parts, **kw)
+    for _ in range(2):
+        g.round()
+        w.round()
+    assert torch.allclose(g.w_global, w.w_global, atol=1e-5), (g.w_global - w.w_global).abs().max()
+
+
+def test_label_flip_attack_hurts_and_median_helps(fp32):
+    arr, data = _data(800)
+    tarr, tdata = _data(300, seed=1)
+    parts = split(8, True, 5, labels=arr.labels)
+    bad = [0, 1]
+    kw = dict(lr=0.1, batch_size=50, local_epochs=1, client_fraction=1.0, seed=5, test_data=tdata)
+    clean = FedAvg(mnist_mlp, data, parts, **kw).run(5).test_accuracy[-1]
+    attacked = FedAvg(mnist_mlp, data, parts, attack=SignFlip(bad, scale=4.0), **kw).run(5).test_accuracy[-1]
+    assert attacked < clean - 30, (clean, attacked)
+    for agg in ("median", "trimmed_mean"):
+        defended = FedAvg(mnist_mlp, data, parts, attack=SignFlip(bad, scale=4.0), aggregator=agg,
+                          agg_kwargs={"trim": 2}, **kw).run(5).test_accuracy[-1]
+        assert defended > attacked + 30, (agg, attacked, defended)
+    lf = FedAvg(mnist_mlp, data, parts, attack=LabelFlip(bad), **kw).run(2)
+    assert len(lf.test_accuracy) == 2
+
+
+# --------------------------------------------------------------------------- distributed (gloo)
+def _dist_worker(rank, world, port, out_dir, agg):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    R._bf = lambda t: t.float()
+    P.CPU_SHADOW_DTYPE = torch.float32
+    from ddl25spring_amd.runtime import dist as rdist
+    ctx = rdist.init(backend="gloo", device="cpu")
+    arr, data = _data(400)
+    parts = split(4, True, 7, labels=arr.labels)
+    fa = FedAvg(mnist_mlp, data, parts, lr=0.1, batch_size=50, client_fraction=1.0, seed=7,
+                ctx=ctx, aggregator=agg)
+    fa.round()
+    fa.round()
+    torch.save(fa.w_global, os.path.join(out_dir, f"w{rank}.pt"))
+    rdist.shutdown()
+
+
+@pytest.mark.parametrize("agg", ["mean", "median"])
+def test_distributed_fedavg_matches_single_process(fp32, agg):
+    arr, data = _data(400)
+    parts = split(4, True, 7, labels=arr.labels)
+    single = FedAvg(mnist_mlp, data, parts, lr=0.1, batch_size=50, client_fraction=1.0, seed=7,
+                    ctx=DistContext(), aggregator=agg)
+    single.round()
+    single.round()
+    with tempfile.TemporaryDirectory() as d:
+        port = 29600 + (os.getpid() % 200) + (0 if agg == "mean" else 1)
+        mp.spawn(_dist_worker, args=(2, port, d, agg), nprocs=2, join=True)
+        w0 = torch.load(os.path.join(d, "w0.pt"), weights_only=True)
+        w1 = torch.load(os.path.join(d, "w1.pt"), weights_only=True)
+    assert torch.equal(w0, w1)  # replicated server state stays identical on every rank
+    assert torch.allclose(w0, single.w_global, atol=1e-5), (w0 - single.w_global).abs().max()
