@@ -68,9 +68,14 @@ class Net:
             ctxs.append(c)
         return x, ctxs
 
+    grad_hook = None  # callable(layer_index) after each layer's weight grads are complete
+
     def backward_native(self, dy, ctxs):
-        for layer, c in zip(reversed(self.layers), reversed(ctxs)):
+        n = len(self.layers)
+        for j, (layer, c) in enumerate(zip(reversed(self.layers), reversed(ctxs))):
             dy = layer.backward(dy, c)
+            if self.grad_hook is not None:
+                self.grad_hook(n - 1 - j)
             if dy is None:
                 break
         return dy

@@ -1,0 +1,305 @@
+"""Autograd-composable ops for ``torch.nn.Module`` models (LLaMA stages, tabular nets, GANs).
+
+On device tensors every op below is a HIP kernel (MFMA implicit-GEMM for the linears, the fused
+LLaMA kernels of csrc/kernels/llama.hip, fused CE over the vocabulary); activations are bf16,
+parameters stay fp32 ``nn.Parameter`` (cast to a bf16 shadow per forward) and weight gradients are
+fp32. On CPU tensors the same functions run plain PyTorch fp32 ops, so module code is written once
+and is testable without a GPU.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from . import functional as Fn
+from ._lib import check, ptr, stream
+
+vp, i32, i64, f32 = _lib.vp, _lib.i32, _lib.i64, _lib.f32
+_lib.register_signatures({
+    "ddl_embedding_fwd": [vp, vp, vp, i32, i32, vp],
+    "ddl_embedding_bwd": [vp, vp, vp, i32, i32, i32, vp],
+    "ddl_rmsnorm_fwd": [vp, vp, vp, vp, i32, i32, f32, vp],
+    "ddl_rmsnorm_bwd": [vp, vp, vp, vp, vp, vp, i32, i32, vp],
+    "ddl_swiglu_fwd": [vp, vp, i32, i32, vp],
+    "ddl_swiglu_bwd": [vp, vp, vp, i32, i32, vp],
+    "ddl_add": [vp, vp, vp, i64, vp],
+    "ddl_attn_fwd": [vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, vp],
+    "ddl_attn_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, vp],
+})
+
+
+def K():
+    return _lib.kernels()
+
+
+def _bf16_weight(w: torch.Tensor) -> torch.Tensor:
+    return Fn.to_bf16(w.detach().contiguous())
+
+
+# ------------------------------------------------------------------------------------- linear
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, residual):
+        C = x.shape[-1]
+        Kout = w.shape[0]
+        x2 = x.reshape(-1, C).contiguous()
+        T = x2.shape[0]
+        geom = Fn.ConvGeom(1, T, 1, 1, C, Kout, 1, 1, 1, 0)
+        wb = _bf16_weight(w).view(1, Kout, 1, 1, C)
+        res = residual.reshape(1, T, 1, 1, Kout).contiguous() if residual is not None else None
+        y = Fn.conv_fwd(x2.view(1, T, 1, 1, C), wb, geom,
+                        bias=None if b is None else b.detach().view(1, Kout), residual=res)
+        ctx.save_for_backward(x2, wb)
+        ctx.geom, ctx.has_b, ctx.has_res, ctx.xshape = geom, b is not None, residual is not None, x.shape
+        return y.view(*x.shape[:-1], Kout)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, wb = ctx.saved_tensors
+        g = ctx.geom
+        dy5 = dy.reshape(1, g.N, 1, 1, g.K).to(torch.bfloat16).contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = Fn.conv_dgrad(dy5, wb, g).view(ctx.xshape)
+        if ctx.needs_input_grad[1]:
+            dw = torch.zeros(1, g.K, 1, 1, g.C, dtype=torch.float32, device=dy.device)
+            Fn.conv_wgrad(dy5, x2.view(1, g.N, 1, 1, g.C), g, dw)
+            dw = dw.view(g.K, g.C)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = torch.zeros(1, g.K, dtype=torch.float32, device=dy.device)
+            Fn.channel_sum(dy5.view(1, g.N, g.K), db)
+            db = db.view(g.K)
+        dres = dy if ctx.has_res else None
+        return dx, dw, db, dres
+
+
+def linear(x, w, b=None, residual=None):
+    """y = x @ w.T (+ b) (+ residual). Device: one MFMA GEMM with the bias / residual in its epilogue."""
+    if not x.is_cuda:
+        y = F.linear(x, w, b)
+        return y + residual if residual is not None else y
+    if x.dtype != torch.bfloat16:
+        x = x.to(torch.bfloat16)
+    if residual is not None and residual.dtype != torch.bfloat16:
+        residual = residual.to(torch.bfloat16)
+    return _Linear.apply(x, w, b, residual)
+
+
+# ------------------------------------------------------------------------------------ rmsnorm
+class _RMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g, eps):
+        D = x.shape[-1]
+        x2 = x.reshape(-1, D).contiguous()
+        T = x2.shape[0]
+        y = torch.empty_like(x2)
+        rstd = torch.empty(T, dtype=torch.float32, device=x.device)
+        gd = g.detach().float().contiguous()
+        check(K().ddl_rmsnorm_fwd(ptr(x2), ptr(gd), ptr(y), ptr(rstd), T, D, float(eps), stream()),
+              "rmsnorm_fwd")
+        ctx.save_for_backward(x2, gd, rstd)
+        ctx.shape = x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, gd, rstd = ctx.saved_tensors
+        T, D = x2.shape
+        dx = torch.empty_like(x2)
+        dg = torch.zeros(D, dtype=torch.float32, device=x2.device)
+        dyc = dy.reshape(T, D).to(torch.bfloat16).contiguous()
+        check(K().ddl_rmsnorm_bwd(ptr(x2), ptr(gd), ptr(rstd), ptr(dyc), ptr(dx), ptr(dg), T, D,
+                                  stream()), "rmsnorm_bwd")
+        return dx.view(ctx.shape), dg, None
+
+
+def rmsnorm(x, g, eps=1e-6):
+    if not x.is_cuda:
+        return x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + eps) * g
+    return _RMSNorm.apply(x.to(torch.bfloat16), g, eps)
+
+
+# ------------------------------------------------------------------------------------- swiglu
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ab):
+        F2 = ab.shape[-1]
+        ab2 = ab.reshape(-1, F2).contiguous()
+        T = ab2.shape[0]
+        h = torch.empty(T, F2 // 2, dtype=torch.bfloat16, device=ab.device)
+        check(K().ddl_swiglu_fwd(ptr(ab2), ptr(h), T, F2 // 2, stream()), "swiglu_fwd")
+        ctx.save_for_backward(ab2)
+        ctx.shape = ab.shape
+        return h.view(*ab.shape[:-1], F2 // 2)
+
+    @staticmethod
+    def backward(ctx, dh):
+        (ab2,) = ctx.saved_tensors
+        T, F2 = ab2.shape
+        dab = torch.empty_like(ab2)
+        dhc = dh.reshape(T, F2 // 2).to(torch.bfloat16).contiguous()
+        check(K().ddl_swiglu_bwd(ptr(ab2), ptr(dhc), ptr(dab), T, F2 // 2, stream()), "swiglu_bwd")
+        return dab.view(ctx.shape)
+
+
+def swiglu(ab):
+    """silu(a) * b for ab = [a | b] along the last dim."""
+    if not ab.is_cuda:
+        a, b = ab.chunk(2, -1)
+        return F.silu(a) * b
+    return _SwiGLU.apply(ab)
+
+
+# ---------------------------------------------------------------------------------- embedding
+class _Embedding(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, idx, w, pad_idx):
+        idx32 = idx.to(torch.int32).contiguous().reshape(-1)
+        T, D = idx32.numel(), w.shape[1]
+        y = torch.empty(T, D, dtype=torch.bfloat16, device=w.device)
+        wd = w.detach().float().contiguous()
+        check(K().ddl_embedding_fwd(ptr(idx32), ptr(wd), ptr(y), T, D, stream()), "embedding_fwd")
+        ctx.save_for_backward(idx32)
+        ctx.wshape, ctx.pad, ctx.ishape = w.shape, pad_idx, idx.shape
+        return y.view(*idx.shape, D)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx32,) = ctx.saved_tensors
+        V, D = ctx.wshape
+        dw = torch.zeros(V, D, dtype=torch.float32, device=dy.device)
+        dyc = dy.reshape(-1, D).to(torch.bfloat16).contiguous()
+        check(K().ddl_embedding_bwd(ptr(idx32), ptr(dyc), ptr(dw), idx32.numel(), D,
+                                    -1 if ctx.pad is None else int(ctx.pad), stream()),
+              "embedding_bwd")
+        return None, dw, None
+
+
+def embedding(idx, w, padding_idx=None):
+    if not w.is_cuda:
+        return F.embedding(idx, w, padding_idx)
+    return _Embedding.apply(idx, w, padding_idx)
+
+
+def add(a, b):
+    if not a.is_cuda:
+        return a + b
+    return _Add.apply(a.to(torch.bfloat16), b.to(torch.bfloat16))
+
+
+class _Add(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        ac, bc = a.contiguous(), b.contiguous()
+        y = torch.empty_like(ac)
+        check(K().ddl_add(ptr(ac), ptr(bc), ptr(y), ac.numel(), stream()), "add")
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy, dy
+
+
+# ---------------------------------------------------------------------------------- attention
+_ROPE: dict = {}
+
+
+def rope_tables(S, hd, device, base=10000.0):
+    key = (S, hd, str(device), base)
+    t = _ROPE.get(key)
+    if t is None:
+        inv = base ** (-torch.arange(0, hd, 2, dtype=torch.float64) / hd)
+        ang = torch.arange(S, dtype=torch.float64)[:, None] * inv[None]
+        t = (torch.cos(ang).float().to(device).contiguous(), torch.sin(ang).float().to(device).contiguous())
+        _ROPE[key] = t
+    return t
+
+
+def apply_rope_ref(x, cos, sin):
+    """x [..., S, H, hd] with interleaved pairs (2i, 2i+1)."""
+    x0, x1 = x[..., 0::2], x[..., 1::2]
+    c = cos[:, None, :]
+    s = sin[:, None, :]
+    out = torch.empty_like(x)
+    out[..., 0::2] = x0 * c - x1 * s
+    out[..., 1::2] = x0 * s + x1 * c
+    return out
+
+
+def attention_ref(qkv, H, hd):
+    B, S, _ = qkv.shape
+    q, k, v = qkv.view(B, S, 3, H, hd).unbind(2)
+    cos, sin = rope_tables(S, hd, qkv.device)
+    q, k = apply_rope_ref(q, cos, sin), apply_rope_ref(k, cos, sin)
+    o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),
+                                       is_causal=True)
+    return o.transpose(1, 2).reshape(B, S, H * hd)
+
+
+class _Attention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, H, hd):
+        B, S, _ = qkv.shape
+        qc = qkv.contiguous()
+        cos, sin = rope_tables(S, hd, qkv.device)
+        o = torch.empty(B, S, H * hd, dtype=torch.bfloat16, device=qkv.device)
+        lse = torch.empty(B, H, S, dtype=torch.float32, device=qkv.device)
+        scale = 1.0 / math.sqrt(hd)
+        check(K().ddl_attn_fwd(ptr(qc), ptr(o), ptr(lse), ptr(cos), ptr(sin), B, S, H, hd, scale,
+                               stream()), "attn_fwd")
+        ctx.save_for_backward(qc, o, lse)
+        ctx.H, ctx.hd, ctx.scale = H, hd, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qc, o, lse = ctx.saved_tensors
+        B, S, _ = qc.shape
+        cos, sin = rope_tables(S, ctx.hd, qc.device)
+        dqkv = torch.empty_like(qc)
+        delta = torch.empty_like(lse)
+        doc = do.to(torch.bfloat16).contiguous()
+        check(K().ddl_attn_bwd(ptr(qc), ptr(o), ptr(doc), ptr(lse), ptr(delta), ptr(dqkv), ptr(cos),
+                               ptr(sin), B, S, ctx.H, ctx.hd, ctx.scale, stream()), "attn_bwd")
+        return dqkv, None, None
+
+
+def causal_attention(qkv, n_heads, head_dim):
+    """Causal multi-head attention with RoPE on q, k. qkv: [B, S, 3*H*hd] -> [B, S, H*hd]."""
+    if not qkv.is_cuda:
+        return attention_ref(qkv, n_heads, head_dim)
+    return _Attention.apply(qkv.to(torch.bfloat16), n_heads, head_dim)
+
+
+# ------------------------------------------------------------------------------- LM loss
+class _VocabCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, targets, ignore_index):
+        V = logits.shape[-1]
+        lg = logits.reshape(-1, V).to(torch.bfloat16).contiguous()
+        R = lg.shape[0]
+        tg = targets.reshape(-1).to(torch.int32).contiguous()
+        valid = max(1, int((tg != ignore_index).sum().item())) if ignore_index >= 0 else R
+        loss = torch.zeros(1, dtype=torch.float32, device=logits.device)
+        d = torch.empty_like(lg)
+        check(K().ddl_ce_vocab(ptr(lg), ptr(tg), R, V, V, 1.0 / valid, int(ignore_index), ptr(loss),
+                               ptr(d), stream()), "ce_vocab")
+        ctx.save_for_backward(d)
+        ctx.shape = logits.shape
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        (d,) = ctx.saved_tensors
+        return (d.float() * g).to(torch.bfloat16).view(ctx.shape), None, None
+
+
+def cross_entropy_vocab(logits, targets, ignore_index=-100):
+    """Mean token cross-entropy; one fused kernel computes loss and d(logits)."""
+    if not logits.is_cuda:
+        return F.cross_entropy(logits.reshape(-1, logits.shape[-1]).float(), targets.reshape(-1).long(),
+                               ignore_index=ignore_index)
+    return _VocabCE.apply(logits, targets, ignore_index)

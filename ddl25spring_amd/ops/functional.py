@@ -78,10 +78,14 @@ def _check_inner(t: torch.Tensor, name: str) -> None:
         raise ValueError(f"{name}: per-group inner dims must be contiguous")
 
 
-def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out=None, cfg=0):
-    """y[G,N,P,Q,K] = conv(x[G,N,H,W,C], w[G,K,R,S,C]) (+bias)(relu); stats[G,2,K] += sum, sumsq."""
+def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out=None, cfg=0,
+             residual=None):
+    """y[G,N,P,Q,K] = conv(x[G,N,H,W,C], w[G,K,R,S,C]) (+bias)(+residual)(relu);
+    stats[G,2,K] += sum, sumsq of y."""
     if not x.is_cuda:
         y = ref.conv_fwd(x, w, geom, bias, relu, stats)
+        if residual is not None:
+            y = (y.float() + residual.float()).to(y.dtype)
         if out is not None:
             out.copy_(y)
             return out
@@ -89,9 +93,12 @@ def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out=None, 
     _check_inner(x, "x"); _check_inner(w, "w")
     y = out if out is not None else torch.empty(geom.G, geom.N, geom.P, geom.Q, geom.K,
                                                 dtype=torch.bfloat16, device=x.device)
+    if residual is not None and (residual.stride(0) != y.stride(0) or not residual.is_contiguous()):
+        residual = residual.contiguous()
     a = _conv_args(geom, x.device, x=ptr(x), w=ptr(w), out=ptr(y), stats=ptr(stats), bias=ptr(bias),
-                   x_gs=_gs(x), w_gs=_gs(w), out_gs=_gs(y), bias_gs=_gs(bias),
-                   stats_gs=0 if stats is None else stats.stride(0), relu=int(relu))
+                   residual=ptr(residual), x_gs=_gs(x), w_gs=_gs(w), out_gs=_gs(y),
+                   bias_gs=_gs(bias), stats_gs=0 if stats is None else stats.stride(0),
+                   relu=int(relu))
     check(_lib.kernels().ddl_conv_fwd(ctypes.byref(a), cfg, stream()), "conv_fwd")
     return y
 
