@@ -150,7 +150,7 @@ def swiglu(ab):
     if not ab.is_cuda:
         a, b = ab.chunk(2, -1)
         return F.silu(a) * b
-    return _SwiGLU.apply(ab)
+    return _SwiGLU.apply(ab.to(torch.bfloat16))
 
 
 # ---------------------------------------------------------------------------------- embedding
@@ -282,7 +282,7 @@ class _VocabCE(torch.autograd.Function):
         lg = logits.reshape(-1, V).to(torch.bfloat16).contiguous()
         R = lg.shape[0]
         tg = targets.reshape(-1).to(torch.int32).contiguous()
-        valid = max(1, int((tg != ignore_index).sum().item())) if ignore_index >= 0 else R
+        valid = max(1, int((tg != ignore_index).sum().item()))
         loss = torch.zeros(1, dtype=torch.float32, device=logits.device)
         d = torch.empty_like(lg)
         check(K().ddl_ce_vocab(ptr(lg), ptr(tg), R, V, V, 1.0 / valid, int(ignore_index), ptr(loss),
