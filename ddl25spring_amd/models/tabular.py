@@ -1,0 +1,312 @@
+"""Tabular models of the generative-modelling and vertical-FL labs (fp32, exact reference numerics).
+
+These nets are a few thousand parameters on <= 1,025 rows; they run as plain fp32 ``nn.Module``s
+(device-agnostic) so accuracy / loss parity with the reference is exact in distribution. Their
+optimizers can be the fused flat HIP ``FlatAdamW`` (``ddl25spring_amd.optim.FlatAdam``) and, in the
+vertical-FL runtime, their activations/gradients cross GPUs over RCCL (``ddl25spring_amd.vfl``).
+
+* ``HeartDiseaseNN``      — lab/tutorial_2a/centralized.py:13-28
+* ``Autoencoder``+``customLoss`` — lab/tutorial_2a/generative-modeling.py:13-130 (tabular VAE;
+  ``sample`` draws from the batch-averaged posterior N(mean mu, mean sigma))
+* ``BottomModel`` / ``TopModel`` / ``VFLNetwork`` — lab/tutorial_2b/vfl.py:11-102
+* ``ClientEncoder`` / ``ClientDecoder`` / ``ServerVAE`` / ``VFLVAE`` / ``combined_loss`` —
+  lab/tutorial_2b/exercise_3.py:10-147
+"""
+from __future__ import annotations
+
+import copy
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def _mlp_bn(dims, final_act=True):
+    layers = []
+    for i, (a, b) in enumerate(zip(dims[:-1], dims[1:])):
+        layers += [nn.Linear(a, b), nn.BatchNorm1d(b)]
+        if final_act or i < len(dims) - 2:
+            layers.append(nn.ReLU())
+    return nn.Sequential(*layers)
+
+
+class HeartDiseaseNN(nn.Module):
+    def __init__(self, in_features: int = 30):
+        super().__init__()
+        self.fc1, self.fc2 = nn.Linear(in_features, 64), nn.Linear(64, 128)
+        self.fc3, self.fc4 = nn.Linear(128, 256), nn.Linear(256, 2)
+        self.act, self.dropout = nn.LeakyReLU(), nn.Dropout(0.1)
+
+    def forward(self, x):
+        x = self.act(self.fc1(x))
+        x = self.act(self.fc2(x))
+        x = self.dropout(self.act(self.fc3(x)))
+        return self.fc4(x)
+
+
+def train_centralized(net, Xtr, ytr, Xte, yte, epochs: int = 49, optimizer=None):
+    """Full-batch training keeping a DEEP copy of the best-test-accuracy weights (fixes the
+    reference's aliasing ``best_params = net.state_dict()``, centralized.py:51,69-70 / SURVEY Q9)."""
+    opt = optimizer or torch.optim.AdamW(net.parameters())
+    crit = nn.CrossEntropyLoss()
+    best, best_sd, hist = -1.0, None, []
+    for _ in range(1, epochs + 1):
+        net.train()
+        opt.zero_grad()
+        out = net(Xtr)
+        loss = crit(out, ytr)
+        loss.backward()
+        opt.step()
+        net.eval()  # the reference scores with dropout still active; we score the deterministic net
+        with torch.no_grad():
+            acc = (net(Xte).argmax(1) == yte).float().mean().item()
+        hist.append((loss.item(), acc))
+        if acc > best:
+            best, best_sd = acc, copy.deepcopy(net.state_dict())
+    net.load_state_dict(best_sd)
+    return best, hist
+
+
+class Autoencoder(nn.Module):
+    """Tabular VAE: encoder D->H->H2->H2->latent (BN+ReLU), mu/logvar heads, mirrored decoder."""
+
+    def __init__(self, D_in, H=50, H2=12, latent_dim=3):
+        super().__init__()
+        self.enc = _mlp_bn([D_in, H, H2, H2, latent_dim])
+        self.fc21, self.fc22 = nn.Linear(latent_dim, latent_dim), nn.Linear(latent_dim, latent_dim)
+        self.dec = nn.Sequential(_mlp_bn([latent_dim, latent_dim, H2, H2, H]),
+                                 nn.Linear(H, D_in), nn.BatchNorm1d(D_in))
+        self.optimizer = self.criterion = None
+
+    def encode(self, x):
+        h = self.enc(x)
+        return self.fc21(h), self.fc22(h)
+
+    def reparameterize(self, mu, logvar):
+        if self.training:
+            return mu + torch.randn_like(mu) * torch.exp(0.5 * logvar)
+        return mu
+
+    def decode(self, z):
+        return self.dec(z)
+
+    def forward(self, x):
+        mu, logvar = self.encode(x)
+        return self.decode(self.reparameterize(mu, logvar)), mu, logvar
+
+    def train_with_settings(self, epochs, batch_sz, real_data, optimizer, loss_fn,
+                            zero_grad_per_batch: bool = True, log=None):
+        """Mini-batch training. ``zero_grad_per_batch=False`` reproduces the reference's
+        once-per-epoch zero_grad (gradient accumulation across the epoch)."""
+        self.optimizer, self.criterion = optimizer, loss_fn
+        n = len(real_data)
+        nb = (n + batch_sz - 1) // batch_sz
+        losses = []
+        for epoch in range(epochs):
+            self.train()
+            if not zero_grad_per_batch:
+                optimizer.zero_grad()
+            total = 0.0
+            for b in range(nb):
+                mb = real_data[b * batch_sz:(b + 1) * batch_sz]
+                if zero_grad_per_batch:
+                    optimizer.zero_grad()
+                out, mu, logvar = self(mb)
+                loss = loss_fn(out, mb, mu, logvar)
+                loss.backward()
+                optimizer.step()
+                total += loss.item()
+            losses.append(total / nb)
+            if log:
+                log(epoch, losses[-1])
+        return losses
+
+    @torch.no_grad()
+    def sample(self, nr_samples, dims, logvar, mu, label_col: bool = True, eval_mode: bool = False):
+        """Decode draws from N(mean(mu), mean(sigma)) (the batch-averaged posterior, as the
+        reference does); clip+round the label column. The reference decodes in whatever mode the
+        model is in (train -> BN uses the sample batch's statistics); ``eval_mode`` switches to
+        running statistics."""
+        sigma = torch.exp(logvar / 2)
+        q = torch.distributions.Normal(mu.mean(0), sigma.mean(0))
+        z = q.rsample((nr_samples,))
+        if eval_mode:
+            self.eval()
+        pred = self.decode(z).cpu().numpy()
+        if label_col:
+            pred[:, -1] = np.round(np.clip(pred[:, -1], 0, 1))
+        return pred
+
+
+class customLoss(nn.Module):  # noqa: N801 - reference name
+    def __init__(self):
+        super().__init__()
+        self.mse = nn.MSELoss(reduction="sum")
+
+    def forward(self, x_recon, x, mu, logvar):
+        return self.mse(x_recon, x) - 0.5 * torch.sum(1 + logvar - mu.pow(2) - logvar.exp())
+
+
+# ----------------------------------------------------------------------------------- split-NN
+class BottomModel(nn.Module):
+    def __init__(self, in_feat, out_feat):
+        super().__init__()
+        self.local_out_dim = out_feat
+        self.fc1, self.fc2 = nn.Linear(in_feat, out_feat), nn.Linear(out_feat, out_feat)
+        self.dropout = nn.Dropout(0.1)
+
+    def forward(self, x):
+        return self.dropout(F.relu(self.fc2(F.relu(self.fc1(x)))))
+
+
+class TopModel(nn.Module):
+    """concat -> 128 -> 256 -> 2, LeakyReLU after EVERY layer incl. the logits, then Dropout
+    (kept: it is the reference architecture, vfl.py:35-40 / SURVEY Q7)."""
+
+    def __init__(self, local_models, n_outs=2):
+        super().__init__()
+        self.in_size = sum(m.local_out_dim for m in local_models)
+        self.fc1, self.fc2, self.fc3 = nn.Linear(self.in_size, 128), nn.Linear(128, 256), nn.Linear(256, n_outs)
+        self.act, self.dropout = nn.LeakyReLU(), nn.Dropout(0.1)
+
+    def forward(self, xs):
+        x = torch.cat(xs, 1) if isinstance(xs, (list, tuple)) else xs
+        return self.dropout(self.act(self.fc3(self.act(self.fc2(self.act(self.fc1(x)))))))
+
+
+class VFLNetwork(nn.Module):
+    """Single-process split-NN. Defaults fix the reference's quirks; ``parity=True`` reproduces
+    them: bottom models NOT registered (plain list -> never optimised, Q5), zero_grad once per
+    epoch (Q6), test() without eval() (Q8)."""
+
+    def __init__(self, local_models, n_outs=2, parity: bool = False, lr: float = 1e-3):
+        super().__init__()
+        self.parity = parity
+        if parity:
+            self.bottom_models = list(local_models)
+        else:
+            self.bottom_models = nn.ModuleList(local_models)
+        self.top_model = TopModel(local_models, n_outs)
+        self.optimizer = torch.optim.AdamW(self.parameters(), lr=lr)
+        self.criterion = nn.CrossEntropyLoss()
+        self.num_cli = self.cli_features = None
+
+    def forward(self, xs):
+        return self.top_model([m(x) for m, x in zip(self.bottom_models, xs)])
+
+    def _tensors(self, x, y, cli_features):
+        xs = [torch.tensor(x[f].values.astype(np.float32)) for f in cli_features]
+        yt = torch.tensor(y.values.astype(np.float32))
+        dev = next(self.parameters()).device
+        return [t.to(dev) for t in xs], yt.to(dev)
+
+    def train_with_settings(self, epochs, batch_sz, n_cli, cli_features, x, y, log_loss=None,
+                            verbose=False):
+        self.num_cli, self.cli_features = n_cli, cli_features
+        xs, yt = self._tensors(x, y, cli_features)
+        n = len(yt)
+        nb = (n + batch_sz - 1) // batch_sz
+        hist = []
+        for epoch in range(epochs):
+            self.train()
+            for m in self.bottom_models:
+                m.train()
+            if self.parity:
+                self.optimizer.zero_grad()
+            total, correct = 0.0, 0
+            for b in range(nb):
+                sl = slice(b * batch_sz, (b + 1) * batch_sz)
+                if not self.parity:
+                    self.optimizer.zero_grad()
+                outs = self.forward([t[sl] for t in xs])
+                loss = self.criterion(outs, yt[sl])
+                loss.backward()
+                self.optimizer.step()
+                total += loss.item()
+                correct += (outs.argmax(1) == yt[sl].argmax(1)).sum().item()
+            hist.append((total / nb, correct / n))
+            if log_loss is not None:
+                log_loss(total / nb)
+            if verbose:
+                print(f"Epoch: {epoch} Train accuracy: {100 * correct / n:.2f}% Loss: {total / nb:.3f}")
+        return hist
+
+    def test(self, x, y):
+        xs, yt = self._tensors(x, y, self.cli_features)
+        if not self.parity:
+            self.eval()
+            for m in self.bottom_models:
+                m.eval()
+        with torch.no_grad():
+            outs = self.forward(xs)
+            acc = (outs.argmax(1) == yt.argmax(1)).float().mean()
+            loss = self.criterion(outs, yt)
+        return acc, loss
+
+
+# ------------------------------------------------------------------------------------ VFL-VAE
+class ClientEncoder(nn.Module):
+    def __init__(self, input_dim, latent_dim):
+        super().__init__()
+        self.net = _mlp_bn([input_dim, 48, 32, 32, latent_dim], final_act=True)
+
+    def forward(self, x):
+        return self.net(x)
+
+
+class ClientDecoder(nn.Module):
+    def __init__(self, latent_dim, output_dim):
+        super().__init__()
+        self.net = nn.Sequential(_mlp_bn([latent_dim, latent_dim, 32, 48]),
+                                 nn.Linear(48, output_dim), nn.BatchNorm1d(output_dim))
+
+    def forward(self, z):
+        return self.net(z)
+
+
+class ServerVAE(nn.Module):
+    def __init__(self, D_in, H=48, H2=32, latent_dim=16):
+        super().__init__()
+        self.enc = _mlp_bn([D_in, H, H2, H2, latent_dim])
+        self.fc21, self.fc22 = nn.Linear(latent_dim, latent_dim), nn.Linear(latent_dim, latent_dim)
+        self.dec = nn.Sequential(_mlp_bn([latent_dim, latent_dim, H2, H2, H]),
+                                 nn.Linear(H, D_in), nn.BatchNorm1d(D_in))
+
+    def encode(self, x):
+        h = self.enc(x)
+        return self.fc21(h), self.fc22(h)
+
+    def reparameterize(self, mu, logvar):
+        if self.training:
+            return mu + torch.randn_like(mu) * torch.exp(0.5 * logvar)
+        return mu
+
+    def decode(self, z):
+        return self.dec(z)
+
+    def forward(self, x):
+        mu, logvar = self.encode(x)
+        return self.decode(self.reparameterize(mu, logvar)), mu, logvar
+
+
+class VFLVAE(nn.Module):
+    def __init__(self, client_encoders, server_vae, client_decoders, client_latent_dim):
+        super().__init__()
+        self.client_encoders = nn.ModuleList(client_encoders)
+        self.server_vae = server_vae
+        self.client_decoders = nn.ModuleList(client_decoders)
+        self.client_latent_dim = client_latent_dim
+
+    def forward(self, x_clients):
+        lat = torch.cat([e(x) for e, x in zip(self.client_encoders, x_clients)], 1)
+        recon_concat, mu, logvar = self.server_vae(lat)
+        d = self.client_latent_dim
+        recon = [dec(recon_concat[:, i * d:(i + 1) * d]) for i, dec in enumerate(self.client_decoders)]
+        return recon, mu, logvar, lat, recon_concat
+
+
+def combined_loss(x_clients, recon_clients, concat_latent, recon_concat, mu, logvar):
+    mse = nn.MSELoss(reduction="sum")
+    client = sum(mse(r, x) for x, r in zip(x_clients, recon_clients))
+    return client + mse(recon_concat, concat_latent) - 0.5 * torch.sum(1 + logvar - mu.pow(2) - logvar.exp())

@@ -99,3 +99,65 @@ class AdamW(Adam):
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.01):
         super().__init__(params, lr, betas, eps, weight_decay)
+
+
+class FlatAdam:
+    """Adam / AdamW for plain ``torch.nn.Module`` parameters (the VFL / VAE / LLaMA nets): every
+    parameter (and its .grad) is re-pointed into ONE contiguous fp32 buffer, so a step is a single
+    fused HIP launch instead of torch's per-tensor foreach chain. Same update rule as
+    ``torch.optim.Adam``/``AdamW`` (vfl.py:50, exercise_3.py:190, intro.py:22).
+
+    ``zero_grad`` zeroes in place (grads must stay views of the flat buffer); parameters whose
+    ``requires_grad`` is False are left alone.
+    """
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0, decoupled: bool = False):
+        self.params = [p for p in params if p.requires_grad]
+        if not self.params:
+            raise ValueError("FlatAdam got no trainable parameters")
+        dev = self.params[0].device
+        n = sum(p.numel() for p in self.params)
+        self.data = torch.empty(n, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(n, dtype=torch.float32, device=dev)
+        off = 0
+        with torch.no_grad():
+            for p in self.params:
+                k = p.numel()
+                self.data[off:off + k].copy_(p.detach().reshape(-1))
+                p.data = self.data[off:off + k].view_as(p)
+                p.grad = self.grad[off:off + k].view_as(p)
+                off += k
+        self.m = torch.zeros_like(self.data)
+        self.v = torch.zeros_like(self.data)
+        self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
+        self.decoupled, self.t = decoupled, 0
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.grad.zero_()
+        for p, g in zip(self.params, self._views()):
+            if p.grad is None or p.grad.data_ptr() != g.data_ptr():
+                p.grad = g  # autograd replaced it (e.g. first backward after set_to_none)
+
+    def _views(self):
+        off = 0
+        for p in self.params:
+            k = p.numel()
+            yield self.grad[off:off + k].view_as(p)
+            off += k
+
+    @torch.no_grad()
+    def step(self):
+        for p, g in zip(self.params, self._views()):
+            if p.grad is not None and p.grad.data_ptr() != g.data_ptr():
+                g.copy_(p.grad)
+                p.grad = g
+        self.t += 1
+        Fn.adam_step(self.data, self.grad, self.m, self.v, None, self.lr, self.betas[0],
+                     self.betas[1], self.eps, self.weight_decay, self.t, self.decoupled)
+
+
+class FlatAdamW(FlatAdam):
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.01):
+        super().__init__(params, lr, betas, eps, weight_decay, decoupled=True)
