@@ -21,7 +21,7 @@
 #include "ddl_common.h"
 
 struct BNArgs {
-  const float* stats;    // [G][2C]: sum | sumsq   (finalize input)
+  const float* stats;    // [G][stripes][2C]: sum | sumsq per stripe   (finalize input)
   const float* gamma;    // [G][C] (group stride gs_param)
   const float* beta;
   float* running_mean;   // [G][C] (group stride gs_buf), nullable
@@ -34,7 +34,7 @@ struct BNArgs {
   int G, C;
   long long count;       // M = N*H*W per group
   float eps, momentum;
-  int training, reserved;
+  int training, stripes;  // stripes <= 1: plain [G][2C]
 };
 
 __global__ void bn_finalize_kernel(BNArgs a) {
@@ -43,10 +43,16 @@ __global__ void bn_finalize_kernel(BNArgs a) {
   const int g = i / a.C, c = i - g * a.C;
   float mean, var;
   if (a.training) {
-    const float* st = a.stats + (long long)g * 2 * a.C;
+    const int ns = a.stripes > 1 ? a.stripes : 1;
+    const float* st = a.stats + (long long)g * ns * 2 * a.C;
+    double s1 = 0.0, s2 = 0.0;
+    for (int k = 0; k < ns; ++k) {
+      s1 += st[(long long)k * 2 * a.C + c];
+      s2 += st[(long long)k * 2 * a.C + a.C + c];
+    }
     const double M = (double)a.count;
-    const double m = st[c] / M;
-    double v = st[a.C + c] / M - m * m;
+    const double m = s1 / M;
+    double v = s2 / M - m * m;
     if (v < 0) v = 0;
     mean = (float)m;
     var = (float)v;
@@ -93,7 +99,7 @@ static unsigned stream_blocks(long long M, int RPI, int G, int rows_per_thread) 
 
 // ---------------------------------------------------------------------------------------------
 // y = act(x*scale[c] + shift[c] + residual_term)     residual_term = r*rs[c]+rb[c] | r | 0
-// act: 0 none, 1 relu, 2 leaky(0.01)
+// act: 0 none, 1 relu, 2 leaky(0.01), 3 leaky(0.2) (DCGAN)
 __global__ __launch_bounds__(256) void bn_apply_kernel(
     const bf16_t* __restrict__ x, const float* __restrict__ scale, const float* __restrict__ shift,
     const bf16_t* __restrict__ r, const float* __restrict__ rscale, const float* __restrict__ rshift,
@@ -133,6 +139,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(
     } else if (act == 2) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.01f * v[k];
+    } else if (act == 3) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.2f * v[k];
     }
     *(i4v*)(y + e) = pack8(v);
   }
@@ -151,11 +160,15 @@ DDL_API int ddl_bn_apply(const void* x, const float* scale, const float* shift, 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Backward reduce: per (g, c): s0 = sum dy_m, s1 = sum dy_m * xhat ; dy_m = dy * (ymask > 0)
+// Backward reduce: per (g, c): s0 = sum dy_m, s1 = sum dy_m * xhat ; dy_m = dy * (ymask > 0).
+// Each block folds its rows through LDS (log-depth tree), then adds into stripe
+// (blockIdx.x % NSTRIPE) of part[G][NSTRIPE][2C]; bn_fold sums the stripes into sums[G][2C] and
+// d(beta) += s0, d(gamma) += s1 (one thread per channel, no contended atomics).
+#define BN_NSTRIPE 32
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ ymask, const bf16_t* __restrict__ x,
-    const float* __restrict__ mean, const float* __restrict__ rstd, float* __restrict__ sums,
-    float* __restrict__ dgamma, float* __restrict__ dbeta, long long gs_param, long long M, int C) {
+    const float* __restrict__ mean, const float* __restrict__ rstd, float* __restrict__ part,
+    long long M, int C) {
   __shared__ float red[256 * 17];
   const int g = blockIdx.y;
   const int TPR = C / 8, RPI = 256 / TPR;
@@ -194,40 +207,62 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     red[tid * 17 + 8 + k] = s1[k];
   }
   __syncthreads();
-  if (tid < TPR) {
-    float t0[8], t1[8];
+  int top = 1;
+  while (top < RPI) top <<= 1;
+  for (int half = top >> 1; half > 0; half >>= 1) {  // RPI need not be a power of two (C = 96 ...)
+    if (row < half && row + half < RPI) {
+      const float* o = red + (tid + half * TPR) * 17;
+      float* m = red + tid * 17;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) t0[k] = t1[k] = 0.f;
-    for (int rr = 0; rr < RPI; ++rr) {
-      const int src = rr * TPR + tid;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        t0[k] += red[src * 17 + k];
-        t1[k] += red[src * 17 + 8 + k];
-      }
+      for (int k = 0; k < 16; ++k) m[k] += o[k];
     }
-    float* sg = sums + (long long)g * 2 * C;
+    __syncthreads();
+  }
+  if (row == 0) {
+    float* pg = part + ((long long)g * BN_NSTRIPE + blockIdx.x % BN_NSTRIPE) * 2 * C;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int c = tid * 8 + k;
-      atomicAdd(sg + c, t0[k]);
-      atomicAdd(sg + C + c, t1[k]);
-      if (dbeta) atomicAdd(dbeta + (long long)g * gs_param + c, t0[k]);
-      if (dgamma) atomicAdd(dgamma + (long long)g * gs_param + c, t1[k]);
+      atomicAdd(pg + cc * 8 + k, red[tid * 17 + k]);
+      atomicAdd(pg + C + cc * 8 + k, red[tid * 17 + 8 + k]);
     }
   }
 }
 
+__global__ void bn_fold_kernel(const float* __restrict__ part, float* __restrict__ sums,
+                               float* __restrict__ dgamma, float* __restrict__ dbeta,
+                               long long gs_param, int C, int G) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= G * C) return;
+  const int g = i / C, c = i - g * C;
+  const float* pg = part + (long long)g * BN_NSTRIPE * 2 * C;
+  float t0 = 0.f, t1 = 0.f;
+#pragma unroll 8
+  for (int k = 0; k < BN_NSTRIPE; ++k) {
+    t0 += pg[(long long)k * 2 * C + c];
+    t1 += pg[(long long)k * 2 * C + C + c];
+  }
+  sums[(long long)g * 2 * C + c] = t0;
+  sums[(long long)g * 2 * C + C + c] = t1;
+  if (dbeta) dbeta[(long long)g * gs_param + c] += t0;
+  if (dgamma) dgamma[(long long)g * gs_param + c] += t1;
+}
+
+// part: zeroed [G][BN_NSTRIPE][2C] scratch; sums: [G][2C] output
 DDL_API int ddl_bn_bwd_reduce(const void* dy, const void* ymask, const void* x, const float* mean,
-                              const float* rstd, float* sums, float* dgamma, float* dbeta,
-                              long long gs_param, long long M, int C, int G, hipStream_t s) {
+                              const float* rstd, float* part, float* sums, float* dgamma,
+                              float* dbeta, long long gs_param, long long M, int C, int G,
+                              hipStream_t s) {
   if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
   const int RPI = 256 / (C / 8);
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(stream_blocks(M, RPI, G, 16), G), dim3(256), 0, s,
-                     (const bf16_t*)dy, (const bf16_t*)ymask, (const bf16_t*)x, mean, rstd, sums,
-                     dgamma, dbeta, gs_param, M, C);
+                     (const bf16_t*)dy, (const bf16_t*)ymask, (const bf16_t*)x, mean, rstd, part,
+                     M, C);
+  hipLaunchKernelGGL(bn_fold_kernel, dim3((G * C + 255) / 256), dim3(256), 0, s, part, sums, dgamma,
+                     dbeta, gs_param, C, G);
   return (int)hipGetLastError();
 }
+
+DDL_API int ddl_bn_nstripe() { return BN_NSTRIPE; }
 
 // dx = gamma*rstd*(dy_m - s0/M - xhat*s1/M) = A*dy_m + B*x + Cc
 __global__ void bn_bwd_coef_kernel(const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -296,3 +331,48 @@ DDL_API int ddl_bn_bwd_apply(const void* dy, const void* ymask, const void* x, c
 }
 
 DDL_API int ddl_bn_args_size() { return (int)sizeof(BNArgs); }
+
+// ---------------------------------------------------------------------------------------------
+// Standalone forward statistics (for producers without the conv epilogue: transposed convs,
+// linears of the GAN / tabular nets): stats[g][stripe][c] += sum x, [..][C + c] += sum x^2
+// (stats is [G][BN_NSTRIPE][2C], finalize with stripes = BN_NSTRIPE).
+// Same streaming layout; the RPI rows of one block are folded through LDS, one atomic per channel
+// per block.
+__global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict__ x,
+                                                       float* __restrict__ stats, long long M, int C) {
+  __shared__ float red[256 * 16];
+  const int g = blockIdx.y;
+  const int TPR = C >> 3, RPI = 256 / TPR;
+  const int cc = threadIdx.x % TPR, row = threadIdx.x / TPR;
+  float s1[8] = {}, s2[8] = {};
+  if (row < RPI) {
+    const long long base = (long long)g * M * C + cc * 8;
+    for (long long p = (long long)blockIdx.x * RPI + row; p < M; p += (long long)gridDim.x * RPI) {
+      float v[8];
+      unpack8(*(const i4v*)(x + base + p * C), v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { s1[k] += v[k]; s2[k] += v[k] * v[k]; }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { red[threadIdx.x * 16 + k] = s1[k]; red[threadIdx.x * 16 + 8 + k] = s2[k]; }
+  __syncthreads();
+  if (row == 0) {
+    for (int r = 1; r < RPI; ++r) {
+      const float* o = red + (r * TPR + cc) * 16;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { s1[k] += o[k]; s2[k] += o[8 + k]; }
+    }
+    float* st = stats + ((long long)g * BN_NSTRIPE + blockIdx.x % BN_NSTRIPE) * 2 * C + cc * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { atomicAdd(st + k, s1[k]); atomicAdd(st + C + k, s2[k]); }
+  }
+}
+
+DDL_API int ddl_bn_stats(const void* x, float* stats, long long M, int C, int G, hipStream_t s) {
+  if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
+  const int RPI = 256 / (C / 8);
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(stream_blocks(M, RPI, G, 16), G), dim3(256), 0, s,
+                     (const bf16_t*)x, stats, M, C);
+  return (int)hipGetLastError();
+}

@@ -43,7 +43,8 @@ struct ConvArgs {
   const void* zero;      // >= 64 zero bytes in global memory (DMA source for padding)
   long long x_gs, w_gs, dy_gs, out_gs, bias_gs, stats_gs;
   int G, N, H, W, C, K, R, S, P, Q, stride, pad;
-  int relu, accumulate, split_k, reserved;
+  int relu, accumulate, split_k;
+  int stats_stripes;     // FWD stats: q-tile t adds into stripe t % stripes of [stripes][2K] (<=1: one)
 };
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
@@ -381,7 +382,11 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     const float* bias = a.bias ? a.bias + (long long)g * a.bias_gs : nullptr;
     const bf16_t* res = a.residual ? (const bf16_t*)a.residual + (long long)g * a.out_gs : nullptr;
     const bf16_t* msk = a.mask ? (const bf16_t*)a.mask + (long long)g * a.out_gs : nullptr;
-    float* stats = a.stats ? a.stats + (long long)g * a.stats_gs : nullptr;
+    // striped accumulation: blocks of different pixel tiles hit different copies, so the fp32
+    // atomics of thousands of blocks do not serialise on the same few cache lines
+    float* stats = a.stats ? a.stats + (long long)g * a.stats_gs +
+                                 (a.stats_stripes > 1 ? (long long)((tile / ntp) % a.stats_stripes) * 2 * K : 0)
+                           : nullptr;
 #pragma unroll
     for (int ti = 0; ti < TP; ++ti) {
       const int p = p0 + wp * WP + ti * 16 + lp;
@@ -494,6 +499,8 @@ static hipError_t dispatch(const ConvArgs& a, int Pd, int Qd, int bp, int bq, in
   DDL_CFG(64, 64, 32, 4) DDL_CFG(64, 128, 32, 4) DDL_CFG(128, 64, 32, 4) DDL_CFG(128, 128, 32, 4)
   DDL_CFG(128, 128, 32, 3) DDL_CFG(64, 128, 64, 3) DDL_CFG(128, 128, 64, 3) DDL_CFG(128, 128, 64, 2)
   DDL_CFG(64, 64, 64, 3) DDL_CFG(128, 64, 64, 3)
+  // 256-wide tiles: 128x64 per wave (1.5x the MFMA work per LDS byte of a 64x64 wave tile)
+  DDL_CFG(256, 128, 32, 3) DDL_CFG(128, 256, 32, 3) DDL_CFG(256, 128, 32, 2) DDL_CFG(128, 256, 32, 2)
 #undef DDL_CFG
   return hipErrorInvalidValue;
 }
@@ -519,11 +526,12 @@ static bool conv_shapes_ok(const ConvArgs& a) {
   return a.P > 0 && a.Q > 0;
 }
 
-// cfg = bp | bq<<8 | bk<<16 | ns<<24 (0 = heuristic); WGRAD split-K count in a.split_k (0 = auto)
+// cfg = bp/16 | (bq/16)<<8 | bk<<16 | ns<<24 (0 = heuristic); WGRAD split-K count in a.split_k
+// (0 = auto). Python: ops.functional.conv_cfg(bp, bq, bk, ns).
 static void decode_cfg(int cfg, int& bp, int& bq, int& bk, int& ns) {
   if (!cfg) return;
-  bp = cfg & 0xff;
-  bq = (cfg >> 8) & 0xff;
+  bp = (cfg & 0xff) * 16;
+  bq = ((cfg >> 8) & 0xff) * 16;
   bk = (cfg >> 16) & 0xff;
   ns = (cfg >> 24) & 0xff;
   if (!ns) ns = bk == 32 ? 4 : 3;

@@ -194,3 +194,31 @@ DDL_API int ddl_mse_kl(const float* xr, const float* x, long long n, const float
                      gs, loss, dxr, dmu, dlv);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// Binary cross-entropy on logits (nn.BCEWithLogitsLoss / BCELoss∘sigmoid of the DCGAN
+// discriminator). logits bf16 [R] with row stride ld (column 0 of a padded linear output);
+// target = targets[r] if given else tval. loss += sum_r bce ; dlogits[r*ld] = (sigmoid(l)-t)*gs.
+__global__ void bce_logits_kernel(const bf16_t* __restrict__ logits, int ld, const float* __restrict__ targets,
+                                  float tval, int R, float gs, float* __restrict__ loss,
+                                  bf16_t* __restrict__ dlogits) {
+  float acc = 0.f;
+  for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < R; r += gridDim.x * blockDim.x) {
+    const float l = bf2f(logits[(long long)r * ld]);
+    const float t = targets ? targets[r] : tval;
+    acc += fmaxf(l, 0.f) - l * t + log1pf(__expf(-fabsf(l)));
+    if (dlogits) dlogits[(long long)r * ld] = f2bf((1.f / (1.f + __expf(-l)) - t) * gs);
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) atomicAdd(loss, acc);
+}
+
+DDL_API int ddl_bce_logits(const void* logits, int ld, const float* targets, float tval, int R,
+                           float gs, float* loss, void* dlogits, hipStream_t s) {
+  int b = (R + 255) / 256;
+  if (b > 256) b = 256;
+  if (b < 1) b = 1;
+  hipLaunchKernelGGL(bce_logits_kernel, dim3(b), dim3(256), 0, s, (const bf16_t*)logits, ld, targets,
+                     tval, R, gs, loss, (bf16_t*)dlogits);
+  return (int)hipGetLastError();
+}

@@ -281,14 +281,19 @@ DDL_API int ddl_dropout(const void* x, void* y, long long n, float p, unsigned l
 }
 
 // ---------------------------------------------------------------------------------------------
-// act fwd: 1 relu, 2 leaky(slope); act bwd: dx = dy * act'(y) (y = fwd output; sign preserved)
+// act fwd: 1 relu, 2 leaky(slope), 3 tanh, 4 sigmoid; act bwd: dx = dy * act'(y) computed from the
+// forward OUTPUT y (relu/leaky: sign preserved; tanh: 1-y^2; sigmoid: y(1-y))
 __global__ void act_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n,
                                int act, float slope) {
   GSTRIDE_LOOP(t, n / 8) {
     float v[8];
     unpack8(*(const i4v*)(x + t * 8), v);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : (act == 2 ? slope * v[k] : 0.f);
+    for (int k = 0; k < 8; ++k) {
+      if (act == 3) v[k] = tanhf(v[k]);
+      else if (act == 4) v[k] = 1.f / (1.f + __expf(-v[k]));
+      else v[k] = v[k] > 0.f ? v[k] : (act == 2 ? slope * v[k] : 0.f);
+    }
     *(i4v*)(y + t * 8) = pack8(v);
   }
 }
@@ -299,7 +304,11 @@ __global__ void act_bwd_kernel(const bf16_t* __restrict__ y, const bf16_t* __res
     unpack8(*(const i4v*)(y + t * 8), v);
     unpack8(*(const i4v*)(dy + t * 8), d);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) d[k] = v[k] > 0.f ? d[k] : (act == 2 ? slope * d[k] : 0.f);
+    for (int k = 0; k < 8; ++k) {
+      if (act == 3) d[k] *= 1.f - v[k] * v[k];
+      else if (act == 4) d[k] *= v[k] * (1.f - v[k]);
+      else d[k] = v[k] > 0.f ? d[k] : (act == 2 ? slope * d[k] : 0.f);
+    }
     *(i4v*)(dx + t * 8) = pack8(d);
   }
 }

@@ -1,0 +1,130 @@
+"""Federated DCGAN (FedAvg over generator AND discriminator weights) [NS].
+
+BASELINE config "federated DCGAN on 2xMI355X": each client trains a local (G, D) pair on its
+private image shard for ``local_steps`` Adam steps, then the server takes the n_k-weighted average
+of both networks (and of the BN running statistics), exactly as FedAvgServer does for classifiers
+(reference hfl_complete.py:336-390 is the aggregation template). One rank per GPU; clients are
+assigned round-robin to ranks; the weighted sums of all ranks meet in ONE all-reduce per round
+over a flat fp32 buffer (G params | D params | BN buffers).
+
+Each client keeps its own Adam moments across rounds (swapped in and out of the fused FlatAdam
+buffers), as a real client device would.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..models.dcgan import Discriminator, GANTrainer, Generator
+
+
+@dataclass
+class GANRunResult:
+    rounds: int = 0
+    loss_d: list = field(default_factory=list)
+    loss_g: list = field(default_factory=list)
+    wall_time: list = field(default_factory=list)
+    samples: int = 0
+
+    def rounds_per_sec(self):
+        return len(self.wall_time) / max(sum(self.wall_time), 1e-9)
+
+
+def _flat_buffers(mods):
+    return [b for m in mods for b in m.buffers() if b.dtype.is_floating_point]
+
+
+class FederatedGAN:
+    def __init__(self, client_data: list[torch.Tensor], ctx=None, nz: int = 100, ngf: int = 64,
+                 ndf: int = 64, lr: float = 2e-4, betas=(0.5, 0.999), local_steps: int = 10,
+                 batch_size: int = 64, client_fraction: float = 1.0, seed: int = 0, device=None):
+        self.ctx = ctx
+        self.rank = ctx.rank if ctx else 0
+        self.world = ctx.world_size if ctx else 1
+        self.device = torch.device(device) if device is not None else client_data[0].device
+        torch.manual_seed(seed)
+        self.G = Generator(nz, ngf).to(self.device)
+        self.D = Discriminator(ndf).to(self.device)
+        self.trainer = GANTrainer(self.G, self.D, lr, betas)
+        self.optG, self.optD = self.trainer.optG, self.trainer.optD
+        if ctx and self.world > 1:
+            for t in self._global_tensors():
+                ctx.broadcast(t, 0)
+        self.data = client_data
+        self.n = np.array([len(d) for d in client_data], dtype=np.float64)
+        self.K = max(1, round(client_fraction * len(client_data)))
+        self.rng = np.random.default_rng(seed)
+        self.local_steps, self.batch_size, self.seed = local_steps, batch_size, seed
+        self._state = {}  # client -> (mG, vG, tG, mD, vD, tD)
+
+    # ---------------------------------------------------------------------------------------
+    def _global_tensors(self):
+        """Everything FedAvg averages: parameters (the FlatAdam flat buffers on device) + BN stats."""
+        if hasattr(self.optG, "data"):
+            params = [self.optG.data, self.optD.data]
+        else:
+            params = [p.data for p in list(self.G.parameters()) + list(self.D.parameters())]
+        return params + _flat_buffers([self.G, self.D])
+
+    def _flat(self):
+        return torch.cat([t.detach().reshape(-1).float() for t in self._global_tensors()])
+
+    def _load_flat(self, flat):
+        off = 0
+        with torch.no_grad():
+            for t in self._global_tensors():
+                k = t.numel()
+                t.copy_(flat[off:off + k].view_as(t))
+                off += k
+
+    def _swap_in(self, c):
+        st = self._state.get(c)
+        for opt, i in ((self.optG, 0), (self.optD, 3)):
+            if not hasattr(opt, "m"):
+                continue
+            if st is None:
+                opt.m.zero_(); opt.v.zero_(); opt.t = 0
+            else:
+                opt.m.copy_(st[i]); opt.v.copy_(st[i + 1]); opt.t = st[i + 2]
+
+    def _swap_out(self, c):
+        if hasattr(self.optG, "m"):
+            self._state[c] = (self.optG.m.clone(), self.optG.v.clone(), self.optG.t,
+                              self.optD.m.clone(), self.optD.v.clone(), self.optD.t)
+
+    # ---------------------------------------------------------------------------------------
+    def run(self, rounds: int) -> GANRunResult:
+        res = GANRunResult()
+        for r in range(rounds):
+            t0 = time.perf_counter()
+            chosen = self.rng.choice(len(self.data), self.K, replace=False)
+            mine = chosen[self.rank::self.world]
+            glob = self._flat()
+            acc = torch.zeros_like(glob)
+            wsum = self.n[chosen].sum()
+            ld_sum = lg_sum = 0.0
+            for c in mine:
+                self._load_flat(glob)
+                self._swap_in(int(c))
+                g = torch.Generator(device="cpu").manual_seed(self.seed + int(c) + 1 + r * self.K)
+                data = self.data[int(c)]
+                for _ in range(self.local_steps):
+                    idx = torch.randint(0, len(data), (self.batch_size,), generator=g).to(data.device)
+                    ld, lg = self.trainer.step(data.index_select(0, idx))
+                    res.samples += self.batch_size
+                ld_sum += float(ld); lg_sum += float(lg)
+                self._swap_out(int(c))
+                acc.add_(self._flat(), alpha=float(self.n[c] / wsum))
+            if self.ctx and self.world > 1:
+                self.ctx.all_reduce(acc)
+            self._load_flat(acc)
+            if self.device.type == "cuda":
+                torch.cuda.synchronize()
+            res.wall_time.append(time.perf_counter() - t0)
+            res.loss_d.append(ld_sum / max(1, len(mine)))
+            res.loss_g.append(lg_sum / max(1, len(mine)))
+            res.rounds += 1
+        return res

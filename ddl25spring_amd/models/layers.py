@@ -133,10 +133,10 @@ class ConvUnit(Layer):
         g = self.geom(x4)
         w = st.shadow_of(self.w)
         if self.bn:
-            stats = ws.zeros((g.G, 2, self.cout), x.device) if train else None
+            stats = Fn.stats_buffer(g.G, self.cout, x.device) if train else None
             c = Fn.conv_fwd(x4, w, g, stats=stats)
             count = g.N * g.P * g.Q
-            sc, sh, mu, rs = Fn.bn_finalize(stats if train else ws.zeros((g.G, 2, self.cout), x.device),
+            sc, sh, mu, rs = Fn.bn_finalize(stats if train else Fn.stats_buffer(g.G, self.cout, x.device),
                                             st.param(self.gamma), st.param(self.beta),
                                             st.buffer(self.rm), st.buffer(self.rv), count,
                                             self.eps, self.momentum, training=train)

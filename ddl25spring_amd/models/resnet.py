@@ -31,7 +31,7 @@ class _BNConv(ConvUnit):
     def conv_stats(self, x, train):
         st = self.store
         g = self.geom(x)
-        stats = torch.zeros(g.G, 2, self.cout, dtype=torch.float32, device=x.device) if train else None
+        stats = Fn.stats_buffer(g.G, self.cout, x.device) if train else None
         c = Fn.conv_fwd(x, st.shadow_of(self.w), g, stats=stats)
         if not train:
             stats = ws.zeros((g.G, 2, self.cout), x.device)

@@ -176,14 +176,19 @@ class TopModel(nn.Module):
 
 
 class VFLNetwork(nn.Module):
-    """Single-process split-NN. Defaults fix the reference's quirks; ``parity=True`` reproduces
-    them: bottom models NOT registered (plain list -> never optimised, Q5), zero_grad once per
-    epoch (Q6), test() without eval() (Q8)."""
+    """Single-process split-NN. Defaults fix the reference's quirks; each can be restored on its
+    own, or all at once with ``parity=True``: ``register_bottoms=False`` keeps the bottom models in
+    a plain list (never optimised, Q5), ``zero_grad_per_batch=False`` zeroes once per epoch
+    (gradient accumulation, Q6), ``eval_in_test=False`` tests with dropout active (Q8)."""
 
-    def __init__(self, local_models, n_outs=2, parity: bool = False, lr: float = 1e-3):
+    def __init__(self, local_models, n_outs=2, parity: bool = False, lr: float = 1e-3,
+                 register_bottoms: bool | None = None, zero_grad_per_batch: bool | None = None,
+                 eval_in_test: bool | None = None):
         super().__init__()
-        self.parity = parity
-        if parity:
+        pick = lambda v: (not parity) if v is None else v  # noqa: E731
+        self.register_bottoms, self.zero_grad_per_batch = pick(register_bottoms), pick(zero_grad_per_batch)
+        self.eval_in_test = pick(eval_in_test)
+        if not self.register_bottoms:
             self.bottom_models = list(local_models)
         else:
             self.bottom_models = nn.ModuleList(local_models)
@@ -212,12 +217,12 @@ class VFLNetwork(nn.Module):
             self.train()
             for m in self.bottom_models:
                 m.train()
-            if self.parity:
+            if not self.zero_grad_per_batch:
                 self.optimizer.zero_grad()
             total, correct = 0.0, 0
             for b in range(nb):
                 sl = slice(b * batch_sz, (b + 1) * batch_sz)
-                if not self.parity:
+                if self.zero_grad_per_batch:
                     self.optimizer.zero_grad()
                 outs = self.forward([t[sl] for t in xs])
                 loss = self.criterion(outs, yt[sl])
@@ -234,7 +239,7 @@ class VFLNetwork(nn.Module):
 
     def test(self, x, y):
         xs, yt = self._tensors(x, y, self.cli_features)
-        if not self.parity:
+        if self.eval_in_test:
             self.eval()
             for m in self.bottom_models:
                 m.eval()

@@ -39,14 +39,14 @@ class ConvArgs(ctypes.Structure):
                 ("stats_gs", i64),
                 ("G", i32), ("N", i32), ("H", i32), ("W", i32), ("C", i32), ("K", i32), ("R", i32),
                 ("S", i32), ("P", i32), ("Q", i32), ("stride", i32), ("pad", i32),
-                ("relu", i32), ("accumulate", i32), ("split_k", i32), ("reserved", i32)]
+                ("relu", i32), ("accumulate", i32), ("split_k", i32), ("stats_stripes", i32)]
 
 
 class BNArgs(ctypes.Structure):
     _fields_ = [("stats", vp), ("gamma", vp), ("beta", vp), ("running_mean", vp),
                 ("running_var", vp), ("scale", vp), ("shift", vp), ("mean", vp), ("rstd", vp),
                 ("gs_param", i64), ("gs_buf", i64), ("G", i32), ("C", i32), ("count", i64),
-                ("eps", f32), ("momentum", f32), ("training", i32), ("reserved", i32)]
+                ("eps", f32), ("momentum", f32), ("training", i32), ("stripes", i32)]
 
 
 class SGDArgs(ctypes.Structure):
@@ -70,8 +70,9 @@ _SIGS = {
     # batchnorm.hip
     "ddl_bn_finalize": [ctypes.POINTER(BNArgs), vp],
     "ddl_bn_apply": [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, vp],
-    "ddl_bn_bwd_reduce": [vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i32, i32, vp],
+    "ddl_bn_bwd_reduce": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i32, i32, vp],
     "ddl_bn_bwd_apply": [vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, i64, i32, i32, vp],
+    "ddl_bn_stats": [vp, vp, i64, i32, i32, vp],
     # nn_ops.hip
     "ddl_prep_images": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
     "ddl_nchw_to_nhwc": [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
@@ -91,6 +92,7 @@ _SIGS = {
     "ddl_ce_fwd_bwd": [vp, vp, vp, i32, i32, i32, i32, f32, vp, vp, vp, vp],
     "ddl_ce_vocab": [vp, vp, i32, i32, i32, f32, i32, vp, vp, vp],
     "ddl_mse_kl": [vp, vp, i64, vp, vp, i64, f32, f32, vp, vp, vp, vp, vp],
+    "ddl_bce_logits": [vp, i32, vp, f32, i32, f32, vp, vp, vp],
     # optim.hip
     "ddl_sgd": [ctypes.POINTER(SGDArgs), vp],
     "ddl_adam": [ctypes.POINTER(AdamArgs), vp],

@@ -303,3 +303,201 @@ def cross_entropy_vocab(logits, targets, ignore_index=-100):
         return F.cross_entropy(logits.reshape(-1, logits.shape[-1]).float(), targets.reshape(-1).long(),
                                ignore_index=ignore_index)
     return _VocabCE.apply(logits, targets, ignore_index)
+
+
+# ===================================================================== image ops (NHWC, GANs)
+# Activations are NHWC [N, H, W, C]; conv weights are fp32 parameters in the kernels' layout
+# [K, R, S, C] (conv) / [Cin, R, S, Cout] (transposed conv). Channel counts must be multiples of
+# 32 on the device (pad small ones, e.g. RGB 3 -> 32, with zero weights: they stay exactly zero).
+def _geom(x_shape, C, K, R, S, stride, pad):
+    N, H, W = x_shape[0], x_shape[1], x_shape[2]
+    return Fn.ConvGeom(1, N, H, W, C, K, R, S, stride, pad)
+
+
+class _Conv2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride, pad, want_stats):
+        Kc, R, S, C = w.shape
+        g = _geom(x.shape, C, Kc, R, S, stride, pad)
+        wb = _bf16_weight(w).view(1, Kc, R, S, C)
+        stats = Fn.stats_buffer(1, Kc, x.device) if want_stats else None
+        y = Fn.conv_fwd(x.contiguous().view(1, *x.shape), wb, g, stats=stats)
+        ctx.save_for_backward(x, wb)
+        ctx.g = g
+        if want_stats:
+            ctx.mark_non_differentiable(stats)
+        return y.view(g.N, g.P, g.Q, Kc), stats
+
+    @staticmethod
+    def backward(ctx, dy, _dstats):
+        x, wb = ctx.saved_tensors
+        g = ctx.g
+        dy5 = dy.to(torch.bfloat16).contiguous().view(1, g.N, g.P, g.Q, g.K)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = Fn.conv_dgrad(dy5, wb, g).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            dw = torch.zeros(1, g.K, g.R, g.S, g.C, dtype=torch.float32, device=dy.device)
+            Fn.conv_wgrad(dy5, x.contiguous().view(1, *x.shape), g, dw)
+            dw = dw.view(g.K, g.R, g.S, g.C)
+        return dx, dw, None, None, None
+
+
+def conv2d(x, w, stride=1, pad=0, with_stats=False):
+    """NHWC conv, weight [K, R, S, C]. with_stats: also return the per-channel (sum, sumsq) [1,2,K]
+    of the output, computed in the MFMA epilogue (feeds ``batch_norm_act``)."""
+    if not x.is_cuda:
+        y = F.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), stride=stride, padding=pad)
+        y = y.permute(0, 2, 3, 1)
+        return (y, None) if with_stats else y
+    if x.dtype != torch.bfloat16:
+        x = x.to(torch.bfloat16)
+    y, st = _Conv2d.apply(x, w, stride, pad, with_stats)
+    return (y, st) if with_stats else y
+
+
+class _ConvT2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride, pad):
+        Cin, R, S, Cout = w.shape
+        N, Hi, Wi, _ = x.shape
+        Ho, Wo = (Hi - 1) * stride - 2 * pad + R, (Wi - 1) * stride - 2 * pad + S
+        g = Fn.ConvGeom(1, N, Ho, Wo, Cout, Cin, R, S, stride, pad)  # the conv this one transposes
+        assert (g.P, g.Q) == (Hi, Wi), "transposed conv geometry must invert exactly"
+        wb = _bf16_weight(w).view(1, Cin, R, S, Cout)
+        y = Fn.conv_dgrad(x.contiguous().view(1, N, Hi, Wi, Cin), wb, g)
+        ctx.save_for_backward(x, wb)
+        ctx.g = g
+        return y.view(N, Ho, Wo, Cout)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wb = ctx.saved_tensors
+        g = ctx.g
+        dy5 = dy.to(torch.bfloat16).contiguous().view(1, g.N, g.H, g.W, g.C)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = Fn.conv_fwd(dy5, wb, g).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            dw = torch.zeros(1, g.K, g.R, g.S, g.C, dtype=torch.float32, device=dy.device)
+            Fn.conv_wgrad(x.contiguous().view(1, *x.shape), dy5, g, dw)
+            dw = dw.view(g.K, g.R, g.S, g.C)
+        return dx, dw, None, None
+
+
+def conv_transpose2d(x, w, stride=1, pad=0):
+    """NHWC transposed conv (nn.ConvTranspose2d, no bias), weight [Cin, R, S, Cout]: runs as the
+    dgrad of the conv it transposes (phase-decomposed for stride 2), backward = conv fwd + wgrad."""
+    if not x.is_cuda:
+        y = F.conv_transpose2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), stride=stride, padding=pad)
+        return y.permute(0, 2, 3, 1)
+    if x.dtype != torch.bfloat16:
+        x = x.to(torch.bfloat16)
+    return _ConvT2d.apply(x, w, stride, pad)
+
+
+_BN_ACT = {"none": 0, "relu": 1, "leaky_relu": 3}  # bn_apply codes (3 = leaky 0.2)
+
+
+class _BatchNormAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, running_mean, running_var, stats, training, momentum, eps, act):
+        C = x.shape[-1]
+        xg = x.contiguous().view(1, -1, C)
+        M = xg.shape[1]
+        if training and stats is None:
+            stats = Fn.bn_stats(xg)
+        if stats is None:
+            stats = torch.zeros(1, 2, C, dtype=torch.float32, device=x.device)
+        ga, be = gamma.detach().view(1, C), beta.detach().view(1, C)
+        rm = running_mean.view(1, C) if running_mean is not None else None
+        rv = running_var.view(1, C) if running_var is not None else None
+        scale, shift, mean, rstd = Fn.bn_finalize(stats, ga, be, rm, rv, M, eps, momentum, training)
+        y = Fn.bn_apply(xg, scale, shift, act=_BN_ACT[act])
+        ctx.save_for_backward(xg, y, mean, rstd, ga)
+        ctx.act, ctx.shape = act, x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xg, y, mean, rstd, ga = ctx.saved_tensors
+        C = xg.shape[-1]
+        d = dy.to(torch.bfloat16).contiguous().view_as(xg)
+        ymask = None
+        if ctx.act == "relu":
+            ymask = y
+        elif ctx.act == "leaky_relu":
+            d = Fn.act_bwd(y, d, 2, 0.2)
+        dgamma = torch.zeros(1, C, dtype=torch.float32, device=dy.device)
+        dbeta = torch.zeros(1, C, dtype=torch.float32, device=dy.device)
+        sums = Fn.bn_bwd_reduce(d, ymask, xg, mean, rstd, dgamma, dbeta)
+        dx = Fn.bn_bwd_apply(d, ymask, xg, mean, rstd, ga, sums)
+        return dx.view(ctx.shape), dgamma.view(C), dbeta.view(C), None, None, None, None, None, None, None
+
+
+def batch_norm_act(x, gamma, beta, running_mean=None, running_var=None, training=True,
+                   momentum=0.1, eps=1e-5, act="none", stats=None):
+    """BatchNorm over all but the last (channel) dim + fused activation ('none' | 'relu' |
+    'leaky_relu' (slope 0.2)). ``stats`` (sum, sumsq) may come from a conv epilogue."""
+    if not x.is_cuda:
+        C = x.shape[-1]
+        y = F.batch_norm(x.reshape(-1, C), running_mean, running_var, gamma, beta, training,
+                         momentum, eps).view(x.shape)
+        return {"none": y, "relu": F.relu(y), "leaky_relu": F.leaky_relu(y, 0.2)}[act]
+    if x.dtype != torch.bfloat16:
+        x = x.to(torch.bfloat16)
+    return _BatchNormAct.apply(x, gamma, beta, running_mean, running_var, stats, training, momentum,
+                               eps, act)
+
+
+_ACT = {"relu": (1, 0.0), "leaky_relu": (2, 0.2), "tanh": (3, 0.0), "sigmoid": (4, 0.0)}
+
+
+class _Act(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, kind):
+        code, slope = _ACT[kind]
+        y = Fn.act_fwd(x.contiguous(), code, slope)
+        ctx.save_for_backward(y)
+        ctx.code, ctx.slope = code, slope
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        return Fn.act_bwd(y, dy.to(torch.bfloat16).contiguous(), ctx.code, ctx.slope), None
+
+
+def activation(x, kind):
+    """'relu' | 'leaky_relu' (0.2) | 'tanh' | 'sigmoid' — one elementwise HIP pass each way."""
+    if not x.is_cuda:
+        return {"relu": F.relu, "leaky_relu": lambda t: F.leaky_relu(t, 0.2),
+                "tanh": torch.tanh, "sigmoid": torch.sigmoid}[kind](x)
+    if x.dtype != torch.bfloat16:
+        x = x.to(torch.bfloat16)
+    return _Act.apply(x, kind)
+
+
+class _BCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target):
+        R = logits.shape[0]
+        loss, dl = Fn.bce_logits(logits.contiguous(), target, scale=1.0 / R)
+        ctx.save_for_backward(dl)
+        return (loss / R).reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        (dl,) = ctx.saved_tensors
+        return (dl.float() * g).to(dl.dtype), None
+
+
+def bce_with_logits(logits, target):
+    """mean BCE-with-logits on column 0 of ``logits`` [R, ld] (the padded 1-unit head);
+    target: python float (all rows) or fp32 [R]."""
+    if not logits.is_cuda:
+        t = target if torch.is_tensor(target) else torch.full((logits.shape[0],), float(target))
+        return F.binary_cross_entropy_with_logits(logits[:, 0].float(), t.float())
+    if logits.dtype != torch.bfloat16:
+        logits = logits.to(torch.bfloat16)
+    return _BCE.apply(logits, target)

@@ -61,6 +61,17 @@ def zero_page(device) -> torch.Tensor:
     return z
 
 
+def conv_cfg(bp: int, bq: int, bk: int, ns: int) -> int:
+    """Explicit conv tile choice (BP x BQ output tile, BK reduction step, NS LDS stages)."""
+    return (bp // 16) | ((bq // 16) << 8) | (bk << 16) | (ns << 24)
+
+
+CONV_TILES = [(64, 64, 32, 4), (64, 128, 32, 4), (128, 64, 32, 4), (128, 128, 32, 4),
+              (128, 128, 32, 3), (64, 128, 64, 3), (128, 128, 64, 3), (128, 128, 64, 2),
+              (64, 64, 64, 3), (128, 64, 64, 3), (256, 128, 32, 3), (128, 256, 32, 3),
+              (256, 128, 32, 2), (128, 256, 32, 2)]
+
+
 def _conv_args(geom: ConvGeom, device=None, **kw) -> _lib.ConvArgs:
     a = _lib.ConvArgs()
     if device is not None:
@@ -78,10 +89,19 @@ def _check_inner(t: torch.Tensor, name: str) -> None:
         raise ValueError(f"{name}: per-group inner dims must be contiguous")
 
 
+BN_STRIPES = 32  # == BN_NSTRIPE in batchnorm.hip
+
+
+def stats_buffer(G: int, C: int, device) -> torch.Tensor:
+    """Zeroed BN statistics accumulator [G, BN_STRIPES, 2, C]: producers (conv epilogue, bn_stats)
+    spread their fp32 atomics over the stripes, bn_finalize folds them."""
+    return ws.zeros((G, BN_STRIPES, 2, C), device)
+
+
 def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out=None, cfg=0,
              residual=None):
     """y[G,N,P,Q,K] = conv(x[G,N,H,W,C], w[G,K,R,S,C]) (+bias)(+residual)(relu);
-    stats[G,2,K] += sum, sumsq of y."""
+    stats ([G,S,2,K] from ``stats_buffer``, or [G,2,K]) += per-channel sum, sumsq of y."""
     if not x.is_cuda:
         y = ref.conv_fwd(x, w, geom, bias, relu, stats)
         if residual is not None:
@@ -98,7 +118,7 @@ def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out=None, 
     a = _conv_args(geom, x.device, x=ptr(x), w=ptr(w), out=ptr(y), stats=ptr(stats), bias=ptr(bias),
                    residual=ptr(residual), x_gs=_gs(x), w_gs=_gs(w), out_gs=_gs(y),
                    bias_gs=_gs(bias), stats_gs=0 if stats is None else stats.stride(0),
-                   relu=int(relu))
+                   relu=int(relu), stats_stripes=stats.shape[1] if stats is not None and stats.dim() == 4 else 1)
     check(_lib.kernels().ddl_conv_fwd(ctypes.byref(a), cfg, stream()), "conv_fwd")
     return y
 
@@ -126,7 +146,7 @@ def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0)
 
 def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0):
     """dw[G,K,R,S,C] (+)= sum over pixels dy (x) x  — fp32, split-K with atomics.
-    cfg = bp | bq<<8 | bk<<16 | stages<<24 (0: tuned default); splits = split-K slices (0: auto)."""
+    cfg = conv_cfg(bp, bq, bk, stages) (0: tuned default); splits = split-K slices (0: auto)."""
     if not dy.is_cuda:
         ref.conv_wgrad(dy, x, geom, dw, accumulate)
         return dw
@@ -155,6 +175,8 @@ def bn_finalize(stats, gamma, beta, running_mean, running_var, count, eps=1e-5, 
     a.gs_buf = _gs(running_mean)
     a.G, a.C, a.count = G, C, int(count)
     a.eps, a.momentum, a.training = float(eps), float(momentum), int(training)
+    a.stripes = stats.shape[1] if stats.dim() == 4 else 1
+    assert stats.is_contiguous()
     check(_lib.kernels().ddl_bn_finalize(ctypes.byref(a), stream()), "bn_finalize")
     return outs[0], outs[1], outs[2], outs[3]
 
@@ -175,15 +197,30 @@ def bn_apply(x, scale, shift, r=None, rscale=None, rshift=None, act=0, out=None)
     return y
 
 
+def bn_stats(x, stats=None):
+    """stats [G, BN_STRIPES, 2, C] fp32 (+)= per-channel (sum, sum of squares) of x [G, ..., C]."""
+    G, C = x.shape[0], x.shape[-1]
+    if stats is None:
+        stats = stats_buffer(G, C, x.device)
+    if not x.is_cuda:
+        ref.bn_stats(x, stats)
+        return stats
+    assert x.is_contiguous() and x.dtype == torch.bfloat16 and stats.shape[1] == BN_STRIPES
+    check(_lib.kernels().ddl_bn_stats(ptr(x), ptr(stats), x[0].numel() // C, C, G, stream()),
+          "bn_stats")
+    return stats
+
+
 def bn_bwd_reduce(dy, ymask, x, mean, rstd, dgamma=None, dbeta=None):
     """-> sums [G, 2, C] = (sum dy_m, sum dy_m*xhat); also accumulates into dgamma/dbeta views."""
     if not dy.is_cuda:
         return ref.bn_bwd_reduce(dy, ymask, x, mean, rstd, dgamma, dbeta)
     G, C = x.shape[0], x.shape[-1]
-    sums = ws.zeros((G, 2, C), x.device)
+    part = ws.zeros((G, BN_STRIPES, 2, C), x.device)
+    sums = ws.scratch((G, 2, C), x.device)
     gs = _gs(dgamma) if dgamma is not None else _gs(dbeta)
     check(_lib.kernels().ddl_bn_bwd_reduce(ptr(dy), ptr(ymask), ptr(x), ptr(mean), ptr(rstd),
-                                           ptr(sums), ptr(dgamma), ptr(dbeta), gs,
+                                           ptr(part), ptr(sums), ptr(dgamma), ptr(dbeta), gs,
                                            x[0].numel() // C, C, G, stream()), "bn_bwd_reduce")
     return sums
 
@@ -251,7 +288,7 @@ def dropout(x, p, seed, offset):
     return y
 
 
-ACT = {"none": 0, "relu": 1, "leaky_relu": 2}
+ACT = {"none": 0, "relu": 1, "leaky_relu": 2, "tanh": 3, "sigmoid": 4}
 
 
 def act_fwd(x, act: int, slope=0.01):
@@ -423,6 +460,28 @@ def adam_step(p, g, m, v, shadow, lr, beta1, beta2, eps, wd, step, decoupled, gr
     a.bc1, a.bc2 = 1 - beta1 ** step, 1 - beta2 ** step
     a.decoupled = int(decoupled)
     check(_lib.kernels().ddl_adam(ctypes.byref(a), stream()), "adam")
+
+
+def bce_logits(logits, target, scale=1.0, want_grad=True):
+    """Binary CE on column 0 of logits [R, ld] (bf16). target: float or fp32 [R] tensor.
+    -> (loss_sum fp32 [1], dlogits [R, ld] bf16 with (sigmoid(l)-t)*scale in column 0, or None)."""
+    R, ld = logits.shape
+    if not logits.is_cuda:
+        t = target if torch.is_tensor(target) else torch.full((R,), float(target))
+        loss, d = ref.bce_logits(logits[:, 0].float(), t.float())
+        dl = None
+        if want_grad:
+            dl = torch.zeros_like(logits)
+            dl[:, 0] = (d * scale).to(logits.dtype)
+        return loss.reshape(1), dl
+    assert logits.is_contiguous() and logits.dtype == torch.bfloat16
+    loss = torch.zeros(1, dtype=torch.float32, device=logits.device)
+    dl = torch.zeros_like(logits) if want_grad else None
+    tt = target.float().contiguous() if torch.is_tensor(target) else None
+    tv = 0.0 if tt is not None else float(target)
+    check(_lib.kernels().ddl_bce_logits(ptr(logits), ld, ptr(tt), tv, R, float(scale), ptr(loss), ptr(dl),
+                                        stream()), "bce_logits")
+    return loss, dl
 
 
 # ------------------------------------------------------------------------------- aggregation

@@ -37,8 +37,9 @@ def conv_fwd(x, w, geom, bias=None, relu=False, stats=None):
             y = y.clamp_min(0)
         if stats is not None:
             flat = y.reshape(-1, geom.K)
-            stats[g, 0] += flat.sum(0)
-            stats[g, 1] += (flat * flat).sum(0)
+            st = stats[g, 0] if stats.dim() == 4 else stats[g]
+            st[0] += flat.sum(0)
+            st[1] += (flat * flat).sum(0)
         outs.append(y)
     return _bf(torch.stack(outs)).contiguous()
 
@@ -73,6 +74,8 @@ def conv_wgrad(dy, x, geom, dw, accumulate=True):
 
 
 def bn_finalize(stats, gamma, beta, running_mean, running_var, count, eps, momentum, training):
+    if stats.dim() == 4:  # striped [G, S, 2, C]
+        stats = stats.sum(1)
     if training:
         mean = stats[:, 0] / count
         var = (stats[:, 1] / count - mean * mean).clamp_min(0)
@@ -96,7 +99,16 @@ def _act(y, act, slope=0.01):
         return y.clamp_min(0)
     if act == 2:
         return torch.where(y > 0, y, slope * y)
+    if act == 3:
+        return torch.tanh(y)
+    if act == 4:
+        return torch.sigmoid(y)
     return y
+
+
+def _bn_act(y, act):
+    # bn_apply's act code 3 is leaky(0.2) (act_fwd's 3 is tanh)
+    return torch.where(y > 0, y, 0.2 * y) if act == 3 else _act(y, act)
 
 
 def _bcast(v, x):
@@ -112,7 +124,7 @@ def bn_apply(x, scale, shift, r=None, rscale=None, rshift=None, act=0):
         if rscale is not None:
             rv = rv * _bcast(rscale, x) + _bcast(rshift, x)
         y = y + rv
-    return _bf(_act(y, act)).contiguous()
+    return _bf(_bn_act(y, act)).contiguous()
 
 
 def bn_bwd_reduce(dy, ymask, x, mean, rstd, dgamma=None, dbeta=None):
@@ -193,9 +205,27 @@ def act_bwd(y, dy, act, slope=0.01):
     d = dy.float()
     if act == 1:
         d = d * (yf > 0)
+    elif act == 3:
+        d = d * (1 - yf * yf)
+    elif act == 4:
+        d = d * yf * (1 - yf)
     else:
         d = torch.where(yf > 0, d, slope * d)
     return _bf(d).contiguous()
+
+
+def bn_stats(x, stats):
+    C = x.shape[-1]
+    xf = x.float().reshape(x.shape[0], -1, C)
+    st = stats[:, 0] if stats.dim() == 4 else stats
+    st[:, 0] += xf.sum(1)
+    st[:, 1] += (xf * xf).sum(1)
+
+
+def bce_logits(l, t):
+    """-> (sum loss, dloss/dl)."""
+    loss = (l.clamp_min(0) - l * t + torch.log1p(torch.exp(-l.abs()))).sum()
+    return loss, torch.sigmoid(l) - t
 
 
 def channel_sum(x, out):

@@ -117,17 +117,20 @@ class FlatAdam:
         if not self.params:
             raise ValueError("FlatAdam got no trainable parameters")
         dev = self.params[0].device
-        n = sum(p.numel() for p in self.params)
-        self.data = torch.empty(n, dtype=torch.float32, device=dev)
+        # every tensor starts on a 256-byte boundary (same alignment class as a fresh allocation,
+        # so BLAS picks the same kernels as for unflattened parameters); gaps stay zero
+        self.offsets, n = [], 0
+        for p in self.params:
+            self.offsets.append(n)
+            n += (p.numel() + 63) // 64 * 64
+        self.data = torch.zeros(n, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(n, dtype=torch.float32, device=dev)
-        off = 0
         with torch.no_grad():
-            for p in self.params:
+            for p, off in zip(self.params, self.offsets):
                 k = p.numel()
                 self.data[off:off + k].copy_(p.detach().reshape(-1))
                 p.data = self.data[off:off + k].view_as(p)
                 p.grad = self.grad[off:off + k].view_as(p)
-                off += k
         self.m = torch.zeros_like(self.data)
         self.v = torch.zeros_like(self.data)
         self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
@@ -140,11 +143,8 @@ class FlatAdam:
                 p.grad = g  # autograd replaced it (e.g. first backward after set_to_none)
 
     def _views(self):
-        off = 0
-        for p in self.params:
-            k = p.numel()
-            yield self.grad[off:off + k].view_as(p)
-            off += k
+        for p, off in zip(self.params, self.offsets):
+            yield self.grad[off:off + p.numel()].view_as(p)
 
     @torch.no_grad()
     def step(self):

@@ -47,8 +47,7 @@ def timeit(fn, reps=10, rounds=5):
     return statistics.median(ts)
 
 
-CFGS = [(64, 64, 32, 4), (64, 128, 32, 4), (128, 64, 32, 4), (128, 128, 32, 4), (128, 128, 32, 3),
-        (64, 128, 64, 3), (128, 128, 64, 3), (128, 128, 64, 2), (64, 64, 64, 3), (128, 64, 64, 3)]
+CFGS = Fn.CONV_TILES
 
 
 def main():
@@ -68,10 +67,11 @@ def main():
         w = (torch.randn(g.G, g.K, g.R, g.S, g.C, device=dev) * 0.05).to(torch.bfloat16)
         dy = torch.randn(g.G, g.N, g.P, g.Q, g.K, device=dev).to(torch.bfloat16)
         dw = torch.zeros(g.G, g.K, g.R, g.S, g.C, device=dev)
+        st = Fn.stats_buffer(g.G, g.K, dev)  # fwd runs with the BN-statistics epilogue, as in training
         fl = g.flops()
         row = {"layer": name, "geom": str(g), "gflop": fl / 1e9}
         modes = {
-            "fwd": lambda cfg: Fn.conv_fwd(x, w, g, cfg=cfg),
+            "fwd": lambda cfg: Fn.conv_fwd(x, w, g, cfg=cfg, stats=st),
             "dgrad": lambda cfg: Fn.conv_dgrad(dy, w, g, cfg=cfg),
             "wgrad": lambda cfg: Fn.conv_wgrad(dy, x, g, dw, cfg=cfg),
         }
@@ -88,7 +88,7 @@ def main():
                         continue
                     if mode == "dgrad" and g.K % bk:
                         continue
-                    cfg = bp | (bq << 8) | (bk << 16) | (ns << 24)
+                    cfg = Fn.conv_cfg(bp, bq, bk, ns)
                     try:
                         tc = timeit(lambda: f(cfg), reps=5, rounds=3)
                     except Exception:

@@ -1,0 +1,117 @@
+"""DCGAN ops (conv / transposed conv / BN+act / act / BCE) vs fp32 PyTorch, and the GAN models."""
+import numpy as np
+import pytest
+import torch
+
+from ddl25spring_amd.models.dcgan import Discriminator, GANTrainer, Generator, to_nhwc_padded
+from ddl25spring_amd.ops import autograd_ops as A
+
+
+def _rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def test_dcgan_cpu_shapes_and_padding_stays_zero():
+    torch.manual_seed(0)
+    G, D = Generator(), Discriminator()
+    tr = GANTrainer(G, D)
+    real = to_nhwc_padded(torch.rand(8, 3, 32, 32) * 2 - 1)
+    assert real.shape == (8, 32, 32, 32)
+    for _ in range(2):
+        ld, lg = tr.step(real)
+    assert torch.isfinite(ld) and torch.isfinite(lg)
+    img = G.sample(4)
+    assert img.shape == (4, 32, 32, 32) and img[..., 3:].abs().max() == 0
+    assert G.up3[..., 3:].abs().max() == 0 and D.c0[..., 3:].abs().max() == 0
+    assert G.proj[:, 100:].abs().max() == 0 and D.head[1:].abs().max() == 0
+    assert D(img).shape == (4, 32)
+
+
+@pytest.mark.gpu
+def test_gan_ops_match_fp32(cuda):
+    torch.manual_seed(0)
+    cases = [
+        ("conv", (4, 16, 16, 64), (128, 4, 4, 64), 2, 1),
+        ("convT", (4, 8, 8, 128), (128, 4, 4, 64), 2, 1),
+        ("convT", (3, 16, 16, 64), (64, 4, 4, 32), 2, 1),
+        ("conv", (2, 32, 32, 32), (64, 4, 4, 32), 2, 1),
+    ]
+    for kind, xs, ws, s, p in cases:
+        x = torch.randn(xs)
+        w = torch.randn(ws) * 0.05
+        xc = x.clone().to(cuda).requires_grad_(True); xh = x.clone().requires_grad_(True)
+        wc = w.clone().to(cuda).requires_grad_(True); wh = w.clone().requires_grad_(True)
+        f = A.conv2d if kind == "conv" else A.conv_transpose2d
+        yc, yh = f(xc, wc, s, p), f(xh, wh, s, p)
+        assert yc.shape == yh.shape
+        assert _rel(yc, yh) < 1e-2, kind
+        g = torch.randn_like(yh)
+        yc.backward(g.to(cuda)); yh.backward(g)
+        assert _rel(xc.grad, xh.grad) < 2e-2 and _rel(wc.grad, wh.grad) < 2e-2, kind
+    # BN + act (batch statistics), tanh / sigmoid / leaky, BCE
+    for act in ("relu", "leaky_relu", "none"):
+        x = torch.randn(4, 8, 8, 96) * 2 + 0.5
+        ga, be = torch.rand(96) + 0.5, torch.randn(96) * 0.1
+        xc = x.clone().to(cuda).requires_grad_(True); xh = x.clone().requires_grad_(True)
+        gc = ga.clone().to(cuda).requires_grad_(True); gh = ga.clone().requires_grad_(True)
+        bc = be.clone().to(cuda).requires_grad_(True); bh = be.clone().requires_grad_(True)
+        rmc, rvc = torch.zeros(96, device=cuda), torch.ones(96, device=cuda)
+        rmh, rvh = torch.zeros(96), torch.ones(96)
+        yc = A.batch_norm_act(xc, gc, bc, rmc, rvc, True, act=act)
+        yh = A.batch_norm_act(xh, gh, bh, rmh, rvh, True, act=act)
+        assert _rel(yc, yh) < 1e-2, act
+        assert _rel(rmc, rmh) < 1e-3 and _rel(rvc, rvh) < 1e-3
+        g = torch.randn_like(yh)
+        yc.backward(g.to(cuda)); yh.backward(g)
+        for a_, b_ in ((xc, xh), (gc, gh), (bc, bh)):
+            assert _rel(a_.grad, b_.grad) < 3e-2, act
+    for kind in ("tanh", "sigmoid", "leaky_relu"):
+        x = torch.randn(2, 4, 4, 32) * 2
+        xc = x.clone().to(cuda).requires_grad_(True); xh = x.clone().requires_grad_(True)
+        yc, yh = A.activation(xc, kind), A.activation(xh, kind)
+        assert _rel(yc, yh) < 1e-2
+        yc.sum().backward(); yh.sum().backward()
+        assert _rel(xc.grad, xh.grad) < 2e-2, kind
+    l = torch.randn(64, 32) * 3
+    lc = l.clone().to(cuda).requires_grad_(True); lh = l.clone().requires_grad_(True)
+    for t in (1.0, 0.0):
+        a, b = A.bce_with_logits(lc, t), A.bce_with_logits(lh, t)
+        assert abs(a.item() - b.item()) < 1e-2 * max(1.0, abs(b.item()))
+        a.backward(); b.backward()
+    assert _rel(lc.grad, lh.grad) < 2e-2
+
+
+@pytest.mark.gpu
+def test_dcgan_gpu_matches_fp32_and_trains(cuda):
+    torch.manual_seed(0)
+    Gh, Dh = Generator(), Discriminator()
+    Gc, Dc = Generator().to(cuda), Discriminator().to(cuda)
+    Gc.load_state_dict(Gh.state_dict()); Dc.load_state_dict(Dh.state_dict())
+    z = torch.randn(16, 100)
+    ih, ic = Gh(z), Gc(z.to(cuda))
+    assert _rel(ic, ih) < 3e-2
+    oh, oc = Dh(ih), Dc(ic)
+    assert _rel(oc[:, 0], oh[:, 0]) < 5e-2
+    tr = GANTrainer(Gc, Dc)
+    real = to_nhwc_padded(torch.rand(32, 3, 32, 32) * 2 - 1).to(cuda)
+    for _ in range(3):
+        ld, lg = tr.step(real)
+    assert torch.isfinite(ld) and torch.isfinite(lg)
+    assert Gc.up3[..., 3:].abs().max().item() == 0 and Dc.c0[..., 3:].abs().max().item() == 0
+
+
+def test_federated_gan_cpu_and_fedavg_identity():
+    from ddl25spring_amd.fl.gan import FederatedGAN
+    torch.manual_seed(0)
+    data = [to_nhwc_padded(torch.rand(40, 3, 32, 32) * 2 - 1) for _ in range(3)]
+    fg = FederatedGAN(data, ngf=32, ndf=32, local_steps=2, batch_size=8, seed=1, device="cpu")
+    res = fg.run(2)
+    assert res.rounds == 2 and res.samples == 2 * 3 * 2 * 8
+    assert all(np.isfinite(res.loss_d)) and all(np.isfinite(res.loss_g))
+    # one client, one local step: FedAvg of a single client == that client's local model
+    fg1 = FederatedGAN(data[:1], ngf=32, ndf=32, local_steps=1, batch_size=8, seed=2, device="cpu")
+    before = fg1._flat().clone()
+    fg1.run(1)
+    assert not torch.equal(before, fg1._flat())
+

@@ -94,10 +94,9 @@ def test_conv_tile_configs(cuda):
     dx_ref = ref.conv_dgrad(dy.cpu(), w.cpu(), geom)
     dw_ref = torch.zeros(geom.G, geom.K, geom.R, geom.S, geom.C)
     ref.conv_wgrad(dy.cpu(), x.cpu(), geom, dw_ref)
-    cfgs = [(64, 64, 32, 4), (64, 128, 32, 4), (128, 64, 32, 4), (128, 128, 32, 4), (128, 128, 32, 3),
-            (64, 128, 64, 3), (128, 128, 64, 3), (128, 128, 64, 2), (64, 64, 64, 3), (128, 64, 64, 3)]
+    cfgs = Fn.CONV_TILES
     for bp, bq, bk, ns in cfgs:
-        cfg = bp | (bq << 8) | (bk << 16) | (ns << 24)
+        cfg = Fn.conv_cfg(bp, bq, bk, ns)
         _close(Fn.conv_fwd(x, w, geom, cfg=cfg), y_ref)
         _close(Fn.conv_dgrad(dy, w, geom, cfg=cfg), dx_ref)
         for splits in (1, 3):
