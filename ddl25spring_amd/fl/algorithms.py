@@ -20,6 +20,7 @@ import torch
 
 from ..ops import functional as Fn
 from ..runtime import dist as rdist
+from ..utils.metrics import PhaseTimer
 from .aggregate import MeanAggregator, make_aggregator
 from .local import LocalTrainer
 from .result import RunResult
@@ -38,7 +39,7 @@ class FederatedBase:
                  aggregator="mean", attack=None, ctx=None, momentum: float = 0.0,
                  weight_decay: float = 0.0, planner: str = "native", use_graph=None,
                  init_fn=None, eval_every: int = 1, eval_limit: int | None = None, name=None,
-                 agg_kwargs=None):
+                 agg_kwargs=None, dropout: float = 0.0):
         self.ctx = ctx or rdist.context()
         self.dev = self.ctx.device
         self.data = train_data
@@ -70,6 +71,47 @@ class FederatedBase:
         self.eval_every, self.eval_limit = eval_every, eval_limit
         self.name = name or self.algorithm
         self.round_idx = 0
+        # [NS] client unavailability: each sampled client independently fails to report with
+        # probability ``dropout`` (own RNG stream, so the client-sampling sequence is unchanged)
+        self.dropout = dropout
+        self.fail_rng = np.random.default_rng([seed, 0xD20])
+        self.dropped: list[list[int]] = []
+        self.timer = PhaseTimer(self.dev)  # download / local_train / aggregate (HIP events + roctx)
+
+    def _sample(self):
+        chosen = self.rng.choice(self.N, self.K, replace=False)
+        if self.dropout > 0:
+            alive = self.fail_rng.random(len(chosen)) >= self.dropout
+            self.dropped.append([int(c) for c in chosen[~alive]])
+            chosen = chosen[alive]
+        return chosen
+
+    # ------------------------------------------------------------------ checkpoint / resume
+    def state_dict(self) -> dict:
+        """Everything needed to continue bit-identically: server model, round counter, RNG streams
+        (loader seeds derive from seed/round/client, so they need no state)."""
+        sd = {"w_global": self.w_global.detach().cpu().clone(),
+              "b_global": self.b_global.detach().cpu().clone(),
+              "round_idx": self.round_idx, "rng": self.rng.bit_generator.state,
+              "fail_rng": self.fail_rng.bit_generator.state, "dropped": self.dropped,
+              "algorithm": self.algorithm, "N": self.N, "K": self.K, "seed": self.seed}
+        for name in ("g_global",):
+            if hasattr(self, name):
+                sd[name] = getattr(self, name).detach().cpu().clone()
+        return sd
+
+    def load_state_dict(self, sd: dict) -> None:
+        if (sd["algorithm"], sd["N"], sd["K"]) != (self.algorithm, self.N, self.K):
+            raise ValueError("checkpoint is for a different federation "
+                             f"{(sd['algorithm'], sd['N'], sd['K'])}")
+        self.w_global.copy_(sd["w_global"].to(self.dev))
+        self.b_global.copy_(sd["b_global"].to(self.dev))
+        if "g_global" in sd and hasattr(self, "g_global"):
+            self.g_global.copy_(sd["g_global"].to(self.dev))
+        self.round_idx = int(sd["round_idx"])
+        self.rng.bit_generator.state = sd["rng"]
+        self.fail_rng.bit_generator.state = sd["fail_rng"]
+        self.dropped = [list(d) for d in sd["dropped"]]
 
     # ------------------------------------------------------------------ helpers
     def _assign(self, chosen):
@@ -119,6 +161,7 @@ class FederatedBase:
             res.round_time.append(dt)
             res.samples.append(samples)
             res.message_count.append(2 * self.round_idx * self.K)
+            res.phase_ms.append(self.timer.summary())
             if self.eval_every and self.round_idx % self.eval_every == 0:
                 res.test_accuracy.append(self.test())
             else:
@@ -148,12 +191,16 @@ class FedAvg(FederatedBase):
     def round(self):
         _sync(self.dev)
         t0 = time.perf_counter()
-        chosen = self.rng.choice(self.N, self.K, replace=False)
+        chosen = self._sample()
+        if len(chosen) == 0:  # every sampled client dropped out: the server model stays
+            self.round_idx += 1
+            return self.ctx.max_scalar(time.perf_counter() - t0), 0
         mine, counts = self._assign(chosen)
         G = len(mine)
         total = float(sum(self.counts[int(c)] for c in chosen))
         r = self.round_idx
-        self._download(G)
+        with self.timer("download"):
+            self._download(G)
         seeds = [self.seed + c + 1 + r * self.K for c in mine]
         gens = [torch.Generator().manual_seed(s) for s in seeds] if self.planner == "torch" else None
         trainer = self._trainer(mine)
@@ -164,14 +211,16 @@ class FedAvg(FederatedBase):
             if len(train_slots) == G:
                 if bsz <= 0:  # B = infinity: full local batch
                     trainer.B = max(self.counts[c] for c in mine)
-                samples = trainer.run([self.client_indices[c] for c in mine], seeds, self.E, gens)
+                with self.timer("local_train"):
+                    samples = trainer.run([self.client_indices[c] for c in mine], seeds, self.E, gens)
         st = self.net.store
         if self.attack is not None and G:
             self.attack.poison_updates(st.data[:G], self.w_global, mine)
         coeffs = torch.tensor([self.counts[c] / total for c in mine], dtype=torch.float32,
                               device=self.dev)
-        self._aggregate(st.data[:G], coeffs, counts)
-        self._mean_buffers(G, coeffs)
+        with self.timer("aggregate"):
+            self._aggregate(st.data[:G], coeffs, counts)
+            self._mean_buffers(G, coeffs)
         _sync(self.dev)
         dt = self.ctx.max_scalar(time.perf_counter() - t0)
         self.round_idx += 1
@@ -201,7 +250,10 @@ class FedSGD(FederatedBase):
     def round(self):
         _sync(self.dev)
         t0 = time.perf_counter()
-        chosen = self.rng.choice(self.N, self.K, replace=False)
+        chosen = self._sample()
+        if len(chosen) == 0:
+            self.round_idx += 1
+            return self.ctx.max_scalar(time.perf_counter() - t0), 0
         mine, counts = self._assign(chosen)
         G = len(mine)
         total = float(sum(self.counts[int(c)] for c in chosen))

@@ -23,11 +23,13 @@ class RunResult:
     # extensions (not in the reference's table; excluded from as_df unless asked)
     round_time: list[float] = field(default_factory=list, repr=False)
     samples: list[int] = field(default_factory=list, repr=False)
+    phase_ms: list[dict] = field(default_factory=list, repr=False)  # per-round device phase times
 
     def as_df(self, skip_wtime: bool = True, with_throughput: bool = False):
         from pandas import DataFrame
         d = asdict(self)
         extra = {"round_time": d.pop("round_time"), "samples": d.pop("samples")}
+        d.pop("phase_ms")
         cols = {k.capitalize().replace("_", " "): v for k, v in d.items()}
         if cols["B"] == -1:
             cols["B"] = "\N{INFINITY}"

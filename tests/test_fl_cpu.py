@@ -159,3 +159,40 @@ def test_distributed_fedavg_matches_single_process(fp32, agg):
         w1 = torch.load(os.path.join(d, "w1.pt"), weights_only=True)
     assert torch.equal(w0, w1)  # replicated server state stays identical on every rank
     assert torch.allclose(w0, single.w_global, atol=1e-5), (w0 - single.w_global).abs().max()
+
+
+@pytest.mark.parametrize("algo", [FedAvg, FedSGD])
+def test_checkpoint_resume_is_identical(fp32, algo):
+    from ddl25spring_amd.fl import checkpoint as ckpt
+    arr, data = _data(400)
+    parts = split(6, True, 10, labels=arr.labels)
+    kw = dict(lr=0.05, batch_size=50, client_fraction=0.5, seed=4, dropout=0.2)
+    ref = algo(mnist_mlp, data, parts, **kw)
+    ref.run(4)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "fl.pt")
+        a = algo(mnist_mlp, data, parts, **kw)
+        res = ckpt.run_with_checkpoints(a, 2, path)
+        assert len(res.message_count) == 2
+        b = algo(mnist_mlp, data, parts, **kw)  # fresh process-equivalent: rebuild, then resume
+        res = ckpt.run_with_checkpoints(b, 4, path)
+        assert res.message_count == [6, 12, 18, 24] and b.round_idx == 4
+    assert torch.equal(b.w_global, ref.w_global)
+    assert b.dropped == ref.dropped
+
+
+def test_client_dropout_keeps_sampling_stream(fp32):
+    arr, data = _data(400)
+    parts = split(8, True, 10, labels=arr.labels)
+    kw = dict(lr=0.05, batch_size=50, client_fraction=0.5, seed=5)
+    full = FedAvg(mnist_mlp, data, parts, **kw)
+    drop = FedAvg(mnist_mlp, data, parts, dropout=0.5, **kw)
+    for _ in range(3):
+        full.round()
+        drop.round()
+    assert full.rng.bit_generator.state == drop.rng.bit_generator.state
+    assert sum(len(d) for d in drop.dropped) > 0
+    total = FedAvg(mnist_mlp, data, parts, dropout=1.0, **kw)
+    w0 = total.w_global.clone()
+    dt, samples = total.round()
+    assert samples == 0 and torch.equal(total.w_global, w0)
