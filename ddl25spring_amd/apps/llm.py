@@ -1,0 +1,124 @@
+"""LLaMA training over a DP x PP grid — the tutorial_1b scripts as one configurable program.
+
+Covers, with one code path (reference lab/tutorial_1b):
+  * intro.py                      dp=1 pp=1
+  * DP/gradient_aggr/intro_DP_GA  dp=W, dp_mode="ga"  (bucketed all-reduce overlapped with backward)
+  * DP/weight_aggr/intro_DP_WA    dp=W, dp_mode="wa"  (averaged weights written back — fixes Q1)
+  * PP/1F1B/intro_PP_1F1B(_MB)    pp=W, schedule naive | gpipe | 1f1b, micro-batches
+  * PP/1F1B/intro_PP_1F1B_MP      dp x pp grid (collective group creation; verified schedule)
+Rank layout: rank = pipe * pp + stage. Every rank of a pipeline reads the same token stream
+(``skip = pipe * 3000`` as the reference), so the last stage has its targets without extra
+messages; stage weights start identical across pipelines (seeded init + broadcast).
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import asdict, dataclass
+
+import torch
+
+from ..data.text import SPTokenizer, TinyStories
+from ..models.llama import LLama, causalLLMLoss, split_stages
+from ..parallel.dp import GradBucketer, average_weights, broadcast_parameters
+from ..parallel.pipeline import PipelineStage, grid_ranks
+
+
+@dataclass
+class LLMConfig:
+    vocab_size: int = 32000
+    dmodel: int = 288
+    num_heads: int = 6
+    n_layers: int = 6
+    ctx_size: int = 256
+    batch_size: int = 3
+    micro_batches: int = 1
+    dp: int = 1
+    pp: int = 1
+    schedule: str = "1f1b"
+    dp_mode: str = "ga"
+    iters: int = 100
+    lr: float = 8e-4
+    seed: int = 0
+    bucket_mb: float = 25.0
+    log_every: int = 10
+    fused_adam: bool = True
+
+
+def train_llm(cfg: LLMConfig, ctx, log=print, warmup: int = 0) -> dict:
+    """Runs ``warmup`` untimed + ``cfg.iters`` timed iterations; returns losses and throughput."""
+    if ctx.world != cfg.dp * cfg.pp:
+        raise ValueError(f"world {ctx.world} != dp {cfg.dp} x pp {cfg.pp}")
+    dev = ctx.device
+    pipe, stage, pipe_ranks, _ = grid_ranks(ctx.rank, cfg.dp, cfg.pp)
+    dp_group = ctx.new_groups("dp", [[p * cfg.pp + s for p in range(cfg.dp)] for s in range(cfg.pp)])
+    torch.manual_seed(cfg.seed)
+    full = LLama(vocab_size=cfg.vocab_size, dmodel=cfg.dmodel, num_heads=cfg.num_heads,
+                 n_layers=cfg.n_layers, ctx_size=cfg.ctx_size)
+    mod = split_stages(full, cfg.pp)[stage].to(dev)
+    if cfg.dp > 1:
+        broadcast_parameters(mod, ctx, src=stage, group=dp_group)  # pipeline 0's stage s is rank s
+    if dev.type == "cuda" and cfg.fused_adam:
+        from ..optim import FlatAdam
+        opt = FlatAdam(mod.parameters(), lr=cfg.lr)
+    else:
+        opt = torch.optim.Adam(mod.parameters(), lr=cfg.lr)
+    sync = GradBucketer(mod, ctx, group=dp_group, bucket_mb=cfg.bucket_mb) \
+        if cfg.dp > 1 and cfg.dp_mode == "ga" else None
+    if cfg.batch_size % cfg.micro_batches:
+        raise ValueError("batch_size must be divisible by micro_batches")
+    mb = cfg.batch_size // cfg.micro_batches
+    act_dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
+    ps = PipelineStage(mod, stage, cfg.pp, ranks=pipe_ranks, act_shape=(mb, cfg.ctx_size, cfg.dmodel),
+                       act_dtype=act_dtype, device=dev) if cfg.pp > 1 else None
+    stream = iter(TinyStories(SPTokenizer(cfg.vocab_size), cfg.batch_size, cfg.ctx_size,
+                              skip=pipe * 3000, seed=1234 + cfg.seed))
+    losses = []
+
+    def step():
+        x = next(stream).to(dev, non_blocking=True)
+        if sync is not None:
+            sync.zero_grad()
+        else:
+            opt.zero_grad()
+        if ps is None:
+            loss = None
+            mbs = torch.chunk(x, cfg.micro_batches)
+            for i, m in enumerate(mbs):
+                l = causalLLMLoss(mod(m), m) / cfg.micro_batches
+                if sync is not None and i < len(mbs) - 1:
+                    with sync.no_sync():
+                        l.backward()
+                else:
+                    l.backward()
+                loss = l.detach() if loss is None else loss + l.detach()
+        else:
+            mbs = list(torch.chunk(x, cfg.micro_batches))
+            loss = ps.run(cfg.schedule, cfg.micro_batches, inputs=mbs, targets=mbs,
+                          loss_fn=causalLLMLoss, grad_sync=sync)
+        if sync is not None:
+            sync.finish()
+        opt.step()
+        if cfg.dp > 1 and cfg.dp_mode == "wa":
+            average_weights(mod, ctx, group=dp_group)
+        return loss
+
+    for _ in range(warmup):
+        step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for it in range(cfg.iters):
+        loss = step()
+        if loss is not None and (it % cfg.log_every == 0 or it == cfg.iters - 1):
+            lv = float(loss)
+            losses.append((it, lv))
+            if log:
+                log(f"[pipe {pipe} stage {stage}] iter {it} loss {lv:.4f}")
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    ctx.barrier()
+    dt = ctx.max_scalar(time.perf_counter() - t0)
+    tokens = cfg.dp * cfg.batch_size * cfg.ctx_size * cfg.iters
+    return {"losses": losses, "seconds": dt, "tokens_per_s": tokens / dt,
+            "ms_per_iter": 1e3 * dt / max(1, cfg.iters), "config": asdict(cfg)}
