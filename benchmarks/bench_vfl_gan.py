@@ -1,0 +1,90 @@
+"""BASELINE config #5: vertical-FL split-NN (2-party feature split) + federated DCGAN.
+
+split-NN: heart-disease table (real CSV if present, else synthetic of the same schema), 2 parties
+with the D6 balanced feature split, batch 64, AdamW. world 2: rank 0 = active party (labels +
+feature block 0), rank 1 = passive party (block 1), cut-layer tensors over RCCL P2P; world 1: both
+parties in one process. Metric: samples/s of split-NN training.
+DCGAN: CIFAR-10-shaped 32x32x3, 2 clients (one per rank at world 2), FedAvg of G and D every
+``--local-steps`` Adam steps. Metric: GAN images/s (real + fake images through D per step).
+"""
+from __future__ import annotations
+
+import argparse
+
+import numpy as np
+import torch
+
+from _common import emit, timed
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=3, help="timed units (split-NN epochs / GAN rounds)")
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--local-steps", type=int, default=20)
+    ap.add_argument("--gan-batch", type=int, default=128)
+    ap.add_argument("--vfl-batch", type=int, default=64)
+    args = ap.parse_args()
+    from ddl25spring_amd.apps.gan import GANConfig, client_images
+    from ddl25spring_amd.data import heart as H
+    from ddl25spring_amd.fl.gan import FederatedGAN
+    from ddl25spring_amd.models import tabular as T
+    from ddl25spring_amd.runtime import dist as rdist
+    from ddl25spring_amd.vfl import SplitNNParty, SplitNNServer
+    ctx = rdist.init()
+    dev = ctx.device
+    # ---------------- split-NN
+    df, real = H.load_heart()
+    X, Y = H.vfl_frame(df)
+    parts = H.partition_balanced(list(X.columns), 2)
+    Xtr, _ = H.row_split(X)
+    Ytr, _ = H.row_split(Y)
+    xs = [torch.tensor(Xtr[p].values.astype(np.float32), device=dev) for p in parts]
+    y = torch.tensor(Ytr.values.astype(np.float32), device=dev)
+    torch.manual_seed(0)
+    bottoms = [T.BottomModel(len(p), 2 * len(p)).to(dev) for p in parts]
+    top = T.TopModel(bottoms, 2).to(dev)
+    if ctx.world == 1:
+        net = T.VFLNetwork(bottoms, 2).to(dev)
+        net.top_model = top
+        net.optimizer = torch.optim.AdamW(net.parameters())
+        crit = torch.nn.CrossEntropyLoss()
+
+        def epoch():
+            for b in range(0, len(y), args.vfl_batch):
+                net.optimizer.zero_grad()
+                crit(net([x[b:b + args.vfl_batch] for x in xs]), y[b:b + args.vfl_batch]).backward()
+                net.optimizer.step()
+    elif ctx.rank == 0:
+        srv = SplitNNServer(top, [1], [2 * len(parts[1])], local_bottom=bottoms[0])
+
+        def epoch():
+            srv.fit(y, 1, args.vfl_batch, x_local=xs[0])
+    else:
+        pty = SplitNNParty(bottoms[1], 2 * len(parts[1]))
+
+        def epoch():
+            pty.fit(xs[1], 1, args.vfl_batch)
+    dt_v = timed(ctx, epoch, args.steps, args.warmup)
+    vfl_sps = len(y) * args.steps / dt_v
+    # ---------------- federated DCGAN (2 clients)
+    gcfg = GANConfig(clients=2, local_steps=args.local_steps, batch_size=args.gan_batch,
+                     train_size=10000)
+    data = client_images(gcfg, dev)
+    fg = FederatedGAN(data, ctx=ctx if ctx.world > 1 else None, local_steps=args.local_steps,
+                      batch_size=args.gan_batch, device=dev)
+    dt_g = timed(ctx, lambda: fg.run(1), args.steps, args.warmup)
+    imgs = 2 * 2 * args.local_steps * args.gan_batch * args.steps  # 2 clients x (real + fake)
+    emit(ctx, metric="VFL split-NN samples/s + federated DCGAN images/s", value=round(vfl_sps, 1),
+         unit="samples/s", n_gpus=ctx.world, steps=args.steps, warmup=args.warmup,
+         ms_per_step=round(1e3 * dt_v / args.steps, 3), higher_is_better=True, scaling="strong",
+         vs_baseline=None, dtype="fp32 (split-NN) / bf16 (DCGAN)",
+         data="heart.csv" if real else "synthetic",
+         gan_images_per_s=round(imgs / dt_g, 1), gan_ms_per_round=round(1e3 * dt_g / args.steps, 3),
+         config={"model": "splitnn-heart-2party + dcgan-cifar32", "global_batch": args.vfl_batch,
+                 "seq_len": None, "parallelism": f"vfl2party-fedgan2-w{ctx.world}"})
+    rdist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

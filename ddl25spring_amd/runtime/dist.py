@@ -116,6 +116,10 @@ def init(backend: str | None = None, device: str | None = None, rank: int | None
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
+        if world > 1 and "OMP_NUM_THREADS" not in os.environ:
+            # ranks sharing a host must split its cores, or their intra-op pools oversubscribe it
+            local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+            torch.set_num_threads(max(1, (os.cpu_count() or 1) // local_world))
     backend = backend or ("nccl" if dev.type == "cuda" else "gloo")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

@@ -65,12 +65,16 @@ class SplitNNParty:
 
 
 class SplitNNServer:
-    """The label holder: top model over the concatenated party activations."""
+    """The label holder: top model over the concatenated party activations. With ``local_bottom``
+    it is also the *active party* (holds a feature block itself, activation first in the concat),
+    so a 2-party split fits on 2 GPUs."""
 
     def __init__(self, top: nn.Module, parties: list[int], out_dims: list[int], optimizer=None,
-                 criterion=None, group=None):
+                 criterion=None, group=None, local_bottom: nn.Module | None = None):
         self.top, self.parties, self.out_dims, self.group = top, parties, out_dims, group
-        self.opt = optimizer or torch.optim.AdamW(top.parameters())
+        self.local = local_bottom
+        params = list(top.parameters()) + (list(local_bottom.parameters()) if local_bottom else [])
+        self.opt = optimizer or torch.optim.AdamW(params)
         self.criterion = criterion or nn.CrossEntropyLoss()
 
     def _recv(self, b, like):
@@ -78,11 +82,15 @@ class SplitNNServer:
         _exchange([], list(zip(acts, self.parties)), self.group)
         return acts
 
-    def train_step(self, y):
+    def train_step(self, y, x_local=None):
         self.opt.zero_grad()
         self.top.train()
         acts = [a.requires_grad_(True) for a in self._recv(len(y), y)]
-        out = self.top(acts)
+        if self.local is not None:
+            self.local.train()
+            out = self.top([self.local(x_local)] + acts)
+        else:
+            out = self.top(acts)
         loss = self.criterion(out, y)
         loss.backward()
         self.opt.step()
@@ -93,16 +101,20 @@ class SplitNNServer:
         return loss.item(), correct
 
     @torch.no_grad()
-    def infer(self, n, like, eval_mode: bool = True):
+    def infer(self, n, like, eval_mode: bool = True, x_local=None):
         self.top.train(not eval_mode)
-        return self.top(self._recv(n, like))
+        acts = self._recv(n, like)
+        if self.local is not None:
+            self.local.train(not eval_mode)
+            acts = [self.local(x_local)] + acts
+        return self.top(acts)
 
-    def fit(self, y, epochs, batch_size, log=None):
+    def fit(self, y, epochs, batch_size, log=None, x_local=None):
         hist = []
         for e in range(epochs):
             tot, cor, bl = 0.0, 0, _batches(len(y), batch_size)
             for sl in bl:
-                l, c = self.train_step(y[sl])
+                l, c = self.train_step(y[sl], None if x_local is None else x_local[sl])
                 tot, cor = tot + l, cor + c
             hist.append((tot / len(bl), cor / len(y)))
             if log:

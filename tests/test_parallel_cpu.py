@@ -198,3 +198,58 @@ def test_dp_x_pp_grid_runs_and_replicas_agree():
         for a, b in zip(res[s]["w"], res[2 + s]["w"]):
             assert torch.allclose(a, b, atol=1e-6)
     assert len(res[1]["losses"]) == 3 and len(res[3]["losses"]) == 3
+
+
+def _native_dp_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    import ddl25spring_amd.ops.reference as R
+    from ddl25spring_amd.models import mnist_mlp
+    from ddl25spring_amd.models import params as P
+    from ddl25spring_amd.optim import SGD
+    from ddl25spring_amd.parallel.dp import NativeGradBucketer
+    from ddl25spring_amd.runtime import dist as rdist
+    R._bf = lambda t: t.float()
+    P.CPU_SHADOW_DTYPE = torch.float32
+    ctx = rdist.init(backend="gloo", device="cpu")
+    net = mnist_mlp().to("cpu", seed=rank)  # different init on purpose: the broadcast fixes it
+    ctx.broadcast(net.store.data, 0)
+    net.store.sync_shadow()
+    bk = NativeGradBucketer(net, ctx, bucket_mb=0.05)  # several buckets
+    assert len(bk.bounds) > 1
+    net.grad_hook = bk.on_layer_done
+    opt = SGD(net, lr=0.1)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(1, 8, 800, generator=g)
+    y = torch.randint(0, 10, (1, 8), generator=g, dtype=torch.int32)
+    for _ in range(2):
+        opt.zero_grad()
+        net.train_step(x[:, rank * 4:(rank + 1) * 4], y[:, rank * 4:(rank + 1) * 4])
+        bk.finish()
+        opt.step()
+    torch.save(net.store.data.clone(), os.path.join(out_dir, f"r{rank}.pt"))
+    rdist.shutdown()
+
+
+def test_native_dp_bucketer_equals_large_batch(monkeypatch):
+    import ddl25spring_amd.ops.reference as R
+    from ddl25spring_amd.models import mnist_mlp
+    from ddl25spring_amd.models import params as P
+    from ddl25spring_amd.optim import SGD
+    monkeypatch.setattr(R, "_bf", lambda t: t.float())
+    monkeypatch.setattr(P, "CPU_SHADOW_DTYPE", torch.float32)
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_native_dp_worker, args=(2, 29955, d), nprocs=2, join=True)
+        w0 = torch.load(os.path.join(d, "r0.pt"), weights_only=True)
+        w1 = torch.load(os.path.join(d, "r1.pt"), weights_only=True)
+    net = mnist_mlp().to("cpu", seed=0)
+    opt = SGD(net, lr=0.1)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(1, 8, 800, generator=g)
+    y = torch.randint(0, 10, (1, 8), generator=g, dtype=torch.int32)
+    for _ in range(2):
+        opt.zero_grad()
+        net.train_step(x, y)
+        opt.step()
+    assert torch.equal(w0, w1)
+    assert torch.allclose(w0, net.store.data, atol=1e-5)

@@ -221,3 +221,36 @@ def test_distributed_vfl_matches_single_process():
         want = list(encs[r - 1].parameters()) + list(decs[r - 1].parameters())
         for g, w in zip(res[r]["vae"], want):
             assert torch.allclose(g, w, atol=1e-5)
+
+
+def _active_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ddl25spring_amd.vfl import SplitNNParty, SplitNNServer
+    bottoms, top, xs, y = _splitnn_models()
+    if rank == 0:  # active party: labels + feature block 0
+        SplitNNServer(top, [1], [2 * DIMS[1]], local_bottom=bottoms[0]).fit(y, EPOCHS, BS, x_local=xs[0])
+        res = [p.detach() for p in list(top.parameters()) + list(bottoms[0].parameters())]
+    else:
+        SplitNNParty(bottoms[1], 2 * DIMS[1]).fit(xs[1], EPOCHS, BS)
+        res = [p.detach() for p in bottoms[1].parameters()]
+    torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_two_party_active_passive_matches_single_process():
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_active_worker, args=(2, 29879, d), nprocs=2, join=True)
+        r0 = torch.load(os.path.join(d, "r0.pt"), weights_only=True)
+        r1 = torch.load(os.path.join(d, "r1.pt"), weights_only=True)
+    bottoms, top, xs, y = _splitnn_models()
+    opt = torch.optim.AdamW([p for m in bottoms + [top] for p in m.parameters()])
+    crit = torch.nn.CrossEntropyLoss()
+    for _ in range(EPOCHS):
+        for b in range(0, N, BS):
+            opt.zero_grad()
+            crit(top([m(x[b:b + BS]) for m, x in zip(bottoms, xs)]), y[b:b + BS]).backward()
+            opt.step()
+    want0 = list(top.parameters()) + list(bottoms[0].parameters())
+    assert all(torch.allclose(g, w, atol=1e-5) for g, w in zip(r0, want0))
+    assert all(torch.allclose(g, w, atol=1e-5) for g, w in zip(r1, bottoms[1].parameters()))
