@@ -13,6 +13,7 @@ checks, rank numbering bugs such as run.bat starting at 1 — SURVEY Q17) with:
 * exit status = the first failure's code (0 if all succeeded).
 
 usage: python -m ddl25spring_amd.runtime.launch -n 4 [--log-dir D] [--timeout S] script.py args...
+       python -m ddl25spring_amd.runtime.launch -n 4 -m ddl25spring_amd llm --dp 2 --pp 2
 """
 from __future__ import annotations
 
@@ -105,10 +106,11 @@ def main(argv=None) -> int:
     ap.add_argument("--timeout", type=float, default=None)
     ap.add_argument("--rank-arg", action="store_true", help="append the rank as the last argv")
     ap.add_argument("--port", type=int, default=None)
+    ap.add_argument("-m", "--module", action="store_true", help="run the target as a module (python -m)")
     ap.add_argument("script")
     ap.add_argument("args", nargs=argparse.REMAINDER)
     a = ap.parse_args(argv)
-    cmd = [sys.executable, "-u", a.script] + a.args
+    cmd = [sys.executable, "-u"] + (["-m"] if a.module else []) + [a.script] + a.args
     res = launch(cmd, a.nproc, a.log_dir, a.timeout, a.rank_arg, a.port)
     if res["failed_rank"] is not None:
         who = "timeout" if res["failed_rank"] == -1 else f"rank {res['failed_rank']}"
