@@ -46,10 +46,22 @@ __global__ void bn_finalize_kernel(BNArgs a) {
     const int ns = a.stripes > 1 ? a.stripes : 1;
     const float* st = a.stats + (long long)g * ns * 2 * a.C;
     double s1 = 0.0, s2 = 0.0;
-    for (int k = 0; k < ns; ++k) {
-      s1 += st[(long long)k * 2 * a.C + c];
-      s2 += st[(long long)k * 2 * a.C + a.C + c];
+    // independent partial sums so the stripe loads issue back to back (latency, not bandwidth)
+    double p1[4] = {0.0, 0.0, 0.0, 0.0}, p2[4] = {0.0, 0.0, 0.0, 0.0};
+    int k = 0;
+    for (; k + 4 <= ns; k += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        p1[u] += st[(long long)(k + u) * 2 * a.C + c];
+        p2[u] += st[(long long)(k + u) * 2 * a.C + a.C + c];
+      }
     }
+    for (; k < ns; ++k) {
+      p1[0] += st[(long long)k * 2 * a.C + c];
+      p2[0] += st[(long long)k * 2 * a.C + a.C + c];
+    }
+    s1 = (p1[0] + p1[1]) + (p1[2] + p1[3]);
+    s2 = (p2[0] + p2[1]) + (p2[2] + p2[3]);
     const double M = (double)a.count;
     const double m = s1 / M;
     double v = s2 / M - m * m;
@@ -374,5 +386,58 @@ DDL_API int ddl_bn_stats(const void* x, float* stats, long long M, int C, int G,
   const int RPI = 256 / (C / 8);
   hipLaunchKernelGGL(bn_stats_kernel, dim3(stream_blocks(M, RPI, G, 16), G), dim3(256), 0, s,
                      (const bf16_t*)x, stats, M, C);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Whole BN backward in three launches: striped reduce -> per-channel fold (d(beta) += s0,
+// d(gamma) += s1, dx coefficients) -> one apply pass.
+__global__ void bn_fold_coef_kernel(const float* __restrict__ part, float* __restrict__ dgamma,
+                                    float* __restrict__ dbeta, long long gs_param,
+                                    const float* __restrict__ mean, const float* __restrict__ rstd,
+                                    const float* __restrict__ gamma, float* __restrict__ coef,
+                                    long long M, int C, int G) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= G * C) return;
+  const int g = i / C, c = i - g * C;
+  const float* pg = part + (long long)g * BN_NSTRIPE * 2 * C;
+  float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < BN_NSTRIPE; k += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a0[u] += pg[(long long)(k + u) * 2 * C + c];
+      a1[u] += pg[(long long)(k + u) * 2 * C + C + c];
+    }
+  }
+  const float s0 = (a0[0] + a0[1]) + (a0[2] + a0[3]), s1 = (a1[0] + a1[1]) + (a1[2] + a1[3]);
+  const long long po = (long long)g * gs_param + c;
+  if (dbeta) dbeta[po] += s0;
+  if (dgamma) dgamma[po] += s1;
+  const float invM = 1.f / (float)M;
+  const float mu = mean[i], rs = rstd[i];
+  const float ga = gamma ? gamma[po] : 1.f;
+  const float A = ga * rs;
+  const float B = -A * rs * s1 * invM;
+  coef[(long long)g * 3 * C + c] = A;
+  coef[(long long)g * 3 * C + C + c] = B;
+  coef[(long long)g * 3 * C + 2 * C + c] = -A * s0 * invM - B * mu;
+}
+
+// part: zeroed [G][BN_NSTRIPE][2C]; coef: [G][3C] scratch
+DDL_API int ddl_bn_backward(const void* dy, const void* ymask, const void* x, const float* mean,
+                            const float* rstd, const float* gamma, long long gs_param, float* part,
+                            float* coef, float* dgamma, float* dbeta, void* dx, void* dym_out,
+                            long long M, int C, int G, hipStream_t s) {
+  if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
+  const int RPI = 256 / (C / 8);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(stream_blocks(M, RPI, G, 16), G), dim3(256), 0, s,
+                     (const bf16_t*)dy, (const bf16_t*)ymask, (const bf16_t*)x, mean, rstd, part,
+                     M, C);
+  hipLaunchKernelGGL(bn_fold_coef_kernel, dim3((G * C + 255) / 256), dim3(256), 0, s, part, dgamma,
+                     dbeta, gs_param, mean, rstd, gamma, coef, M, C, G);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_blocks(M, RPI, G, 4), G), dim3(256), 0, s,
+                     (const bf16_t*)dy, (const bf16_t*)ymask, (const bf16_t*)x, coef, (bf16_t*)dx,
+                     (bf16_t*)dym_out, M, C);
   return (int)hipGetLastError();
 }

@@ -11,12 +11,15 @@
 // the accumulator layout (lane holds 4 consecutive p for one q) gives 8-byte contiguous NHWC
 // stores in FWD/DGRAD and 64-byte row segments for the fp32 WGRAD atomics.
 //
-// Operand staging: LDS-DMA (`global_load_lds_dwordx4`, 1 KiB per wave-instruction) into an
+// Operand staging: LDS-DMA (`buffer_load_dwordx4 ... lds`, 1 KiB per wave-instruction) into an
 // NSTAGE-deep LDS ring, one raw s_barrier per K-step and COUNTED `s_waitcnt vmcnt(N)` so the next
 // NSTAGE-2 stages stay in flight across the barrier (cdna_hip_programming.md §5 "Pipelining across
-// barriers"). The implicit-GEMM gather is expressed purely through the per-lane SOURCE address:
-// padding / out-of-range taps point at a zero page, and the LDS swizzles are applied by
-// permuting which logical 16-byte chunk each lane fetches (the DMA destination is lane-linear).
+// barriers"). The implicit-GEMM gather is expressed purely through the per-lane SOURCE offset
+// (lane base + one wave-uniform cursor term per K-step): padding / out-of-range taps use an
+// offset past the buffer descriptor's range, which the hardware reads as zeros, and the LDS
+// swizzles are applied by permuting which logical 16-byte chunk each lane fetches (the DMA
+// destination is lane-linear). With >= 4 stages the next K-step's fragments are read from LDS
+// while the current MFMAs run.
 // Two LDS images:
 //   * K-major  [BK/32][rows][32] bf16, 16-B chunk XOR swizzle -> one ds_read_b128 per fragment,
 //     for operands whose reduction index is contiguous (W and X in FWD, dY in DGRAD);
@@ -101,12 +104,6 @@ __device__ __forceinline__ s8v mn_frag(const char* lds, int cb, int u, int lane)
   return r;
 }
 
-// one LDS-DMA wave-instruction: lane L's 16 source bytes land at lds_base + 16*L
-__device__ __forceinline__ void dma16(const void* src, char* lds_base) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
-}
-
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -122,10 +119,13 @@ __device__ __forceinline__ void cta_barrier() {
 //                        rows 16*(j%(ROWS/16)) .. +15 ; lane L -> row +L/4, phys chunk L%4
 //   MN-major BK x COLS : NI = BK*COLS/512, instr j -> k-rows (512/COLS)*j .. ; lane L ->
 //                        k-row + L/(COLS/8), phys chunk L%(COLS/8)
-template <int MODE, int BP, int BQ, int BK, int NS>
+// WLP = waves along P (1, 2 or 4; the other 4/WLP waves split Q). 2x2 is the default; 1x4 gives
+// a 64-channel tile (layer-1 convs) 64x64 per wave instead of 32x(BQ/2).
+template <int MODE, int BP, int BQ, int BK, int NS, int WLP = 2>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   constexpr int P_BYTES = BP * BK * 2, Q_BYTES = BQ * BK * 2, STAGE = P_BYTES + Q_BYTES;
-  constexpr int WP = BP / 2, WQ = BQ / 2, TP = WP / 16, TQ = WQ / 16;
+  constexpr int WP = BP / WLP, WQ = BQ / (4 / WLP), TP = WP / 16, TQ = WQ / 16;
+  static_assert(WLP == 1 || WLP == 2 || WLP == 4, "4 waves");
   constexpr bool P_KMAJOR = (MODE == MODE_FWD);
   constexpr bool Q_KMAJOR = (MODE != MODE_WGRAD);
   constexpr int P_NI = BP * BK / 512, Q_NI = BQ * BK / 512;  // wave-instructions per tile
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wp = wid >> 1, wq = wid & 1;
+  const int wp = wid / (4 / WLP), wq = wid % (4 / WLP);
   const int g = blockIdx.z;
   const int H = a.H, W = a.W, C = a.C, K = a.K, R = a.R, S = a.S, P = a.P, Q = a.Q;
   const int st = a.stride, pd = a.pad;
@@ -183,82 +183,105 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   const bf16_t* X = (const bf16_t*)a.x + (long long)g * a.x_gs;
   const bf16_t* Wt = (const bf16_t*)a.w + (long long)g * a.w_gs;
   const bf16_t* DY = (const bf16_t*)a.dy + (long long)g * a.dy_gs;
-  const bf16_t* ZERO = (const bf16_t*)a.zero;
 
-  // ---------------- per-lane DMA source precompute ----------------
-  // P operand
-  int pr_row[P_PW], pr_col[P_PW];  // K-major: (row, k-offset within stage) | MN-major: (k-row, col)
+  // ---------------- operand sources: buffer descriptors + per-lane base offsets ----------------
+  // Every LDS-DMA is `buffer_load_dwordx4 ... offen lds` at byte offset (lane base + wave-uniform
+  // cursor). Padding taps, tile overhang and the partial last WGRAD step use an offset beyond
+  // the descriptor's range, which the hardware returns as zeros: no branches, no zero page.
+  const unsigned x_bytes = (unsigned)((long long)a.N * H * W * C * 2);
+  const unsigned w_bytes = (unsigned)((long long)K * RSC * 2);
+  const unsigned dy_bytes = (unsigned)((long long)a.N * P * Q * K * 2);
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)X, 0, (int)x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc((void*)Wt, 0, (int)w_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc((void*)DY, 0, (int)dy_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rP = (MODE == MODE_WGRAD) ? rD : rW;
+  const __amdgpu_buffer_rsrc_t rQ = (MODE == MODE_DGRAD) ? rD : rX;
+  constexpr unsigned OOB = 0xFFFFFFF0u;
+  const int wsc = __builtin_amdgcn_readfirstlane(wid);  // wave id in an SGPR: LDS bases stay scalar
+
+  // P operand: element offset = p_base[i] + wave-uniform cursor term; p_base < 0 = never valid
+  int p_base[P_PW];
 #pragma unroll
   for (int i = 0; i < P_PW; ++i) {
     const int j = wid + 4 * i;
-    if constexpr (P_KMAJOR) {
+    if constexpr (P_KMAJOR) {  // FWD weights [K][RSC]: row = output channel
       const int u = j / (BP / 16), rb = 16 * (j % (BP / 16));
       const int row = rb + lane / 4;
-      pr_row[i] = row;
-      pr_col[i] = u * 32 + (((lane & 3) ^ km_swz(row)) << 3);
+      const int col = u * 32 + (((lane & 3) ^ km_swz(row)) << 3);
+      const int kk = p0 + row;
+      p_base[i] = kk < K ? kk * RSC + col : -1;
     } else {
       constexpr int CPR = BP / 8, RPIN = 512 / BP;
-      const int kr = RPIN * j + lane / CPR;
-      pr_row[i] = kr;
-      pr_col[i] = ((lane % CPR) ^ mn_swz<BP>(kr)) << 3;
+      const int kr = RPIN * j + lane / CPR;                 // reduction row within the stage
+      const int col = p0 + (((lane % CPR) ^ mn_swz<BP>(kr)) << 3);
+      if constexpr (MODE == MODE_DGRAD)  // weights [k][(r,s)][c]: + t_c*RSC + (r*S+s)*C
+        p_base[i] = col < C ? kr * RSC + col : -1;
+      else  // WGRAD dY [pix][k]: + kg*K ; the pixel row must stay < Kr
+        p_base[i] = col < K ? kr * K + col : -1;
     }
   }
   // Q operand
-  int qa[Q_PW], qb[Q_PW], qc[Q_PW], qd[Q_PW];
+  int q_base[Q_PW], q_h[Q_PW], q_w[Q_PW];
 #pragma unroll
   for (int i = 0; i < Q_PW; ++i) {
     const int j = wid + 4 * i;
     if constexpr (Q_KMAJOR) {
       const int u = j / (BQ / 16), rb = 16 * (j % (BQ / 16));
       const int row = rb + lane / 4;
-      qd[i] = u * 32 + (((lane & 3) ^ km_swz(row)) << 3);  // k offset within stage
+      const int kd = u * 32 + (((lane & 3) ^ km_swz(row)) << 3);  // k offset within stage
       const int qq = q0 + row;
-      if (qq < Qd) {
-        if constexpr (MODE == MODE_FWD) {
-          const int n = qq / (P * Q), rem = qq - n * (P * Q);
-          const int op = rem / Q, oq = rem - op * Q;
-          qa[i] = n * H * W;
-          qb[i] = op * st - pd;
-          qc[i] = oq * st - pd;
-        } else {
-          const int n = qq / (Hs * Ws), rem = qq - n * (Hs * Ws);
-          const int hi = rem / Ws, wi = rem - hi * Ws;
-          qa[i] = n * P * Q;
-          qb[i] = hi * tstep + ph_a + pd;
-          qc[i] = wi * tstep + ph_b + pd;
-        }
+      if constexpr (MODE == MODE_FWD) {
+        // X pixel (n, op*st - pd + r, oq*st - pd + s): + (t_r*W + t_s)*C + t_c
+        const int n = qq / (P * Q), rem = qq - n * (P * Q);
+        const int op = rem / Q, oq = rem - op * Q;
+        q_h[i] = op * st - pd;
+        q_w[i] = oq * st - pd;
+        q_base[i] = ((n * H + q_h[i]) * W + q_w[i]) * C + kd;
       } else {
-        qa[i] = 0;
-        qb[i] = -(1 << 28);
-        qc[i] = -(1 << 28);
+        // dY pixel (n, q_h - jr, q_w - js) for the jr-th / js-th tap of this phase
+        const int n = qq / (Hs * Ws), rem = qq - n * (Hs * Ws);
+        const int hi = rem / Ws, wi = rem - hi * Ws;
+        if (st <= 2) {
+          q_h[i] = hi + (ph_a + pd - r0) / st;
+          q_w[i] = wi + (ph_b + pd - s0) / st;
+          q_base[i] = ((n * P + q_h[i]) * Q + q_w[i]) * K + kd;
+        } else {  // generic stride: recomputed per step (rare)
+          q_h[i] = hi + pd;
+          q_w[i] = wi + pd;
+          q_base[i] = n * P * Q;
+        }
       }
-    } else {  // WGRAD X gather MN-major: k-row = pixel, col chunk = (r,s,c)
+      if (qq >= Qd) q_h[i] = -(1 << 28);  // tile overhang: always out of range
+      if constexpr (MODE == MODE_DGRAD) if (st > 2) q_w[i] = (q_w[i] & 0xffff) | (kd << 16);
+    } else {  // WGRAD X gather MN-major: k-row = pixel, col = (r, s, c)
       constexpr int CPR = BQ / 8, RPIN = 512 / BQ;
       const int kr = RPIN * j + lane / CPR;
       const int col = q0 + (((lane % CPR) ^ mn_swz<BQ>(kr)) << 3);
-      qd[i] = kr;
+      q_base[i] = kr;
       if (col < Qd) {
         const int rs = col / C;
-        qc[i] = col - rs * C;
-        qa[i] = rs / S;
-        qb[i] = rs - qa[i] * S;
+        const int c = col - rs * C;
+        const int r = rs / S;
+        q_h[i] = r - pd;
+        q_w[i] = ((rs - r * S - pd) & 0xffff) | (c << 16);  // packed (s - pad, c)
       } else {
-        qa[i] = -(1 << 28);
-        qb[i] = 0;
-        qc[i] = 0;
+        q_h[i] = -(1 << 28);
+        q_w[i] = 0;
       }
     }
   }
 
-  // running (r, s, channel-offset) of the reduction index for FWD/DGRAD: issue() is called for
-  // consecutive K-steps, so the tap decomposition advances incrementally (no divisions in-loop)
+  // reduction cursor for FWD/DGRAD: tap (t_r, t_s) [jr, js = tap index within the phase],
+  // channel run t_c; issue() is called for consecutive K-steps, so it advances without divisions
   const int CR = (MODE == MODE_FWD) ? C : K;  // contiguous reduction run per tap
-  int kg_run = kt0 * BK, t_r = 0, t_s = 0, t_c = 0;
+  int kg_run = kt0 * BK, t_r = 0, t_s = 0, t_c = 0, jr = 0, js = 0;
   if constexpr (MODE != MODE_WGRAD) {
     const int ti = kg_run / CR;  // tap index among the (phase's) valid taps
     t_c = kg_run - ti * CR;
-    t_r = r0 + tstep * (ti / Sn);
-    t_s = s0 + tstep * (ti % Sn);
+    jr = ti / Sn;
+    js = ti - jr * Sn;
+    t_r = r0 + tstep * jr;
+    t_s = s0 + tstep * js;
   }
 
   auto issue = [&](int slot) {
@@ -266,56 +289,56 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     char* Qs = Ps + P_BYTES;
     const int kg = kg_run;
     // ---- P ----
+    int pcur;  // wave-uniform element offset of this step
+    if constexpr (MODE == MODE_FWD) pcur = kg;
+    else if constexpr (MODE == MODE_DGRAD) pcur = t_c * RSC + (t_r * S + t_s) * C;
+    else pcur = kg * K;
 #pragma unroll
     for (int i = 0; i < P_PW; ++i) {
-      const int j = wid + 4 * i;
-      const bf16_t* src = ZERO;
-      if constexpr (MODE == MODE_FWD) {
-        const int kk = p0 + pr_row[i];
-        if (kk < K) src = Wt + (long long)kk * RSC + kg + pr_col[i];
-      } else if constexpr (MODE == MODE_DGRAD) {
-        const int c = p0 + pr_col[i];
-        if (c < C) src = Wt + (long long)(t_c + pr_row[i]) * RSC + (t_r * S + t_s) * C + c;
-      } else {
-        const int pix = kg + pr_row[i];
-        const int kch = p0 + pr_col[i];
-        if (pix < Kr && kch < K) src = DY + (long long)pix * K + kch;
+      bool ok = p_base[i] >= 0;
+      if constexpr (MODE == MODE_WGRAD) {
+        constexpr int RPIN = 512 / BP, CPR = BP / 8;
+        ok = ok && (RPIN * (wid + 4 * i) + lane / CPR) < Kr - kg;
       }
-      dma16(src, Ps + j * 1024);
+      const unsigned off = ok ? (unsigned)(p_base[i] + pcur) * 2u : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rP, (__attribute__((address_space(3))) void*)(Ps + (wsc + 4 * i) * 1024), 16, off, 0, 0, 0);
     }
     // ---- Q ----
 #pragma unroll
     for (int i = 0; i < Q_PW; ++i) {
-      const int j = wid + 4 * i;
-      const bf16_t* src = ZERO;
+      unsigned off = OOB;
       if constexpr (MODE == MODE_FWD) {
-        const int ih = qb[i] + t_r, iw = qc[i] + t_s;
+        const int ih = q_h[i] + t_r, iw = q_w[i] + t_s;
         if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
-          src = X + (long long)(qa[i] + ih * W + iw) * C + t_c + qd[i];
+          off = (unsigned)(q_base[i] + (t_r * W + t_s) * C + t_c) * 2u;
       } else if constexpr (MODE == MODE_DGRAD) {
-        int ph = qb[i] - t_r, pw = qc[i] - t_s;
-        bool ok = ph >= 0 && pw >= 0;
-        if (st == 2) {
-          ok = ok && (((ph | pw) & 1) == 0);
-          ph >>= 1;
-          pw >>= 1;
-        } else if (st > 2) {
-          ok = ok && (ph % st == 0) && (pw % st == 0);
-          ph /= st;
-          pw /= st;
+        if (st <= 2) {
+          const int ph = q_h[i] - jr, pw = q_w[i] - js;
+          if ((unsigned)ph < (unsigned)P && (unsigned)pw < (unsigned)Q)
+            off = (unsigned)(q_base[i] - (jr * Q + js) * K + t_c) * 2u;
+        } else {
+          int ph = q_h[i] - t_r, pw = (q_w[i] & 0xffff) - t_s;
+          const int kd = q_w[i] >> 16;
+          if (ph >= 0 && pw >= 0 && ph % st == 0 && pw % st == 0) {
+            ph /= st;
+            pw /= st;
+            if (ph < P && pw < Q) off = (unsigned)((q_base[i] + ph * Q + pw) * K + t_c + kd) * 2u;
+          }
         }
-        if (ok && ph < P && pw < Q) src = DY + (long long)(qa[i] + ph * Q + pw) * K + t_c + qd[i];
       } else {
-        const int pix = kg + qd[i];
-        if (qa[i] >= 0 && pix < Kr) {
+        const int pix = kg + q_base[i];
+        if (q_h[i] > -(1 << 27) && pix < Kr) {
           const int n = fdiv(pix, div_pq), rem = pix - n * (P * Q);
           const int op = fdiv(rem, div_q), oq = rem - op * Q;
-          const int ih = op * st - pd + qa[i], iw = oq * st - pd + qb[i];
+          const int sw = (int)(short)(q_w[i] & 0xffff), c = q_w[i] >> 16;
+          const int ih = op * st + q_h[i], iw = oq * st + sw;
           if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
-            src = X + ((long long)(n * H + ih) * W + iw) * C + qc[i];
+            off = (unsigned)(((n * H + ih) * W + iw) * C + c) * 2u;
         }
       }
-      dma16(src, Qs + j * 1024);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rQ, (__attribute__((address_space(3))) void*)(Qs + (wsc + 4 * i) * 1024), 16, off, 0, 0, 0);
     }
     // advance the reduction cursor by one K-step
     kg_run += BK;
@@ -324,7 +347,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       if (t_c >= CR) {
         t_c = 0;
         t_s += tstep;
-        if (t_s >= S) { t_s = s0; t_r += tstep; }
+        ++js;
+        if (t_s >= S) { t_s = s0; js = 0; t_r += tstep; ++jr; }
       }
     }
   };
@@ -335,42 +359,86 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < TQ; ++j) acc[i][j] = (f4v){0.f, 0.f, 0.f, 0.f};
 
+  auto load_frags = [&](const char* Ps, int u, s8v* pf, s8v* qf) {
+    const char* Qs = Ps + P_BYTES;
+#pragma unroll
+    for (int t = 0; t < TP; ++t) {
+      if constexpr (P_KMAJOR) pf[t] = km_frag<BP>(Ps, wp * WP + t * 16, u, lane);
+      else pf[t] = mn_frag<BP>(Ps, wp * WP + t * 16, u, lane);
+    }
+#pragma unroll
+    for (int t = 0; t < TQ; ++t) {
+      if constexpr (Q_KMAJOR) qf[t] = km_frag<BQ>(Qs, wq * WQ + t * 16, u, lane);
+      else qf[t] = mn_frag<BQ>(Qs, wq * WQ + t * 16, u, lane);
+    }
+  };
+  auto mfma_all = [&](const s8v* pf, const s8v* qf) {
+#pragma unroll
+    for (int ti = 0; ti < TP; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < TQ; ++tj)
+        acc[ti][tj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[ti], qf[tj], acc[ti][tj], 0, 0, 0);
+  };
+
   // prologue: stages 0 .. NS-2 in flight
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < nk) issue(s);
 
-  for (int i = 0; i < nk; ++i) {
-    // retire stage i: at most (stages issued after it) * LPS DMA ops may stay outstanding
-    if constexpr (NS >= 3) {
-      if (i + NS - 2 < nk) wait_vm<(NS - 2) * LPS>();
-      else if (NS >= 4 && i + NS - 3 < nk) wait_vm<(NS >= 4 ? (NS - 3) * LPS : 0)>();
+  if constexpr (NS >= 4 && BK == 32) {
+    // Fragment prefetch: the fragments of K-step i+1 are read from LDS while the MFMAs of step i
+    // run (two register sets). Stage i+1 is waited for one step early, so NS-3 stages stay in
+    // flight across each barrier. WAR on the slot refilled at step i (stage i-1's): its fragments
+    // were consumed by step i-1's MFMAs, which every wave issued before this step's barrier.
+    s8v pfA[TP], qfA[TQ], pfB[TP], qfB[TQ];
+    if (nk > 0) {
+      if (NS - 2 < nk) wait_vm<(NS - 2) * LPS>();
       else wait_vm<0>();
-    } else {
-      wait_vm<0>();
+      cta_barrier();
+      load_frags(smem, 0, pfA, qfA);
     }
-    cta_barrier();  // stage i visible to all waves; slot of stage i-1 free for reuse
-    if (i + NS - 1 < nk) issue((i + NS - 1) % NS);
-    const char* Ps = smem + (i % NS) * STAGE;
-    const char* Qs = Ps + P_BYTES;
-#pragma unroll
-    for (int u = 0; u < BK / 32; ++u) {
-      s8v pf[TP], qf[TQ];
-#pragma unroll
-      for (int t = 0; t < TP; ++t) {
-        if constexpr (P_KMAJOR) pf[t] = km_frag<BP>(Ps, wp * WP + t * 16, u, lane);
-        else pf[t] = mn_frag<BP>(Ps, wp * WP + t * 16, u, lane);
+    auto step = [&](int i, s8v* pc, s8v* qc, s8v* pn, s8v* qn) {
+      if (i + 1 < nk) {  // retire stage i+1: stages i+2 .. min(nk-1, i+NS-2) may stay in flight
+        if (i + NS - 2 < nk) wait_vm<(NS - 3) * LPS>();
+        else if (NS >= 5 && i + NS - 3 < nk) wait_vm<(NS >= 5 ? (NS - 4) * LPS : 0)>();
+        else wait_vm<0>();
       }
-#pragma unroll
-      for (int t = 0; t < TQ; ++t) {
-        if constexpr (Q_KMAJOR) qf[t] = km_frag<BQ>(Qs, wq * WQ + t * 16, u, lane);
-        else qf[t] = mn_frag<BQ>(Qs, wq * WQ + t * 16, u, lane);
+      cta_barrier();
+      if (i + NS - 1 < nk) issue((i + NS - 1) % NS);
+      if (i + 1 < nk) load_frags(smem + ((i + 1) % NS) * STAGE, 0, pn, qn);
+      mfma_all(pc, qc);
+    };
+    int i = 0;
+    for (; i + 1 < nk; i += 2) {
+      step(i, pfA, qfA, pfB, qfB);
+      step(i + 1, pfB, qfB, pfA, qfA);
+    }
+    if (i < nk) step(i, pfA, qfA, pfB, qfB);
+  } else {
+    for (int i = 0; i < nk; ++i) {
+      // retire stage i: at most (stages issued after it) * LPS DMA ops may stay outstanding
+      if constexpr (NS >= 3) {
+        if (i + NS - 2 < nk) wait_vm<(NS - 2) * LPS>();
+        else if (NS >= 4 && i + NS - 3 < nk) wait_vm<(NS >= 4 ? (NS - 3) * LPS : 0)>();
+        else wait_vm<0>();
+      } else {
+        wait_vm<0>();
       }
+      cta_barrier();  // stage i visible to all waves; slot of stage i-1 free for reuse
+      if (i + NS - 1 < nk) issue((i + NS - 1) % NS);
+      const char* Ps = smem + (i % NS) * STAGE;
+      // within a stage, the next 32-deep fragments load while the current ones feed the MFMAs
+      s8v pfA[TP], qfA[TQ], pfB[TP], qfB[TQ];
+      load_frags(Ps, 0, pfA, qfA);
 #pragma unroll
-      for (int ti = 0; ti < TP; ++ti)
-#pragma unroll
-        for (int tj = 0; tj < TQ; ++tj)
-          acc[ti][tj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[ti], qf[tj], acc[ti][tj], 0, 0, 0);
+      for (int u = 0; u < BK / 32; u += 2) {
+        if (u + 1 < BK / 32) load_frags(Ps, u + 1, pfB, qfB);
+        mfma_all(pfA, qfA);
+        if (u + 1 < BK / 32) {
+          if (u + 2 < BK / 32) load_frags(Ps, u + 2, pfA, qfA);
+          mfma_all(pfB, qfB);
+        }
+      }
     }
   }
 
@@ -479,11 +547,11 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   }
 }
 
-template <int MODE, int BP, int BQ, int BK, int NS>
+template <int MODE, int BP, int BQ, int BK, int NS, int WLP = 2>
 static hipError_t launch_cfg(const ConvArgs& a, int Pd, int Qd, int gy, hipStream_t stream) {
   const int ntp = (Pd + BP - 1) / BP, ntq = (Qd + BQ - 1) / BQ;
   dim3 grid(ntp * ntq, gy, a.G);
-  hipLaunchKernelGGL((conv_igemm_kernel<MODE, BP, BQ, BK, NS>), grid, dim3(256), 0, stream, a);
+  hipLaunchKernelGGL((conv_igemm_kernel<MODE, BP, BQ, BK, NS, WLP>), grid, dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 
@@ -502,6 +570,12 @@ static hipError_t dispatch(const ConvArgs& a, int Pd, int Qd, int bp, int bq, in
   // 256-wide tiles: 128x64 per wave (1.5x the MFMA work per LDS byte of a 64x64 wave tile)
   DDL_CFG(256, 128, 32, 3) DDL_CFG(128, 256, 32, 3) DDL_CFG(256, 128, 32, 2) DDL_CFG(128, 256, 32, 2)
 #undef DDL_CFG
+  // 64-wide P tiles with the 4 waves side by side along Q (64x64 per wave); encoded as bp = 48
+#define DDL_CFG1(BQ_, BK_, NS_) \
+  if (bp == 48 && bq == BQ_ && bk == BK_ && ns == NS_) \
+    return launch_cfg<MODE, 64, BQ_, BK_, NS_, 1>(a, Pd, Qd, gy, s);
+  DDL_CFG1(256, 32, 4) DDL_CFG1(256, 64, 3) DDL_CFG1(256, 64, 2) DDL_CFG1(256, 32, 3)
+#undef DDL_CFG1
   return hipErrorInvalidValue;
 }
 
@@ -522,7 +596,10 @@ static bool conv_shapes_ok(const ConvArgs& a) {
   if (a.stride <= 0 || a.pad < 0 || !a.zero) return false;
   if (a.P != (a.H + 2 * a.pad - a.R) / a.stride + 1) return false;
   if (a.Q != (a.W + 2 * a.pad - a.S) / a.stride + 1) return false;
-  if ((long long)a.N * a.H * a.W * (a.C > a.K ? a.C : a.K) >= (1LL << 31)) return false;
+  // 32-bit element offsets and buffer byte ranges (< the out-of-range sentinel 0xFFFFFFF0)
+  if ((long long)a.N * a.H * a.W * (a.C > a.K ? a.C : a.K) >= (1LL << 31) - 64) return false;
+  if ((long long)a.N * a.P * a.Q * (a.C > a.K ? a.C : a.K) >= (1LL << 31) - 64) return false;
+  if ((long long)a.K * a.R * a.S * a.C >= (1LL << 31) - 64) return false;
   return a.P > 0 && a.Q > 0;
 }
 
@@ -537,6 +614,20 @@ static void decode_cfg(int cfg, int& bp, int& bq, int& bk, int& ns) {
   if (!ns) ns = bk == 32 ? 4 : 3;
 }
 
+// Grid-size-aware fallback (G=1 sweep, profiles/conv_sweep_g1.log): when the tuned tile leaves
+// CUs without a workgroup, a 64-wide tile (BK=64 when the reduction run allows) gets more CUs
+// working: 64x128 while that gives >= 1 workgroup per CU, else 64x64. (At 1-2 workgroups per CU
+// the big tile still wins: profiles/conv_sweep_r1d.log, layer 4 at G=8.)
+static void small_grid_tiles(int Pd, long long Qd, int G, bool bk64_ok, int& bp, int& bq, int& bk,
+                             int& ns) {
+  auto tiles = [&](int p, int q) { return (long long)((Pd + p - 1) / p) * ((Qd + q - 1) / q) * G; };
+  if (tiles(bp, bq) >= num_cus()) return;
+  bk = bk64_ok ? 64 : 32;
+  ns = bk64_ok ? 3 : 4;
+  bp = 64;
+  bq = tiles(64, 128) >= num_cus() ? 128 : 64;
+}
+
 DDL_API int ddl_conv_fwd(const ConvArgs* ap, int cfg, hipStream_t stream) {
   const ConvArgs& a = *ap;
   if (!conv_shapes_ok(a)) return (int)hipErrorInvalidValue;
@@ -544,6 +635,7 @@ DDL_API int ddl_conv_fwd(const ConvArgs* ap, int cfg, hipStream_t stream) {
   // sweep-tuned (profiles/conv_sweep_r1.log): 128x128x64 / 2 stages for >=128 output channels
   int bp = 64, bq = 128, bk = 32, ns = 4;
   if (a.K >= 128 && a.C % 64 == 0) { bp = 128; bk = 64; ns = 2; }
+  small_grid_tiles(Pd, Qd, a.G, a.C % 64 == 0, bp, bq, bk, ns);
   decode_cfg(cfg, bp, bq, bk, ns);
   if (a.C % bk) return (int)hipErrorInvalidValue;
   return (int)dispatch<MODE_FWD>(a, Pd, Qd, bp, bq, bk, ns, 1, stream);
@@ -558,6 +650,7 @@ DDL_API int ddl_conv_dgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
   const int Qd = phased ? a.N * ((a.H + 1) / 2) * ((a.W + 1) / 2) : a.N * a.H * a.W;
   int bp = 64, bq = 128, bk = 32, ns = 4;
   if (a.C >= 128 && a.K % 64 == 0) { bp = 128; bk = 64; ns = 2; }
+  small_grid_tiles(Pd, Qd * (phased ? 4 : 1), a.G, a.K % 64 == 0, bp, bq, bk, ns);
   decode_cfg(cfg, bp, bq, bk, ns);
   if (a.K % bk) return (int)hipErrorInvalidValue;
   return (int)dispatch<MODE_DGRAD>(a, Pd, Qd, bp, bq, bk, ns, phased ? 4 : 1, stream);
@@ -571,18 +664,20 @@ DDL_API int ddl_conv_wgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
   int bp = a.K >= 128 ? 128 : 64, bq = Qd >= 128 ? 128 : 64, bk = 32, ns = 4;
   if (a.K >= 128 && Qd >= 128) ns = 3;
   if (Qd < 128) { bp = 64; bq = 64; bk = 64; ns = 3; }
-  decode_cfg(cfg, bp, bq, bk, ns);
-  const long long tiles = (long long)((Pd + bp - 1) / bp) * ((Qd + bq - 1) / bq) * a.G;
-  const long long nk = (Kr + bk - 1) / bk;
-  int splits = a.split_k;
-  if (!splits) {
-    // aim for ~2 waves of workgroups over the CUs, keep >= 16 K-steps per split
+  // aim for ~2 waves of workgroups over the CUs, keep >= 16 K-steps per split
+  auto auto_splits = [&](int p, int q, int k) {
+    const long long tiles = (long long)((Pd + p - 1) / p) * ((Qd + q - 1) / q) * a.G;
+    const long long nk = (Kr + k - 1) / k;
     long long want = (2LL * num_cus() + tiles - 1) / tiles;
     long long maxs = nk / 16 > 0 ? nk / 16 : 1;
-    splits = (int)(want < maxs ? want : maxs);
-    if (splits < 1) splits = 1;
-    if (splits > 1024) splits = 1024;
-  }
+    long long sp = want < maxs ? want : maxs;
+    return (int)(sp < 1 ? 1 : (sp > 1024 ? 1024 : sp));
+  };
+  // few tiles and a shallow reduction (one client, deep layers: profiles/conv_sweep_g1.log): the
+  // splits would be too short to fill the LDS pipeline, so trade split depth for 4x the tiles
+  if (!cfg && ((Kr + bk - 1) / bk) / auto_splits(bp, bq, bk) < 32) { bp = 64; bq = 64; bk = 64; ns = 3; }
+  decode_cfg(cfg, bp, bq, bk, ns);
+  int splits = a.split_k ? a.split_k : auto_splits(bp, bq, bk);
   if (splits > 1 && !a.accumulate) return (int)hipErrorInvalidValue;  // needs zeroed fp32 output
   return (int)dispatch<MODE_WGRAD>(a, Pd, Qd, bp, bq, bk, ns, splits, stream);
 }

@@ -253,8 +253,13 @@ DDL_API int ddl_avgpool_bwd(const void* dy, void* dx, int NB, int HW, int C, hip
 
 // ---------------------------------------------------------------------------------------------
 // dropout: keep iff philox(seed, element/4)[element%4] >= p ; scale 1/(1-p). Mask recomputed.
+// The Philox counter base = offset + *offset_dev (if given): a device-resident per-layer counter
+// advanced by ddl_u64_add after each backward, so a captured HIP graph draws a fresh mask on
+// every replay while forward and backward of one step share it.
 __global__ void dropout_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n,
-                               float p, unsigned long long seed, unsigned long long offset) {
+                               float p, unsigned long long seed, unsigned long long offset,
+                               const unsigned long long* __restrict__ offset_dev) {
+  if (offset_dev) offset += *offset_dev;
   const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
   const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
   GSTRIDE_LOOP(t, n / 8) {
@@ -273,10 +278,17 @@ __global__ void dropout_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict_
   }
 }
 DDL_API int ddl_dropout(const void* x, void* y, long long n, float p, unsigned long long seed,
-                        unsigned long long offset, hipStream_t s) {
+                        unsigned long long offset, const unsigned long long* offset_dev,
+                        hipStream_t s) {
   if (n % 8) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n / 8, 256)), dim3(256), 0, s, (const bf16_t*)x,
-                     (bf16_t*)y, n, p, seed, offset);
+                     (bf16_t*)y, n, p, seed, offset, offset_dev);
+  return (int)hipGetLastError();
+}
+
+__global__ void u64_add_kernel(unsigned long long* p, unsigned long long inc) { *p += inc; }
+DDL_API int ddl_u64_add(unsigned long long* p, unsigned long long inc, hipStream_t s) {
+  hipLaunchKernelGGL(u64_add_kernel, dim3(1), dim3(1), 0, s, p, inc);
   return (int)hipGetLastError();
 }
 

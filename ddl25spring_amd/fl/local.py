@@ -61,7 +61,8 @@ class LocalTrainer:
         st, opt = self.net.store, self.opt
         # the warm-up steps really train: snapshot and restore so the first graph step is exact
         snap = (st.data[:G].clone(), st.buffers[:G].clone(),
-                None if opt.mom is None else opt.mom[:G].clone(), opt.steps)
+                None if opt.mom is None else opt.mom[:G].clone(), opt.steps,
+                [c.clone() for c in self.net.rng_counters()])
         static_idx = torch.empty(G, self.B, dtype=torch.int32, device=self.net.device)
         static_idx.copy_(idx_row)
         s = torch.cuda.Stream()
@@ -81,6 +82,8 @@ class LocalTrainer:
         if snap[2] is not None:
             opt.mom[:G].copy_(snap[2])
         opt.steps = snap[3]
+        for c, saved in zip(self.net.rng_counters(), snap[4]):
+            c.copy_(saved)  # warm-up steps advanced the dropout counters: rewind them too
         st.sync_shadow()
         return graph, static_idx, loss
 

@@ -160,8 +160,8 @@ class ConvUnit(Layer):
             ymask = y if (self.act == RELU and not self.grad_premasked) else None
             if self.act == LEAKY and not self.grad_premasked:
                 dy = Fn.act_bwd(y, dy, LEAKY)
-            sums = Fn.bn_bwd_reduce(dy, ymask, c, mu, rs, st.grad_of(self.gamma), st.grad_of(self.beta))
-            dc = Fn.bn_bwd_apply(dy, ymask, c, mu, rs, st.param(self.gamma), sums)
+            dc = Fn.bn_backward(dy, ymask, c, mu, rs, st.param(self.gamma), st.grad_of(self.gamma),
+                                st.grad_of(self.beta))
         else:
             dc = dy
             if self.act and not self.grad_premasked:
@@ -242,27 +242,34 @@ class Flatten(Layer):
 
 
 class Dropout(Layer):
+    """Philox dropout whose counter lives on the device: forward and backward of a step share
+    the mask, ``backward`` advances the counter by a stream-ordered kernel, so HIP-graph replays
+    draw fresh masks and two nets built with the same seed draw identical ones (the seed comes
+    from the net seed and the layer's position, set in ``Net.to``)."""
     name = "dropout"
-    _counter = 0
 
     def __init__(self, p):
         self.p = float(p)
         self.seed = 0x5EED
-        Dropout._counter += 1
-        self.uid = Dropout._counter
+        self.uid = 1
+        self.ctr = None
+
+    def bind(self, store) -> None:
+        super().bind(store)
+        self.ctr = torch.zeros(1, dtype=torch.int64, device=store.data.device)
 
     def forward(self, x, train):
         if not train or self.p <= 0:
             return x, None
-        # counter-based RNG: (seed, per-call offset) fully determines the mask
-        self.offset = getattr(self, "offset", 0) + x.numel()
-        off = self.offset + self.uid * (1 << 40)
-        return Fn.dropout(x, self.p, self.seed, off), off
+        off = self.uid << 40
+        return Fn.dropout(x, self.p, self.seed, off, self.ctr), off
 
     def backward(self, dy, off):
         if off is None:
             return dy
-        return Fn.dropout(dy.contiguous(), self.p, self.seed, off)
+        dx = Fn.dropout(dy.contiguous(), self.p, self.seed, off, self.ctr)
+        Fn.u64_add(self.ctr, dy.numel())
+        return dx
 
 
 def fan_in_of(layer: ConvUnit) -> int:

@@ -13,7 +13,7 @@ import torch
 
 from ..ops import functional as Fn
 from ..ops.workspace import Workspace
-from .layers import RELU, ConvUnit, Layer
+from .layers import RELU, ConvUnit, Dropout, Layer
 from .params import ParamStore
 
 
@@ -47,9 +47,16 @@ class Net:
     def to(self, device, seed: int = 0, generator=None):
         self.device = torch.device(device)
         self.store.materialize(self.device, seed=seed, generator=generator)
-        for layer in self.layers:
+        for i, layer in enumerate(self.layers):
             layer.bind(self.store)
+            if isinstance(layer, Dropout):  # deterministic per (net seed, position)
+                layer.seed = (int(seed) * 0x9E3779B97F4A7C15 + i * 0xBF58476D1CE4E5B9) & (2 ** 63 - 1)
+                layer.uid = i + 1
         return self
+
+    def rng_counters(self) -> list:
+        """Device-resident RNG counters (dropout Philox offsets) — part of the training state."""
+        return [layer.ctr for layer in self.layers if isinstance(layer, Dropout) and layer.ctr is not None]
 
     def train(self, mode: bool = True):
         self.training = mode

@@ -42,8 +42,8 @@ class _BNConv(ConvUnit):
 
     def bn_backward(self, dy, ymask, c, mu, rs, emit_dym=False):
         st = self.store
-        sums = Fn.bn_bwd_reduce(dy, ymask, c, mu, rs, st.grad_of(self.gamma), st.grad_of(self.beta))
-        return Fn.bn_bwd_apply(dy, ymask, c, mu, rs, st.param(self.gamma), sums, emit_dym=emit_dym)
+        return Fn.bn_backward(dy, ymask, c, mu, rs, st.param(self.gamma), st.grad_of(self.gamma),
+                              st.grad_of(self.beta), emit_dym=emit_dym)
 
 
 class BasicBlock(Layer):

@@ -73,6 +73,7 @@ _SIGS = {
     "ddl_bn_bwd_reduce": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i32, i32, vp],
     "ddl_bn_bwd_apply": [vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, i64, i32, i32, vp],
     "ddl_bn_stats": [vp, vp, i64, i32, i32, vp],
+    "ddl_bn_backward": [vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp],
     # nn_ops.hip
     "ddl_prep_images": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
     "ddl_nchw_to_nhwc": [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
@@ -82,7 +83,8 @@ _SIGS = {
     "ddl_maxpool2_bwd": [vp, vp, vp, i32, i32, i32, i32, vp],
     "ddl_avgpool_fwd": [vp, vp, i32, i32, i32, vp],
     "ddl_avgpool_bwd": [vp, vp, i32, i32, i32, vp],
-    "ddl_dropout": [vp, vp, i64, f32, u64, u64, vp],
+    "ddl_dropout": [vp, vp, i64, f32, u64, u64, vp, vp],
+    "ddl_u64_add": [vp, u64, vp],
     "ddl_act_fwd": [vp, vp, i64, i32, f32, vp],
     "ddl_act_bwd": [vp, vp, vp, i64, i32, f32, vp],
     "ddl_channel_sum": [vp, vp, i64, i64, i32, i32, vp],

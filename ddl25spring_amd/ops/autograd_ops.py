@@ -430,8 +430,7 @@ class _BatchNormAct(torch.autograd.Function):
             d = Fn.act_bwd(y, d, 2, 0.2)
         dgamma = torch.zeros(1, C, dtype=torch.float32, device=dy.device)
         dbeta = torch.zeros(1, C, dtype=torch.float32, device=dy.device)
-        sums = Fn.bn_bwd_reduce(d, ymask, xg, mean, rstd, dgamma, dbeta)
-        dx = Fn.bn_bwd_apply(d, ymask, xg, mean, rstd, ga, sums)
+        dx = Fn.bn_backward(d, ymask, xg, mean, rstd, ga, dgamma, dbeta)
         return dx.view(ctx.shape), dgamma.view(C), dbeta.view(C), None, None, None, None, None, None, None
 
 

