@@ -43,7 +43,7 @@ struct ConvArgs {
   const float* bias;     // FWD: [K] fp32 (optional)
   const void* residual;  // DGRAD: bf16 added to dx (optional), same layout as out
   const void* mask;      // DGRAD: dx *= (mask > 0) (optional), same layout as out
-  const void* zero;      // >= 64 zero bytes in global memory (DMA source for padding)
+  const void* zero;      // legacy zero page (padding now reads past the buffer descriptor's range)
   long long x_gs, w_gs, dy_gs, out_gs, bias_gs, stats_gs;
   int G, N, H, W, C, K, R, S, P, Q, stride, pad;
   int relu, accumulate, split_k;
@@ -304,19 +304,22 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rP, (__attribute__((address_space(3))) void*)(Ps + (wsc + 4 * i) * 1024), 16, off, 0, 0, 0);
     }
-    // ---- Q ----
+    // ---- Q ----  (wave-uniform tap term computed once; per lane: add + range test + select)
+    int qcur = 0;
+    if constexpr (MODE == MODE_FWD) qcur = (t_r * W + t_s) * C + t_c;
+    else if constexpr (MODE == MODE_DGRAD) qcur = t_c - (jr * Q + js) * K;
 #pragma unroll
     for (int i = 0; i < Q_PW; ++i) {
       unsigned off = OOB;
       if constexpr (MODE == MODE_FWD) {
         const int ih = q_h[i] + t_r, iw = q_w[i] + t_s;
-        if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
-          off = (unsigned)(q_base[i] + (t_r * W + t_s) * C + t_c) * 2u;
+        const bool ok = ((unsigned)ih < (unsigned)H) & ((unsigned)iw < (unsigned)W);
+        off = ok ? (unsigned)(q_base[i] + qcur) * 2u : OOB;
       } else if constexpr (MODE == MODE_DGRAD) {
         if (st <= 2) {
           const int ph = q_h[i] - jr, pw = q_w[i] - js;
-          if ((unsigned)ph < (unsigned)P && (unsigned)pw < (unsigned)Q)
-            off = (unsigned)(q_base[i] - (jr * Q + js) * K + t_c) * 2u;
+          const bool ok = ((unsigned)ph < (unsigned)P) & ((unsigned)pw < (unsigned)Q);
+          off = ok ? (unsigned)(q_base[i] + qcur) * 2u : OOB;
         } else {
           int ph = q_h[i] - t_r, pw = (q_w[i] & 0xffff) - t_s;
           const int kd = q_w[i] >> 16;
@@ -390,30 +393,26 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     // run (two register sets). Stage i+1 is waited for one step early, so NS-3 stages stay in
     // flight across each barrier. WAR on the slot refilled at step i (stage i-1's): its fragments
     // were consumed by step i-1's MFMAs, which every wave issued before this step's barrier.
+    // The prefetch read is unconditional (past the last step it reads a stale slot, unused) so
+    // the compiler's lgkmcnt tracking stays exact: a conditional read would make it wait for the
+    // freshly issued reads before the current MFMAs.
     s8v pfA[TP], qfA[TQ], pfB[TP], qfB[TQ];
-    if (nk > 0) {
-      if (NS - 2 < nk) wait_vm<(NS - 2) * LPS>();
+    if (NS - 2 < nk) wait_vm<(NS - 2) * LPS>();
+    else wait_vm<0>();
+    cta_barrier();
+    load_frags(smem, 0, pfA, qfA);
+    for (int i = 0; i < nk; ++i) {
+      if (i + NS - 2 < nk) wait_vm<(NS - 3) * LPS>();  // retire stage i+1 (stages i+2.. may fly)
       else wait_vm<0>();
       cta_barrier();
-      load_frags(smem, 0, pfA, qfA);
-    }
-    auto step = [&](int i, s8v* pc, s8v* qc, s8v* pn, s8v* qn) {
-      if (i + 1 < nk) {  // retire stage i+1: stages i+2 .. min(nk-1, i+NS-2) may stay in flight
-        if (i + NS - 2 < nk) wait_vm<(NS - 3) * LPS>();
-        else if (NS >= 5 && i + NS - 3 < nk) wait_vm<(NS >= 5 ? (NS - 4) * LPS : 0)>();
-        else wait_vm<0>();
-      }
-      cta_barrier();
       if (i + NS - 1 < nk) issue((i + NS - 1) % NS);
-      if (i + 1 < nk) load_frags(smem + ((i + 1) % NS) * STAGE, 0, pn, qn);
-      mfma_all(pc, qc);
-    };
-    int i = 0;
-    for (; i + 1 < nk; i += 2) {
-      step(i, pfA, qfA, pfB, qfB);
-      step(i + 1, pfB, qfB, pfA, qfA);
+      load_frags(smem + ((i + 1) % NS) * STAGE, 0, pfB, qfB);
+      mfma_all(pfA, qfA);
+#pragma unroll
+      for (int t = 0; t < TP; ++t) pfA[t] = pfB[t];
+#pragma unroll
+      for (int t = 0; t < TQ; ++t) qfA[t] = qfB[t];
     }
-    if (i < nk) step(i, pfA, qfA, pfB, qfB);
   } else {
     for (int i = 0; i < nk; ++i) {
       // retire stage i: at most (stages issued after it) * LPS DMA ops may stay outstanding
