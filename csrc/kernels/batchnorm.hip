@@ -37,34 +37,44 @@ struct BNArgs {
   int training, stripes;  // stripes <= 1: plain [G][2C]
 };
 
-__global__ void bn_finalize_kernel(BNArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.G * a.C) return;
-  const int g = i / a.C, c = i - g * a.C;
+// Stripe fold shared by finalize / fold_coef: a 256-thread block owns 32 channels of one group;
+// thread (sg, cl) sums stripes sg, sg+8, ... (independent loads, one memory round trip), then
+// the 8 partial sums of each channel meet in LDS. Returns the totals on threads with sg == 0.
+__device__ __forceinline__ void stripe_fold(const float* __restrict__ base, int ns, int C, int c,
+                                            bool valid, float* red, float& t0, float& t1) {
+  const int sg = threadIdx.x >> 5, cl = threadIdx.x & 31;
+  float a0 = 0.f, a1 = 0.f;
+  if (valid)
+    for (int k = sg; k < ns; k += 8) {
+      a0 += base[(long long)k * 2 * C + c];
+      a1 += base[(long long)k * 2 * C + C + c];
+    }
+  red[sg * 64 + cl] = a0;
+  red[sg * 64 + 32 + cl] = a1;
+  __syncthreads();
+  t0 = t1 = 0.f;
+  if (sg == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      t0 += red[k * 64 + cl];
+      t1 += red[k * 64 + 32 + cl];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_finalize_kernel(BNArgs a) {
+  __shared__ float red[8 * 64];
+  const int g = blockIdx.y, c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const bool valid = c < a.C;
   float mean, var;
   if (a.training) {
     const int ns = a.stripes > 1 ? a.stripes : 1;
-    const float* st = a.stats + (long long)g * ns * 2 * a.C;
-    double s1 = 0.0, s2 = 0.0;
-    // independent partial sums so the stripe loads issue back to back (latency, not bandwidth)
-    double p1[4] = {0.0, 0.0, 0.0, 0.0}, p2[4] = {0.0, 0.0, 0.0, 0.0};
-    int k = 0;
-    for (; k + 4 <= ns; k += 4) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        p1[u] += st[(long long)(k + u) * 2 * a.C + c];
-        p2[u] += st[(long long)(k + u) * 2 * a.C + a.C + c];
-      }
-    }
-    for (; k < ns; ++k) {
-      p1[0] += st[(long long)k * 2 * a.C + c];
-      p2[0] += st[(long long)k * 2 * a.C + a.C + c];
-    }
-    s1 = (p1[0] + p1[1]) + (p1[2] + p1[3]);
-    s2 = (p2[0] + p2[1]) + (p2[2] + p2[3]);
+    float s1f, s2f;
+    stripe_fold(a.stats + (long long)g * ns * 2 * a.C, ns, a.C, c, valid, red, s1f, s2f);
+    if ((threadIdx.x >> 5) != 0 || !valid) return;
     const double M = (double)a.count;
-    const double m = s1 / M;
-    double v = s2 / M - m * m;
+    const double m = (double)s1f / M;
+    double v = (double)s2f / M - m * m;
     if (v < 0) v = 0;
     mean = (float)m;
     var = (float)v;
@@ -75,10 +85,12 @@ __global__ void bn_finalize_kernel(BNArgs a) {
       a.running_var[o] = (1.f - a.momentum) * a.running_var[o] + a.momentum * unb;
     }
   } else {
+    if ((threadIdx.x >> 5) != 0 || !valid) return;
     const long long o = (long long)g * a.gs_buf + c;
     mean = a.running_mean[o];
     var = a.running_var[o];
   }
+  const int i = g * a.C + c;
   const float rs = rsqrtf(var + a.eps);
   const long long po = (long long)g * a.gs_param + c;
   const float ga = a.gamma ? a.gamma[po] : 1.f, be = a.beta ? a.beta[po] : 0.f;
@@ -89,8 +101,7 @@ __global__ void bn_finalize_kernel(BNArgs a) {
 }
 
 DDL_API int ddl_bn_finalize(const BNArgs* a, hipStream_t s) {
-  const int n = a->G * a->C;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, s, *a);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((a->C + 31) / 32, a->G), dim3(256), 0, s, *a);
   return (int)hipGetLastError();
 }
 
@@ -392,25 +403,17 @@ DDL_API int ddl_bn_stats(const void* x, float* stats, long long M, int C, int G,
 // ---------------------------------------------------------------------------------------------
 // Whole BN backward in three launches: striped reduce -> per-channel fold (d(beta) += s0,
 // d(gamma) += s1, dx coefficients) -> one apply pass.
-__global__ void bn_fold_coef_kernel(const float* __restrict__ part, float* __restrict__ dgamma,
-                                    float* __restrict__ dbeta, long long gs_param,
-                                    const float* __restrict__ mean, const float* __restrict__ rstd,
-                                    const float* __restrict__ gamma, float* __restrict__ coef,
-                                    long long M, int C, int G) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= G * C) return;
-  const int g = i / C, c = i - g * C;
-  const float* pg = part + (long long)g * BN_NSTRIPE * 2 * C;
-  float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int k = 0; k < BN_NSTRIPE; k += 4) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      a0[u] += pg[(long long)(k + u) * 2 * C + c];
-      a1[u] += pg[(long long)(k + u) * 2 * C + C + c];
-    }
-  }
-  const float s0 = (a0[0] + a0[1]) + (a0[2] + a0[3]), s1 = (a1[0] + a1[1]) + (a1[2] + a1[3]);
+__global__ __launch_bounds__(256) void bn_fold_coef_kernel(
+    const float* __restrict__ part, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    long long gs_param, const float* __restrict__ mean, const float* __restrict__ rstd,
+    const float* __restrict__ gamma, float* __restrict__ coef, long long M, int C, int G) {
+  __shared__ float red[8 * 64];
+  const int g = blockIdx.y, c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const bool valid = c < C;
+  float s0, s1;
+  stripe_fold(part + (long long)g * BN_NSTRIPE * 2 * C, BN_NSTRIPE, C, c, valid, red, s0, s1);
+  if ((threadIdx.x >> 5) != 0 || !valid) return;
+  const int i = g * C + c;
   const long long po = (long long)g * gs_param + c;
   if (dbeta) dbeta[po] += s0;
   if (dgamma) dgamma[po] += s1;
@@ -434,7 +437,7 @@ DDL_API int ddl_bn_backward(const void* dy, const void* ymask, const void* x, co
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(stream_blocks(M, RPI, G, 16), G), dim3(256), 0, s,
                      (const bf16_t*)dy, (const bf16_t*)ymask, (const bf16_t*)x, mean, rstd, part,
                      M, C);
-  hipLaunchKernelGGL(bn_fold_coef_kernel, dim3((G * C + 255) / 256), dim3(256), 0, s, part, dgamma,
+  hipLaunchKernelGGL(bn_fold_coef_kernel, dim3((C + 31) / 32, G), dim3(256), 0, s, part, dgamma,
                      dbeta, gs_param, mean, rstd, gamma, coef, M, C, G);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_blocks(M, RPI, G, 4), G), dim3(256), 0, s,
                      (const bf16_t*)dy, (const bf16_t*)ymask, (const bf16_t*)x, coef, (bf16_t*)dx,
