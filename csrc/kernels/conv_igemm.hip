@@ -271,6 +271,26 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     }
   }
 
+  // WGRAD: per-lane output-pixel cursor (n, op, oq) of k-row kr, advanced by BK pixels per step
+  // with constant carries (no divisions in the loop)
+  int wn[MODE == MODE_WGRAD ? Q_PW : 1], wop[MODE == MODE_WGRAD ? Q_PW : 1],
+      woq[MODE == MODE_WGRAD ? Q_PW : 1];
+  int w_dn = 0, w_dp = 0, w_dq = 0;
+  if constexpr (MODE == MODE_WGRAD) {
+    const int pq = P * Q;
+    w_dn = BK / pq;
+    w_dp = (BK - w_dn * pq) / Q;
+    w_dq = BK - w_dn * pq - w_dp * Q;
+#pragma unroll
+    for (int i = 0; i < Q_PW; ++i) {
+      const int pix = kt0 * BK + q_base[i];
+      wn[i] = fdiv(pix, div_pq);
+      const int rem = pix - wn[i] * pq;
+      wop[i] = fdiv(rem, div_q);
+      woq[i] = rem - wop[i] * Q;
+    }
+  }
+
   // reduction cursor for FWD/DGRAD: tap (t_r, t_s) [jr, js = tap index within the phase],
   // channel run t_c; issue() is called for consecutive K-steps, so it advances without divisions
   const int CR = (MODE == MODE_FWD) ? C : K;  // contiguous reduction run per tap
@@ -330,15 +350,19 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
           }
         }
       } else {
-        const int pix = kg + q_base[i];
-        if (q_h[i] > -(1 << 27) && pix < Kr) {
-          const int n = fdiv(pix, div_pq), rem = pix - n * (P * Q);
-          const int op = fdiv(rem, div_q), oq = rem - op * Q;
-          const int sw = (int)(short)(q_w[i] & 0xffff), c = q_w[i] >> 16;
-          const int ih = op * st + q_h[i], iw = oq * st + sw;
-          if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
-            off = (unsigned)(((n * H + ih) * W + iw) * C + c) * 2u;
-        }
+        const int sw = (int)(short)(q_w[i] & 0xffff), c = q_w[i] >> 16;
+        const int ih = wop[i] * st + q_h[i], iw = woq[i] * st + sw;
+        const bool ok = (q_base[i] < Kr - kg) & ((unsigned)ih < (unsigned)H) &
+                        ((unsigned)iw < (unsigned)W);
+        off = ok ? (unsigned)(((wn[i] * H + ih) * W + iw) * C + c) * 2u : OOB;
+        // advance this lane's pixel by BK: (n, op, oq) += (w_dn, w_dp, w_dq) with carries
+        int oq = woq[i] + w_dq;
+        const int cq = oq >= Q;
+        woq[i] = cq ? oq - Q : oq;
+        int op = wop[i] + w_dp + cq;
+        const int cp = op >= P;
+        wop[i] = cp ? op - P : op;
+        wn[i] += w_dn + cp;
       }
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rQ, (__attribute__((address_space(3))) void*)(Qs + (wsc + 4 * i) * 1024), 16, off, 0, 0, 0);
