@@ -411,7 +411,9 @@ DDL_API int ddl_cast_bf16_f32(const void* x, float* y, long long n, hipStream_t 
 
 // ---------------------------------------------------------------------------------------------
 // general k x k / stride / pad max pool (ImageNet stem 3x3/2 p1); -inf padding like torch
-__global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int NB,
+// am (optional): window-local argmax r*k+s per output element (uint8), consumed by the backward
+__global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                   unsigned char* __restrict__ am, int NB,
                                    int H, int W, int C, int k, int st, int pd, int Ho, int Wo) {
   const int CC = C / 8;
   const long long total = (long long)NB * Ho * Wo * CC;
@@ -423,8 +425,9 @@ __global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restr
     const int ho = (int)(p % Ho);
     const int n = (int)(p / Ho);
     float m[8];
+    int ai[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
+    for (int e = 0; e < 8; ++e) { m[e] = -INFINITY; ai[e] = 0; }
     for (int r = 0; r < k; ++r) {
       const int ih = ho * st - pd + r;
       if ((unsigned)ih >= (unsigned)H) continue;
@@ -434,10 +437,50 @@ __global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restr
         float v[8];
         unpack8(*(const i4v*)(x + (((long long)n * H + ih) * W + iw) * C + cc * 8), v);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) m[e] = (v[e] > m[e] || v[e] != v[e]) ? v[e] : m[e];
+        for (int e = 0; e < 8; ++e)
+          if (v[e] > m[e] || (v[e] != v[e] && m[e] == m[e])) { m[e] = v[e]; ai[e] = r * k + s2; }
       }
     }
     *(i4v*)(y + t * 8) = pack8(m);
+    if (am) {
+      unsigned long long packed = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) packed |= (unsigned long long)(ai[e] & 0xff) << (8 * e);
+      *(unsigned long long*)(am + t * 8) = packed;
+    }
+  }
+}
+
+// backward from the saved argmax: each input pixel gathers dy of the (<= ceil(k/st)^2) windows
+// that contain it and chose it — one byte + one bf16 per window and channel, no recomputation
+__global__ void maxpool_bwd_am_kernel(const unsigned char* __restrict__ am,
+                                      const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx,
+                                      int NB, int H, int W, int C, int k, int st, int pd, int Ho,
+                                      int Wo) {
+  const int CC = C / 8;
+  const long long total = (long long)NB * H * W * CC;
+  GSTRIDE_LOOP(t, total) {
+    const int cc = (int)(t % CC);
+    long long p = t / CC;
+    const int iw0 = (int)(p % W);
+    p /= W;
+    const int ih0 = (int)(p % H);
+    const int n = (int)(p / H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int ho_lo = max(0, (ih0 + pd - k + st) / st), ho_hi = min(Ho - 1, (ih0 + pd) / st);
+    const int wo_lo = max(0, (iw0 + pd - k + st) / st), wo_hi = min(Wo - 1, (iw0 + pd) / st);
+    for (int ho = ho_lo; ho <= ho_hi; ++ho)
+      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+        const int local = (ih0 - (ho * st - pd)) * k + (iw0 - (wo * st - pd));
+        const long long o = (((long long)n * Ho + ho) * Wo + wo) * C + cc * 8;
+        const unsigned long long a8 = *(const unsigned long long*)(am + o);
+        float d[8];
+        unpack8(*(const i4v*)(dy + o), d);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if ((int)((a8 >> (8 * e)) & 0xff) == local) acc[e] += d[e];
+      }
+    *(i4v*)(dx + t * 8) = pack8(acc);
   }
 }
 // backward as a gather over the windows that contain each input pixel (no atomics): an input
@@ -485,20 +528,27 @@ __global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ x, const bf16_t* _
     *(i4v*)(dx + t * 8) = pack8(acc);
   }
 }
-DDL_API int ddl_maxpool_fwd(const void* x, void* y, int NB, int H, int W, int C, int k, int st,
-                            int pd, hipStream_t s) {
+DDL_API int ddl_maxpool_fwd(const void* x, void* y, void* am, int NB, int H, int W, int C, int k,
+                            int st, int pd, hipStream_t s) {
   if (C % 8) return (int)hipErrorInvalidValue;
   const int Ho = (H + 2 * pd - k) / st + 1, Wo = (W + 2 * pd - k) / st + 1;
   const long long total = (long long)NB * Ho * Wo * (C / 8);
+  if (k > 15) return (int)hipErrorInvalidValue;  // argmax index must fit a byte
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s,
-                     (const bf16_t*)x, (bf16_t*)y, NB, H, W, C, k, st, pd, Ho, Wo);
+                     (const bf16_t*)x, (bf16_t*)y, (unsigned char*)am, NB, H, W, C, k, st, pd, Ho, Wo);
   return (int)hipGetLastError();
 }
-DDL_API int ddl_maxpool_bwd(const void* x, const void* dy, void* dx, int NB, int H, int W, int C,
-                            int k, int st, int pd, hipStream_t s) {
+DDL_API int ddl_maxpool_bwd(const void* x, const void* dy, const void* am, void* dx, int NB, int H,
+                            int W, int C, int k, int st, int pd, hipStream_t s) {
   if (C % 8) return (int)hipErrorInvalidValue;
   const int Ho = (H + 2 * pd - k) / st + 1, Wo = (W + 2 * pd - k) / st + 1;
   const long long total = (long long)NB * H * W * (C / 8);
+  if (am) {
+    hipLaunchKernelGGL(maxpool_bwd_am_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s,
+                       (const unsigned char*)am, (const bf16_t*)dy, (bf16_t*)dx, NB, H, W, C, k, st,
+                       pd, Ho, Wo);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s,
                      (const bf16_t*)x, (const bf16_t*)dy, (bf16_t*)dx, NB, H, W, C, k, st, pd, Ho, Wo);
   return (int)hipGetLastError();

@@ -206,10 +206,14 @@ class MaxPool3s2(Layer):
     name = "maxpool3"
 
     def forward(self, x, train):
-        return Fn.maxpool_fwd(x, 3, 2, 1), x
+        if not train:
+            return Fn.maxpool_fwd(x, 3, 2, 1), None
+        y, am = Fn.maxpool_fwd(x, 3, 2, 1, want_argmax=True)
+        return y, (x, am)
 
-    def backward(self, dy, x):
-        return Fn.maxpool_bwd(x, dy, 3, 2, 1)
+    def backward(self, dy, ctx):
+        x, am = ctx
+        return Fn.maxpool_bwd(x, dy, 3, 2, 1, argmax=am)
 
     def out_shape(self, s):
         G, N, H, W, C = s

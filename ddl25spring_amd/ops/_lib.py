@@ -77,8 +77,8 @@ _SIGS = {
     # nn_ops.hip
     "ddl_prep_images": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
     "ddl_nchw_to_nhwc": [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
-    "ddl_maxpool_fwd": [vp, vp, i32, i32, i32, i32, i32, i32, i32, vp],
-    "ddl_maxpool_bwd": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp],
+    "ddl_maxpool_fwd": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp],
+    "ddl_maxpool_bwd": [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp],
     "ddl_maxpool2_fwd": [vp, vp, i32, i32, i32, i32, vp],
     "ddl_maxpool2_bwd": [vp, vp, vp, i32, i32, i32, i32, vp],
     "ddl_avgpool_fwd": [vp, vp, i32, i32, i32, vp],

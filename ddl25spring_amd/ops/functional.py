@@ -422,20 +422,23 @@ def prep_images(src_u8, idx, mean, inv_std, cpad, im2col=0, pad=0, stride=1, out
     return out
 
 
-def maxpool_fwd(x, k, stride, pad):
+def maxpool_fwd(x, k, stride, pad, want_argmax=False):
+    """-> y, or (y, argmax) with the window-local uint8 argmax that makes the backward a gather."""
     G, N, H, W, C = x.shape
     Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
     if not x.is_cuda:
         xi = x.float().reshape(G * N, H, W, C).permute(0, 3, 1, 2)
         y = torch.nn.functional.max_pool2d(xi, k, stride, pad)
-        return y.permute(0, 2, 3, 1).reshape(G, N, Ho, Wo, C).to(torch.bfloat16).contiguous()
+        y = y.permute(0, 2, 3, 1).reshape(G, N, Ho, Wo, C).to(torch.bfloat16).contiguous()
+        return (y, None) if want_argmax else y
     y = torch.empty(G, N, Ho, Wo, C, dtype=x.dtype, device=x.device)
-    check(_lib.kernels().ddl_maxpool_fwd(ptr(x), ptr(y), G * N, H, W, C, k, stride, pad, stream()),
-          "maxpool_fwd")
-    return y
+    am = torch.empty(G, N, Ho, Wo, C, dtype=torch.uint8, device=x.device) if want_argmax else None
+    check(_lib.kernels().ddl_maxpool_fwd(ptr(x), ptr(y), ptr(am), G * N, H, W, C, k, stride, pad,
+                                         stream()), "maxpool_fwd")
+    return (y, am) if want_argmax else y
 
 
-def maxpool_bwd(x, dy, k, stride, pad):
+def maxpool_bwd(x, dy, k, stride, pad, argmax=None):
     G, N, H, W, C = x.shape
     if not x.is_cuda:
         with torch.enable_grad():
@@ -445,8 +448,8 @@ def maxpool_bwd(x, dy, k, stride, pad):
             (dx,) = torch.autograd.grad(y, xi, g)
         return dx.permute(0, 2, 3, 1).reshape(G, N, H, W, C).to(torch.bfloat16).contiguous()
     dx = torch.empty_like(x)
-    check(_lib.kernels().ddl_maxpool_bwd(ptr(x), ptr(dy), ptr(dx), G * N, H, W, C, k, stride, pad,
-                                         stream()), "maxpool_bwd")
+    check(_lib.kernels().ddl_maxpool_bwd(ptr(x), ptr(dy), ptr(argmax), ptr(dx), G * N, H, W, C, k,
+                                         stride, pad, stream()), "maxpool_bwd")
     return dx
 
 

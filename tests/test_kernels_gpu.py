@@ -147,6 +147,16 @@ def test_pools_act_dropout(cuda):
     _close(Fn.maxpool2_fwd(x), ref.maxpool2_fwd(x.cpu()), rel=0, abs_=0)
     dy = _rand(2, 3, 4, 3, 64, dev=cuda)
     _close(Fn.maxpool2_bwd(x, dy), ref.maxpool2_bwd(x.cpu(), dy.cpu()), rel=0, abs_=0)
+    # general k/s/p max-pool (ResNet-50 3x3/2 pad 1): recompute and saved-argmax backward
+    for k_, s_, p_ in ((3, 2, 1), (2, 2, 0), (3, 1, 1)):
+        y = Fn.maxpool_fwd(x, k_, s_, p_)
+        y2, am = Fn.maxpool_fwd(x, k_, s_, p_, want_argmax=True)
+        _close(y, Fn.maxpool_fwd(x.cpu(), k_, s_, p_), rel=0, abs_=0)
+        assert torch.equal(y, y2)
+        dyp = _rand(*y.shape, dev=cuda)
+        want = Fn.maxpool_bwd(x.cpu(), dyp.cpu(), k_, s_, p_)
+        _close(Fn.maxpool_bwd(x, dyp, k_, s_, p_), want)
+        _close(Fn.maxpool_bwd(x, dyp, k_, s_, p_, argmax=am), want)
     _close(Fn.avgpool_fwd(x), ref.avgpool_fwd(x.cpu()))
     d2 = _rand(2, 3, 64, dev=cuda)
     _close(Fn.avgpool_bwd(d2, 8, 6), ref.avgpool_bwd(d2.cpu(), 8, 6))
