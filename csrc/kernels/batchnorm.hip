@@ -428,13 +428,15 @@ __global__ __launch_bounds__(256) void bn_fold_coef_kernel(
 }
 
 // part: zeroed [G][BN_NSTRIPE][2C]; coef: [G][3C] scratch
+// do_reduce = 0: `part` was already filled by the producer of dy (conv dgrad epilogue with the
+// fused BN reduce), so the backward is two launches.
 DDL_API int ddl_bn_backward(const void* dy, const void* ymask, const void* x, const float* mean,
                             const float* rstd, const float* gamma, long long gs_param, float* part,
                             float* coef, float* dgamma, float* dbeta, void* dx, void* dym_out,
-                            long long M, int C, int G, hipStream_t s) {
+                            long long M, int C, int G, int do_reduce, hipStream_t s) {
   if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
   const int RPI = 256 / (C / 8);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(stream_blocks(M, RPI, G, 16), G), dim3(256), 0, s,
+  if (do_reduce) hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(stream_blocks(M, RPI, G, 16), G), dim3(256), 0, s,
                      (const bf16_t*)dy, (const bf16_t*)ymask, (const bf16_t*)x, mean, rstd, part,
                      M, C);
   hipLaunchKernelGGL(bn_fold_coef_kernel, dim3((C + 31) / 32, G), dim3(256), 0, s, part, dgamma,

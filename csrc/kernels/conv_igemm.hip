@@ -47,7 +47,13 @@ struct ConvArgs {
   long long x_gs, w_gs, dy_gs, out_gs, bias_gs, stats_gs;
   int G, N, H, W, C, K, R, S, P, Q, stride, pad;
   int relu, accumulate, split_k;
-  int stats_stripes;     // FWD stats: q-tile t adds into stripe t % stripes of [stripes][2K] (<=1: one)
+  int stats_stripes;     // stats: q-tile t adds into stripe t % stripes of [stripes][2*Pd] (<=1: one)
+  // DGRAD fused BatchNorm-backward reduce (optional): with bn_x set, `stats` receives per channel
+  // (sum dy_m, sum dy_m * xhat) of the stored (masked, residual-added) output, xhat =
+  // (bn_x - bn_mean) * bn_rstd — the reduce pass of the preceding BN's backward.
+  const void* bn_x;      // BN input (the previous conv's output), same layout as out
+  const float* bn_mean;  // [G][C]
+  const float* bn_rstd;  // [G][C]
 };
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
@@ -476,16 +482,26 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     // striped accumulation: blocks of different pixel tiles hit different copies, so the fp32
     // atomics of thousands of blocks do not serialise on the same few cache lines
     float* stats = a.stats ? a.stats + (long long)g * a.stats_gs +
-                                 (a.stats_stripes > 1 ? (long long)((tile / ntp) % a.stats_stripes) * 2 * K : 0)
+                                 (a.stats_stripes > 1 ? (long long)((tile / ntp) % a.stats_stripes) * 2 * Pd : 0)
                            : nullptr;
+    const bf16_t* bnx = (MODE == MODE_DGRAD && a.bn_x) ? (const bf16_t*)a.bn_x + (long long)g * a.out_gs
+                                                        : nullptr;
+    const bool want_stats = stats && (MODE == MODE_FWD || bnx);
 #pragma unroll
     for (int ti = 0; ti < TP; ++ti) {
       const int p = p0 + wp * WP + ti * 16 + lp;
       float bsum[4] = {0.f, 0.f, 0.f, 0.f}, bsq[4] = {0.f, 0.f, 0.f, 0.f};
-      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      float bv[4] = {0.f, 0.f, 0.f, 0.f}, bmu[4] = {0.f, 0.f, 0.f, 0.f}, brs[4] = {0.f, 0.f, 0.f, 0.f};
       if (bias && p < Pd) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) bv[e] = bias[p + e];
+      }
+      if (bnx && p < Pd) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bmu[e] = a.bn_mean[(long long)g * Pd + p + e];
+          brs[e] = a.bn_rstd[(long long)g * Pd + p + e];
+        }
       }
 #pragma unroll
       for (int tj = 0; tj < TQ; ++tj) {
@@ -520,14 +536,25 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
           ov[0] = (int)pack_bf2(v[0], v[1]);
           ov[1] = (int)pack_bf2(v[2], v[3]);
           *(i2v*)(O + o) = ov;
+          if (bnx) {
+            const i2v xv = *(const i2v*)(bnx + o);
+            const float xs[4] = {lo_bf((uint32_t)xv[0]), hi_bf((uint32_t)xv[0]),
+                                 lo_bf((uint32_t)xv[1]), hi_bf((uint32_t)xv[1])};
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            bsum[e] += v[e];
-            bsq[e] += v[e] * v[e];
+            for (int e = 0; e < 4; ++e) {
+              bsum[e] += v[e];
+              bsq[e] += v[e] * ((xs[e] - bmu[e]) * brs[e]);
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              bsum[e] += v[e];
+              bsq[e] += v[e] * v[e];
+            }
           }
         }
       }
-      if (MODE == MODE_FWD && stats) {
+      if (want_stats) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float s = bsum[e], s2 = bsq[e];
@@ -543,7 +570,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             atomicAdd(stats + p + e, bsum[e]);
-            atomicAdd(stats + K + p + e, bsq[e]);
+            atomicAdd(stats + Pd + p + e, bsq[e]);
           }
         }
       }

@@ -40,10 +40,10 @@ class _BNConv(ConvUnit):
                                         self.eps, self.momentum, training=train)
         return c, sc, sh, mu, rs, g
 
-    def bn_backward(self, dy, ymask, c, mu, rs, emit_dym=False):
+    def bn_backward(self, dy, ymask, c, mu, rs, emit_dym=False, part=None):
         st = self.store
         return Fn.bn_backward(dy, ymask, c, mu, rs, st.param(self.gamma), st.grad_of(self.gamma),
-                              st.grad_of(self.beta), emit_dym=emit_dym)
+                              st.grad_of(self.beta), emit_dym=emit_dym, part=part)
 
 
 class BasicBlock(Layer):
@@ -99,8 +99,9 @@ class BasicBlock(Layer):
         else:
             dres = dym
         Fn.conv_wgrad(dc2, a1, g2, st.grad_of(self.conv2.w))
-        da1 = Fn.conv_dgrad(dc2, st.shadow_of(self.conv2.w), g2)
-        dc1 = self.conv1.bn_backward(da1, a1, c1, mu1, rs1)
+        # dgrad epilogue applies bn1's ReLU mask and reduces bn1's backward sums (no reduce pass)
+        da1, part1 = Fn.conv_dgrad(dc2, st.shadow_of(self.conv2.w), g2, mask=a1, bn=(c1, mu1, rs1))
+        dc1 = self.conv1.bn_backward(da1, None, c1, mu1, rs1, part=part1)
         Fn.conv_wgrad(dc1, x, g1, st.grad_of(self.conv1.w))
         if not self.needs_input_grad:
             return None
@@ -176,11 +177,11 @@ class Bottleneck(Layer):
         else:
             dres = dym
         Fn.conv_wgrad(dc3, a2, g3, st.grad_of(self.conv3.w))
-        da2 = Fn.conv_dgrad(dc3, st.shadow_of(self.conv3.w), g3)
-        dc2 = self.conv2.bn_backward(da2, a2, c2, mu2, rs2)
+        da2, part2 = Fn.conv_dgrad(dc3, st.shadow_of(self.conv3.w), g3, mask=a2, bn=(c2, mu2, rs2))
+        dc2 = self.conv2.bn_backward(da2, None, c2, mu2, rs2, part=part2)
         Fn.conv_wgrad(dc2, a1, g2, st.grad_of(self.conv2.w))
-        da1 = Fn.conv_dgrad(dc2, st.shadow_of(self.conv2.w), g2)
-        dc1 = self.conv1.bn_backward(da1, a1, c1, mu1, rs1)
+        da1, part1 = Fn.conv_dgrad(dc2, st.shadow_of(self.conv2.w), g2, mask=a1, bn=(c1, mu1, rs1))
+        dc1 = self.conv1.bn_backward(da1, None, c1, mu1, rs1, part=part1)
         Fn.conv_wgrad(dc1, x, g1, st.grad_of(self.conv1.w))
         if not self.needs_input_grad:
             return None

@@ -39,7 +39,8 @@ class ConvArgs(ctypes.Structure):
                 ("stats_gs", i64),
                 ("G", i32), ("N", i32), ("H", i32), ("W", i32), ("C", i32), ("K", i32), ("R", i32),
                 ("S", i32), ("P", i32), ("Q", i32), ("stride", i32), ("pad", i32),
-                ("relu", i32), ("accumulate", i32), ("split_k", i32), ("stats_stripes", i32)]
+                ("relu", i32), ("accumulate", i32), ("split_k", i32), ("stats_stripes", i32),
+                ("bn_x", vp), ("bn_mean", vp), ("bn_rstd", vp)]
 
 
 class BNArgs(ctypes.Structure):
@@ -73,7 +74,7 @@ _SIGS = {
     "ddl_bn_bwd_reduce": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i32, i32, vp],
     "ddl_bn_bwd_apply": [vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, i64, i32, i32, vp],
     "ddl_bn_stats": [vp, vp, i64, i32, i32, vp],
-    "ddl_bn_backward": [vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp],
+    "ddl_bn_backward": [vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, vp],
     # nn_ops.hip
     "ddl_prep_images": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
     "ddl_nchw_to_nhwc": [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],

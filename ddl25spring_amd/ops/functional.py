@@ -125,14 +125,26 @@ def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out=None, 
     return y
 
 
-def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0):
-    """dx[G,N,H,W,C] = conv_transpose(dy, w) (+residual) * (mask > 0)."""
+def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0, bn=None):
+    """dx[G,N,H,W,C] = conv_transpose(dy, w) (+residual) * (mask > 0).
+
+    bn = (x, mean, rstd): also reduce, in the epilogue, the preceding BatchNorm's backward sums
+    (sum dx, sum dx * (x - mean) * rstd) into a striped [G, BN_STRIPES, 2, C] buffer; returns
+    (dx, part) for ``bn_backward(..., part=part)``."""
     if not dy.is_cuda:
         dx = ref.conv_dgrad(dy, w, geom, residual, mask)
         if out is not None:
             out.copy_(dx)
-            return out
-        return dx
+            dx = out
+        if bn is None:
+            return dx
+        x, mean, rstd = bn
+        part = torch.zeros(geom.G, BN_STRIPES, 2, geom.C)
+        d = dx.float().reshape(geom.G, -1, geom.C)
+        xh = (x.float().reshape(geom.G, -1, geom.C) - mean[:, None]) * rstd[:, None]
+        part[:, 0, 0] = d.sum(1)
+        part[:, 0, 1] = (d * xh).sum(1)
+        return dx, part
     _check_inner(dy, "dy"); _check_inner(w, "w")
     dx = out if out is not None else torch.empty(geom.G, geom.N, geom.H, geom.W, geom.C,
                                                  dtype=torch.bfloat16, device=dy.device)
@@ -140,10 +152,18 @@ def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0)
         residual = residual.contiguous()
     if mask is not None and mask.stride(0) != dx.stride(0):
         mask = mask.contiguous()
+    part = None
+    kw = {}
+    if bn is not None:
+        x, mean, rstd = bn
+        assert x.is_contiguous() and x.stride(0) == dx.stride(0) and mean.is_contiguous() and rstd.is_contiguous()
+        part = ws.zeros((geom.G, BN_STRIPES, 2, geom.C), dy.device)
+        kw = dict(stats=ptr(part), stats_gs=part.stride(0), stats_stripes=BN_STRIPES, bn_x=ptr(x),
+                  bn_mean=ptr(mean), bn_rstd=ptr(rstd))
     a = _conv_args(geom, dy.device, w=ptr(w), dy=ptr(dy), out=ptr(dx), residual=ptr(residual),
-                   mask=ptr(mask), w_gs=_gs(w), dy_gs=_gs(dy), out_gs=_gs(dx))
+                   mask=ptr(mask), w_gs=_gs(w), dy_gs=_gs(dy), out_gs=_gs(dx), **kw)
     check(_lib.kernels().ddl_conv_dgrad(ctypes.byref(a), cfg, stream()), "conv_dgrad")
-    return dx
+    return dx if bn is None else (dx, part)
 
 
 def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0):
@@ -227,14 +247,26 @@ def bn_bwd_reduce(dy, ymask, x, mean, rstd, dgamma=None, dbeta=None):
     return sums
 
 
-def bn_backward(dy, ymask, x, mean, rstd, gamma, dgamma=None, dbeta=None, emit_dym=False):
+def bn_backward(dy, ymask, x, mean, rstd, gamma, dgamma=None, dbeta=None, emit_dym=False,
+                part=None):
     """Whole BN backward (= bn_bwd_reduce + bn_bwd_apply) in three launches; accumulates
-    d(gamma), d(beta) into the given [G, C] views. -> dx (, dy_m if emit_dym)."""
+    d(gamma), d(beta) into the given [G, C] views. -> dx (, dy_m if emit_dym).
+    ``part``: the striped reduce sums already produced by dy's producer (``conv_dgrad(bn=...)``,
+    which also applied the mask) — the reduce pass is skipped (two launches)."""
     if not dy.is_cuda:
-        sums = ref.bn_bwd_reduce(dy, ymask, x, mean, rstd, dgamma, dbeta)
+        if part is not None:
+            sums = part.sum(1)
+            if dbeta is not None:
+                dbeta += sums[:, 0]
+            if dgamma is not None:
+                dgamma += sums[:, 1]
+        else:
+            sums = ref.bn_bwd_reduce(dy, ymask, x, mean, rstd, dgamma, dbeta)
         return ref.bn_bwd_apply(dy, ymask, x, mean, rstd, gamma, sums, emit_dym)
     G, C = x.shape[0], x.shape[-1]
-    part = ws.zeros((G, BN_STRIPES, 2, C), x.device)
+    do_reduce = part is None
+    if part is None:
+        part = ws.zeros((G, BN_STRIPES, 2, C), x.device)
     coef = ws.scratch((G, 3, C), x.device)
     dx = torch.empty_like(x)
     dym = torch.empty_like(x) if emit_dym else None
@@ -246,7 +278,7 @@ def bn_backward(dy, ymask, x, mean, rstd, gamma, dgamma=None, dbeta=None, emit_d
     check(_lib.kernels().ddl_bn_backward(ptr(dy), ptr(ymask), ptr(x), ptr(mean), ptr(rstd),
                                          ptr(gamma), gs, ptr(part), ptr(coef), ptr(dgamma),
                                          ptr(dbeta), ptr(dx), ptr(dym), x[0].numel() // C, C, G,
-                                         stream()), "bn_backward")
+                                         int(do_reduce), stream()), "bn_backward")
     return (dx, dym) if emit_dym else dx
 
 

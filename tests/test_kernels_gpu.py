@@ -249,3 +249,31 @@ def test_prep_images(cuda):
         _close(a, b, rel=1e-2)
     x = torch.randn(4, 1, 28, 28)
     _close(Fn.nchw_to_nhwc(x.to(cuda), 32, True, 0), Fn.nchw_to_nhwc(x, 32, True, 0))
+
+
+@pytest.mark.parametrize("geom", [ConvGeom(G=2, N=3, H=8, W=8, C=64, K=96, R=3, S=3, stride=1, pad=1),
+                                  ConvGeom(G=1, N=2, H=9, W=7, C=128, K=64, R=3, S=3, stride=2, pad=1)])
+def test_conv_dgrad_fused_bn_reduce(cuda, geom):
+    """dgrad epilogue = mask + the preceding BN's backward reduce; bn_backward(part=) then matches
+    the unfused three-launch backward."""
+    g = geom
+    dy = _rand(g.G, g.N, g.P, g.Q, g.K, dev=cuda)
+    w = _weights(g, cuda)
+    xbn = _rand(g.G, g.N, g.H, g.W, g.C, dev=cuda, scale=2.0) + 0.3
+    ymask = _rand(g.G, g.N, g.H, g.W, g.C, dev=cuda)
+    mean = torch.randn(g.G, g.C, device=cuda) * 0.2 + 0.3
+    rstd = torch.rand(g.G, g.C, device=cuda) + 0.5
+    gamma = torch.rand(g.G, g.C, device=cuda) + 0.5
+    dxm, part = Fn.conv_dgrad(dy, w, g, mask=ymask, bn=(xbn, mean, rstd))
+    plain = Fn.conv_dgrad(dy, w, g, mask=ymask)
+    assert torch.equal(dxm, plain)
+    d = plain.float().reshape(g.G, -1, g.C)
+    xh = (xbn.float().reshape(g.G, -1, g.C) - mean[:, None]) * rstd[:, None]
+    _close(part.sum(1)[:, 0], d.sum(1), rel=2e-2)
+    _close(part.sum(1)[:, 1], (d * xh).sum(1), rel=2e-2)
+    dg1, db1 = torch.zeros(g.G, g.C, device=cuda), torch.zeros(g.G, g.C, device=cuda)
+    dg2, db2 = torch.zeros(g.G, g.C, device=cuda), torch.zeros(g.G, g.C, device=cuda)
+    fused = Fn.bn_backward(dxm, None, xbn, mean, rstd, gamma, dg1, db1, part=part)
+    unfused = Fn.bn_backward(plain, None, xbn, mean, rstd, gamma, dg2, db2)
+    _close(fused, unfused, rel=2e-2)
+    _close(dg1, dg2, rel=2e-2); _close(db1, db2, rel=2e-2)
