@@ -40,10 +40,13 @@ def main():
     ap.add_argument("--model", default="resnet18")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--eval", action="store_true", help="also report test accuracy (untimed)")
+    ap.add_argument("--backend", default=None,
+                    help="collective backend (default: nccl = RCCL on GPUs); gloo lets several "
+                         "ranks share one GPU for a functional rehearsal")
     args = ap.parse_args()
 
     from ddl25spring_amd.runtime import dist as rdist
-    ctx = rdist.init()
+    ctx = rdist.init(backend=args.backend)
     if ctx.device.type != "cuda":
         print("bench.py needs a GPU", file=sys.stderr)
     from ddl25spring_amd.data.images import DeviceImageDataset, synthetic_images

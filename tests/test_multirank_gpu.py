@@ -1,0 +1,62 @@
+"""Multi-rank FL on the device: 2 ranks share the one GPU of the test box over gloo (RCCL needs one
+GPU per rank; the 8-GPU RCCL run is the driver's), exercising slot assignment, device-tensor
+collectives and the replicated server state exactly as the 8-GPU bench does."""
+import os
+import subprocess
+import sys
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from ddl25spring_amd.data.images import DeviceImageDataset, synthetic_images
+from ddl25spring_amd.data.split import split
+from ddl25spring_amd.fl.algorithms import FedAvg
+from ddl25spring_amd.models import mnist_mlp
+from ddl25spring_amd.runtime.dist import DistContext
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from ddl25spring_amd.runtime import dist as rdist
+    ctx = rdist.init(backend="gloo", device="cuda")
+    arr = synthetic_images("mnist", 800, seed=0)
+    parts = split(4, True, 1, labels=arr.labels)
+    fa = FedAvg(mnist_mlp, DeviceImageDataset(arr, ctx.device), parts, lr=0.05, batch_size=50,
+                client_fraction=1.0, seed=1, ctx=ctx, eval_every=0)
+    fa.round()
+    fa.round()
+    torch.save(fa.w_global.cpu(), os.path.join(out, f"w{rank}.pt"))
+    rdist.shutdown()
+
+
+def test_two_ranks_one_gpu_match_single_process(cuda):
+    arr = synthetic_images("mnist", 800, seed=0)
+    parts = split(4, True, 1, labels=arr.labels)
+    single = FedAvg(mnist_mlp, DeviceImageDataset(arr, cuda), parts, lr=0.05, batch_size=50,
+                    client_fraction=1.0, seed=1, ctx=DistContext(device=cuda), eval_every=0)
+    w0 = single.w_global.clone()
+    single.round()
+    single.round()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(2, 29733, d), nprocs=2, join=True)
+        ws = [torch.load(os.path.join(d, f"w{r}.pt"), weights_only=True) for r in range(2)]
+    assert torch.equal(ws[0], ws[1])  # replicated server state
+    upd = (single.w_global - w0).norm()
+    assert ((ws[0].to(cuda) - single.w_global).norm() / upd).item() < 2e-2
+
+
+def test_bench_two_ranks_gloo(cuda):
+    """bench.py end to end with world 2 (the driver's torchrun path, gloo instead of RCCL)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", "29741", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "1", "--warmup", "1", "--backend", "gloo", "--train-size", "8000"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and '"n_gpus": 2' in lines[0], out.stdout[-2000:]
