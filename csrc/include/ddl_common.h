@@ -14,6 +14,18 @@
 
 #define DDL_API extern "C" __attribute__((visibility("default")))
 
+// Host helper: 1-D grid for a grid-stride loop over `work` items (capped: waves re-use blocks).
+static inline int grid_for(long long work, int block, int cap = 8192) {
+  long long b = (work + block - 1) / block;
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+#define GSTRIDE_LOOP(t, total) \
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < (total); \
+       t += (long long)gridDim.x * blockDim.x)
+
+
 typedef uint16_t bf16_t;
 typedef short s8v __attribute__((ext_vector_type(8)));   // 8 x bf16 MFMA operand (4 VGPRs)
 typedef short s4v __attribute__((ext_vector_type(4)));   // 4 x bf16

@@ -13,13 +13,6 @@
 //                        in-register bitonic sort per coordinate (Yin et al. 2018) [north-star].
 #include "ddl_common.h"
 
-static int grid_for(long long work, int block, int cap = 8192) {
-  long long b = (work + block - 1) / block;
-  if (b > cap) b = cap;
-  if (b < 1) b = 1;
-  return (int)b;
-}
-
 __global__ void weighted_sum_kernel(const float* __restrict__ src, long long ld,
                                     const float* __restrict__ coeff, int G, long long n,
                                     float* __restrict__ out, int accumulate) {

@@ -13,13 +13,6 @@
 // model's FLOPs); the projections / FFN / LM head run on the MFMA implicit-GEMM kernel.
 #include "ddl_common.h"
 
-static int grid_for(long long work, int block, int cap = 8192) {
-  long long b = (work + block - 1) / block;
-  if (b > cap) b = cap;
-  if (b < 1) b = 1;
-  return (int)b;
-}
-
 // ---------------------------------------------------------------------------------------------
 __global__ void embedding_fwd_kernel(const int* __restrict__ idx, const float* __restrict__ w,
                                      bf16_t* __restrict__ y, int T, int D) {

@@ -16,16 +16,6 @@
 // (reference lab/tutorial_1a/hfl_complete.py:50-62) and transforms.Normalize (:19-24).
 #include "ddl_common.h"
 
-static int grid_for(long long work, int block) {
-  long long b = (work + block - 1) / block;
-  if (b > 8192) b = 8192;
-  if (b < 1) b = 1;
-  return (int)b;
-}
-#define GSTRIDE_LOOP(t, total) \
-  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < (total); \
-       t += (long long)gridDim.x * blockDim.x)
-
 // ---------------------------------------------------------------------------------------------
 // src: uint8 [num_samples][Hs][Ws][Cs]; idx: int32 [G*B] sample ids (row-major over g,b)
 // im2col=0: out [G*B][Hs][Ws][Cout], channel c<Cs normalised, c>=Cs zero

@@ -6,13 +6,6 @@
 // vfl.py:50 AdamW; generative-modeling.py:154 Adam).
 #include "ddl_common.h"
 
-static int grid_for(long long work, int block) {
-  long long b = (work + block - 1) / block;
-  if (b > 8192) b = 8192;
-  if (b < 1) b = 1;
-  return (int)b;
-}
-
 struct SGDArgs {
   float* p; const float* g; float* mom; bf16_t* shadow;
   long long n;

@@ -1,9 +1,11 @@
 """Tabular models of the generative-modelling and vertical-FL labs (fp32, exact reference numerics).
 
-These nets are a few thousand parameters on <= 1,025 rows; they run as plain fp32 ``nn.Module``s
-(device-agnostic) so accuracy / loss parity with the reference is exact in distribution. Their
-optimizers can be the fused flat HIP ``FlatAdamW`` (``ddl25spring_amd.optim.FlatAdam``) and, in the
-vertical-FL runtime, their activations/gradients cross GPUs over RCCL (``ddl25spring_amd.vfl``).
+These nets are a few thousand parameters on <= 1,025 rows, trained in exact fp32 like the
+reference. On the device every layer is a fused HIP kernel of csrc/kernels/tabular.hip (linear +
+bias + activation on fp32 MFMA, BatchNorm1d + activation, soft-target CE, MSE+KL, Philox
+reparameterisation — ``ops/tabular_ops.py``); on the CPU the same modules run the identical torch
+composition. Their optimizers can be the fused flat ``optim.FlatAdam`` and, in the vertical-FL
+runtime, their cut-layer tensors cross GPUs over RCCL (``ddl25spring_amd.vfl``).
 
 * ``HeartDiseaseNN``      — lab/tutorial_2a/centralized.py:13-28
 * ``Autoencoder``+``customLoss`` — lab/tutorial_2a/generative-modeling.py:13-130 (tabular VAE;
@@ -21,35 +23,67 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import tabular_ops as TO
+
+
+class FLinear(nn.Linear):
+    """nn.Linear with a fused activation ('none' | 'relu' | 'leaky_relu'); one kernel on device."""
+
+    def __init__(self, in_features, out_features, act="none", slope=0.01, bias=True):
+        super().__init__(in_features, out_features, bias=bias)
+        self.act_kind, self.slope = act, slope
+
+    def forward(self, x):
+        return TO.linear_act(x, self.weight, self.bias, self.act_kind, self.slope)
+
+
+class FBatchNorm1d(nn.BatchNorm1d):
+    """nn.BatchNorm1d (batch statistics in training, running statistics in eval) + fused act."""
+
+    def __init__(self, num_features, act="none", slope=0.01):
+        super().__init__(num_features)
+        self.act_kind, self.slope = act, slope
+
+    def forward(self, x):
+        if self.training:
+            self.num_batches_tracked.add_(1)
+        return TO.batch_norm1d_act(x, self.weight, self.bias, self.running_mean, self.running_var,
+                                   self.training, self.momentum, self.eps, self.act_kind, self.slope)
+
+
+class SoftCrossEntropy(nn.Module):
+    """nn.CrossEntropyLoss (mean; hard labels or probability targets), fused on device."""
+
+    def forward(self, logits, target):
+        return TO.cross_entropy(logits, target)
+
 
 def _mlp_bn(dims, final_act=True):
     layers = []
     for i, (a, b) in enumerate(zip(dims[:-1], dims[1:])):
-        layers += [nn.Linear(a, b), nn.BatchNorm1d(b)]
-        if final_act or i < len(dims) - 2:
-            layers.append(nn.ReLU())
+        act = "relu" if (final_act or i < len(dims) - 2) else "none"
+        layers += [FLinear(a, b), FBatchNorm1d(b, act)]
     return nn.Sequential(*layers)
 
 
 class HeartDiseaseNN(nn.Module):
     def __init__(self, in_features: int = 30):
         super().__init__()
-        self.fc1, self.fc2 = nn.Linear(in_features, 64), nn.Linear(64, 128)
-        self.fc3, self.fc4 = nn.Linear(128, 256), nn.Linear(256, 2)
-        self.act, self.dropout = nn.LeakyReLU(), nn.Dropout(0.1)
+        self.fc1 = FLinear(in_features, 64, "leaky_relu")
+        self.fc2 = FLinear(64, 128, "leaky_relu")
+        self.fc3 = FLinear(128, 256, "leaky_relu")
+        self.fc4 = FLinear(256, 2)
+        self.dropout = nn.Dropout(0.1)
 
     def forward(self, x):
-        x = self.act(self.fc1(x))
-        x = self.act(self.fc2(x))
-        x = self.dropout(self.act(self.fc3(x)))
-        return self.fc4(x)
+        return self.fc4(self.dropout(self.fc3(self.fc2(self.fc1(x)))))
 
 
 def train_centralized(net, Xtr, ytr, Xte, yte, epochs: int = 49, optimizer=None):
     """Full-batch training keeping a DEEP copy of the best-test-accuracy weights (fixes the
     reference's aliasing ``best_params = net.state_dict()``, centralized.py:51,69-70 / SURVEY Q9)."""
     opt = optimizer or torch.optim.AdamW(net.parameters())
-    crit = nn.CrossEntropyLoss()
+    crit = SoftCrossEntropy()
     best, best_sd, hist = -1.0, None, []
     for _ in range(1, epochs + 1):
         net.train()
@@ -74,9 +108,9 @@ class Autoencoder(nn.Module):
     def __init__(self, D_in, H=50, H2=12, latent_dim=3):
         super().__init__()
         self.enc = _mlp_bn([D_in, H, H2, H2, latent_dim])
-        self.fc21, self.fc22 = nn.Linear(latent_dim, latent_dim), nn.Linear(latent_dim, latent_dim)
+        self.fc21, self.fc22 = FLinear(latent_dim, latent_dim), FLinear(latent_dim, latent_dim)
         self.dec = nn.Sequential(_mlp_bn([latent_dim, latent_dim, H2, H2, H]),
-                                 nn.Linear(H, D_in), nn.BatchNorm1d(D_in))
+                                 FLinear(H, D_in), FBatchNorm1d(D_in))
         self.optimizer = self.criterion = None
 
     def encode(self, x):
@@ -85,7 +119,7 @@ class Autoencoder(nn.Module):
 
     def reparameterize(self, mu, logvar):
         if self.training:
-            return mu + torch.randn_like(mu) * torch.exp(0.5 * logvar)
+            return TO.reparameterize(mu, logvar)
         return mu
 
     def decode(self, z):
@@ -140,12 +174,10 @@ class Autoencoder(nn.Module):
 
 
 class customLoss(nn.Module):  # noqa: N801 - reference name
-    def __init__(self):
-        super().__init__()
-        self.mse = nn.MSELoss(reduction="sum")
+    """MSE(sum) + KL — one fused reduction with its gradients on the device."""
 
     def forward(self, x_recon, x, mu, logvar):
-        return self.mse(x_recon, x) - 0.5 * torch.sum(1 + logvar - mu.pow(2) - logvar.exp())
+        return TO.mse_kl(x_recon, x, mu, logvar)
 
 
 # ----------------------------------------------------------------------------------- split-NN
@@ -153,11 +185,12 @@ class BottomModel(nn.Module):
     def __init__(self, in_feat, out_feat):
         super().__init__()
         self.local_out_dim = out_feat
-        self.fc1, self.fc2 = nn.Linear(in_feat, out_feat), nn.Linear(out_feat, out_feat)
+        self.fc1 = FLinear(in_feat, out_feat, "relu")
+        self.fc2 = FLinear(out_feat, out_feat, "relu")
         self.dropout = nn.Dropout(0.1)
 
     def forward(self, x):
-        return self.dropout(F.relu(self.fc2(F.relu(self.fc1(x)))))
+        return self.dropout(self.fc2(self.fc1(x)))
 
 
 class TopModel(nn.Module):
@@ -167,12 +200,14 @@ class TopModel(nn.Module):
     def __init__(self, local_models, n_outs=2):
         super().__init__()
         self.in_size = sum(m.local_out_dim for m in local_models)
-        self.fc1, self.fc2, self.fc3 = nn.Linear(self.in_size, 128), nn.Linear(128, 256), nn.Linear(256, n_outs)
-        self.act, self.dropout = nn.LeakyReLU(), nn.Dropout(0.1)
+        self.fc1 = FLinear(self.in_size, 128, "leaky_relu")
+        self.fc2 = FLinear(128, 256, "leaky_relu")
+        self.fc3 = FLinear(256, n_outs, "leaky_relu")
+        self.dropout = nn.Dropout(0.1)
 
     def forward(self, xs):
         x = torch.cat(xs, 1) if isinstance(xs, (list, tuple)) else xs
-        return self.dropout(self.act(self.fc3(self.act(self.fc2(self.act(self.fc1(x)))))))
+        return self.dropout(self.fc3(self.fc2(self.fc1(x))))
 
 
 class VFLNetwork(nn.Module):
@@ -194,7 +229,7 @@ class VFLNetwork(nn.Module):
             self.bottom_models = nn.ModuleList(local_models)
         self.top_model = TopModel(local_models, n_outs)
         self.optimizer = torch.optim.AdamW(self.parameters(), lr=lr)
-        self.criterion = nn.CrossEntropyLoss()
+        self.criterion = SoftCrossEntropy()
         self.num_cli = self.cli_features = None
 
     def forward(self, xs):
@@ -264,7 +299,7 @@ class ClientDecoder(nn.Module):
     def __init__(self, latent_dim, output_dim):
         super().__init__()
         self.net = nn.Sequential(_mlp_bn([latent_dim, latent_dim, 32, 48]),
-                                 nn.Linear(48, output_dim), nn.BatchNorm1d(output_dim))
+                                 FLinear(48, output_dim), FBatchNorm1d(output_dim))
 
     def forward(self, z):
         return self.net(z)
@@ -274,9 +309,9 @@ class ServerVAE(nn.Module):
     def __init__(self, D_in, H=48, H2=32, latent_dim=16):
         super().__init__()
         self.enc = _mlp_bn([D_in, H, H2, H2, latent_dim])
-        self.fc21, self.fc22 = nn.Linear(latent_dim, latent_dim), nn.Linear(latent_dim, latent_dim)
+        self.fc21, self.fc22 = FLinear(latent_dim, latent_dim), FLinear(latent_dim, latent_dim)
         self.dec = nn.Sequential(_mlp_bn([latent_dim, latent_dim, H2, H2, H]),
-                                 nn.Linear(H, D_in), nn.BatchNorm1d(D_in))
+                                 FLinear(H, D_in), FBatchNorm1d(D_in))
 
     def encode(self, x):
         h = self.enc(x)
@@ -284,7 +319,7 @@ class ServerVAE(nn.Module):
 
     def reparameterize(self, mu, logvar):
         if self.training:
-            return mu + torch.randn_like(mu) * torch.exp(0.5 * logvar)
+            return TO.reparameterize(mu, logvar)
         return mu
 
     def decode(self, z):
@@ -312,6 +347,5 @@ class VFLVAE(nn.Module):
 
 
 def combined_loss(x_clients, recon_clients, concat_latent, recon_concat, mu, logvar):
-    mse = nn.MSELoss(reduction="sum")
-    client = sum(mse(r, x) for x, r in zip(x_clients, recon_clients))
-    return client + mse(recon_concat, concat_latent) - 0.5 * torch.sum(1 + logvar - mu.pow(2) - logvar.exp())
+    client = sum(F.mse_loss(r, x, reduction="sum") for x, r in zip(x_clients, recon_clients))
+    return client + TO.mse_kl(recon_concat, concat_latent, mu, logvar)

@@ -22,6 +22,8 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from ..ops import tabular_ops as TO
+
 
 def _exchange(sends, recvs, group=None):
     ops = [dist.P2POp(dist.isend, t, peer, group) for t, peer in sends]
@@ -167,7 +169,7 @@ class VAEServer:
         _exchange([(s.detach().contiguous(), p) for s, p in zip(slices, self.parties)],
                   [(g, p) for g, p in zip(grads, self.parties)] +
                   [(c, p) for c, p in zip(closs, self.parties)], self.group)
-        sloss = self.mse(recon, lat) - 0.5 * torch.sum(1 + logvar - mu.pow(2) - logvar.exp())
+        sloss = TO.mse_kl(recon, lat, mu, logvar)
         surrogate = sloss + (recon * torch.cat(grads, 1)).sum()
         surrogate.backward()
         self.opt.step()
