@@ -28,7 +28,10 @@
 //     X in WGRAD).
 // Both swizzles are bank-conflict-free for the fragment reads.
 // Workgroup = 4 waves (2x2) on a BP x BQ tile; blockIdx.z = client group, blockIdx.y = split-K
-// slice (WGRAD), blockIdx.x = tile id remapped XCD-aware.
+// slice x stride-2 DGRAD phase, blockIdx.x = tile id remapped XCD-aware.
+// Split-K: WGRAD adds fp32 partials atomically into the zeroed gradient; FWD / DGRAD (grids too
+// small to fill the CUs: one client, deep layers) store per-split fp32 slices and a streaming
+// epilogue kernel sums them and applies the fused epilogue (BN statistics / BN backward reduce).
 //
 // Reference parity: replaces the stock nn.Conv2d / nn.Linear of MnistCnn
 // (reference lab/tutorial_1a/hfl_complete.py:43-61) and the ResNets of the north-star configs.
@@ -54,6 +57,10 @@ struct ConvArgs {
   const void* bn_x;      // BN input (the previous conv's output), same layout as out
   const float* bn_mean;  // [G][C]
   const float* bn_rstd;  // [G][C]
+  // FWD / DGRAD split-K (small grids): with split_k > 1 the kernel stores raw fp32 partial sums
+  // to partial[split][G][rows][Pd] and conv_splitk_epilogue applies the epilogue above.
+  float* partial;
+  long long partial_cap;  // floats available at `partial` (0: no split-K for FWD / DGRAD)
 };
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
@@ -160,8 +167,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   int ph_a = 0, ph_b = 0, Hs = H, Ws = W, r0 = 0, s0 = 0, tstep = 1, Rn = R, Sn = S;
   constexpr bool PHASED_MODE = (MODE == MODE_DGRAD);
   const bool phased = PHASED_MODE && st == 2;
+  const int nph = phased ? 4 : 1;
   if (phased) {
-    ph_a = blockIdx.y >> 1;
+    ph_a = (blockIdx.y >> 1) & 1;
     ph_b = blockIdx.y & 1;
     Hs = (H - ph_a + 1) >> 1;
     Ws = (W - ph_b + 1) >> 1;
@@ -178,7 +186,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int p0 = (tile % ntp) * BP, q0 = (tile / ntp) * BQ;
   if (q0 >= Qd) return;  // smaller phases of a phased launch
-  const int nsplit = PHASED_MODE ? 1 : gridDim.y, split = PHASED_MODE ? 0 : blockIdx.y;
+  const int nsplit = gridDim.y / nph, split = blockIdx.y / nph;
   const int nk_total = (Kr + BK - 1) / BK;
   const int per = (nk_total + nsplit - 1) / nsplit;
   const int kt0 = split * per;
@@ -474,6 +482,28 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   // ---------------- epilogue ----------------
   const int lq = lane & 15, lp = 4 * (lane >> 4);
   if constexpr (MODE == MODE_FWD || MODE == MODE_DGRAD) {
+    if (nsplit > 1) {  // raw fp32 partial slice [split][g][rows][Pd]; conv_splitk_epilogue finishes
+      const long long rows = MODE == MODE_FWD ? (long long)a.N * P * Q : (long long)a.N * H * W;
+      float* PO = a.partial + ((long long)split * a.G + g) * rows * Pd;
+#pragma unroll
+      for (int ti = 0; ti < TP; ++ti) {
+        const int p = p0 + wp * WP + ti * 16 + lp;
+#pragma unroll
+        for (int tj = 0; tj < TQ; ++tj) {
+          const int q = q0 + wq * WQ + tj * 16 + lq;
+          if (p < Pd && q < Qd) {
+            long long o = (long long)q * Pd + p;
+            if (phased) {
+              const int n = q / (Hs * Ws), rem = q - n * (Hs * Ws);
+              const int hi = rem / Ws, wi = rem - hi * Ws;
+              o = ((long long)(n * H + 2 * hi + ph_a) * W + 2 * wi + ph_b) * Pd + p;
+            }
+            *(f4v*)(PO + o) = acc[ti][tj];
+          }
+        }
+      }
+      return;
+    }
     bf16_t* O = (bf16_t*)a.out + (long long)g * a.out_gs;
     const int ldo = Pd;  // NHWC: channel contiguous
     const float* bias = a.bias ? a.bias + (long long)g * a.bias_gs : nullptr;
@@ -597,6 +627,120 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   }
 }
 
+// Split-K epilogue for FWD / DGRAD: out = epi(sum_s partial[s]) with the same fused terms as the
+// conv epilogue (bias, residual, mask, relu, BN statistics or the BN backward reduce). Each thread
+// owns one 8-channel chunk; per-block sums fold through LDS and go to stripe blockIdx.x % stripes.
+__global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvArgs a, int mode, int Pd,
+                                                                   long long rows, int nsplit) {
+  __shared__ float red[256 * 16];
+  const int g = blockIdx.y;
+  const int TPR = Pd >> 3, RPI = 256 / TPR;
+  const int cc = threadIdx.x % TPR, row = threadIdx.x / TPR, c0 = cc * 8;
+  const long long slice = (long long)a.G * rows * Pd;
+  const float* part = a.partial + (long long)g * rows * Pd + c0;
+  bf16_t* O = (bf16_t*)a.out + (long long)g * a.out_gs + c0;
+  const bf16_t* res = a.residual ? (const bf16_t*)a.residual + (long long)g * a.out_gs + c0 : nullptr;
+  const bf16_t* msk = a.mask ? (const bf16_t*)a.mask + (long long)g * a.out_gs + c0 : nullptr;
+  const bf16_t* bnx = (mode == MODE_DGRAD && a.bn_x) ? (const bf16_t*)a.bn_x + (long long)g * a.out_gs + c0
+                                                      : nullptr;
+  const bool want_stats = a.stats && (mode == MODE_FWD || bnx);
+  float bv[8] = {}, bmu[8] = {}, brs[8] = {}, s1[8] = {}, s2[8] = {};
+  if (a.bias) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) bv[k] = a.bias[(long long)g * a.bias_gs + c0 + k];
+  }
+  if (bnx) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      bmu[k] = a.bn_mean[(long long)g * Pd + c0 + k];
+      brs[k] = a.bn_rstd[(long long)g * Pd + c0 + k];
+    }
+  }
+  // RB rows per thread per pass, all their slice loads issued before any use; few enough blocks
+  // that the per-block statistics atomics (2 x Pd each) stay cheap
+  constexpr int RB = 4;
+  const long long stride = (long long)gridDim.x * RPI;
+  if (row < RPI) {
+    for (long long r0 = (long long)blockIdx.x * RPI + row; r0 < rows; r0 += stride * RB) {
+      float v[RB][8];
+#pragma unroll
+      for (int b = 0; b < RB; ++b)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[b][k] = bv[k];
+      for (int sp = 0; sp < nsplit; ++sp) {
+        f4v lo[RB], hi[RB];
+#pragma unroll
+        for (int b = 0; b < RB; ++b) {
+          const long long r = r0 + b * stride;
+          const long long e = (r < rows ? r : r0) * Pd + sp * slice;
+          lo[b] = *(const f4v*)(part + e);
+          hi[b] = *(const f4v*)(part + e + 4);
+        }
+#pragma unroll
+        for (int b = 0; b < RB; ++b) {
+          v[b][0] += lo[b][0]; v[b][1] += lo[b][1]; v[b][2] += lo[b][2]; v[b][3] += lo[b][3];
+          v[b][4] += hi[b][0]; v[b][5] += hi[b][1]; v[b][6] += hi[b][2]; v[b][7] += hi[b][3];
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < RB; ++b) {
+        const long long r = r0 + b * stride;
+        if (r >= rows) break;
+        const long long e = r * Pd;
+        float t[8];
+        if (res) {
+          unpack8(*(const i4v*)(res + e), t);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[b][k] += t[k];
+        }
+        if (msk) {
+          unpack8(*(const i4v*)(msk + e), t);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) if (!(t[k] > 0.f)) v[b][k] = 0.f;
+        }
+        if (a.relu) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[b][k] = fmaxf(v[b][k], 0.f);
+        }
+        *(i4v*)(O + e) = pack8(v[b]);
+        if (bnx) {
+          unpack8(*(const i4v*)(bnx + e), t);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { s1[k] += v[b][k]; s2[k] += v[b][k] * ((t[k] - bmu[k]) * brs[k]); }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { s1[k] += v[b][k]; s2[k] += v[b][k] * v[b][k]; }
+        }
+      }
+    }
+  }
+  if (!want_stats) return;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { red[threadIdx.x * 16 + k] = s1[k]; red[threadIdx.x * 16 + 8 + k] = s2[k]; }
+  __syncthreads();
+  if (row != 0) return;
+  for (int r = 1; r < RPI; ++r) {
+    const float* o = red + (r * TPR + cc) * 16;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { s1[k] += o[k]; s2[k] += o[8 + k]; }
+  }
+  float* st = a.stats + (long long)g * a.stats_gs +
+              (a.stats_stripes > 1 ? (long long)(blockIdx.x % a.stats_stripes) * 2 * Pd : 0) + c0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { atomicAdd(st + k, s1[k]); atomicAdd(st + Pd + k, s2[k]); }
+}
+
+static hipError_t splitk_epilogue(const ConvArgs& a, int mode, int Pd, long long rows, int nsplit,
+                                  hipStream_t s) {
+  const int RPI = 256 / (Pd / 8);
+  long long want = (rows + RPI * 4LL - 1) / (RPI * 4LL);  // RB = 4 rows per thread
+  const long long cap = (2048 + a.G - 1) / a.G;
+  if (want > cap) want = cap;
+  hipLaunchKernelGGL(conv_splitk_epilogue_kernel, dim3((unsigned)(want < 1 ? 1 : want), a.G), dim3(256), 0, s,
+                     a, mode, Pd, rows, nsplit);
+  return hipGetLastError();
+}
+
 template <int MODE, int BP, int BQ, int BK, int NS, int WLP = 2>
 static hipError_t launch_cfg(const ConvArgs& a, int Pd, int Qd, int gy, hipStream_t stream) {
   const int ntp = (Pd + BP - 1) / BP, ntq = (Qd + BQ - 1) / BQ;
@@ -678,6 +822,29 @@ static void small_grid_tiles(int Pd, long long Qd, int G, bool bk64_ok, int& bp,
   bq = tiles(64, 128) >= num_cus() ? 128 : 64;
 }
 
+// FWD / DGRAD split-K count: automatic only for unphased DGRAD (deep_only) with grids under one
+// workgroup per CU — ~3 per CU from K-splits of >= 8 steps — bounded by the caller's partial
+// workspace; split_k = 1 disables, > 1 forces (any mode).
+static int fd_splits(const ConvArgs& a, int Pd, long long tiles, long long nk, long long out_elems,
+                     bool deep_only) {
+  if (!a.partial || a.split_k == 1 || Pd % 8 || Pd / 8 > 256) return 1;
+  long long sp;
+  if (a.split_k > 1) {
+    sp = a.split_k;
+  } else {
+    // the extra pass moves (splits + 0.5) x 4 B per output and the split kernels are bandwidth-
+    // bound like the unsplit ones, so it only pays for deep reductions on small outputs
+    // (profiles/conv_split_g1.log: 1-client layer-4 DGRAD 48 -> 29-34 us; everything else loses)
+    if (!deep_only || tiles >= num_cus() || out_elems * a.G > (1LL << 20) || nk < 48) return 1;
+    sp = (3LL * num_cus() + tiles / 2) / tiles;
+    if (sp > nk / 8) sp = nk / 8;
+  }
+  const long long fit = a.partial_cap / (out_elems * a.G);
+  if (sp > fit) sp = fit;
+  if (sp > 64) sp = 64;
+  return sp > 1 ? (int)sp : 1;
+}
+
 DDL_API int ddl_conv_fwd(const ConvArgs* ap, int cfg, hipStream_t stream) {
   const ConvArgs& a = *ap;
   if (!conv_shapes_ok(a)) return (int)hipErrorInvalidValue;
@@ -688,7 +855,13 @@ DDL_API int ddl_conv_fwd(const ConvArgs* ap, int cfg, hipStream_t stream) {
   small_grid_tiles(Pd, Qd, a.G, a.C % 64 == 0, bp, bq, bk, ns);
   decode_cfg(cfg, bp, bq, bk, ns);
   if (a.C % bk) return (int)hipErrorInvalidValue;
-  return (int)dispatch<MODE_FWD>(a, Pd, Qd, bp, bq, bk, ns, 1, stream);
+  const int bpe = bp == 48 ? 64 : bp;
+  const long long tiles = (long long)((Pd + bpe - 1) / bpe) * ((Qd + bq - 1) / bq) * a.G;
+  const int sp = fd_splits(a, Pd, tiles, ((long long)a.R * a.S * a.C + bk - 1) / bk, (long long)Qd * Pd,
+                           false);
+  hipError_t e = dispatch<MODE_FWD>(a, Pd, Qd, bp, bq, bk, ns, sp, stream);
+  if (e != hipSuccess || sp == 1) return (int)e;
+  return (int)splitk_epilogue(a, MODE_FWD, Pd, Qd, sp, stream);
 }
 
 DDL_API int ddl_conv_dgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
@@ -703,7 +876,16 @@ DDL_API int ddl_conv_dgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
   small_grid_tiles(Pd, Qd * (phased ? 4 : 1), a.G, a.K % 64 == 0, bp, bq, bk, ns);
   decode_cfg(cfg, bp, bq, bk, ns);
   if (a.K % bk) return (int)hipErrorInvalidValue;
-  return (int)dispatch<MODE_DGRAD>(a, Pd, Qd, bp, bq, bk, ns, phased ? 4 : 1, stream);
+  const int nph = phased ? 4 : 1;
+  const long long rows = (long long)a.N * a.H * a.W;
+  const int bpe = bp == 48 ? 64 : bp;
+  const long long tiles = (long long)((Pd + bpe - 1) / bpe) * ((Qd + bq - 1) / bq) * a.G * nph;
+  // the (0, 0) phase has the most taps: ceil(R/2) x ceil(S/2) for pad-parity 0
+  const int rn = phased ? (a.R - (a.pad & 1) + 1) / 2 : a.R, sn = phased ? (a.S - (a.pad & 1) + 1) / 2 : a.S;
+  const int sp = fd_splits(a, Pd, tiles, ((long long)rn * sn * a.K + bk - 1) / bk, rows * Pd, !phased);
+  hipError_t e = dispatch<MODE_DGRAD>(a, Pd, Qd, bp, bq, bk, ns, nph * sp, stream);
+  if (e != hipSuccess || sp == 1) return (int)e;
+  return (int)splitk_epilogue(a, MODE_DGRAD, Pd, rows, sp, stream);
 }
 
 DDL_API int ddl_conv_wgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {

@@ -74,10 +74,34 @@ CONV_TILES = [(64, 64, 32, 4), (64, 128, 32, 4), (128, 64, 32, 4), (128, 128, 32
               (48, 256, 32, 4), (48, 256, 64, 3), (48, 256, 64, 2), (48, 256, 32, 3)]
 
 
-def _conv_args(geom: ConvGeom, device=None, **kw) -> _lib.ConvArgs:
+SPLITK_CAP = 1 << 24  # fp32 elements (64 MiB) of split-K partial slices per device
+_SPLITK: dict = {}
+
+
+def splitk_workspace(device) -> torch.Tensor | None:
+    """Per-device fp32 scratch for FWD / DGRAD split-K partial sums (small grids: one client, deep
+    layers). Convs on one stream use it one after another; it is allocated outside graph capture
+    (the first, eager step) — a conv first seen inside a capture simply runs unsplit."""
+    key = str(device)
+    b = _SPLITK.get(key)
+    if b is None:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        b = torch.empty(SPLITK_CAP, dtype=torch.float32, device=device)
+        _SPLITK[key] = b
+    return b
+
+
+def _conv_args(geom: ConvGeom, device=None, split_k: int = 0, partial: bool = False,
+               **kw) -> _lib.ConvArgs:
     a = _lib.ConvArgs()
     if device is not None:
         a.zero = zero_page(device).data_ptr()
+        if partial and split_k != 1:
+            pw = splitk_workspace(device)
+            if pw is not None:
+                a.partial, a.partial_cap = pw.data_ptr(), pw.numel()
+    a.split_k = split_k
     for k, v in kw.items():
         setattr(a, k, v)
     a.G, a.N, a.H, a.W, a.C, a.K = geom.G, geom.N, geom.H, geom.W, geom.C, geom.K
@@ -101,9 +125,10 @@ def stats_buffer(G: int, C: int, device) -> torch.Tensor:
 
 
 def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out=None, cfg=0,
-             residual=None):
+             residual=None, split_k=0):
     """y[G,N,P,Q,K] = conv(x[G,N,H,W,C], w[G,K,R,S,C]) (+bias)(+residual)(relu);
-    stats ([G,S,2,K] from ``stats_buffer``, or [G,2,K]) += per-channel sum, sumsq of y."""
+    stats ([G,S,2,K] from ``stats_buffer``, or [G,2,K]) += per-channel sum, sumsq of y.
+    split_k: 0 = automatic split-K for grids too small to fill the GPU, 1 = off, n = n slices."""
     if not x.is_cuda:
         y = ref.conv_fwd(x, w, geom, bias, relu, stats)
         if residual is not None:
@@ -117,7 +142,7 @@ def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out=None, 
                                                 dtype=torch.bfloat16, device=x.device)
     if residual is not None and (residual.stride(0) != y.stride(0) or not residual.is_contiguous()):
         residual = residual.contiguous()
-    a = _conv_args(geom, x.device, x=ptr(x), w=ptr(w), out=ptr(y), stats=ptr(stats), bias=ptr(bias),
+    a = _conv_args(geom, x.device, split_k, True, x=ptr(x), w=ptr(w), out=ptr(y), stats=ptr(stats), bias=ptr(bias),
                    residual=ptr(residual), x_gs=_gs(x), w_gs=_gs(w), out_gs=_gs(y),
                    bias_gs=_gs(bias), stats_gs=0 if stats is None else stats.stride(0),
                    relu=int(relu), stats_stripes=stats.shape[1] if stats is not None and stats.dim() == 4 else 1)
@@ -125,7 +150,7 @@ def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out=None, 
     return y
 
 
-def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0, bn=None):
+def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0, bn=None, split_k=0):
     """dx[G,N,H,W,C] = conv_transpose(dy, w) (+residual) * (mask > 0).
 
     bn = (x, mean, rstd): also reduce, in the epilogue, the preceding BatchNorm's backward sums
@@ -160,7 +185,7 @@ def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0,
         part = ws.zeros((geom.G, BN_STRIPES, 2, geom.C), dy.device)
         kw = dict(stats=ptr(part), stats_gs=part.stride(0), stats_stripes=BN_STRIPES, bn_x=ptr(x),
                   bn_mean=ptr(mean), bn_rstd=ptr(rstd))
-    a = _conv_args(geom, dy.device, w=ptr(w), dy=ptr(dy), out=ptr(dx), residual=ptr(residual),
+    a = _conv_args(geom, dy.device, split_k, True, w=ptr(w), dy=ptr(dy), out=ptr(dx), residual=ptr(residual),
                    mask=ptr(mask), w_gs=_gs(w), dy_gs=_gs(dy), out_gs=_gs(dx), **kw)
     check(_lib.kernels().ddl_conv_dgrad(ctypes.byref(a), cfg, stream()), "conv_dgrad")
     return dx if bn is None else (dx, part)
@@ -173,9 +198,8 @@ def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0):
         ref.conv_wgrad(dy, x, geom, dw, accumulate)
         return dw
     _check_inner(dy, "dy"); _check_inner(x, "x"); _check_inner(dw, "dw")
-    a = _conv_args(geom, dy.device, x=ptr(x), dy=ptr(dy), out=ptr(dw), x_gs=_gs(x), dy_gs=_gs(dy),
-                   out_gs=_gs(dw), accumulate=int(accumulate),
-                   split_k=1 if not accumulate else int(splits))
+    a = _conv_args(geom, dy.device, 1 if not accumulate else int(splits), x=ptr(x), dy=ptr(dy),
+                   out=ptr(dw), x_gs=_gs(x), dy_gs=_gs(dy), out_gs=_gs(dw), accumulate=int(accumulate))
     check(_lib.kernels().ddl_conv_wgrad(ctypes.byref(a), cfg, stream()), "conv_wgrad")
     return dw
 

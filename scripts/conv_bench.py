@@ -2,7 +2,8 @@
 optionally sweeping tile configs and comparing against PyTorch/MIOpen on the same shapes.
 
     python scripts/conv_bench.py [--sweep] [--miopen] [--G 8 --N 100]
-Timing: HIP events around R back-to-back launches, median of 5 repeats, random bf16 data.
+Timing: HIP events around a captured graph of R back-to-back launches, median of 5 replays,
+random bf16 data.
 """
 from __future__ import annotations
 
@@ -33,14 +34,26 @@ def resnet18_shapes(G, N):
 
 
 def timeit(fn, reps=10, rounds=5):
+    """Median per-call time of `reps` calls replayed from one captured HIP graph (so small-grid
+    kernels are not timed against Python/ctypes launch overhead, as in graph-captured training)."""
     fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for _ in range(reps):
+            fn()
+    graph.replay()
     torch.cuda.synchronize()
     ts = []
     for _ in range(rounds):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        for _ in range(reps):
-            fn()
+        graph.replay()
         b.record()
         b.synchronize()
         ts.append(a.elapsed_time(b) / reps)
@@ -57,12 +70,17 @@ def main():
     ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--miopen", action="store_true")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--layers", default="", help="comma list of layer names to run (default all)")
+    ap.add_argument("--splits", default="", help="FWD/DGRAD split-K counts to time, e.g. 1,2,4")
+    ap.add_argument("--split-sweep", action="store_true", help="also sweep tiles x splits")
     args = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
     results = []
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0, "miopen": 0.0}
     for name, g in resnet18_shapes(args.G, args.N):
+        if args.layers and name not in args.layers.split(","):
+            continue
         x = torch.randn(g.G, g.N, g.H, g.W, g.C, device=dev).to(torch.bfloat16)
         w = (torch.randn(g.G, g.K, g.R, g.S, g.C, device=dev) * 0.05).to(torch.bfloat16)
         dy = torch.randn(g.G, g.N, g.P, g.Q, g.K, device=dev).to(torch.bfloat16)
@@ -71,8 +89,8 @@ def main():
         fl = g.flops()
         row = {"layer": name, "geom": str(g), "gflop": fl / 1e9}
         modes = {
-            "fwd": lambda cfg: Fn.conv_fwd(x, w, g, cfg=cfg, stats=st),
-            "dgrad": lambda cfg: Fn.conv_dgrad(dy, w, g, cfg=cfg),
+            "fwd": lambda cfg, sk=0: Fn.conv_fwd(x, w, g, cfg=cfg, stats=st, split_k=sk),
+            "dgrad": lambda cfg, sk=0: Fn.conv_dgrad(dy, w, g, cfg=cfg, split_k=sk),
             "wgrad": lambda cfg: Fn.conv_wgrad(dy, x, g, dw, cfg=cfg),
         }
         for mode, f in modes.items():
@@ -81,6 +99,21 @@ def main():
             t = timeit(lambda: f(0))
             row[mode] = {"ms": t, "tflops": fl / t / 1e9}
             tot[mode] += t
+            if args.splits and mode != "wgrad":
+                row[mode]["splits_us"] = {int(k): round(1e3 * timeit(lambda: f(0, int(k))), 1)
+                                          for k in args.splits.split(",")}
+                if args.split_sweep:  # (tile x split) grid: best combination
+                    best = (1e9, None)
+                    for bp, bq, bk, ns in [(128, 128, 64, 2), (128, 128, 32, 3), (64, 128, 64, 3),
+                                           (128, 64, 64, 3), (64, 64, 64, 3), (128, 256, 32, 2),
+                                           (256, 128, 32, 2)]:
+                        if (g.C if mode == "fwd" else g.K) % bk:
+                            continue
+                        for k in [int(v) for v in args.splits.split(",")]:
+                            tc = timeit(lambda: f(Fn.conv_cfg(bp, bq, bk, ns), k), reps=5, rounds=3)
+                            if tc < best[0]:
+                                best = (tc, f"{bp}x{bq}x{bk}s{ns}/k{k}")
+                    row[mode]["splits_us"]["best"] = f"{best[0] * 1e3:.1f}@{best[1]}"
             if args.sweep:
                 best = (t, 0)
                 for bp, bq, bk, ns in CFGS:
@@ -113,6 +146,8 @@ def main():
         for mode in ("fwd", "dgrad", "wgrad"):
             if mode in row:
                 msg += f" | {mode} {row[mode]['ms'] * 1e3:7.1f}us {row[mode]['tflops']:6.0f}TF"
+                if "splits_us" in row[mode]:
+                    msg += f" split{row[mode]['splits_us']}"
                 if "best_cfg" in row[mode]:
                     msg += f" (best {row[mode]['best_tflops']:.0f} @{row[mode]['best_cfg']:#x})"
         if "miopen_fwd" in row:

@@ -1,0 +1,17 @@
+"""Print one training step's kernel sequence from a rocprofv3 kernel trace (between two sgd launches)."""
+import csv
+import sys
+
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+marker = sys.argv[2] if len(sys.argv) > 2 else "sgd_kernel"
+idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
+a, b = idx[-3], idx[-2]
+tot = 0.0
+span = (int(rows[b]["End_Timestamp"]) - int(rows[a]["End_Timestamp"])) / 1e3
+for r in rows[a + 1:b + 1]:
+    d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    tot += d
+    wg = int(r["Workgroup_Size_X"]) * int(r["Workgroup_Size_Y"]) * int(r["Workgroup_Size_Z"])
+    grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"]) // max(wg, 1)
+    print(f"{d:8.1f} us  wgs {grid:6d}  {r['Kernel_Name'][:70]}")
+print(f"kernel sum {tot:.1f} us, span {span:.1f} us")

@@ -277,3 +277,36 @@ def test_conv_dgrad_fused_bn_reduce(cuda, geom):
     unfused = Fn.bn_backward(plain, None, xbn, mean, rstd, gamma, dg2, db2)
     _close(fused, unfused, rel=2e-2)
     _close(dg1, dg2, rel=2e-2); _close(db1, db2, rel=2e-2)
+
+
+SPLIT_GEOMS = [GEOMS[0], GEOMS[1], GEOMS[2], GEOMS[6], GEOMS[7],
+               ConvGeom(G=1, N=8, H=4, W=4, C=512, K=512, R=3, S=3, stride=1, pad=1)]  # layer-4, 1 client
+
+
+@pytest.mark.parametrize("split", [0, 3])
+@pytest.mark.parametrize("geom", SPLIT_GEOMS, ids=lambda g: f"{g.C}x{g.K}_{g.H}_{g.R}s{g.stride}p{g.pad}")
+def test_conv_split_k(cuda, geom, split):
+    """FWD / DGRAD split-K (fp32 partial slices + streaming epilogue) == the direct epilogue: bias,
+    relu, BN statistics, residual, mask and the fused BN backward reduce. split 0 = automatic."""
+    g = geom
+    x = _rand(g.G, g.N, g.H, g.W, g.C, dev=cuda)
+    w = _weights(g, cuda)
+    bias = torch.randn(g.G, g.K, device=cuda)
+    st1, st2 = Fn.stats_buffer(g.G, g.K, cuda), Fn.stats_buffer(g.G, g.K, cuda)
+    y1 = Fn.conv_fwd(x, w, g, bias=bias, relu=True, stats=st1, split_k=1)
+    y2 = Fn.conv_fwd(x, w, g, bias=bias, relu=True, stats=st2, split_k=split)
+    _close(y2, ref.conv_fwd(x.cpu(), w.cpu(), g, bias=bias.cpu(), relu=True))
+    _close(y2, y1, rel=1e-2)
+    _close(st2.sum(1), st1.sum(1), rel=1e-2)
+    dy = _rand(g.G, g.N, g.P, g.Q, g.K, dev=cuda)
+    res = _rand(g.G, g.N, g.H, g.W, g.C, dev=cuda)
+    mask = _rand(g.G, g.N, g.H, g.W, g.C, dev=cuda)
+    dx = Fn.conv_dgrad(dy, w, g, residual=res, mask=mask, split_k=split)
+    _close(dx, ref.conv_dgrad(dy.cpu(), w.cpu(), g, residual=res.cpu(), mask=mask.cpu()))
+    xbn = _rand(g.G, g.N, g.H, g.W, g.C, dev=cuda) + 0.3
+    mean = torch.randn(g.G, g.C, device=cuda) * 0.2
+    rstd = torch.rand(g.G, g.C, device=cuda) + 0.5
+    dxa, pa = Fn.conv_dgrad(dy, w, g, mask=mask, bn=(xbn, mean, rstd), split_k=1)
+    dxb, pb = Fn.conv_dgrad(dy, w, g, mask=mask, bn=(xbn, mean, rstd), split_k=split)
+    _close(dxb, dxa, rel=1e-2)
+    _close(pb.sum(1), pa.sum(1), rel=2e-2)
