@@ -193,15 +193,69 @@ def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0,
 
 def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0):
     """dw[G,K,R,S,C] (+)= sum over pixels dy (x) x  — fp32, split-K with atomics.
-    cfg = conv_cfg(bp, bq, bk, stages) (0: tuned default); splits = split-K slices (0: auto)."""
+    cfg = conv_cfg(bp, bq, bk, stages) (0: tuned default); splits = split-K slices (0: auto).
+    Inside ``wgrad_overlap`` the launch goes to the side stream (see there)."""
     if not dy.is_cuda:
         ref.conv_wgrad(dy, x, geom, dw, accumulate)
         return dw
     _check_inner(dy, "dy"); _check_inner(x, "x"); _check_inner(dw, "dw")
     a = _conv_args(geom, dy.device, 1 if not accumulate else int(splits), x=ptr(x), dy=ptr(dy),
                    out=ptr(dw), x_gs=_gs(x), dy_gs=_gs(dy), out_gs=_gs(dw), accumulate=int(accumulate))
-    check(_lib.kernels().ddl_conv_wgrad(ctypes.byref(a), cfg, stream()), "conv_wgrad")
+    side = _WGRAD_SIDE
+    if side is None:
+        check(_lib.kernels().ddl_conv_wgrad(ctypes.byref(a), cfg, stream()), "conv_wgrad")
+        return dw
+    side.wait_stream(torch.cuda.current_stream())
+    dy.record_stream(side)
+    x.record_stream(side)
+    with torch.cuda.stream(side):
+        check(_lib.kernels().ddl_conv_wgrad(ctypes.byref(a), cfg, stream()), "conv_wgrad")
     return dw
+
+
+# ------------------------------------------------------------------- wgrad / dgrad overlap
+_WGRAD_SIDE: "torch.cuda.Stream | None" = None
+_SIDE_STREAMS: dict = {}
+
+
+class wgrad_overlap:
+    """Backward-pass stream split: inside this context every ``conv_wgrad`` runs on a side stream
+    (after an event on the main stream), so a layer's weight gradient can overlap the main
+    stream's dgrad -> BN-backward chain of the layers below it (the two are independent: wgrad
+    only accumulates into the fp32 grad buffer). Leaving the context joins the side stream back;
+    captured in a HIP graph this is a fork/join per layer. Opt-in (``Net.overlap_wgrad``): on the
+    graph-replayed ResNet-18 step the cross-queue synchronisation cost more than the overlap won.
+    ``run_joined(fn)`` runs ``fn`` (e.g. a DP all-reduce hook) ordered after both streams."""
+
+    def __init__(self, device, enabled: bool = True):
+        self.enabled = enabled and torch.device(device).type == "cuda"
+        self.device = torch.device(device)
+
+    def __enter__(self):
+        global _WGRAD_SIDE
+        self.prev = _WGRAD_SIDE
+        if self.enabled:
+            key = str(self.device)
+            if key not in _SIDE_STREAMS:
+                _SIDE_STREAMS[key] = torch.cuda.Stream(self.device)
+            _WGRAD_SIDE = _SIDE_STREAMS[key]
+        return self
+
+    def __exit__(self, *exc):
+        global _WGRAD_SIDE
+        if _WGRAD_SIDE is not None and _WGRAD_SIDE is not self.prev:
+            torch.cuda.current_stream().wait_stream(_WGRAD_SIDE)
+        _WGRAD_SIDE = self.prev
+        return False
+
+    @staticmethod
+    def run_joined(fn):
+        side = _WGRAD_SIDE
+        if side is None:
+            return fn()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            return fn()
 
 
 # ------------------------------------------------------------------------------------- BN
