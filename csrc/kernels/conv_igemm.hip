@@ -27,8 +27,10 @@
 //     (gfx950 transpose read), for operands whose output index is contiguous (W in DGRAD, dY and
 //     X in WGRAD).
 // Both swizzles are bank-conflict-free for the fragment reads.
-// Workgroup = 4 waves (2x2) on a BP x BQ tile; blockIdx.z = client group, blockIdx.y = split-K
-// slice x stride-2 DGRAD phase, blockIdx.x = tile id remapped XCD-aware.
+// Workgroup = 4 waves (2x2) on a BP x BQ tile; grid (tile, split-K slice x stride-2 DGRAD phase,
+// client group). The WHOLE linear block id is remapped XCD-aware (bx fastest), so every tile of
+// one (group, slice, phase) lands on the same XCD and shares its L2: WGRAD's split-K slices read
+// one pixel chunk of dY and X from all their tiles.
 // Split-K: WGRAD adds fp32 partials atomically into the zeroed gradient; FWD / DGRAD (grids too
 // small to fill the CUs: one client, deep layers) store per-split fp32 slices and a streaming
 // epilogue kernel sums them and applies the fused epilogue (BN statistics / BN backward reduce).
@@ -150,7 +152,16 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wp = wid / (4 / WLP), wq = wid % (4 / WLP);
-  const int g = blockIdx.z;
+  // XCD-aware decode of the linear block id: the dispatcher deals workgroups round-robin over
+  // the 8 XCDs; consecutive logical ids u share an XCD (and its L2).
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int u = xcd_remap(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
+  // Stride-2 DGRAD keeps the per-phase remap of the tile index only (measured: grouping the
+  // phases of a tile, or the tiles of a phase, on one XCD both lose 10-20% there).
+  const bool per_phase = MODE == MODE_DGRAD && a.stride == 2;
+  const int bx = per_phase ? xcd_remap(blockIdx.x, gx) : u % gx;
+  const int by = per_phase ? (int)blockIdx.y : (u / gx) % gy;
+  const int g = per_phase ? (int)blockIdx.z : u / (gx * gy);
   const int H = a.H, W = a.W, C = a.C, K = a.K, R = a.R, S = a.S, P = a.P, Q = a.Q;
   const int st = a.stride, pd = a.pad;
   const int RSC = R * S * C;
@@ -169,8 +180,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   const bool phased = PHASED_MODE && st == 2;
   const int nph = phased ? 4 : 1;
   if (phased) {
-    ph_a = (blockIdx.y >> 1) & 1;
-    ph_b = blockIdx.y & 1;
+    ph_a = (by >> 1) & 1;
+    ph_b = by & 1;
     Hs = (H - ph_a + 1) >> 1;
     Ws = (W - ph_b + 1) >> 1;
     r0 = (ph_a + pd) & 1;
@@ -183,10 +194,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   }
 
   const int ntp = (Pd + BP - 1) / BP;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = bx;
   const int p0 = (tile % ntp) * BP, q0 = (tile / ntp) * BQ;
   if (q0 >= Qd) return;  // smaller phases of a phased launch
-  const int nsplit = gridDim.y / nph, split = blockIdx.y / nph;
+  const int nsplit = gy / nph, split = by / nph;
   const int nk_total = (Kr + BK - 1) / BK;
   const int per = (nk_total + nsplit - 1) / nsplit;
   const int kt0 = split * per;
