@@ -157,6 +157,93 @@ DDL_API int ddl_ce_vocab(const void* logits, const int* labels, int R, int V, in
 }
 
 // ---------------------------------------------------------------------------------------------
+// Split LM-head CE for autograd without host syncs or extra passes over the [rows, V] logits:
+//   fwd : lse[row] and loss += (lse - z_y) * (*inv)          (inv = 1 / #non-ignored rows, device)
+//   bwd : dz = (*g) * (*inv) * (softmax(z) - onehot(y))      (g = upstream grad, device scalar)
+// so the mean normaliser and the upstream scale (e.g. 1/micro-batches) never leave the device, and
+// the gradient is produced in backward, in one read of z and one write of dz.
+__global__ __launch_bounds__(256) void ce_vocab_lse_kernel(const bf16_t* __restrict__ logits,
+                                                           const int* __restrict__ labels, int V,
+                                                           int ld, const float* __restrict__ inv,
+                                                           int ignore_index, float* __restrict__ loss,
+                                                           float* __restrict__ lse_out) {
+  __shared__ float sm[2][4];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const bf16_t* z = logits + (long long)row * ld;
+  float m = -INFINITY, se = 0.f;
+  for (int c = tid * 8; c < V; c += 256 * 8) {
+    float v[8];
+    unpack8(*(const i4v*)(z + c), v);
+    float lm = v[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) lm = fmaxf(lm, v[k]);
+    const float nm = fmaxf(m, lm);
+    se = se * __expf(m - nm);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) se += __expf(v[k] - nm);
+    m = nm;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64), os = __shfl_xor(se, o, 64);
+    const float nm = fmaxf(m, om);
+    se = (m == -INFINITY ? 0.f : se * __expf(m - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    m = nm;
+  }
+  if (lane == 0) { sm[0][w] = m; sm[1][w] = se; }
+  __syncthreads();
+  if (tid != 0) return;
+  float M = sm[0][0];
+  for (int i = 1; i < 4; ++i) M = fmaxf(M, sm[0][i]);
+  float SE = 0.f;
+  for (int i = 0; i < 4; ++i) SE += sm[1][i] * __expf(sm[0][i] - M);
+  const float lse = M + __logf(SE);
+  lse_out[row] = lse;
+  const int y = labels[row];
+  if (y != ignore_index) atomicAdd(loss, (lse - bf2f(z[y])) * (*inv));
+}
+
+__global__ __launch_bounds__(256) void ce_vocab_grad_kernel(const bf16_t* __restrict__ logits,
+                                                            const int* __restrict__ labels, int V,
+                                                            int ld, const float* __restrict__ lse,
+                                                            const float* __restrict__ inv,
+                                                            const float* __restrict__ g,
+                                                            int ignore_index,
+                                                            bf16_t* __restrict__ dlogits) {
+  const int row = blockIdx.x;
+  const int y = labels[row];
+  const bool ign = y == ignore_index;
+  const float sc = (*g) * (*inv), L = lse[row];
+  const bf16_t* z = logits + (long long)row * ld;
+  bf16_t* dz = dlogits + (long long)row * ld;
+  for (int c = threadIdx.x * 8; c < V; c += 256 * 8) {
+    float v[8];
+    unpack8(*(const i4v*)(z + c), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = ign ? 0.f : sc * (__expf(v[k] - L) - ((c + k) == y ? 1.f : 0.f));
+    *(i4v*)(dz + c) = pack8(v);
+  }
+}
+
+DDL_API int ddl_ce_vocab_lse(const void* logits, const int* labels, int R, int V, int ld,
+                             const float* inv, int ignore_index, float* loss, float* lse,
+                             hipStream_t s) {
+  if (V % 8 || ld % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ce_vocab_lse_kernel, dim3(R), dim3(256), 0, s, (const bf16_t*)logits, labels, V,
+                     ld, inv, ignore_index, loss, lse);
+  return (int)hipGetLastError();
+}
+
+DDL_API int ddl_ce_vocab_grad(const void* logits, const int* labels, int R, int V, int ld,
+                              const float* lse, const float* inv, const float* g, int ignore_index,
+                              void* dlogits, hipStream_t s) {
+  if (V % 8 || ld % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ce_vocab_grad_kernel, dim3(R), dim3(256), 0, s, (const bf16_t*)logits, labels,
+                     V, ld, lse, inv, g, ignore_index, (bf16_t*)dlogits);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 // loss += sum (xr - x)^2 + kl_w * -0.5*sum(1 + lv - mu^2 - exp(lv));  fp32 tensors
 // grads: dxr = 2(xr - x)*gs ; dmu = kl_w*mu*gs ; dlv = kl_w*0.5*(exp(lv) - 1)*gs
 __global__ void mse_kl_kernel(const float* __restrict__ xr, const float* __restrict__ x, long long n,

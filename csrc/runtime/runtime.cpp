@@ -270,4 +270,28 @@ API int ddl_bucket_plan(const int64_t* sizes, int n, int64_t cap_bytes, int elem
   return n ? bucket + 1 : 0;
 }
 
+// Token-stream generator (data/text.py::TinyStories): walks B Markov chains of length S over a
+// sparse transition table. next_tok [V0][br] token ids, cum [V0][br] cumulative probabilities,
+// cur0 [B] first tokens, U [B][S] uniforms (drawn per sequence by numpy from (seed, index), so
+// the stream stays a pure function of the sequence index). out [B][S]: out[b][0] = bos, then
+// out[b][t] = cur; cur <- next_tok[cur][#{k : cum[cur][k] < U[b][t]}] (numpy searchsorted, left).
+API int ddl_markov_walk(const int64_t* next_tok, const double* cum, int br, const int64_t* cur0,
+                        const double* U, int B, int S, int64_t bos, int64_t* out) {
+  for (int b = 0; b < B; ++b) {
+    int64_t cur = cur0[b];
+    int64_t* o = out + (size_t)b * S;
+    const double* u = U + (size_t)b * S;
+    o[0] = bos;
+    for (int t = 1; t < S; ++t) {
+      o[t] = cur;
+      const double* c = cum + (size_t)cur * br;
+      int j = 0;
+      while (j < br && c[j] < u[t]) ++j;
+      if (j > br - 1) j = br - 1;
+      cur = next_tok[(size_t)cur * br + j];
+    }
+  }
+  return 0;
+}
+
 API int ddl_runtime_version() { return 1; }

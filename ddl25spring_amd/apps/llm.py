@@ -44,6 +44,29 @@ class LLMConfig:
     fused_adam: bool = True
 
 
+class _PinnedH2D:
+    """Token batches to the device without a host<->device sync: two pinned staging buffers used
+    alternately, each refilled only after the copy that last read it has completed (a pageable
+    copy would make the host wait for the GPU to drain, so it could not queue the next step)."""
+
+    def __init__(self, shape, dtype, device):
+        self.bufs = [torch.empty(shape, dtype=dtype).pin_memory() for _ in range(2)]
+        self.events = [None, None]
+        self.i, self.device = 0, device
+
+    def __call__(self, x):
+        i = self.i
+        self.i ^= 1
+        if self.events[i] is not None:
+            self.events[i].synchronize()
+        self.bufs[i].copy_(x)
+        out = self.bufs[i].to(self.device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[i] = ev
+        return out
+
+
 def train_llm(cfg: LLMConfig, ctx, log=print, warmup: int = 0) -> dict:
     """Runs ``warmup`` untimed + ``cfg.iters`` timed iterations; returns losses and throughput."""
     if ctx.world != cfg.dp * cfg.pp:
@@ -59,7 +82,9 @@ def train_llm(cfg: LLMConfig, ctx, log=print, warmup: int = 0) -> dict:
         broadcast_parameters(mod, ctx, src=stage, group=dp_group)  # pipeline 0's stage s is rank s
     if dev.type == "cuda" and cfg.fused_adam:
         from ..optim import FlatAdam
-        opt = FlatAdam(mod.parameters(), lr=cfg.lr)
+        # one fused Adam launch that also refreshes the bf16 weight shadow the GEMMs read;
+        # weight grads accumulate straight into the flat grad buffer (or the DP buckets)
+        opt = FlatAdam(mod.parameters(), lr=cfg.lr, fused=True, bf16_shadow=True)
     else:
         opt = torch.optim.Adam(mod.parameters(), lr=cfg.lr)
     sync = GradBucketer(mod, ctx, group=dp_group, bucket_mb=cfg.bucket_mb) \
@@ -72,10 +97,12 @@ def train_llm(cfg: LLMConfig, ctx, log=print, warmup: int = 0) -> dict:
                        act_dtype=act_dtype, device=dev) if cfg.pp > 1 else None
     stream = iter(TinyStories(SPTokenizer(cfg.vocab_size), cfg.batch_size, cfg.ctx_size,
                               skip=pipe * 3000, seed=1234 + cfg.seed))
+    h2d = _PinnedH2D((cfg.batch_size, cfg.ctx_size), torch.int64, dev) if dev.type == "cuda" else None
     losses = []
 
     def step():
-        x = next(stream).to(dev, non_blocking=True)
+        x = next(stream)
+        x = h2d(x) if h2d is not None else x.to(dev)
         if sync is not None:
             sync.zero_grad()
         else:
@@ -100,6 +127,8 @@ def train_llm(cfg: LLMConfig, ctx, log=print, warmup: int = 0) -> dict:
         opt.step()
         if cfg.dp > 1 and cfg.dp_mode == "wa":
             average_weights(mod, ctx, group=dp_group)
+            if hasattr(opt, "sync_shadow"):
+                opt.sync_shadow()
         return loss
 
     for _ in range(warmup):

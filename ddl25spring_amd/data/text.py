@@ -13,8 +13,12 @@ is available offline, so:
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 import torch
+
+from ..ops import _lib
 
 
 class SPTokenizer:
@@ -41,6 +45,8 @@ class TinyStories:
         p = rng.dirichlet(np.full(branching, 0.3), V + 3)
         self.cum = np.cumsum(p, 1)
         self.seed = seed
+        self._next = np.ascontiguousarray(self.next_tok, dtype=np.int64)
+        self._cum = np.ascontiguousarray(self.cum, dtype=np.float64)
 
     def _sequence(self, index: int) -> np.ndarray:
         rng = np.random.default_rng((self.seed, index))
@@ -54,8 +60,28 @@ class TinyStories:
             cur = int(self.next_tok[cur, min(j, self.next_tok.shape[1] - 1)])
         return out
 
+    def batch(self, start: int) -> np.ndarray:
+        """Sequences start .. start+B-1, identical to ``_sequence``: numpy draws each sequence's
+        first token and uniforms from (seed, index); the chain walk runs in the C++ runtime
+        (``ddl_markov_walk``) — the per-token Python loop cost ~25 ms per 32x256 batch, longer
+        than the GPU step it feeds."""
+        B, S = self.B, self.S
+        cur0 = np.empty(B, dtype=np.int64)
+        U = np.empty((B, S), dtype=np.float64)
+        for b in range(B):
+            rng = np.random.default_rng((self.seed, start + b))
+            cur0[b] = rng.integers(3, 3 + self.V)
+            U[b] = rng.random(S)
+        out = np.empty((B, S), dtype=np.int64)
+        i64p, f64p = ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)
+        _lib.runtime().ddl_markov_walk(self._next.ctypes.data_as(i64p), self._cum.ctypes.data_as(f64p),
+                                       self._next.shape[1], cur0.ctypes.data_as(i64p),
+                                       U.ctypes.data_as(f64p), B, S, self.tok.bos_id,
+                                       out.ctypes.data_as(i64p))
+        return out
+
     def __iter__(self):
         i = self.skip * self.B
         while True:
-            yield torch.from_numpy(np.stack([self._sequence(i + b) for b in range(self.B)]))
+            yield torch.from_numpy(self.batch(i))
             i += self.B

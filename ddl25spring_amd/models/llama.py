@@ -153,7 +153,12 @@ def split_stages(model: LLama, n_stages: int):
 
 
 def causalLLMLoss(logits, target, vocab_size=None, ignore_index=-100):  # noqa: N802 (reference name)
-    """Next-token CE: logits[:, :-1] vs target[:, 1:] (one fused kernel on device)."""
-    lg = logits[:, :-1]
-    tg = target[:, 1:]
-    return A.cross_entropy_vocab(lg.contiguous(), tg.contiguous(), ignore_index)
+    """Next-token CE: logits[:, :-1] vs target[:, 1:]. On the device every row of the [B, S, V]
+    logits goes to the fused kernel with the last position's label set to ``ignore_index`` (same
+    mean, no copy of the [B, S-1, V] slice)."""
+    if not logits.is_cuda:
+        return A.cross_entropy_vocab(logits[:, :-1].contiguous(), target[:, 1:].contiguous(), ignore_index)
+    lab = torch.empty(target.shape, dtype=torch.int32, device=target.device)
+    lab[:, :-1] = target[:, 1:]
+    lab[:, -1] = ignore_index
+    return A.cross_entropy_vocab(logits, lab, ignore_index)

@@ -166,7 +166,10 @@ def runtime():
         lib.ddl_sched_verify.argtypes = [p32, i32, i32]
         lib.ddl_plan_epoch.argtypes = [p32, i32, i32, i32, ctypes.POINTER(ctypes.c_uint64), i32, p32]
         lib.ddl_bucket_plan.argtypes = [ctypes.POINTER(ctypes.c_int64), i32, ctypes.c_int64, i32, p32]
-        for f in ("ddl_sched_build", "ddl_sched_verify", "ddl_plan_epoch", "ddl_bucket_plan"):
+        i64p, f64p = ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)
+        lib.ddl_markov_walk.argtypes = [i64p, f64p, i32, i64p, f64p, i32, i32, ctypes.c_int64, i64p]
+        for f in ("ddl_sched_build", "ddl_sched_verify", "ddl_plan_epoch", "ddl_bucket_plan",
+                  "ddl_markov_walk"):
             getattr(lib, f).restype = ctypes.c_int
         _runtime = lib
     return _runtime

@@ -28,6 +28,8 @@ _lib.register_signatures({
     "ddl_add": [vp, vp, vp, i64, vp],
     "ddl_attn_fwd": [vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, vp],
     "ddl_attn_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, vp],
+    "ddl_ce_vocab_lse": [vp, vp, i32, i32, i32, vp, i32, vp, vp, vp],
+    "ddl_ce_vocab_grad": [vp, vp, i32, i32, i32, vp, vp, vp, i32, vp, vp],
 })
 
 
@@ -36,7 +38,31 @@ def K():
 
 
 def _bf16_weight(w: torch.Tensor) -> torch.Tensor:
+    sh = getattr(w, "_ddl_bf16", None)  # FlatAdam(bf16_shadow=True) keeps it current: no cast
+    if sh is not None:
+        return sh
     return Fn.to_bf16(w.detach().contiguous())
+
+
+def _grad_sink(p: torch.Tensor):
+    """``p.grad`` itself when the parameter's optimizer lets backward accumulate into it in place
+    (``FlatAdam(fused=True)`` marks its parameters), else None and autograd accumulates. Saves the
+    zero-fill of a fresh gradient and AccumulateGrad's add pass (37 MB each for the 32k x 288
+    embedding / LM head, per micro-batch)."""
+    if not getattr(p, "_ddl_fuse_grad", False):
+        return None
+    g = p.grad
+    if g is None or g.dtype != torch.float32 or not g.is_contiguous() or g.device != p.device:
+        return None
+    return g
+
+
+def _grad_ready(p: torch.Tensor) -> None:
+    """A fused accumulation bypasses AccumulateGrad, so run what its post-accumulate hook would:
+    the DP bucketer registers its hook as ``p._ddl_on_grad``."""
+    cb = getattr(p, "_ddl_on_grad", None)
+    if cb is not None:
+        cb(p)
 
 
 # ------------------------------------------------------------------------------------- linear
@@ -54,6 +80,7 @@ class _Linear(torch.autograd.Function):
                         bias=None if b is None else b.detach().view(1, Kout), residual=res)
         ctx.save_for_backward(x2, wb)
         ctx.geom, ctx.has_b, ctx.has_res, ctx.xshape = geom, b is not None, residual is not None, x.shape
+        ctx.w = w
         return y.view(*x.shape[:-1], Kout)
 
     @staticmethod
@@ -65,9 +92,14 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = Fn.conv_dgrad(dy5, wb, g).view(ctx.xshape)
         if ctx.needs_input_grad[1]:
-            dw = torch.zeros(1, g.K, 1, 1, g.C, dtype=torch.float32, device=dy.device)
-            Fn.conv_wgrad(dy5, x2.view(1, g.N, 1, 1, g.C), g, dw)
-            dw = dw.view(g.K, g.C)
+            sink = _grad_sink(ctx.w)
+            if sink is not None:  # accumulate straight into the parameter's grad
+                Fn.conv_wgrad(dy5, x2.view(1, g.N, 1, 1, g.C), g, sink.view(1, g.K, 1, 1, g.C))
+                _grad_ready(ctx.w)
+            else:
+                dw = torch.zeros(1, g.K, 1, 1, g.C, dtype=torch.float32, device=dy.device)
+                Fn.conv_wgrad(dy5, x2.view(1, g.N, 1, 1, g.C), g, dw)
+                dw = dw.view(g.K, g.C)
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = torch.zeros(1, g.K, dtype=torch.float32, device=dy.device)
             Fn.channel_sum(dy5.view(1, g.N, g.K), db)
@@ -101,7 +133,7 @@ class _RMSNorm(torch.autograd.Function):
         check(K().ddl_rmsnorm_fwd(ptr(x2), ptr(gd), ptr(y), ptr(rstd), T, D, float(eps), stream()),
               "rmsnorm_fwd")
         ctx.save_for_backward(x2, gd, rstd)
-        ctx.shape = x.shape
+        ctx.shape, ctx.g = x.shape, g
         return y.view(x.shape)
 
     @staticmethod
@@ -109,10 +141,14 @@ class _RMSNorm(torch.autograd.Function):
         x2, gd, rstd = ctx.saved_tensors
         T, D = x2.shape
         dx = torch.empty_like(x2)
-        dg = torch.zeros(D, dtype=torch.float32, device=x2.device)
+        sink = _grad_sink(ctx.g) if ctx.needs_input_grad[1] else None
+        dg = sink if sink is not None else torch.zeros(D, dtype=torch.float32, device=x2.device)
         dyc = dy.reshape(T, D).to(torch.bfloat16).contiguous()
         check(K().ddl_rmsnorm_bwd(ptr(x2), ptr(gd), ptr(rstd), ptr(dyc), ptr(dx), ptr(dg), T, D,
                                   stream()), "rmsnorm_bwd")
+        if sink is not None:
+            _grad_ready(ctx.g)
+            dg = None
         return dx.view(ctx.shape), dg, None
 
 
@@ -163,18 +199,22 @@ class _Embedding(torch.autograd.Function):
         wd = w.detach().float().contiguous()
         check(K().ddl_embedding_fwd(ptr(idx32), ptr(wd), ptr(y), T, D, stream()), "embedding_fwd")
         ctx.save_for_backward(idx32)
-        ctx.wshape, ctx.pad, ctx.ishape = w.shape, pad_idx, idx.shape
+        ctx.wshape, ctx.pad, ctx.ishape, ctx.w = w.shape, pad_idx, idx.shape, w
         return y.view(*idx.shape, D)
 
     @staticmethod
     def backward(ctx, dy):
         (idx32,) = ctx.saved_tensors
         V, D = ctx.wshape
-        dw = torch.zeros(V, D, dtype=torch.float32, device=dy.device)
+        sink = _grad_sink(ctx.w) if ctx.needs_input_grad[1] else None
+        dw = sink if sink is not None else torch.zeros(V, D, dtype=torch.float32, device=dy.device)
         dyc = dy.reshape(-1, D).to(torch.bfloat16).contiguous()
         check(K().ddl_embedding_bwd(ptr(idx32), ptr(dyc), ptr(dw), idx32.numel(), D,
                                     -1 if ctx.pad is None else int(ctx.pad), stream()),
               "embedding_bwd")
+        if sink is not None:
+            _grad_ready(ctx.w)
+            dw = None
         return None, dw, None
 
 
@@ -276,25 +316,36 @@ def causal_attention(qkv, n_heads, head_dim):
 
 # ------------------------------------------------------------------------------- LM loss
 class _VocabCE(torch.autograd.Function):
+    """Mean token CE over the rows of bf16 logits [..., V] with int32 labels. No host sync (the
+    1/#valid normaliser is a device scalar) and the gradient is made in backward from the saved
+    logits and per-row log-sum-exp, already scaled by the upstream gradient (e.g. 1/micro-batches)."""
+
     @staticmethod
-    def forward(ctx, logits, targets, ignore_index):
+    def forward(ctx, logits, labels, ignore_index):
         V = logits.shape[-1]
-        lg = logits.reshape(-1, V).to(torch.bfloat16).contiguous()
+        lg = logits.reshape(-1, V)
+        if not lg.is_contiguous():
+            lg = lg.contiguous()
         R = lg.shape[0]
-        tg = targets.reshape(-1).to(torch.int32).contiguous()
-        valid = max(1, int((tg != ignore_index).sum().item()))
-        loss = torch.zeros(1, dtype=torch.float32, device=logits.device)
-        d = torch.empty_like(lg)
-        check(K().ddl_ce_vocab(ptr(lg), ptr(tg), R, V, V, 1.0 / valid, int(ignore_index), ptr(loss),
-                               ptr(d), stream()), "ce_vocab")
-        ctx.save_for_backward(d)
-        ctx.shape = logits.shape
+        lab = labels.reshape(-1)
+        inv = (lab != ignore_index).sum(dtype=torch.float32).clamp_min_(1.0).reciprocal_().reshape(1)
+        loss = torch.zeros(1, dtype=torch.float32, device=lg.device)
+        lse = torch.empty(R, dtype=torch.float32, device=lg.device)
+        check(K().ddl_ce_vocab_lse(ptr(lg), ptr(lab), R, V, V, ptr(inv), int(ignore_index), ptr(loss),
+                                   ptr(lse), stream()), "ce_vocab_lse")
+        ctx.save_for_backward(lg, lab, lse, inv)
+        ctx.shape, ctx.ignore = logits.shape, int(ignore_index)
         return loss[0]
 
     @staticmethod
     def backward(ctx, g):
-        (d,) = ctx.saved_tensors
-        return (d.float() * g).to(torch.bfloat16).view(ctx.shape), None, None
+        lg, lab, lse, inv = ctx.saved_tensors
+        R, V = lg.shape
+        gg = g.detach().to(torch.float32).reshape(1).contiguous()
+        d = torch.empty_like(lg)
+        check(K().ddl_ce_vocab_grad(ptr(lg), ptr(lab), R, V, V, ptr(lse), ptr(inv), ptr(gg),
+                                    ctx.ignore, ptr(d), stream()), "ce_vocab_grad")
+        return d.view(ctx.shape), None, None
 
 
 def cross_entropy_vocab(logits, targets, ignore_index=-100):
@@ -302,7 +353,9 @@ def cross_entropy_vocab(logits, targets, ignore_index=-100):
     if not logits.is_cuda:
         return F.cross_entropy(logits.reshape(-1, logits.shape[-1]).float(), targets.reshape(-1).long(),
                                ignore_index=ignore_index)
-    return _VocabCE.apply(logits, targets, ignore_index)
+    if logits.dtype != torch.bfloat16:
+        logits = logits.to(torch.bfloat16)
+    return _VocabCE.apply(logits, targets.to(torch.int32).contiguous(), ignore_index)
 
 
 # ===================================================================== image ops (NHWC, GANs)

@@ -109,10 +109,16 @@ class FlatAdam:
 
     ``zero_grad`` zeroes in place (grads must stay views of the flat buffer); parameters whose
     ``requires_grad`` is False are left alone.
+
+    ``fused=True``: backward accumulates weight gradients straight into ``p.grad`` (no zero-filled
+    temporary, no AccumulateGrad add; ``autograd_ops._grad_sink``). ``bf16_shadow=True``: a bf16
+    copy of the weights, refreshed by the Adam kernel itself, is what the MFMA ops read (no cast
+    per forward); call ``sync_shadow()`` after changing parameters outside ``step()``.
     """
 
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0, decoupled: bool = False):
+                 weight_decay: float = 0.0, decoupled: bool = False, fused: bool = False,
+                 bf16_shadow: bool = False):
         self.params = [p for p in params if p.requires_grad]
         if not self.params:
             raise ValueError("FlatAdam got no trainable parameters")
@@ -135,6 +141,19 @@ class FlatAdam:
         self.v = torch.zeros_like(self.data)
         self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
         self.decoupled, self.t = decoupled, 0
+        self.shadow = None
+        if bf16_shadow and dev.type == "cuda":
+            self.shadow = torch.empty(n, dtype=torch.bfloat16, device=dev)
+            self.sync_shadow()
+            for p, off in zip(self.params, self.offsets):
+                p._ddl_bf16 = self.shadow[off:off + p.numel()].view_as(p)
+        if fused:
+            for p in self.params:
+                p._ddl_fuse_grad = True
+
+    def sync_shadow(self):
+        if self.shadow is not None:
+            Fn.to_bf16(self.data, out=self.shadow)
 
     def zero_grad(self, set_to_none: bool = False):
         self.grad.zero_()
@@ -150,10 +169,11 @@ class FlatAdam:
     def step(self):
         for p, g in zip(self.params, self._views()):
             if p.grad is not None and p.grad.data_ptr() != g.data_ptr():
+                # grads live elsewhere (e.g. the DP bucketer's all-reduce buckets): copy, and
+                # leave p.grad pointing where the bucketer (and fused backward) accumulate
                 g.copy_(p.grad)
-                p.grad = g
         self.t += 1
-        Fn.adam_step(self.data, self.grad, self.m, self.v, None, self.lr, self.betas[0],
+        Fn.adam_step(self.data, self.grad, self.m, self.v, self.shadow, self.lr, self.betas[0],
                      self.betas[1], self.eps, self.weight_decay, self.t, self.decoupled)
 
 

@@ -74,6 +74,8 @@ class GradBucketer:
                 self.owner[p] = bi
         self.enabled = True
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
+        for p in params:  # fused-accumulation backward (autograd_ops._grad_ready) calls this
+            p._ddl_on_grad = self._hook
 
     def _hook(self, p):
         if not self.enabled or not self.ctx.is_distributed:

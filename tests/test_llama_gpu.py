@@ -102,3 +102,29 @@ def test_llama_model_fwd_bwd_matches_fp32(cuda):
     lh.backward(); lc.backward()
     for (n, ph), (_, pc) in zip(mh.named_parameters(), mc.named_parameters()):
         assert _rel(pc.grad, ph.grad) < 5e-2, n
+
+
+def test_fused_grad_accumulation_and_bf16_shadow(cuda):
+    """FlatAdam(fused=True, bf16_shadow=True): weight grads accumulate straight into the flat grad
+    buffer and the GEMMs read the optimizer-refreshed bf16 shadow; three steps of two
+    micro-batches track the plain path (fresh grads + AccumulateGrad, per-forward casts)."""
+    from ddl25spring_amd.optim import FlatAdam
+    cfg = dict(vocab_size=512, dmodel=96, num_heads=2, n_layers=2, ctx_size=64)
+    models, opts = [], []
+    for fused in (False, True):
+        torch.manual_seed(0)
+        m = LLama(**cfg).to(cuda)
+        models.append(m)
+        opts.append(FlatAdam(m.parameters(), lr=1e-3, fused=fused, bf16_shadow=fused))
+    torch.manual_seed(1)
+    xs = [torch.randint(0, 512, (4, 64), device=cuda) for _ in range(3)]
+    for x in xs:
+        for m, opt in zip(models, opts):
+            opt.zero_grad()
+            for mb in x.chunk(2):
+                (causalLLMLoss(m(mb), mb) / 2).backward()
+            opt.step()
+    for (n, a), (_, b) in zip(models[0].named_parameters(), models[1].named_parameters()):
+        assert _rel(b, a) < 1e-2, n
+    # the shadow is the bf16 image of the updated weights
+    assert _rel(opts[1].shadow.float(), opts[1].data) < 1e-2
