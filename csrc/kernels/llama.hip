@@ -5,12 +5,12 @@
 //   ddl_rmsnorm_fwd/bwd   : one wave per row, rstd saved, gamma grad reduced per block then atomics
 //   ddl_swiglu_fwd/bwd    : h = silu(a) * b over the fused [a | b] projection
 //   ddl_add               : bf16 residual add
-//   ddl_attn_fwd/bwd      : causal attention with RoPE applied on the fly to q and k (so RoPE costs
-//                           no HBM pass), online softmax, log-sum-exp saved; backward recomputes P
-//                           (flash-attention style) in two kernels (dQ; dK+dV) and writes the
+//   ddl_attn_fwd/bwd      : causal flash attention on MFMA (16x16x16 bf16: head_dim 32/48/64/128
+//                           are all multiples of 16) with RoPE applied as q / k tiles are staged
+//                           (so RoPE costs no HBM pass), online softmax, log-sum-exp saved;
+//                           backward recomputes P in two kernels (dQ; dK+dV) and writes the
 //                           un-rotated gradients straight into the fused dQKV buffer.
-// Attention is VALU fp32 (head_dim 48 is not an MFMA K multiple and S=256 makes it ~1% of the
-// model's FLOPs); the projections / FFN / LM head run on the MFMA implicit-GEMM kernel.
+// The projections / FFN / LM head run on the MFMA implicit-GEMM conv kernel.
 #include "ddl_common.h"
 
 // ---------------------------------------------------------------------------------------------
@@ -222,27 +222,102 @@ DDL_API int ddl_add(const void* a, const void* b, void* y, long long n, hipStrea
 }
 
 // ---------------------------------------------------------------------------------------------
-// Causal attention. qkv: [B][S][3][H][HD] bf16 (the fused projection output), o: [B][S][H][HD],
-// lse: [B][H][S] fp32, rope: cos/sin tables [S][HD/2] fp32 (interleaved pairs (2i, 2i+1)).
-// Block = 64 query rows x 4 lanes per row (each lane owns HD/4 dims); K/V tiles of 64 keys in LDS.
-constexpr int QT = 64;
+// Causal attention on MFMA (v_mfma_f32_16x16x16_bf16, fp32 accumulate). qkv: [B][S][3][H][HD]
+// bf16 (the fused projection output), o / dout: [B][S][H][HD], lse / delta: [B][H][S] fp32, RoPE
+// tables cos/sin [S][HD/2] fp32 (interleaved pairs (2i, 2i+1)), applied as tiles are staged.
+// A workgroup owns 64 query rows (forward, dQ) or 64 key rows (dK/dV), each of its 4 waves 16 of
+// them. Every product is oriented so that the softmax-side tile an MFMA produces (accumulator:
+// lane l holds rows 4(l/16)+i of column l%16) is directly the B operand (lane l holds k-rows
+// 4(l/16)+j of column l%16) of the next MFMA:
+//   forward : S^T = K Q^T (keys x queries)  -> P^T   -> O^T  += V^T P^T
+//   dQ      : S^T = K Q^T, dP^T = V dO^T    -> dS^T  -> dQ^T += K^T dS^T
+//   dK, dV  : S = Q K^T,   dP = dO V^T      -> P, dS -> dV^T += dO^T P, dK^T += Q^T dS
+// so no computed tile is ever transposed; the staged K / V / Q / dO tiles are also written
+// transposed into LDS where they are A operands over the head dimension. Online softmax in the
+// exp2 domain; the backward recomputes P from the saved log-sum-exp (flash-attention 2).
+constexpr int AT = 64;  // rows per workgroup tile
+constexpr float LOG2E = 1.4426950408889634f;
 
-template <int HD>
-__device__ __forceinline__ void load_rot(const bf16_t* __restrict__ src, const float* __restrict__ cs,
-                                         const float* __restrict__ sn, int d0, float* out, bool rot) {
-  constexpr int DL = HD / 4;
+__device__ __forceinline__ f4v mma16(s4v a, s4v b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ s4v bf4(float a, float b, float c, float d) {
+  s4v r;
+  r[0] = (short)f2bf(a);
+  r[1] = (short)f2bf(b);
+  r[2] = (short)f2bf(c);
+  r[3] = (short)f2bf(d);
+  return r;
+}
+__device__ __forceinline__ s4v lds4(const bf16_t* p) { return *(const s4v*)p; }
+
+// dims d0..d0+3 (d0 % 4 == 0) of one row, RoPE-rotated when cs != nullptr
+__device__ __forceinline__ void row4(const bf16_t* row, const float* cs, const float* sn, int d0,
+                                     float* v) {
+  const i2v raw = *(const i2v*)(row + d0);
+  v[0] = lo_bf((uint32_t)raw[0]);
+  v[1] = hi_bf((uint32_t)raw[0]);
+  v[2] = lo_bf((uint32_t)raw[1]);
+  v[3] = hi_bf((uint32_t)raw[1]);
+  if (cs) {
 #pragma unroll
-  for (int k = 0; k < DL; k += 2) {
-    const float x0 = bf2f(src[d0 + k]), x1 = bf2f(src[d0 + k + 1]);
-    if (rot) {
-      const int pi = (d0 + k) >> 1;
-      const float c = cs[pi], s = sn[pi];
-      out[k] = x0 * c - x1 * s;
-      out[k + 1] = x0 * s + x1 * c;
-    } else {
-      out[k] = x0;
-      out[k + 1] = x1;
+    for (int p = 0; p < 2; ++p) {
+      const float c = cs[d0 / 2 + p], s = sn[d0 / 2 + p], x0 = v[2 * p], x1 = v[2 * p + 1];
+      v[2 * p] = x0 * c - x1 * s;
+      v[2 * p + 1] = x0 * s + x1 * c;
     }
+  }
+}
+
+// inverse rotation of a gradient's dims d0..d0+3 and bf16 store
+__device__ __forceinline__ void store4_unrot(bf16_t* dst, const float* cs, const float* sn, int d0,
+                                             const f4v& g, bool rot) {
+  float r[4] = {g[0], g[1], g[2], g[3]};
+  if (rot) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const float c = cs[d0 / 2 + p], s = sn[d0 / 2 + p], g0 = g[2 * p], g1 = g[2 * p + 1];
+      r[2 * p] = g0 * c + g1 * s;
+      r[2 * p + 1] = -g0 * s + g1 * c;
+    }
+  }
+  i2v v;
+  v[0] = (int)pack_bf2(r[0], r[1]);
+  v[1] = (int)pack_bf2(r[2], r[3]);
+  *(i2v*)(dst + d0) = v;
+}
+
+// Stage rows r0..r0+63 (row t at src + t*rs) into LDS: row-major [64][HD+4] and/or transposed
+// [HD][64+4] (the padded strides keep the 8-byte fragment reads bank-conflict free); rows >= S
+// are zeros.
+template <int HD>
+__device__ __forceinline__ void stage_rows(const bf16_t* src, long long rs, int r0, int S,
+                                           const float* rcos, const float* rsin, bf16_t* rm,
+                                           bf16_t* tr) {
+  constexpr int C4 = HD / 4, KP = HD + 4, VP = AT + 4;
+  for (int e = threadIdx.x; e < AT * C4; e += 256) {
+    const int r = e / C4, d0 = (e - r * C4) * 4, t = r0 + r;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (t < S)
+      row4(src + (long long)t * rs, rcos ? rcos + (long long)t * (HD / 2) : nullptr,
+           rsin ? rsin + (long long)t * (HD / 2) : nullptr, d0, v);
+    if (rm) *(s4v*)(rm + r * KP + d0) = bf4(v[0], v[1], v[2], v[3]);
+    if (tr) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) tr[(d0 + k) * VP + r] = f2bf(v[k]);
+    }
+  }
+}
+
+// this lane's B fragments of one row (dims 16t + 4(l/16) + j), zeros when !valid
+template <int HD>
+__device__ __forceinline__ void row_frags(const bf16_t* row, const float* cs, const float* sn,
+                                          int lg, bool valid, s4v* f) {
+#pragma unroll
+  for (int t = 0; t < HD / 16; ++t) {
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (valid) row4(row, cs, sn, 16 * t + 4 * lg, v);
+    f[t] = bf4(v[0], v[1], v[2], v[3]);
   }
 }
 
@@ -253,240 +328,219 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
                                                        const float* __restrict__ rcos,
                                                        const float* __restrict__ rsin, int S, int H,
                                                        float scale) {
-  constexpr int DL = HD / 4;
-  __shared__ float Ks[QT][HD + 1], Vs[QT][HD + 1];
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QT;
-  const int tid = threadIdx.x, qi = q0 + tid / 4, sub = tid & 3, d0 = sub * DL;
-  const long long rs = 3LL * H * HD;  // token stride in qkv
-  const bf16_t* base = qkv + (long long)b * S * rs;
-  float q[DL], acc[DL];
-  const bool valid = qi < S;
-  if (valid)
-    load_rot<HD>(base + (long long)qi * rs + 0 * H * HD + h * HD, rcos + (long long)qi * (HD / 2),
-                 rsin + (long long)qi * (HD / 2), d0, q, true);
+  constexpr int NT = HD / 16, KP = HD + 4, VP = AT + 4;
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[AT * KP];
+  __shared__ __attribute__((aligned(16))) bf16_t Vt[HD * VP];
+  const int b = blockIdx.z, h = blockIdx.y, qt = blockIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, lq = lane & 15, lg = lane >> 4;
+  const long long rs = 3LL * H * HD, ro = (long long)H * HD;
+  const bf16_t* base = qkv + (long long)b * S * rs + h * HD;
+  const int q = qt * AT + wv * 16 + lq, qmax = qt * AT + wv * 16 + 15;
+  const bool qv = q < S;
+  const float sl2 = scale * LOG2E;
+  s4v qf[NT];
+  row_frags<HD>(base + (long long)q * rs, rcos + (long long)q * (HD / 2),
+                rsin + (long long)q * (HD / 2), lg, qv, qf);
+  f4v acc[NT];
 #pragma unroll
-  for (int k = 0; k < DL; ++k) { acc[k] = 0.f; if (!valid) q[k] = 0.f; }
+  for (int t = 0; t < NT; ++t) acc[t] = f4v{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.f;
-  const int kend = min(S, q0 + QT);
-  for (int k0 = 0; k0 < kend; k0 += QT) {
+  for (int kt = 0; kt <= qt; ++kt) {
     __syncthreads();
-    for (int e = tid; e < QT * (HD / 2); e += 256) {
-      const int kr = e / (HD / 2), p = e % (HD / 2), kj = k0 + kr;
-      float kx0 = 0, kx1 = 0, vx0 = 0, vx1 = 0;
-      if (kj < S) {
-        const bf16_t* kp = base + (long long)kj * rs + 1 * H * HD + h * HD + 2 * p;
-        const bf16_t* vp = base + (long long)kj * rs + 2 * H * HD + h * HD + 2 * p;
-        const float c = rcos[(long long)kj * (HD / 2) + p], s = rsin[(long long)kj * (HD / 2) + p];
-        const float a0 = bf2f(kp[0]), a1 = bf2f(kp[1]);
-        kx0 = a0 * c - a1 * s;
-        kx1 = a0 * s + a1 * c;
-        vx0 = bf2f(vp[0]);
-        vx1 = bf2f(vp[1]);
+    stage_rows<HD>(base + ro, rs, kt * AT, S, rcos, rsin, Ks, nullptr);
+    stage_rows<HD>(base + 2 * ro, rs, kt * AT, S, nullptr, nullptr, nullptr, Vt);
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < AT / 16; ++ks) {
+      const int key0 = kt * AT + ks * 16;
+      if (key0 > qmax || key0 >= S) break;  // wave-uniform: the causal / sequence edge
+      f4v s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < NT; ++t) s = mma16(lds4(Ks + (ks * 16 + lq) * KP + 16 * t + 4 * lg), qf[t], s);
+      float x[4], mx = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = key0 + 4 * lg + i;
+        x[i] = (key <= q && key < S) ? s[i] * sl2 : -INFINITY;
+        mx = fmaxf(mx, x[i]);
       }
-      Ks[kr][2 * p] = kx0; Ks[kr][2 * p + 1] = kx1;
-      Vs[kr][2 * p] = vx0; Vs[kr][2 * p + 1] = vx1;
-    }
-    __syncthreads();
-    const int jmax = min(QT, kend - k0);
-    for (int jj = 0; jj < jmax; ++jj) {
-      const int kj = k0 + jj;
-      float s = 0.f;
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m, mx);
+      const float corr = (mn == -INFINITY) ? 1.f : exp2f(m - mn);
+      float p[4], ps = 0.f;
 #pragma unroll
-      for (int k = 0; k < DL; ++k) s += q[k] * Ks[jj][d0 + k];
-      s += __shfl_xor(s, 1, 64);
-      s += __shfl_xor(s, 2, 64);
-      s *= scale;
-      if (kj > qi) s = -INFINITY;
-      const float mn = fmaxf(m, s);
-      const float corr = (m == -INFINITY) ? 0.f : __expf(m - mn);
-      const float p = (s == -INFINITY) ? 0.f : __expf(s - mn);
-      l = l * corr + p;
-#pragma unroll
-      for (int k = 0; k < DL; ++k) acc[k] = acc[k] * corr + p * Vs[jj][d0 + k];
+      for (int i = 0; i < 4; ++i) {
+        p[i] = (x[i] == -INFINITY) ? 0.f : exp2f(x[i] - mn);
+        ps += p[i];
+      }
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      l = l * corr + ps;
       m = mn;
+      const s4v pb = bf4(p[0], p[1], p[2], p[3]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        acc[t] *= corr;
+        acc[t] = mma16(lds4(Vt + (16 * t + lq) * VP + ks * 16 + 4 * lg), pb, acc[t]);
+      }
     }
   }
-  if (valid) {
+  if (qv) {
     const float inv = 1.f / l;
-    bf16_t* op = o + ((long long)b * S + qi) * H * HD + h * HD + d0;
+    bf16_t* op = o + ((long long)b * S + q) * ro + h * HD;
 #pragma unroll
-    for (int k = 0; k < DL; ++k) op[k] = f2bf(acc[k] * inv);
-    if (sub == 0) lse[((long long)b * H + h) * S + qi] = m + __logf(l);
+    for (int t = 0; t < NT; ++t) store4_unrot(op, nullptr, nullptr, 16 * t + 4 * lg, acc[t] * inv, false);
+    if (lg == 0) lse[((long long)b * H + h) * S + q] = (m + log2f(l)) * 0.6931471805599453f;
   }
 }
 
-// dQ (+ delta = rowsum(dO*O)), un-rotated into dqkv's q slot
+// dQ (+ delta = rowsum(dO * O)), un-rotated into dqkv's q slot
 template <int HD>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout,
     const float* __restrict__ lse, float* __restrict__ delta, bf16_t* __restrict__ dqkv,
     const float* __restrict__ rcos, const float* __restrict__ rsin, int S, int H, float scale) {
-  constexpr int DL = HD / 4;
-  __shared__ float Ks[QT][HD + 1], Vs[QT][HD + 1];
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QT;
-  const int tid = threadIdx.x, qi = q0 + tid / 4, sub = tid & 3, d0 = sub * DL;
-  const long long rs = 3LL * H * HD;
-  const bf16_t* base = qkv + (long long)b * S * rs;
-  const bool valid = qi < S;
-  float q[DL], dq[DL], dov[DL];
-  float D = 0.f, L = 0.f;
-  if (valid) {
-    load_rot<HD>(base + (long long)qi * rs + h * HD, rcos + (long long)qi * (HD / 2),
-                 rsin + (long long)qi * (HD / 2), d0, q, true);
-    const bf16_t* op = o + ((long long)b * S + qi) * H * HD + h * HD + d0;
-    const bf16_t* dp = dout + ((long long)b * S + qi) * H * HD + h * HD + d0;
+  constexpr int NT = HD / 16, KP = HD + 4, VP = AT + 4;
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[AT * KP];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[AT * KP];
+  __shared__ __attribute__((aligned(16))) bf16_t Kt[HD * VP];
+  const int b = blockIdx.z, h = blockIdx.y, qt = blockIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, lq = lane & 15, lg = lane >> 4;
+  const long long rs = 3LL * H * HD, ro = (long long)H * HD;
+  const bf16_t* base = qkv + (long long)b * S * rs + h * HD;
+  const int q = qt * AT + wv * 16 + lq, qmax = qt * AT + wv * 16 + 15;
+  const bool qv = q < S;
+  const float sl2 = scale * LOG2E;
+  const float* cs = rcos + (long long)q * (HD / 2);
+  const float* sn = rsin + (long long)q * (HD / 2);
+  s4v qf[NT], df[NT];
+  row_frags<HD>(base + (long long)q * rs, cs, sn, lg, qv, qf);
+  const bf16_t* orow = o + ((long long)b * S + q) * ro + h * HD;
+  const bf16_t* drow = dout + ((long long)b * S + q) * ro + h * HD;
+  float dd = 0.f;
 #pragma unroll
-    for (int k = 0; k < DL; ++k) {
-      dov[k] = bf2f(dp[k]);
-      D += dov[k] * bf2f(op[k]);
+  for (int t = 0; t < NT; ++t) {
+    float dv[4] = {0.f, 0.f, 0.f, 0.f}, ov[4] = {0.f, 0.f, 0.f, 0.f};
+    if (qv) {
+      row4(drow, nullptr, nullptr, 16 * t + 4 * lg, dv);
+      row4(orow, nullptr, nullptr, 16 * t + 4 * lg, ov);
     }
-    L = lse[((long long)b * H + h) * S + qi];
-  } else {
-#pragma unroll
-    for (int k = 0; k < DL; ++k) { q[k] = 0.f; dov[k] = 0.f; }
+    df[t] = bf4(dv[0], dv[1], dv[2], dv[3]);
+    dd += dv[0] * ov[0] + dv[1] * ov[1] + dv[2] * ov[2] + dv[3] * ov[3];
   }
-  D += __shfl_xor(D, 1, 64);
-  D += __shfl_xor(D, 2, 64);
-  if (valid && sub == 0) delta[((long long)b * H + h) * S + qi] = D;
+  dd += __shfl_xor(dd, 16, 64);
+  dd += __shfl_xor(dd, 32, 64);
+  if (qv && lg == 0) delta[((long long)b * H + h) * S + q] = dd;
+  const float L2 = qv ? lse[((long long)b * H + h) * S + q] * LOG2E : 0.f;
+  f4v acc[NT];
 #pragma unroll
-  for (int k = 0; k < DL; ++k) dq[k] = 0.f;
-  const int kend = min(S, q0 + QT);
-  for (int k0 = 0; k0 < kend; k0 += QT) {
+  for (int t = 0; t < NT; ++t) acc[t] = f4v{0.f, 0.f, 0.f, 0.f};
+  for (int kt = 0; kt <= qt; ++kt) {
     __syncthreads();
-    for (int e = tid; e < QT * (HD / 2); e += 256) {
-      const int kr = e / (HD / 2), p = e % (HD / 2), kj = k0 + kr;
-      float kx0 = 0, kx1 = 0, vx0 = 0, vx1 = 0;
-      if (kj < S) {
-        const bf16_t* kp = base + (long long)kj * rs + 1 * H * HD + h * HD + 2 * p;
-        const bf16_t* vp = base + (long long)kj * rs + 2 * H * HD + h * HD + 2 * p;
-        const float c = rcos[(long long)kj * (HD / 2) + p], s = rsin[(long long)kj * (HD / 2) + p];
-        const float a0 = bf2f(kp[0]), a1 = bf2f(kp[1]);
-        kx0 = a0 * c - a1 * s;
-        kx1 = a0 * s + a1 * c;
-        vx0 = bf2f(vp[0]);
-        vx1 = bf2f(vp[1]);
-      }
-      Ks[kr][2 * p] = kx0; Ks[kr][2 * p + 1] = kx1;
-      Vs[kr][2 * p] = vx0; Vs[kr][2 * p + 1] = vx1;
-    }
+    stage_rows<HD>(base + ro, rs, kt * AT, S, rcos, rsin, Ks, Kt);
+    stage_rows<HD>(base + 2 * ro, rs, kt * AT, S, nullptr, nullptr, Vs, nullptr);
     __syncthreads();
-    const int jmax = min(QT, kend - k0);
-    for (int jj = 0; jj < jmax; ++jj) {
-      const int kj = k0 + jj;
-      float s = 0.f, dpv = 0.f;
 #pragma unroll
-      for (int k = 0; k < DL; ++k) {
-        s += q[k] * Ks[jj][d0 + k];
-        dpv += dov[k] * Vs[jj][d0 + k];
+    for (int ks = 0; ks < AT / 16; ++ks) {
+      const int key0 = kt * AT + ks * 16;
+      if (key0 > qmax || key0 >= S) break;
+      f4v s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        s = mma16(lds4(Ks + (ks * 16 + lq) * KP + 16 * t + 4 * lg), qf[t], s);
+        dp = mma16(lds4(Vs + (ks * 16 + lq) * KP + 16 * t + 4 * lg), df[t], dp);
       }
-      s += __shfl_xor(s, 1, 64);
-      s += __shfl_xor(s, 2, 64);
-      dpv += __shfl_xor(dpv, 1, 64);
-      dpv += __shfl_xor(dpv, 2, 64);
-      const float p = (kj > qi || !valid) ? 0.f : __expf(s * scale - L);
-      const float ds = p * (dpv - D) * scale;
+      float ds[4];
 #pragma unroll
-      for (int k = 0; k < DL; ++k) dq[k] += ds * Ks[jj][d0 + k];
+      for (int i = 0; i < 4; ++i) {
+        const int key = key0 + 4 * lg + i;
+        const float pr = (qv && key <= q && key < S) ? exp2f(s[i] * sl2 - L2) : 0.f;
+        ds[i] = pr * (dp[i] - dd) * scale;
+      }
+      const s4v db = bf4(ds[0], ds[1], ds[2], ds[3]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        acc[t] = mma16(lds4(Kt + (16 * t + lq) * VP + ks * 16 + 4 * lg), db, acc[t]);
     }
   }
-  if (valid) {
-    bf16_t* out = dqkv + ((long long)b * S + qi) * rs + h * HD + d0;
-    const float* cs = rcos + (long long)qi * (HD / 2);
-    const float* sn = rsin + (long long)qi * (HD / 2);
+  if (qv) {
+    bf16_t* out = dqkv + ((long long)b * S + q) * rs + h * HD;
 #pragma unroll
-    for (int k = 0; k < DL; k += 2) {  // inverse rotation (transpose)
-      const int pi = (d0 + k) >> 1;
-      const float c = cs[pi], s = sn[pi];
-      out[k] = f2bf(dq[k] * c + dq[k + 1] * s);
-      out[k + 1] = f2bf(-dq[k] * s + dq[k + 1] * c);
-    }
+    for (int t = 0; t < NT; ++t) store4_unrot(out, cs, sn, 16 * t + 4 * lg, acc[t], true);
   }
 }
 
-// dK, dV: block = 64 keys x 4 lanes, loop over query tiles >= key tile
+// dK, dV: a workgroup owns 64 keys and walks the query tiles at or after them
 template <int HD>
 __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, bf16_t* __restrict__ dqkv, const float* __restrict__ rcos,
     const float* __restrict__ rsin, int S, int H, float scale) {
-  constexpr int DL = HD / 4;
-  __shared__ float Qs[QT][HD + 1], Ds[QT][HD + 1];
-  __shared__ float Ls[QT], Dl[QT];
-  const int b = blockIdx.z, h = blockIdx.y, k0 = blockIdx.x * QT;
-  const int tid = threadIdx.x, kj = k0 + tid / 4, sub = tid & 3, d0 = sub * DL;
-  const long long rs = 3LL * H * HD;
-  const bf16_t* base = qkv + (long long)b * S * rs;
-  const bool valid = kj < S;
-  float kv[DL], vv[DL], dk[DL], dv[DL];
-  if (valid) {
-    load_rot<HD>(base + (long long)kj * rs + 1 * H * HD + h * HD, rcos + (long long)kj * (HD / 2),
-                 rsin + (long long)kj * (HD / 2), d0, kv, true);
-    load_rot<HD>(base + (long long)kj * rs + 2 * H * HD + h * HD, nullptr, nullptr, d0, vv, false);
-  } else {
+  constexpr int NT = HD / 16, KP = HD + 4, VP = AT + 4;
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[AT * KP];
+  __shared__ __attribute__((aligned(16))) bf16_t Ds[AT * KP];
+  __shared__ __attribute__((aligned(16))) bf16_t Qt[HD * VP];
+  __shared__ __attribute__((aligned(16))) bf16_t Dt[HD * VP];
+  __shared__ float Ls[AT], Dl[AT];
+  const int b = blockIdx.z, h = blockIdx.y, kt = blockIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, lq = lane & 15, lg = lane >> 4;
+  const long long rs = 3LL * H * HD, ro = (long long)H * HD;
+  const bf16_t* base = qkv + (long long)b * S * rs + h * HD;
+  const bf16_t* dbase = dout + (long long)b * S * ro + h * HD;
+  const int key = kt * AT + wv * 16 + lq, kmin = kt * AT + wv * 16;
+  const bool kv = key < S;
+  const float sl2 = scale * LOG2E;
+  const float* cs = rcos + (long long)key * (HD / 2);
+  const float* sn = rsin + (long long)key * (HD / 2);
+  s4v kf[NT], vf[NT];
+  row_frags<HD>(base + ro + (long long)key * rs, cs, sn, lg, kv, kf);
+  row_frags<HD>(base + 2 * ro + (long long)key * rs, nullptr, nullptr, lg, kv, vf);
+  f4v dk[NT], dv[NT];
 #pragma unroll
-    for (int k = 0; k < DL; ++k) { kv[k] = 0.f; vv[k] = 0.f; }
-  }
-#pragma unroll
-  for (int k = 0; k < DL; ++k) { dk[k] = 0.f; dv[k] = 0.f; }
-  for (int q0 = k0; q0 < S; q0 += QT) {
+  for (int t = 0; t < NT; ++t) dk[t] = dv[t] = f4v{0.f, 0.f, 0.f, 0.f};
+  for (int qt = kt; qt * AT < S; ++qt) {
     __syncthreads();
-    for (int e = tid; e < QT * (HD / 2); e += 256) {
-      const int qr = e / (HD / 2), p = e % (HD / 2), qi = q0 + qr;
-      float x0 = 0, x1 = 0, g0 = 0, g1 = 0;
-      if (qi < S) {
-        const bf16_t* qp = base + (long long)qi * rs + h * HD + 2 * p;
-        const bf16_t* dp = dout + ((long long)b * S + qi) * H * HD + h * HD + 2 * p;
-        const float c = rcos[(long long)qi * (HD / 2) + p], s = rsin[(long long)qi * (HD / 2) + p];
-        const float a0 = bf2f(qp[0]), a1 = bf2f(qp[1]);
-        x0 = a0 * c - a1 * s;
-        x1 = a0 * s + a1 * c;
-        g0 = bf2f(dp[0]);
-        g1 = bf2f(dp[1]);
-      }
-      Qs[qr][2 * p] = x0; Qs[qr][2 * p + 1] = x1;
-      Ds[qr][2 * p] = g0; Ds[qr][2 * p + 1] = g1;
-    }
-    for (int e = tid; e < QT; e += 256) {
-      const int qi = q0 + e;
-      Ls[e] = qi < S ? lse[((long long)b * H + h) * S + qi] : 0.f;
+    stage_rows<HD>(base, rs, qt * AT, S, rcos, rsin, Qs, Qt);
+    stage_rows<HD>(dbase, ro, qt * AT, S, nullptr, nullptr, Ds, Dt);
+    for (int e = threadIdx.x; e < AT; e += 256) {
+      const int qi = qt * AT + e;
+      Ls[e] = qi < S ? lse[((long long)b * H + h) * S + qi] * LOG2E : 0.f;
       Dl[e] = qi < S ? delta[((long long)b * H + h) * S + qi] : 0.f;
     }
     __syncthreads();
-    const int imax = min(QT, S - q0);
-    for (int ii = 0; ii < imax; ++ii) {
-      const int qi = q0 + ii;
-      float s = 0.f, dpv = 0.f;
 #pragma unroll
-      for (int k = 0; k < DL; ++k) {
-        s += Qs[ii][d0 + k] * kv[k];
-        dpv += Ds[ii][d0 + k] * vv[k];
+    for (int qs = 0; qs < AT / 16; ++qs) {
+      const int q0 = qt * AT + qs * 16;
+      if (q0 >= S) break;
+      if (q0 + 15 < kmin) continue;  // every query of the subtile precedes every key of the wave
+      f4v s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        s = mma16(lds4(Qs + (qs * 16 + lq) * KP + 16 * t + 4 * lg), kf[t], s);
+        dp = mma16(lds4(Ds + (qs * 16 + lq) * KP + 16 * t + 4 * lg), vf[t], dp);
       }
-      s += __shfl_xor(s, 1, 64);
-      s += __shfl_xor(s, 2, 64);
-      dpv += __shfl_xor(dpv, 1, 64);
-      dpv += __shfl_xor(dpv, 2, 64);
-      const float p = (qi < kj || !valid) ? 0.f : __expf(s * scale - Ls[ii]);
-      const float ds = p * (dpv - Dl[ii]) * scale;
+      float p[4], ds[4];
 #pragma unroll
-      for (int k = 0; k < DL; ++k) {
-        dv[k] += p * Ds[ii][d0 + k];
-        dk[k] += ds * Qs[ii][d0 + k];
+      for (int i = 0; i < 4; ++i) {
+        const int r = qs * 16 + 4 * lg + i, qi = qt * AT + r;
+        p[i] = (kv && qi >= key && qi < S) ? exp2f(s[i] * sl2 - Ls[r]) : 0.f;
+        ds[i] = p[i] * (dp[i] - Dl[r]) * scale;
+      }
+      const s4v pb = bf4(p[0], p[1], p[2], p[3]), db = bf4(ds[0], ds[1], ds[2], ds[3]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        dv[t] = mma16(lds4(Dt + (16 * t + lq) * VP + qs * 16 + 4 * lg), pb, dv[t]);
+        dk[t] = mma16(lds4(Qt + (16 * t + lq) * VP + qs * 16 + 4 * lg), db, dk[t]);
       }
     }
   }
-  if (valid) {
-    bf16_t* ko = dqkv + ((long long)b * S + kj) * rs + 1 * H * HD + h * HD + d0;
-    bf16_t* vo = dqkv + ((long long)b * S + kj) * rs + 2 * H * HD + h * HD + d0;
-    const float* cs = rcos + (long long)kj * (HD / 2);
-    const float* sn = rsin + (long long)kj * (HD / 2);
+  if (kv) {
+    bf16_t* ko = dqkv + ((long long)b * S + key) * rs + ro + h * HD;
 #pragma unroll
-    for (int k = 0; k < DL; k += 2) {
-      const int pi = (d0 + k) >> 1;
-      const float c = cs[pi], s = sn[pi];
-      ko[k] = f2bf(dk[k] * c + dk[k + 1] * s);
-      ko[k + 1] = f2bf(-dk[k] * s + dk[k + 1] * c);
-      vo[k] = f2bf(dv[k]);
-      vo[k + 1] = f2bf(dv[k + 1]);
+    for (int t = 0; t < NT; ++t) {
+      store4_unrot(ko, cs, sn, 16 * t + 4 * lg, dk[t], true);
+      store4_unrot(ko + ro, nullptr, nullptr, 16 * t + 4 * lg, dv[t], false);
     }
   }
 }
@@ -502,7 +556,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
 
 DDL_API int ddl_attn_fwd(const void* qkv, void* o, float* lse, const float* rcos, const float* rsin,
                          int B, int S, int H, int HD, float scale, hipStream_t s) {
-  dim3 grid((S + QT - 1) / QT, H, B);
+  dim3 grid((S + AT - 1) / AT, H, B);
   ATTN_DISPATCH(attn_fwd_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, (bf16_t*)o, lse, rcos,
                 rsin, S, H, scale)
   return (int)hipGetLastError();
@@ -511,7 +565,7 @@ DDL_API int ddl_attn_fwd(const void* qkv, void* o, float* lse, const float* rcos
 DDL_API int ddl_attn_bwd(const void* qkv, const void* o, const void* dout, const float* lse,
                          float* delta, void* dqkv, const float* rcos, const float* rsin, int B, int S,
                          int H, int HD, float scale, hipStream_t s) {
-  dim3 grid((S + QT - 1) / QT, H, B);
+  dim3 grid((S + AT - 1) / AT, H, B);
   ATTN_DISPATCH(attn_bwd_dq_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, (const bf16_t*)o,
                 (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, rcos, rsin, S, H, scale)
   ATTN_DISPATCH(attn_bwd_dkv_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, (const bf16_t*)dout,

@@ -72,11 +72,20 @@ struct AdamArgs {
   float lr, beta1, beta2, eps, wd, grad_scale;
   float bc1, bc2;  // 1 - beta^t
   int decoupled, amsgrad_unused;
+  // optional device step counter (advanced by ddl_u64_add before the launch): the bias corrections
+  // are then computed on the device, so a captured HIP graph stays exact on every replay
+  const unsigned long long* step_dev;
 };
 
 __global__ void adam_kernel(AdamArgs a) {
-  const float sbc2 = sqrtf(a.bc2);
-  const float step = a.lr / a.bc1;
+  float bc1 = a.bc1, bc2 = a.bc2;
+  if (a.step_dev) {
+    const float t = (float)*a.step_dev;
+    bc1 = 1.f - powf(a.beta1, t);
+    bc2 = 1.f - powf(a.beta2, t);
+  }
+  const float sbc2 = sqrtf(bc2);
+  const float step = a.lr / bc1;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < a.n;
        e += (long long)gridDim.x * blockDim.x) {
     float p = a.p[e];

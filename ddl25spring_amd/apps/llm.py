@@ -42,6 +42,7 @@ class LLMConfig:
     bucket_mb: float = 25.0
     log_every: int = 10
     fused_adam: bool = True
+    graph: bool = True  # dp = pp = 1 on a GPU: replay the whole step (fwd, bwd, Adam) as a HIP graph
 
 
 class _PinnedH2D:
@@ -100,9 +101,51 @@ def train_llm(cfg: LLMConfig, ctx, log=print, warmup: int = 0) -> dict:
     h2d = _PinnedH2D((cfg.batch_size, cfg.ctx_size), torch.int64, dev) if dev.type == "cuda" else None
     losses = []
 
+    use_graph = (cfg.graph and dev.type == "cuda" and cfg.dp == 1 and cfg.pp == 1
+                 and hasattr(opt, "t_dev"))
+    gstate: dict = {}
+
+    def body(xd):  # one dp = pp = 1 step on a static input buffer (capturable: no host syncs)
+        opt.zero_grad()
+        loss = None
+        for m in torch.chunk(xd, cfg.micro_batches):
+            l = causalLLMLoss(mod(m), m) / cfg.micro_batches
+            l.backward()
+            loss = l.detach() if loss is None else loss + l.detach()
+        opt.step()
+        return loss
+
+    def graph_step(xd):
+        if not gstate:
+            sx = xd.clone()
+            # the warm-up steps really train: snapshot the optimizer state and restore it after
+            # capture, so the first replay is exactly step 1
+            snap = [t.clone() for t in (opt.data, opt.m, opt.v, opt.t_dev)]
+            t_host = opt.t
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    body(sx)
+            torch.cuda.current_stream().wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                out = body(sx)
+            for t, v in zip((opt.data, opt.m, opt.v, opt.t_dev), snap):
+                t.copy_(v)
+            opt.t = t_host
+            opt.sync_shadow()
+            gstate.update(g=g, x=sx, loss=out)
+        gstate["x"].copy_(xd)
+        gstate["g"].replay()
+        opt.t += 1
+        return gstate["loss"]
+
     def step():
         x = next(stream)
         x = h2d(x) if h2d is not None else x.to(dev)
+        if use_graph:
+            return graph_step(x)
         if sync is not None:
             sync.zero_grad()
         else:

@@ -598,7 +598,10 @@ def sgd_step(p, g, mom, shadow, lr, wd=0.0, momentum=0.0, dampening=0.0, nestero
     check(_lib.kernels().ddl_sgd(ctypes.byref(a), stream()), "sgd")
 
 
-def adam_step(p, g, m, v, shadow, lr, beta1, beta2, eps, wd, step, decoupled, grad_scale=1.0):
+def adam_step(p, g, m, v, shadow, lr, beta1, beta2, eps, wd, step, decoupled, grad_scale=1.0,
+              step_dev=None):
+    """One fused Adam/AdamW pass over flat buffers. ``step_dev`` (int64 [1] on the device, already
+    advanced to this step) makes the bias correction device-side (HIP-graph capturable)."""
     if not p.is_cuda:
         ref.adam(p, g, m, v, shadow, lr, beta1, beta2, eps, wd, step, decoupled, grad_scale)
         return
@@ -608,6 +611,7 @@ def adam_step(p, g, m, v, shadow, lr, beta1, beta2, eps, wd, step, decoupled, gr
     a.lr, a.beta1, a.beta2, a.eps, a.wd, a.grad_scale = lr, beta1, beta2, eps, wd, grad_scale
     a.bc1, a.bc2 = 1 - beta1 ** step, 1 - beta2 ** step
     a.decoupled = int(decoupled)
+    a.step_dev = ptr(step_dev)
     check(_lib.kernels().ddl_adam(ctypes.byref(a), stream()), "adam")
 
 

@@ -141,6 +141,8 @@ class FlatAdam:
         self.v = torch.zeros_like(self.data)
         self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
         self.decoupled, self.t = decoupled, 0
+        # device-side step counter: the update stays exact when captured in a HIP graph
+        self.t_dev = torch.zeros(1, dtype=torch.int64, device=dev) if dev.type == "cuda" else None
         self.shadow = None
         if bf16_shadow and dev.type == "cuda":
             self.shadow = torch.empty(n, dtype=torch.bfloat16, device=dev)
@@ -173,8 +175,11 @@ class FlatAdam:
                 # leave p.grad pointing where the bucketer (and fused backward) accumulate
                 g.copy_(p.grad)
         self.t += 1
+        if self.t_dev is not None:
+            Fn.u64_add(self.t_dev, 1)
         Fn.adam_step(self.data, self.grad, self.m, self.v, self.shadow, self.lr, self.betas[0],
-                     self.betas[1], self.eps, self.weight_decay, self.t, self.decoupled)
+                     self.betas[1], self.eps, self.weight_decay, self.t, self.decoupled,
+                     step_dev=self.t_dev)
 
 
 class FlatAdamW(FlatAdam):
