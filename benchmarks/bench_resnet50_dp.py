@@ -56,10 +56,18 @@ def main():
 
     dt = timed(ctx, step, args.steps, args.warmup)
     ips = ctx.world * args.batch * args.steps / dt
+    # all-reduce bus bandwidth on the gradient buffer itself (25.6M fp32), as the rccl-tests
+    # convention: busbw = bytes / t * 2 (W - 1) / W; no communication at W = 1
+    busbw = None
+    if ctx.world > 1:
+        g = net.store.grad
+        t_ar = timed(ctx, lambda: ctx.all_reduce(g), 10, 3)
+        busbw = g.numel() * 4 * 10 / t_ar * 2 * (ctx.world - 1) / ctx.world / 1e9
     emit(ctx, metric="ResNet-50 DP all-reduce SGD images/s (ImageNet-shape)", value=round(ips, 1),
          unit="images/s", n_gpus=ctx.world, steps=args.steps, warmup=args.warmup,
          ms_per_step=round(1e3 * dt / args.steps, 3), higher_is_better=True, scaling="weak",
          vs_baseline=None, dtype="bf16", data="synthetic",
+         allreduce_busbw_GBps=None if busbw is None else round(busbw, 1),
          config={"model": "resnet50-imagenet", "global_batch": ctx.world * args.batch,
                  "seq_len": None, "parallelism": f"dp{ctx.world}", "per_gpu_batch": args.batch})
     rdist.shutdown()
