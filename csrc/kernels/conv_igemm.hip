@@ -39,6 +39,8 @@
 // (reference lab/tutorial_1a/hfl_complete.py:43-61) and the ResNets of the north-star configs.
 #include "ddl_common.h"
 
+#include <cstdlib>
+
 struct ConvArgs {
   const void* x;         // [G][N][H][W][C] bf16
   const void* w;         // [G][K][R][S][C] bf16
@@ -136,9 +138,26 @@ __device__ __forceinline__ void cta_barrier() {
 //                        k-row + L/(COLS/8), phys chunk L%(COLS/8)
 // WLP = waves along P (1, 2 or 4; the other 4/WLP waves split Q). 2x2 is the default; 1x4 gives
 // a 64-channel tile (layer-1 convs) 64x64 per wave instead of 32x(BQ/2).
-template <int MODE, int BP, int BQ, int BK, int NS, int WLP = 2>
+//
+// HALO (FWD / DGRAD of 3x3, stride 1, pad 1 convs whose BQ-pixel tile is whole image rows): the
+// activation operand is NOT streamed per K-step. The reduction runs channel-block-major (32
+// channels, then the 9 taps), and per channel block the tile's rows plus a one-pixel halo
+// ((BQ/W + 2) x (W + 2) pixels x 32 channels) are DMA'd into LDS once; the 9 taps read shifted
+// windows of that image. The 9x per-tap re-fetch of the activations through L2 -> LDS-DMA was the
+// bound of the streamed kernel on the 32x32 / 16x16 layers (PMC: MFMA busy ~20%, L2 -> CU reads
+// ~9x the activation bytes). The next block's halo is DMA'd one piece per K-step during taps
+// NS-1 .. of the current block into the other of two halo buffers; the weight operand keeps
+// the NS-deep per-step ring. Halo image: 64 B per pixel, 16-B chunk c stored at c ^ 2*((pixel>>2)&1):
+// for the ds_read_b128 lane groups ({0-3,12-15,20-27}, ...) every window of 16 consecutive
+// pixels, at any shift (every tap of a fragment on >= 16-wide rows), reads conflict-free.
+template <int MODE, int BP, int BQ, int BK, int NS, int WLP = 2, bool HALO = false>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   constexpr int P_BYTES = BP * BK * 2, Q_BYTES = BQ * BK * 2, STAGE = P_BYTES + Q_BYTES;
+  static_assert(!HALO || (MODE != MODE_WGRAD && BK == 32 && NS >= 4), "halo: FWD/DGRAD, BK 32, >= 4 stages");
+  // halo pieces (1 KiB DMA wave-instructions) per wave: issued at taps NS-1 .. 8 of a block
+  constexpr int HPW_MAX = HALO ? (BQ >= 256 ? 10 - NS : (10 - NS < 4 ? 10 - NS : 4)) : 0;
+  constexpr int HALO_BYTES = HPW_MAX * 4 * 1024;
+  constexpr int SMEM_BYTES = HALO ? NS * P_BYTES + 2 * HALO_BYTES : NS * STAGE;
   constexpr int WP = BP / WLP, WQ = BQ / (4 / WLP), TP = WP / 16, TQ = WQ / 16;
   static_assert(WLP == 1 || WLP == 2 || WLP == 4, "4 waves");
   constexpr bool P_KMAJOR = (MODE == MODE_FWD);
@@ -148,7 +167,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   constexpr int LPS = P_PW + Q_PW;                           // DMA instructions per wave per stage
   static_assert(P_PW >= 1 && Q_PW >= 1, "tile too small");
 
-  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
+  __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wp = wid / (4 / WLP), wq = wid % (4 / WLP);
@@ -245,6 +264,163 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         p_base[i] = col < K ? kr * K + col : -1;
     }
   }
+  f4v acc[TP][TQ];
+#pragma unroll
+  for (int i = 0; i < TP; ++i)
+#pragma unroll
+    for (int j = 0; j < TQ; ++j) acc[i][j] = (f4v){0.f, 0.f, 0.f, 0.f};
+  auto mfma_all = [&](const s8v* pf, const s8v* qf) {
+#pragma unroll
+    for (int ti = 0; ti < TP; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < TQ; ++tj)
+        acc[ti][tj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[ti], qf[tj], acc[ti][tj], 0, 0, 0);
+  };
+
+  if constexpr (HALO) {
+    // host contract (halo_ok): stride 1, R = S = 3, pad 1, P = H, Q = W, tiles of whole rows of
+    // one image or of whole images, halo pieces per wave <= HPW_MAX; no split-K, no phases.
+    // The tile is TRh whole rows of one image (BQ <= H*W) or BQ/(H*W) whole images; its halo
+    // image holds one (TRh+2) x (W+2) segment per image covered.
+    const int CRh = (MODE == MODE_FWD) ? C : K;  // channels of the staged activation
+    const int ncb = CRh >> 5;
+    const int W2 = W + 2, TRh = min(BQ / W, H);
+    const int HS = (TRh + 2) * W2, TPX = TRh * W;  // halo / output pixels per segment
+    const int hpx = (BQ / TPX) * HS;
+    const int hpw = (((hpx + 15) >> 4) + 3) >> 2;  // pieces per wave
+    const int img = q0 / (H * W);
+    const int row0 = (q0 - img * H * W) / W;
+    const int img_base = img * H * W;
+    const __amdgpu_buffer_rsrc_t rA = (MODE == MODE_FWD) ? rX : rD;
+    char* const halo0 = smem + NS * P_BYTES;
+
+    // Everything per lane that does not change with the channel block is computed once, so the
+    // K-steps (taps fully unrolled) carry no address arithmetic beyond a scalar base:
+    //   hsrc[j]     source element offset (block 0) of this lane's 16 B of halo piece j, -1 = zero;
+    //   qoff[r][t]  LDS byte offset, inside a halo image, of Q fragment t for tap r.
+    int hsrc[HPW_MAX];
+    {
+      const FastDiv div_w2 = make_fdiv(W2), div_hs = make_fdiv(HS);
+#pragma unroll
+      for (int j = 0; j < HPW_MAX; ++j) {
+        const int hp = (wsc + 4 * j) * 16 + (lane >> 2);
+        const int seg = fdiv(hp, div_hs), sp = hp - seg * HS;
+        const int hr = fdiv(sp, div_w2), hc = sp - hr * W2;
+        const int h = row0 - 1 + hr, w = hc - 1;
+        const int lc = (lane & 3) ^ (((hp >> 2) & 1) << 1);
+        const bool ok = (j < hpw) & (hp < hpx) & ((unsigned)h < (unsigned)H) & ((unsigned)w < (unsigned)W);
+        hsrc[j] = ok ? (img_base + seg * H * W + h * W + w) * CRh + lc * 8 : -1;
+      }
+    }
+    int qoff[9][TQ];
+#pragma unroll
+    for (int t = 0; t < TQ; ++t) {
+      const int lpix = wq * WQ + t * 16 + (lane & 15);
+      const int seg = lpix / TPX, sp = lpix - seg * TPX;
+      const int th = sp / W, tw = sp - th * W;
+      const int hq = seg * HS + th * W2 + tw;
+#pragma unroll
+      for (int r = 0; r < 9; ++r) {
+        const int tr = r / 3, ts = r % 3;
+        const int hp = hq + ((MODE == MODE_FWD) ? tr * W2 + ts : (2 - tr) * W2 + (2 - ts));
+        qoff[r][t] = hp * 64 + (((lane >> 4) ^ (((hp >> 2) & 1) << 1)) << 4);
+      }
+    }
+
+    // DMA ops a stage issues per wave: its weight pieces + one halo piece at taps NS-1 .. NS-2+hpw
+    auto stage_ops = [&](int s) {
+      const int t = s % 9 - (NS - 1);
+      return P_PW + ((t >= 0) & (t < hpw) ? 1 : 0);
+    };
+    // ops issued after stage s0 up to stage s1 (inclusive, clipped to the last stage)
+    auto ops_between = [&](int s0, int s1, int nkk) {
+      int n = 0;
+      for (int s = s0 + 1; s <= s1 && s < nkk; ++s) n += stage_ops(s);
+      return n;
+    };
+    // s_waitcnt vmcnt needs an immediate: dispatch the (wave-uniform) count
+    auto wait_dyn = [&](int n) {
+      switch (n) {
+        case 0: wait_vm<0>(); break;
+        case 1: wait_vm<1>(); break;
+        case 2: wait_vm<2>(); break;
+        case 3: wait_vm<3>(); break;
+        case 4: wait_vm<4>(); break;
+        case 5: wait_vm<5>(); break;
+        case 6: wait_vm<6>(); break;
+        case 7: wait_vm<7>(); break;
+        default: wait_vm<0>(); break;  // conservative
+      }
+    };
+    // stage (scb, stap): the weights of tap stap / channel block scb into ring slot `slot`, and
+    // piece stap-(NS-1) of block scb+1's halo (taps NS-1.. only: the other halo buffer's last
+    // reader, block scb-1, has then retired on every wave)
+    auto issue_h = [&](int slot, int scb, int stap) {
+      char* Ps = smem + slot * P_BYTES;
+      const int pcur = (MODE == MODE_FWD) ? stap * C + scb * 32 : scb * 32 * RSC + stap * C;
+#pragma unroll
+      for (int i = 0; i < P_PW; ++i) {
+        const unsigned off = p_base[i] >= 0 ? (unsigned)(p_base[i] + pcur) * 2u : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rP, (__attribute__((address_space(3))) void*)(Ps + (wsc + 4 * i) * 1024), 16, off, 0, 0, 0);
+      }
+      const int j = stap - (NS - 1);
+      if (j >= 0 && j < HPW_MAX && j < hpw) {
+        const int src = hsrc[j < HPW_MAX ? j : 0];
+        const unsigned off = (src >= 0 && scb + 1 < ncb) ? (unsigned)(src + (scb + 1) * 32) * 2u : OOB;
+        char* hb = halo0 + ((scb + 1) & 1) * HALO_BYTES + (wsc + 4 * j) * 1024;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (__attribute__((address_space(3))) void*)hb, 16, off,
+                                                 0, 0, 0);
+      }
+    };
+    auto load_frags_h = [&](int slot, const char* hb, int tap, s8v* pf, s8v* qf) {
+      const char* Ps = smem + slot * P_BYTES;
+#pragma unroll
+      for (int t = 0; t < TP; ++t) {
+        if constexpr (P_KMAJOR) pf[t] = km_frag<BP>(Ps, wp * WP + t * 16, 0, lane);
+        else pf[t] = mn_frag<BP>(Ps, wp * WP + t * 16, 0, lane);
+      }
+#pragma unroll
+      for (int t = 0; t < TQ; ++t) qf[t] = *(const s8v*)(hb + qoff[tap][t]);
+    };
+
+    const int nkh = ncb * 9;
+    // prologue: block 0's halo, then stages 0 .. NS-2 (block 0, taps 0 .. NS-2)
+#pragma unroll
+    for (int j = 0; j < HPW_MAX; ++j) {
+      if (j < hpw) {
+        const unsigned off = hsrc[j] >= 0 ? (unsigned)hsrc[j] * 2u : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rA, (__attribute__((address_space(3))) void*)(halo0 + (wsc + 4 * j) * 1024), 16, off, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s) issue_h(s, 0, s);
+    wait_dyn(ops_between(0, NS - 2, nkh));  // retire stage 0 (and the halo before it)
+    cta_barrier();
+    s8v pfA[TP], qfA[TQ], pfB[TP], qfB[TQ];
+    load_frags_h(0, halo0, 0, pfA, qfA);
+    for (int cb = 0; cb < ncb; ++cb) {
+      const char* hb = halo0 + (cb & 1) * HALO_BYTES;
+      const char* hbn = halo0 + ((cb + 1) & 1) * HALO_BYTES;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int i = cb * 9 + tap;
+        wait_dyn(ops_between(i + 1, i + NS - 2, nkh));  // retire stage i+1; stages i+2.. may fly
+        cta_barrier();
+        if (i + NS - 1 < nkh) {
+          issue_h((i + NS - 1) % NS, cb + (tap + NS - 1) / 9, (tap + NS - 1) % 9);
+        }
+        // the next step's fragments (past the last step: a stale read, unused)
+        load_frags_h((i + 1) % NS, tap == 8 ? hbn : hb, tap == 8 ? 0 : tap + 1, pfB, qfB);
+        mfma_all(pfA, qfA);
+#pragma unroll
+        for (int t = 0; t < TP; ++t) pfA[t] = pfB[t];
+#pragma unroll
+        for (int t = 0; t < TQ; ++t) qfA[t] = qfB[t];
+      }
+    }
+  } else {
   // Q operand
   int q_base[Q_PW], q_h[Q_PW], q_w[Q_PW];
 #pragma unroll
@@ -405,12 +581,6 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     }
   };
 
-  f4v acc[TP][TQ];
-#pragma unroll
-  for (int i = 0; i < TP; ++i)
-#pragma unroll
-    for (int j = 0; j < TQ; ++j) acc[i][j] = (f4v){0.f, 0.f, 0.f, 0.f};
-
   auto load_frags = [&](const char* Ps, int u, s8v* pf, s8v* qf) {
     const char* Qs = Ps + P_BYTES;
 #pragma unroll
@@ -424,14 +594,6 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       else qf[t] = mn_frag<BQ>(Qs, wq * WQ + t * 16, u, lane);
     }
   };
-  auto mfma_all = [&](const s8v* pf, const s8v* qf) {
-#pragma unroll
-    for (int ti = 0; ti < TP; ++ti)
-#pragma unroll
-      for (int tj = 0; tj < TQ; ++tj)
-        acc[ti][tj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[ti], qf[tj], acc[ti][tj], 0, 0, 0);
-  };
-
   // prologue: stages 0 .. NS-2 in flight
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
@@ -489,6 +651,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       }
     }
   }
+  }  // !HALO
 
   // ---------------- epilogue ----------------
   const int lq = lane & 15, lp = 4 * (lane >> 4);
@@ -752,11 +915,11 @@ static hipError_t splitk_epilogue(const ConvArgs& a, int mode, int Pd, long long
   return hipGetLastError();
 }
 
-template <int MODE, int BP, int BQ, int BK, int NS, int WLP = 2>
+template <int MODE, int BP, int BQ, int BK, int NS, int WLP = 2, bool HALO = false>
 static hipError_t launch_cfg(const ConvArgs& a, int Pd, int Qd, int gy, hipStream_t stream) {
   const int ntp = (Pd + BP - 1) / BP, ntq = (Qd + BQ - 1) / BQ;
   dim3 grid(ntp * ntq, gy, a.G);
-  hipLaunchKernelGGL((conv_igemm_kernel<MODE, BP, BQ, BK, NS, WLP>), grid, dim3(256), 0, stream, a);
+  hipLaunchKernelGGL((conv_igemm_kernel<MODE, BP, BQ, BK, NS, WLP, HALO>), grid, dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 
@@ -782,6 +945,43 @@ static hipError_t dispatch(const ConvArgs& a, int Pd, int Qd, int bp, int bq, in
   DDL_CFG1(256, 32, 4) DDL_CFG1(256, 64, 3) DDL_CFG1(256, 64, 2) DDL_CFG1(256, 32, 3)
 #undef DDL_CFG1
   return hipErrorInvalidValue;
+}
+
+// Halo-staged 3x3 stride-1 FWD / DGRAD (BK = 32); bp = 48 again selects 64 with 1x4 waves.
+template <int MODE>
+static hipError_t dispatch_halo(const ConvArgs& a, int Pd, int Qd, int bp, int bq, int ns, hipStream_t s) {
+#define DDL_HCFG(BP_, BQ_, NS_, BPE_, WLP_) \
+  if (bp == BP_ && bq == BQ_ && ns == NS_) \
+    return launch_cfg<MODE, BPE_, BQ_, 32, NS_, WLP_, true>(a, Pd, Qd, 1, s);
+  DDL_HCFG(48, 256, 4, 64, 1) DDL_HCFG(48, 128, 4, 64, 1) DDL_HCFG(64, 128, 4, 64, 2)
+  DDL_HCFG(128, 128, 4, 128, 2) DDL_HCFG(128, 256, 4, 128, 2) DDL_HCFG(48, 256, 5, 64, 1)
+  DDL_HCFG(48, 128, 6, 64, 1) DDL_HCFG(128, 128, 6, 128, 2)
+#undef DDL_HCFG
+  return hipErrorInvalidValue;
+}
+
+// Halo eligibility (the kernel's HALO contract): 3x3 / stride 1 / pad 1 with same-size output,
+// tiles of whole rows inside one image or of whole images, and a halo image that fits the pieces the taps of one
+// channel block can issue (NS-1 .. 8) and the LDS buffer (4 pieces per wave at BQ 128).
+static bool halo_ok(const ConvArgs& a, int bq, int ns) {
+  if (a.stride != 1 || a.R != 3 || a.S != 3 || a.pad != 1 || a.P != a.H || a.Q != a.W) return false;
+  const int hw = a.H * a.W;
+  if (hw >= bq ? (bq % a.W || hw % bq) : bq % hw) return false;  // whole rows / whole images
+  const int trh = bq / a.W < a.H ? bq / a.W : a.H;
+  const int hpx = bq / (trh * a.W) * (trh + 2) * (a.W + 2);
+  const int hpw = ((hpx + 15) / 16 + 3) / 4;
+  const int cap = bq >= 256 ? 10 - ns : (10 - ns < 4 ? 10 - ns : 4);
+  return hpw <= cap;
+}
+
+// DDL_CONV_HALO=0 disables the halo kernels' automatic use (explicit cfgs still run them)
+static bool halo_auto() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DDL_CONV_HALO");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
 }
 
 static int num_cus() {
@@ -815,8 +1015,8 @@ static void decode_cfg(int cfg, int& bp, int& bq, int& bk, int& ns) {
   bp = (cfg & 0xff) * 16;
   bq = ((cfg >> 8) & 0xff) * 16;
   bk = (cfg >> 16) & 0xff;
-  ns = (cfg >> 24) & 0xff;
-  if (!ns) ns = bk == 32 ? 4 : 3;
+  ns = (cfg >> 24) & 0xff;  // bit 0x40: halo-staged kernel
+  if (!(ns & 0x3f)) ns |= bk == 32 ? 4 : 3;
 }
 
 // Grid-size-aware fallback (G=1 sweep, profiles/conv_sweep_g1.log): when the tuned tile leaves
@@ -864,7 +1064,20 @@ DDL_API int ddl_conv_fwd(const ConvArgs* ap, int cfg, hipStream_t stream) {
   int bp = 64, bq = 128, bk = 32, ns = 4;
   if (a.K >= 128 && a.C % 64 == 0) { bp = 128; bk = 64; ns = 2; }
   small_grid_tiles(Pd, Qd, a.G, a.C % 64 == 0, bp, bq, bk, ns);
-  decode_cfg(cfg, bp, bq, bk, ns);
+  bool halo = false;
+  if (cfg) {
+    decode_cfg(cfg, bp, bq, bk, ns);
+    halo = ns & 0x40;
+    ns &= 0x3f;
+  } else if (halo_auto()) {
+    // sweep (profiles/conv_halo_sweep_r1_g8.log): 64 x 256 tiles, 4 waves along Q
+    const long long ht = (long long)((Pd + 63) / 64) * (Qd / 256) * a.G;
+    if (halo_ok(a, 256, 4) && ht >= num_cus()) { halo = true; bp = 48; bq = 256; bk = 32; ns = 4; }
+  }
+  if (halo) {
+    if (!halo_ok(a, bq, ns) || bk != 32) return (int)hipErrorInvalidValue;
+    return (int)dispatch_halo<MODE_FWD>(a, Pd, Qd, bp, bq, ns, stream);
+  }
   if (a.C % bk) return (int)hipErrorInvalidValue;
   const int bpe = bp == 48 ? 64 : bp;
   const long long tiles = (long long)((Pd + bpe - 1) / bpe) * ((Qd + bq - 1) / bq) * a.G;
@@ -885,7 +1098,20 @@ DDL_API int ddl_conv_dgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
   int bp = 64, bq = 128, bk = 32, ns = 4;
   if (a.C >= 128 && a.K % 64 == 0) { bp = 128; bk = 64; ns = 2; }
   small_grid_tiles(Pd, Qd * (phased ? 4 : 1), a.G, a.K % 64 == 0, bp, bq, bk, ns);
-  decode_cfg(cfg, bp, bq, bk, ns);
+  bool halo = false;
+  if (cfg) {
+    decode_cfg(cfg, bp, bq, bk, ns);
+    halo = ns & 0x40;
+    ns &= 0x3f;
+  } else if (halo_auto() && !phased) {
+    // sweep (profiles/conv_halo_sweep_r1_g8.log): 64 x 128 tiles, 4 waves along Q
+    const long long ht = (long long)((Pd + 63) / 64) * (Qd / 128) * a.G;
+    if (halo_ok(a, 128, 4) && ht >= num_cus()) { halo = true; bp = 48; bq = 128; bk = 32; ns = 4; }
+  }
+  if (halo) {
+    if (phased || !halo_ok(a, bq, ns) || bk != 32) return (int)hipErrorInvalidValue;
+    return (int)dispatch_halo<MODE_DGRAD>(a, Pd, Qd, bp, bq, ns, stream);
+  }
   if (a.K % bk) return (int)hipErrorInvalidValue;
   const int nph = phased ? 4 : 1;
   const long long rows = (long long)a.N * a.H * a.W;

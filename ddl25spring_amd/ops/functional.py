@@ -61,9 +61,10 @@ def zero_page(device) -> torch.Tensor:
     return z
 
 
-def conv_cfg(bp: int, bq: int, bk: int, ns: int) -> int:
-    """Explicit conv tile choice (BP x BQ output tile, BK reduction step, NS LDS stages)."""
-    return (bp // 16) | ((bq // 16) << 8) | (bk << 16) | (ns << 24)
+def conv_cfg(bp: int, bq: int, bk: int, ns: int, halo: bool = False) -> int:
+    """Explicit conv tile choice (BP x BQ output tile, BK reduction step, NS LDS stages).
+    halo: the halo-staged 3x3 / stride-1 FWD / DGRAD kernel (BK 32; tiles in ``HALO_TILES``)."""
+    return (bp // 16) | ((bq // 16) << 8) | (bk << 16) | ((ns | (0x40 if halo else 0)) << 24)
 
 
 CONV_TILES = [(64, 64, 32, 4), (64, 128, 32, 4), (128, 64, 32, 4), (128, 128, 32, 4),
@@ -72,6 +73,26 @@ CONV_TILES = [(64, 64, 32, 4), (64, 128, 32, 4), (128, 64, 32, 4), (128, 128, 32
               (256, 128, 32, 2), (128, 256, 32, 2),
               # bp = 48 selects BP = 64 with the 4 waves along Q (1x4, 64x64 per wave)
               (48, 256, 32, 4), (48, 256, 64, 3), (48, 256, 64, 2), (48, 256, 32, 3)]
+
+
+# halo-staged 3x3 stride-1 tiles (bp, bq, ns); bp = 48: 64 channels with the 4 waves along Q
+HALO_TILES = [(48, 256, 4), (48, 128, 4), (64, 128, 4), (128, 128, 4), (128, 256, 4), (48, 256, 5),
+              (48, 128, 6), (128, 128, 6)]
+
+
+def halo_eligible(geom: ConvGeom, bq: int, ns: int) -> bool:
+    """Mirror of conv_igemm.hip ``halo_ok``: 3x3 / stride 1 / pad 1, tiles of whole rows of one
+    image or of whole images, and a halo image the taps of one channel block can DMA."""
+    g = geom
+    if (g.stride, g.R, g.S, g.pad) != (1, 3, 3, 1):
+        return False
+    hw = g.H * g.W
+    if (bq % g.W or hw % bq) if hw >= bq else bq % hw:
+        return False
+    trh = min(bq // g.W, g.H)
+    hpx = bq // (trh * g.W) * (trh + 2) * (g.W + 2)
+    cap = 10 - ns if bq >= 256 else min(10 - ns, 4)
+    return ((hpx + 15) // 16 + 3) // 4 <= cap
 
 
 SPLITK_CAP = 1 << 24  # fp32 elements (64 MiB) of split-K partial slices per device

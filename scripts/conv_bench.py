@@ -116,17 +116,18 @@ def main():
                     row[mode]["splits_us"]["best"] = f"{best[0] * 1e3:.1f}@{best[1]}"
             if args.sweep:
                 best = (t, 0)
-                for bp, bq, bk, ns in CFGS:
-                    if mode == "fwd" and g.C % bk:
-                        continue
-                    if mode == "dgrad" and g.K % bk:
-                        continue
-                    cfg = Fn.conv_cfg(bp, bq, bk, ns)
+                cands = [(f"{bp}x{bq}x{bk}s{ns}", Fn.conv_cfg(bp, bq, bk, ns))
+                         for bp, bq, bk, ns in CFGS
+                         if not ((mode == "fwd" and g.C % bk) or (mode == "dgrad" and g.K % bk))]
+                if mode != "wgrad":  # halo-staged 3x3 stride-1 kernels (raise where ineligible)
+                    cands += [(f"halo{bp}x{bq}s{ns}", Fn.conv_cfg(bp, bq, 32, ns, halo=True))
+                              for bp, bq, ns in Fn.HALO_TILES]
+                for label, cfg in cands:
                     try:
                         tc = timeit(lambda: f(cfg), reps=5, rounds=3)
                     except Exception:
                         continue
-                    row.setdefault(mode + "_sweep", {})[f"{bp}x{bq}x{bk}s{ns}"] = round(fl / tc / 1e9, 1)
+                    row.setdefault(mode + "_sweep", {})[label] = round(fl / tc / 1e9, 1)
                     if tc < best[0]:
                         best = (tc, cfg)
                 row[mode]["best_cfg"] = best[1]
@@ -150,6 +151,10 @@ def main():
                     msg += f" split{row[mode]['splits_us']}"
                 if "best_cfg" in row[mode]:
                     msg += f" (best {row[mode]['best_tflops']:.0f} @{row[mode]['best_cfg']:#x})"
+                if mode + "_sweep" in row:
+                    halo = {k: v for k, v in row[mode + "_sweep"].items() if k.startswith("halo")}
+                    if halo:
+                        msg += f" halo{halo}"
         if "miopen_fwd" in row:
             msg += f" | miopen fwd {row['miopen_fwd']['tflops']:6.0f}TF"
         print(msg, flush=True)

@@ -105,6 +105,47 @@ def test_conv_tile_configs(cuda):
             _close(dw, dw_ref, rel=2e-3)
 
 
+HALO_GEOMS = [
+    ConvGeom(G=2, N=3, H=32, W=32, C=64, K=64, R=3, S=3, stride=1, pad=1),    # layer-1 shape
+    ConvGeom(G=1, N=2, H=16, W=16, C=96, K=160, R=3, S=3, stride=1, pad=1),   # odd block counts
+    ConvGeom(G=2, N=3, H=8, W=8, C=256, K=128, R=3, S=3, stride=1, pad=1),    # 2 images per tile
+    ConvGeom(G=1, N=5, H=8, W=8, C=64, K=64, R=3, S=3, stride=1, pad=1),      # partial last tile
+    ConvGeom(G=1, N=4, H=4, W=32, C=32, K=64, R=3, S=3, stride=1, pad=1),     # 1 channel block
+]
+
+
+@pytest.mark.parametrize("geom", HALO_GEOMS, ids=lambda g: f"{g.C}x{g.K}_{g.H}x{g.W}")
+def test_conv_halo(cuda, geom):
+    """Halo-staged 3x3 stride-1 kernels (activation tile + halo DMA'd once per channel block)
+    match the fp32 reference for every tile config the shape admits, with the fused epilogues."""
+    g = geom
+    x = _rand(g.G, g.N, g.H, g.W, g.C, dev=cuda)
+    w = _weights(g, cuda)
+    dy = _rand(g.G, g.N, g.P, g.Q, g.K, dev=cuda)
+    bias = torch.randn(g.G, g.K, device=cuda)
+    res = _rand(g.G, g.N, g.H, g.W, g.C, dev=cuda)
+    mask = _rand(g.G, g.N, g.H, g.W, g.C, dev=cuda)
+    st_ref = torch.zeros(g.G, 2, g.K)
+    y_ref = ref.conv_fwd(x.cpu(), w.cpu(), g, bias=bias.cpu(), relu=True, stats=st_ref)
+    dx_ref = ref.conv_dgrad(dy.cpu(), w.cpu(), g, residual=res.cpu(), mask=mask.cpu())
+    ran = 0
+    for bp, bq, ns in Fn.HALO_TILES:
+        cfg = Fn.conv_cfg(bp, bq, 32, ns, halo=True)
+        if not Fn.halo_eligible(g, bq, ns):
+            with pytest.raises(RuntimeError):
+                Fn.conv_fwd(x, w, g, cfg=cfg)
+            continue
+        ran += 1
+        st = Fn.stats_buffer(g.G, g.K, cuda)
+        _close(Fn.conv_fwd(x, w, g, bias=bias, relu=True, stats=st, cfg=cfg), y_ref)
+        _close(st.sum(1), st_ref, rel=2e-3)
+        _close(Fn.conv_dgrad(dy, w, g, residual=res, mask=mask, cfg=cfg), dx_ref)
+    assert ran > 0
+    # the automatic choice (halo where eligible) agrees too
+    _close(Fn.conv_fwd(x, w, g, bias=bias, relu=True), y_ref)
+    _close(Fn.conv_dgrad(dy, w, g, residual=res, mask=mask), dx_ref)
+
+
 def test_batchnorm(cuda):
     G, N, H, W, C = 2, 5, 6, 6, 64
     x = _rand(G, N, H, W, C, dev=cuda, scale=2.0) + 0.5
