@@ -679,7 +679,6 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       return;
     }
     bf16_t* O = (bf16_t*)a.out + (long long)g * a.out_gs;
-    const int ldo = Pd;  // NHWC: channel contiguous
     const float* bias = a.bias ? a.bias + (long long)g * a.bias_gs : nullptr;
     const bf16_t* res = a.residual ? (const bf16_t*)a.residual + (long long)g * a.out_gs : nullptr;
     const bf16_t* msk = a.mask ? (const bf16_t*)a.mask + (long long)g * a.out_gs : nullptr;
@@ -691,91 +690,90 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     const bf16_t* bnx = (MODE == MODE_DGRAD && a.bn_x) ? (const bf16_t*)a.bn_x + (long long)g * a.out_gs
                                                         : nullptr;
     const bool want_stats = stats && (MODE == MODE_FWD || bnx);
+    // LDS-restaged epilogue. The MFMA accumulator gives a lane 4 channels of one pixel, so a direct
+    // epilogue moves 8 B per lane at a pixel stride (residual / mask / BN-input reads, output
+    // stores): 4 instructions share every 128-B line. Instead, per 16-pixel strip of every wave
+    // column (tj), the tile's fp32 accumulators go through LDS and come back as 8 consecutive
+    // channels of one pixel per thread: 16-B coalesced loads / stores, and per-thread channel
+    // chunks fixed across strips for the BN statistics.
+    {
+      constexpr int NPX = (4 / WLP) * 16;  // pixels per strip
+      constexpr int LROW = BP + 4;         // fp32 row pitch (+16 B: conflict-free b128 writes)
+      constexpr int NCH = BP / 8;          // 8-channel chunks per pixel
+      constexpr int PSTEP = 256 / NCH;     // pixels per thread-iteration
+      static_assert(NPX * LROW * 4 <= SMEM_BYTES && 256 * 16 * 4 <= SMEM_BYTES, "epilogue LDS");
+      static_assert(256 % NCH == 0, "chunks");
+      float* const et = (float*)smem;
+      const int c8 = tid % NCH, prow = tid / NCH;
+      const int p = p0 + c8 * 8;
+      const bool pok = p < Pd;
+      float bv[8], bmu[8], brs[8], s1[8], s2[8];
 #pragma unroll
-    for (int ti = 0; ti < TP; ++ti) {
-      const int p = p0 + wp * WP + ti * 16 + lp;
-      float bsum[4] = {0.f, 0.f, 0.f, 0.f}, bsq[4] = {0.f, 0.f, 0.f, 0.f};
-      float bv[4] = {0.f, 0.f, 0.f, 0.f}, bmu[4] = {0.f, 0.f, 0.f, 0.f}, brs[4] = {0.f, 0.f, 0.f, 0.f};
-      if (bias && p < Pd) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bv[e] = bias[p + e];
+      for (int k = 0; k < 8; ++k) {
+        bv[k] = (bias && pok) ? bias[p + k] : 0.f;
+        bmu[k] = (bnx && pok) ? a.bn_mean[(long long)g * Pd + p + k] : 0.f;
+        brs[k] = (bnx && pok) ? a.bn_rstd[(long long)g * Pd + p + k] : 0.f;
+        s1[k] = s2[k] = 0.f;
       }
-      if (bnx && p < Pd) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          bmu[e] = a.bn_mean[(long long)g * Pd + p + e];
-          brs[e] = a.bn_rstd[(long long)g * Pd + p + e];
-        }
-      }
+      __syncthreads();  // every wave is done with the main loop's LDS (ring, halo)
 #pragma unroll
       for (int tj = 0; tj < TQ; ++tj) {
-        const int q = q0 + wq * WQ + tj * 16 + lq;
-        if (p < Pd && q < Qd) {
-          float v[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = acc[ti][tj][e] + bv[e];
-          long long o = (long long)q * ldo + p;
+        for (int ti = 0; ti < TP; ++ti)
+          *(f4v*)(et + (wq * 16 + lq) * LROW + wp * WP + ti * 16 + lp) = acc[ti][tj];
+        __syncthreads();
+        for (int px = prow; px < NPX; px += PSTEP) {
+          const int q = q0 + (px >> 4) * WQ + tj * 16 + (px & 15);
+          if (!pok || q >= Qd) continue;
+          const f4v lo = *(const f4v*)(et + px * LROW + c8 * 8);
+          const f4v hi = *(const f4v*)(et + px * LROW + c8 * 8 + 4);
+          float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] += bv[k];
+          long long o = (long long)q * Pd + p;
           if (phased) {  // phase-local pixel (n, i, j) -> NHWC offset of (n, 2i+a, 2j+b)
             const int n = q / (Hs * Ws), rem = q - n * (Hs * Ws);
-            const int hi = rem / Ws, wi = rem - hi * Ws;
-            o = ((long long)(n * H + 2 * hi + ph_a) * W + 2 * wi + ph_b) * ldo + p;
+            const int hi2 = rem / Ws, wi = rem - hi2 * Ws;
+            o = ((long long)(n * H + 2 * hi2 + ph_a) * W + 2 * wi + ph_b) * Pd + p;
           }
+          float t[8];
           if (res) {
-            const i2v rv = *(const i2v*)(res + o);
-            v[0] += lo_bf((uint32_t)rv[0]); v[1] += hi_bf((uint32_t)rv[0]);
-            v[2] += lo_bf((uint32_t)rv[1]); v[3] += hi_bf((uint32_t)rv[1]);
+            unpack8(*(const i4v*)(res + o), t);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] += t[k];
           }
           if (msk) {
-            const i2v mv = *(const i2v*)(msk + o);
-            if (!(lo_bf((uint32_t)mv[0]) > 0.f)) v[0] = 0.f;
-            if (!(hi_bf((uint32_t)mv[0]) > 0.f)) v[1] = 0.f;
-            if (!(lo_bf((uint32_t)mv[1]) > 0.f)) v[2] = 0.f;
-            if (!(hi_bf((uint32_t)mv[1]) > 0.f)) v[3] = 0.f;
+            unpack8(*(const i4v*)(msk + o), t);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) if (!(t[k] > 0.f)) v[k] = 0.f;
           }
           if (a.relu) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+            for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
           }
-          i2v ov;
-          ov[0] = (int)pack_bf2(v[0], v[1]);
-          ov[1] = (int)pack_bf2(v[2], v[3]);
-          *(i2v*)(O + o) = ov;
+          *(i4v*)(O + o) = pack8(v);
           if (bnx) {
-            const i2v xv = *(const i2v*)(bnx + o);
-            const float xs[4] = {lo_bf((uint32_t)xv[0]), hi_bf((uint32_t)xv[0]),
-                                 lo_bf((uint32_t)xv[1]), hi_bf((uint32_t)xv[1])};
+            unpack8(*(const i4v*)(bnx + o), t);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              bsum[e] += v[e];
-              bsq[e] += v[e] * ((xs[e] - bmu[e]) * brs[e]);
-            }
+            for (int k = 0; k < 8; ++k) { s1[k] += v[k]; s2[k] += v[k] * ((t[k] - bmu[k]) * brs[k]); }
           } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              bsum[e] += v[e];
-              bsq[e] += v[e] * v[e];
-            }
+            for (int k = 0; k < 8; ++k) { s1[k] += v[k]; s2[k] += v[k] * v[k]; }
           }
         }
+        __syncthreads();
       }
       if (want_stats) {
+        // fold the partial sums of the PSTEP threads that share each channel chunk
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float s = bsum[e], s2 = bsq[e];
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) {
-            s += __shfl_xor(s, o, 64);
-            s2 += __shfl_xor(s2, o, 64);
-          }
-          bsum[e] = s;
-          bsq[e] = s2;
-        }
-        if (lq == 0 && p < Pd) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            atomicAdd(stats + p + e, bsum[e]);
-            atomicAdd(stats + Pd + p + e, bsq[e]);
-          }
+        for (int k = 0; k < 8; ++k) { et[tid * 16 + k] = s1[k]; et[tid * 16 + 8 + k] = s2[k]; }
+        __syncthreads();
+        for (int j = tid; j < 2 * BP; j += 256) {
+          const int which = j / BP, ch = j - which * BP;
+          const int chunk = ch >> 3, k = ch & 7;
+          float sum = 0.f;
+          for (int r = 0; r < PSTEP; ++r) sum += et[(r * NCH + chunk) * 16 + which * 8 + k];
+          if (p0 + ch < Pd) atomicAdd(stats + which * Pd + p0 + ch, sum);
         }
       }
     }

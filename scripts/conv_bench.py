@@ -73,6 +73,8 @@ def main():
     ap.add_argument("--layers", default="", help="comma list of layer names to run (default all)")
     ap.add_argument("--splits", default="", help="FWD/DGRAD split-K counts to time, e.g. 1,2,4")
     ap.add_argument("--split-sweep", action="store_true", help="also sweep tiles x splits")
+    ap.add_argument("--epi", action="store_true",
+                    help="time with the fused epilogues of training (residual; mask + BN-backward reduce)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -88,9 +90,16 @@ def main():
         st = Fn.stats_buffer(g.G, g.K, dev)  # fwd runs with the BN-statistics epilogue, as in training
         fl = g.flops()
         row = {"layer": name, "geom": str(g), "gflop": fl / 1e9}
+        if args.epi:  # the training step's fused epilogues: fwd + residual, dgrad + mask + BN reduce
+            res = torch.randn(g.G, g.N, g.P, g.Q, g.K, device=dev).to(torch.bfloat16)
+            msk = torch.randn(g.G, g.N, g.H, g.W, g.C, device=dev).to(torch.bfloat16)
+            mean = torch.zeros(g.G, g.C, device=dev)
+            rstd = torch.ones(g.G, g.C, device=dev)
         modes = {
-            "fwd": lambda cfg, sk=0: Fn.conv_fwd(x, w, g, cfg=cfg, stats=st, split_k=sk),
-            "dgrad": lambda cfg, sk=0: Fn.conv_dgrad(dy, w, g, cfg=cfg, split_k=sk),
+            "fwd": (lambda cfg, sk=0: Fn.conv_fwd(x, w, g, cfg=cfg, stats=st, split_k=sk, residual=res))
+            if args.epi else (lambda cfg, sk=0: Fn.conv_fwd(x, w, g, cfg=cfg, stats=st, split_k=sk)),
+            "dgrad": (lambda cfg, sk=0: Fn.conv_dgrad(dy, w, g, cfg=cfg, split_k=sk, mask=msk, bn=(x, mean, rstd)))
+            if args.epi else (lambda cfg, sk=0: Fn.conv_dgrad(dy, w, g, cfg=cfg, split_k=sk)),
             "wgrad": lambda cfg: Fn.conv_wgrad(dy, x, g, dw, cfg=cfg),
         }
         for mode, f in modes.items():
