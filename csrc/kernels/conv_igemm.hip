@@ -65,6 +65,10 @@ struct ConvArgs {
   // to partial[split][G][rows][Pd] and conv_splitk_epilogue applies the epilogue above.
   float* partial;
   long long partial_cap;  // floats available at `partial` (0: no split-K for FWD / DGRAD)
+  // DGRAD: ReLU mask recomputed from the BN input instead of read: keep dx where
+  // bn_x * mask_scale + mask_shift > 0 (the forward bn_apply's pre-activation; needs bn_x)
+  const float* mask_scale;  // [G][C]
+  const float* mask_shift;
 };
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
@@ -707,12 +711,15 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       const int c8 = tid % NCH, prow = tid / NCH;
       const int p = p0 + c8 * 8;
       const bool pok = p < Pd;
-      float bv[8], bmu[8], brs[8], s1[8], s2[8];
+      const bool mbn = bnx && a.mask_scale;  // mask from the BN input (no mask read)
+      float bv[8], bmu[8], brs[8], msc[8], msh[8], s1[8], s2[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         bv[k] = (bias && pok) ? bias[p + k] : 0.f;
         bmu[k] = (bnx && pok) ? a.bn_mean[(long long)g * Pd + p + k] : 0.f;
         brs[k] = (bnx && pok) ? a.bn_rstd[(long long)g * Pd + p + k] : 0.f;
+        msc[k] = (mbn && pok) ? a.mask_scale[(long long)g * Pd + p + k] : 0.f;
+        msh[k] = (mbn && pok) ? a.mask_shift[(long long)g * Pd + p + k] : 0.f;
         s1[k] = s2[k] = 0.f;
       }
       __syncthreads();  // every wave is done with the main loop's LDS (ring, halo)
@@ -736,7 +743,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
             const int hi2 = rem / Ws, wi = rem - hi2 * Ws;
             o = ((long long)(n * H + 2 * hi2 + ph_a) * W + 2 * wi + ph_b) * Pd + p;
           }
-          float t[8];
+          float t[8], xb[8];
+          if (bnx) unpack8(*(const i4v*)(bnx + o), xb);
           if (res) {
             unpack8(*(const i4v*)(res + o), t);
 #pragma unroll
@@ -746,6 +754,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
             unpack8(*(const i4v*)(msk + o), t);
 #pragma unroll
             for (int k = 0; k < 8; ++k) if (!(t[k] > 0.f)) v[k] = 0.f;
+          } else if (mbn) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) if (!(xb[k] * msc[k] + msh[k] > 0.f)) v[k] = 0.f;
           }
           if (a.relu) {
 #pragma unroll
@@ -753,9 +764,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
           }
           *(i4v*)(O + o) = pack8(v);
           if (bnx) {
-            unpack8(*(const i4v*)(bnx + o), t);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) { s1[k] += v[k]; s2[k] += v[k] * ((t[k] - bmu[k]) * brs[k]); }
+            for (int k = 0; k < 8; ++k) { s1[k] += v[k]; s2[k] += v[k] * ((xb[k] - bmu[k]) * brs[k]); }
           } else {
 #pragma unroll
             for (int k = 0; k < 8; ++k) { s1[k] += v[k]; s2[k] += v[k] * v[k]; }
@@ -816,7 +826,8 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvArgs a, i
   const bf16_t* bnx = (mode == MODE_DGRAD && a.bn_x) ? (const bf16_t*)a.bn_x + (long long)g * a.out_gs + c0
                                                       : nullptr;
   const bool want_stats = a.stats && (mode == MODE_FWD || bnx);
-  float bv[8] = {}, bmu[8] = {}, brs[8] = {}, s1[8] = {}, s2[8] = {};
+  const bool mbn = bnx && a.mask_scale;
+  float bv[8] = {}, bmu[8] = {}, brs[8] = {}, msc[8] = {}, msh[8] = {}, s1[8] = {}, s2[8] = {};
   if (a.bias) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) bv[k] = a.bias[(long long)g * a.bias_gs + c0 + k];
@@ -826,6 +837,13 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvArgs a, i
     for (int k = 0; k < 8; ++k) {
       bmu[k] = a.bn_mean[(long long)g * Pd + c0 + k];
       brs[k] = a.bn_rstd[(long long)g * Pd + c0 + k];
+    }
+  }
+  if (mbn) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      msc[k] = a.mask_scale[(long long)g * Pd + c0 + k];
+      msh[k] = a.mask_shift[(long long)g * Pd + c0 + k];
     }
   }
   // RB rows per thread per pass, all their slice loads issued before any use; few enough blocks
@@ -859,7 +877,8 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvArgs a, i
         const long long r = r0 + b * stride;
         if (r >= rows) break;
         const long long e = r * Pd;
-        float t[8];
+        float t[8], xb[8];
+        if (bnx) unpack8(*(const i4v*)(bnx + e), xb);
         if (res) {
           unpack8(*(const i4v*)(res + e), t);
 #pragma unroll
@@ -869,6 +888,9 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvArgs a, i
           unpack8(*(const i4v*)(msk + e), t);
 #pragma unroll
           for (int k = 0; k < 8; ++k) if (!(t[k] > 0.f)) v[b][k] = 0.f;
+        } else if (mbn) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) if (!(xb[k] * msc[k] + msh[k] > 0.f)) v[b][k] = 0.f;
         }
         if (a.relu) {
 #pragma unroll
@@ -876,9 +898,8 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvArgs a, i
         }
         *(i4v*)(O + e) = pack8(v[b]);
         if (bnx) {
-          unpack8(*(const i4v*)(bnx + e), t);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) { s1[k] += v[b][k]; s2[k] += v[b][k] * ((t[k] - bmu[k]) * brs[k]); }
+          for (int k = 0; k < 8; ++k) { s1[k] += v[b][k]; s2[k] += v[b][k] * ((xb[k] - bmu[k]) * brs[k]); }
         } else {
 #pragma unroll
           for (int k = 0; k < 8; ++k) { s1[k] += v[b][k]; s2[k] += v[b][k] * v[b][k]; }

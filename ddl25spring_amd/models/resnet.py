@@ -85,10 +85,10 @@ class BasicBlock(Layer):
         else:
             out = Fn.bn_apply(c2, sc2, sh2, r=x, act=RELU)
             dctx = None
-        return out, (x, c1, a1, mu1, rs1, g1, c2, mu2, rs2, g2, out, dctx)
+        return out, (x, c1, a1, sc1, sh1, mu1, rs1, g1, c2, mu2, rs2, g2, out, dctx)
 
     def backward(self, dout, ctx):
-        x, c1, a1, mu1, rs1, g1, c2, mu2, rs2, g2, out, dctx = ctx
+        x, c1, a1, sc1, sh1, mu1, rs1, g1, c2, mu2, rs2, g2, out, dctx = ctx
         st = self.store
         dc2, dym = self.conv2.bn_backward(dout, out, c2, mu2, rs2, emit_dym=True)
         if dctx is not None:
@@ -99,8 +99,10 @@ class BasicBlock(Layer):
         else:
             dres = dym
         Fn.conv_wgrad(dc2, a1, g2, st.grad_of(self.conv2.w))
-        # dgrad epilogue applies bn1's ReLU mask and reduces bn1's backward sums (no reduce pass)
-        da1, part1 = Fn.conv_dgrad(dc2, st.shadow_of(self.conv2.w), g2, mask=a1, bn=(c1, mu1, rs1))
+        # dgrad epilogue applies bn1's ReLU mask (recomputed from c1: no read of a1) and reduces
+        # bn1's backward sums (no reduce pass)
+        da1, part1 = Fn.conv_dgrad(dc2, st.shadow_of(self.conv2.w), g2, bn=(c1, mu1, rs1),
+                                   mask_bn=(sc1, sh1))
         dc1 = self.conv1.bn_backward(da1, None, c1, mu1, rs1, part=part1)
         Fn.conv_wgrad(dc1, x, g1, st.grad_of(self.conv1.w))
         if not self.needs_input_grad:
@@ -163,10 +165,11 @@ class Bottleneck(Layer):
         else:
             out = Fn.bn_apply(c3, sc3, sh3, r=x, act=RELU)
             dctx = None
-        return out, (x, (c1, a1, mu1, rs1, g1), (c2, a2, mu2, rs2, g2), (c3, mu3, rs3, g3), out, dctx)
+        return out, (x, (c1, a1, sc1, sh1, mu1, rs1, g1), (c2, a2, sc2, sh2, mu2, rs2, g2),
+                     (c3, mu3, rs3, g3), out, dctx)
 
     def backward(self, dout, ctx):
-        x, (c1, a1, mu1, rs1, g1), (c2, a2, mu2, rs2, g2), (c3, mu3, rs3, g3), out, dctx = ctx
+        x, (c1, a1, sc1, sh1, mu1, rs1, g1), (c2, a2, sc2, sh2, mu2, rs2, g2), (c3, mu3, rs3, g3), out, dctx = ctx
         st = self.store
         dc3, dym = self.conv3.bn_backward(dout, out, c3, mu3, rs3, emit_dym=True)
         if dctx is not None:
@@ -177,10 +180,10 @@ class Bottleneck(Layer):
         else:
             dres = dym
         Fn.conv_wgrad(dc3, a2, g3, st.grad_of(self.conv3.w))
-        da2, part2 = Fn.conv_dgrad(dc3, st.shadow_of(self.conv3.w), g3, mask=a2, bn=(c2, mu2, rs2))
+        da2, part2 = Fn.conv_dgrad(dc3, st.shadow_of(self.conv3.w), g3, bn=(c2, mu2, rs2), mask_bn=(sc2, sh2))
         dc2 = self.conv2.bn_backward(da2, None, c2, mu2, rs2, part=part2)
         Fn.conv_wgrad(dc2, a1, g2, st.grad_of(self.conv2.w))
-        da1, part1 = Fn.conv_dgrad(dc2, st.shadow_of(self.conv2.w), g2, mask=a1, bn=(c1, mu1, rs1))
+        da1, part1 = Fn.conv_dgrad(dc2, st.shadow_of(self.conv2.w), g2, bn=(c1, mu1, rs1), mask_bn=(sc1, sh1))
         dc1 = self.conv1.bn_backward(da1, None, c1, mu1, rs1, part=part1)
         Fn.conv_wgrad(dc1, x, g1, st.grad_of(self.conv1.w))
         if not self.needs_input_grad:

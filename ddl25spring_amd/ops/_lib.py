@@ -40,7 +40,8 @@ class ConvArgs(ctypes.Structure):
                 ("G", i32), ("N", i32), ("H", i32), ("W", i32), ("C", i32), ("K", i32), ("R", i32),
                 ("S", i32), ("P", i32), ("Q", i32), ("stride", i32), ("pad", i32),
                 ("relu", i32), ("accumulate", i32), ("split_k", i32), ("stats_stripes", i32),
-                ("bn_x", vp), ("bn_mean", vp), ("bn_rstd", vp), ("partial", vp), ("partial_cap", i64)]
+                ("bn_x", vp), ("bn_mean", vp), ("bn_rstd", vp), ("partial", vp), ("partial_cap", i64),
+                ("mask_scale", vp), ("mask_shift", vp)]
 
 
 class BNArgs(ctypes.Structure):

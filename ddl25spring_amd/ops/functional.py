@@ -171,13 +171,23 @@ def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out=None, 
     return y
 
 
-def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0, bn=None, split_k=0):
+def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0, bn=None, split_k=0,
+               mask_bn=None):
     """dx[G,N,H,W,C] = conv_transpose(dy, w) (+residual) * (mask > 0).
 
     bn = (x, mean, rstd): also reduce, in the epilogue, the preceding BatchNorm's backward sums
     (sum dx, sum dx * (x - mean) * rstd) into a striped [G, BN_STRIPES, 2, C] buffer; returns
-    (dx, part) for ``bn_backward(..., part=part)``."""
+    (dx, part) for ``bn_backward(..., part=part)``.
+    mask_bn = (scale, shift) [G, C] (with bn): the ReLU mask of ``bn_apply(x, scale, shift, relu)``
+    recomputed from x in the epilogue, (x * scale + shift > 0), instead of read from its output."""
+    if mask_bn is not None:
+        assert bn is not None and mask is None, "mask_bn recomputes the mask from bn's x"
     if not dy.is_cuda:
+        if mask_bn is not None:
+            sc, sh = mask_bn
+            xs = bn[0].float()
+            bshape = (geom.G,) + (1,) * (xs.dim() - 2) + (geom.C,)
+            mask = ((xs * sc.float().reshape(bshape) + sh.float().reshape(bshape)) > 0).to(dy.dtype)
         dx = ref.conv_dgrad(dy, w, geom, residual, mask)
         if out is not None:
             out.copy_(dx)
@@ -206,6 +216,10 @@ def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0,
         part = ws.zeros((geom.G, BN_STRIPES, 2, geom.C), dy.device)
         kw = dict(stats=ptr(part), stats_gs=part.stride(0), stats_stripes=BN_STRIPES, bn_x=ptr(x),
                   bn_mean=ptr(mean), bn_rstd=ptr(rstd))
+        if mask_bn is not None:
+            sc, sh = mask_bn
+            assert sc.is_contiguous() and sh.is_contiguous() and sc.numel() == geom.G * geom.C
+            kw.update(mask_scale=ptr(sc), mask_shift=ptr(sh))
     a = _conv_args(geom, dy.device, split_k, True, w=ptr(w), dy=ptr(dy), out=ptr(dx), residual=ptr(residual),
                    mask=ptr(mask), w_gs=_gs(w), dy_gs=_gs(dy), out_gs=_gs(dx), **kw)
     check(_lib.kernels().ddl_conv_dgrad(ctypes.byref(a), cfg, stream()), "conv_dgrad")

@@ -314,6 +314,14 @@ def test_conv_dgrad_fused_bn_reduce(cuda, geom):
     _close(part.sum(1)[:, 1], (d * xh).sum(1), rel=2e-2)
     dg1, db1 = torch.zeros(g.G, g.C, device=cuda), torch.zeros(g.G, g.C, device=cuda)
     dg2, db2 = torch.zeros(g.G, g.C, device=cuda), torch.zeros(g.G, g.C, device=cuda)
+    # the mask recomputed from the BN input (x * scale + shift > 0) == the stored ReLU output's mask
+    sc = torch.randn(g.G, g.C, device=cuda)
+    sh = torch.randn(g.G, g.C, device=cuda) * 0.3
+    relu_out = (xbn.float() * sc[:, None, None, None] + sh[:, None, None, None]).clamp_min(0).to(torch.bfloat16)
+    dxa, pa = Fn.conv_dgrad(dy, w, g, mask=relu_out, bn=(xbn, mean, rstd))
+    dxb, pb = Fn.conv_dgrad(dy, w, g, bn=(xbn, mean, rstd), mask_bn=(sc, sh))
+    assert (dxa.float() - dxb.float()).abs().max().item() <= 1e-2 * dxa.float().abs().max().item()
+    _close(pb.sum(1), pa.sum(1), rel=1e-2)
     fused = Fn.bn_backward(dxm, None, xbn, mean, rstd, gamma, dg1, db1, part=part)
     unfused = Fn.bn_backward(plain, None, xbn, mean, rstd, gamma, dg2, db2)
     _close(fused, unfused, rel=2e-2)
@@ -351,3 +359,9 @@ def test_conv_split_k(cuda, geom, split):
     dxb, pb = Fn.conv_dgrad(dy, w, g, mask=mask, bn=(xbn, mean, rstd), split_k=split)
     _close(dxb, dxa, rel=1e-2)
     _close(pb.sum(1), pa.sum(1), rel=2e-2)
+    sc = torch.randn(g.G, g.C, device=cuda)
+    sh = torch.randn(g.G, g.C, device=cuda) * 0.3
+    dxc, pc = Fn.conv_dgrad(dy, w, g, bn=(xbn, mean, rstd), mask_bn=(sc, sh), split_k=1)
+    dxd, pd_ = Fn.conv_dgrad(dy, w, g, bn=(xbn, mean, rstd), mask_bn=(sc, sh), split_k=split)
+    _close(dxd, dxc, rel=1e-2)
+    _close(pd_.sum(1), pc.sum(1), rel=2e-2)
