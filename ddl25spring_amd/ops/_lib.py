@@ -18,7 +18,9 @@ from pathlib import Path
 import torch
 
 LIBDIR = Path(__file__).resolve().parent.parent / "lib"
-KERNEL_LIB_PATH = LIBDIR / "libddl_kernels.so"
+# DDL_KERNEL_LIB: an alternative build of the kernel library (A/B timing of two builds)
+KERNEL_LIB_PATH = Path(os.environ["DDL_KERNEL_LIB"]) if os.environ.get("DDL_KERNEL_LIB") else \
+    LIBDIR / "libddl_kernels.so"
 RUNTIME_LIB_PATH = LIBDIR / "libddl_runtime.so"
 
 _kernels = None

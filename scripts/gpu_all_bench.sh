@@ -12,4 +12,5 @@ run llm 300 python benchmarks/bench_llm.py --steps 20 --warmup 3
 run vflgan 300 python benchmarks/bench_vfl_gan.py
 run byz 300 python benchmarks/bench_byzantine.py
 run prof8 300 rocprofv3 --kernel-trace --stats -d $out/prof8 -o run -- python bench.py --steps 2 --warmup 1
+run prof1 300 rocprofv3 --kernel-trace --stats -d $out/prof1 -o run -- python bench.py --clients 1 --train-size 6250 --steps 3 --warmup 1
 echo ALLDONE
