@@ -156,19 +156,24 @@ __device__ __forceinline__ void cta_barrier() {
 // pixels, at any shift (every tap of a fragment on >= 16-wide rows), reads conflict-free.
 template <int MODE, int BP, int BQ, int BK, int NS, int WLP = 2, bool HALO = false>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
-  constexpr int P_BYTES = BP * BK * 2, Q_BYTES = BQ * BK * 2, STAGE = P_BYTES + Q_BYTES;
-  static_assert(!HALO || (MODE != MODE_WGRAD && BK == 32 && NS >= 4), "halo: FWD/DGRAD, BK 32, >= 4 stages");
+  constexpr bool HALO_FD = HALO && MODE != MODE_WGRAD;  // halo FWD / DGRAD (channel-block-major)
+  constexpr bool HALO_W = HALO && MODE == MODE_WGRAD;   // halo WGRAD (per-step row window)
+  constexpr int WPW = 2;  // halo WGRAD: window pieces per wave per stage
+  constexpr int P_BYTES = BP * BK * 2, Q_BYTES = HALO_W ? WPW * 4 * 1024 : BQ * BK * 2;
+  constexpr int STAGE = P_BYTES + Q_BYTES;
+  static_assert(!HALO || (BK == 32 && NS >= 4), "halo: BK 32, >= 4 stages");
+  static_assert(!HALO_W || (BP == 64 && BQ == 288 && WLP == 2), "halo WGRAD: 64 x (9 taps x 32) tiles");
   // halo pieces (1 KiB DMA wave-instructions) per wave: issued at taps NS-1 .. 8 of a block
-  constexpr int HPW_MAX = HALO ? (BQ >= 256 ? 10 - NS : (10 - NS < 4 ? 10 - NS : 4)) : 0;
+  constexpr int HPW_MAX = HALO_FD ? (BQ >= 256 ? 10 - NS : (10 - NS < 4 ? 10 - NS : 4)) : 0;
   constexpr int HALO_BYTES = HPW_MAX * 4 * 1024;
-  constexpr int SMEM_BYTES = HALO ? NS * P_BYTES + 2 * HALO_BYTES : NS * STAGE;
+  constexpr int SMEM_BYTES = HALO_FD ? NS * P_BYTES + 2 * HALO_BYTES : NS * STAGE;
   constexpr int WP = BP / WLP, WQ = BQ / (4 / WLP), TP = WP / 16, TQ = WQ / 16;
   static_assert(WLP == 1 || WLP == 2 || WLP == 4, "4 waves");
   constexpr bool P_KMAJOR = (MODE == MODE_FWD);
   constexpr bool Q_KMAJOR = (MODE != MODE_WGRAD);
   constexpr int P_NI = BP * BK / 512, Q_NI = BQ * BK / 512;  // wave-instructions per tile
   constexpr int P_PW = P_NI / 4, Q_PW = Q_NI / 4;            // per wave
-  constexpr int LPS = P_PW + Q_PW;                           // DMA instructions per wave per stage
+  constexpr int LPS = P_PW + (HALO_W ? WPW : Q_PW);          // DMA instructions per wave per stage
   static_assert(P_PW >= 1 && Q_PW >= 1, "tile too small");
 
   __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
@@ -281,7 +286,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         acc[ti][tj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[ti], qf[tj], acc[ti][tj], 0, 0, 0);
   };
 
-  if constexpr (HALO) {
+  if constexpr (HALO_FD) {
     // host contract (halo_ok): stride 1, R = S = 3, pad 1, P = H, Q = W, tiles of whole rows of
     // one image or of whole images, halo pieces per wave <= HPW_MAX; no split-K, no phases.
     // The tile is TRh whole rows of one image (BQ <= H*W) or BQ/(H*W) whole images; its halo
@@ -428,7 +433,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   // Q operand
   int q_base[Q_PW], q_h[Q_PW], q_w[Q_PW];
 #pragma unroll
-  for (int i = 0; i < Q_PW; ++i) {
+  for (int i = 0; i < (HALO_W ? 0 : Q_PW); ++i) {
     const int j = wid + 4 * i;
     if constexpr (Q_KMAJOR) {
       const int u = j / (BQ / 16), rb = 16 * (j % (BQ / 16));
@@ -481,7 +486,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   int wn[MODE == MODE_WGRAD ? Q_PW : 1], wop[MODE == MODE_WGRAD ? Q_PW : 1],
       woq[MODE == MODE_WGRAD ? Q_PW : 1];
   int w_dn = 0, w_dp = 0, w_dq = 0;
-  if constexpr (MODE == MODE_WGRAD) {
+  if constexpr (MODE == MODE_WGRAD && !HALO_W) {
     const int pq = P * Q;
     w_dn = BK / pq;
     w_dp = (BK - w_dn * pq) / Q;
@@ -494,6 +499,44 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       wop[i] = fdiv(rem, div_q);
       woq[i] = rem - wop[i] * Q;
     }
+  }
+
+  // Halo WGRAD (3x3 / stride 1 / pad 1, W in {8, 16, 32}; host: wgrad_halo_ok): a K-step is 32
+  // output pixels = TRW = 32/W whole rows of one image; its activation operand is those rows plus
+  // a one-pixel halo, (TRW+2) x (W+2) pixels x 32 channels, DMA'd once and read by all 9 taps of
+  // the tile (64 output channels x 9 taps x 32 channels) as shifted windows, instead of one
+  // gathered DMA per tap. Pixel rows are 64 B; 16-B chunk c at c ^ 2*((pixel>>3)&1) keeps the
+  // transpose reads (8 pixels {0-3, 8-11} + shift per lane group) conflict-free for W >= 16.
+  int w_lane[WPW], w_hr[WPW], w_ok[WPW], qadr[HALO_W ? TQ : 1][2];
+  int wpix = 0, wrow = 0, TRW = 1;
+  if constexpr (HALO_W) {
+    TRW = 32 / W;
+    const int W2 = W + 2, hpx = (TRW + 2) * W2, c0 = q0 / 9;
+#pragma unroll
+    for (int j = 0; j < WPW; ++j) {
+      const int hp = (wsc + 4 * j) * 16 + (lane >> 2);
+      const int hr = hp / W2, hc = hp - hr * W2;
+      const int lc = (lane & 3) ^ (((hp >> 3) & 1) << 1);
+      w_ok[j] = (hp < hpx) & (hc >= 1) & (hc <= W);
+      w_hr[j] = hr - 1;
+      w_lane[j] = ((hr - 1) * W + (hc - 1)) * C + c0 + lc * 8;
+    }
+    const int g4 = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+#pragma unroll
+    for (int t = 0; t < TQ; ++t) {
+      const int f = wq * TQ + t, tap = f >> 1, cb16 = f & 1;
+      const int r = tap / 3, sx = tap - 3 * r;
+      const int col = cb16 * 16 + 4 * p4, cc = col >> 3, half = (col >> 2) & 1;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int k = 8 * g4 + q4 + 4 * e;
+        const int tt = k / W, ww = k - tt * W;
+        const int hp = (tt + r) * W2 + ww + sx;
+        qadr[t][e] = hp * 64 + ((cc ^ (((hp >> 3) & 1) << 1)) << 4) + half * 8;
+      }
+    }
+    wpix = kt0 * BK;
+    wrow = (wpix % (H * W)) / W;
   }
 
   // reduction cursor for FWD/DGRAD: tap (t_r, t_s) [jr, js = tap index within the phase],
@@ -530,11 +573,23 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
           rP, (__attribute__((address_space(3))) void*)(Ps + (wsc + 4 * i) * 1024), 16, off, 0, 0, 0);
     }
     // ---- Q ----  (wave-uniform tap term computed once; per lane: add + range test + select)
+    if constexpr (HALO_W) {
+#pragma unroll
+      for (int j = 0; j < WPW; ++j) {
+        const bool ok = w_ok[j] && (unsigned)(wrow + w_hr[j]) < (unsigned)H;
+        const unsigned off = ok ? (unsigned)(w_lane[j] + wpix * C) * 2u : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rX, (__attribute__((address_space(3))) void*)(Qs + (wsc + 4 * j) * 1024), 16, off, 0, 0, 0);
+      }
+      wpix += BK;
+      wrow += TRW;
+      if (wrow >= H) wrow = 0;
+    }
     int qcur = 0;
     if constexpr (MODE == MODE_FWD) qcur = (t_r * W + t_s) * C + t_c;
     else if constexpr (MODE == MODE_DGRAD) qcur = t_c - (jr * Q + js) * K;
 #pragma unroll
-    for (int i = 0; i < Q_PW; ++i) {
+    for (int i = 0; i < (HALO_W ? 0 : Q_PW); ++i) {
       unsigned off = OOB;
       if constexpr (MODE == MODE_FWD) {
         const int ih = q_h[i] + t_r, iw = q_w[i] + t_s;
@@ -594,7 +649,14 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     }
 #pragma unroll
     for (int t = 0; t < TQ; ++t) {
-      if constexpr (Q_KMAJOR) qf[t] = km_frag<BQ>(Qs, wq * WQ + t * 16, u, lane);
+      if constexpr (HALO_W) {
+        s4v r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(Qs + qadr[t][0]));
+        s4v r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(Qs + qadr[t][1]));
+        s8v r;
+        r[0] = r1[0]; r[1] = r1[1]; r[2] = r1[2]; r[3] = r1[3];
+        r[4] = r2[0]; r[5] = r2[1]; r[6] = r2[2]; r[7] = r2[3];
+        qf[t] = r;
+      } else if constexpr (Q_KMAJOR) qf[t] = km_frag<BQ>(Qs, wq * WQ + t * 16, u, lane);
       else qf[t] = mn_frag<BQ>(Qs, wq * WQ + t * 16, u, lane);
     }
   };
@@ -794,7 +856,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     for (int ti = 0; ti < TP; ++ti) {
 #pragma unroll
       for (int tj = 0; tj < TQ; ++tj) {
-        const int q = q0 + wq * WQ + tj * 16 + lq;
+        // halo tiles: column fragment f = (tap, 16-channel half) of the tile's 32 channels
+        const int q = HALO_W ? ((wq * TQ + tj) >> 1) * C + q0 / 9 + ((wq * TQ + tj) & 1) * 16 + lq
+                             : q0 + wq * WQ + tj * 16 + lq;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int p = p0 + wp * WP + ti * 16 + lp + e;
@@ -1144,9 +1208,39 @@ DDL_API int ddl_conv_dgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
   return (int)splitk_epilogue(a, MODE_DGRAD, Pd, rows, sp, stream);
 }
 
+// Halo WGRAD contract: 3x3 / stride 1 / pad 1, same-size output, 32-pixel K-steps of whole rows.
+static bool wgrad_halo_ok(const ConvArgs& a) {
+  if (a.stride != 1 || a.R != 3 || a.S != 3 || a.pad != 1 || a.P != a.H || a.Q != a.W) return false;
+  if (!(a.W == 8 || a.W == 16 || a.W == 32) || a.H % (32 / a.W)) return false;
+  return a.K % 64 == 0 && a.C % 32 == 0;
+}
+
 DDL_API int ddl_conv_wgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
   const ConvArgs& a = *ap;
   if (!conv_shapes_ok(a)) return (int)hipErrorInvalidValue;
+  const bool halo_cfg = cfg && (((cfg >> 24) & 0xff) & 0x40);
+  bool halo_pick = false;
+  if (!cfg && halo_auto() && a.accumulate && wgrad_halo_ok(a) && a.W >= 16) {
+    // ~2 workgroups per CU, and only with >= 64 K-steps per split: the halo tile covers all 9
+    // taps of 32 channels, so grids of few clients would need splits too short to pay for the
+    // per-step row window (sweep: profiles/conv_wgrad_halo_r1.log; 8 clients: layer 1 155 ->
+    // 102 us, layer 2 107 -> 100 us; 1 client and 8x8 layers stay streamed)
+    const long long tiles = (long long)(a.K / 64) * (a.C / 32) * a.G;
+    const long long nk = (long long)a.N * a.H * a.W / 32;
+    const long long sp = (2LL * num_cus() + tiles - 1) / tiles;
+    halo_pick = nk / sp >= 64;
+  }
+  if (halo_cfg || halo_pick) {  // halo tile: 64 x (9 taps x 32 channels)
+    if (!wgrad_halo_ok(a) || (halo_cfg && ((cfg & 0xff) != 4 || ((cfg >> 8) & 0xff) != 18)))
+      return (int)hipErrorInvalidValue;
+    const long long tiles = (long long)(a.K / 64) * (a.C / 32) * a.G;
+    const long long nk = (long long)a.N * a.H * a.W / 32;
+    long long sp = a.split_k ? a.split_k : (2LL * num_cus() + tiles - 1) / tiles;
+    if (sp > nk / 8) sp = nk / 8 > 0 ? nk / 8 : 1;
+    if (sp > 1024) sp = 1024;
+    if (sp > 1 && !a.accumulate) return (int)hipErrorInvalidValue;
+    return (int)launch_cfg<MODE_WGRAD, 64, 288, 32, 4, 2, true>(a, a.K, a.R * a.S * a.C, (int)sp, stream);
+  }
   const int Pd = a.K, Qd = a.R * a.S * a.C;
   const long long Kr = (long long)a.N * a.P * a.Q;
   int bp = a.K >= 128 ? 128 : 64, bq = Qd >= 128 ? 128 : 64, bk = 32, ns = 4;

@@ -73,6 +73,7 @@ def main():
     ap.add_argument("--layers", default="", help="comma list of layer names to run (default all)")
     ap.add_argument("--splits", default="", help="FWD/DGRAD split-K counts to time, e.g. 1,2,4")
     ap.add_argument("--split-sweep", action="store_true", help="also sweep tiles x splits")
+    ap.add_argument("--wh-splits", default="", help="halo WGRAD split-K counts to time, e.g. 4,8,16")
     ap.add_argument("--epi", action="store_true",
                     help="time with the fused epilogues of training (residual; mask + BN-backward reduce)")
     args = ap.parse_args()
@@ -108,6 +109,15 @@ def main():
             t = timeit(lambda: f(0))
             row[mode] = {"ms": t, "tflops": fl / t / 1e9}
             tot[mode] += t
+            if args.wh_splits and mode == "wgrad":
+                hcfg = Fn.conv_cfg(64, 288, 32, 4, halo=True)
+                row[mode]["halo_splits_us"] = {}
+                for k in args.wh_splits.split(","):
+                    try:
+                        row[mode]["halo_splits_us"][int(k)] = round(1e3 * timeit(
+                            lambda: Fn.conv_wgrad(dy, x, g, dw, cfg=hcfg, splits=int(k))), 1)
+                    except Exception:
+                        pass
             if args.splits and mode != "wgrad":
                 row[mode]["splits_us"] = {int(k): round(1e3 * timeit(lambda: f(0, int(k))), 1)
                                           for k in args.splits.split(",")}
@@ -131,6 +141,8 @@ def main():
                 if mode != "wgrad":  # halo-staged 3x3 stride-1 kernels (raise where ineligible)
                     cands += [(f"halo{bp}x{bq}s{ns}", Fn.conv_cfg(bp, bq, 32, ns, halo=True))
                               for bp, bq, ns in Fn.HALO_TILES]
+                else:
+                    cands.append(("halo64x288s4", Fn.conv_cfg(64, 288, 32, 4, halo=True)))
                 for label, cfg in cands:
                     try:
                         tc = timeit(lambda: f(cfg), reps=5, rounds=3)
@@ -156,6 +168,8 @@ def main():
         for mode in ("fwd", "dgrad", "wgrad"):
             if mode in row:
                 msg += f" | {mode} {row[mode]['ms'] * 1e3:7.1f}us {row[mode]['tflops']:6.0f}TF"
+                if "halo_splits_us" in row[mode]:
+                    msg += f" halo-splits{row[mode]['halo_splits_us']}"
                 if "splits_us" in row[mode]:
                     msg += f" split{row[mode]['splits_us']}"
                 if "best_cfg" in row[mode]:

@@ -146,6 +146,37 @@ def test_conv_halo(cuda, geom):
     _close(Fn.conv_dgrad(dy, w, g, residual=res, mask=mask), dx_ref)
 
 
+WGRAD_HALO_GEOMS = [
+    ConvGeom(G=2, N=3, H=32, W=32, C=64, K=64, R=3, S=3, stride=1, pad=1),
+    ConvGeom(G=1, N=2, H=16, W=16, C=96, K=128, R=3, S=3, stride=1, pad=1),
+    ConvGeom(G=2, N=3, H=8, W=8, C=32, K=64, R=3, S=3, stride=1, pad=1),
+    ConvGeom(G=1, N=2, H=4, W=32, C=64, K=192, R=3, S=3, stride=1, pad=1),
+]
+
+
+@pytest.mark.parametrize("geom", WGRAD_HALO_GEOMS, ids=lambda g: f"{g.C}x{g.K}_{g.H}x{g.W}")
+def test_conv_wgrad_halo(cuda, geom):
+    """Halo WGRAD (a 32-pixel K-step's rows + halo DMA'd once, 9 taps read shifted windows) ==
+    the fp32 reference, for split-K counts 1, 3 and automatic, accumulating into a strided view."""
+    g = geom
+    x = _rand(g.G, g.N, g.H, g.W, g.C, dev=cuda)
+    dy = _rand(g.G, g.N, g.P, g.Q, g.K, dev=cuda)
+    dw_ref = torch.zeros(g.G, g.K, g.R, g.S, g.C)
+    ref.conv_wgrad(dy.cpu(), x.cpu(), g, dw_ref)
+    cfg = Fn.conv_cfg(64, 288, 32, 4, halo=True)
+    inner = g.K * g.R * g.S * g.C
+    for splits in (1, 3, 0):
+        flat = torch.zeros(g.G, inner + 64, device=cuda)
+        dw = flat[:, 32:32 + inner].unflatten(1, (g.K, g.R, g.S, g.C))
+        Fn.conv_wgrad(dy, x, g, dw, accumulate=True, cfg=cfg, splits=splits)
+        _close(dw, dw_ref, rel=2e-3)
+        assert flat[:, :32].abs().max().item() == 0 and flat[:, 32 + inner:].abs().max().item() == 0
+    with pytest.raises(RuntimeError):  # not eligible: stride 2
+        g2 = ConvGeom(G=1, N=2, H=8, W=8, C=64, K=64, R=3, S=3, stride=2, pad=1)
+        Fn.conv_wgrad(_rand(1, 2, 4, 4, 64, dev=cuda), _rand(1, 2, 8, 8, 64, dev=cuda), g2,
+                      torch.zeros(1, 64, 3, 3, 64, device=cuda), cfg=cfg)
+
+
 def test_batchnorm(cuda):
     G, N, H, W, C = 2, 5, 6, 6, 64
     x = _rand(G, N, H, W, C, dev=cuda, scale=2.0) + 0.5
