@@ -38,6 +38,16 @@ class Layer:
     # set by Net when the next layer already applied this layer's output activation mask.
     grad_premasked = False
     needs_input_grad = True
+    # Cross-layer BN-backward fusion (Net._plan_fusions): a layer whose output is
+    # relu(BN(c) [+ residual]) exposes (c, mean, rstd) via ``bn_out``; the consuming layer's final
+    # dgrad (``fuse_out_bn``) then applies that ReLU mask and reduces the BN's backward sums in its
+    # epilogue and returns (dx_masked, part); the producer's ``backward(..., part=part)`` skips its
+    # reduce pass, the mask read and the masked-gradient copy.
+    fuse_out_bn = False
+    accepts_part = False
+
+    def bn_out(self, ctx):
+        return None
 
     def declare(self, store: ParamStore, prefix: str) -> None:
         self.prefix = prefix
@@ -152,16 +162,20 @@ class ConvUnit(Layer):
             y = y.reshape(g.G, g.N, self.cout)
         return y, ctx
 
-    def backward(self, dy, ctx):
+    def bn_out(self, ctx):
+        return (ctx[1], ctx[3], ctx[4]) if (self.bn and self.act == RELU and not self.linear) else None
+
+    def backward(self, dy, ctx, part=None):
         st = self.store
         x4, c, y, mu, rs, g = ctx
         dy = dy.reshape(y.shape)
         if self.bn:
-            ymask = y if (self.act == RELU and not self.grad_premasked) else None
-            if self.act == LEAKY and not self.grad_premasked:
+            premasked = self.grad_premasked or part is not None
+            ymask = y if (self.act == RELU and not premasked) else None
+            if self.act == LEAKY and not premasked:
                 dy = Fn.act_bwd(y, dy, LEAKY)
             dc = Fn.bn_backward(dy, ymask, c, mu, rs, st.param(self.gamma), st.grad_of(self.gamma),
-                                st.grad_of(self.beta))
+                                st.grad_of(self.beta), part=part)
         else:
             dc = dy
             if self.act and not self.grad_premasked:

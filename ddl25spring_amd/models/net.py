@@ -42,6 +42,14 @@ class Net:
                     and not getattr(prev, "residual_out", False):
                 cur.mask_input = True
                 prev.grad_premasked = True
+        # residual blocks whose input is relu(BN(c) [+ r]) of the previous layer take over that
+        # BN's ReLU mask and backward reduce in their last dgrad epilogue (Layer.fuse_out_bn)
+        for prev, cur in zip(self.layers[:-1], self.layers[1:]):
+            if getattr(cur, "residual_out", False) and hasattr(cur, "bn_out") \
+                    and type(prev).bn_out is not Layer.bn_out and prev.out_act == RELU \
+                    and os.environ.get("DDL_FUSE_BN_BWD", "1") != "0":
+                cur.fuse_out_bn = True
+                prev.accepts_part = True
         if self.layers:
             self.layers[0].needs_input_grad = False
 
@@ -85,8 +93,17 @@ class Net:
     def backward_native(self, dy, ctxs):
         n = len(self.layers)
         with Fn.wgrad_overlap(self.device, self.overlap_wgrad) as ov:
+            part = None
             for j, (layer, c) in enumerate(zip(reversed(self.layers), reversed(ctxs))):
-                dy = layer.backward(dy, c)
+                i = n - 1 - j
+                kw = {"part": part} if part is not None else {}
+                fuse = None
+                if layer.fuse_out_bn and layer.needs_input_grad and i > 0:
+                    fuse = self.layers[i - 1].bn_out(ctxs[i - 1])
+                if fuse is not None:
+                    kw["fuse"] = fuse
+                r = layer.backward(dy, c, **kw)
+                dy, part = r if fuse is not None else (r, None)
                 if self.grad_hook is not None:
                     # the hook (a bucket all-reduce) must see this layer's grads from both streams
                     ov.run_joined(lambda i=n - 1 - j: self.grad_hook(i))

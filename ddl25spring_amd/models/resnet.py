@@ -87,10 +87,16 @@ class BasicBlock(Layer):
             dctx = None
         return out, (x, c1, a1, sc1, sh1, mu1, rs1, g1, c2, mu2, rs2, g2, out, dctx)
 
-    def backward(self, dout, ctx):
+    def bn_out(self, ctx):
+        return (ctx[8], ctx[9], ctx[10])  # (c2, mu2, rs2): out = relu(bn2(c2) + shortcut)
+
+    def backward(self, dout, ctx, part=None, fuse=None):
         x, c1, a1, sc1, sh1, mu1, rs1, g1, c2, mu2, rs2, g2, out, dctx = ctx
         st = self.store
-        dc2, dym = self.conv2.bn_backward(dout, out, c2, mu2, rs2, emit_dym=True)
+        if part is not None:  # dout arrives masked by (out > 0) with bn2's reduce sums
+            dc2, dym = self.conv2.bn_backward(dout, None, c2, mu2, rs2, part=part), dout
+        else:
+            dc2, dym = self.conv2.bn_backward(dout, out, c2, mu2, rs2, emit_dym=True)
         if dctx is not None:
             cs, mus, rss, gs = dctx
             dcs = self.down.bn_backward(dym, None, cs, mus, rss)
@@ -107,6 +113,8 @@ class BasicBlock(Layer):
         Fn.conv_wgrad(dc1, x, g1, st.grad_of(self.conv1.w))
         if not self.needs_input_grad:
             return None
+        if fuse is not None:  # the producer's ReLU mask (x > 0) and BN reduce in this epilogue
+            return Fn.conv_dgrad(dc1, st.shadow_of(self.conv1.w), g1, residual=dres, mask=x, bn=fuse)
         return Fn.conv_dgrad(dc1, st.shadow_of(self.conv1.w), g1, residual=dres)
 
     def flops(self, s):
@@ -168,10 +176,16 @@ class Bottleneck(Layer):
         return out, (x, (c1, a1, sc1, sh1, mu1, rs1, g1), (c2, a2, sc2, sh2, mu2, rs2, g2),
                      (c3, mu3, rs3, g3), out, dctx)
 
-    def backward(self, dout, ctx):
+    def bn_out(self, ctx):
+        return ctx[3][:3]  # (c3, mu3, rs3): out = relu(bn3(c3) + shortcut)
+
+    def backward(self, dout, ctx, part=None, fuse=None):
         x, (c1, a1, sc1, sh1, mu1, rs1, g1), (c2, a2, sc2, sh2, mu2, rs2, g2), (c3, mu3, rs3, g3), out, dctx = ctx
         st = self.store
-        dc3, dym = self.conv3.bn_backward(dout, out, c3, mu3, rs3, emit_dym=True)
+        if part is not None:  # dout arrives masked by (out > 0) with bn3's reduce sums
+            dc3, dym = self.conv3.bn_backward(dout, None, c3, mu3, rs3, part=part), dout
+        else:
+            dc3, dym = self.conv3.bn_backward(dout, out, c3, mu3, rs3, emit_dym=True)
         if dctx is not None:
             cs, mus, rss, gs = dctx
             dcs = self.down.bn_backward(dym, None, cs, mus, rss)
@@ -188,6 +202,8 @@ class Bottleneck(Layer):
         Fn.conv_wgrad(dc1, x, g1, st.grad_of(self.conv1.w))
         if not self.needs_input_grad:
             return None
+        if fuse is not None:
+            return Fn.conv_dgrad(dc1, st.shadow_of(self.conv1.w), g1, residual=dres, mask=x, bn=fuse)
         return Fn.conv_dgrad(dc1, st.shadow_of(self.conv1.w), g1, residual=dres)
 
     def flops(self, s):

@@ -60,3 +60,18 @@ def test_wgrad_side_stream_resnet_within_noise_floor(cuda):
     for graph in (False, True):
         rel = _rel(_grads(cuda, resnet18_cifar, "cifar10", True, graph), ref)
         assert rel < 1.5 * floor + 0.02, (graph, rel, floor)
+
+
+def test_cross_block_bn_backward_fusion_within_noise_floor(cuda, monkeypatch):
+    """Residual blocks fuse the previous layer's ReLU mask + BN backward reduce into their last
+    dgrad epilogue (Net._plan_fusions). Same gradients as the unfused backward, within the
+    BN-atomics noise floor of two identical runs."""
+    monkeypatch.setenv("DDL_FUSE_BN_BWD", "0")
+    ref = _grads(cuda, resnet18_cifar, "cifar10", False, False)
+    floor = _rel(_grads(cuda, resnet18_cifar, "cifar10", False, False), ref)
+    monkeypatch.setenv("DDL_FUSE_BN_BWD", "1")
+    net = resnet18_cifar(groups=2)
+    assert sum(bool(layer.fuse_out_bn) for layer in net.layers) == 8
+    for graph in (False, True):
+        rel = _rel(_grads(cuda, resnet18_cifar, "cifar10", False, graph), ref)
+        assert rel < 1.5 * floor + 0.02, (graph, rel, floor)
