@@ -1,0 +1,108 @@
+"""Per-shape conv tile autotuner (on-device, first eager use).
+
+The conv kernels have a built-in heuristic (conv_igemm.hip: tile by channel count, small-grid
+fallbacks, automatic halo / split-K), but the best tile moves with the client count per GPU: at
+1-8 clients per GPU the same ResNet-18 layer has a different winner (profiles/conv_halo_sweep_*,
+conv_wgrad_halo_r1.log; the FedAvg scaling runs put 8, 4, 2 and 1 clients on a GPU). So the first
+EAGER call of each (mode, shape, fused-epilogue) key times the heuristic and a short list of
+candidate tiles (streamed, halo-staged, halo WGRAD split counts) on scratch outputs, HIP events
+around a few back-to-back launches, and caches the fastest. Later calls — including the ones
+captured into the training step's HIP graph — use the cached pick. A key first met during graph
+capture runs the heuristic (nothing is timed inside a capture).
+
+DDL_CONV_AUTOTUNE=0 disables it (the heuristic everywhere).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from . import workspace as ws
+
+ENABLED = os.environ.get("DDL_CONV_AUTOTUNE", "1") != "0"
+_CACHE: dict = {}
+
+_FD_TILES = [(64, 128, 32, 4), (128, 128, 32, 3), (128, 128, 64, 2), (128, 256, 32, 2),
+             (48, 256, 64, 2), (64, 128, 64, 3), (64, 64, 64, 3), (128, 64, 64, 3), (48, 256, 32, 4)]
+_FD_HALO = [(48, 256, 4), (48, 128, 4), (128, 128, 4)]
+_WG_TILES = [(128, 128, 32, 3), (64, 128, 32, 4), (64, 64, 64, 3), (128, 64, 64, 3), (128, 128, 64, 2)]
+
+
+def _cfg(bp, bq, bk, ns, halo=False):
+    from .functional import conv_cfg
+    return conv_cfg(bp, bq, bk, ns, halo)
+
+
+def candidates(mode: str, geom, accumulate: bool = True) -> list:
+    """(cfg, splits) pairs; cfg None = the kernel heuristic."""
+    from .functional import halo_eligible
+    out = [(None, 0)]
+    if mode in ("fwd", "dgrad"):
+        red = geom.C if mode == "fwd" else geom.K
+        out += [(_cfg(*t), 0) for t in _FD_TILES if red % t[2] == 0]
+        out += [(_cfg(bp, bq, 32, ns, True), 0) for bp, bq, ns in _FD_HALO
+                if halo_eligible(geom, bq, ns) and red % 32 == 0]
+    else:
+        out += [(_cfg(*t), 0) for t in _WG_TILES if accumulate]
+        if accumulate and wgrad_halo_eligible(geom):
+            tiles = (geom.K // 64) * (geom.C // 32) * geom.G
+            nk = geom.N * geom.H * geom.W // 32
+            sp = max(1, -(-512 // tiles))
+            for s in sorted({max(1, sp // 2), sp, 2 * sp, 4 * sp}):
+                if s <= max(1, nk // 8):
+                    out.append((_cfg(64, 288, 32, 4, True), s))
+    return out
+
+
+def wgrad_halo_eligible(g) -> bool:
+    """Mirror of conv_igemm.hip ``wgrad_halo_ok``."""
+    return ((g.stride, g.R, g.S, g.pad) == (1, 3, 3, 1) and g.W in (8, 16, 32)
+            and g.H % (32 // g.W) == 0 and g.K % 64 == 0 and g.C % 32 == 0)
+
+
+def _key(mode, geom, flags):
+    return (mode, geom.G, geom.N, geom.H, geom.W, geom.C, geom.K, geom.R, geom.S, geom.stride,
+            geom.pad, flags)
+
+
+def _time(run, cfg, sp, reps=4) -> float:
+    run(cfg, sp)  # warm (and validity: raises on an ineligible tile)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        run(cfg, sp)
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def pick(mode: str, geom, flags: tuple, run, accumulate: bool = True):
+    """The cached (cfg, splits) for this key, tuning it now if allowed. ``run(cfg, splits)`` must
+    launch the op with scratch outputs (cfg None = heuristic)."""
+    key = _key(mode, geom, flags)
+    hit = _CACHE.get(key)
+    if hit is not None:
+        return hit
+    if not ENABLED or torch.cuda.is_current_stream_capturing():
+        return (None, 0)
+    from ._lib import KernelError
+    saved = ws._CURRENT
+    ws._CURRENT = None  # scratch sums from torch.zeros, not the step arena
+    try:
+        best, best_t = (None, 0), float("inf")
+        for cfg, sp in candidates(mode, geom, accumulate):
+            try:
+                t = _time(run, cfg, sp)
+            except KernelError:
+                continue
+            if t < best_t * 0.97 or (cfg is None and t < best_t):  # ties keep the heuristic
+                best, best_t = (cfg, sp), t
+    finally:
+        ws._CURRENT = saved
+    _CACHE[key] = best
+    return best
+
+
+def cache() -> dict:
+    return dict(_CACHE)

@@ -14,6 +14,7 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib
+from . import autotune
 from . import reference as ref
 from . import workspace as ws
 from ._lib import check, ptr, stream
@@ -146,7 +147,7 @@ def stats_buffer(G: int, C: int, device) -> torch.Tensor:
 
 
 def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out=None, cfg=0,
-             residual=None, split_k=0):
+             residual=None, split_k=0, _tune=True):
     """y[G,N,P,Q,K] = conv(x[G,N,H,W,C], w[G,K,R,S,C]) (+bias)(+residual)(relu);
     stats ([G,S,2,K] from ``stats_buffer``, or [G,2,K]) += per-channel sum, sumsq of y.
     split_k: 0 = automatic split-K for grids too small to fill the GPU, 1 = off, n = n slices."""
@@ -163,6 +164,14 @@ def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out=None, 
                                                 dtype=torch.bfloat16, device=x.device)
     if residual is not None and (residual.stride(0) != y.stride(0) or not residual.is_contiguous()):
         residual = residual.contiguous()
+    if _tune and cfg == 0 and split_k == 0 and autotune.ENABLED:
+        def run(c, sp):
+            conv_fwd(x, w, geom, bias=bias, relu=relu, out=torch.empty_like(y), cfg=c or 0,
+                     stats=None if stats is None else torch.zeros_like(stats), residual=residual,
+                     split_k=sp, _tune=False)
+        c, split_k = autotune.pick("fwd", geom, (bias is not None, bool(relu), stats is not None,
+                                                 residual is not None), run)
+        cfg = c or 0
     a = _conv_args(geom, x.device, split_k, True, x=ptr(x), w=ptr(w), out=ptr(y), stats=ptr(stats), bias=ptr(bias),
                    residual=ptr(residual), x_gs=_gs(x), w_gs=_gs(w), out_gs=_gs(y),
                    bias_gs=_gs(bias), stats_gs=0 if stats is None else stats.stride(0),
@@ -172,7 +181,7 @@ def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out=None, 
 
 
 def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0, bn=None, split_k=0,
-               mask_bn=None):
+               mask_bn=None, _tune=True):
     """dx[G,N,H,W,C] = conv_transpose(dy, w) (+residual) * (mask > 0).
 
     bn = (x, mean, rstd): also reduce, in the epilogue, the preceding BatchNorm's backward sums
@@ -208,6 +217,13 @@ def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0,
         residual = residual.contiguous()
     if mask is not None and mask.stride(0) != dx.stride(0):
         mask = mask.contiguous()
+    if _tune and cfg == 0 and split_k == 0 and autotune.ENABLED:
+        def run(c, sp):
+            conv_dgrad(dy, w, geom, residual=residual, mask=mask, out=torch.empty_like(dx), cfg=c or 0,
+                       bn=bn, split_k=sp, mask_bn=mask_bn, _tune=False)
+        c, split_k = autotune.pick("dgrad", geom, (residual is not None, mask is not None, bn is not None,
+                                                   mask_bn is not None), run)
+        cfg = c or 0
     part = None
     kw = {}
     if bn is not None:
@@ -226,7 +242,7 @@ def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0,
     return dx if bn is None else (dx, part)
 
 
-def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0):
+def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0, _tune=True):
     """dw[G,K,R,S,C] (+)= sum over pixels dy (x) x  — fp32, split-K with atomics.
     cfg = conv_cfg(bp, bq, bk, stages) (0: tuned default); splits = split-K slices (0: auto).
     Inside ``wgrad_overlap`` the launch goes to the side stream (see there)."""
@@ -234,6 +250,16 @@ def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0):
         ref.conv_wgrad(dy, x, geom, dw, accumulate)
         return dw
     _check_inner(dy, "dy"); _check_inner(x, "x"); _check_inner(dw, "dw")
+    if _tune and cfg == 0 and splits == 0 and autotune.ENABLED:
+        def run(c, sp):
+            global _WGRAD_SIDE
+            side, _WGRAD_SIDE = _WGRAD_SIDE, None  # timed on the current stream
+            try:
+                conv_wgrad(dy, x, geom, torch.zeros_like(dw), accumulate, cfg=c or 0, splits=sp, _tune=False)
+            finally:
+                _WGRAD_SIDE = side
+        c, splits = autotune.pick("wgrad", geom, (bool(accumulate),), run, accumulate=bool(accumulate))
+        cfg = c or 0
     a = _conv_args(geom, dy.device, 1 if not accumulate else int(splits), x=ptr(x), dy=ptr(dy),
                    out=ptr(dw), x_gs=_gs(x), dy_gs=_gs(dy), out_gs=_gs(dw), accumulate=int(accumulate))
     side = _WGRAD_SIDE

@@ -13,3 +13,9 @@ if [ -n "$ITER_R50" ]; then
   timeout -k 10 300 python benchmarks/bench_resnet50_dp.py --steps 10 --warmup 3 > gpurun_out/r50.log 2>&1 || { tail -20 gpurun_out/r50.log; exit 1; }
   grep '^{' gpurun_out/r50.log | cut -c1-160
 fi
+if [ -n "$ITER_G42" ]; then
+  timeout -k 10 200 python bench.py --clients 4 --train-size 25000 --steps 3 --warmup 1 > gpurun_out/hb4.log 2>&1 || { tail -20 gpurun_out/hb4.log; exit 1; }
+  grep '^{' gpurun_out/hb4.log | cut -c1-160
+  timeout -k 10 200 python bench.py --clients 2 --train-size 12500 --steps 3 --warmup 1 > gpurun_out/hb2.log 2>&1 || { tail -20 gpurun_out/hb2.log; exit 1; }
+  grep '^{' gpurun_out/hb2.log | cut -c1-160
+fi

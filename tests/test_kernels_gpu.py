@@ -325,9 +325,11 @@ def test_prep_images(cuda):
 
 @pytest.mark.parametrize("geom", [ConvGeom(G=2, N=3, H=8, W=8, C=64, K=96, R=3, S=3, stride=1, pad=1),
                                   ConvGeom(G=1, N=2, H=9, W=7, C=128, K=64, R=3, S=3, stride=2, pad=1)])
-def test_conv_dgrad_fused_bn_reduce(cuda, geom):
+def test_conv_dgrad_fused_bn_reduce(cuda, geom, monkeypatch):
     """dgrad epilogue = mask + the preceding BN's backward reduce; bn_backward(part=) then matches
-    the unfused three-launch backward."""
+    the unfused three-launch backward. (Autotuner off: the bitwise check needs one tile for both.)"""
+    from ddl25spring_amd.ops import autotune
+    monkeypatch.setattr(autotune, "ENABLED", False)
     g = geom
     dy = _rand(g.G, g.N, g.P, g.Q, g.K, dev=cuda)
     w = _weights(g, cuda)
