@@ -1,0 +1,57 @@
+"""Conv autotuner bookkeeping (no GPU): candidate lists respect each kernel family's contract,
+the heuristic is always a candidate, and picks are cached per (mode, shape, epilogue) key."""
+from ddl25spring_amd.ops import autotune
+from ddl25spring_amd.ops import functional as Fn
+from ddl25spring_amd.ops.functional import ConvGeom
+
+
+def _decode(cfg):
+    ns = (cfg >> 24) & 0xFF
+    return (cfg & 0xFF) * 16, ((cfg >> 8) & 0xFF) * 16, (cfg >> 16) & 0xFF, ns & 0x3F, bool(ns & 0x40)
+
+
+def test_candidates_respect_kernel_contracts():
+    g = ConvGeom(G=8, N=100, H=32, W=32, C=64, K=64, R=3, S=3, stride=1, pad=1)
+    for mode in ("fwd", "dgrad", "wgrad"):
+        cands = autotune.candidates(mode, g)
+        assert cands[0] == (None, 0)
+        halos = [c for c, _ in cands[1:] if _decode(c)[4]]
+        assert halos, mode  # layer-1 shape admits halo tiles in every mode
+        for c, sp in cands[1:]:
+            bp, bq, bk, ns, halo = _decode(c)
+            if halo and mode != "wgrad":
+                assert bk == 32 and Fn.halo_eligible(g, bq, ns)
+            if halo and mode == "wgrad":
+                assert (bp, bq) == (64, 288) and sp >= 1
+    # stride 2 / 1x1: no halo candidates, and the reduction must divide BK
+    g2 = ConvGeom(G=1, N=4, H=16, W=16, C=96, K=128, R=1, S=1, stride=2, pad=0)
+    for mode in ("fwd", "dgrad", "wgrad"):
+        for c, _ in autotune.candidates(mode, g2)[1:]:
+            bp, bq, bk, ns, halo = _decode(c)
+            assert not halo
+            if mode == "fwd":
+                assert g2.C % bk == 0
+            if mode == "dgrad":
+                assert g2.K % bk == 0
+    # non-accumulating WGRAD cannot split-K: only the heuristic
+    assert autotune.candidates("wgrad", g, accumulate=False) == [(None, 0)]
+
+
+def test_halo_wgrad_eligibility_mirror():
+    ok = ConvGeom(G=1, N=2, H=16, W=16, C=32, K=64, R=3, S=3, stride=1, pad=1)
+    assert autotune.wgrad_halo_eligible(ok)
+    for bad in (ConvGeom(1, 2, 16, 16, 32, 96, 3, 3, 1, 1),   # K % 64
+                ConvGeom(1, 2, 4, 4, 32, 64, 3, 3, 1, 1),     # W = 4
+                ConvGeom(1, 2, 56, 56, 32, 64, 3, 3, 1, 1),   # W = 56
+                ConvGeom(1, 2, 16, 16, 32, 64, 3, 3, 2, 1)):  # stride 2
+        assert not autotune.wgrad_halo_eligible(bad)
+
+
+def test_pick_caches_and_respects_disable(monkeypatch):
+    g = ConvGeom(G=1, N=2, H=8, W=8, C=32, K=32, R=3, S=3, stride=1, pad=1)
+    monkeypatch.setattr(autotune, "ENABLED", False)
+    calls = []
+    assert autotune.pick("fwd", g, (False,), lambda c, s: calls.append(c)) == (None, 0)
+    assert not calls
+    monkeypatch.setitem(autotune._CACHE, autotune._key("fwd", g, (True,)), (123, 0))
+    assert autotune.pick("fwd", g, (True,), lambda c, s: calls.append(c)) == (123, 0)
