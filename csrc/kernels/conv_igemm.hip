@@ -784,36 +784,62 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         msh[k] = (mbn && pok) ? a.mask_shift[(long long)g * Pd + p + k] : 0.f;
         s1[k] = s2[k] = 0.f;
       }
+      // The strip's global inputs (BN input, residual, mask) are loaded one strip ahead, so their
+      // HBM latency overlaps the LDS round trip and the previous strip's arithmetic instead of
+      // being paid once per strip.
+      constexpr int IT = (NPX + PSTEP - 1) / PSTEP;  // items per thread per strip
+      auto item_off = [&](int tj, int it, long long& o) {
+        const int px = prow + it * PSTEP;
+        const int q = q0 + (px >> 4) * WQ + tj * 16 + (px & 15);
+        if (px >= NPX || !pok || q >= Qd) return false;
+        o = (long long)q * Pd + p;
+        if (phased) {  // phase-local pixel (n, i, j) -> NHWC offset of (n, 2i+a, 2j+b)
+          const int n = q / (Hs * Ws), rem = q - n * (Hs * Ws);
+          const int hi2 = rem / Ws, wi = rem - hi2 * Ws;
+          o = ((long long)(n * H + 2 * hi2 + ph_a) * W + 2 * wi + ph_b) * Pd + p;
+        }
+        return true;
+      };
+      auto load_in = [&](int tj, i4v* X, i4v* R, i4v* M) {
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+          long long o = 0;
+          const bool ok = item_off(tj, it, o);
+          X[it] = (ok && bnx) ? *(const i4v*)(bnx + o) : (i4v){0, 0, 0, 0};
+          R[it] = (ok && res) ? *(const i4v*)(res + o) : (i4v){0, 0, 0, 0};
+          M[it] = (ok && msk) ? *(const i4v*)(msk + o) : (i4v){0, 0, 0, 0};
+        }
+      };
+      i4v cX[IT], cR[IT], cM[IT];
+      load_in(0, cX, cR, cM);
       __syncthreads();  // every wave is done with the main loop's LDS (ring, halo)
 #pragma unroll
       for (int tj = 0; tj < TQ; ++tj) {
 #pragma unroll
         for (int ti = 0; ti < TP; ++ti)
           *(f4v*)(et + (wq * 16 + lq) * LROW + wp * WP + ti * 16 + lp) = acc[ti][tj];
+        i4v nX[IT], nR[IT], nM[IT];
+        if (tj + 1 < TQ) load_in(tj + 1, nX, nR, nM);
         __syncthreads();
-        for (int px = prow; px < NPX; px += PSTEP) {
-          const int q = q0 + (px >> 4) * WQ + tj * 16 + (px & 15);
-          if (!pok || q >= Qd) continue;
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+          long long o = 0;
+          if (!item_off(tj, it, o)) continue;
+          const int px = prow + it * PSTEP;
           const f4v lo = *(const f4v*)(et + px * LROW + c8 * 8);
           const f4v hi = *(const f4v*)(et + px * LROW + c8 * 8 + 4);
           float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[k] += bv[k];
-          long long o = (long long)q * Pd + p;
-          if (phased) {  // phase-local pixel (n, i, j) -> NHWC offset of (n, 2i+a, 2j+b)
-            const int n = q / (Hs * Ws), rem = q - n * (Hs * Ws);
-            const int hi2 = rem / Ws, wi = rem - hi2 * Ws;
-            o = ((long long)(n * H + 2 * hi2 + ph_a) * W + 2 * wi + ph_b) * Pd + p;
-          }
           float t[8], xb[8];
-          if (bnx) unpack8(*(const i4v*)(bnx + o), xb);
+          if (bnx) unpack8(cX[it], xb);
           if (res) {
-            unpack8(*(const i4v*)(res + o), t);
+            unpack8(cR[it], t);
 #pragma unroll
             for (int k = 0; k < 8; ++k) v[k] += t[k];
           }
           if (msk) {
-            unpack8(*(const i4v*)(msk + o), t);
+            unpack8(cM[it], t);
 #pragma unroll
             for (int k = 0; k < 8; ++k) if (!(t[k] > 0.f)) v[k] = 0.f;
           } else if (mbn) {
@@ -834,6 +860,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
           }
         }
         __syncthreads();
+        if (tj + 1 < TQ) {
+#pragma unroll
+          for (int it = 0; it < IT; ++it) { cX[it] = nX[it]; cR[it] = nR[it]; cM[it] = nM[it]; }
+        }
       }
       if (want_stats) {
         // fold the partial sums of the PSTEP threads that share each channel chunk
