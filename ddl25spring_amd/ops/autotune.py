@@ -24,9 +24,13 @@ ENABLED = os.environ.get("DDL_CONV_AUTOTUNE", "1") != "0"
 _CACHE: dict = {}
 
 _FD_TILES = [(64, 128, 32, 4), (128, 128, 32, 3), (128, 128, 64, 2), (128, 256, 32, 2),
-             (48, 256, 64, 2), (64, 128, 64, 3), (64, 64, 64, 3), (128, 64, 64, 3), (48, 256, 32, 4)]
+             (48, 256, 64, 2), (64, 128, 64, 3), (64, 64, 64, 3), (128, 64, 64, 3), (48, 256, 32, 4),
+             (256, 128, 32, 3)]
 _FD_HALO = [(48, 256, 4), (48, 128, 4), (128, 128, 4)]
-_WG_TILES = [(128, 128, 32, 3), (64, 128, 32, 4), (64, 64, 64, 3), (128, 64, 64, 3), (128, 128, 64, 2)]
+# WGRAD re-fetches dy once per column tile and x once per (row tile, tap): the 256-wide tiles
+# halve one of the two on the deep layers (512 x 4608 outputs)
+_WG_TILES = [(128, 128, 32, 3), (64, 128, 32, 4), (64, 64, 64, 3), (128, 64, 64, 3), (128, 128, 64, 2),
+             (256, 128, 32, 3), (128, 256, 32, 3), (256, 128, 32, 2), (128, 256, 32, 2)]
 
 
 def _cfg(bp, bq, bk, ns, halo=False):
