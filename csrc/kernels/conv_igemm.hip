@@ -1269,6 +1269,12 @@ DDL_API int ddl_conv_wgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
     if (sp > nk / 8) sp = nk / 8 > 0 ? nk / 8 : 1;
     if (sp > 1024) sp = 1024;
     if (sp > 1 && !a.accumulate) return (int)hipErrorInvalidValue;
+    const int hns = halo_cfg ? ((cfg >> 24) & 0x3f) : 4;  // LDS stages (12 KiB each)
+    if (hns == 6)
+      return (int)launch_cfg<MODE_WGRAD, 64, 288, 32, 6, 2, true>(a, a.K, a.R * a.S * a.C, (int)sp, stream);
+    if (hns == 5)
+      return (int)launch_cfg<MODE_WGRAD, 64, 288, 32, 5, 2, true>(a, a.K, a.R * a.S * a.C, (int)sp, stream);
+    if (hns != 4) return (int)hipErrorInvalidValue;
     return (int)launch_cfg<MODE_WGRAD, 64, 288, 32, 4, 2, true>(a, a.K, a.R * a.S * a.C, (int)sp, stream);
   }
   const int Pd = a.K, Qd = a.R * a.S * a.C;

@@ -55,7 +55,7 @@ def candidates(mode: str, geom, accumulate: bool = True) -> list:
             sp = max(1, -(-512 // tiles))
             for s in sorted({max(1, sp // 2), sp, 2 * sp, 4 * sp}):
                 if s <= max(1, nk // 8):
-                    out.append((_cfg(64, 288, 32, 4, True), s))
+                    out.append((_cfg(64, 288, 32, 4, True), s))  # 5-6 stages: no faster
     return out
 
 

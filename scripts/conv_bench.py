@@ -110,14 +110,15 @@ def main():
             row[mode] = {"ms": t, "tflops": fl / t / 1e9}
             tot[mode] += t
             if args.wh_splits and mode == "wgrad":
-                hcfg = Fn.conv_cfg(64, 288, 32, 4, halo=True)
                 row[mode]["halo_splits_us"] = {}
-                for k in args.wh_splits.split(","):
-                    try:
-                        row[mode]["halo_splits_us"][int(k)] = round(1e3 * timeit(
-                            lambda: Fn.conv_wgrad(dy, x, g, dw, cfg=hcfg, splits=int(k))), 1)
-                    except Exception:
-                        pass
+                for ns in (4, 5, 6):
+                    hcfg = Fn.conv_cfg(64, 288, 32, ns, halo=True)
+                    for k in args.wh_splits.split(","):
+                        try:
+                            row[mode]["halo_splits_us"][f"s{ns}/{k}"] = round(1e3 * timeit(
+                                lambda: Fn.conv_wgrad(dy, x, g, dw, cfg=hcfg, splits=int(k))), 1)
+                        except Exception:
+                            pass
             if args.splits and mode != "wgrad":
                 row[mode]["splits_us"] = {int(k): round(1e3 * timeit(lambda: f(0, int(k))), 1)
                                           for k in args.splits.split(",")}
