@@ -49,6 +49,9 @@ def candidates(mode: str, geom, accumulate: bool = True) -> list:
                 if halo_eligible(geom, bq, ns) and red % 32 == 0]
     else:
         out += [(_cfg(*t), 0) for t in _WG_TILES if accumulate]
+        if accumulate:  # the heuristic tile at explicit split-K depths (small grids: 1-2 clients)
+            nk = geom.N * geom.P * geom.Q // 32
+            out += [(None, s) for s in (4, 8, 16, 32, 64) if s <= max(1, nk // 8)]
         if accumulate and wgrad_halo_eligible(geom):
             tiles = (geom.K // 64) * (geom.C // 32) * geom.G
             nk = geom.N * geom.H * geom.W // 32
