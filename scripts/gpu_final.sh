@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-end rehearsal: what the driver runs (GPU tests, smoke, 1-GPU bench) + every BASELINE
+# config bench and the headline profile. Stops at the first failure.
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out/final
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/final/tests.log 2>&1 || { tail -30 gpurun_out/final/tests.log; exit 1; }
+tail -1 gpurun_out/final/tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/final/smoke.log 2>&1 || { tail -20 gpurun_out/final/smoke.log; exit 1; }
+grep smoke gpurun_out/final/smoke.log | cut -c1-200
+timeout -k 10 300 python bench.py > gpurun_out/final/bench_default.log 2>&1 || { tail -20 gpurun_out/final/bench_default.log; exit 1; }
+grep '^{' gpurun_out/final/bench_default.log | cut -c1-220
+bash scripts/gpu_all_bench.sh
