@@ -908,6 +908,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 // Split-K epilogue for FWD / DGRAD: out = epi(sum_s partial[s]) with the same fused terms as the
 // conv epilogue (bias, residual, mask, relu, BN statistics or the BN backward reduce). Each thread
 // owns one 8-channel chunk; per-block sums fold through LDS and go to stripe blockIdx.x % stripes.
+#ifndef SPLITK_EPI_RB
+#define SPLITK_EPI_RB 2
+#endif
 __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvArgs a, int mode, int Pd,
                                                                    long long rows, int nsplit) {
   __shared__ float red[256 * 16];
@@ -942,9 +945,10 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvArgs a, i
       msh[k] = a.mask_shift[(long long)g * Pd + c0 + k];
     }
   }
-  // RB rows per thread per pass, all their slice loads issued before any use; few enough blocks
-  // that the per-block statistics atomics (2 x Pd each) stay cheap
-  constexpr int RB = 4;
+  // RB rows per thread per pass; the slices are summed SPB at a time with all RB x SPB loads
+  // issued before any use (one memory round trip per SPB slices, not one per slice: the 1-client
+  // deep layers run 4-8 slices and this kernel was latency-bound on the serial slice loop).
+  constexpr int RB = SPLITK_EPI_RB, SPB = 4;
   const long long stride = (long long)gridDim.x * RPI;
   if (row < RPI) {
     for (long long r0 = (long long)blockIdx.x * RPI + row; r0 < rows; r0 += stride * RB) {
@@ -953,19 +957,39 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvArgs a, i
       for (int b = 0; b < RB; ++b)
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[b][k] = bv[k];
-      for (int sp = 0; sp < nsplit; ++sp) {
-        f4v lo[RB], hi[RB];
+      long long eb[RB];
 #pragma unroll
-        for (int b = 0; b < RB; ++b) {
-          const long long r = r0 + b * stride;
-          const long long e = (r < rows ? r : r0) * Pd + sp * slice;
-          lo[b] = *(const f4v*)(part + e);
-          hi[b] = *(const f4v*)(part + e + 4);
+      for (int b = 0; b < RB; ++b) {
+        const long long r = r0 + b * stride;
+        eb[b] = (r < rows ? r : r0) * Pd;
+      }
+      // the bf16 side operands do not depend on the sums: issue them with the first slices
+      i4v xres[RB], xmsk[RB], xbnx[RB];
+#pragma unroll
+      for (int b = 0; b < RB; ++b) {
+        if (res) xres[b] = *(const i4v*)(res + eb[b]);
+        if (msk) xmsk[b] = *(const i4v*)(msk + eb[b]);
+        if (bnx) xbnx[b] = *(const i4v*)(bnx + eb[b]);
+      }
+      for (int sp0 = 0; sp0 < nsplit; sp0 += SPB) {
+        f4v lo[SPB][RB], hi[SPB][RB];
+#pragma unroll
+        for (int j = 0; j < SPB; ++j) {
+          const long long so = (long long)(sp0 + j < nsplit ? sp0 + j : sp0) * slice;
+#pragma unroll
+          for (int b = 0; b < RB; ++b) {
+            lo[j][b] = *(const f4v*)(part + eb[b] + so);
+            hi[j][b] = *(const f4v*)(part + eb[b] + so + 4);
+          }
         }
 #pragma unroll
-        for (int b = 0; b < RB; ++b) {
-          v[b][0] += lo[b][0]; v[b][1] += lo[b][1]; v[b][2] += lo[b][2]; v[b][3] += lo[b][3];
-          v[b][4] += hi[b][0]; v[b][5] += hi[b][1]; v[b][6] += hi[b][2]; v[b][7] += hi[b][3];
+        for (int j = 0; j < SPB; ++j) {
+          if (sp0 + j >= nsplit) break;
+#pragma unroll
+          for (int b = 0; b < RB; ++b) {
+            v[b][0] += lo[j][b][0]; v[b][1] += lo[j][b][1]; v[b][2] += lo[j][b][2]; v[b][3] += lo[j][b][3];
+            v[b][4] += hi[j][b][0]; v[b][5] += hi[j][b][1]; v[b][6] += hi[j][b][2]; v[b][7] += hi[j][b][3];
+          }
         }
       }
 #pragma unroll
@@ -974,14 +998,14 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvArgs a, i
         if (r >= rows) break;
         const long long e = r * Pd;
         float t[8], xb[8];
-        if (bnx) unpack8(*(const i4v*)(bnx + e), xb);
+        if (bnx) unpack8(xbnx[b], xb);
         if (res) {
-          unpack8(*(const i4v*)(res + e), t);
+          unpack8(xres[b], t);
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[b][k] += t[k];
         }
         if (msk) {
-          unpack8(*(const i4v*)(msk + e), t);
+          unpack8(xmsk[b], t);
 #pragma unroll
           for (int k = 0; k < 8; ++k) if (!(t[k] > 0.f)) v[b][k] = 0.f;
         } else if (mbn) {
@@ -1022,7 +1046,7 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvArgs a, i
 static hipError_t splitk_epilogue(const ConvArgs& a, int mode, int Pd, long long rows, int nsplit,
                                   hipStream_t s) {
   const int RPI = 256 / (Pd / 8);
-  long long want = (rows + RPI * 4LL - 1) / (RPI * 4LL);  // RB = 4 rows per thread
+  long long want = (rows + RPI * (long long)SPLITK_EPI_RB - 1) / (RPI * (long long)SPLITK_EPI_RB);
   const long long cap = (2048 + a.G - 1) / a.G;
   if (want > cap) want = cap;
   hipLaunchKernelGGL(conv_splitk_epilogue_kernel, dim3((unsigned)(want < 1 ? 1 : want), a.G), dim3(256), 0, s,
