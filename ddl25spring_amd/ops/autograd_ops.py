@@ -23,6 +23,7 @@ _lib.register_signatures({
     "ddl_embedding_bwd": [vp, vp, vp, i32, i32, i32, vp],
     "ddl_rmsnorm_fwd": [vp, vp, vp, vp, i32, i32, f32, vp],
     "ddl_rmsnorm_bwd": [vp, vp, vp, vp, vp, vp, i32, i32, vp],
+    "ddl_rmsnorm_bwd_set_rows": [i32],
     "ddl_swiglu_fwd": [vp, vp, i32, i32, vp],
     "ddl_swiglu_bwd": [vp, vp, vp, i32, i32, vp],
     "ddl_add": [vp, vp, vp, i64, vp],

@@ -20,6 +20,22 @@ def _pair(t, cuda):
     return c, h
 
 
+@pytest.mark.parametrize("T,D", [(2048, 288), (4096, 288), (3, 2048), (1000, 520)])
+def test_rmsnorm_backward_shapes(cuda, T, D):
+    """Register-accumulated d(gamma): the LLaMA shape (8 x 256 tokens, 288 dims), more rows than the
+    grid covers in one sweep, the widest supported D (all 4 lane chunks) and a partly filled chunk."""
+    torch.manual_seed(1)
+    x = torch.randn(T, D)
+    gam = torch.rand(D) + 0.5
+    xc, xh = _pair(x, cuda); gc, gh = _pair(gam, cuda)
+    yc, yh = A.rmsnorm(xc, gc), A.rmsnorm(xh, gh)
+    assert _rel(yc, yh) < 1e-2
+    g = torch.randn_like(yh)
+    yc.backward(g.to(cuda)); yh.backward(g)
+    assert _rel(xc.grad, xh.grad) < 2e-2
+    assert _rel(gc.grad, gh.grad) < 1e-2
+
+
 def test_linear_rmsnorm_swiglu_embedding(cuda):
     torch.manual_seed(0)
     x = torch.randn(2, 37, 96)
