@@ -98,6 +98,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const bf16_t* __restri
                                                           const float* __restrict__ g,
                                                           const float* __restrict__ rstd,
                                                           const bf16_t* __restrict__ dy,
+                                                          const bf16_t* __restrict__ dres,
                                                           bf16_t* __restrict__ dx,
                                                           float* __restrict__ dg, int T, int D) {
   extern __shared__ float dg_part[];  // [4][D]
@@ -155,9 +156,10 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const bf16_t* __restri
       const int ch = lane + 64 * c;
       if (ch < NC) {
         float o[8];
+        if (dres) unpack8(*(const i4v*)(dres + (long long)row * D + ch * 8), o);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          o[k] = r * gv[c][k] * dv[c][k] - xv[c][k] * r3;
+          o[k] = (dres ? o[k] : 0.f) + r * gv[c][k] * dv[c][k] - xv[c][k] * r3;
           acc[c][k] += dv[c][k] * xv[c][k] * r;
         }
         *(i4v*)(dx + (long long)row * D + ch * 8) = pack8(o);
@@ -202,14 +204,16 @@ DDL_API int ddl_rmsnorm_fwd(const void* x, const float* g, void* y, float* rstd,
                      (bf16_t*)y, rstd, T, D, eps);
   return (int)hipGetLastError();
 }
-DDL_API int ddl_rmsnorm_bwd(const void* x, const float* g, const float* rstd, const void* dy, void* dx,
-                            float* dg, int T, int D, hipStream_t s) {
+// dres (nullable): gradient arriving through the residual branch of the same x, added into dx
+// (the residual fork of a pre-norm block; saves the separate gradient-sum pass).
+DDL_API int ddl_rmsnorm_bwd(const void* x, const float* g, const float* rstd, const void* dy,
+                            const void* dres, void* dx, float* dg, int T, int D, hipStream_t s) {
   if (D % 8 || D > 64 * 8 * 4) return (int)hipErrorInvalidValue;
   int rows = g_rmsnorm_bwd_rows_per_wave;
   if (rows <= 0) rows = (T + 1023) / 1024 > 4 ? (T + 1023) / 1024 : 4;
   const int blocks = grid_for(T, 4 * rows, 1 << 20);
   hipLaunchKernelGGL(rmsnorm_bwd_kernel<4>, dim3(blocks), dim3(256), 4 * D * sizeof(float), s,
-                     (const bf16_t*)x, g, rstd, (const bf16_t*)dy, (bf16_t*)dx, dg, T, D);
+                     (const bf16_t*)x, g, rstd, (const bf16_t*)dy, (const bf16_t*)dres, (bf16_t*)dx, dg, T, D);
   return (int)hipGetLastError();
 }
 

@@ -46,11 +46,11 @@ class Block(nn.Module):
             self.w2.mul_(1 / math.sqrt(2))
 
     def forward(self, x):  # x [B, S, D]
-        h = A.rmsnorm(x, self.norm1)
+        h, x = A.rmsnorm_fork(x, self.norm1)
         qkv = A.linear(h, self.wqkv)
         att = A.causal_attention(qkv, self.h, self.hd)
         x = A.linear(att, self.wo, residual=x)
-        h = A.rmsnorm(x, self.norm2)
+        h, x = A.rmsnorm_fork(x, self.norm2)
         return A.linear(A.swiglu(A.linear(h, self.w13)), self.w2, residual=x)
 
 

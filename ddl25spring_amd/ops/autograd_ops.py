@@ -22,7 +22,7 @@ _lib.register_signatures({
     "ddl_embedding_fwd": [vp, vp, vp, i32, i32, vp],
     "ddl_embedding_bwd": [vp, vp, vp, i32, i32, i32, vp],
     "ddl_rmsnorm_fwd": [vp, vp, vp, vp, i32, i32, f32, vp],
-    "ddl_rmsnorm_bwd": [vp, vp, vp, vp, vp, vp, i32, i32, vp],
+    "ddl_rmsnorm_bwd": [vp, vp, vp, vp, vp, vp, vp, i32, i32, vp],
     "ddl_rmsnorm_bwd_set_rows": [i32],
     "ddl_swiglu_fwd": [vp, vp, i32, i32, vp],
     "ddl_swiglu_bwd": [vp, vp, vp, i32, i32, vp],
@@ -123,8 +123,13 @@ def linear(x, w, b=None, residual=None):
 
 # ------------------------------------------------------------------------------------ rmsnorm
 class _RMSNorm(torch.autograd.Function):
+    """y = x * rsqrt(mean(x^2) + eps) * g. With ``fork`` the function also returns x itself (a view)
+    for a pre-norm block's residual branch, so the two gradients of x arrive in one backward call
+    and the residual one is added inside the RMSNorm backward kernel instead of by a separate
+    autograd gradient-sum pass."""
+
     @staticmethod
-    def forward(ctx, x, g, eps):
+    def forward(ctx, x, g, eps, fork):
         D = x.shape[-1]
         x2 = x.reshape(-1, D).contiguous()
         T = x2.shape[0]
@@ -135,28 +140,41 @@ class _RMSNorm(torch.autograd.Function):
               "rmsnorm_fwd")
         ctx.save_for_backward(x2, gd, rstd)
         ctx.shape, ctx.g = x.shape, g
+        if fork:
+            return y.view(x.shape), x.view_as(x)
         return y.view(x.shape)
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dres=None):
         x2, gd, rstd = ctx.saved_tensors
         T, D = x2.shape
         dx = torch.empty_like(x2)
         sink = _grad_sink(ctx.g) if ctx.needs_input_grad[1] else None
         dg = sink if sink is not None else torch.zeros(D, dtype=torch.float32, device=x2.device)
+        if dy is None:
+            dy = torch.zeros_like(x2)
         dyc = dy.reshape(T, D).to(torch.bfloat16).contiguous()
-        check(K().ddl_rmsnorm_bwd(ptr(x2), ptr(gd), ptr(rstd), ptr(dyc), ptr(dx), ptr(dg), T, D,
-                                  stream()), "rmsnorm_bwd")
+        drc = None if dres is None else dres.reshape(T, D).to(torch.bfloat16).contiguous()
+        check(K().ddl_rmsnorm_bwd(ptr(x2), ptr(gd), ptr(rstd), ptr(dyc), ptr(drc), ptr(dx), ptr(dg),
+                                  T, D, stream()), "rmsnorm_bwd")
         if sink is not None:
             _grad_ready(ctx.g)
             dg = None
-        return dx.view(ctx.shape), dg, None
+        return dx.view(ctx.shape), dg, None, None
 
 
 def rmsnorm(x, g, eps=1e-6):
     if not x.is_cuda:
         return x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + eps) * g
-    return _RMSNorm.apply(x.to(torch.bfloat16), g, eps)
+    return _RMSNorm.apply(x.to(torch.bfloat16), g, eps, False)
+
+
+def rmsnorm_fork(x, g, eps=1e-6):
+    """(rmsnorm(x, g), x) for a pre-norm residual block; on the GPU the residual branch's gradient
+    is summed into dx by the RMSNorm backward kernel."""
+    if not x.is_cuda:
+        return rmsnorm(x, g, eps), x
+    return _RMSNorm.apply(x.to(torch.bfloat16), g, eps, True)
 
 
 # ------------------------------------------------------------------------------------- swiglu

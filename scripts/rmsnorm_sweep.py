@@ -23,18 +23,18 @@ lib = K()
 for rows in (1, 2, 4, 8, 16, 0):
     lib.ddl_rmsnorm_bwd_set_rows(rows)
     for _ in range(20):
-        lib.ddl_rmsnorm_bwd(ptr(x), ptr(g), ptr(rstd), ptr(dy), ptr(dx), ptr(dg), T, D, stream())
+        lib.ddl_rmsnorm_bwd(ptr(x), ptr(g), ptr(rstd), ptr(dy), None, ptr(dx), ptr(dg), T, D, stream())
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(200):
-        lib.ddl_rmsnorm_bwd(ptr(x), ptr(g), ptr(rstd), ptr(dy), ptr(dx), ptr(dg), T, D, stream())
+        lib.ddl_rmsnorm_bwd(ptr(x), ptr(g), ptr(rstd), ptr(dy), None, ptr(dx), ptr(dg), T, D, stream())
     e1.record()
     torch.cuda.synchronize()
     print(f"T={T} D={D} rows/wave={rows or 'auto'}: {e0.elapsed_time(e1) / 200 * 1000:.2f} us per launch", flush=True)
 # numerics at the last setting vs fp32
 dg.zero_()
-lib.ddl_rmsnorm_bwd(ptr(x), ptr(g), ptr(rstd), ptr(dy), ptr(dx), ptr(dg), T, D, stream())
+lib.ddl_rmsnorm_bwd(ptr(x), ptr(g), ptr(rstd), ptr(dy), None, ptr(dx), ptr(dg), T, D, stream())
 xf, dyf = x.float(), dy.float()
 r = rstd[:, None]
 dot = (g * dyf * xf).sum(-1, keepdim=True) / D

@@ -36,6 +36,31 @@ def test_rmsnorm_backward_shapes(cuda, T, D):
     assert _rel(gc.grad, gh.grad) < 1e-2
 
 
+def test_rmsnorm_fork_sums_residual_gradient(cuda):
+    """rmsnorm_fork(x) = (rmsnorm(x), x): the residual branch's gradient is added inside the HIP
+    backward; compare with the fp32 op where autograd sums the two paths."""
+    torch.manual_seed(2)
+    x = torch.randn(4, 64, 288)
+    gam = torch.rand(288) + 0.5
+    w = torch.randn(288, 288) * 0.05
+    xc, xh = _pair(x, cuda); gc, gh = _pair(gam, cuda)
+    hc, rc = A.rmsnorm_fork(xc, gc)
+    hh, rh = A.rmsnorm_fork(xh, gh)
+    assert _rel(rc, xh) < 1e-2
+    yc = A.linear(hc, w.to(cuda), residual=rc)
+    yh = hh @ w.t() + rh
+    g = torch.randn_like(yh)
+    yc.backward(g.to(cuda)); yh.backward(g)
+    assert _rel(xc.grad, xh.grad) < 2e-2 and _rel(gc.grad, gh.grad) < 2e-2
+    # residual output unused: the fork's second gradient is None
+    xc2 = x.detach().clone().to(cuda).requires_grad_(True)
+    h2, _ = A.rmsnorm_fork(xc2, gc.detach())
+    h2.float().sum().backward()
+    xr = x.detach().clone().requires_grad_(True)
+    A.rmsnorm(xr, gam).sum().backward()
+    assert _rel(xc2.grad, xr.grad) < 2e-2
+
+
 def test_linear_rmsnorm_swiglu_embedding(cuda):
     torch.manual_seed(0)
     x = torch.randn(2, 37, 96)
