@@ -110,3 +110,18 @@ def test_mlp():
     g = convert.export_torch(net, tm, mnist_mlp_mapping(), grads=True)
     for name, p in tm.named_parameters():
         assert _cos(g[name], p.grad) > 0.99, name
+
+
+def test_rmsnorm_fork_cpu_matches_separate_paths():
+    """CPU contract of the LLaMA pre-norm fork: (rmsnorm(x), x), gradients summed over both uses."""
+    from ddl25spring_amd.models.llama import LLama  # noqa: F401  (module imports the op)
+    from ddl25spring_amd.ops import autograd_ops as A
+    torch.manual_seed(0)
+    x = torch.randn(2, 5, 16, requires_grad=True)
+    g = torch.rand(16) + 0.5
+    h, r = A.rmsnorm_fork(x, g)
+    assert r is x
+    (h * 2 + r * 3).sum().backward()
+    x2 = x.detach().clone().requires_grad_(True)
+    (A.rmsnorm(x2, g) * 2 + x2 * 3).sum().backward()
+    torch.testing.assert_close(x.grad, x2.grad)
