@@ -54,6 +54,9 @@ def plan_epoch(client_indices: list[np.ndarray], batch: int, seeds: list[int], s
         out = -np.ones((steps, G, batch), dtype=np.int32)
         for g, (ci, sd) in enumerate(zip(client_indices, seeds)):
             gen = torch.Generator().manual_seed(int(sd) & 0x7FFFFFFFFFFFFFFF)
+            # first epoch of DataLoader(shuffle=True, generator=gen): the loader's base-seed draw
+            # precedes the sampler's randperm (see fl.local.LocalTrainer._torch_plan)
+            torch.empty((), dtype=torch.int64).random_(generator=gen)
             perm = torch.randperm(count, generator=gen).numpy() if shuffle else np.arange(count)
             seq = np.asarray(ci)[perm]
             for s in range(steps):

@@ -98,6 +98,8 @@ class FederatedBase:
         for name in ("g_global",):
             if hasattr(self, name):
                 sd[name] = getattr(self, name).detach().cpu().clone()
+        if self.attack is not None:
+            sd["attack"] = self.attack.state_dict()
         return sd
 
     def load_state_dict(self, sd: dict) -> None:
@@ -112,6 +114,8 @@ class FederatedBase:
         self.rng.bit_generator.state = sd["rng"]
         self.fail_rng.bit_generator.state = sd["fail_rng"]
         self.dropped = [list(d) for d in sd["dropped"]]
+        if self.attack is not None and "attack" in sd:
+            self.attack.load_state_dict(sd["attack"])
 
     # ------------------------------------------------------------------ helpers
     def _assign(self, chosen):
@@ -183,9 +187,10 @@ class FedAvg(FederatedBase):
         if self.trainer is None:
             self.trainer = LocalTrainer(self.net, self.data, self.lr, self.B, self.momentum,
                                         self.weight_decay, self.planner, self.use_graph)
+            self._graph_default = self.trainer.use_graph
         self.trainer.label_transform = lt
-        if lt is not None:
-            self.trainer.use_graph = False
+        # a label transform is not graph-captured: eager steps only for rounds that need one
+        self.trainer.use_graph = self._graph_default and lt is None
         return self.trainer
 
     def round(self):
@@ -207,12 +212,14 @@ class FedAvg(FederatedBase):
         bsz = self.B
         samples = 0
         if G:
-            train_slots = [c for c in mine if not (self.attack and self.attack.skip_training(c))]
-            if len(train_slots) == G:
-                if bsz <= 0:  # B = infinity: full local batch
-                    trainer.B = max(self.counts[c] for c in mine)
-                with self.timer("local_train"):
-                    samples = trainer.run([self.client_indices[c] for c in mine], seeds, self.E, gens)
+            # every slot trains in the one client-batched launch; a free rider's row is then
+            # overwritten with w_global by its poison_updates (no separate code path per client)
+            if bsz <= 0:  # B = infinity: full local batch
+                trainer.B = max(self.counts[c] for c in mine)
+            with self.timer("local_train"):
+                samples = trainer.run([self.client_indices[c] for c in mine], seeds, self.E, gens)
+            if self.attack is not None:  # free riders did no useful work: do not count it
+                samples -= sum(self.E * self.counts[c] for c in mine if self.attack.skip_training(c))
         st = self.net.store
         if self.attack is not None and G:
             self.attack.poison_updates(st.data[:G], self.w_global, mine)

@@ -25,6 +25,13 @@ class Attack:
     def skip_training(self, client: int) -> bool:
         return False
 
+    # RNG state of stochastic attacks, so a resumed run poisons exactly like an uninterrupted one
+    def state_dict(self) -> dict:
+        return {}
+
+    def load_state_dict(self, sd: dict) -> None:
+        pass
+
 
 class LabelFlip(Attack):
     def label_transform_for(self, slot_clients, num_classes):
@@ -68,6 +75,17 @@ class GaussianNoise(Attack):
                     self.gen = torch.Generator(device=rows.device).manual_seed(self.seed)
                 noise = torch.randn(rows.shape[1], generator=self.gen, device=rows.device)
                 rows[i].copy_(w_global + self.sigma * noise)
+
+    def state_dict(self):
+        return {"gen": None if self.gen is None else self.gen.get_state(),
+                "device": None if self.gen is None else str(self.gen.device)}
+
+    def load_state_dict(self, sd):
+        if sd.get("gen") is None:
+            self.gen = None
+            return
+        self.gen = torch.Generator(device=sd["device"])
+        self.gen.set_state(sd["gen"])
 
 
 class FreeRider(Attack):

@@ -111,11 +111,18 @@ class LocalTrainer:
         return samples
 
     def _torch_plan(self, idxs, gens):
+        """One epoch of ``DataLoader(subset, B, shuffle=True, generator=gen)`` order. Each
+        ``iter(loader)`` consumes, in this order: one int64 ``random_`` (the loader's base seed,
+        torch/utils/data/dataloader.py ``_BaseDataLoaderIter.__init__``), the epoch's
+        ``randperm(n)``, and a trailing ``randperm(n)`` that ``RandomSampler.__iter__`` draws for
+        its ``num_samples % n`` tail (empty here, but the draw still advances the generator)."""
         count = len(idxs[0])
         steps = (count + self.B - 1) // self.B
         out = -np.ones((steps, len(idxs), self.B), dtype=np.int32)
         for g, (ci, gen) in enumerate(zip(idxs, gens)):
+            torch.empty((), dtype=torch.int64).random_(generator=gen)
             perm = torch.randperm(count, generator=gen).numpy()
+            torch.randperm(count, generator=gen)
             seq = np.asarray(ci)[perm]
             for s in range(steps):
                 chunk = seq[s * self.B:(s + 1) * self.B]

@@ -196,3 +196,74 @@ def test_client_dropout_keeps_sampling_stream(fp32):
     w0 = total.w_global.clone()
     dt, samples = total.round()
     assert samples == 0 and torch.equal(total.w_global, w0)
+
+
+def test_free_rider_does_not_stall_honest_clients(fp32):
+    """A sampled free rider must not stop the honest clients of the same GPU from training."""
+    from ddl25spring_amd.fl.attacks import FreeRider
+    arr, data = _data(600)
+    parts = split(6, True, 10, labels=arr.labels)
+    kw = dict(lr=0.1, batch_size=50, client_fraction=1.0, seed=10)
+    fa = FedAvg(mnist_mlp, data, parts, attack=FreeRider([0]), **kw)
+    w0 = fa.w_global.clone()
+    dt, samples = fa.round()
+    assert samples == 500  # 5 honest clients x 100 samples (the free rider's work is not counted)
+    assert (fa.w_global - w0).abs().max() > 1e-3
+    # the free rider's row is the server model: FedAvg == honest-only FedAvg scaled by 5/6
+    clean = FedAvg(mnist_mlp, data, parts, **kw)
+    clean.round()
+    st = clean.net.store
+    upd = (st.data[:6] - w0)
+    mine, _ = clean._assign(np.random.default_rng(10).choice(6, 6, replace=False))
+    keep = torch.tensor([c != 0 for c in mine])
+    expect = w0 + upd[keep].sum(0) / 6
+    assert torch.allclose(fa.w_global, expect, atol=1e-5)
+
+
+def test_torch_planner_matches_dataloader_shuffle():
+    """planner='torch' yields exactly DataLoader(shuffle=True, generator=g)'s batches, epoch after
+    epoch with the same generator (as WeightClient.update runs E epochs)."""
+    from torch.utils.data import DataLoader
+    from ddl25spring_amd.fl.local import LocalTrainer
+    n, B = 23, 5
+    ci = np.arange(100, 100 + n)
+    dl = DataLoader(torch.utils.data.TensorDataset(torch.as_tensor(ci)), batch_size=B,
+                    shuffle=True, generator=torch.Generator().manual_seed(5))
+    want = [[b[0].tolist() for b in dl] for _ in range(2)]
+    tr = LocalTrainer.__new__(LocalTrainer)
+    tr.B = B
+    gen = torch.Generator().manual_seed(5)
+    for ep in range(2):
+        plan = tr._torch_plan([ci], [gen])
+        got = [[int(v) for v in plan[s, 0] if v >= 0] for s in range(plan.shape[0])]
+        assert got == want[ep], ep
+    first = plan_epoch([ci], B, [5], True, "torch")
+    assert [[int(v) for v in first[s, 0] if v >= 0] for s in range(first.shape[0])] == want[0]
+
+
+def test_label_flip_round_does_not_disable_graphs_for_later_rounds(fp32):
+    arr, data = _data(400)
+    parts = split(4, True, 3, labels=arr.labels)
+    fa = FedAvg(mnist_mlp, data, parts, lr=0.05, batch_size=50, client_fraction=1.0, seed=3,
+                attack=LabelFlip([1]), use_graph=True)
+    tr = fa._trainer([0, 1])
+    assert tr.label_transform is not None and tr.use_graph is False
+    tr = fa._trainer([0, 2])
+    assert tr.label_transform is None and tr.use_graph == fa._graph_default
+
+
+def test_checkpoint_resume_under_gaussian_attack(fp32):
+    from ddl25spring_amd.fl import checkpoint as ckpt
+    from ddl25spring_amd.fl.attacks import GaussianNoise
+    arr, data = _data(400)
+    parts = split(4, True, 2, labels=arr.labels)
+    kw = dict(lr=0.05, batch_size=50, client_fraction=1.0, seed=2)
+    ref = FedAvg(mnist_mlp, data, parts, attack=GaussianNoise([1], sigma=0.1, seed=9), **kw)
+    ref.run(3)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "fl.pt")
+        a = FedAvg(mnist_mlp, data, parts, attack=GaussianNoise([1], sigma=0.1, seed=9), **kw)
+        ckpt.run_with_checkpoints(a, 2, path)
+        b = FedAvg(mnist_mlp, data, parts, attack=GaussianNoise([1], sigma=0.1, seed=9), **kw)
+        ckpt.run_with_checkpoints(b, 3, path)
+    assert torch.equal(b.w_global, ref.w_global)
