@@ -154,8 +154,22 @@ __device__ __forceinline__ void cta_barrier() {
 // the NS-deep per-step ring. Halo image: 64 B per pixel, 16-B chunk c stored at c ^ 2*((pixel>>2)&1):
 // for the ds_read_b128 lane groups ({0-3,12-15,20-27}, ...) every window of 16 consecutive
 // pixels, at any shift (every tap of a fragment on >= 16-wide rows), reads conflict-free.
-template <int MODE, int BP, int BQ, int BK, int NS, int WLP = 2, bool HALO = false>
-__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
+//
+// The kernel body is a device function over a VIRTUAL block id `lin` of a virtual (gx, gy, gz)
+// grid, so that two convolutions can share one launch (conv_pair_kernel below); the plain
+// conv_igemm_kernel passes its own linear block id and gridDim.
+template <int MODE, int BP, int BQ, int BK, int NS, int WLP, bool HALO>
+struct ConvTile {
+  static constexpr bool HALO_FD = HALO && MODE != MODE_WGRAD;
+  static constexpr bool HALO_W = HALO && MODE == MODE_WGRAD;
+  static constexpr int P_BYTES = BP * BK * 2, Q_BYTES = HALO_W ? 2 * 4 * 1024 : BQ * BK * 2;
+  static constexpr int HPW_MAX = HALO_FD ? (BQ >= 256 ? 10 - NS : (10 - NS < 4 ? 10 - NS : 4)) : 0;
+  static constexpr int SMEM = HALO_FD ? NS * P_BYTES + 2 * HPW_MAX * 4 * 1024 : NS * (P_BYTES + Q_BYTES);
+};
+
+template <int MODE, int BP, int BQ, int BK, int NS, int WLP, bool HALO>
+__device__ __forceinline__ void conv_body(const ConvArgs& a, char* smem, int lin, int gx, int gy,
+                                          int gz) {
   constexpr bool HALO_FD = HALO && MODE != MODE_WGRAD;  // halo FWD / DGRAD (channel-block-major)
   constexpr bool HALO_W = HALO && MODE == MODE_WGRAD;   // halo WGRAD (per-step row window)
   constexpr int WPW = 2;  // halo WGRAD: window pieces per wave per stage
@@ -175,21 +189,19 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   constexpr int P_PW = P_NI / 4, Q_PW = Q_NI / 4;            // per wave
   constexpr int LPS = P_PW + (HALO_W ? WPW : Q_PW);          // DMA instructions per wave per stage
   static_assert(P_PW >= 1 && Q_PW >= 1, "tile too small");
-
-  __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
+  static_assert(SMEM_BYTES == ConvTile<MODE, BP, BQ, BK, NS, WLP, HALO>::SMEM, "LDS size");
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wp = wid / (4 / WLP), wq = wid % (4 / WLP);
   // XCD-aware decode of the linear block id: the dispatcher deals workgroups round-robin over
   // the 8 XCDs; consecutive logical ids u share an XCD (and its L2).
-  const int gx = gridDim.x, gy = gridDim.y;
-  const int u = xcd_remap(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
+  const int u = xcd_remap(lin, gx * gy * gz);
   // Stride-2 DGRAD keeps the per-phase remap of the tile index only (measured: grouping the
   // phases of a tile, or the tiles of a phase, on one XCD both lose 10-20% there).
   const bool per_phase = MODE == MODE_DGRAD && a.stride == 2;
-  const int bx = per_phase ? xcd_remap(blockIdx.x, gx) : u % gx;
-  const int by = per_phase ? (int)blockIdx.y : (u / gx) % gy;
-  const int g = per_phase ? (int)blockIdx.z : u / (gx * gy);
+  const int bx = per_phase ? xcd_remap(lin % gx, gx) : u % gx;
+  const int by = per_phase ? (lin / gx) % gy : (u / gx) % gy;
+  const int g = per_phase ? lin / (gx * gy) : u / (gx * gy);
   const int H = a.H, W = a.W, C = a.C, K = a.K, R = a.R, S = a.S, P = a.P, Q = a.Q;
   const int st = a.stride, pd = a.pad;
   const int RSC = R * S * C;
@@ -883,7 +895,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     }
   } else {  // WGRAD: dW[p=k][q=rsc] fp32
     float* O = (float*)a.out + (long long)g * a.out_gs;
-    const bool atomic = a.accumulate || gridDim.y > 1;
+    const bool atomic = a.accumulate || gy > 1;
 #pragma unroll
     for (int ti = 0; ti < TP; ++ti) {
 #pragma unroll
@@ -903,6 +915,14 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       }
     }
   }
+}
+
+template <int MODE, int BP, int BQ, int BK, int NS, int WLP = 2, bool HALO = false>
+__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[ConvTile<MODE, BP, BQ, BK, NS, WLP, HALO>::SMEM];
+  conv_body<MODE, BP, BQ, BK, NS, WLP, HALO>(
+      a, smem, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), gridDim.x, gridDim.y,
+      gridDim.z);
 }
 
 // Split-K epilogue for FWD / DGRAD: out = epi(sum_s partial[s]) with the same fused terms as the
@@ -1195,8 +1215,23 @@ static int fd_splits(const ConvArgs& a, int Pd, long long tiles, long long nk, l
   return sp > 1 ? (int)sp : 1;
 }
 
-DDL_API int ddl_conv_fwd(const ConvArgs* ap, int cfg, hipStream_t stream) {
-  const ConvArgs& a = *ap;
+// A resolved launch: which instantiation (tile code bp — 48 = 64 channels with the 4 waves
+// along Q — bq, bk, ns, halo), its virtual grid (ntp * ntq, gy, G) and the FWD / DGRAD split-K
+// epilogue (sp > 1). Every entry point plans first, so a single launch and a paired launch
+// (ddl_conv_pair) of the same op run the same tile on the same grid.
+struct ConvPlan {
+  int mode, bp, bq, bk, ns, halo;
+  int Pd, Qd, gy, sp;
+  long long rows;
+};
+
+static int plan_bpe(const ConvPlan& p) { return p.bp == 48 ? 64 : p.bp; }
+static int plan_blocks(const ConvPlan& p, int G) {
+  const int bpe = plan_bpe(p);
+  return ((p.Pd + bpe - 1) / bpe) * ((p.Qd + p.bq - 1) / p.bq) * p.gy * G;
+}
+
+static int plan_fwd(const ConvArgs& a, int cfg, ConvPlan& pl) {
   if (!conv_shapes_ok(a)) return (int)hipErrorInvalidValue;
   const int Pd = a.K, Qd = a.N * a.P * a.Q;
   // sweep-tuned (profiles/conv_sweep_r1.log): 128x128x64 / 2 stages for >=128 output channels
@@ -1213,22 +1248,17 @@ DDL_API int ddl_conv_fwd(const ConvArgs* ap, int cfg, hipStream_t stream) {
     const long long ht = (long long)((Pd + 63) / 64) * (Qd / 256) * a.G;
     if (halo_ok(a, 256, 4) && ht >= num_cus()) { halo = true; bp = 48; bq = 256; bk = 32; ns = 4; }
   }
-  if (halo) {
-    if (!halo_ok(a, bq, ns) || bk != 32) return (int)hipErrorInvalidValue;
-    return (int)dispatch_halo<MODE_FWD>(a, Pd, Qd, bp, bq, ns, stream);
-  }
+  pl = ConvPlan{MODE_FWD, bp, bq, bk, ns, halo, Pd, Qd, 1, 1, Qd};
+  if (halo) return (!halo_ok(a, bq, ns) || bk != 32) ? (int)hipErrorInvalidValue : 0;
   if (a.C % bk) return (int)hipErrorInvalidValue;
   const int bpe = bp == 48 ? 64 : bp;
   const long long tiles = (long long)((Pd + bpe - 1) / bpe) * ((Qd + bq - 1) / bq) * a.G;
-  const int sp = fd_splits(a, Pd, tiles, ((long long)a.R * a.S * a.C + bk - 1) / bk, (long long)Qd * Pd,
-                           false);
-  hipError_t e = dispatch<MODE_FWD>(a, Pd, Qd, bp, bq, bk, ns, sp, stream);
-  if (e != hipSuccess || sp == 1) return (int)e;
-  return (int)splitk_epilogue(a, MODE_FWD, Pd, Qd, sp, stream);
+  pl.sp = fd_splits(a, Pd, tiles, ((long long)a.R * a.S * a.C + bk - 1) / bk, (long long)Qd * Pd, false);
+  pl.gy = pl.sp;
+  return 0;
 }
 
-DDL_API int ddl_conv_dgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
-  const ConvArgs& a = *ap;
+static int plan_dgrad(const ConvArgs& a, int cfg, ConvPlan& pl) {
   if (!conv_shapes_ok(a)) return (int)hipErrorInvalidValue;
   // stride 2 runs as 4 sub-pixel phases (blockIdx.y); grid sized for the largest (phase 0,0)
   const bool phased = a.stride == 2;
@@ -1247,21 +1277,18 @@ DDL_API int ddl_conv_dgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
     const long long ht = (long long)((Pd + 63) / 64) * (Qd / 128) * a.G;
     if (halo_ok(a, 128, 4) && ht >= num_cus()) { halo = true; bp = 48; bq = 128; bk = 32; ns = 4; }
   }
-  if (halo) {
-    if (phased || !halo_ok(a, bq, ns) || bk != 32) return (int)hipErrorInvalidValue;
-    return (int)dispatch_halo<MODE_DGRAD>(a, Pd, Qd, bp, bq, ns, stream);
-  }
+  const long long rows = (long long)a.N * a.H * a.W;
+  pl = ConvPlan{MODE_DGRAD, bp, bq, bk, ns, halo, Pd, Qd, 1, 1, rows};
+  if (halo) return (phased || !halo_ok(a, bq, ns) || bk != 32) ? (int)hipErrorInvalidValue : 0;
   if (a.K % bk) return (int)hipErrorInvalidValue;
   const int nph = phased ? 4 : 1;
-  const long long rows = (long long)a.N * a.H * a.W;
   const int bpe = bp == 48 ? 64 : bp;
   const long long tiles = (long long)((Pd + bpe - 1) / bpe) * ((Qd + bq - 1) / bq) * a.G * nph;
   // the (0, 0) phase has the most taps: ceil(R/2) x ceil(S/2) for pad-parity 0
   const int rn = phased ? (a.R - (a.pad & 1) + 1) / 2 : a.R, sn = phased ? (a.S - (a.pad & 1) + 1) / 2 : a.S;
-  const int sp = fd_splits(a, Pd, tiles, ((long long)rn * sn * a.K + bk - 1) / bk, rows * Pd, !phased);
-  hipError_t e = dispatch<MODE_DGRAD>(a, Pd, Qd, bp, bq, bk, ns, nph * sp, stream);
-  if (e != hipSuccess || sp == 1) return (int)e;
-  return (int)splitk_epilogue(a, MODE_DGRAD, Pd, rows, sp, stream);
+  pl.sp = fd_splits(a, Pd, tiles, ((long long)rn * sn * a.K + bk - 1) / bk, rows * Pd, !phased);
+  pl.gy = nph * pl.sp;
+  return 0;
 }
 
 // Halo WGRAD contract: 3x3 / stride 1 / pad 1, same-size output, 32-pixel K-steps of whole rows.
@@ -1271,8 +1298,7 @@ static bool wgrad_halo_ok(const ConvArgs& a) {
   return a.K % 64 == 0 && a.C % 32 == 0;
 }
 
-DDL_API int ddl_conv_wgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
-  const ConvArgs& a = *ap;
+static int plan_wgrad(const ConvArgs& a, int cfg, ConvPlan& pl) {
   if (!conv_shapes_ok(a)) return (int)hipErrorInvalidValue;
   const bool halo_cfg = cfg && (((cfg >> 24) & 0xff) & 0x40);
   bool halo_pick = false;
@@ -1296,12 +1322,9 @@ DDL_API int ddl_conv_wgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
     if (sp > 1024) sp = 1024;
     if (sp > 1 && !a.accumulate) return (int)hipErrorInvalidValue;
     const int hns = halo_cfg ? ((cfg >> 24) & 0x3f) : 4;  // LDS stages (12 KiB each)
-    if (hns == 6)
-      return (int)launch_cfg<MODE_WGRAD, 64, 288, 32, 6, 2, true>(a, a.K, a.R * a.S * a.C, (int)sp, stream);
-    if (hns == 5)
-      return (int)launch_cfg<MODE_WGRAD, 64, 288, 32, 5, 2, true>(a, a.K, a.R * a.S * a.C, (int)sp, stream);
-    if (hns != 4) return (int)hipErrorInvalidValue;
-    return (int)launch_cfg<MODE_WGRAD, 64, 288, 32, 4, 2, true>(a, a.K, a.R * a.S * a.C, (int)sp, stream);
+    if (hns < 4 || hns > 6) return (int)hipErrorInvalidValue;
+    pl = ConvPlan{MODE_WGRAD, 64, 288, 32, hns, 1, a.K, a.R * a.S * a.C, (int)sp, 1, 0};
+    return 0;
   }
   const int Pd = a.K, Qd = a.R * a.S * a.C;
   const long long Kr = (long long)a.N * a.P * a.Q;
@@ -1321,9 +1344,172 @@ DDL_API int ddl_conv_wgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
   // splits would be too short to fill the LDS pipeline, so trade split depth for 4x the tiles
   if (!cfg && ((Kr + bk - 1) / bk) / auto_splits(bp, bq, bk) < 32) { bp = 64; bq = 64; bk = 64; ns = 3; }
   decode_cfg(cfg, bp, bq, bk, ns);
-  int splits = a.split_k ? a.split_k : auto_splits(bp, bq, bk);
+  const int splits = a.split_k ? a.split_k : auto_splits(bp, bq, bk);
   if (splits > 1 && !a.accumulate) return (int)hipErrorInvalidValue;  // needs zeroed fp32 output
-  return (int)dispatch<MODE_WGRAD>(a, Pd, Qd, bp, bq, bk, ns, splits, stream);
+  pl = ConvPlan{MODE_WGRAD, bp, bq, bk, ns, 0, Pd, Qd, splits, 1, 0};
+  return 0;
+}
+
+static int plan_mode(int mode, const ConvArgs& a, int cfg, ConvPlan& pl) {
+  if (mode == MODE_FWD) return plan_fwd(a, cfg, pl);
+  if (mode == MODE_DGRAD) return plan_dgrad(a, cfg, pl);
+  if (mode == MODE_WGRAD) return plan_wgrad(a, cfg, pl);
+  return (int)hipErrorInvalidValue;
+}
+
+template <int MODE>
+static hipError_t launch_single(const ConvArgs& a, const ConvPlan& p, hipStream_t s) {
+  if (p.halo) {
+    if constexpr (MODE == MODE_WGRAD) {
+      if (p.ns == 4) return launch_cfg<MODE_WGRAD, 64, 288, 32, 4, 2, true>(a, p.Pd, p.Qd, p.gy, s);
+      if (p.ns == 5) return launch_cfg<MODE_WGRAD, 64, 288, 32, 5, 2, true>(a, p.Pd, p.Qd, p.gy, s);
+      if (p.ns == 6) return launch_cfg<MODE_WGRAD, 64, 288, 32, 6, 2, true>(a, p.Pd, p.Qd, p.gy, s);
+      return hipErrorInvalidValue;
+    } else {
+      return dispatch_halo<MODE>(a, p.Pd, p.Qd, p.bp, p.bq, p.ns, s);
+    }
+  }
+  return dispatch<MODE>(a, p.Pd, p.Qd, p.bp, p.bq, p.bk, p.ns, p.gy, s);
+}
+
+static int launch_plan(const ConvArgs& a, const ConvPlan& p, hipStream_t s) {
+  hipError_t e;
+  if (p.mode == MODE_FWD) e = launch_single<MODE_FWD>(a, p, s);
+  else if (p.mode == MODE_DGRAD) e = launch_single<MODE_DGRAD>(a, p, s);
+  else e = launch_single<MODE_WGRAD>(a, p, s);
+  return (int)e;
+}
+
+// FWD / DGRAD with fd split-K: the epilogue pass after the partial-sum kernel
+static int finish_plan(const ConvArgs& a, const ConvPlan& p, hipStream_t s) {
+  if (p.mode == MODE_WGRAD || p.sp <= 1) return 0;
+  return (int)splitk_epilogue(a, p.mode, p.Pd, p.rows, p.sp, s);
+}
+
+static int run_mode(int mode, const ConvArgs* ap, int cfg, hipStream_t stream) {
+  ConvPlan pl;
+  int e = plan_mode(mode, *ap, cfg, pl);
+  if (e) return e;
+  e = launch_plan(*ap, pl, stream);
+  if (e) return e;
+  return finish_plan(*ap, pl, stream);
+}
+
+DDL_API int ddl_conv_fwd(const ConvArgs* ap, int cfg, hipStream_t stream) {
+  return run_mode(MODE_FWD, ap, cfg, stream);
+}
+DDL_API int ddl_conv_dgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
+  return run_mode(MODE_DGRAD, ap, cfg, stream);
+}
+DDL_API int ddl_conv_wgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
+  return run_mode(MODE_WGRAD, ap, cfg, stream);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Paired launch: two independent convolutions of one layer in ONE grid — the DGRAD and WGRAD of
+// a backward conv (both read dY), or the two FWD convs that read a block's input (conv1 and the
+// projection shortcut). Few-client grids fill a fraction of the 256 CUs per op (1 client, 8x8
+// layer: 200 DGRAD workgroups); pairing lets the second op's workgroups run in the first op's
+// tail and idle CU slots instead of after it, without the cross-queue synchronisation a second
+// stream costs inside a HIP graph (docs/KERNELS.md, dead ends). Blocks [0, nA8) run op A (nA
+// rounded up to 8 so op B's virtual block ids keep their XCD residue), the rest op B; the LDS
+// image is the larger of the two.
+template <class TA, class TB>
+__global__ __launch_bounds__(256) void conv_pair_kernel(ConvArgs a, ConvArgs b, int4 ga, int3 gb) {
+  __shared__ __attribute__((aligned(16))) char smem[TA::SMEM > TB::SMEM ? TA::SMEM : TB::SMEM];
+  const int bid = blockIdx.x;
+  if (bid < ga.w) {
+    if (bid < ga.x * ga.y * ga.z) TA::run(a, smem, bid, ga.x, ga.y, ga.z);
+  } else {
+    TB::run(b, smem, bid - ga.w, gb.x, gb.y, gb.z);
+  }
+}
+
+template <int MODE, int BP, int BQ, int BK, int NS, int WLP, bool HALO>
+struct TileOp : ConvTile<MODE, BP, BQ, BK, NS, WLP, HALO> {
+  static constexpr int M = MODE, BPC = (WLP == 1 && BP == 64) ? 48 : BP, BQC = BQ, BKC = BK, NSC = NS;
+  static constexpr bool H = HALO;
+  __device__ __forceinline__ static void run(const ConvArgs& a, char* smem, int lin, int gx, int gy,
+                                             int gz) {
+    conv_body<MODE, BP, BQ, BK, NS, WLP, HALO>(a, smem, lin, gx, gy, gz);
+  }
+  static bool match(const ConvPlan& p) {
+    return p.mode == MODE && p.bp == BPC && p.bq == BQ && p.bk == BK && p.ns == NS && (bool)p.halo == HALO;
+  }
+};
+
+template <class TA, class TB>
+static bool try_pair(const ConvArgs& a, const ConvPlan& pa, const ConvArgs& b, const ConvPlan& pb,
+                     hipStream_t s, int& err) {
+  if (!TA::match(pa) || !TB::match(pb)) return false;
+  const int bpa = plan_bpe(pa), bpb = plan_bpe(pb);
+  const int gxa = ((pa.Pd + bpa - 1) / bpa) * ((pa.Qd + pa.bq - 1) / pa.bq);
+  const int gxb = ((pb.Pd + bpb - 1) / bpb) * ((pb.Qd + pb.bq - 1) / pb.bq);
+  const int na = gxa * pa.gy * a.G, na8 = (na + 7) & ~7, nb = gxb * pb.gy * b.G;
+  hipLaunchKernelGGL((conv_pair_kernel<TA, TB>), dim3(na8 + nb), dim3(256), 0, s, a, b,
+                     make_int4(gxa, pa.gy, a.G, na8), make_int3(gxb, pb.gy, b.G));
+  err = (int)hipGetLastError();
+  return true;
+}
+
+// Tile menu of the paired kernels (instantiated combinations; ops/autotune.py mirrors it in
+// PAIR_DGRAD / PAIR_WGRAD / PAIR_FWD). bp 48 = 64 channels, 4 waves along Q.
+using DgH256 = TileOp<MODE_DGRAD, 64, 256, 32, 4, 1, true>;
+using DgH128 = TileOp<MODE_DGRAD, 64, 128, 32, 4, 1, true>;
+using Dg128x128k64 = TileOp<MODE_DGRAD, 128, 128, 64, 2, 2, false>;
+using Dg64x128k64 = TileOp<MODE_DGRAD, 64, 128, 64, 3, 2, false>;
+using Dg128x64k64 = TileOp<MODE_DGRAD, 128, 64, 64, 3, 2, false>;
+using Dg48x256k64 = TileOp<MODE_DGRAD, 64, 256, 64, 2, 1, false>;
+using Wg64x64k64 = TileOp<MODE_WGRAD, 64, 64, 64, 3, 2, false>;
+using Wg128x64k64 = TileOp<MODE_WGRAD, 128, 64, 64, 3, 2, false>;
+using Wg128x128k32 = TileOp<MODE_WGRAD, 128, 128, 32, 3, 2, false>;
+using Wg128x128k64 = TileOp<MODE_WGRAD, 128, 128, 64, 2, 2, false>;
+using Wg64x128k32 = TileOp<MODE_WGRAD, 64, 128, 32, 4, 2, false>;
+
+static int pair_dispatch(const ConvArgs& a, const ConvPlan& pa, const ConvArgs& b, const ConvPlan& pb,
+                         hipStream_t s) {
+  int err = 0;
+#define DDL_PAIR_W(TA)                                                                         \
+  if (try_pair<TA, Wg64x64k64>(a, pa, b, pb, s, err) || try_pair<TA, Wg128x64k64>(a, pa, b, pb, s, err) || \
+      try_pair<TA, Wg128x128k32>(a, pa, b, pb, s, err) ||                                      \
+      try_pair<TA, Wg128x128k64>(a, pa, b, pb, s, err) || try_pair<TA, Wg64x128k32>(a, pa, b, pb, s, err)) \
+    return err;
+  DDL_PAIR_W(DgH256) DDL_PAIR_W(DgH128) DDL_PAIR_W(Dg128x128k64) DDL_PAIR_W(Dg64x128k64)
+  DDL_PAIR_W(Dg128x64k64) DDL_PAIR_W(Dg48x256k64)
+#undef DDL_PAIR_W
+  return -1;  // no paired instantiation for these tiles
+}
+
+// mode_a / mode_b: 0 FWD, 1 DGRAD, 2 WGRAD; cfg_* as the single-op entry points (0 = heuristic).
+// Returns -1 (nothing launched) when the two plans have no paired kernel: the caller launches
+// them one after the other instead.
+DDL_API int ddl_conv_pair(const ConvArgs* ap, int mode_a, int cfg_a, const ConvArgs* bp, int mode_b,
+                          int cfg_b, hipStream_t stream) {
+  ConvPlan pa, pb;
+  int e = plan_mode(mode_a, *ap, cfg_a, pa);
+  if (e) return e;
+  e = plan_mode(mode_b, *bp, cfg_b, pb);
+  if (e) return e;
+  e = pair_dispatch(*ap, pa, *bp, pb, stream);
+  if (e) return e;
+  e = finish_plan(*ap, pa, stream);
+  if (e) return e;
+  return finish_plan(*bp, pb, stream);
+}
+
+// Whether (mode_a, cfg_a) + (mode_b, cfg_b) on these shapes has a paired kernel (no launch).
+DDL_API int ddl_conv_pair_supported(const ConvArgs* ap, int mode_a, int cfg_a, const ConvArgs* bp,
+                                    int mode_b, int cfg_b) {
+  ConvPlan pa, pb;
+  if (plan_mode(mode_a, *ap, cfg_a, pa) || plan_mode(mode_b, *bp, cfg_b, pb)) return 0;
+  bool ok = false;
+#define DDL_PAIR_W(TA) \
+  ok = ok || (TA::match(pa) && (Wg64x64k64::match(pb) || Wg128x64k64::match(pb) || Wg128x128k32::match(pb) || \
+                                Wg128x128k64::match(pb) || Wg64x128k32::match(pb)));
+  DDL_PAIR_W(DgH256) DDL_PAIR_W(DgH128) DDL_PAIR_W(Dg128x128k64) DDL_PAIR_W(Dg64x128k64)
+  DDL_PAIR_W(Dg128x64k64) DDL_PAIR_W(Dg48x256k64)
+#undef DDL_PAIR_W
+  return ok ? 1 : 0;
 }
 
 DDL_API int ddl_conv_args_size() { return (int)sizeof(ConvArgs); }

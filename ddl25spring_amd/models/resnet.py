@@ -97,25 +97,23 @@ class BasicBlock(Layer):
             dc2, dym = self.conv2.bn_backward(dout, None, c2, mu2, rs2, part=part), dout
         else:
             dc2, dym = self.conv2.bn_backward(dout, out, c2, mu2, rs2, emit_dym=True)
+        # every conv's DGRAD and WGRAD read the same dY: one (possibly paired) launch each
         if dctx is not None:
             cs, mus, rss, gs = dctx
             dcs = self.down.bn_backward(dym, None, cs, mus, rss)
-            Fn.conv_wgrad(dcs, x, gs, st.grad_of(self.down.w))
-            dres = Fn.conv_dgrad(dcs, st.shadow_of(self.down.w), gs) if self.needs_input_grad else None
+            dres = Fn.conv_dgrad_wgrad(dcs, st.shadow_of(self.down.w), x, gs, st.grad_of(self.down.w),
+                                       want_dx=self.needs_input_grad)
         else:
             dres = dym
-        Fn.conv_wgrad(dc2, a1, g2, st.grad_of(self.conv2.w))
         # dgrad epilogue applies bn1's ReLU mask (recomputed from c1: no read of a1) and reduces
         # bn1's backward sums (no reduce pass)
-        da1, part1 = Fn.conv_dgrad(dc2, st.shadow_of(self.conv2.w), g2, bn=(c1, mu1, rs1),
-                                   mask_bn=(sc1, sh1))
+        da1, part1 = Fn.conv_dgrad_wgrad(dc2, st.shadow_of(self.conv2.w), a1, g2, st.grad_of(self.conv2.w),
+                                         bn=(c1, mu1, rs1), mask_bn=(sc1, sh1))
         dc1 = self.conv1.bn_backward(da1, None, c1, mu1, rs1, part=part1)
-        Fn.conv_wgrad(dc1, x, g1, st.grad_of(self.conv1.w))
-        if not self.needs_input_grad:
-            return None
-        if fuse is not None:  # the producer's ReLU mask (x > 0) and BN reduce in this epilogue
-            return Fn.conv_dgrad(dc1, st.shadow_of(self.conv1.w), g1, residual=dres, mask=x, bn=fuse)
-        return Fn.conv_dgrad(dc1, st.shadow_of(self.conv1.w), g1, residual=dres)
+        # with fuse: the producer's ReLU mask (x > 0) and BN reduce in this dgrad's epilogue
+        return Fn.conv_dgrad_wgrad(dc1, st.shadow_of(self.conv1.w), x, g1, st.grad_of(self.conv1.w),
+                                   residual=dres, mask=x if fuse is not None else None, bn=fuse,
+                                   want_dx=self.needs_input_grad)
 
     def flops(self, s):
         G, N, H, W, _ = s
@@ -189,22 +187,19 @@ class Bottleneck(Layer):
         if dctx is not None:
             cs, mus, rss, gs = dctx
             dcs = self.down.bn_backward(dym, None, cs, mus, rss)
-            Fn.conv_wgrad(dcs, x, gs, st.grad_of(self.down.w))
-            dres = Fn.conv_dgrad(dcs, st.shadow_of(self.down.w), gs) if self.needs_input_grad else None
+            dres = Fn.conv_dgrad_wgrad(dcs, st.shadow_of(self.down.w), x, gs, st.grad_of(self.down.w),
+                                       want_dx=self.needs_input_grad)
         else:
             dres = dym
-        Fn.conv_wgrad(dc3, a2, g3, st.grad_of(self.conv3.w))
-        da2, part2 = Fn.conv_dgrad(dc3, st.shadow_of(self.conv3.w), g3, bn=(c2, mu2, rs2), mask_bn=(sc2, sh2))
+        da2, part2 = Fn.conv_dgrad_wgrad(dc3, st.shadow_of(self.conv3.w), a2, g3, st.grad_of(self.conv3.w),
+                                         bn=(c2, mu2, rs2), mask_bn=(sc2, sh2))
         dc2 = self.conv2.bn_backward(da2, None, c2, mu2, rs2, part=part2)
-        Fn.conv_wgrad(dc2, a1, g2, st.grad_of(self.conv2.w))
-        da1, part1 = Fn.conv_dgrad(dc2, st.shadow_of(self.conv2.w), g2, bn=(c1, mu1, rs1), mask_bn=(sc1, sh1))
+        da1, part1 = Fn.conv_dgrad_wgrad(dc2, st.shadow_of(self.conv2.w), a1, g2, st.grad_of(self.conv2.w),
+                                         bn=(c1, mu1, rs1), mask_bn=(sc1, sh1))
         dc1 = self.conv1.bn_backward(da1, None, c1, mu1, rs1, part=part1)
-        Fn.conv_wgrad(dc1, x, g1, st.grad_of(self.conv1.w))
-        if not self.needs_input_grad:
-            return None
-        if fuse is not None:
-            return Fn.conv_dgrad(dc1, st.shadow_of(self.conv1.w), g1, residual=dres, mask=x, bn=fuse)
-        return Fn.conv_dgrad(dc1, st.shadow_of(self.conv1.w), g1, residual=dres)
+        return Fn.conv_dgrad_wgrad(dc1, st.shadow_of(self.conv1.w), x, g1, st.grad_of(self.conv1.w),
+                                   residual=dres, mask=x if fuse is not None else None, bn=fuse,
+                                   want_dx=self.needs_input_grad)
 
     def flops(self, s):
         G, N, H, W, _ = s

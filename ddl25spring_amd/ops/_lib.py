@@ -71,6 +71,8 @@ _SIGS = {
     "ddl_conv_fwd": [ctypes.POINTER(ConvArgs), i32, vp],
     "ddl_conv_dgrad": [ctypes.POINTER(ConvArgs), i32, vp],
     "ddl_conv_wgrad": [ctypes.POINTER(ConvArgs), i32, vp],
+    "ddl_conv_pair": [ctypes.POINTER(ConvArgs), i32, i32, ctypes.POINTER(ConvArgs), i32, i32, vp],
+    "ddl_conv_pair_supported": [ctypes.POINTER(ConvArgs), i32, i32, ctypes.POINTER(ConvArgs), i32, i32],
     # batchnorm.hip
     "ddl_bn_finalize": [ctypes.POINTER(BNArgs), vp],
     "ddl_bn_apply": [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, vp],

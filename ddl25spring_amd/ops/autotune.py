@@ -111,5 +111,38 @@ def pick(mode: str, geom, flags: tuple, run, accumulate: bool = True):
     return best
 
 
+def pick_pair(tag, geom, dpick, wpick, supported, run_pair, run_seq, dmenu, wmenu):
+    """Paired DGRAD + WGRAD launch (functional.conv_dgrad_wgrad): the fastest of the two tuned
+    single launches back to back (-> None) and the paired kernels over (the tuned pick or a menu
+    tile) x (the tuned pick or a menu tile) -> (dcfg, dsplit, wcfg, wsplit)."""
+    key = _key("pair", geom, tag)
+    if key in _CACHE:
+        return _CACHE[key]
+    if not ENABLED or torch.cuda.is_current_stream_capturing():
+        return None
+    from ._lib import KernelError
+    saved = ws._CURRENT
+    ws._CURRENT = None
+    try:
+        best, best_t = None, _time(lambda c, s: run_seq(), None, 0)
+        seen = set()
+        for dc, dsp in [dpick] + list(dmenu):
+            for wc, wsp in [wpick] + list(wmenu):
+                cand = (dc, dsp, wc, wsp)
+                if cand in seen or not supported(*cand):
+                    continue
+                seen.add(cand)
+                try:
+                    t = _time(lambda c, s: run_pair(cand), None, 0)
+                except KernelError:
+                    continue
+                if t < best_t * 0.97:
+                    best, best_t = cand, t
+    finally:
+        ws._CURRENT = saved
+    _CACHE[key] = best
+    return best
+
+
 def cache() -> dict:
     return dict(_CACHE)

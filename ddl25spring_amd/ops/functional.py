@@ -224,6 +224,13 @@ def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0,
         c, split_k = autotune.pick("dgrad", geom, (residual is not None, mask is not None, bn is not None,
                                                    mask_bn is not None), run)
         cfg = c or 0
+    a, part = _dgrad_args(dy, w, geom, dx, residual, mask, bn, mask_bn, split_k)
+    check(_lib.kernels().ddl_conv_dgrad(ctypes.byref(a), cfg, stream()), "conv_dgrad")
+    return dx if bn is None else (dx, part)
+
+
+def _dgrad_args(dy, w, geom, dx, residual, mask, bn, mask_bn, split_k):
+    """ConvArgs of a DGRAD launch (+ the zeroed BN-backward partial sums when bn is fused)."""
     part = None
     kw = {}
     if bn is not None:
@@ -238,8 +245,12 @@ def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0,
             kw.update(mask_scale=ptr(sc), mask_shift=ptr(sh))
     a = _conv_args(geom, dy.device, split_k, True, w=ptr(w), dy=ptr(dy), out=ptr(dx), residual=ptr(residual),
                    mask=ptr(mask), w_gs=_gs(w), dy_gs=_gs(dy), out_gs=_gs(dx), **kw)
-    check(_lib.kernels().ddl_conv_dgrad(ctypes.byref(a), cfg, stream()), "conv_dgrad")
-    return dx if bn is None else (dx, part)
+    return a, part
+
+
+def _wgrad_args(dy, x, geom, dw, accumulate, splits):
+    return _conv_args(geom, dy.device, 1 if not accumulate else int(splits), x=ptr(x), dy=ptr(dy),
+                      out=ptr(dw), x_gs=_gs(x), dy_gs=_gs(dy), out_gs=_gs(dw), accumulate=int(accumulate))
 
 
 def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0, _tune=True):
@@ -260,8 +271,7 @@ def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0, _tun
                 _WGRAD_SIDE = side
         c, splits = autotune.pick("wgrad", geom, (bool(accumulate),), run, accumulate=bool(accumulate))
         cfg = c or 0
-    a = _conv_args(geom, dy.device, 1 if not accumulate else int(splits), x=ptr(x), dy=ptr(dy),
-                   out=ptr(dw), x_gs=_gs(x), dy_gs=_gs(dy), out_gs=_gs(dw), accumulate=int(accumulate))
+    a = _wgrad_args(dy, x, geom, dw, accumulate, splits)
     side = _WGRAD_SIDE
     if side is None:
         check(_lib.kernels().ddl_conv_wgrad(ctypes.byref(a), cfg, stream()), "conv_wgrad")
@@ -277,6 +287,96 @@ def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0, _tun
 # ------------------------------------------------------------------- wgrad / dgrad overlap
 _WGRAD_SIDE: "torch.cuda.Stream | None" = None
 _SIDE_STREAMS: dict = {}
+
+
+# Paired DGRAD + WGRAD of one conv in one launch (conv_igemm.hip ``ddl_conv_pair``). The pair
+# tuner (autotune.pick_pair) times it against the two tuned single launches per shape; DDL_CONV_PAIR=0
+# keeps the single launches everywhere.
+PAIR_ENABLED = __import__("os").environ.get("DDL_CONV_PAIR", "1") != "0"
+# the paired kernels' tile menu (mirrors the TileOp list of conv_igemm.hip)
+PAIR_DGRAD = [(48, 256, 32, 4, True), (48, 128, 32, 4, True), (128, 128, 64, 2, False),
+              (64, 128, 64, 3, False), (128, 64, 64, 3, False), (48, 256, 64, 2, False)]
+PAIR_WGRAD = [(64, 64, 64, 3), (128, 64, 64, 3), (128, 128, 32, 3), (128, 128, 64, 2), (64, 128, 32, 4)]
+MODE_FWD, MODE_DGRAD, MODE_WGRAD = 0, 1, 2
+
+
+def conv_pair(dy, w, x, geom: ConvGeom, dw, dcfg: int, dsplit: int, wcfg: int, wsplit: int,
+              residual=None, mask=None, bn=None, mask_bn=None, out=None):
+    """Explicit paired launch: DGRAD (tile ``dcfg``, split ``dsplit``, fused epilogue as conv_dgrad)
+    and WGRAD (``wcfg``, ``wsplit``, accumulating into dw) in one grid. -> (dx, part | None).
+    Raises KernelError when the two tiles have no paired instantiation."""
+    dx = out if out is not None else torch.empty(geom.G, geom.N, geom.H, geom.W, geom.C,
+                                                 dtype=torch.bfloat16, device=dy.device)
+    ad, part = _dgrad_args(dy, w, geom, dx, residual, mask, bn, mask_bn, dsplit)
+    aw = _wgrad_args(dy, x, geom, dw, True, wsplit)
+    rc = _lib.kernels().ddl_conv_pair(ctypes.byref(ad), MODE_DGRAD, dcfg, ctypes.byref(aw), MODE_WGRAD,
+                                      wcfg, stream())
+    if rc == -1:
+        raise _lib.KernelError("no paired kernel for these tiles")
+    check(rc, "conv_pair")
+    return dx, part
+
+
+def conv_dgrad_wgrad(dy, w, x, geom: ConvGeom, dw, residual=None, mask=None, bn=None, mask_bn=None,
+                     want_dx: bool = True):
+    """``conv_wgrad(dy, x, geom, dw)`` and (if want_dx) ``conv_dgrad(dy, w, geom, residual, mask,
+    bn=bn, mask_bn=mask_bn)`` — both read dy and are independent, so on the GPU they may run as
+    ONE paired launch (whichever of paired / back-to-back the tuner measured faster for this
+    shape). Returns what conv_dgrad returns (None without want_dx)."""
+    if not want_dx or not dy.is_cuda or not PAIR_ENABLED or _WGRAD_SIDE is not None \
+            or not autotune.ENABLED:
+        conv_wgrad(dy, x, geom, dw)
+        if not want_dx:
+            return None
+        return conv_dgrad(dy, w, geom, residual=residual, mask=mask, bn=bn, mask_bn=mask_bn)
+    _check_inner(dy, "dy"); _check_inner(w, "w"); _check_inner(x, "x"); _check_inner(dw, "dw")
+    dx = torch.empty(geom.G, geom.N, geom.H, geom.W, geom.C, dtype=torch.bfloat16, device=dy.device)
+    if residual is not None and residual.stride(0) != dx.stride(0):
+        residual = residual.contiguous()
+    if mask is not None and mask.stride(0) != dx.stride(0):
+        mask = mask.contiguous()
+    dflags = (residual is not None, mask is not None, bn is not None, mask_bn is not None)
+    lib = _lib.kernels()
+
+    def run_d(c, sp, out=None):
+        return conv_dgrad(dy, w, geom, residual=residual, mask=mask, out=out if out is not None else torch.empty_like(dx),
+                          cfg=c or 0, bn=bn, split_k=sp, mask_bn=mask_bn, _tune=False)
+
+    def run_w(c, sp, out=None):
+        conv_wgrad(dy, x, geom, out if out is not None else torch.zeros_like(dw), True, cfg=c or 0,
+                   splits=sp, _tune=False)
+
+    def launch_pair(dcfg, dsp, wcfg, wsp, dx_out, dw_out):
+        return conv_pair(dy, w, x, geom, dw_out, dcfg or 0, dsp, wcfg or 0, wsp, residual=residual,
+                         mask=mask, bn=bn, mask_bn=mask_bn, out=dx_out)[1]
+
+    dpick = autotune.pick("dgrad", geom, dflags, run_d)
+    wpick = autotune.pick("wgrad", geom, (True,), run_w)
+
+    def supported(dc, dsp, wc, wsp):
+        ad, _ = _dgrad_args(dy, w, geom, dx, residual, mask, bn, mask_bn, dsp)
+        aw = _wgrad_args(dy, x, geom, dw, True, wsp)
+        return bool(lib.ddl_conv_pair_supported(ctypes.byref(ad), MODE_DGRAD, dc or 0,
+                                                ctypes.byref(aw), MODE_WGRAD, wc or 0))
+
+    def run_pair(cand):
+        dc, dsp, wc, wsp = cand
+        launch_pair(dc, dsp, wc, wsp, torch.empty_like(dx), torch.zeros_like(dw))
+
+    def run_seq():
+        run_w(*wpick)
+        run_d(*dpick)
+
+    choice = autotune.pick_pair(("pair", dflags), geom, dpick, wpick, supported, run_pair, run_seq,
+                                [(conv_cfg(bp, bq, bk, ns, h), 0) for bp, bq, bk, ns, h in PAIR_DGRAD],
+                                [(conv_cfg(*t), 0) for t in PAIR_WGRAD])
+    if choice is None:  # back-to-back single launches
+        conv_wgrad(dy, x, geom, dw, cfg=wpick[0] or 0, splits=wpick[1], _tune=False)
+        return conv_dgrad(dy, w, geom, residual=residual, mask=mask, out=dx, cfg=dpick[0] or 0, bn=bn,
+                          split_k=dpick[1], mask_bn=mask_bn, _tune=False)
+    dc, dsp, wc, wsp = choice
+    part = launch_pair(dc, dsp, wc, wsp, dx, dw)
+    return dx if bn is None else (dx, part)
 
 
 class wgrad_overlap:

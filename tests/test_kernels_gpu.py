@@ -398,3 +398,57 @@ def test_conv_split_k(cuda, geom, split):
     dxd, pd_ = Fn.conv_dgrad(dy, w, g, bn=(xbn, mean, rstd), mask_bn=(sc, sh), split_k=split)
     _close(dxd, dxc, rel=1e-2)
     _close(pd_.sum(1), pc.sum(1), rel=2e-2)
+
+
+PAIR_GEOMS = [
+    ConvGeom(G=1, N=4, H=32, W=32, C=64, K=64, R=3, S=3, stride=1, pad=1),    # layer 1
+    ConvGeom(G=2, N=3, H=16, W=16, C=64, K=128, R=3, S=3, stride=2, pad=1),   # stride-2 (phased)
+    ConvGeom(G=1, N=5, H=8, W=8, C=256, K=256, R=3, S=3, stride=1, pad=1),    # layer 3, ragged tiles
+    ConvGeom(G=2, N=3, H=8, W=8, C=128, K=256, R=1, S=1, stride=2, pad=0),    # projection shortcut
+]
+
+
+@pytest.mark.parametrize("geom", PAIR_GEOMS, ids=lambda g: f"{g.C}x{g.K}_{g.H}_{g.R}s{g.stride}")
+def test_conv_pair(cuda, geom):
+    """DGRAD + WGRAD in one paired grid == the fp32 references, for every (DGRAD, WGRAD) tile of
+    the paired menu the shape admits, with the training epilogue (residual, mask, BN-backward
+    reduce) and split-K WGRAD accumulating into a strided view; the tuned entry point agrees."""
+    g = geom
+    x = _rand(g.G, g.N, g.H, g.W, g.C, dev=cuda)
+    w = _weights(g, cuda)
+    dy = _rand(g.G, g.N, g.P, g.Q, g.K, dev=cuda)
+    res = _rand(g.G, g.N, g.H, g.W, g.C, dev=cuda)
+    mask = _rand(g.G, g.N, g.H, g.W, g.C, dev=cuda)
+    mean = torch.randn(g.G, g.C, device=cuda) * 0.1
+    rstd = torch.rand(g.G, g.C, device=cuda) + 0.5
+    dx_ref = ref.conv_dgrad(dy.cpu(), w.cpu(), g, residual=res.cpu(), mask=mask.cpu())
+    xh = (x.float() - mean[:, None, None, None]) * rstd[:, None, None, None]
+    s0_ref = dx_ref.float().sum((1, 2, 3))
+    s1_ref = (dx_ref.float() * xh.cpu()).sum((1, 2, 3))
+    dw_ref = torch.zeros(g.G, g.K, g.R, g.S, g.C)
+    ref.conv_wgrad(dy.cpu(), x.cpu(), g, dw_ref)
+    inner = g.K * g.R * g.S * g.C
+    ran = 0
+    for bp, bq, bk, ns, halo in Fn.PAIR_DGRAD:
+        dcfg = Fn.conv_cfg(bp, bq, bk, ns, halo)
+        for wt in Fn.PAIR_WGRAD:
+            wcfg = Fn.conv_cfg(*wt)
+            for wsp in (1, 3):
+                flat = torch.zeros(g.G, inner + 64, device=cuda)
+                dw = flat[:, 32:32 + inner].unflatten(1, (g.K, g.R, g.S, g.C))
+                try:
+                    dx, part = Fn.conv_pair(dy, w, x, g, dw, dcfg, 1, wcfg, wsp, residual=res, mask=mask,
+                                            bn=(x, mean, rstd))
+                except RuntimeError:
+                    continue  # tile not eligible for this shape (or reduction step)
+                ran += 1
+                _close(dx, dx_ref)
+                _close(part[:, :, 0].sum(1), s0_ref, rel=5e-3)
+                _close(part[:, :, 1].sum(1), s1_ref, rel=5e-3)
+                _close(dw, dw_ref, rel=2e-3)
+                assert flat[:, :32].abs().max().item() == 0 and flat[:, 32 + inner:].abs().max().item() == 0
+    assert ran > 0
+    dw = torch.zeros(g.G, g.K, g.R, g.S, g.C, device=cuda)
+    dx, part = Fn.conv_dgrad_wgrad(dy, w, x, g, dw, residual=res, mask=mask, bn=(x, mean, rstd))
+    _close(dx, dx_ref)
+    _close(dw, dw_ref, rel=2e-3)
