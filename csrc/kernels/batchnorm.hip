@@ -20,6 +20,8 @@
 // lab/tutorial_2b/exercise_3.py:17-81) and the north-star ResNets.
 #include "ddl_common.h"
 
+#define BN_NSTRIPE 32  // stats / backward-partial stripes (== ops.functional.BN_STRIPES)
+
 struct BNArgs {
   const float* stats;    // [G][stripes][2C]: sum | sumsq per stripe   (finalize input)
   const float* gamma;    // [G][C] (group stride gs_param)
@@ -38,17 +40,26 @@ struct BNArgs {
 };
 
 // Stripe fold shared by finalize / fold_coef: a 256-thread block owns 32 channels of one group;
-// thread (sg, cl) sums stripes sg, sg+8, ... (independent loads, one memory round trip), then
-// the 8 partial sums of each channel meet in LDS. Returns the totals on threads with sg == 0.
+// thread (sg, cl) sums stripes sg, sg+8, ... then the 8 partial sums of each channel meet in LDS.
+// Returns the totals on threads with sg == 0. The stripe count is a template constant so every
+// load is issued before the first add: one memory round trip (the atomics that filled the stripes
+// ran at the memory side, so these reads miss in L2), not one per stripe pair.
+template <int NSTR>
 __device__ __forceinline__ void stripe_fold(const float* __restrict__ base, int ns, int C, int c,
                                             bool valid, float* red, float& t0, float& t1) {
+  constexpr int PER = (NSTR + 7) / 8;
   const int sg = threadIdx.x >> 5, cl = threadIdx.x & 31;
+  float v0[PER], v1[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int k = sg + 8 * j;
+    const bool ok = valid && k < NSTR && k < ns;
+    v0[j] = ok ? base[(long long)k * 2 * C + c] : 0.f;
+    v1[j] = ok ? base[(long long)k * 2 * C + C + c] : 0.f;
+  }
   float a0 = 0.f, a1 = 0.f;
-  if (valid)
-    for (int k = sg; k < ns; k += 8) {
-      a0 += base[(long long)k * 2 * C + c];
-      a1 += base[(long long)k * 2 * C + C + c];
-    }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) { a0 += v0[j]; a1 += v1[j]; }
   red[sg * 64 + cl] = a0;
   red[sg * 64 + 32 + cl] = a1;
   __syncthreads();
@@ -66,12 +77,18 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(BNArgs a) {
   __shared__ float red[8 * 64];
   const int g = blockIdx.y, c = blockIdx.x * 32 + (threadIdx.x & 31);
   const bool valid = c < a.C;
+  const bool lead = (threadIdx.x >> 5) == 0 && valid;
+  // everything the tail reads is loaded up front, alongside the stripe fold's loads
+  const long long po = (long long)g * a.gs_param + c, o = (long long)g * a.gs_buf + c;
+  const float ga = (lead && a.gamma) ? a.gamma[po] : 1.f, be = (lead && a.beta) ? a.beta[po] : 0.f;
+  const bool rs_io = lead && a.running_mean;
+  const float rm0 = rs_io ? a.running_mean[o] : 0.f, rv0 = rs_io ? a.running_var[o] : 0.f;
   float mean, var;
   if (a.training) {
-    const int ns = a.stripes > 1 ? a.stripes : 1;
     float s1f, s2f;
-    stripe_fold(a.stats + (long long)g * ns * 2 * a.C, ns, a.C, c, valid, red, s1f, s2f);
-    if ((threadIdx.x >> 5) != 0 || !valid) return;
+    const float* base = a.stats + (long long)g * (a.stripes > 1 ? a.stripes : 1) * 2 * a.C;
+    stripe_fold<BN_NSTRIPE>(base, a.stripes > 1 ? a.stripes : 1, a.C, c, valid, red, s1f, s2f);
+    if (!lead) return;
     const double M = (double)a.count;
     const double m = (double)s1f / M;
     double v = (double)s2f / M - m * m;
@@ -79,21 +96,17 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(BNArgs a) {
     mean = (float)m;
     var = (float)v;
     if (a.running_mean) {
-      const long long o = (long long)g * a.gs_buf + c;
       const float unb = a.count > 1 ? (float)(v * M / (M - 1.0)) : (float)v;
-      a.running_mean[o] = (1.f - a.momentum) * a.running_mean[o] + a.momentum * mean;
-      a.running_var[o] = (1.f - a.momentum) * a.running_var[o] + a.momentum * unb;
+      a.running_mean[o] = (1.f - a.momentum) * rm0 + a.momentum * mean;
+      a.running_var[o] = (1.f - a.momentum) * rv0 + a.momentum * unb;
     }
   } else {
-    if ((threadIdx.x >> 5) != 0 || !valid) return;
-    const long long o = (long long)g * a.gs_buf + c;
-    mean = a.running_mean[o];
-    var = a.running_var[o];
+    if (!lead) return;
+    mean = rm0;
+    var = rv0;
   }
   const int i = g * a.C + c;
   const float rs = rsqrtf(var + a.eps);
-  const long long po = (long long)g * a.gs_param + c;
-  const float ga = a.gamma ? a.gamma[po] : 1.f, be = a.beta ? a.beta[po] : 0.f;
   a.scale[i] = ga * rs;
   a.shift[i] = be - mean * ga * rs;
   a.mean[i] = mean;
@@ -101,6 +114,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(BNArgs a) {
 }
 
 DDL_API int ddl_bn_finalize(const BNArgs* a, hipStream_t s) {
+  if (a->stripes > BN_NSTRIPE) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((a->C + 31) / 32, a->G), dim3(256), 0, s, *a);
   return (int)hipGetLastError();
 }
@@ -139,34 +153,51 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(
     load8f(rshift + (long long)g * C + cc * 8, rsh);
   }
   const long long base = (long long)g * M * C + cc * 8;
-  for (long long p = (long long)blockIdx.x * RPI + row; p < M; p += (long long)gridDim.x * RPI) {
-    const long long e = base + p * C;
-    float v[8];
-    unpack8(*(const i4v*)(x + e), v);
+  // RB rows per thread per pass, all loads issued before any use: a few-client grid gives each
+  // thread ~4 rows, which a one-row loop paid as 4 dependent memory round trips
+  constexpr int RB = 4;
+  const long long stride = (long long)gridDim.x * RPI;
+  for (long long p0 = (long long)blockIdx.x * RPI + row; p0 < M; p0 += stride * RB) {
+    i4v xv[RB], rv[RB];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = v[k] * sc[k] + sh[k];
-    if (r) {
-      float rv[8];
-      unpack8(*(const i4v*)(r + e), rv);
-      if (rscale) {
+    for (int b = 0; b < RB; ++b) {
+      const long long p = p0 + b * stride;
+      const long long e = base + (p < M ? p : p0) * C;
+      xv[b] = *(const i4v*)(x + e);
+      if (r) rv[b] = *(const i4v*)(r + e);
+    }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] += rv[k] * rsc[k] + rsh[k];
-      } else {
+    for (int b = 0; b < RB; ++b) {
+      const long long p = p0 + b * stride;
+      if (p >= M) break;
+      const long long e = base + p * C;
+      float v[8];
+      unpack8(xv[b], v);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] += rv[k];
+      for (int k = 0; k < 8; ++k) v[k] = v[k] * sc[k] + sh[k];
+      if (r) {
+        float rr[8];
+        unpack8(rv[b], rr);
+        if (rscale) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] += rr[k] * rsc[k] + rsh[k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] += rr[k];
+        }
       }
+      if (act == 1) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
+      } else if (act == 2) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.01f * v[k];
+      } else if (act == 3) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.2f * v[k];
+      }
+      *(i4v*)(y + e) = pack8(v);
     }
-    if (act == 1) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
-    } else if (act == 2) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.01f * v[k];
-    } else if (act == 3) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.2f * v[k];
-    }
-    *(i4v*)(y + e) = pack8(v);
   }
 }
 
@@ -187,7 +218,6 @@ DDL_API int ddl_bn_apply(const void* x, const float* scale, const float* shift, 
 // Each block folds its rows through LDS (log-depth tree), then adds into stripe
 // (blockIdx.x % NSTRIPE) of part[G][NSTRIPE][2C]; bn_fold sums the stripes into sums[G][2C] and
 // d(beta) += s0, d(gamma) += s1 (one thread per channel, no contended atomics).
-#define BN_NSTRIPE 32
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ ymask, const bf16_t* __restrict__ x,
     const float* __restrict__ mean, const float* __restrict__ rstd, float* __restrict__ part,
@@ -320,22 +350,38 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   load8f(cg + C, B);
   load8f(cg + 2 * C, Cc);
   const long long base = (long long)g * M * C + cc * 8;
-  for (long long p = (long long)blockIdx.x * RPI + row; p < M; p += (long long)gridDim.x * RPI) {
-    const long long e = base + p * C;
-    float d[8], xv[8];
-    unpack8(*(const i4v*)(dy + e), d);
-    unpack8(*(const i4v*)(x + e), xv);
-    if (ymask) {
-      float yv[8];
-      unpack8(*(const i4v*)(ymask + e), yv);
+  constexpr int RB = 4;  // rows per thread per pass, loads first (see bn_apply_kernel)
+  const long long stride = (long long)gridDim.x * RPI;
+  for (long long p0 = (long long)blockIdx.x * RPI + row; p0 < M; p0 += stride * RB) {
+    i4v dv[RB], xv[RB], mv[RB];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) if (!(yv[k] > 0.f)) d[k] = 0.f;
+    for (int b = 0; b < RB; ++b) {
+      const long long p = p0 + b * stride;
+      const long long e = base + (p < M ? p : p0) * C;
+      dv[b] = *(const i4v*)(dy + e);
+      xv[b] = *(const i4v*)(x + e);
+      if (ymask) mv[b] = *(const i4v*)(ymask + e);
     }
-    if (dym_out) *(i4v*)(dym_out + e) = pack8(d);
-    float o[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = A[k] * d[k] + B[k] * xv[k] + Cc[k];
-    *(i4v*)(dx + e) = pack8(o);
+    for (int b = 0; b < RB; ++b) {
+      const long long p = p0 + b * stride;
+      if (p >= M) break;
+      const long long e = base + p * C;
+      float d[8], xf[8];
+      unpack8(dv[b], d);
+      unpack8(xv[b], xf);
+      if (ymask) {
+        float yv[8];
+        unpack8(mv[b], yv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) if (!(yv[k] > 0.f)) d[k] = 0.f;
+      }
+      if (dym_out) *(i4v*)(dym_out + e) = pack8(d);
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = A[k] * d[k] + B[k] * xf[k] + Cc[k];
+      *(i4v*)(dx + e) = pack8(o);
+    }
   }
 }
 
@@ -410,16 +456,19 @@ __global__ __launch_bounds__(256) void bn_fold_coef_kernel(
   __shared__ float red[8 * 64];
   const int g = blockIdx.y, c = blockIdx.x * 32 + (threadIdx.x & 31);
   const bool valid = c < C;
-  float s0, s1;
-  stripe_fold(part + (long long)g * BN_NSTRIPE * 2 * C, BN_NSTRIPE, C, c, valid, red, s0, s1);
-  if ((threadIdx.x >> 5) != 0 || !valid) return;
+  const bool lead = (threadIdx.x >> 5) == 0 && valid;
   const int i = g * C + c;
   const long long po = (long long)g * gs_param + c;
-  if (dbeta) dbeta[po] += s0;
-  if (dgamma) dgamma[po] += s1;
+  // the tail's inputs load with the stripe fold's (one round trip)
+  const float mu = lead ? mean[i] : 0.f, rs = lead ? rstd[i] : 0.f;
+  const float ga = (lead && gamma) ? gamma[po] : 1.f;
+  const float db0 = (lead && dbeta) ? dbeta[po] : 0.f, dg0 = (lead && dgamma) ? dgamma[po] : 0.f;
+  float s0, s1;
+  stripe_fold<BN_NSTRIPE>(part + (long long)g * BN_NSTRIPE * 2 * C, BN_NSTRIPE, C, c, valid, red, s0, s1);
+  if (!lead) return;
+  if (dbeta) dbeta[po] = db0 + s0;
+  if (dgamma) dgamma[po] = dg0 + s1;
   const float invM = 1.f / (float)M;
-  const float mu = mean[i], rs = rstd[i];
-  const float ga = gamma ? gamma[po] : 1.f;
   const float A = ga * rs;
   const float B = -A * rs * s1 * invM;
   coef[(long long)g * 3 * C + c] = A;

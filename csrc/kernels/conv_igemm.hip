@@ -1096,6 +1096,10 @@ static hipError_t dispatch(const ConvArgs& a, int Pd, int Qd, int bp, int bq, in
   DDL_CFG(64, 64, 64, 3) DDL_CFG(128, 64, 64, 3)
   // 256-wide tiles: 128x64 per wave (1.5x the MFMA work per LDS byte of a 64x64 wave tile)
   DDL_CFG(256, 128, 32, 3) DDL_CFG(128, 256, 32, 3) DDL_CFG(256, 128, 32, 2) DDL_CFG(128, 256, 32, 2)
+  // deep rings for few-workgroup grids (one client): a 64-wide wave tile issues 4-8 MFMAs per
+  // K-step, far less than one L2 round trip, so more K-steps must be in flight per workgroup
+  DDL_CFG(64, 64, 32, 6) DDL_CFG(64, 64, 32, 8) DDL_CFG(64, 128, 32, 6) DDL_CFG(64, 128, 32, 8)
+  DDL_CFG(128, 64, 32, 6) DDL_CFG(128, 128, 32, 6)
 #undef DDL_CFG
   // 64-wide P tiles with the 4 waves side by side along Q (64x64 per wave); encoded as bp = 48
 #define DDL_CFG1(BQ_, BK_, NS_) \

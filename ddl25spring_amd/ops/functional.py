@@ -73,7 +73,10 @@ CONV_TILES = [(64, 64, 32, 4), (64, 128, 32, 4), (128, 64, 32, 4), (128, 128, 32
               (64, 64, 64, 3), (128, 64, 64, 3), (256, 128, 32, 3), (128, 256, 32, 3),
               (256, 128, 32, 2), (128, 256, 32, 2),
               # bp = 48 selects BP = 64 with the 4 waves along Q (1x4, 64x64 per wave)
-              (48, 256, 32, 4), (48, 256, 64, 3), (48, 256, 64, 2), (48, 256, 32, 3)]
+              (48, 256, 32, 4), (48, 256, 64, 3), (48, 256, 64, 2), (48, 256, 32, 3),
+              # deep LDS rings for few-workgroup grids
+              (64, 64, 32, 6), (64, 64, 32, 8), (64, 128, 32, 6), (64, 128, 32, 8), (128, 64, 32, 6),
+              (128, 128, 32, 6)]
 
 
 # halo-staged 3x3 stride-1 tiles (bp, bq, ns); bp = 48: 64 channels with the 4 waves along Q
