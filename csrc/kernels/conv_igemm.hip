@@ -69,6 +69,11 @@ struct ConvArgs {
   // bn_x * mask_scale + mask_shift > 0 (the forward bn_apply's pre-activation; needs bn_x)
   const float* mask_scale;  // [G][C]
   const float* mask_shift;
+  // DGRAD residual on the stride-2 subgrid (res_sub = 2): `residual` is compact
+  // [G][N][ceil(H/2)][ceil(W/2)][C] (group stride res_gs) and adds to the dx pixels (2i, 2j) only —
+  // the gradient of a 1x1 / stride-2 projection shortcut, computed without the 3/4 zero pixels.
+  long long res_gs;
+  int res_sub;
 };
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
@@ -758,7 +763,9 @@ __device__ __forceinline__ void conv_body(const ConvArgs& a, char* smem, int lin
     }
     bf16_t* O = (bf16_t*)a.out + (long long)g * a.out_gs;
     const float* bias = a.bias ? a.bias + (long long)g * a.bias_gs : nullptr;
-    const bf16_t* res = a.residual ? (const bf16_t*)a.residual + (long long)g * a.out_gs : nullptr;
+    const bool rsub = MODE == MODE_DGRAD && a.res_sub == 2;
+    const bf16_t* res = a.residual ? (const bf16_t*)a.residual + (long long)g * (rsub ? a.res_gs : a.out_gs)
+                                   : nullptr;
     const bf16_t* msk = a.mask ? (const bf16_t*)a.mask + (long long)g * a.out_gs : nullptr;
     // striped accumulation: blocks of different pixel tiles hit different copies, so the fp32
     // atomics of thousands of blocks do not serialise on the same few cache lines
@@ -812,13 +819,28 @@ __device__ __forceinline__ void conv_body(const ConvArgs& a, char* smem, int lin
         }
         return true;
       };
+      // residual element offset of output item (tj, it) at offset o; false: no residual term there
+      auto res_off = [&](int tj, int it, long long o, long long& ro) {
+        ro = o;
+        if (!rsub) return true;
+        const int px = prow + it * PSTEP;
+        const int q = q0 + (px >> 4) * WQ + tj * 16 + (px & 15);
+        if (phased) {  // phase (0, 0)'s local pixel index is the compact index
+          ro = (long long)q * Pd + p;
+          return (ph_a | ph_b) == 0;
+        }
+        const int n = q / (H * W), rem = q - n * (H * W);
+        const int h = rem / W, w = rem - h * W;
+        ro = ((long long)(n * ((H + 1) >> 1) + (h >> 1)) * ((W + 1) >> 1) + (w >> 1)) * Pd + p;
+        return ((h | w) & 1) == 0;
+      };
       auto load_in = [&](int tj, i4v* X, i4v* R, i4v* M) {
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-          long long o = 0;
+          long long o = 0, ro = 0;
           const bool ok = item_off(tj, it, o);
           X[it] = (ok && bnx) ? *(const i4v*)(bnx + o) : (i4v){0, 0, 0, 0};
-          R[it] = (ok && res) ? *(const i4v*)(res + o) : (i4v){0, 0, 0, 0};
+          R[it] = (ok && res && res_off(tj, it, o, ro)) ? *(const i4v*)(res + ro) : (i4v){0, 0, 0, 0};
           M[it] = (ok && msk) ? *(const i4v*)(msk + o) : (i4v){0, 0, 0, 0};
         }
       };
@@ -940,7 +962,9 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvArgs a, i
   const long long slice = (long long)a.G * rows * Pd;
   const float* part = a.partial + (long long)g * rows * Pd + c0;
   bf16_t* O = (bf16_t*)a.out + (long long)g * a.out_gs + c0;
-  const bf16_t* res = a.residual ? (const bf16_t*)a.residual + (long long)g * a.out_gs + c0 : nullptr;
+  const bool rsub = mode == MODE_DGRAD && a.res_sub == 2;  // compact stride-2 residual (ConvArgs)
+  const bf16_t* res = a.residual ? (const bf16_t*)a.residual + (long long)g * (rsub ? a.res_gs : a.out_gs) + c0
+                                 : nullptr;
   const bf16_t* msk = a.mask ? (const bf16_t*)a.mask + (long long)g * a.out_gs + c0 : nullptr;
   const bf16_t* bnx = (mode == MODE_DGRAD && a.bn_x) ? (const bf16_t*)a.bn_x + (long long)g * a.out_gs + c0
                                                       : nullptr;
@@ -987,7 +1011,19 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvArgs a, i
       i4v xres[RB], xmsk[RB], xbnx[RB];
 #pragma unroll
       for (int b = 0; b < RB; ++b) {
-        if (res) xres[b] = *(const i4v*)(res + eb[b]);
+        xres[b] = (i4v){0, 0, 0, 0};
+        if (res) {
+          long long ro = eb[b];
+          bool ok = true;
+          if (rsub) {  // row r = (n*H + h)*W + w of dx; the residual lives on even (h, w) only
+            const long long r = eb[b] / Pd;
+            const long long n = r / ((long long)a.H * a.W), rem = r - n * a.H * a.W;
+            const int h = (int)(rem / a.W), w = (int)(rem - (long long)h * a.W);
+            ok = ((h | w) & 1) == 0;
+            ro = ((n * ((a.H + 1) >> 1) + (h >> 1)) * ((a.W + 1) >> 1) + (w >> 1)) * Pd;
+          }
+          if (ok) xres[b] = *(const i4v*)(res + ro);
+        }
         if (msk) xmsk[b] = *(const i4v*)(msk + eb[b]);
         if (bnx) xbnx[b] = *(const i4v*)(bnx + eb[b]);
       }
@@ -1355,6 +1391,7 @@ static int plan_wgrad(const ConvArgs& a, int cfg, ConvPlan& pl) {
 }
 
 static int plan_mode(int mode, const ConvArgs& a, int cfg, ConvPlan& pl) {
+  if (a.res_sub == 2 && (mode != MODE_DGRAD || !a.residual)) return (int)hipErrorInvalidValue;
   if (mode == MODE_FWD) return plan_fwd(a, cfg, pl);
   if (mode == MODE_DGRAD) return plan_dgrad(a, cfg, pl);
   if (mode == MODE_WGRAD) return plan_wgrad(a, cfg, pl);

@@ -46,7 +46,24 @@ class _BNConv(ConvUnit):
                               st.grad_of(self.beta), emit_dym=emit_dym, part=part)
 
 
-class BasicBlock(Layer):
+class _ShortcutGrad:
+    def _shortcut_backward(self, dym, dctx, x):
+        """Projection shortcut backward: its BN, then its conv's WGRAD and (if the block input needs a
+        gradient) DGRAD. A 1x1 / stride-2 shortcut's input gradient is nonzero only on the (2i, 2j)
+        pixels, so its DGRAD runs as a dense 1x1 conv on the compact grid and the block's first
+        DGRAD adds it there (residual_sub = 2) instead of materialising 3/4 zeros.
+        -> (residual for the first conv's DGRAD, residual_sub)."""
+        cs, mus, rss, gs = dctx
+        st = self.store
+        dcs = self.down.bn_backward(dym, None, cs, mus, rss)
+        sub = gs.stride == 2 and gs.R == 1 and gs.S == 1 and gs.pad == 0
+        dgeom = Fn.ConvGeom(gs.G, gs.N, gs.P, gs.Q, gs.C, gs.K, 1, 1, 1, 0) if sub else None
+        dres = Fn.conv_dgrad_wgrad(dcs, st.shadow_of(self.down.w), x, gs, st.grad_of(self.down.w),
+                                   want_dx=self.needs_input_grad, dgeom=dgeom)
+        return dres, (2 if sub else 1)
+
+
+class BasicBlock(_ShortcutGrad, Layer):
     name = "basic"
     residual_out = True
     expansion = 1
@@ -98,13 +115,7 @@ class BasicBlock(Layer):
         else:
             dc2, dym = self.conv2.bn_backward(dout, out, c2, mu2, rs2, emit_dym=True)
         # every conv's DGRAD and WGRAD read the same dY: one (possibly paired) launch each
-        if dctx is not None:
-            cs, mus, rss, gs = dctx
-            dcs = self.down.bn_backward(dym, None, cs, mus, rss)
-            dres = Fn.conv_dgrad_wgrad(dcs, st.shadow_of(self.down.w), x, gs, st.grad_of(self.down.w),
-                                       want_dx=self.needs_input_grad)
-        else:
-            dres = dym
+        dres, rsub = self._shortcut_backward(dym, dctx, x) if dctx is not None else (dym, 1)
         # dgrad epilogue applies bn1's ReLU mask (recomputed from c1: no read of a1) and reduces
         # bn1's backward sums (no reduce pass)
         da1, part1 = Fn.conv_dgrad_wgrad(dc2, st.shadow_of(self.conv2.w), a1, g2, st.grad_of(self.conv2.w),
@@ -113,7 +124,7 @@ class BasicBlock(Layer):
         # with fuse: the producer's ReLU mask (x > 0) and BN reduce in this dgrad's epilogue
         return Fn.conv_dgrad_wgrad(dc1, st.shadow_of(self.conv1.w), x, g1, st.grad_of(self.conv1.w),
                                    residual=dres, mask=x if fuse is not None else None, bn=fuse,
-                                   want_dx=self.needs_input_grad)
+                                   want_dx=self.needs_input_grad, residual_sub=rsub)
 
     def flops(self, s):
         G, N, H, W, _ = s
@@ -128,7 +139,7 @@ class BasicBlock(Layer):
         return (G, N, (H + 2 - 3) // self.stride + 1, (W + 2 - 3) // self.stride + 1, self.cout)
 
 
-class Bottleneck(Layer):
+class Bottleneck(_ShortcutGrad, Layer):
     name = "bottleneck"
     residual_out = True
     expansion = 4
@@ -184,13 +195,7 @@ class Bottleneck(Layer):
             dc3, dym = self.conv3.bn_backward(dout, None, c3, mu3, rs3, part=part), dout
         else:
             dc3, dym = self.conv3.bn_backward(dout, out, c3, mu3, rs3, emit_dym=True)
-        if dctx is not None:
-            cs, mus, rss, gs = dctx
-            dcs = self.down.bn_backward(dym, None, cs, mus, rss)
-            dres = Fn.conv_dgrad_wgrad(dcs, st.shadow_of(self.down.w), x, gs, st.grad_of(self.down.w),
-                                       want_dx=self.needs_input_grad)
-        else:
-            dres = dym
+        dres, rsub = self._shortcut_backward(dym, dctx, x) if dctx is not None else (dym, 1)
         da2, part2 = Fn.conv_dgrad_wgrad(dc3, st.shadow_of(self.conv3.w), a2, g3, st.grad_of(self.conv3.w),
                                          bn=(c2, mu2, rs2), mask_bn=(sc2, sh2))
         dc2 = self.conv2.bn_backward(da2, None, c2, mu2, rs2, part=part2)
@@ -199,7 +204,7 @@ class Bottleneck(Layer):
         dc1 = self.conv1.bn_backward(da1, None, c1, mu1, rs1, part=part1)
         return Fn.conv_dgrad_wgrad(dc1, st.shadow_of(self.conv1.w), x, g1, st.grad_of(self.conv1.w),
                                    residual=dres, mask=x if fuse is not None else None, bn=fuse,
-                                   want_dx=self.needs_input_grad)
+                                   want_dx=self.needs_input_grad, residual_sub=rsub)
 
     def flops(self, s):
         G, N, H, W, _ = s

@@ -43,7 +43,7 @@ class ConvArgs(ctypes.Structure):
                 ("S", i32), ("P", i32), ("Q", i32), ("stride", i32), ("pad", i32),
                 ("relu", i32), ("accumulate", i32), ("split_k", i32), ("stats_stripes", i32),
                 ("bn_x", vp), ("bn_mean", vp), ("bn_rstd", vp), ("partial", vp), ("partial_cap", i64),
-                ("mask_scale", vp), ("mask_shift", vp)]
+                ("mask_scale", vp), ("mask_shift", vp), ("res_gs", i64), ("res_sub", i32)]
 
 
 class BNArgs(ctypes.Structure):

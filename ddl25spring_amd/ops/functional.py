@@ -184,14 +184,16 @@ def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out=None, 
 
 
 def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0, bn=None, split_k=0,
-               mask_bn=None, _tune=True):
+               mask_bn=None, residual_sub=1, _tune=True):
     """dx[G,N,H,W,C] = conv_transpose(dy, w) (+residual) * (mask > 0).
 
     bn = (x, mean, rstd): also reduce, in the epilogue, the preceding BatchNorm's backward sums
     (sum dx, sum dx * (x - mean) * rstd) into a striped [G, BN_STRIPES, 2, C] buffer; returns
     (dx, part) for ``bn_backward(..., part=part)``.
     mask_bn = (scale, shift) [G, C] (with bn): the ReLU mask of ``bn_apply(x, scale, shift, relu)``
-    recomputed from x in the epilogue, (x * scale + shift > 0), instead of read from its output."""
+    recomputed from x in the epilogue, (x * scale + shift > 0), instead of read from its output.
+    residual_sub = 2: ``residual`` is compact [G, N, ceil(H/2), ceil(W/2), C] and adds to the
+    pixels (2i, 2j) only (a 1x1 / stride-2 shortcut's input gradient without its zero pixels)."""
     if mask_bn is not None:
         assert bn is not None and mask is None, "mask_bn recomputes the mask from bn's x"
     if not dy.is_cuda:
@@ -200,6 +202,8 @@ def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0,
             xs = bn[0].float()
             bshape = (geom.G,) + (1,) * (xs.dim() - 2) + (geom.C,)
             mask = ((xs * sc.float().reshape(bshape) + sh.float().reshape(bshape)) > 0).to(dy.dtype)
+        if residual is not None and residual_sub == 2:
+            residual = expand_sub2(residual, geom.H, geom.W)
         dx = ref.conv_dgrad(dy, w, geom, residual, mask)
         if out is not None:
             out.copy_(dx)
@@ -216,23 +220,45 @@ def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0,
     _check_inner(dy, "dy"); _check_inner(w, "w")
     dx = out if out is not None else torch.empty(geom.G, geom.N, geom.H, geom.W, geom.C,
                                                  dtype=torch.bfloat16, device=dy.device)
-    if residual is not None and residual.stride(0) != dx.stride(0):
-        residual = residual.contiguous()
-    if mask is not None and mask.stride(0) != dx.stride(0):
-        mask = mask.contiguous()
+    residual, mask = _dgrad_side_inputs(geom, dx, residual, mask, residual_sub)
     if _tune and cfg == 0 and split_k == 0 and autotune.ENABLED:
         def run(c, sp):
             conv_dgrad(dy, w, geom, residual=residual, mask=mask, out=torch.empty_like(dx), cfg=c or 0,
-                       bn=bn, split_k=sp, mask_bn=mask_bn, _tune=False)
-        c, split_k = autotune.pick("dgrad", geom, (residual is not None, mask is not None, bn is not None,
-                                                   mask_bn is not None), run)
+                       bn=bn, split_k=sp, mask_bn=mask_bn, residual_sub=residual_sub, _tune=False)
+        c, split_k = autotune.pick("dgrad", geom, _dgrad_flags(residual, mask, bn, mask_bn, residual_sub), run)
         cfg = c or 0
-    a, part = _dgrad_args(dy, w, geom, dx, residual, mask, bn, mask_bn, split_k)
+    a, part = _dgrad_args(dy, w, geom, dx, residual, mask, bn, mask_bn, split_k, residual_sub)
     check(_lib.kernels().ddl_conv_dgrad(ctypes.byref(a), cfg, stream()), "conv_dgrad")
     return dx if bn is None else (dx, part)
 
 
-def _dgrad_args(dy, w, geom, dx, residual, mask, bn, mask_bn, split_k):
+def expand_sub2(r: torch.Tensor, H: int, W: int) -> torch.Tensor:
+    """Compact stride-2 residual [G, N, ceil(H/2), ceil(W/2), C] -> full [G, N, H, W, C] (zeros
+    off the (2i, 2j) pixels)."""
+    full = torch.zeros(r.shape[0], r.shape[1], H, W, r.shape[-1], dtype=r.dtype, device=r.device)
+    full[:, :, ::2, ::2] = r
+    return full
+
+
+def _dgrad_flags(residual, mask, bn, mask_bn, residual_sub):
+    return (residual is not None, mask is not None, bn is not None, mask_bn is not None) + \
+        ((True,) if residual is not None and residual_sub == 2 else ())
+
+
+def _dgrad_side_inputs(geom, dx, residual, mask, residual_sub):
+    if residual is not None:
+        if residual_sub == 2:
+            want = (geom.G, geom.N, (geom.H + 1) // 2, (geom.W + 1) // 2, geom.C)
+            assert tuple(residual.shape) == want, (tuple(residual.shape), want)
+            residual = residual.contiguous()
+        elif residual.stride(0) != dx.stride(0):
+            residual = residual.contiguous()
+    if mask is not None and mask.stride(0) != dx.stride(0):
+        mask = mask.contiguous()
+    return residual, mask
+
+
+def _dgrad_args(dy, w, geom, dx, residual, mask, bn, mask_bn, split_k, residual_sub=1):
     """ConvArgs of a DGRAD launch (+ the zeroed BN-backward partial sums when bn is fused)."""
     part = None
     kw = {}
@@ -246,6 +272,8 @@ def _dgrad_args(dy, w, geom, dx, residual, mask, bn, mask_bn, split_k):
             sc, sh = mask_bn
             assert sc.is_contiguous() and sh.is_contiguous() and sc.numel() == geom.G * geom.C
             kw.update(mask_scale=ptr(sc), mask_shift=ptr(sh))
+    if residual is not None and residual_sub == 2:
+        kw.update(res_sub=2, res_gs=residual.stride(0))
     a = _conv_args(geom, dy.device, split_k, True, w=ptr(w), dy=ptr(dy), out=ptr(dx), residual=ptr(residual),
                    mask=ptr(mask), w_gs=_gs(w), dy_gs=_gs(dy), out_gs=_gs(dx), **kw)
     return a, part
@@ -304,13 +332,15 @@ MODE_FWD, MODE_DGRAD, MODE_WGRAD = 0, 1, 2
 
 
 def conv_pair(dy, w, x, geom: ConvGeom, dw, dcfg: int, dsplit: int, wcfg: int, wsplit: int,
-              residual=None, mask=None, bn=None, mask_bn=None, out=None):
-    """Explicit paired launch: DGRAD (tile ``dcfg``, split ``dsplit``, fused epilogue as conv_dgrad)
-    and WGRAD (``wcfg``, ``wsplit``, accumulating into dw) in one grid. -> (dx, part | None).
-    Raises KernelError when the two tiles have no paired instantiation."""
-    dx = out if out is not None else torch.empty(geom.G, geom.N, geom.H, geom.W, geom.C,
+              residual=None, mask=None, bn=None, mask_bn=None, out=None, residual_sub=1, dgeom=None):
+    """Explicit paired launch: DGRAD (tile ``dcfg``, split ``dsplit``, fused epilogue as conv_dgrad;
+    geometry ``dgeom`` or ``geom``) and WGRAD (``wcfg``, ``wsplit``, accumulating into dw) in one
+    grid. -> (dx, part | None). Raises KernelError when the tiles have no paired instantiation."""
+    dg = dgeom or geom
+    dx = out if out is not None else torch.empty(dg.G, dg.N, dg.H, dg.W, dg.C,
                                                  dtype=torch.bfloat16, device=dy.device)
-    ad, part = _dgrad_args(dy, w, geom, dx, residual, mask, bn, mask_bn, dsplit)
+    residual, mask = _dgrad_side_inputs(dg, dx, residual, mask, residual_sub)
+    ad, part = _dgrad_args(dy, w, dg, dx, residual, mask, bn, mask_bn, dsplit, residual_sub)
     aw = _wgrad_args(dy, x, geom, dw, True, wsplit)
     rc = _lib.kernels().ddl_conv_pair(ctypes.byref(ad), MODE_DGRAD, dcfg, ctypes.byref(aw), MODE_WGRAD,
                                       wcfg, stream())
@@ -321,64 +351,62 @@ def conv_pair(dy, w, x, geom: ConvGeom, dw, dcfg: int, dsplit: int, wcfg: int, w
 
 
 def conv_dgrad_wgrad(dy, w, x, geom: ConvGeom, dw, residual=None, mask=None, bn=None, mask_bn=None,
-                     want_dx: bool = True):
-    """``conv_wgrad(dy, x, geom, dw)`` and (if want_dx) ``conv_dgrad(dy, w, geom, residual, mask,
-    bn=bn, mask_bn=mask_bn)`` — both read dy and are independent, so on the GPU they may run as
-    ONE paired launch (whichever of paired / back-to-back the tuner measured faster for this
-    shape). Returns what conv_dgrad returns (None without want_dx)."""
+                     want_dx: bool = True, residual_sub: int = 1, dgeom: ConvGeom | None = None):
+    """``conv_wgrad(dy, x, geom, dw)`` and (if want_dx) ``conv_dgrad(dy, w, dgeom or geom, residual,
+    mask, bn=bn, mask_bn=mask_bn, residual_sub=...)`` — both read dy and are independent, so on
+    the GPU they may run as ONE paired launch (whichever of paired / back-to-back the tuner
+    measured faster for this shape). ``dgeom``: the DGRAD's own geometry (a stride-2 1x1
+    shortcut's input gradient on the compact grid). Returns what conv_dgrad returns (None
+    without want_dx)."""
+    dg = dgeom or geom
+    dkw = dict(residual=residual, mask=mask, bn=bn, mask_bn=mask_bn, residual_sub=residual_sub)
     if not want_dx or not dy.is_cuda or not PAIR_ENABLED or _WGRAD_SIDE is not None \
             or not autotune.ENABLED:
         conv_wgrad(dy, x, geom, dw)
         if not want_dx:
             return None
-        return conv_dgrad(dy, w, geom, residual=residual, mask=mask, bn=bn, mask_bn=mask_bn)
+        return conv_dgrad(dy, w, dg, **dkw)
     _check_inner(dy, "dy"); _check_inner(w, "w"); _check_inner(x, "x"); _check_inner(dw, "dw")
-    dx = torch.empty(geom.G, geom.N, geom.H, geom.W, geom.C, dtype=torch.bfloat16, device=dy.device)
-    if residual is not None and residual.stride(0) != dx.stride(0):
-        residual = residual.contiguous()
-    if mask is not None and mask.stride(0) != dx.stride(0):
-        mask = mask.contiguous()
-    dflags = (residual is not None, mask is not None, bn is not None, mask_bn is not None)
+    dx = torch.empty(dg.G, dg.N, dg.H, dg.W, dg.C, dtype=torch.bfloat16, device=dy.device)
+    residual, mask = _dgrad_side_inputs(dg, dx, residual, mask, residual_sub)
+    dkw.update(residual=residual, mask=mask)
+    dflags = _dgrad_flags(residual, mask, bn, mask_bn, residual_sub)
     lib = _lib.kernels()
 
-    def run_d(c, sp, out=None):
-        return conv_dgrad(dy, w, geom, residual=residual, mask=mask, out=out if out is not None else torch.empty_like(dx),
-                          cfg=c or 0, bn=bn, split_k=sp, mask_bn=mask_bn, _tune=False)
+    def run_d(c, sp):
+        return conv_dgrad(dy, w, dg, out=torch.empty_like(dx), cfg=c or 0, split_k=sp, _tune=False, **dkw)
 
-    def run_w(c, sp, out=None):
-        conv_wgrad(dy, x, geom, out if out is not None else torch.zeros_like(dw), True, cfg=c or 0,
-                   splits=sp, _tune=False)
+    def run_w(c, sp):
+        conv_wgrad(dy, x, geom, torch.zeros_like(dw), True, cfg=c or 0, splits=sp, _tune=False)
 
-    def launch_pair(dcfg, dsp, wcfg, wsp, dx_out, dw_out):
-        return conv_pair(dy, w, x, geom, dw_out, dcfg or 0, dsp, wcfg or 0, wsp, residual=residual,
-                         mask=mask, bn=bn, mask_bn=mask_bn, out=dx_out)[1]
-
-    dpick = autotune.pick("dgrad", geom, dflags, run_d)
+    dpick = autotune.pick("dgrad", dg, dflags, run_d)
     wpick = autotune.pick("wgrad", geom, (True,), run_w)
 
     def supported(dc, dsp, wc, wsp):
-        ad, _ = _dgrad_args(dy, w, geom, dx, residual, mask, bn, mask_bn, dsp)
+        ad, _ = _dgrad_args(dy, w, dg, dx, residual, mask, bn, mask_bn, dsp, residual_sub)
         aw = _wgrad_args(dy, x, geom, dw, True, wsp)
         return bool(lib.ddl_conv_pair_supported(ctypes.byref(ad), MODE_DGRAD, dc or 0,
                                                 ctypes.byref(aw), MODE_WGRAD, wc or 0))
 
-    def run_pair(cand):
+    def launch_pair(cand, dx_out, dw_out):
         dc, dsp, wc, wsp = cand
-        launch_pair(dc, dsp, wc, wsp, torch.empty_like(dx), torch.zeros_like(dw))
+        return conv_pair(dy, w, x, geom, dw_out, dc or 0, dsp, wc or 0, wsp, out=dx_out, dgeom=dgeom,
+                         **dkw)[1]
 
     def run_seq():
         run_w(*wpick)
         run_d(*dpick)
 
-    choice = autotune.pick_pair(("pair", dflags), geom, dpick, wpick, supported, run_pair, run_seq,
+    tag = ("pair", dflags) + ((dg.H, dg.W, dg.R, dg.stride) if dgeom is not None else ())
+    choice = autotune.pick_pair(tag, geom, dpick, wpick, supported,
+                                lambda cand: launch_pair(cand, torch.empty_like(dx), torch.zeros_like(dw)),
+                                run_seq,
                                 [(conv_cfg(bp, bq, bk, ns, h), 0) for bp, bq, bk, ns, h in PAIR_DGRAD],
                                 [(conv_cfg(*t), 0) for t in PAIR_WGRAD])
     if choice is None:  # back-to-back single launches
         conv_wgrad(dy, x, geom, dw, cfg=wpick[0] or 0, splits=wpick[1], _tune=False)
-        return conv_dgrad(dy, w, geom, residual=residual, mask=mask, out=dx, cfg=dpick[0] or 0, bn=bn,
-                          split_k=dpick[1], mask_bn=mask_bn, _tune=False)
-    dc, dsp, wc, wsp = choice
-    part = launch_pair(dc, dsp, wc, wsp, dx, dw)
+        return conv_dgrad(dy, w, dg, out=dx, cfg=dpick[0] or 0, split_k=dpick[1], _tune=False, **dkw)
+    part = launch_pair(choice, dx, dw)
     return dx if bn is None else (dx, part)
 
 

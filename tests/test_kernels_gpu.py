@@ -452,3 +452,34 @@ def test_conv_pair(cuda, geom):
     dx, part = Fn.conv_dgrad_wgrad(dy, w, x, g, dw, residual=res, mask=mask, bn=(x, mean, rstd))
     _close(dx, dx_ref)
     _close(dw, dw_ref, rel=2e-3)
+
+
+SUB2_GEOMS = [
+    ConvGeom(G=2, N=3, H=16, W=16, C=64, K=128, R=3, S=3, stride=2, pad=1),   # BasicBlock conv1 (phased)
+    ConvGeom(G=1, N=2, H=8, W=8, C=128, K=64, R=1, S=1, stride=1, pad=0),     # Bottleneck conv1 (unphased)
+    ConvGeom(G=1, N=3, H=7, W=7, C=64, K=64, R=3, S=3, stride=2, pad=1),      # odd size
+]
+
+
+@pytest.mark.parametrize("geom", SUB2_GEOMS, ids=lambda g: f"{g.C}x{g.K}_{g.H}_{g.R}s{g.stride}")
+def test_conv_dgrad_residual_sub2(cuda, geom):
+    """A compact stride-2 residual (the 1x1 / stride-2 shortcut's input gradient) adds to the (2i, 2j)
+    pixels of dx only: single launch, forced split-K (the split epilogue's path), tuned pair."""
+    g = geom
+    dy = _rand(g.G, g.N, g.P, g.Q, g.K, dev=cuda)
+    w = _weights(g, cuda)
+    x = _rand(g.G, g.N, g.H, g.W, g.C, dev=cuda)
+    res = _rand(g.G, g.N, (g.H + 1) // 2, (g.W + 1) // 2, g.C, dev=cuda)
+    mask = _rand(g.G, g.N, g.H, g.W, g.C, dev=cuda)
+    full = Fn.expand_sub2(res.cpu(), g.H, g.W)
+    dx_ref = ref.conv_dgrad(dy.cpu(), w.cpu(), g, residual=full, mask=mask.cpu())
+    _close(Fn.conv_dgrad(dy, w, g, residual=res, mask=mask, residual_sub=2), dx_ref)
+    _close(Fn.conv_dgrad(dy, w, g, residual=res, mask=mask, residual_sub=2, split_k=2), dx_ref)
+    dw = torch.zeros(g.G, g.K, g.R, g.S, g.C, device=cuda)
+    dx = Fn.conv_dgrad_wgrad(dy, w, x, g, dw, residual=res, mask=mask, residual_sub=2)
+    _close(dx, dx_ref)
+    dw_ref = torch.zeros(g.G, g.K, g.R, g.S, g.C)
+    ref.conv_wgrad(dy.cpu(), x.cpu(), g, dw_ref)
+    _close(dw, dw_ref, rel=2e-3)
+    # the CPU op path agrees with the reference composition
+    _close(Fn.conv_dgrad(dy.cpu(), w.cpu(), g, residual=res.cpu(), mask=mask.cpu(), residual_sub=2), dx_ref)
