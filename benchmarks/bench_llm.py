@@ -14,13 +14,17 @@ def main():
     ap.add_argument("--dp", type=int, default=0, help="default: world // pp")
     ap.add_argument("--pp", type=int, default=1)
     ap.add_argument("--batch", type=int, default=32, help="per-pipeline batch")
-    ap.add_argument("--micro", type=int, default=4)
+    ap.add_argument("--micro", type=int, default=0,
+                    help="micro-batches per pipeline (default: 4 with a pipeline, 1 without — at pp=1 "
+                         "micro-batching is only gradient accumulation: same batch, 2.2x slower)")
     ap.add_argument("--schedule", default="1f1b")
     args = ap.parse_args()
     from ddl25spring_amd.apps.llm import LLMConfig, train_llm
     from ddl25spring_amd.runtime import dist as rdist
     ctx = rdist.init()
     dp = args.dp or ctx.world // args.pp
+    if not args.micro:
+        args.micro = 4 if args.pp > 1 else 1
     cfg = LLMConfig(dp=dp, pp=args.pp, batch_size=args.batch, micro_batches=args.micro,
                     schedule=args.schedule, iters=args.steps, log_every=10 ** 9)
     out = train_llm(cfg, ctx, log=None, warmup=args.warmup)

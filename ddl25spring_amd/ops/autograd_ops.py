@@ -90,17 +90,22 @@ class _Linear(torch.autograd.Function):
         g = ctx.geom
         dy5 = dy.reshape(1, g.N, 1, 1, g.K).to(torch.bfloat16).contiguous()
         dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            dx = Fn.conv_dgrad(dy5, wb, g).view(ctx.xshape)
         if ctx.needs_input_grad[1]:
             sink = _grad_sink(ctx.w)
-            if sink is not None:  # accumulate straight into the parameter's grad
-                Fn.conv_wgrad(dy5, x2.view(1, g.N, 1, 1, g.C), g, sink.view(1, g.K, 1, 1, g.C))
+            # accumulate straight into the parameter's grad when it has a flat-buffer sink
+            dwt = sink.view(1, g.K, 1, 1, g.C) if sink is not None else \
+                torch.zeros(1, g.K, 1, 1, g.C, dtype=torch.float32, device=dy.device)
+            # dX and dW read the same dY: one (possibly paired) launch
+            dx = Fn.conv_dgrad_wgrad(dy5, wb, x2.view(1, g.N, 1, 1, g.C), g, dwt,
+                                     want_dx=ctx.needs_input_grad[0])
+            if dx is not None:
+                dx = dx.view(ctx.xshape)
+            if sink is not None:
                 _grad_ready(ctx.w)
             else:
-                dw = torch.zeros(1, g.K, 1, 1, g.C, dtype=torch.float32, device=dy.device)
-                Fn.conv_wgrad(dy5, x2.view(1, g.N, 1, 1, g.C), g, dw)
-                dw = dw.view(g.K, g.C)
+                dw = dwt.view(g.K, g.C)
+        elif ctx.needs_input_grad[0]:
+            dx = Fn.conv_dgrad(dy5, wb, g).view(ctx.xshape)
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = torch.zeros(1, g.K, dtype=torch.float32, device=dy.device)
             Fn.channel_sum(dy5.view(1, g.N, g.K), db)
@@ -406,12 +411,14 @@ class _Conv2d(torch.autograd.Function):
         g = ctx.g
         dy5 = dy.to(torch.bfloat16).contiguous().view(1, g.N, g.P, g.Q, g.K)
         dx = dw = None
-        if ctx.needs_input_grad[0]:
-            dx = Fn.conv_dgrad(dy5, wb, g).view(x.shape)
         if ctx.needs_input_grad[1]:
             dw = torch.zeros(1, g.K, g.R, g.S, g.C, dtype=torch.float32, device=dy.device)
-            Fn.conv_wgrad(dy5, x.contiguous().view(1, *x.shape), g, dw)
+            dx = Fn.conv_dgrad_wgrad(dy5, wb, x.contiguous().view(1, *x.shape), g, dw,
+                                     want_dx=ctx.needs_input_grad[0])
+            dx = None if dx is None else dx.view(x.shape)
             dw = dw.view(g.K, g.R, g.S, g.C)
+        elif ctx.needs_input_grad[0]:
+            dx = Fn.conv_dgrad(dy5, wb, g).view(x.shape)
         return dx, dw, None, None, None
 
 
