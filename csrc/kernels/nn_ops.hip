@@ -21,10 +21,13 @@
 // im2col=0: out [G*B][Hs][Ws][Cout], channel c<Cs normalised, c>=Cs zero
 // im2col=k>0: out [G*B][Ho][Wo][Cout] with Ho=(Hs+2pad-k)/stride+1, channel j=(r*k+s)*Cs+c
 // (< k*k*Cs), rest 0 — the stem conv then runs as a 1x1 GEMM on MFMA.
+// Also gathers the labels (labels_out[b] = labels[idx[b]], nullable) so a training step's whole
+// batch materialisation is one launch.
 __global__ void prep_images_kernel(const uint8_t* __restrict__ src, const int* __restrict__ idx,
                                    const float* __restrict__ mean, const float* __restrict__ inv_std,
                                    bf16_t* __restrict__ out, int nimg, int Hs, int Ws, int Cs,
-                                   int Ho, int Wo, int Cout, int im2col, int pad, int stride) {
+                                   int Ho, int Wo, int Cout, int im2col, int pad, int stride,
+                                   const int* __restrict__ labels, int* __restrict__ labels_out) {
   const long long total = (long long)nimg * Ho * Wo * (Cout / 8);
   GSTRIDE_LOOP(t, total) {
     const int cchunk = (int)(t % (Cout / 8));
@@ -33,7 +36,9 @@ __global__ void prep_images_kernel(const uint8_t* __restrict__ src, const int* _
     pix /= Wo;
     const int h = (int)(pix % Ho);
     const int b = (int)(pix / Ho);
-    const long long sbase = (long long)idx[b] * Hs * Ws * Cs;
+    const int id = idx[b];
+    const long long sbase = (long long)id * Hs * Ws * Cs;
+    if (labels && (cchunk | h | w) == 0) labels_out[b] = labels[id];
     float v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -57,15 +62,16 @@ __global__ void prep_images_kernel(const uint8_t* __restrict__ src, const int* _
 
 DDL_API int ddl_prep_images(const void* src, const int* idx, const float* mean, const float* inv_std,
                             void* out, int nimg, int Hs, int Ws, int Cs, int Cout, int im2col,
-                            int pad, int stride, hipStream_t s) {
+                            int pad, int stride, const int* labels, int* labels_out, hipStream_t s) {
   if (Cout % 8 || stride < 1) return (int)hipErrorInvalidValue;
   if (im2col && im2col * im2col * Cs > Cout) return (int)hipErrorInvalidValue;
+  if ((labels == nullptr) != (labels_out == nullptr)) return (int)hipErrorInvalidValue;
   const int Ho = im2col ? (Hs + 2 * pad - im2col) / stride + 1 : Hs;
   const int Wo = im2col ? (Ws + 2 * pad - im2col) / stride + 1 : Ws;
   const long long total = (long long)nimg * Ho * Wo * (Cout / 8);
   hipLaunchKernelGGL(prep_images_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s,
                      (const uint8_t*)src, idx, mean, inv_std, (bf16_t*)out, nimg, Hs, Ws, Cs, Ho, Wo,
-                     Cout, im2col, pad, stride);
+                     Cout, im2col, pad, stride, labels, labels_out);
   return (int)hipGetLastError();
 }
 

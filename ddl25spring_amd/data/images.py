@@ -130,20 +130,22 @@ class DeviceImageDataset:
         return self.labels.numel()
 
     def batch(self, idx: torch.Tensor, out: torch.Tensor | None = None):
-        """idx int32 [G, B] (device) -> (x [G, B, H', W', cpad] | [G, B, F] bf16, y int32 [G, B])."""
+        """idx int32 [G, B] (device) -> (x [G, B, H', W', cpad] | [G, B, F] bf16, y int32 [G, B]).
+        One launch gathers images and labels."""
         G, B = idx.shape
+        y = torch.empty(G, B, dtype=torch.int32, device=self.device)
+        kw = dict(labels=self.labels, labels_out=y)
         if self.flat:
-            x = Fn.prep_images(self.images, idx.reshape(-1), self.mean, self.inv_std, 8, 0, 0, 1)
+            x = Fn.prep_images(self.images, idx, self.mean, self.inv_std, 8, 0, 0, 1, **kw)
             # [n, H, W, 8] -> keep the real channel(s), flatten, pad to cpad
             C = self.images.shape[-1]
             flat = x[..., :C].reshape(G, B, -1)
             xo = torch.zeros(G, B, self.cpad, dtype=torch.bfloat16, device=self.device)
             xo[..., :flat.shape[-1]] = flat
         else:
-            x = Fn.prep_images(self.images, idx.reshape(-1), self.mean, self.inv_std, self.cpad,
-                               self.k, self.pad, self.stride, out=out)
+            x = Fn.prep_images(self.images, idx, self.mean, self.inv_std, self.cpad,
+                               self.k, self.pad, self.stride, out=out, **kw)
             xo = x.reshape(G, B, *x.shape[1:])
-        y = self.labels[idx.long()]
         return xo, y
 
     def full(self, n: int | None = None):

@@ -7,8 +7,8 @@ DataLoader and copied host<->device every round). Here:
   * weights of all clients live in one flat [G, P] buffer, already on the device;
   * the round's batch plan (which sample ids each client sees at each step) is computed once on
     the host (native planner or torch.randperm for DataLoader-identical order) and uploaded once;
-  * the steady-state step (gather+normalise -> fwd -> fused CE -> bwd -> fused SGD) is captured in
-    a HIP graph and replayed, so the inner loop costs one graph launch per step.
+  * the round's steady-state steps (gather+normalise -> fwd -> fused CE -> bwd -> fused SGD, once
+    per local step) are captured as ONE HIP graph and replayed, so a round costs one graph launch.
 """
 from __future__ import annotations
 
@@ -45,38 +45,40 @@ class LocalTrainer:
             self.opt.select(g0, g1).step()
         return loss
 
-    # ---------------------------------------------------------------- graph-captured step
-    def _graph_step(self, idx_host_row: torch.Tensor, G: int):
-        key = (G, self.B)
+    # ---------------------------------------------------------------- graph-captured round
+    def _graph_run(self, plan_dev: torch.Tensor, nsteps: int, G: int):
+        """Steps 0 .. nsteps-1 of the round's plan [steps, G, B] as ONE graph replay: the whole
+        sequence of local SGD steps is captured once (every step's batch launch reads its own row
+        of a static plan buffer), so a round costs one plan copy and one graph launch."""
+        key = (G, self.B, nsteps)
         ent = self._graphs.get(key)
         if ent is None:
-            ent = self._capture(idx_host_row, G)
+            ent = self._capture(plan_dev, nsteps, G)
             self._graphs[key] = ent
-        graph, static_idx, loss = ent
-        static_idx.copy_(idx_host_row, non_blocking=True)
-        graph.replay()
-        self.last_loss = loss
+        ent["plan"].copy_(plan_dev[:nsteps])
+        ent["graph"].replay()
+        self.last_loss = ent["loss"]
 
-    def _capture(self, idx_row: torch.Tensor, G: int):
+    def _capture(self, plan_dev: torch.Tensor, nsteps: int, G: int):
         st, opt = self.net.store, self.opt
         # the warm-up steps really train: snapshot and restore so the first graph step is exact
         snap = (st.data[:G].clone(), st.buffers[:G].clone(),
                 None if opt.mom is None else opt.mom[:G].clone(), opt.steps,
                 [c.clone() for c in self.net.rng_counters()])
-        static_idx = torch.empty(G, self.B, dtype=torch.int32, device=self.net.device)
-        static_idx.copy_(idx_row)
+        plan = plan_dev[:nsteps].clone()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            for _ in range(2):
-                self._step(static_idx, 0, G)
+            for i in range(2):
+                self._step(plan[i % nsteps], 0, G)
         torch.cuda.current_stream().wait_stream(s)
         # zero-initialised momentum == torch's "buffer = first grad" when dampening == 0, so the
         # frozen first_step=False inside the graph is exact for every step of a round
         assert opt.dampening == 0.0
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
-            loss = self._step(static_idx, 0, G)
+            for i in range(nsteps):
+                loss = self._step(plan[i], 0, G)
         st.data[:G].copy_(snap[0])
         st.buffers[:G].copy_(snap[1])
         if snap[2] is not None:
@@ -85,7 +87,7 @@ class LocalTrainer:
         for c, saved in zip(self.net.rng_counters(), snap[4]):
             c.copy_(saved)  # warm-up steps advanced the dropout counters: rewind them too
         st.sync_shadow()
-        return graph, static_idx, loss
+        return {"graph": graph, "plan": plan, "loss": loss}
 
     # ---------------------------------------------------------------- public
     def run(self, slot_indices: list[np.ndarray], seeds, epochs: int = 1, generators=None) -> int:
@@ -136,12 +138,16 @@ class LocalTrainer:
         plan_dev = torch.from_numpy(plan).to(dev, non_blocking=True)
         samples = 0
         G = g1 - g0
-        for s in range(steps):
+        s = 0
+        if self.use_graph and g0 == 0:
+            nfull = int(np.argmin(full)) if not full.all() else steps  # leading full steps
+            if nfull:
+                self._graph_run(plan_dev, nfull, G)
+                samples += nfull * G * self.B
+                s = nfull
+        for s in range(s, steps):
             if full[s]:
-                if self.use_graph and g0 == 0:
-                    self._graph_step(plan_dev[s], G)
-                else:
-                    self.last_loss = self._step(plan_dev[s], g0, g1)
+                self.last_loss = self._step(plan_dev[s], g0, g1)
                 samples += G * self.B
             else:
                 n = int((plan[s, 0] >= 0).sum())

@@ -81,7 +81,7 @@ _SIGS = {
     "ddl_bn_stats": [vp, vp, i64, i32, i32, vp],
     "ddl_bn_backward": [vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, vp],
     # nn_ops.hip
-    "ddl_prep_images": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
+    "ddl_prep_images": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp],
     "ddl_nchw_to_nhwc": [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
     "ddl_maxpool_fwd": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp],
     "ddl_maxpool_bwd": [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp],

@@ -705,8 +705,10 @@ def nchw_to_nhwc(x: torch.Tensor, cpad: int, im2col=0, pad: int = 0, stride: int
     return out
 
 
-def prep_images(src_u8, idx, mean, inv_std, cpad, im2col=0, pad=0, stride=1, out=None):
-    """Gather uint8 HWC samples by id, normalise, NHWC bf16 (channel-padded / stem-im2col)."""
+def prep_images(src_u8, idx, mean, inv_std, cpad, im2col=0, pad=0, stride=1, out=None,
+                labels=None, labels_out=None):
+    """Gather uint8 HWC samples by id, normalise, NHWC bf16 (channel-padded / stem-im2col).
+    labels / labels_out: also gather the int32 labels of the batch (same launch)."""
     k = _im2col_k(im2col)
     n = idx.numel()
     Hs, Ws, Cs = src_u8.shape[1:]
@@ -714,12 +716,19 @@ def prep_images(src_u8, idx, mean, inv_std, cpad, im2col=0, pad=0, stride=1, out
     if out is None:
         out = torch.empty(n, Ho, Wo, cpad, dtype=torch.bfloat16, device=src_u8.device)
     if not src_u8.is_cuda:
-        x = src_u8[idx.long().reshape(-1)].float() / 255.0
+        ids = idx.long().reshape(-1)
+        x = src_u8[ids].float() / 255.0
         x = (x - mean) * inv_std
         out.copy_(_im2col_cpu(x.permute(0, 3, 1, 2), k, pad, stride, cpad)[0].reshape(out.shape))
+        if labels is not None:
+            labels_out.copy_(labels[ids].reshape(labels_out.shape))
         return out
+    assert idx.dtype == torch.int32 and idx.is_contiguous()
+    assert labels is None or (labels.dtype == torch.int32 and labels_out.dtype == torch.int32
+                              and labels_out.numel() == n)
     check(_lib.kernels().ddl_prep_images(ptr(src_u8), ptr(idx), ptr(mean), ptr(inv_std), ptr(out),
-                                         n, Hs, Ws, Cs, cpad, k, pad, stride, stream()),
+                                         n, Hs, Ws, Cs, cpad, k, pad, stride, ptr(labels),
+                                         ptr(labels_out), stream()),
           "prep_images")
     return out
 

@@ -28,6 +28,8 @@ class DistContext:
     device: torch.device = field(default_factory=lambda: torch.device("cpu"))
     backend: str = "none"
     groups: dict = field(default_factory=dict)
+    ipc: object = None          # runtime.ipc.IpcAllReduce (peer-read all-reduce) when enabled
+    ipc_max_bytes: int = 0
 
     @property
     def is_distributed(self) -> bool:
@@ -40,7 +42,12 @@ class DistContext:
     # ------------------------------------------------------------- collectives (no-ops at world 1)
     def all_reduce(self, t: torch.Tensor, op=None, group=None):
         if self.is_distributed:
-            dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=group)
+            if (self.ipc is not None and group is None and op in (None, dist.ReduceOp.SUM)
+                    and t.dtype == torch.float32 and t.is_contiguous() and t.is_cuda
+                    and t.numel() * 4 <= self.ipc_max_bytes and t.data_ptr() % 16 == 0):
+                self.ipc.all_reduce(t)  # small message: one peer-read kernel over xGMI
+            else:
+                dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=group)
         return t
 
     def broadcast(self, t: torch.Tensor, src: int = 0, group=None):
@@ -130,6 +137,13 @@ def init(backend: str | None = None, device: str | None = None, rank: int | None
         dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
     _CTX = DistContext(rank, world, local, dev, backend if world > 1 else "none")
+    # peer-read all-reduce for small messages (runtime/ipc.py): one node, RCCL backend, opt-in
+    # until measured against RCCL on a multi-GPU node (benchmarks/bench_comm.py)
+    if (world > 1 and backend == "nccl" and os.environ.get("DDL_IPC_ALLREDUCE", "0") == "1"
+            and int(os.environ.get("LOCAL_WORLD_SIZE", world)) == world and world <= 8):
+        from .ipc import IpcAllReduce
+        _CTX.ipc_max_bytes = int(os.environ.get("DDL_IPC_MAX_BYTES", str(8 << 20)))
+        _CTX.ipc = IpcAllReduce(rank, world, dev, capacity=_CTX.ipc_max_bytes)
     return _CTX
 
 
@@ -139,6 +153,8 @@ def context() -> DistContext:
 
 def shutdown():
     global _CTX
+    if _CTX is not None and _CTX.ipc is not None:
+        _CTX.ipc.close()
     if dist.is_initialized():
         dist.destroy_process_group()
     _CTX = None

@@ -1,0 +1,72 @@
+"""Peer-read all-reduce over hipIPC-mapped uncached buffers (csrc/kernels/ipc_allreduce.hip).
+
+The test box has one GPU, so the ranks share it: every rank still maps every other rank's buffer
+through hipIpcOpenMemHandle from a different process and the kernels synchronise through the
+peers' signal words, exactly as on an 8-GPU node (where the loads cross xGMI instead)."""
+import os
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _worker(rank, world, port, out, sizes, two_shot_bytes):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from ddl25spring_amd.runtime.ipc import IpcAllReduce
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    ar = IpcAllReduce(rank, world, dev, capacity=max(sizes) * 4, two_shot_bytes=two_shot_bytes,
+                      nblocks=8, timeout_s=10.0)
+    res = {}
+    for rep in range(3):  # parity slots and the device epoch advance across calls
+        for n in sizes:
+            g = torch.Generator().manual_seed(1000 * rep + 7 * n + rank)
+            x = torch.randn(n, generator=g).to(dev)
+            ar.all_reduce(x)
+            res[(rep, n)] = x.cpu()
+    # graph-captured calls replay with the device-resident epoch
+    x = torch.full((4099,), float(rank + 1), device=dev)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ar.all_reduce(x)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        ar.all_reduce(x)
+    x.fill_(float(rank + 1))
+    dist.barrier()
+    graph.replay()
+    res["graph"] = x.cpu()
+    ar.check()
+    torch.save(res, os.path.join(out, f"r{rank}.pt"))
+    dist.barrier()
+    ar.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,two_shot_bytes", [(2, 1 << 30), (3, 1 << 30), (4, 256)],
+                         ids=["2ranks-oneshot", "3ranks-oneshot", "4ranks-twoshot"])
+def test_ipc_allreduce_matches_sum(cuda, world, two_shot_bytes):
+    sizes = [1, 5, 1000, 4099, 65536 + 3]
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, 29751 + world, d, sizes, two_shot_bytes), nprocs=world,
+                 join=True)
+        outs = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    for rep in range(3):
+        for n in sizes:
+            want = sum(torch.randn(n, generator=torch.Generator().manual_seed(1000 * rep + 7 * n + r))
+                       for r in range(world))
+            for r in range(world):
+                got = outs[r][(rep, n)]
+                assert torch.equal(got, outs[0][(rep, n)]), "ranks disagree"  # bit-identical
+                assert torch.allclose(got, want, rtol=1e-5, atol=1e-5)
+    tot = float(sum(range(1, world + 1)))
+    for r in range(world):
+        assert torch.equal(outs[r]["graph"], torch.full((4099,), tot))

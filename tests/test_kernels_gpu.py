@@ -323,6 +323,19 @@ def test_prep_images(cuda):
     _close(Fn.nchw_to_nhwc(x.to(cuda), 32, True, 0), Fn.nchw_to_nhwc(x, 32, True, 0))
 
 
+def test_prep_images_labels(cuda):
+    """The batch launch gathers the labels too (one launch per training-step batch)."""
+    src = torch.randint(0, 256, (300, 32, 32, 3), dtype=torch.uint8, device=cuda)
+    labels = torch.randint(0, 10, (300,), dtype=torch.int32, device=cuda)
+    mean = torch.tensor([0.4914, 0.4822, 0.4465], device=cuda)
+    inv = 1 / torch.tensor([0.247, 0.243, 0.261], device=cuda)
+    idx = torch.randint(0, 300, (3, 70), dtype=torch.int32, device=cuda)
+    y = torch.empty(3, 70, dtype=torch.int32, device=cuda)
+    a = Fn.prep_images(src, idx, mean, inv, 32, True, 1, labels=labels, labels_out=y)
+    assert torch.equal(a, Fn.prep_images(src, idx, mean, inv, 32, True, 1))
+    assert torch.equal(y, labels[idx.long()])
+
+
 @pytest.mark.parametrize("geom", [ConvGeom(G=2, N=3, H=8, W=8, C=64, K=96, R=3, S=3, stride=1, pad=1),
                                   ConvGeom(G=1, N=2, H=9, W=7, C=128, K=64, R=3, S=3, stride=2, pad=1)])
 def test_conv_dgrad_fused_bn_reduce(cuda, geom, monkeypatch):
