@@ -1,0 +1,97 @@
+"""Homework 2 (reference lab/homework-2.ipynb) — vertical FL experiments.
+
+  Ex1  feature partition by random permutation of the 30 encoded columns, seeds 42 / 43 / 44,
+       splits [7, 7, 7, 9] (exercise_1.py:117-135; published 86.76 / 92.16 / 83.82 %, L95-101)
+  Ex2  number of parties 2 / 4 / 6 / 8 with a balanced partition (exercise_2.py:111-139;
+       published 90.20 / 84.31 / 83.33 / 79.90 %, L302-314)
+  Ex3  VFL-VAE: 4 parties, client latent 8, server VAE latent 16, full batch, Adam 1e-3,
+       1000 epochs (exercise_3.py:161-203; published loss 114,117.9 -> 22,412.9 -> 13,898.3 at
+       epochs 1 / 500 / 1000, L531 / L1030 / L1530)
+
+Loss curves per run (the homework's Figure_1.png / Figure_2.png) and result tables.
+
+    python examples/homework_2.py --out lab_out/hw2 [--parts ex1,ex2,ex3] [--parity] [--quick]
+"""
+from __future__ import annotations
+
+import sys
+
+import pandas as pd
+import torch
+
+from _common import lineplot, outdir, parser, save_table
+from lab_2b_vfl import train_splitnn
+
+PUBLISHED_EX1 = {42: 86.76, 43: 92.16, 44: 83.82}
+PUBLISHED_EX2 = {2: 90.20, 4: 84.31, 6: 83.33, 8: 79.90}
+
+
+def vfl_vae(epochs: int, parties: int = 4, latent: int = 8, seed: int = 42):
+    from ddl25spring_amd.compat.exercise_3 import ClientDecoder, ClientEncoder, ServerVAE, VFLVAE, combined_loss
+    from ddl25spring_amd.data import heart as H
+    df, _ = H.load_heart()
+    torch.manual_seed(seed)
+    std = H.standard_frame(df)
+    parts = H.partition_balanced(list(std.columns), parties)
+    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    xs = [torch.tensor(std[p].values).float().to(dev) for p in parts]
+    m = VFLVAE([ClientEncoder(len(p), latent) for p in parts], ServerVAE(parties * latent, 48, 32, 16),
+               [ClientDecoder(latent, len(p)) for p in parts], latent).to(dev)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    losses = []
+    for _ in range(epochs):
+        opt.zero_grad()
+        rc, mu, lv, lat, rcat = m(xs)
+        loss = combined_loss(xs, rc, lat, rcat, mu, lv)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    return pd.DataFrame({"Epoch": range(1, epochs + 1), "Loss": losses})
+
+
+def main(argv=None):
+    ap = parser(__doc__)
+    ap.add_argument("--parts", default="ex1,ex2,ex3")
+    ap.add_argument("--parity", action="store_true")
+    a = ap.parse_args(argv)
+    out = outdir(a.out)
+    parts = set(a.parts.split(","))
+    epochs = 5 if a.quick else 300
+    res = {}
+    if "ex1" in parts:
+        rows, curves = [], []
+        for seed in (42, 43, 44):
+            curve, acc, loss = train_splitnn("random", 4, epochs, perm_seed=seed, parity=a.parity)
+            curve["Run"] = f"permutation seed {seed}"
+            curves.append(curve)
+            rows.append({"Seed": seed, "Test accuracy": 100 * acc, "Test loss": loss,
+                         "Published accuracy": PUBLISHED_EX1[seed]})
+        res["ex1"] = pd.DataFrame(rows)
+        print(res["ex1"].to_string(index=False))
+        save_table(res["ex1"], out, "ex1_permutations")
+        lineplot(pd.concat(curves), "Epoch", "Loss", "Run", out, "ex1_permutations", "Feature permutations")
+    if "ex2" in parts:
+        rows, curves = [], []
+        for n in (2, 4, 6, 8):
+            curve, acc, loss = train_splitnn("balanced", n, epochs, parity=a.parity)
+            curve["Run"] = f"{n} parties"
+            curves.append(curve)
+            rows.append({"Parties": n, "Test accuracy": 100 * acc, "Test loss": loss,
+                         "Published accuracy": PUBLISHED_EX2[n]})
+        res["ex2"] = pd.DataFrame(rows)
+        print(res["ex2"].to_string(index=False))
+        save_table(res["ex2"], out, "ex2_parties")
+        lineplot(pd.concat(curves), "Epoch", "Loss", "Run", out, "ex2_parties", "Number of parties")
+    if "ex3" in parts:
+        curve = vfl_vae(10 if a.quick else 1000)
+        curve["Run"] = "VFL-VAE"
+        res["ex3"] = curve
+        marks = curve[curve["Epoch"].isin([1, 500, 1000])]
+        print(marks.to_string(index=False), "(published 114117.9 / 22412.9 / 13898.3)")
+        save_table(curve, out, "ex3_vflvae_loss")
+        lineplot(curve, "Epoch", "Loss", "Run", out, "ex3_vflvae_loss", "VFL-VAE loss")
+    return res
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
