@@ -7,6 +7,7 @@ mkdir -p $out
 run() { local name=$1 secs=$2; shift 2; timeout -k 10 $secs "$@" > $out/$name.log 2>&1; local rc=$?; grep '^{' $out/$name.log; [ $rc -eq 0 ] || { echo "$name rc=$rc"; tail -5 $out/$name.log; exit $rc; }; }
 run headline8 300 python bench.py --steps 3 --warmup 1
 run headline1 300 python bench.py --clients 1 --train-size 6250 --steps 3 --warmup 1
+run mnist 300 python benchmarks/bench_mnist_fedavg.py --steps 20 --warmup 2
 run resnet50 300 python benchmarks/bench_resnet50_dp.py --steps 10 --warmup 3
 run llm 300 python benchmarks/bench_llm.py --steps 20 --warmup 3
 run vflgan 300 python benchmarks/bench_vfl_gan.py
