@@ -60,6 +60,50 @@ __global__ void prep_images_kernel(const uint8_t* __restrict__ src, const int* _
   }
 }
 
+// Fast path of the 32-channel stem im2col (CIFAR 3x3x3 = 27, MNIST 3x3x1 = 9 of 32 channels): one
+// thread per output pixel with 32-bit index math, the k x k x CS neighbourhood read once, and the
+// pixel's 64 B written as four 16-B stores. The generic kernel above decodes 64-bit indices and
+// re-gathers the neighbourhood per 8-channel chunk (ALU-bound: 57 us for the 8-client CIFAR
+// batch, ~1 TB/s of output).
+template <int K, int CS>
+__global__ __launch_bounds__(256) void prep_stem32_kernel(
+    const uint8_t* __restrict__ src, const int* __restrict__ idx, const float* __restrict__ mean,
+    const float* __restrict__ inv_std, bf16_t* __restrict__ out, int nimg, int Hs, int Ws, int Ho,
+    int Wo, int pad, int stride, const int* __restrict__ labels, int* __restrict__ labels_out) {
+  static_assert(K * K * CS <= 32, "stem im2col fits 32 channels");
+  const int hw = Ho * Wo;
+  const int pix = blockIdx.x * 256 + threadIdx.x;
+  if (pix >= nimg * hw) return;
+  const int b = pix / hw, r = pix - b * hw;
+  const int h = r / Wo, w = r - h * Wo;
+  const int id = idx[b];
+  if (labels && r == 0) labels_out[b] = labels[id];
+  const uint8_t* img = src + (long long)id * Hs * Ws * CS;
+  float m[CS], is[CS];
+#pragma unroll
+  for (int c = 0; c < CS; ++c) { m[c] = mean[c]; is[c] = inv_std[c]; }
+  float v[32];
+#pragma unroll
+  for (int j = 0; j < 32; ++j) v[j] = 0.f;
+#pragma unroll
+  for (int tr = 0; tr < K; ++tr) {
+    const int ih = h * stride - pad + tr;
+#pragma unroll
+    for (int ts = 0; ts < K; ++ts) {
+      const int iw = w * stride - pad + ts;
+      if ((unsigned)ih < (unsigned)Hs && (unsigned)iw < (unsigned)Ws) {
+        const uint8_t* px = img + (ih * Ws + iw) * CS;
+#pragma unroll
+        for (int c = 0; c < CS; ++c)
+          v[(tr * K + ts) * CS + c] = ((float)px[c] * (1.f / 255.f) - m[c]) * is[c];
+      }
+    }
+  }
+  i4v* o = (i4v*)(out + (long long)pix * 32);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) o[q] = pack8(v + 8 * q);
+}
+
 DDL_API int ddl_prep_images(const void* src, const int* idx, const float* mean, const float* inv_std,
                             void* out, int nimg, int Hs, int Ws, int Cs, int Cout, int im2col,
                             int pad, int stride, const int* labels, int* labels_out, hipStream_t s) {
@@ -68,6 +112,17 @@ DDL_API int ddl_prep_images(const void* src, const int* idx, const float* mean, 
   if ((labels == nullptr) != (labels_out == nullptr)) return (int)hipErrorInvalidValue;
   const int Ho = im2col ? (Hs + 2 * pad - im2col) / stride + 1 : Hs;
   const int Wo = im2col ? (Ws + 2 * pad - im2col) / stride + 1 : Ws;
+  const long long pixels = (long long)nimg * Ho * Wo;
+  if (Cout == 32 && im2col == 3 && (Cs == 3 || Cs == 1) && pixels < (1LL << 31) - 256) {
+    const dim3 grid((unsigned)((pixels + 255) / 256));
+    if (Cs == 3)
+      hipLaunchKernelGGL((prep_stem32_kernel<3, 3>), grid, dim3(256), 0, s, (const uint8_t*)src, idx,
+                         mean, inv_std, (bf16_t*)out, nimg, Hs, Ws, Ho, Wo, pad, stride, labels, labels_out);
+    else
+      hipLaunchKernelGGL((prep_stem32_kernel<3, 1>), grid, dim3(256), 0, s, (const uint8_t*)src, idx,
+                         mean, inv_std, (bf16_t*)out, nimg, Hs, Ws, Ho, Wo, pad, stride, labels, labels_out);
+    return (int)hipGetLastError();
+  }
   const long long total = (long long)nimg * Ho * Wo * (Cout / 8);
   hipLaunchKernelGGL(prep_images_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s,
                      (const uint8_t*)src, idx, mean, inv_std, (bf16_t*)out, nimg, Hs, Ws, Cs, Ho, Wo,

@@ -321,6 +321,14 @@ def test_prep_images(cuda):
         _close(a, b, rel=1e-2)
     x = torch.randn(4, 1, 28, 28)
     _close(Fn.nchw_to_nhwc(x.to(cuda), 32, True, 0), Fn.nchw_to_nhwc(x, 32, True, 0))
+    # the 32-channel stem fast path (CIFAR 3x3x3, MNIST 3x3x1) == the generic kernel (cpad 40)
+    for shape, m, s, pad in (((50, 32, 32, 3), mean, inv, 1), ((50, 28, 28, 1), mean[:1], inv[:1], 0)):
+        src = torch.randint(0, 256, shape, dtype=torch.uint8)
+        args = (src.to(cuda), idx.to(cuda), m.to(cuda), s.to(cuda))
+        fast = Fn.prep_images(*args, 32, True, pad)
+        generic = Fn.prep_images(*args, 40, True, pad)
+        assert torch.equal(fast, generic[..., :32].contiguous())
+        _close(fast, Fn.prep_images(src, idx, m, s, 32, True, pad), rel=1e-2)
 
 
 def test_prep_images_labels(cuda):
