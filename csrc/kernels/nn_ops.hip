@@ -289,6 +289,88 @@ __global__ void avgpool_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __rest
     *(i4v*)(dx + t * 8) = pack8(v);
   }
 }
+// Global-average-pool backward fused with the backward reduce of the BatchNorm that produced the
+// pooled input (a ResNet's last block: x = relu(bn(c) + shortcut)): dx = dy / HW masked by
+// (x > 0), written once, and per channel s0 = sum dx, s1 = sum dx * (c - mean) * rstd added into
+// stripe (blockIdx.x % 32) of part [G][32][2C] — the reduce pass of that BN's backward, which
+// then runs fold + apply only (the block's bn_backward(part=...)). Layout as the BN passes: a
+// 256-thread block covers RPI = 256 / (C/8) pixel rows, each thread one fixed 8-channel chunk.
+__global__ __launch_bounds__(256) void avgpool_bwd_bn_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ c,
+    const float* __restrict__ mean, const float* __restrict__ rstd, bf16_t* __restrict__ dx,
+    float* __restrict__ part, int N, int HW, int C) {
+  __shared__ float red[256 * 17];
+  const int g = blockIdx.y;
+  const int TPR = C / 8, RPI = 256 / TPR;
+  const int tid = threadIdx.x, cc = tid % TPR, row = tid / TPR;
+  const long long M = (long long)N * HW;
+  float s0[8], s1[8], m8[8], r8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s0[k] = s1[k] = 0.f;
+  const float* mg = mean + (long long)g * C + cc * 8;
+  const float* rg = rstd + (long long)g * C + cc * 8;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { m8[k] = mg[k]; r8[k] = rg[k]; }
+  const float inv = 1.f / HW;
+  if (row < RPI) {
+    for (long long p = (long long)blockIdx.x * RPI + row; p < M; p += (long long)gridDim.x * RPI) {
+      const long long e = ((long long)g * M + p) * C + cc * 8;
+      const long long n = p / HW;
+      float d[8], xv[8], cv[8];
+      unpack8(*(const i4v*)(dy + ((long long)g * N + n) * C + cc * 8), d);
+      unpack8(*(const i4v*)(x + e), xv);
+      unpack8(*(const i4v*)(c + e), cv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        d[k] = xv[k] > 0.f ? d[k] * inv : 0.f;
+        s0[k] += d[k];
+        s1[k] += d[k] * (cv[k] - m8[k]) * r8[k];
+      }
+      *(i4v*)(dx + e) = pack8(d);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    red[tid * 17 + k] = s0[k];
+    red[tid * 17 + 8 + k] = s1[k];
+  }
+  __syncthreads();
+  int top = 1;
+  while (top < RPI) top <<= 1;
+  for (int half = top >> 1; half > 0; half >>= 1) {
+    if (row < half && row + half < RPI) {
+      const float* o = red + (tid + half * TPR) * 17;
+      float* m = red + tid * 17;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) m[k] += o[k];
+    }
+    __syncthreads();
+  }
+  if (row == 0) {
+    float* pg = part + ((long long)g * 32 + blockIdx.x % 32) * 2 * C;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      atomicAdd(pg + cc * 8 + k, red[tid * 17 + k]);
+      atomicAdd(pg + C + cc * 8 + k, red[tid * 17 + 8 + k]);
+    }
+  }
+}
+
+// dy [G][N][C], x / c / dx [G][N][HW][C] bf16, mean / rstd [G][C], part zeroed [G][32][2C]
+DDL_API int ddl_avgpool_bwd_bn(const void* dy, const void* x, const void* c, const float* mean,
+                               const float* rstd, void* dx, float* part, int G, int N, int HW, int C,
+                               hipStream_t s) {
+  if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
+  const int RPI = 256 / (C / 8);
+  long long want = ((long long)N * HW + RPI * 4 - 1) / (RPI * 4);
+  long long cap = (2048 + G - 1) / G;
+  if (want > cap) want = cap;
+  hipLaunchKernelGGL(avgpool_bwd_bn_kernel, dim3((unsigned)(want < 1 ? 1 : want), G), dim3(256), 0, s,
+                     (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)c, mean, rstd, (bf16_t*)dx,
+                     part, N, HW, C);
+  return (int)hipGetLastError();
+}
+
 DDL_API int ddl_avgpool_fwd(const void* x, void* y, int NB, int HW, int C, hipStream_t s) {
   if (C % 8) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(grid_for((long long)NB * C / 8, 256)), dim3(256), 0,

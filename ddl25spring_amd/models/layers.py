@@ -237,10 +237,13 @@ class GlobalAvgPool(Layer):
     name = "avgpool"
 
     def forward(self, x, train):
-        return Fn.avgpool_fwd(x), (x.shape[2], x.shape[3])
+        return Fn.avgpool_fwd(x), (x.shape[2], x.shape[3], x)
 
-    def backward(self, dy, hw):
-        return Fn.avgpool_bwd(dy, *hw)
+    def backward(self, dy, ctx, fuse=None):
+        H, W, x = ctx
+        if fuse is not None:  # the producer's output ReLU mask + BN backward reduce (Net fusion)
+            return Fn.avgpool_bwd_bn(dy, x, fuse)
+        return Fn.avgpool_bwd(dy, H, W)
 
 
 class Flatten(Layer):

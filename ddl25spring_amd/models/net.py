@@ -50,6 +50,13 @@ class Net:
                     and os.environ.get("DDL_FUSE_BN_BWD", "1") != "0":
                 cur.fuse_out_bn = True
                 prev.accepts_part = True
+            # a global average pool after such a block: the pool's backward applies the mask and
+            # reduces the block's output BN (one pass instead of pool-bwd + BN reduce)
+            if cur.name == "avgpool" and type(prev).bn_out is not Layer.bn_out \
+                    and getattr(prev, "residual_out", False) and prev.out_act == RELU \
+                    and os.environ.get("DDL_FUSE_BN_BWD", "1") != "0":
+                cur.fuse_out_bn = True
+                prev.accepts_part = True
         if self.layers:
             self.layers[0].needs_input_grad = False
 

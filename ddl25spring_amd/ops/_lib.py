@@ -89,6 +89,7 @@ _SIGS = {
     "ddl_maxpool2_bwd": [vp, vp, vp, i32, i32, i32, i32, vp],
     "ddl_avgpool_fwd": [vp, vp, i32, i32, i32, vp],
     "ddl_avgpool_bwd": [vp, vp, i32, i32, i32, vp],
+    "ddl_avgpool_bwd_bn": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp],
     "ddl_dropout": [vp, vp, i64, f32, u64, u64, vp, vp],
     "ddl_u64_add": [vp, u64, vp],
     "ddl_act_fwd": [vp, vp, i64, i32, f32, vp],

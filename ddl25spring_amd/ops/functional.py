@@ -604,6 +604,29 @@ def avgpool_bwd(dy, H, W):
     return dx
 
 
+def avgpool_bwd_bn(dy, x, bn):
+    """Global-average-pool backward for a pooled input x = relu(BN(c) [+ r]) fused with that BN's
+    backward reduce: -> (dx = dy/HW * (x > 0), part [G, BN_STRIPES, 2, C] with (sum dx,
+    sum dx * (c - mean) * rstd)) for ``bn_backward(..., part=part)``. bn = (c, mean, rstd)."""
+    c, mean, rstd = bn
+    G, N, H, W, C = x.shape
+    if not dy.is_cuda:
+        d = dy.float().reshape(G, N, 1, 1, C) / (H * W) * (x.float() > 0)
+        dx = d.to(dy.dtype).contiguous()
+        xh = (c.float() - mean.reshape(G, 1, 1, 1, C)) * rstd.reshape(G, 1, 1, 1, C)
+        part = torch.zeros(G, BN_STRIPES, 2, C)
+        df = dx.float()
+        part[:, 0, 0] = df.reshape(G, -1, C).sum(1)
+        part[:, 0, 1] = (df * xh).reshape(G, -1, C).sum(1)
+        return dx, part
+    assert x.is_contiguous() and c.is_contiguous() and dy.is_contiguous()
+    dx = torch.empty_like(x)
+    part = ws.zeros((G, BN_STRIPES, 2, C), x.device)
+    check(_lib.kernels().ddl_avgpool_bwd_bn(ptr(dy), ptr(x), ptr(c), ptr(mean), ptr(rstd), ptr(dx),
+                                            ptr(part), G, N, H * W, C, stream()), "avgpool_bwd_bn")
+    return dx, part
+
+
 def dropout(x, p, seed, offset, offset_dev=None):
     """Philox dropout; the counter base is ``offset`` (+ the int64 device scalar ``offset_dev``)."""
     if p <= 0:
