@@ -329,6 +329,13 @@ def test_prep_images(cuda):
         generic = Fn.prep_images(*args, 40, True, pad)
         assert torch.equal(fast, generic[..., :32].contiguous())
         _close(fast, Fn.prep_images(src, idx, m, s, 32, True, pad), rel=1e-2)
+    # the ImageNet 7x7 / stride-2 stem (147 of 160 channels) on its fast path == the generic (168)
+    src = torch.randint(0, 256, (6, 37, 41, 3), dtype=torch.uint8)
+    args = (src.to(cuda), idx.to(cuda) % 6, mean.to(cuda), inv.to(cuda))
+    fast = Fn.prep_images(*args, 160, 7, 3, 2)
+    generic = Fn.prep_images(*args, 168, 7, 3, 2)
+    assert torch.equal(fast, generic[..., :160].contiguous())
+    _close(fast, Fn.prep_images(src, idx % 6, mean, inv, 160, 7, 3, 2), rel=1e-2)
 
 
 def test_prep_images_labels(cuda):
