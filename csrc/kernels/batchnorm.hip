@@ -73,8 +73,7 @@ __device__ __forceinline__ void stripe_fold(const float* __restrict__ base, int 
   }
 }
 
-__global__ __launch_bounds__(256) void bn_finalize_kernel(BNArgs a) {
-  __shared__ float red[8 * 64];
+__device__ __forceinline__ void bn_finalize_body(const BNArgs& a, float* red) {
   const int g = blockIdx.y, c = blockIdx.x * 32 + (threadIdx.x & 31);
   const bool valid = c < a.C;
   const bool lead = (threadIdx.x >> 5) == 0 && valid;
@@ -113,9 +112,28 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(BNArgs a) {
   a.rstd[i] = rs;
 }
 
+__global__ __launch_bounds__(256) void bn_finalize_kernel(BNArgs a) {
+  __shared__ float red[8 * 64];
+  bn_finalize_body(a, red);
+}
+
+// Two independent BatchNorms in one launch (blockIdx.z): a residual block's output BN and its
+// projected shortcut's BN, whose statistics are both complete once the two convs have run.
+__global__ __launch_bounds__(256) void bn_finalize2_kernel(BNArgs a, BNArgs b) {
+  __shared__ float red[8 * 64];
+  bn_finalize_body(blockIdx.z ? b : a, red);
+}
+
 DDL_API int ddl_bn_finalize(const BNArgs* a, hipStream_t s) {
   if (a->stripes > BN_NSTRIPE) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((a->C + 31) / 32, a->G), dim3(256), 0, s, *a);
+  return (int)hipGetLastError();
+}
+
+DDL_API int ddl_bn_finalize2(const BNArgs* a, const BNArgs* b, hipStream_t s) {
+  if (a->stripes > BN_NSTRIPE || b->stripes > BN_NSTRIPE || a->G != b->G) return (int)hipErrorInvalidValue;
+  const int C = a->C > b->C ? a->C : b->C;
+  hipLaunchKernelGGL(bn_finalize2_kernel, dim3((C + 31) / 32, a->G, 2), dim3(256), 0, s, *a, *b);
   return (int)hipGetLastError();
 }
 
@@ -449,11 +467,10 @@ DDL_API int ddl_bn_stats(const void* x, float* stats, long long M, int C, int G,
 // ---------------------------------------------------------------------------------------------
 // Whole BN backward in three launches: striped reduce -> per-channel fold (d(beta) += s0,
 // d(gamma) += s1, dx coefficients) -> one apply pass.
-__global__ __launch_bounds__(256) void bn_fold_coef_kernel(
+__device__ __forceinline__ void bn_fold_coef_body(
     const float* __restrict__ part, float* __restrict__ dgamma, float* __restrict__ dbeta,
     long long gs_param, const float* __restrict__ mean, const float* __restrict__ rstd,
-    const float* __restrict__ gamma, float* __restrict__ coef, long long M, int C, int G) {
-  __shared__ float red[8 * 64];
+    const float* __restrict__ gamma, float* __restrict__ coef, long long M, int C, float* red) {
   const int g = blockIdx.y, c = blockIdx.x * 32 + (threadIdx.x & 31);
   const bool valid = c < C;
   const bool lead = (threadIdx.x >> 5) == 0 && valid;
@@ -474,6 +491,106 @@ __global__ __launch_bounds__(256) void bn_fold_coef_kernel(
   coef[(long long)g * 3 * C + c] = A;
   coef[(long long)g * 3 * C + C + c] = B;
   coef[(long long)g * 3 * C + 2 * C + c] = -A * s0 * invM - B * mu;
+}
+
+__global__ __launch_bounds__(256) void bn_fold_coef_kernel(
+    const float* __restrict__ part, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    long long gs_param, const float* __restrict__ mean, const float* __restrict__ rstd,
+    const float* __restrict__ gamma, float* __restrict__ coef, long long M, int C, int G) {
+  __shared__ float red[8 * 64];
+  bn_fold_coef_body(part, dgamma, dbeta, gs_param, mean, rstd, gamma, coef, M, C, red);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Two BatchNorm backwards that share their (already masked) input gradient dy: a residual block's
+// output BN and its projected shortcut's BN, both fed by the block's output gradient. One fold
+// launch (blockIdx.z) and one apply pass that reads dy once and writes both input gradients.
+struct BNBwdArgs {
+  const void* x;         // BN input [G][M][C] bf16
+  const float* mean;     // [G][C]
+  const float* rstd;
+  const float* gamma;    // [G][C] (group stride gs_param), nullable
+  float* dgamma;         // nullable
+  float* dbeta;
+  const float* part;     // complete striped reduce sums [G][BN_NSTRIPE][2C]
+  float* coef;           // [G][3C] scratch
+  void* dx;              // [G][M][C] bf16 output
+  long long gs_param;
+};
+
+__global__ __launch_bounds__(256) void bn_fold_coef2_kernel(BNBwdArgs a, BNBwdArgs b, long long M, int C) {
+  __shared__ float red[8 * 64];
+  const BNBwdArgs& t = blockIdx.z ? b : a;
+  bn_fold_coef_body(t.part, t.dgamma, t.dbeta, t.gs_param, t.mean, t.rstd, t.gamma, t.coef, M, C, red);
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply2_kernel(const bf16_t* __restrict__ dy, BNBwdArgs a,
+                                                            BNBwdArgs b, long long M, int C) {
+  const int g = blockIdx.y;
+  const int TPR = C >> 3, RPI = 256 / TPR;
+  const int cc = threadIdx.x % TPR, row = threadIdx.x / TPR;
+  if (row >= RPI) return;
+  float Aa[8], Ba[8], Ca[8], Ab[8], Bb[8], Cb[8];
+  const float* ca = a.coef + (long long)g * 3 * C + cc * 8;
+  const float* cb = b.coef + (long long)g * 3 * C + cc * 8;
+  load8f(ca, Aa); load8f(ca + C, Ba); load8f(ca + 2 * C, Ca);
+  load8f(cb, Ab); load8f(cb + C, Bb); load8f(cb + 2 * C, Cb);
+  const bf16_t* __restrict__ xa = (const bf16_t*)a.x;
+  const bf16_t* __restrict__ xb = (const bf16_t*)b.x;
+  bf16_t* __restrict__ dxa = (bf16_t*)a.dx;
+  bf16_t* __restrict__ dxb = (bf16_t*)b.dx;
+  const long long base = (long long)g * M * C + cc * 8;
+  constexpr int RB = 4;
+  const long long stride = (long long)gridDim.x * RPI;
+  for (long long p0 = (long long)blockIdx.x * RPI + row; p0 < M; p0 += stride * RB) {
+    i4v dv[RB], av[RB], bv[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const long long p = p0 + r * stride;
+      const long long e = base + (p < M ? p : p0) * C;
+      dv[r] = *(const i4v*)(dy + e);
+      av[r] = *(const i4v*)(xa + e);
+      bv[r] = *(const i4v*)(xb + e);
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const long long p = p0 + r * stride;
+      if (p >= M) break;
+      const long long e = base + p * C;
+      float d[8], xf[8], o[8];
+      unpack8(dv[r], d);
+      unpack8(av[r], xf);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = Aa[k] * d[k] + Ba[k] * xf[k] + Ca[k];
+      *(i4v*)(dxa + e) = pack8(o);
+      unpack8(bv[r], xf);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = Ab[k] * d[k] + Bb[k] * xf[k] + Cb[k];
+      *(i4v*)(dxb + e) = pack8(o);
+    }
+  }
+}
+
+DDL_API int ddl_bn_bwd_args_size() { return (int)sizeof(BNBwdArgs); }
+
+DDL_API int ddl_bn_backward2(const void* dy, const BNBwdArgs* a, const BNBwdArgs* b, long long M, int C,
+                             int G, hipStream_t s) {
+  if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_fold_coef2_kernel, dim3((C + 31) / 32, G, 2), dim3(256), 0, s, *a, *b, M, C);
+  const int RPI = 256 / (C / 8);
+  hipLaunchKernelGGL(bn_bwd_apply2_kernel, dim3(stream_blocks(M, RPI, G, 4), G), dim3(256), 0, s,
+                     (const bf16_t*)dy, *a, *b, M, C);
+  return (int)hipGetLastError();
+}
+
+// striped reduce sums only (part zeroed [G][BN_NSTRIPE][2C]): s0 = sum dy_m, s1 = sum dy_m * xhat
+DDL_API int ddl_bn_bwd_reduce_part(const void* dy, const void* ymask, const void* x, const float* mean,
+                                   const float* rstd, float* part, long long M, int C, int G, hipStream_t s) {
+  if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
+  const int RPI = 256 / (C / 8);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(stream_blocks(M, RPI, G, 16), G), dim3(256), 0, s,
+                     (const bf16_t*)dy, (const bf16_t*)ymask, (const bf16_t*)x, mean, rstd, part, M, C);
+  return (int)hipGetLastError();
 }
 
 // part: zeroed [G][BN_NSTRIPE][2C]; coef: [G][3C] scratch

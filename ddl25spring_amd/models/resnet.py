@@ -28,16 +28,25 @@ class _BNConv(ConvUnit):
     def __init__(self, cin, cout, k, stride, pad):
         super().__init__(cin, cout, k=k, stride=stride, pad=pad, bias=False, bn=True, act=None)
 
-    def conv_stats(self, x, train):
-        st = self.store
+    def conv_raw(self, x, train):
+        """The conv with its BN-statistics epilogue -> (c, stats | None, geom)."""
         g = self.geom(x)
         stats = Fn.stats_buffer(g.G, self.cout, x.device) if train else None
-        c = Fn.conv_fwd(x, st.shadow_of(self.w), g, stats=stats)
+        return Fn.conv_fwd(x, self.store.shadow_of(self.w), g, stats=stats), stats, g
+
+    def bn_inputs(self, stats, g):
+        st = self.store
+        return (stats, st.param(self.gamma), st.param(self.beta), st.buffer(self.rm),
+                st.buffer(self.rv), g.N * g.P * g.Q)
+
+    def finalize(self, stats, g, train):
         if not train:
-            stats = ws.zeros((g.G, 2, self.cout), x.device)
-        sc, sh, mu, rs = Fn.bn_finalize(stats, st.param(self.gamma), st.param(self.beta),
-                                        st.buffer(self.rm), st.buffer(self.rv), g.N * g.P * g.Q,
-                                        self.eps, self.momentum, training=train)
+            stats = ws.zeros((g.G, 2, self.cout), self.store.data.device)
+        return Fn.bn_finalize(*self.bn_inputs(stats, g), self.eps, self.momentum, training=train)
+
+    def conv_stats(self, x, train):
+        c, stats, g = self.conv_raw(x, train)
+        sc, sh, mu, rs = self.finalize(stats, g, train)
         return c, sc, sh, mu, rs, g
 
     def bn_backward(self, dy, ymask, c, mu, rs, emit_dym=False, part=None):
@@ -45,17 +54,43 @@ class _BNConv(ConvUnit):
         return Fn.bn_backward(dy, ymask, c, mu, rs, st.param(self.gamma), st.grad_of(self.gamma),
                               st.grad_of(self.beta), emit_dym=emit_dym, part=part)
 
+    def bn_bwd_inputs(self, c, mu, rs, part):
+        st = self.store
+        return (c, mu, rs, st.param(self.gamma), st.grad_of(self.gamma), st.grad_of(self.beta), part)
+
+
+def _conv_pair_bn(main: _BNConv, y, down: _BNConv, x, train):
+    """A block's last conv (on y) and its projection shortcut (on the block input x) with both
+    BatchNorms finalized in one launch -> (c, bn, g), (cs, bn_s, gs); bn = (scale, shift, mean, rstd)."""
+    c, st, g = main.conv_raw(y, train)
+    cs, sts, gs = down.conv_raw(x, train)
+    if train:
+        bn, bns = Fn.bn_finalize2(main.bn_inputs(st, g), down.bn_inputs(sts, gs), main.eps, main.momentum)
+    else:
+        bn, bns = main.finalize(st, g, train), down.finalize(sts, gs, train)
+    return (c, bn, g), (cs, bns, gs)
+
 
 class _ShortcutGrad:
-    def _shortcut_backward(self, dym, dctx, x):
-        """Projection shortcut backward: its BN, then its conv's WGRAD and (if the block input needs a
-        gradient) DGRAD. A 1x1 / stride-2 shortcut's input gradient is nonzero only on the (2i, 2j)
-        pixels, so its DGRAD runs as a dense 1x1 conv on the compact grid and the block's first
-        DGRAD adds it there (residual_sub = 2) instead of materialising 3/4 zeros.
-        -> (residual for the first conv's DGRAD, residual_sub)."""
+    def _out_and_shortcut_bn_backward(self, main: _BNConv, dout, c, mu, rs, part, dctx):
+        """The block's output BN and its shortcut's BN both take the (masked) block output gradient:
+        the shortcut's reduce, then ONE fold launch and ONE apply pass for both (bn_backward2).
+        -> (d main conv output, d shortcut conv output)."""
+        cs, mus, rss, gs = dctx
+        part_s = Fn.bn_bwd_reduce_part(dout, None, cs, mus, rss)
+        return Fn.bn_backward2(dout, main.bn_bwd_inputs(c, mu, rs, part),
+                               self.down.bn_bwd_inputs(cs, mus, rss, part_s))
+
+    def _shortcut_backward(self, dym, dctx, x, dcs=None):
+        """Projection shortcut backward: its BN (unless ``dcs`` is given), then its conv's WGRAD
+        and (if the block input needs a gradient) DGRAD. A 1x1 / stride-2 shortcut's input
+        gradient is nonzero only on the (2i, 2j) pixels, so its DGRAD runs as a dense 1x1 conv on
+        the compact grid and the block's first DGRAD adds it there (residual_sub = 2) instead of
+        materialising 3/4 zeros. -> (residual for the first conv's DGRAD, residual_sub)."""
         cs, mus, rss, gs = dctx
         st = self.store
-        dcs = self.down.bn_backward(dym, None, cs, mus, rss)
+        if dcs is None:
+            dcs = self.down.bn_backward(dym, None, cs, mus, rss)
         sub = gs.stride == 2 and gs.R == 1 and gs.S == 1 and gs.pad == 0
         dgeom = Fn.ConvGeom(gs.G, gs.N, gs.P, gs.Q, gs.C, gs.K, 1, 1, 1, 0) if sub else None
         dres = Fn.conv_dgrad_wgrad(dcs, st.shadow_of(self.down.w), x, gs, st.grad_of(self.down.w),
@@ -94,12 +129,13 @@ class BasicBlock(_ShortcutGrad, Layer):
     def forward(self, x, train):
         c1, sc1, sh1, mu1, rs1, g1 = self.conv1.conv_stats(x, train)
         a1 = Fn.bn_apply(c1, sc1, sh1, act=RELU)
-        c2, sc2, sh2, mu2, rs2, g2 = self.conv2.conv_stats(a1, train)
         if self.down is not None:
-            cs, scs, shs, mus, rss, gs = self.down.conv_stats(x, train)
+            (c2, (sc2, sh2, mu2, rs2), g2), (cs, (scs, shs, mus, rss), gs) = \
+                _conv_pair_bn(self.conv2, a1, self.down, x, train)
             out = Fn.bn_apply(c2, sc2, sh2, r=cs, rscale=scs, rshift=shs, act=RELU)
             dctx = (cs, mus, rss, gs)
         else:
+            c2, sc2, sh2, mu2, rs2, g2 = self.conv2.conv_stats(a1, train)
             out = Fn.bn_apply(c2, sc2, sh2, r=x, act=RELU)
             dctx = None
         return out, (x, c1, a1, sc1, sh1, mu1, rs1, g1, c2, mu2, rs2, g2, out, dctx)
@@ -110,12 +146,16 @@ class BasicBlock(_ShortcutGrad, Layer):
     def backward(self, dout, ctx, part=None, fuse=None):
         x, c1, a1, sc1, sh1, mu1, rs1, g1, c2, mu2, rs2, g2, out, dctx = ctx
         st = self.store
-        if part is not None:  # dout arrives masked by (out > 0) with bn2's reduce sums
+        dcs = None
+        if part is not None and dctx is not None:  # output + shortcut BN backwards together
+            (dc2, dcs), dym = self._out_and_shortcut_bn_backward(self.conv2, dout, c2, mu2, rs2, part,
+                                                                 dctx), dout
+        elif part is not None:  # dout arrives masked by (out > 0) with bn2's reduce sums
             dc2, dym = self.conv2.bn_backward(dout, None, c2, mu2, rs2, part=part), dout
         else:
             dc2, dym = self.conv2.bn_backward(dout, out, c2, mu2, rs2, emit_dym=True)
         # every conv's DGRAD and WGRAD read the same dY: one (possibly paired) launch each
-        dres, rsub = self._shortcut_backward(dym, dctx, x) if dctx is not None else (dym, 1)
+        dres, rsub = self._shortcut_backward(dym, dctx, x, dcs) if dctx is not None else (dym, 1)
         # dgrad epilogue applies bn1's ReLU mask (recomputed from c1: no read of a1) and reduces
         # bn1's backward sums (no reduce pass)
         da1, part1 = Fn.conv_dgrad_wgrad(dc2, st.shadow_of(self.conv2.w), a1, g2, st.grad_of(self.conv2.w),
@@ -174,12 +214,13 @@ class Bottleneck(_ShortcutGrad, Layer):
         a1 = Fn.bn_apply(c1, sc1, sh1, act=RELU)
         c2, sc2, sh2, mu2, rs2, g2 = self.conv2.conv_stats(a1, train)
         a2 = Fn.bn_apply(c2, sc2, sh2, act=RELU)
-        c3, sc3, sh3, mu3, rs3, g3 = self.conv3.conv_stats(a2, train)
         if self.down is not None:
-            cs, scs, shs, mus, rss, gs = self.down.conv_stats(x, train)
+            (c3, (sc3, sh3, mu3, rs3), g3), (cs, (scs, shs, mus, rss), gs) = \
+                _conv_pair_bn(self.conv3, a2, self.down, x, train)
             out = Fn.bn_apply(c3, sc3, sh3, r=cs, rscale=scs, rshift=shs, act=RELU)
             dctx = (cs, mus, rss, gs)
         else:
+            c3, sc3, sh3, mu3, rs3, g3 = self.conv3.conv_stats(a2, train)
             out = Fn.bn_apply(c3, sc3, sh3, r=x, act=RELU)
             dctx = None
         return out, (x, (c1, a1, sc1, sh1, mu1, rs1, g1), (c2, a2, sc2, sh2, mu2, rs2, g2),
@@ -191,11 +232,15 @@ class Bottleneck(_ShortcutGrad, Layer):
     def backward(self, dout, ctx, part=None, fuse=None):
         x, (c1, a1, sc1, sh1, mu1, rs1, g1), (c2, a2, sc2, sh2, mu2, rs2, g2), (c3, mu3, rs3, g3), out, dctx = ctx
         st = self.store
-        if part is not None:  # dout arrives masked by (out > 0) with bn3's reduce sums
+        dcs = None
+        if part is not None and dctx is not None:  # output + shortcut BN backwards together
+            (dc3, dcs), dym = self._out_and_shortcut_bn_backward(self.conv3, dout, c3, mu3, rs3, part,
+                                                                 dctx), dout
+        elif part is not None:  # dout arrives masked by (out > 0) with bn3's reduce sums
             dc3, dym = self.conv3.bn_backward(dout, None, c3, mu3, rs3, part=part), dout
         else:
             dc3, dym = self.conv3.bn_backward(dout, out, c3, mu3, rs3, emit_dym=True)
-        dres, rsub = self._shortcut_backward(dym, dctx, x) if dctx is not None else (dym, 1)
+        dres, rsub = self._shortcut_backward(dym, dctx, x, dcs) if dctx is not None else (dym, 1)
         da2, part2 = Fn.conv_dgrad_wgrad(dc3, st.shadow_of(self.conv3.w), a2, g3, st.grad_of(self.conv3.w),
                                          bn=(c2, mu2, rs2), mask_bn=(sc2, sh2))
         dc2 = self.conv2.bn_backward(da2, None, c2, mu2, rs2, part=part2)

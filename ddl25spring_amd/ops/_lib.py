@@ -53,6 +53,11 @@ class BNArgs(ctypes.Structure):
                 ("eps", f32), ("momentum", f32), ("training", i32), ("stripes", i32)]
 
 
+class BNBwdArgs(ctypes.Structure):
+    _fields_ = [("x", vp), ("mean", vp), ("rstd", vp), ("gamma", vp), ("dgamma", vp), ("dbeta", vp),
+                ("part", vp), ("coef", vp), ("dx", vp), ("gs_param", i64)]
+
+
 class SGDArgs(ctypes.Structure):
     _fields_ = [("p", vp), ("g", vp), ("mom", vp), ("shadow", vp), ("n", i64), ("lr", f32),
                 ("wd", f32), ("momentum", f32), ("dampening", f32), ("grad_scale", f32),
@@ -80,6 +85,9 @@ _SIGS = {
     "ddl_bn_bwd_apply": [vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, i64, i32, i32, vp],
     "ddl_bn_stats": [vp, vp, i64, i32, i32, vp],
     "ddl_bn_backward": [vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, vp],
+    "ddl_bn_finalize2": [ctypes.POINTER(BNArgs), ctypes.POINTER(BNArgs), vp],
+    "ddl_bn_backward2": [vp, ctypes.POINTER(BNBwdArgs), ctypes.POINTER(BNBwdArgs), i64, i32, i32, vp],
+    "ddl_bn_bwd_reduce_part": [vp, vp, vp, vp, vp, vp, i64, i32, i32, vp],
     # nn_ops.hip
     "ddl_prep_images": [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp],
     "ddl_nchw_to_nhwc": [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp],
@@ -149,6 +157,7 @@ def kernels():
         _declare(lib, _OPTIONAL_SIGS)
         for name, size_fn, cls in (("ConvArgs", "ddl_conv_args_size", ConvArgs),
                                    ("BNArgs", "ddl_bn_args_size", BNArgs),
+                                   ("BNBwdArgs", "ddl_bn_bwd_args_size", BNBwdArgs),
                                    ("SGDArgs", "ddl_sgd_args_size", SGDArgs),
                                    ("AdamArgs", "ddl_adam_args_size", AdamArgs)):
             f = getattr(lib, size_fn)

@@ -473,6 +473,81 @@ def bn_finalize(stats, gamma, beta, running_mean, running_var, count, eps=1e-5, 
     return outs[0], outs[1], outs[2], outs[3]
 
 
+def _bn_fin_args(stats, gamma, beta, running_mean, running_var, count, eps, momentum, outs):
+    G, C = stats.shape[0], stats.shape[-1]
+    a = _lib.BNArgs()
+    a.stats, a.gamma, a.beta = ptr(stats), ptr(gamma), ptr(beta)
+    a.running_mean, a.running_var = ptr(running_mean), ptr(running_var)
+    a.scale, a.shift, a.mean, a.rstd = (ptr(outs[i]) for i in range(4))
+    a.gs_param = _gs(gamma) if gamma is not None else _gs(beta)
+    a.gs_buf = _gs(running_mean)
+    a.G, a.C, a.count = G, C, int(count)
+    a.eps, a.momentum, a.training = float(eps), float(momentum), 1
+    a.stripes = stats.shape[1] if stats.dim() == 4 else 1
+    assert stats.is_contiguous()
+    return a
+
+
+def bn_finalize2(bn_a, bn_b, eps=1e-5, momentum=0.1):
+    """Training-mode bn_finalize of two independent BatchNorms in one launch (a residual block's
+    output BN and its projected shortcut's BN). bn_* = (stats, gamma, beta, running_mean,
+    running_var, count) -> ((scale, shift, mean, rstd), (scale, shift, mean, rstd))."""
+    if not bn_a[0].is_cuda:
+        return (bn_finalize(*bn_a, eps, momentum), bn_finalize(*bn_b, eps, momentum))
+    outs = []
+    for bn in (bn_a, bn_b):
+        G, C = bn[0].shape[0], bn[0].shape[-1]
+        outs.append(torch.empty(4, G, C, dtype=torch.float32, device=bn[0].device))
+    a = _bn_fin_args(*bn_a, eps, momentum, outs[0])
+    b = _bn_fin_args(*bn_b, eps, momentum, outs[1])
+    check(_lib.kernels().ddl_bn_finalize2(ctypes.byref(a), ctypes.byref(b), stream()), "bn_finalize2")
+    return tuple(outs[0]), tuple(outs[1])
+
+
+def bn_bwd_reduce_part(dy, ymask, x, mean, rstd):
+    """Striped BN backward reduce sums [G, BN_STRIPES, 2, C] (sum dy_m, sum dy_m * xhat) for
+    ``bn_backward(..., part=)`` / ``bn_backward2``; dy_m = dy * (ymask > 0) (ymask nullable)."""
+    G, C = x.shape[0], x.shape[-1]
+    if not dy.is_cuda:
+        sums = ref.bn_bwd_reduce(dy, ymask, x, mean, rstd)
+        part = torch.zeros(G, BN_STRIPES, 2, C)
+        part[:, 0] = sums
+        return part
+    part = ws.zeros((G, BN_STRIPES, 2, C), x.device)
+    check(_lib.kernels().ddl_bn_bwd_reduce_part(ptr(dy), ptr(ymask), ptr(x), ptr(mean), ptr(rstd),
+                                                ptr(part), x[0].numel() // C, C, G, stream()),
+          "bn_bwd_reduce_part")
+    return part
+
+
+def bn_backward2(dy, bn_a, bn_b):
+    """Two BatchNorm backwards sharing the already-masked input gradient dy (a block's output BN and
+    its shortcut's BN): one fold launch for both and one apply pass that reads dy once.
+    bn_* = (x, mean, rstd, gamma, dgamma, dbeta, part) -> (dx_a, dx_b)."""
+    if not dy.is_cuda:
+        return tuple(bn_backward(dy, None, bn[0], bn[1], bn[2], bn[3], bn[4], bn[5], part=bn[6])
+                     for bn in (bn_a, bn_b))
+    xa = bn_a[0]
+    G, C = xa.shape[0], xa.shape[-1]
+    assert bn_b[0].shape == xa.shape and dy.is_contiguous()
+    args, outs = [], []
+    for x, mean, rstd, gamma, dgamma, dbeta, part in (bn_a, bn_b):
+        t = _lib.BNBwdArgs()
+        dx = torch.empty_like(x)
+        coef = ws.scratch((G, 3, C), x.device)
+        gs = _gs(gamma) if gamma is not None else 0
+        if dgamma is not None or dbeta is not None:
+            gs = _gs(dgamma) if dgamma is not None else _gs(dbeta)
+        t.x, t.mean, t.rstd, t.gamma = ptr(x), ptr(mean), ptr(rstd), ptr(gamma)
+        t.dgamma, t.dbeta, t.part, t.coef, t.dx, t.gs_param = ptr(dgamma), ptr(dbeta), ptr(part), \
+            ptr(coef), ptr(dx), gs
+        args.append(t)
+        outs.append(dx)
+    check(_lib.kernels().ddl_bn_backward2(ptr(dy), ctypes.byref(args[0]), ctypes.byref(args[1]),
+                                          xa[0].numel() // C, C, G, stream()), "bn_backward2")
+    return outs[0], outs[1]
+
+
 def bn_apply(x, scale, shift, r=None, rscale=None, rshift=None, act=0, out=None):
     if not x.is_cuda:
         y = ref.bn_apply(x, scale, shift, r, rscale, rshift, act)

@@ -214,6 +214,39 @@ def test_batchnorm(cuda):
     _close(sc2, sc_r, rel=1e-4); _close(sh2, sh_r, rel=1e-4)
 
 
+def test_bn_dual_finalize_and_backward(cuda):
+    """bn_finalize2 / bn_backward2 (a block's output BN and its shortcut's BN in one launch each)
+    == the single-BN kernels, including the running statistics and d(gamma) / d(beta)."""
+    G, N, H, W, C = 2, 3, 5, 6, 128
+    M = N * H * W
+    xs = [_rand(G, N, H, W, C, dev=cuda, scale=1.5) + 0.2 for _ in range(2)]
+    bns = []
+    for x in xs:
+        st = Fn.bn_stats(x)
+        bns.append([st, torch.rand(G, C, device=cuda) + 0.5, torch.randn(G, C, device=cuda),
+                    torch.randn(G, C, device=cuda), torch.rand(G, C, device=cuda) + 0.5, M])
+    copies = [[t.clone() if torch.is_tensor(t) else t for t in bn] for bn in bns]
+    o1, o2 = Fn.bn_finalize2(bns[0], bns[1])
+    for got, bn in zip((o1, o2), copies):
+        want = Fn.bn_finalize(*bn)
+        for a, b in zip(got, want):
+            _close(a, b, rel=1e-5)
+    for bn, cp in zip(bns, copies):  # running statistics updated identically
+        _close(bn[3], cp[3], rel=1e-5); _close(bn[4], cp[4], rel=1e-5)
+    dy = _rand(G, N, H, W, C, dev=cuda)
+    args, ref_out = [], []
+    for x, (sc, sh, mu, rs), bn in zip(xs, (o1, o2), bns):
+        part = Fn.bn_bwd_reduce_part(dy, None, x, mu, rs)
+        dg, db = torch.zeros(G, C, device=cuda), torch.zeros(G, C, device=cuda)
+        dg2, db2 = dg.clone(), db.clone()
+        args.append((x, mu, rs, bn[1], dg, db, part))
+        ref_out.append((Fn.bn_backward(dy, None, x, mu, rs, bn[1], dg2, db2, part=part.clone()), dg2, db2))
+    dxa, dxb = Fn.bn_backward2(dy, args[0], args[1])
+    for dx, a, (rdx, rdg, rdb) in zip((dxa, dxb), args, ref_out):
+        _close(dx, rdx, rel=1e-2)
+        _close(a[4], rdg, rel=1e-4); _close(a[5], rdb, rel=1e-4)
+
+
 def test_pools_act_dropout(cuda):
     x = _rand(2, 3, 8, 6, 64, dev=cuda)
     _close(Fn.maxpool2_fwd(x), ref.maxpool2_fwd(x.cpu()), rel=0, abs_=0)
