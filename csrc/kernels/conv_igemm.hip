@@ -1448,8 +1448,8 @@ DDL_API int ddl_conv_wgrad(const ConvArgs* ap, int cfg, hipStream_t stream) {
 
 // ---------------------------------------------------------------------------------------------
 // Paired launch: two independent convolutions of one layer in ONE grid — the DGRAD and WGRAD of
-// a backward conv (both read dY), or the two FWD convs that read a block's input (conv1 and the
-// projection shortcut). Few-client grids fill a fraction of the 256 CUs per op (1 client, 8x8
+// a backward conv (both read dY), or the two FWD convs of a downsample block that are independent
+// (its last 3x3 conv and the 1x1 projection shortcut on the block input). Few-client grids fill a fraction of the 256 CUs per op (1 client, 8x8
 // layer: 200 DGRAD workgroups); pairing lets the second op's workgroups run in the first op's
 // tail and idle CU slots instead of after it, without the cross-queue synchronisation a second
 // stream costs inside a HIP graph (docs/KERNELS.md, dead ends). Blocks [0, nA8) run op A (nA
@@ -1506,18 +1506,37 @@ using Wg128x64k64 = TileOp<MODE_WGRAD, 128, 64, 64, 3, 2, false>;
 using Wg128x128k32 = TileOp<MODE_WGRAD, 128, 128, 32, 3, 2, false>;
 using Wg128x128k64 = TileOp<MODE_WGRAD, 128, 128, 64, 2, 2, false>;
 using Wg64x128k32 = TileOp<MODE_WGRAD, 64, 128, 32, 4, 2, false>;
+// FWD + FWD: a block's last 3x3 conv (A) and its 1x1 projection shortcut (B)
+using Fw64x64k64 = TileOp<MODE_FWD, 64, 64, 64, 3, 2, false>;
+using Fw64x128k64 = TileOp<MODE_FWD, 64, 128, 64, 3, 2, false>;
+using Fw128x128k32 = TileOp<MODE_FWD, 128, 128, 32, 3, 2, false>;
+using Fw128x64k64 = TileOp<MODE_FWD, 128, 64, 64, 3, 2, false>;
+using Fw64x128k32 = TileOp<MODE_FWD, 64, 128, 32, 4, 2, false>;
+
+// The instantiated (A, B) combinations, applied to a macro P(TA, TB).
+#define DDL_PAIR_LIST(P)                                                                          \
+  P(DgH256, Wg64x64k64) P(DgH256, Wg128x64k64) P(DgH256, Wg128x128k32) P(DgH256, Wg128x128k64)   \
+  P(DgH256, Wg64x128k32) P(DgH128, Wg64x64k64) P(DgH128, Wg128x64k64) P(DgH128, Wg128x128k32)    \
+  P(DgH128, Wg128x128k64) P(DgH128, Wg64x128k32) P(Dg128x128k64, Wg64x64k64)                     \
+  P(Dg128x128k64, Wg128x64k64) P(Dg128x128k64, Wg128x128k32) P(Dg128x128k64, Wg128x128k64)       \
+  P(Dg128x128k64, Wg64x128k32) P(Dg64x128k64, Wg64x64k64) P(Dg64x128k64, Wg128x64k64)            \
+  P(Dg64x128k64, Wg128x128k32) P(Dg64x128k64, Wg128x128k64) P(Dg64x128k64, Wg64x128k32)          \
+  P(Dg128x64k64, Wg64x64k64) P(Dg128x64k64, Wg128x64k64) P(Dg128x64k64, Wg128x128k32)            \
+  P(Dg128x64k64, Wg128x128k64) P(Dg128x64k64, Wg64x128k32) P(Dg48x256k64, Wg64x64k64)            \
+  P(Dg48x256k64, Wg128x64k64) P(Dg48x256k64, Wg128x128k32) P(Dg48x256k64, Wg128x128k64)          \
+  P(Dg48x256k64, Wg64x128k32)                                                                    \
+  P(Fw64x64k64, Fw64x128k32) P(Fw64x64k64, Fw64x64k64) P(Fw64x64k64, Fw64x128k64)                \
+  P(Fw64x128k64, Fw64x128k32) P(Fw64x128k64, Fw64x64k64) P(Fw64x128k64, Fw64x128k64)             \
+  P(Fw128x128k32, Fw64x128k32) P(Fw128x128k32, Fw64x64k64) P(Fw128x128k32, Fw64x128k64)          \
+  P(Fw128x64k64, Fw64x128k32) P(Fw128x64k64, Fw64x64k64) P(Fw128x64k64, Fw64x128k64)
 
 static int pair_dispatch(const ConvArgs& a, const ConvPlan& pa, const ConvArgs& b, const ConvPlan& pb,
                          hipStream_t s) {
   int err = 0;
-#define DDL_PAIR_W(TA)                                                                         \
-  if (try_pair<TA, Wg64x64k64>(a, pa, b, pb, s, err) || try_pair<TA, Wg128x64k64>(a, pa, b, pb, s, err) || \
-      try_pair<TA, Wg128x128k32>(a, pa, b, pb, s, err) ||                                      \
-      try_pair<TA, Wg128x128k64>(a, pa, b, pb, s, err) || try_pair<TA, Wg64x128k32>(a, pa, b, pb, s, err)) \
-    return err;
-  DDL_PAIR_W(DgH256) DDL_PAIR_W(DgH128) DDL_PAIR_W(Dg128x128k64) DDL_PAIR_W(Dg64x128k64)
-  DDL_PAIR_W(Dg128x64k64) DDL_PAIR_W(Dg48x256k64)
-#undef DDL_PAIR_W
+#define DDL_PAIR_TRY(TA, TB) \
+  if (try_pair<TA, TB>(a, pa, b, pb, s, err)) return err;
+  DDL_PAIR_LIST(DDL_PAIR_TRY)
+#undef DDL_PAIR_TRY
   return -1;  // no paired instantiation for these tiles
 }
 
@@ -1544,12 +1563,9 @@ DDL_API int ddl_conv_pair_supported(const ConvArgs* ap, int mode_a, int cfg_a, c
   ConvPlan pa, pb;
   if (plan_mode(mode_a, *ap, cfg_a, pa) || plan_mode(mode_b, *bp, cfg_b, pb)) return 0;
   bool ok = false;
-#define DDL_PAIR_W(TA) \
-  ok = ok || (TA::match(pa) && (Wg64x64k64::match(pb) || Wg128x64k64::match(pb) || Wg128x128k32::match(pb) || \
-                                Wg128x128k64::match(pb) || Wg64x128k32::match(pb)));
-  DDL_PAIR_W(DgH256) DDL_PAIR_W(DgH128) DDL_PAIR_W(Dg128x128k64) DDL_PAIR_W(Dg64x128k64)
-  DDL_PAIR_W(Dg128x64k64) DDL_PAIR_W(Dg48x256k64)
-#undef DDL_PAIR_W
+#define DDL_PAIR_OK(TA, TB) ok = ok || (TA::match(pa) && TB::match(pb));
+  DDL_PAIR_LIST(DDL_PAIR_OK)
+#undef DDL_PAIR_OK
   return ok ? 1 : 0;
 }
 

@@ -309,3 +309,271 @@ DDL_API int ddl_bce_logits(const void* logits, int ld, const float* targets, flo
                      tval, R, gs, loss, (bf16_t*)dlogits);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// Fused classifier head of a training step: global average pool -> Linear (+bias) -> softmax CE
+// with hard labels -> the Linear's weight / bias gradients -> the pool's input gradient, masked by
+// the pooled input's ReLU and reduced for the BatchNorm that produced it. The unfused chain is
+// seven launches (avgpool, FC FWD, CE, bias sum, FC WGRAD, FC DGRAD, pool backward), four of them
+// single-digit-workgroup grids whose dependent latency is most of their cost at one client per GPU
+// (profiles/step_trace_r2_1client.txt: ~70 us per step). Here it is two:
+//   head_train_kernel : a workgroup owns S samples of one client group; the class rows of W are
+//                       staged in LDS once; logits, softmax and the pooled vectors stay fp32 in LDS;
+//                       it writes the pooled means and d logits to scratch for
+//   head_wgrad_kernel : dW = dlogits^T . pooled and db, one workgroup per (64 channels, <= 32
+//                       samples, group), so each gradient element takes a handful of atomics —
+//                       the single-launch form (every sample block adding its dW) put ~100 atomics
+//                       on every address and took 68 us at one client.
+struct HeadArgs {
+  const bf16_t* x;     // [G][N][HW][C]: the pooled input
+  const bf16_t* w;     // group g at g * w_gs: [Kp][C] bf16 (the Linear's shadow weight)
+  const float* b;      // group g at g * b_gs: [Kp] fp32 (null: no bias)
+  const int* labels;   // [G][N]
+  float* loss;         // [G]  += scale * sum of the rows' CE
+  int* correct;        // [G]  += (argmax == label) (null: off)
+  float* dw;           // group g at g * dw_gs: [Kp][C] fp32, accumulated
+  float* db;           // group g at g * db_gs: [Kp] fp32, accumulated (null: no bias)
+  bf16_t* dx;          // [G][N][HW][C]
+  const bf16_t* c;     // BN fusion (null: plain pool backward): the BN's input [G][N][HW][C]
+  const float* mean;   // [G][C]
+  const float* rstd;   // [G][C]
+  float* part;         // [G][32][2][C] zeroed: (sum dx, sum dx * (c - mean) * rstd)
+  float* pooled;       // scratch [G][N][C] fp32: pooled means
+  float* dlog;         // scratch [G][N][64] fp32: d logits
+  long long w_gs, b_gs, dw_gs, db_gs;
+  int G, N, HW, C, ncls, S;
+  float scale;
+};
+
+// One sample per workgroup; a thread owns one 8-channel chunk (cc) and every RP-th pixel (row).
+// With CACHE, the thread's (<= 4) pixels of x and of the BN input are loaded once, at the start,
+// together with everything else the block reads (W rows, bias, label, BN mean / rstd), so the
+// block's dependent chain has one load round trip; without it (large HW) they are re-read.
+template <bool CACHE>
+__global__ __launch_bounds__(256) void head_train_kernel(HeadArgs a) {
+  extern __shared__ float hsm[];
+  const int C = a.C, CC = C / 8, RP = 256 / CC, HW = a.HW, g = blockIdx.y, n = blockIdx.x;
+  float* pooled = hsm;         // [C] pooled mean
+  float* dp = pooled + C;      // [C] d pooled / HW
+  float* zl = dp + C;          // [64] logits, then d logits
+  float* rb = zl + 64;         // [RP][C] row partials (RP * C = 2048)
+  bf16_t* wl = (bf16_t*)(rb + 2048);  // [ncls][C] the class rows of W
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, cc = tid % CC, row = tid / CC;
+  const float inv = 1.f / HW;
+  const long long rowg = (long long)g * a.N + n;
+  const bf16_t* wg = a.w + g * a.w_gs;
+  const bool bn = a.c != nullptr;
+  const long long base = rowg * HW * C + cc * 8;
+  // all independent loads first
+  for (int t = tid; t < a.ncls * CC; t += 256)
+    *(i4v*)(wl + t * 8) = *(const i4v*)(wg + t * 8);
+  i4v xr[CACHE ? 4 : 1], cr[CACHE ? 4 : 1];
+  if constexpr (CACHE) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = row + i * RP;
+      if (p < HW) {
+        xr[i] = *(const i4v*)(a.x + base + (long long)p * C);
+        if (bn) cr[i] = *(const i4v*)(a.c + base + (long long)p * C);
+      }
+    }
+  }
+  const int y = a.labels[rowg];
+  const float bias = (a.b && lane < a.ncls) ? a.b[g * a.b_gs + lane] : 0.f;
+  float m8[8], r8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    m8[k] = bn ? a.mean[(long long)g * C + cc * 8 + k] : 0.f;
+    r8[k] = bn ? a.rstd[(long long)g * C + cc * 8 + k] : 0.f;
+  }
+  // 1. pool: registers over the thread's pixels, then the RP row partials
+  {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if constexpr (CACHE) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (row + i * RP < HW) {
+          float v[8];
+          unpack8(xr[i], v);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[k] += v[k];
+        }
+      }
+    } else {
+      for (int p = row; p < HW; p += RP) {
+        float v[8];
+        unpack8(*(const i4v*)(a.x + base + (long long)p * C), v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += v[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) rb[row * C + cc * 8 + k] = acc[k];
+  }
+  __syncthreads();
+  for (int t = tid; t < C; t += 256) {
+    float v = 0.f;
+    for (int r = 0; r < RP; ++r) v += rb[r * C + t];
+    pooled[t] = v * inv;
+  }
+  __syncthreads();
+  // 2. logits: one wave per class, lanes over channels
+  for (int k = wv; k < a.ncls; k += 4) {
+    float acc = 0.f;
+    for (int c8 = lane; c8 < CC; c8 += 64) {
+      float w8[8];
+      unpack8(*(const i4v*)(wl + k * C + c8 * 8), w8);
+      const float* pp = pooled + c8 * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += pp[j] * w8[j];
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) zl[k] = acc;
+  }
+  __syncthreads();
+  // 3. softmax CE on wave 0, one lane per class
+  if (wv == 0) {
+    const bool on = lane < a.ncls;
+    const float z = on ? zl[lane] + bias : -INFINITY;
+    float mx = z;
+    int am = on ? lane : 0x7fffffff;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {  // argmax, first max wins (torch.argmax)
+      const float om = __shfl_xor(mx, o, 64);
+      const int oa = __shfl_xor(am, o, 64);
+      if (om > mx || (om == mx && oa < am)) { mx = om; am = oa; }
+    }
+    const float e = on ? __expf(z - mx) : 0.f;
+    const float lse = mx + __logf(wave_sum(e));
+    const float zy = __shfl(z, y, 64);
+    const float d = on ? a.scale * (__expf(z - lse) - (lane == y ? 1.f : 0.f)) : 0.f;
+    zl[lane] = d;
+    a.dlog[rowg * 64 + lane] = d;
+    if (lane == 0) {
+      atomicAdd(a.loss + g, (lse - zy) * a.scale);
+      if (a.correct && am == y) atomicAdd(a.correct + g, 1);
+    }
+  }
+  for (int t = tid; t < C; t += 256) a.pooled[rowg * C + t] = pooled[t];
+  __syncthreads();
+  // 4. d pooled = dl . W (/ HW for the pool backward)
+  for (int c8 = tid; c8 < CC; c8 += 256) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < a.ncls; ++k) {
+      const float d = zl[k];
+      float w8[8];
+      unpack8(*(const i4v*)(wl + k * C + c8 * 8), w8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += d * w8[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dp[c8 * 8 + j] = acc[j] * inv;
+  }
+  __syncthreads();
+  // 5. pool backward (+ the BN's ReLU mask and backward reduce)
+  float d0[8], s0[8], s1[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    d0[k] = dp[cc * 8 + k];
+    s0[k] = s1[k] = 0.f;
+  }
+  auto one = [&](long long e, const i4v& xv4, const i4v& cv4) {
+    float d[8];
+    if (bn) {
+      float xv[8], cv[8];
+      unpack8(xv4, xv);
+      unpack8(cv4, cv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        d[k] = xv[k] > 0.f ? d0[k] : 0.f;
+        const float dr = bf2f(f2bf(d[k]));  // the sums see the stored (bf16) gradient
+        s0[k] += dr;
+        s1[k] += dr * (cv[k] - m8[k]) * r8[k];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) d[k] = d0[k];
+    }
+    *(i4v*)(a.dx + e) = pack8(d);
+  };
+  if constexpr (CACHE) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = row + i * RP;
+      if (p < HW) one(base + (long long)p * C, xr[i], cr[i]);
+    }
+  } else {
+    for (int p = row; p < HW; p += RP) {
+      const long long e = base + (long long)p * C;
+      const i4v zero4 = {0, 0, 0, 0};
+      one(e, bn ? *(const i4v*)(a.x + e) : zero4, bn ? *(const i4v*)(a.c + e) : zero4);
+    }
+  }
+  if (!bn) return;
+  float* pg = a.part + ((long long)g * 32 + n % 32) * 2 * C;
+  for (int h = 0; h < 2; ++h) {  // fold the RP row partials of s0, then of s1
+#pragma unroll
+    for (int k = 0; k < 8; ++k) rb[row * C + cc * 8 + k] = h ? s1[k] : s0[k];
+    __syncthreads();
+    for (int t = tid; t < C; t += 256) {
+      float v = 0.f;
+      for (int r = 0; r < RP; ++r) v += rb[r * C + t];
+      atomicAdd(pg + h * C + t, v);
+    }
+    __syncthreads();
+  }
+}
+
+// dW[k][c] += sum_n dl[n][k] * pooled[n][c] ; db[k] += sum_n dl[n][k]: grid (C/64, N/32, G); a
+// thread owns one channel and the classes k = kg, kg + 4, ... (kg = its wave); its <= 32 pooled
+// values are loaded up front.
+constexpr int HEAD_WG_ROWS = 32;
+__global__ __launch_bounds__(256) void head_wgrad_kernel(HeadArgs a) {
+  __shared__ float dls[HEAD_WG_ROWS * 64];
+  const int g = blockIdx.z, tid = threadIdx.x, kg = tid >> 6;
+  const int c = blockIdx.x * 64 + (tid & 63);
+  const int n0 = blockIdx.y * HEAD_WG_ROWS;
+  const int nr = a.N - n0 < HEAD_WG_ROWS ? a.N - n0 : HEAD_WG_ROWS;
+  const long long row0 = (long long)g * a.N + n0;
+  float pv[HEAD_WG_ROWS];
+  const float* pc = a.pooled + row0 * a.C + (c < a.C ? c : 0);
+#pragma unroll
+  for (int i = 0; i < HEAD_WG_ROWS; ++i) pv[i] = i < nr ? pc[(long long)i * a.C] : 0.f;
+  for (int t = tid; t < HEAD_WG_ROWS * 64; t += 256) dls[t] = t < nr * 64 ? a.dlog[row0 * 64 + t] : 0.f;
+  __syncthreads();
+  if (blockIdx.x == 0 && a.db && tid < a.ncls) {
+    float s = 0.f;
+    for (int i = 0; i < nr; ++i) s += dls[i * 64 + tid];
+    atomicAdd(a.db + g * a.db_gs + tid, s);
+  }
+  if (c >= a.C) return;
+  float* dwg = a.dw + g * a.dw_gs + c;
+  for (int k = kg; k < a.ncls; k += 4) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < HEAD_WG_ROWS; ++i) acc += dls[i * 64 + k] * pv[i];
+    atomicAdd(dwg + (long long)k * a.C, acc);
+  }
+}
+
+static int head_lds_bytes(int C, int ncls) { return (2 * C + 64 + 2048) * 4 + ncls * C * 2; }
+
+DDL_API int ddl_head_args_size() { return (int)sizeof(HeadArgs); }
+
+DDL_API int ddl_head_train(const HeadArgs* ap, hipStream_t s) {
+  HeadArgs a = *ap;
+  if (a.C % 8 || 256 % (a.C / 8) || a.ncls < 1 || a.ncls > 64 || a.N < 1 || a.G < 1 || a.HW < 1 ||
+      a.ncls * a.C * 2 > 32 * 1024 || !a.pooled || !a.dlog)
+    return (int)hipErrorInvalidValue;
+  a.S = 1;
+  const int rp = 256 / (a.C / 8);
+  if (a.HW <= 4 * rp)
+    hipLaunchKernelGGL(head_train_kernel<true>, dim3(a.N, a.G), dim3(256), head_lds_bytes(a.C, a.ncls), s, a);
+  else
+    hipLaunchKernelGGL(head_train_kernel<false>, dim3(a.N, a.G), dim3(256), head_lds_bytes(a.C, a.ncls), s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(head_wgrad_kernel, dim3((a.C + 63) / 64, (a.N + HEAD_WG_ROWS - 1) / HEAD_WG_ROWS, a.G),
+                     dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}

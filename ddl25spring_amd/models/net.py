@@ -97,11 +97,13 @@ class Net:
     # slower on the graph-replayed ResNet-18 step (1 client: 138 -> 152 ms per round)
     overlap_wgrad = os.environ.get("DDL_WGRAD_OVERLAP", "0") != "0"
 
-    def backward_native(self, dy, ctxs):
-        n = len(self.layers)
+    def backward_native(self, dy, ctxs, part=None):
+        """Backward through the first len(ctxs) layers (all of them unless a fused head already
+        took the last ones); ``part``: BN backward sums the caller's fused op left for the last of
+        those layers."""
+        n = len(ctxs)
         with Fn.wgrad_overlap(self.device, self.overlap_wgrad) as ov:
-            part = None
-            for j, (layer, c) in enumerate(zip(reversed(self.layers), reversed(ctxs))):
+            for j, (layer, c) in enumerate(zip(reversed(self.layers[:n]), reversed(ctxs))):
                 i = n - 1 - j
                 kw = {"part": part} if part is not None else {}
                 fuse = None
@@ -119,13 +121,18 @@ class Net:
         return dy
 
     def train_step(self, x, labels, ncls=None, scale=None, targets=None, with_correct=False):
-        """forward + fused softmax-CE (mean over each client's batch) + backward.
-        Grads ACCUMULATE into store.grad (zero them per optimizer step). Returns (loss[G], correct).
-        The returned loss lives in the step's scratch arena: read it before the next step."""
+        """forward + fused softmax-CE (mean over each client's batch) + backward. A net ending in
+        global average pool -> Linear runs its head as two fused launches (``Fn.head_train``;
+        DDL_FUSED_HEAD=0 keeps the per-layer path). Grads ACCUMULATE into store.grad (zero them
+        per optimizer step). Returns (loss[G], correct). The returned loss lives in the step's
+        scratch arena: read it before the next step."""
         if not hasattr(self, "_ws"):
             self._ws = Workspace()
         self._ws.begin(self.device)
         try:
+            head = self._fused_head(x, targets, ncls)
+            if head is not None:
+                return self._train_step_fused_head(x, labels, head, scale, with_correct)
             logits, ctxs = self.forward_native(x, True)
             N = logits.shape[1]
             loss, dlogits, correct = Fn.cross_entropy(
@@ -134,6 +141,38 @@ class Net:
             self.backward_native(dlogits, ctxs)
         finally:
             self._ws.end()
+        return loss, correct
+
+    def _fused_head(self, x, targets, ncls):
+        """(pool, linear, ncls) when the step can end in ``Fn.head_train``: the net ends in a global
+        average pool and a plain Linear (bias or not, no BN / activation), hard labels, on the GPU."""
+        if not (x.is_cuda and Fn.HEAD_FUSED and targets is None and len(self.layers) >= 3):
+            return None
+        pool, lin = self.layers[-2], self.layers[-1]
+        if pool.name != "avgpool" or not isinstance(lin, ConvUnit) or not lin.linear or lin.bn or lin.act:
+            return None
+        ncls = ncls or self.num_classes or lin.cout
+        if not Fn.head_train_ok(lin.cin, ncls) or ncls > lin.cout:
+            return None
+        return pool, lin, ncls
+
+    def _train_step_fused_head(self, x, labels, head, scale, with_correct):
+        pool, lin, ncls = head
+        ctxs = []
+        for layer in self.layers[:-2]:
+            x, c = layer.forward(x, True)
+            ctxs.append(c)
+        st = self.store
+        fuse = self.layers[-3].bn_out(ctxs[-1]) if pool.fuse_out_bn else None
+        loss, correct, dx, part = Fn.head_train(
+            x, st.shadow_of(lin.w), st.param(lin.b) if lin.bias else None,
+            labels.to(torch.int32).contiguous(), ncls, (1.0 / x.shape[1]) if scale is None else scale,
+            st.grad_of(lin.w), st.grad_of(lin.b) if lin.bias else None, bn=fuse, with_correct=with_correct)
+        n = len(self.layers)
+        if self.grad_hook is not None:
+            self.grad_hook(n - 1)
+            self.grad_hook(n - 2)
+        self.backward_native(dx, ctxs, part=part)
         return loss, correct
 
     @torch.no_grad()

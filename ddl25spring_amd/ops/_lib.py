@@ -58,6 +58,14 @@ class BNBwdArgs(ctypes.Structure):
                 ("part", vp), ("coef", vp), ("dx", vp), ("gs_param", i64)]
 
 
+class HeadArgs(ctypes.Structure):
+    _fields_ = [("x", vp), ("w", vp), ("b", vp), ("labels", vp), ("loss", vp), ("correct", vp),
+                ("dw", vp), ("db", vp), ("dx", vp), ("c", vp), ("mean", vp), ("rstd", vp), ("part", vp),
+                ("pooled", vp), ("dlog", vp),
+                ("w_gs", i64), ("b_gs", i64), ("dw_gs", i64), ("db_gs", i64), ("G", i32), ("N", i32),
+                ("HW", i32), ("C", i32), ("ncls", i32), ("S", i32), ("scale", f32)]
+
+
 class SGDArgs(ctypes.Structure):
     _fields_ = [("p", vp), ("g", vp), ("mom", vp), ("shadow", vp), ("n", i64), ("lr", f32),
                 ("wd", f32), ("momentum", f32), ("dampening", f32), ("grad_scale", f32),
@@ -110,6 +118,7 @@ _SIGS = {
     "ddl_ce_vocab": [vp, vp, i32, i32, i32, f32, i32, vp, vp, vp],
     "ddl_mse_kl": [vp, vp, i64, vp, vp, i64, f32, f32, vp, vp, vp, vp, vp],
     "ddl_bce_logits": [vp, i32, vp, f32, i32, f32, vp, vp, vp],
+    "ddl_head_train": [ctypes.POINTER(HeadArgs), vp],
     # optim.hip
     "ddl_sgd": [ctypes.POINTER(SGDArgs), vp],
     "ddl_adam": [ctypes.POINTER(AdamArgs), vp],
@@ -158,6 +167,7 @@ def kernels():
         for name, size_fn, cls in (("ConvArgs", "ddl_conv_args_size", ConvArgs),
                                    ("BNArgs", "ddl_bn_args_size", BNArgs),
                                    ("BNBwdArgs", "ddl_bn_bwd_args_size", BNBwdArgs),
+                                   ("HeadArgs", "ddl_head_args_size", HeadArgs),
                                    ("SGDArgs", "ddl_sgd_args_size", SGDArgs),
                                    ("AdamArgs", "ddl_adam_args_size", AdamArgs)):
             f = getattr(lib, size_fn)

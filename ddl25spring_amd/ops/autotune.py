@@ -112,9 +112,10 @@ def pick(mode: str, geom, flags: tuple, run, accumulate: bool = True):
 
 
 def pick_pair(tag, geom, dpick, wpick, supported, run_pair, run_seq, dmenu, wmenu):
-    """Paired DGRAD + WGRAD launch (functional.conv_dgrad_wgrad): the fastest of the two tuned
-    single launches back to back (-> None) and the paired kernels over (the tuned pick or a menu
-    tile) x (the tuned pick or a menu tile) -> (dcfg, dsplit, wcfg, wsplit)."""
+    """Paired launch of two independent convs (functional.conv_dgrad_wgrad: DGRAD + WGRAD;
+    functional.conv_fwd2: FWD + FWD): the fastest of the two tuned single launches back to back
+    (-> None) and the paired kernels over (op A's tuned pick or a menu tile) x (op B's tuned pick or
+    a menu tile) -> (cfg_a, split_a, cfg_b, split_b)."""
     key = _key("pair", geom, tag)
     if key in _CACHE:
         return _CACHE[key]

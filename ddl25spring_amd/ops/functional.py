@@ -410,6 +410,88 @@ def conv_dgrad_wgrad(dy, w, x, geom: ConvGeom, dw, residual=None, mask=None, bn=
     return dx if bn is None else (dx, part)
 
 
+# Paired FWD + FWD (a downsample block's last 3x3 conv, A, and its 1x1 projection shortcut, B)
+PAIR_FWD_A = [(64, 64, 64, 3), (64, 128, 64, 3), (128, 128, 32, 3), (128, 64, 64, 3)]
+PAIR_FWD_B = [(64, 128, 32, 4), (64, 64, 64, 3), (64, 128, 64, 3)]
+PAIR_FWD_ENABLED = __import__("os").environ.get("DDL_CONV_PAIR_FWD", "1") != "0"
+
+
+def _fwd_pair_args(x, w, geom, y, stats, split_k, partial):
+    return _conv_args(geom, x.device, split_k, partial, x=ptr(x), w=ptr(w), out=ptr(y), stats=ptr(stats),
+                      x_gs=_gs(x), w_gs=_gs(w), out_gs=_gs(y),
+                      stats_gs=0 if stats is None else stats.stride(0),
+                      stats_stripes=stats.shape[1] if stats is not None and stats.dim() == 4 else 1)
+
+
+def conv_fwd_pair(xa, wa, ga: ConvGeom, stats_a, acfg: int, asplit: int, xb, wb, gb: ConvGeom, stats_b,
+                  bcfg: int, out_a=None, out_b=None, check_only: bool = False):
+    """Explicit paired launch of two independent FWD convs (tiles ``acfg`` / ``bcfg``, 0 = the
+    heuristic; op A may split-K with ``asplit``, op B never does: the split workspace is one per
+    device) -> (ya, yb). Raises KernelError when the tiles have no paired instantiation;
+    ``check_only`` -> whether they have one (nothing launched)."""
+    dev = xa.device
+    ya = out_a if out_a is not None else torch.empty(ga.G, ga.N, ga.P, ga.Q, ga.K, dtype=torch.bfloat16, device=dev)
+    yb = out_b if out_b is not None else torch.empty(gb.G, gb.N, gb.P, gb.Q, gb.K, dtype=torch.bfloat16, device=dev)
+    a = _fwd_pair_args(xa, wa, ga, ya, stats_a, asplit, True)
+    b = _fwd_pair_args(xb, wb, gb, yb, stats_b, 1, False)
+    lib = _lib.kernels()
+    if check_only:
+        return bool(lib.ddl_conv_pair_supported(ctypes.byref(a), MODE_FWD, acfg, ctypes.byref(b), MODE_FWD, bcfg))
+    rc = lib.ddl_conv_pair(ctypes.byref(a), MODE_FWD, acfg, ctypes.byref(b), MODE_FWD, bcfg, stream())
+    if rc == -1:
+        raise _lib.KernelError("no paired kernel for these tiles")
+    check(rc, "conv_pair")
+    return ya, yb
+
+
+def conv_fwd2(xa, wa, ga: ConvGeom, stats_a, xb, wb, gb: ConvGeom, stats_b):
+    """Two independent convolutions, each ``conv_fwd(x, w, geom, stats=stats)`` -> (ya, yb): a
+    downsample block's last conv (A) and its projection shortcut on the block input (B). On the
+    GPU they may run as ONE paired launch (whichever of paired / back-to-back the pair tuner
+    measured faster for these shapes)."""
+    if not xa.is_cuda or not PAIR_ENABLED or not PAIR_FWD_ENABLED or not autotune.ENABLED:
+        return conv_fwd(xa, wa, ga, stats=stats_a), conv_fwd(xb, wb, gb, stats=stats_b)
+    _check_inner(xa, "xa"); _check_inner(wa, "wa"); _check_inner(xb, "xb"); _check_inner(wb, "wb")
+    dev = xa.device
+    ya = torch.empty(ga.G, ga.N, ga.P, ga.Q, ga.K, dtype=torch.bfloat16, device=dev)
+    yb = torch.empty(gb.G, gb.N, gb.P, gb.Q, gb.K, dtype=torch.bfloat16, device=dev)
+    fa, fb = (False, False, stats_a is not None, False), (False, False, stats_b is not None, False)
+
+    def scratch(st):
+        return None if st is None else torch.zeros_like(st)
+
+    def run_a(c, sp):
+        conv_fwd(xa, wa, ga, out=torch.empty_like(ya), cfg=c or 0, stats=scratch(stats_a), split_k=sp, _tune=False)
+
+    def run_b(c, sp):
+        conv_fwd(xb, wb, gb, out=torch.empty_like(yb), cfg=c or 0, stats=scratch(stats_b), split_k=sp, _tune=False)
+
+    apick = autotune.pick("fwd", ga, fa, run_a)
+    bpick = autotune.pick("fwd", gb, fb, run_b)
+
+    def pair(cand, **kw):
+        ac, asp, bc, _ = cand
+        return conv_fwd_pair(xa, wa, ga, kw.pop("sa", stats_a), ac or 0, asp, xb, wb, gb,
+                             kw.pop("sb", stats_b), bc or 0, **kw)
+
+    def run_seq():
+        run_a(*apick)
+        run_b(*bpick)
+
+    tag = ("fwd2", fa, fb, gb.N, gb.H, gb.W, gb.C, gb.K, gb.R, gb.S, gb.stride, gb.pad)
+    choice = autotune.pick_pair(tag, ga, apick, bpick,
+                                lambda *cand: pair(cand, out_a=ya, out_b=yb, check_only=True),
+                                lambda cand: pair(cand, sa=scratch(stats_a), sb=scratch(stats_b)),
+                                run_seq,
+                                [(conv_cfg(*t), 0) for t in PAIR_FWD_A],
+                                [(conv_cfg(*t), 0) for t in PAIR_FWD_B])
+    if choice is None:  # back-to-back single launches
+        conv_fwd(xa, wa, ga, out=ya, cfg=apick[0] or 0, stats=stats_a, split_k=apick[1], _tune=False)
+        conv_fwd(xb, wb, gb, out=yb, cfg=bpick[0] or 0, stats=stats_b, split_k=bpick[1], _tune=False)
+        return ya, yb
+    return pair(choice, out_a=ya, out_b=yb)
+
+
 class wgrad_overlap:
     """Backward-pass stream split: inside this context every ``conv_wgrad`` runs on a side stream
     (after an event on the main stream), so a layer's weight gradient can overlap the main
@@ -881,6 +963,87 @@ def cross_entropy(logits, labels=None, targets=None, ncls=None, scale=1.0, want_
                                         float(scale), ptr(loss), ptr(d), ptr(correct), stream()),
           "ce_fwd_bwd")
     return loss, d, correct
+
+
+HEAD_FUSED = __import__("os").environ.get("DDL_FUSED_HEAD", "1") != "0"
+
+
+def head_train_ok(C: int, ncls: int) -> bool:
+    """Shapes the fused classifier head (``head_train``) takes: 8-channel chunks that tile a
+    256-thread block, at most 64 classes (one lane per class), class rows of W that fit 32 KiB
+    of LDS."""
+    return C % 8 == 0 and 256 % (C // 8) == 0 and 1 <= ncls <= 64 and ncls * C * 2 <= 32 * 1024
+
+
+def head_train(x, w, b, labels, ncls: int, scale: float, dw, db, bn=None, with_correct=False):
+    """Training step of a classifier head in two launches (loss.hip ``ddl_head_train``): global
+    average pool of x [G, N, H, W, C] -> logits = pooled @ w[:, :ncls]^T + b -> softmax CE with hard labels [G, N] (loss[G] =
+    scale * sum of the rows' CE) -> dw (+)= dlogits^T @ pooled, db (+)= sum dlogits -> dx = the
+    pool's input gradient. w: [G, Kp, (1, 1,) C] bf16 (group-strided view), b: [G, Kp] fp32 or
+    None, dw / db: fp32 gradient views of the same shapes. bn = (c, mean, rstd) of the BatchNorm
+    whose relu output x is: dx is masked by (x > 0) and the BN's backward sums come back as part
+    (as ``avgpool_bwd_bn``). -> (loss[G], correct[G] | None, dx bf16, part | None)."""
+    G, N, H, W, C = x.shape
+    HW = H * W
+    Kp = w.shape[1]
+    dev = x.device
+    assert ncls <= Kp and head_train_ok(C, ncls), (C, ncls, Kp)
+    if not x.is_cuda:
+        w2 = w.reshape(G, Kp, C).float()
+        pooled = x.float().reshape(G, N, HW, C).mean(2)
+        z = torch.einsum("gnc,gkc->gnk", pooled, w2[:, :ncls])
+        if b is not None:
+            z = z + b.reshape(G, Kp)[:, None, :ncls].float()
+        lse = torch.logsumexp(z, -1)
+        lab = labels.long().reshape(G, N)
+        loss = scale * (lse - z.gather(-1, lab[..., None])[..., 0]).sum(1)
+        correct = (z.argmax(-1) == lab).sum(1).to(torch.int32) if with_correct else None
+        dl = scale * (torch.softmax(z, -1) - torch.nn.functional.one_hot(lab, ncls).float())
+        dw.reshape(G, Kp, C)[:, :ncls] += torch.einsum("gnk,gnc->gkc", dl, pooled)
+        if b is not None:
+            db.reshape(G, Kp)[:, :ncls] += dl.sum(1)
+        dp = torch.einsum("gnk,gkc->gnc", dl, w2[:, :ncls]) / HW
+        if bn is None:
+            dx = dp[:, :, None, None, :].expand(G, N, H, W, C).to(torch.bfloat16).contiguous()
+            return loss, correct, dx, None
+        dx, part = _head_pool_bwd_bn_ref(dp, x, bn)
+        return loss, correct, dx, part
+    assert x.is_contiguous() and labels.is_contiguous()
+    loss = ws.zeros((G,), dev)
+    correct = torch.zeros(G, dtype=torch.int32, device=dev) if with_correct else None
+    dx = torch.empty_like(x)
+    a = _lib.HeadArgs()
+    a.x, a.w, a.b, a.labels = ptr(x), ptr(w), ptr(b), ptr(labels)
+    a.loss, a.correct, a.dw, a.db, a.dx = ptr(loss), ptr(correct), ptr(dw), ptr(db), ptr(dx)
+    a.w_gs, a.dw_gs = _gs(w), _gs(dw)
+    a.b_gs, a.db_gs = (_gs(b), _gs(db)) if b is not None else (0, 0)
+    part = None
+    if bn is not None:
+        c, mean, rstd = bn
+        assert c.is_contiguous() and mean.is_contiguous() and rstd.is_contiguous()
+        part = ws.zeros((G, BN_STRIPES, 2, C), dev)
+        a.c, a.mean, a.rstd, a.part = ptr(c), ptr(mean), ptr(rstd), ptr(part)
+    pooled = torch.empty(G, N, C, dtype=torch.float32, device=dev)
+    dlog = torch.empty(G, N, 64, dtype=torch.float32, device=dev)
+    a.pooled, a.dlog = ptr(pooled), ptr(dlog)
+    a.G, a.N, a.HW, a.C, a.ncls, a.scale = G, N, HW, C, ncls, float(scale)
+    check(_lib.kernels().ddl_head_train(ctypes.byref(a), stream()), "head_train")
+    return loss, correct, dx, part
+
+
+def _head_pool_bwd_bn_ref(dp, x, bn):
+    """fp32 reference of the head's pool backward with the BN mask and reduce (as avgpool_bwd_bn,
+    from an fp32 pooled gradient already divided by HW)."""
+    c, mean, rstd = bn
+    G, N, H, W, C = x.shape
+    d = dp.reshape(G, N, 1, 1, C) * (x.float() > 0)
+    dx = d.to(torch.bfloat16).contiguous()
+    xh = (c.float() - mean.reshape(G, 1, 1, 1, C)) * rstd.reshape(G, 1, 1, 1, C)
+    part = torch.zeros(G, BN_STRIPES, 2, C)
+    df = dx.float()
+    part[:, 0, 0] = df.reshape(G, -1, C).sum(1)
+    part[:, 0, 1] = (df * xh).reshape(G, -1, C).sum(1)
+    return dx, part
 
 
 # --------------------------------------------------------------------------------- optimizers

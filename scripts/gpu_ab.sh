@@ -1,14 +1,25 @@
 #!/bin/bash
-# A/B of two kernel-library builds (new in-tree vs scratch/ab/libddl_kernels_prev.so): kernel
-# tests on the new one, then the headline bench alternating builds.
+# A/B of one env switch (0 vs 1) on bench.py at 1 and 8 clients, after the GPU tests matching -k.
+#   gpurun -- bash scripts/gpu_ab.sh <tag> <ENV_VAR> "<pytest -k expr>"
 set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/tk.log 2>&1 || { tail -30 gpurun_out/tk.log; exit 1; }
-tail -1 gpurun_out/tk.log
-for i in 1 2; do
-  for v in new prev; do
-    if [ $v = prev ]; then export DDL_KERNEL_LIB=$PWD/scratch/ab/libddl_kernels_prev.so; else unset DDL_KERNEL_LIB; fi
-    timeout -k 10 200 python bench.py --steps 3 --warmup 1 ${AB_ARGS} > gpurun_out/ab_$v$i.log 2>&1 || { tail -20 gpurun_out/ab_$v$i.log; exit 1; }
-    echo "$v$i $(grep -o '"value": [0-9.]*' gpurun_out/ab_$v$i.log)"
+tag=${1:-ab}
+var=${2:-DDL_FUSED_HEAD}
+kexpr=${3:-head}
+out=gpurun_out/$tag
+mkdir -p $out
+export TMPDIR=/tmp
+step() {
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "$out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc $(grep -h '^{' "$out/$name.log" | cut -c1-110) $(tail -n 1 "$out/$name.log" | cut -c1-80)"
+  [ $rc -eq 0 ] || { tail -n 30 "$out/$name.log"; exit $rc; }
+}
+step ktests 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "$kexpr"
+for rep in 1 2; do
+  for v in 0 1; do
+    step "c1_${v}_$rep" 200 env $var=$v python bench.py --clients 1 --train-size 6250 --steps 4 --warmup 1
+    step "c8_${v}_$rep" 200 env $var=$v python bench.py --steps 3 --warmup 1
   done
 done
+echo ALLDONE

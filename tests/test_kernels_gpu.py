@@ -515,6 +515,53 @@ def test_conv_pair(cuda, geom):
     _close(dw, dw_ref, rel=2e-3)
 
 
+FWD_PAIR_GEOMS = [  # (block's last 3x3 conv, its 1x1 / stride-2 shortcut)
+    (ConvGeom(G=1, N=4, H=16, W=16, C=128, K=128, R=3, S=3, stride=1, pad=1),
+     ConvGeom(G=1, N=4, H=32, W=32, C=64, K=128, R=1, S=1, stride=2, pad=0)),
+    (ConvGeom(G=2, N=3, H=4, W=4, C=512, K=512, R=3, S=3, stride=1, pad=1),
+     ConvGeom(G=2, N=3, H=8, W=8, C=256, K=512, R=1, S=1, stride=2, pad=0)),
+]
+
+
+@pytest.mark.parametrize("geoms", FWD_PAIR_GEOMS, ids=lambda gs: f"{gs[0].K}_{gs[0].H}")
+def test_conv_fwd_pair(cuda, geoms):
+    """Two FWD convs in one paired grid (a downsample block's last conv + its shortcut) == the fp32
+    references, outputs and BN statistics, for every (A, B) tile of the paired menu the shapes
+    admit (A also split-K); the tuned entry point agrees."""
+    ga, gb = geoms
+    xa, wa = _rand(ga.G, ga.N, ga.H, ga.W, ga.C, dev=cuda), _weights(ga, cuda)
+    xb, wb = _rand(gb.G, gb.N, gb.H, gb.W, gb.C, dev=cuda), _weights(gb, cuda)
+    ya_ref = ref.conv_fwd(xa.cpu(), wa.cpu(), ga)
+    yb_ref = ref.conv_fwd(xb.cpu(), wb.cpu(), gb)
+
+    def stats_ok(st, y):
+        _close(st[:, :, 0].sum(1), y.float().sum((1, 2, 3)), rel=5e-3)
+        _close(st[:, :, 1].sum(1), y.float().square().sum((1, 2, 3)), rel=5e-3)
+
+    ran = 0
+    for ta in Fn.PAIR_FWD_A:
+        for tb in Fn.PAIR_FWD_B:
+            for asp in (1, 2):
+                sa, sb = Fn.stats_buffer(ga.G, ga.K, cuda), Fn.stats_buffer(gb.G, gb.K, cuda)
+                try:
+                    ya, yb = Fn.conv_fwd_pair(xa, wa, ga, sa, Fn.conv_cfg(*ta), asp, xb, wb, gb, sb,
+                                              Fn.conv_cfg(*tb))
+                except RuntimeError:
+                    continue  # tile not eligible for these shapes
+                ran += 1
+                _close(ya, ya_ref)
+                _close(yb, yb_ref)
+                stats_ok(sa.cpu(), ya_ref)
+                stats_ok(sb.cpu(), yb_ref)
+    assert ran > 0
+    sa, sb = Fn.stats_buffer(ga.G, ga.K, cuda), Fn.stats_buffer(gb.G, gb.K, cuda)
+    ya, yb = Fn.conv_fwd2(xa, wa, ga, sa, xb, wb, gb, sb)
+    _close(ya, ya_ref)
+    _close(yb, yb_ref)
+    stats_ok(sa.cpu(), ya_ref)
+    stats_ok(sb.cpu(), yb_ref)
+
+
 SUB2_GEOMS = [
     ConvGeom(G=2, N=3, H=16, W=16, C=64, K=128, R=3, S=3, stride=2, pad=1),   # BasicBlock conv1 (phased)
     ConvGeom(G=1, N=2, H=8, W=8, C=128, K=64, R=1, S=1, stride=1, pad=0),     # Bottleneck conv1 (unphased)
@@ -544,3 +591,47 @@ def test_conv_dgrad_residual_sub2(cuda, geom):
     _close(dw, dw_ref, rel=2e-3)
     # the CPU op path agrees with the reference composition
     _close(Fn.conv_dgrad(dy.cpu(), w.cpu(), g, residual=res.cpu(), mask=mask.cpu(), residual_sub=2), dx_ref)
+
+
+HEAD_CASES = [  # (G, N, H, W, C, Kp, ncls, bias, bn)
+    (2, 7, 4, 4, 512, 32, 10, True, True),     # ResNet-18 CIFAR head, fused with the last BN
+    (1, 5, 2, 3, 64, 64, 33, False, False),    # plain pool backward, no bias
+    (3, 4, 1, 1, 256, 64, 64, True, True),     # 1x1 input, 64 classes (one lane each)
+    (1, 40, 7, 7, 2048, 32, 8, True, True),    # ResNet-50-size input (re-read path), 33 samples/block row
+]
+
+
+@pytest.mark.parametrize("case", HEAD_CASES, ids=lambda c: f"C{c[4]}_k{c[6]}_bn{int(c[8])}")
+def test_head_train(cuda, case):
+    """The fused classifier head (pool -> Linear -> CE -> Linear grads -> pool backward [+ BN mask
+    and reduce]) == its fp32 reference."""
+    G, N, H, W, C, Kp, ncls, bias, bn = case
+    x = _rand(G, N, H, W, C, dev=cuda).relu()
+    flat = _rand(G, Kp * C + 64, dev=cuda, scale=0.05)
+    w = flat[:, 32:32 + Kp * C].unflatten(1, (Kp, 1, 1, C))       # group-strided, like the store
+    b = (torch.randn(G, Kp + 3, device=cuda) * 0.1)[:, :Kp] if bias else None
+    labels = torch.randint(0, ncls, (G, N), dtype=torch.int32, device=cuda)
+    c = _rand(G, N, H, W, C, dev=cuda)
+    mean = torch.randn(G, C, device=cuda) * 0.1
+    rstd = torch.rand(G, C, device=cuda) + 0.5
+    bnt = (c, mean, rstd) if bn else None
+    dw_ref = torch.zeros(G, Kp, 1, 1, C)
+    db_ref = torch.zeros(G, Kp) if bias else None
+    loss_r, corr_r, dx_r, part_r = Fn.head_train(
+        x.cpu(), w.cpu(), None if b is None else b.cpu(), labels.cpu(), ncls, 1.0 / N, dw_ref, db_ref,
+        bn=None if bnt is None else tuple(t.cpu() for t in bnt), with_correct=True)
+    for _ in range(2):  # the second call accumulates into fresh buffers identically
+        gflat = torch.zeros(G, Kp * C + 40, device=cuda)
+        dw = gflat[:, 8:8 + Kp * C].unflatten(1, (Kp, 1, 1, C))
+        db = torch.zeros(G, Kp, device=cuda) if bias else None
+        loss, corr, dx, part = Fn.head_train(x, w, b, labels, ncls, 1.0 / N, dw, db, bn=bnt,
+                                             with_correct=True)
+        _close(loss, loss_r, rel=1e-3)
+        assert torch.equal(corr.cpu(), corr_r), (corr, corr_r)
+        _close(dw, dw_ref, rel=2e-3)
+        assert gflat[:, :8].abs().max().item() == 0 and gflat[:, 8 + Kp * C:].abs().max().item() == 0
+        if bias:
+            _close(db, db_ref, rel=2e-3)
+        _close(dx, dx_r, rel=1e-2)
+        if bn:
+            _close(part.sum(1), part_r.sum(1), rel=5e-3)

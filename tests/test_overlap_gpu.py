@@ -75,3 +75,23 @@ def test_cross_block_bn_backward_fusion_within_noise_floor(cuda, monkeypatch):
     for graph in (False, True):
         rel = _rel(_grads(cuda, resnet18_cifar, "cifar10", False, graph), ref)
         assert rel < 1.5 * floor + 0.02, (graph, rel, floor)
+
+
+def test_fused_head_matches_per_layer_head(cuda, monkeypatch):
+    """ResNet-18's pool -> fc -> CE -> fc grads -> pool backward (+ the last BN's reduce) in two
+    launches (Fn.head_train): the fc gradients match the per-layer path's to bf16 rounding (that
+    path rounds the pooled vector, logits and their gradients to bf16), every other gradient
+    within the BN-atomics noise floor, eagerly and graph-replayed."""
+    from ddl25spring_amd.ops import functional as Fn
+    monkeypatch.setattr(Fn, "HEAD_FUSED", False)
+    ref = _grads(cuda, resnet18_cifar, "cifar10", False, False)
+    floor = _rel(_grads(cuda, resnet18_cifar, "cifar10", False, False), ref)
+    monkeypatch.setattr(Fn, "HEAD_FUSED", True)
+    net = resnet18_cifar(groups=2)
+    lin = net.layers[-1]
+    sw, sb = net.store.specs[lin.w], net.store.specs[lin.b]
+    fc = slice(sw.offset, sb.offset + sb.numel)
+    for graph in (False, True):
+        g = _grads(cuda, resnet18_cifar, "cifar10", False, graph)
+        assert _rel(g, ref) < 1.5 * floor + 0.02, (graph, _rel(g, ref), floor)
+        assert _rel(g[:, fc], ref[:, fc]) < 2e-2, graph
