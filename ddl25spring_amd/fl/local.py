@@ -46,31 +46,39 @@ class LocalTrainer:
         return loss
 
     # ---------------------------------------------------------------- graph-captured round
-    def _graph_run(self, plan_dev: torch.Tensor, nsteps: int, G: int):
-        """Steps 0 .. nsteps-1 of the round's plan [steps, G, B] as ONE graph replay: the whole
-        sequence of local SGD steps is captured once (every step's batch launch reads its own row
-        of a static plan buffer), so a round costs one plan copy and one graph launch."""
-        key = (G, self.B, nsteps)
+    def _graph_run(self, plan_dev: torch.Tensor, nsteps: int, G: int, tail=None):
+        """Steps 0 .. nsteps-1 of the round's plan [steps, G, B] (+ the epoch's short last step
+        ``tail`` [G, n], when every slot has the same n) as ONE graph replay: the whole sequence
+        of local SGD steps is captured once (every step's batch launch reads its own row of a
+        static plan buffer), so a round costs one plan copy and one graph launch. Without the tail
+        in the graph, the short step (6,250 samples per client at B=100: 62 steps + 50 samples)
+        ran eagerly every round, ~130 host-side launches."""
+        key = (G, self.B, nsteps, None if tail is None else tail.shape[-1])
         ent = self._graphs.get(key)
         if ent is None:
-            ent = self._capture(plan_dev, nsteps, G)
+            ent = self._capture(plan_dev, nsteps, G, tail)
             self._graphs[key] = ent
         ent["plan"].copy_(plan_dev[:nsteps])
+        if tail is not None:
+            ent["tail"].copy_(tail)
         ent["graph"].replay()
         self.last_loss = ent["loss"]
 
-    def _capture(self, plan_dev: torch.Tensor, nsteps: int, G: int):
+    def _capture(self, plan_dev: torch.Tensor, nsteps: int, G: int, tail=None):
         st, opt = self.net.store, self.opt
         # the warm-up steps really train: snapshot and restore so the first graph step is exact
         snap = (st.data[:G].clone(), st.buffers[:G].clone(),
                 None if opt.mom is None else opt.mom[:G].clone(), opt.steps,
                 [c.clone() for c in self.net.rng_counters()])
         plan = plan_dev[:nsteps].clone()
+        tl = None if tail is None else tail.clone()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for i in range(2):
                 self._step(plan[i % nsteps], 0, G)
+            if tl is not None:  # the short step's shapes (tuned on first eager use)
+                self._step(tl, 0, G)
         torch.cuda.current_stream().wait_stream(s)
         # zero-initialised momentum == torch's "buffer = first grad" when dampening == 0, so the
         # frozen first_step=False inside the graph is exact for every step of a round
@@ -79,6 +87,8 @@ class LocalTrainer:
         with torch.cuda.graph(graph):
             for i in range(nsteps):
                 loss = self._step(plan[i], 0, G)
+            if tl is not None:
+                loss = self._step(tl, 0, G)
         st.data[:G].copy_(snap[0])
         st.buffers[:G].copy_(snap[1])
         if snap[2] is not None:
@@ -87,7 +97,7 @@ class LocalTrainer:
         for c, saved in zip(self.net.rng_counters(), snap[4]):
             c.copy_(saved)  # warm-up steps advanced the dropout counters: rewind them too
         st.sync_shadow()
-        return {"graph": graph, "plan": plan, "loss": loss}
+        return {"graph": graph, "plan": plan, "tail": tl, "loss": loss}
 
     # ---------------------------------------------------------------- public
     def run(self, slot_indices: list[np.ndarray], seeds, epochs: int = 1, generators=None) -> int:
@@ -141,10 +151,16 @@ class LocalTrainer:
         s = 0
         if self.use_graph and g0 == 0:
             nfull = int(np.argmin(full)) if not full.all() else steps  # leading full steps
+            tail = None
+            if nfull and nfull == steps - 1:  # one short last step, the same n in every slot
+                cnt = (plan[-1] >= 0).sum(1)
+                n = int(cnt[0])
+                if n > 0 and cnt.min() == n and cnt.max() == n and (plan[-1, :, :n] >= 0).all():
+                    tail = plan_dev[-1, :, :n].contiguous()
             if nfull:
-                self._graph_run(plan_dev, nfull, G)
-                samples += nfull * G * self.B
-                s = nfull
+                self._graph_run(plan_dev, nfull, G, tail)
+                samples += nfull * G * self.B + (0 if tail is None else G * tail.shape[-1])
+                s = nfull + (0 if tail is None else 1)
         for s in range(s, steps):
             if full[s]:
                 self.last_loss = self._step(plan_dev[s], g0, g1)

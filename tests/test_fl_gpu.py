@@ -16,9 +16,11 @@ def _ctx(cuda):
     return DistContext(device=cuda)
 
 
-def test_graph_replay_equals_eager(cuda):
+@pytest.mark.parametrize("batch", [50, 60])
+def test_graph_replay_equals_eager(cuda, batch):
     """Captured local steps == eager steps, including dropout: its Philox counter lives on the
-    device and advances inside the graph, so every replay draws a fresh mask.
+    device and advances inside the graph, so every replay draws a fresh mask. batch 60: 200
+    samples per client end in a short step of 20, captured in the same graph.
 
     MnistCnn (no BatchNorm): with BN, the fp32-atomic order noise of the statistics (~1e-7) is
     amplified chaotically by bf16 rounding (two identical eager runs of ResNet-18 differ by ~35%
@@ -29,7 +31,7 @@ def test_graph_replay_equals_eager(cuda):
     ws = []
     for graph in (True, False):
         data = DeviceImageDataset(arr, cuda)
-        fa = FedAvg(mnist_cnn, data, parts, lr=0.05, batch_size=50, client_fraction=1.0,
+        fa = FedAvg(mnist_cnn, data, parts, lr=0.05, batch_size=batch, client_fraction=1.0,
                     seed=3, ctx=_ctx(cuda), use_graph=graph, eval_every=0)
         w0 = fa.w_global.clone()
         fa.round()
