@@ -20,7 +20,8 @@ from _common import emit, timed
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=3, help="timed units (split-NN epochs / GAN rounds)")
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=2,
+                    help="untimed units (the first runs eagerly, the second captures the HIP graphs)")
     ap.add_argument("--local-steps", type=int, default=20)
     ap.add_argument("--gan-batch", type=int, default=128)
     ap.add_argument("--vfl-batch", type=int, default=64)
@@ -29,7 +30,9 @@ def main():
     from ddl25spring_amd.data import heart as H
     from ddl25spring_amd.fl.gan import FederatedGAN
     from ddl25spring_amd.models import tabular as T
+    from ddl25spring_amd.optim import FlatAdamW
     from ddl25spring_amd.runtime import dist as rdist
+    from ddl25spring_amd.runtime.graphs import CapturedStep
     from ddl25spring_amd.vfl import SplitNNParty, SplitNNServer
     ctx = rdist.init()
     dev = ctx.device
@@ -47,14 +50,19 @@ def main():
     if ctx.world == 1:
         net = T.VFLNetwork(bottoms, 2).to(dev)
         net.top_model = top
-        net.optimizer = torch.optim.AdamW(net.parameters())
-        crit = torch.nn.CrossEntropyLoss()
+        # the framework's fused AdamW (one launch per step, device-side step counter) and fused
+        # soft-target CE; on the GPU an epoch (13 fixed-order mini-batches, vfl.py:58-82)
+        # replays from one HIP graph
+        net.optimizer = FlatAdamW(net.parameters()) if dev.type == "cuda" else torch.optim.AdamW(net.parameters())
+        crit = T.SoftCrossEntropy()
 
-        def epoch():
+        def one_epoch():
             for b in range(0, len(y), args.vfl_batch):
                 net.optimizer.zero_grad()
                 crit(net([x[b:b + args.vfl_batch] for x in xs]), y[b:b + args.vfl_batch]).backward()
                 net.optimizer.step()
+
+        epoch = CapturedStep(one_epoch, warmup=1, enabled=dev.type == "cuda")
     elif ctx.rank == 0:
         srv = SplitNNServer(top, [1], [2 * len(parts[1])], local_bottom=bottoms[0])
 

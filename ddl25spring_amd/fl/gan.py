@@ -7,8 +7,11 @@ of both networks (and of the BN running statistics), exactly as FedAvgServer doe
 assigned round-robin to ranks; the weighted sums of all ranks meet in ONE all-reduce per round
 over a flat fp32 buffer (G params | D params | BN buffers).
 
-Each client keeps its own Adam moments across rounds (swapped in and out of the fused FlatAdam
-buffers), as a real client device would.
+Each client keeps its own Adam moments and step count across rounds (swapped in and out of the
+fused FlatAdam buffers), as a real client device would. On the GPU a client's ``local_steps``
+steps replay from one HIP graph per client (``runtime.graphs.CapturedStep``): the batch indices
+of the round are drawn on the host from the client's seeded generator as before and uploaded into
+a static buffer the graph reads.
 """
 from __future__ import annotations
 
@@ -19,6 +22,7 @@ import numpy as np
 import torch
 
 from ..models.dcgan import Discriminator, GANTrainer, Generator
+from ..runtime.graphs import CapturedStep
 
 
 @dataclass
@@ -40,7 +44,8 @@ def _flat_buffers(mods):
 class FederatedGAN:
     def __init__(self, client_data: list[torch.Tensor], ctx=None, nz: int = 100, ngf: int = 64,
                  ndf: int = 64, lr: float = 2e-4, betas=(0.5, 0.999), local_steps: int = 10,
-                 batch_size: int = 64, client_fraction: float = 1.0, seed: int = 0, device=None):
+                 batch_size: int = 64, client_fraction: float = 1.0, seed: int = 0, device=None,
+                 use_graph: bool = True):
         self.ctx = ctx
         self.rank = ctx.rank if ctx else 0
         self.world = ctx.world_size if ctx else 1
@@ -58,7 +63,10 @@ class FederatedGAN:
         self.K = max(1, round(client_fraction * len(client_data)))
         self.rng = np.random.default_rng(seed)
         self.local_steps, self.batch_size, self.seed = local_steps, batch_size, seed
-        self._state = {}  # client -> (mG, vG, tG, mD, vD, tD)
+        self._state = {}  # client -> (mG, vG, tG, mD, vD, tD, tG_dev, tD_dev)
+        self.use_graph = use_graph and self.device.type == "cuda"
+        self._idx: dict = {}    # client -> static [local_steps, batch] device index buffer
+        self._graphs: dict = {}  # client -> CapturedStep over its local steps
 
     # ---------------------------------------------------------------------------------------
     def _global_tensors(self):
@@ -87,13 +95,25 @@ class FederatedGAN:
                 continue
             if st is None:
                 opt.m.zero_(); opt.v.zero_(); opt.t = 0
+                if opt.t_dev is not None:
+                    opt.t_dev.zero_()
             else:
                 opt.m.copy_(st[i]); opt.v.copy_(st[i + 1]); opt.t = st[i + 2]
+                if opt.t_dev is not None:  # the device step counter drives the bias correction
+                    opt.t_dev.copy_(st[6 + i // 3])
 
     def _swap_out(self, c):
         if hasattr(self.optG, "m"):
+            tdev = [None if o.t_dev is None else o.t_dev.clone() for o in (self.optG, self.optD)]
             self._state[c] = (self.optG.m.clone(), self.optG.v.clone(), self.optG.t,
-                              self.optD.m.clone(), self.optD.v.clone(), self.optD.t)
+                              self.optD.m.clone(), self.optD.v.clone(), self.optD.t, *tdev)
+
+    def _local_steps(self, c):
+        data, idx = self.data[c], self._idx[c]
+        ld = lg = None
+        for i in range(self.local_steps):
+            ld, lg = self.trainer.step(data.index_select(0, idx[i]))
+        return ld, lg
 
     # ---------------------------------------------------------------------------------------
     def run(self, rounds: int) -> GANRunResult:
@@ -111,10 +131,18 @@ class FederatedGAN:
                 self._swap_in(int(c))
                 g = torch.Generator(device="cpu").manual_seed(self.seed + int(c) + 1 + r * self.K)
                 data = self.data[int(c)]
-                for _ in range(self.local_steps):
-                    idx = torch.randint(0, len(data), (self.batch_size,), generator=g).to(data.device)
-                    ld, lg = self.trainer.step(data.index_select(0, idx))
-                    res.samples += self.batch_size
+                idx = torch.stack([torch.randint(0, len(data), (self.batch_size,), generator=g)
+                                   for _ in range(self.local_steps)])
+                if int(c) not in self._idx:
+                    self._idx[int(c)] = torch.empty_like(idx, device=data.device)
+                self._idx[int(c)].copy_(idx)
+                if self.use_graph:
+                    if int(c) not in self._graphs:
+                        self._graphs[int(c)] = CapturedStep(lambda c=int(c): self._local_steps(c), warmup=1)
+                    ld, lg = self._graphs[int(c)]()
+                else:
+                    ld, lg = self._local_steps(int(c))
+                res.samples += self.batch_size * self.local_steps
                 ld_sum += float(ld); lg_sum += float(lg)
                 self._swap_out(int(c))
                 acc.add_(self._flat(), alpha=float(self.n[c] / wsum))
