@@ -189,8 +189,9 @@ class FedAvg(FederatedBase):
                                         self.weight_decay, self.planner, self.use_graph)
             self._graph_default = self.trainer.use_graph
         self.trainer.label_transform = lt
-        # a label transform is not graph-captured: eager steps only for rounds that need one
-        self.trainer.use_graph = self._graph_default and lt is None
+        # a label transform is graph-captured only if it declares a graph_key (pure device ops,
+        # e.g. LabelFlip); otherwise eager steps for the rounds that need one
+        self.trainer.use_graph = self._graph_default and (lt is None or hasattr(lt, "graph_key"))
         return self.trainer
 
     def round(self):

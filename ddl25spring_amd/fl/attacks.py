@@ -34,19 +34,39 @@ class Attack:
 
 
 class LabelFlip(Attack):
+    """Malicious clients train on labels y -> (num_classes - 1 - y). The per-slot flip mask lives
+    in ONE persistent device buffer per (device, slot count): each round's transform refreshes it
+    (``refresh``, also on its first eager call), so a captured round graph, which reads the buffer,
+    replays correctly whichever slots the round's sampling put the attackers in."""
+
+    def __init__(self, malicious):
+        super().__init__(malicious)
+        self._masks: dict = {}
+
     def label_transform_for(self, slot_clients, num_classes):
         bad = [i for i, c in enumerate(slot_clients) if c in self.malicious]
         if not bad:
             return None
-        mask_cpu = torch.zeros(len(slot_clients), dtype=torch.bool)
+        n = len(slot_clients)
+        mask_cpu = torch.zeros(n, dtype=torch.bool)
         mask_cpu[bad] = True
-        cache = {}
+        fresh: set = set()
+
+        def refresh(device):
+            key = (torch.device(device), n)
+            if key not in self._masks:
+                self._masks[key] = torch.zeros(n, dtype=torch.bool, device=device)
+            if key not in fresh:
+                self._masks[key].copy_(mask_cpu)
+                fresh.add(key)
+            return self._masks[key]
 
         def f(y, g0, g1):
-            key = (y.device, g0, g1)
-            if key not in cache:
-                cache[key] = mask_cpu[g0:g1].to(y.device).reshape(-1, *([1] * (y.dim() - 1)))
-            return torch.where(cache[key], (num_classes - 1) - y, y)
+            m = refresh(y.device)[g0:g1]
+            return torch.where(m.reshape(-1, *([1] * (y.dim() - 1))), (num_classes - 1) - y, y)
+        f.refresh = refresh
+        # pure device ops on the persistent mask: a captured round replays it for any slot set
+        f.graph_key = ("label_flip", n, num_classes)
         return f
 
 

@@ -29,7 +29,8 @@ class LocalTrainer:
         self.planner = planner
         dev = net.device
         self.use_graph = (dev.type == "cuda") if use_graph is None else (use_graph and dev.type == "cuda")
-        self.label_transform = label_transform  # callable(y [G,B]) -> y (attacks)
+        self.label_transform = label_transform  # callable(y [G,B], g0, g1) -> y (attacks); with a
+        # ``graph_key`` attribute it is pure device ops and may be captured in the round graph
         self._graphs: dict = {}
         self.last_loss = None
 
@@ -53,7 +54,8 @@ class LocalTrainer:
         static plan buffer), so a round costs one plan copy and one graph launch. Without the tail
         in the graph, the short step (6,250 samples per client at B=100: 62 steps + 50 samples)
         ran eagerly every round, ~130 host-side launches."""
-        key = (G, self.B, nsteps, None if tail is None else tail.shape[-1])
+        key = (G, self.B, nsteps, None if tail is None else tail.shape[-1],
+               getattr(self.label_transform, "graph_key", None))
         ent = self._graphs.get(key)
         if ent is None:
             ent = self._capture(plan_dev, nsteps, G, tail)
@@ -61,6 +63,8 @@ class LocalTrainer:
         ent["plan"].copy_(plan_dev[:nsteps])
         if tail is not None:
             ent["tail"].copy_(tail)
+        if hasattr(self.label_transform, "refresh"):  # this round's device-side transform state
+            self.label_transform.refresh(plan_dev.device)
         ent["graph"].replay()
         self.last_loss = ent["loss"]
 

@@ -241,15 +241,30 @@ def test_torch_planner_matches_dataloader_shuffle():
     assert [[int(v) for v in first[s, 0] if v >= 0] for s in range(first.shape[0])] == want[0]
 
 
-def test_label_flip_round_does_not_disable_graphs_for_later_rounds(fp32):
+def test_label_transform_graph_policy(fp32):
+    """LabelFlip's transform is pure device ops with a graph_key: its rounds stay graph-replayed
+    (the key tells the trainer which captured round fits). A transform without one runs that
+    round eagerly, and later rounds without a transform get the graphs back."""
+    from ddl25spring_amd.fl.attacks import Attack
     arr, data = _data(400)
     parts = split(4, True, 3, labels=arr.labels)
     fa = FedAvg(mnist_mlp, data, parts, lr=0.05, batch_size=50, client_fraction=1.0, seed=3,
                 attack=LabelFlip([1]), use_graph=True)
     tr = fa._trainer([0, 1])
-    assert tr.label_transform is not None and tr.use_graph is False
+    assert tr.label_transform.graph_key == ("label_flip", 2, 10)
+    assert tr.use_graph == fa._graph_default
     tr = fa._trainer([0, 2])
     assert tr.label_transform is None and tr.use_graph == fa._graph_default
+
+    class Custom(Attack):
+        def label_transform_for(self, slot_clients, num_classes):
+            return lambda y, g0, g1: y
+
+    fa.attack = Custom([1])
+    tr = fa._trainer([0, 1])
+    assert tr.label_transform is not None and tr.use_graph is False
+    fa.attack = None
+    assert fa._trainer([0, 1]).use_graph == fa._graph_default
 
 
 def test_checkpoint_resume_under_gaussian_attack(fp32):

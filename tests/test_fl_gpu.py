@@ -6,6 +6,7 @@ import torch
 from ddl25spring_amd.data.images import DeviceImageDataset, synthetic_images
 from ddl25spring_amd.data.split import split
 from ddl25spring_amd.fl.algorithms import FedAvg, FedSGD
+from ddl25spring_amd.fl.attacks import LabelFlip
 from ddl25spring_amd.models import mnist_cnn, mnist_mlp
 from ddl25spring_amd.runtime.dist import DistContext
 
@@ -16,11 +17,12 @@ def _ctx(cuda):
     return DistContext(device=cuda)
 
 
-@pytest.mark.parametrize("batch", [50, 60])
-def test_graph_replay_equals_eager(cuda, batch):
+@pytest.mark.parametrize("batch,flip", [(50, False), (60, False), (50, True)])
+def test_graph_replay_equals_eager(cuda, batch, flip):
     """Captured local steps == eager steps, including dropout: its Philox counter lives on the
     device and advances inside the graph, so every replay draws a fresh mask. batch 60: 200
-    samples per client end in a short step of 20, captured in the same graph.
+    samples per client end in a short step of 20, captured in the same graph. flip: a
+    label-flipping client (LabelFlip's device-side transform replays inside the graph).
 
     MnistCnn (no BatchNorm): with BN, the fp32-atomic order noise of the statistics (~1e-7) is
     amplified chaotically by bf16 rounding (two identical eager runs of ResNet-18 differ by ~35%
@@ -32,7 +34,8 @@ def test_graph_replay_equals_eager(cuda, batch):
     for graph in (True, False):
         data = DeviceImageDataset(arr, cuda)
         fa = FedAvg(mnist_cnn, data, parts, lr=0.05, batch_size=batch, client_fraction=1.0,
-                    seed=3, ctx=_ctx(cuda), use_graph=graph, eval_every=0)
+                    seed=3, ctx=_ctx(cuda), use_graph=graph, eval_every=0,
+                    attack=LabelFlip([1]) if flip else None)
         w0 = fa.w_global.clone()
         fa.round()
         fa.round()
