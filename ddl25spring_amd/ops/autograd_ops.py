@@ -67,6 +67,14 @@ def _grad_ready(p: torch.Tensor) -> None:
 
 
 # ------------------------------------------------------------------------------------- linear
+# A plain (no bias / residual epilogue) linear with a vocabulary-sized output runs its forward on
+# hipBLASLt (torch.matmul): on the LLaMA-288 LM head (8192 x 288 -> 32000, K = 288) it takes
+# 264 us against 389 us for the MFMA conv-GEMM, whose 9-step reduction leaves the 524 MB bf16
+# output write exposed; every block-sized linear is as fast or faster on the conv-GEMM, and so is
+# the LM head's backward (scripts/gemm_vs_blas.py, profiles/gemm_vs_blas_r2f.txt).
+BLAS_FWD_MIN_OUT = 8192
+
+
 class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, residual):
@@ -77,8 +85,11 @@ class _Linear(torch.autograd.Function):
         geom = Fn.ConvGeom(1, T, 1, 1, C, Kout, 1, 1, 1, 0)
         wb = _bf16_weight(w).view(1, Kout, 1, 1, C)
         res = residual.reshape(1, T, 1, 1, Kout).contiguous() if residual is not None else None
-        y = Fn.conv_fwd(x2.view(1, T, 1, 1, C), wb, geom,
-                        bias=None if b is None else b.detach().view(1, Kout), residual=res)
+        if b is None and res is None and Kout >= BLAS_FWD_MIN_OUT:
+            y = torch.matmul(x2, wb.view(Kout, C).t())
+        else:
+            y = Fn.conv_fwd(x2.view(1, T, 1, 1, C), wb, geom,
+                            bias=None if b is None else b.detach().view(1, Kout), residual=res)
         ctx.save_for_backward(x2, wb)
         ctx.geom, ctx.has_b, ctx.has_res, ctx.xshape = geom, b is not None, residual is not None, x.shape
         ctx.w = w
