@@ -157,6 +157,111 @@ DDL_API int ddl_ce_vocab(const void* logits, const int* labels, int R, int V, in
 }
 
 // ---------------------------------------------------------------------------------------------
+// LM-head CE for autograd in ONE read of the logits: the forward writes the loss AND the
+// gradient at unit upstream scale, d = (*inv) * (softmax(z) - onehot(y)) (0 for ignored rows);
+// the backward only rescales it by the upstream gradient, in place, and only when that is not 1
+// (ce_vocab_scale_kernel reads it on the device: no host sync). Against lse-in-forward +
+// gradient-in-backward this reads the [rows, V] logits once instead of twice. The normaliser
+// stays a device scalar (*inv).
+// The row stays in registers between the two sweeps (16 chunks of 8 bf16 per thread: V <= 32768)
+// so the logits are read from HBM once; a row is 64 KB at V = 32000 and the rows of the blocks in
+// flight on an XCD overflow its L2, so a second load would go to HBM again.
+constexpr int CE_RC = 16;
+__global__ __launch_bounds__(256) void ce_vocab_fused_kernel(const bf16_t* __restrict__ logits,
+                                                             const int* __restrict__ labels, int V,
+                                                             int ld, const float* __restrict__ inv,
+                                                             int ignore_index, float* __restrict__ loss,
+                                                             bf16_t* __restrict__ dlogits) {
+  __shared__ float sm[2][4];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const bf16_t* z = logits + (long long)row * ld;
+  const int y = labels[row];
+  const float sc = *inv;
+  i4v raw[CE_RC];
+#pragma unroll
+  for (int i = 0; i < CE_RC; ++i) {
+    const int c = (i * 256 + tid) * 8;
+    if (c < V) raw[i] = *(const i4v*)(z + c);
+  }
+  float m = -INFINITY, se = 0.f;
+#pragma unroll
+  for (int i = 0; i < CE_RC; ++i) {
+    const int c = (i * 256 + tid) * 8;
+    if (c < V) {
+      float v[8];
+      unpack8(raw[i], v);
+      float lm = v[0];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) lm = fmaxf(lm, v[k]);
+      const float nm = fmaxf(m, lm);
+      se = se * __expf(m - nm);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) se += __expf(v[k] - nm);
+      m = nm;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64), os = __shfl_xor(se, o, 64);
+    const float nm = fmaxf(m, om);
+    se = (m == -INFINITY ? 0.f : se * __expf(m - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    m = nm;
+  }
+  if (lane == 0) { sm[0][w] = m; sm[1][w] = se; }
+  __syncthreads();
+  float M = sm[0][0];
+  for (int i = 1; i < 4; ++i) M = fmaxf(M, sm[0][i]);
+  float SE = 0.f;
+  for (int i = 0; i < 4; ++i) SE += sm[1][i] * __expf(sm[0][i] - M);
+  const float lse = M + __logf(SE);
+  const bool ign = (y == ignore_index);
+  if (tid == 0 && !ign) atomicAdd(loss, (lse - bf2f(z[y])) * sc);
+  bf16_t* dz = dlogits + (long long)row * ld;
+#pragma unroll
+  for (int i = 0; i < CE_RC; ++i) {
+    const int c = (i * 256 + tid) * 8;
+    if (c < V) {
+      float v[8];
+      unpack8(raw[i], v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = ign ? 0.f : sc * (__expf(v[k] - lse) - ((c + k) == y ? 1.f : 0.f));
+      *(i4v*)(dz + c) = pack8(v);
+    }
+  }
+}
+
+// x *= *g in place, unless *g == 1 (every block reads it first and returns: the common
+// loss.backward() case costs one near-empty launch)
+__global__ void ce_vocab_scale_kernel(bf16_t* __restrict__ x, long long n8, const float* __restrict__ g) {
+  const float s = *g;
+  if (s == 1.f) return;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8;
+       i += (long long)gridDim.x * blockDim.x) {
+    float v[8];
+    unpack8(*(const i4v*)(x + i * 8), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] *= s;
+    *(i4v*)(x + i * 8) = pack8(v);
+  }
+}
+
+DDL_API int ddl_ce_vocab_fused(const void* logits, const int* labels, int R, int V, int ld,
+                               const float* inv, int ignore_index, float* loss, void* dlogits,
+                               hipStream_t s) {
+  if (V % 8 || ld % 8 || V > CE_RC * 256 * 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ce_vocab_fused_kernel, dim3(R), dim3(256), 0, s, (const bf16_t*)logits, labels, V,
+                     ld, inv, ignore_index, loss, (bf16_t*)dlogits);
+  return (int)hipGetLastError();
+}
+
+DDL_API int ddl_ce_vocab_scale(void* x, long long n, const float* g, hipStream_t s) {
+  if (n % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ce_vocab_scale_kernel, dim3(grid_for(n / 8, 256, 2048)), dim3(256), 0, s,
+                     (bf16_t*)x, n / 8, g);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 // Split LM-head CE for autograd without host syncs or extra passes over the [rows, V] logits:
 //   fwd : lse[row] and loss += (lse - z_y) * (*inv)          (inv = 1 / #non-ignored rows, device)
 //   bwd : dz = (*g) * (*inv) * (softmax(z) - onehot(y))      (g = upstream grad, device scalar)

@@ -109,7 +109,7 @@ def train_llm(cfg: LLMConfig, ctx, log=print, warmup: int = 0) -> dict:
         opt.zero_grad()
         loss = None
         for m in torch.chunk(xd, cfg.micro_batches):
-            l = causalLLMLoss(mod(m), m) / cfg.micro_batches
+            l = causalLLMLoss(mod(m), m, scale=1.0 / cfg.micro_batches)
             l.backward()
             loss = l.detach() if loss is None else loss + l.detach()
         opt.step()
@@ -154,7 +154,7 @@ def train_llm(cfg: LLMConfig, ctx, log=print, warmup: int = 0) -> dict:
             loss = None
             mbs = torch.chunk(x, cfg.micro_batches)
             for i, m in enumerate(mbs):
-                l = causalLLMLoss(mod(m), m) / cfg.micro_batches
+                l = causalLLMLoss(mod(m), m, scale=1.0 / cfg.micro_batches)
                 if sync is not None and i < len(mbs) - 1:
                     with sync.no_sync():
                         l.backward()

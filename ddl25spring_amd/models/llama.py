@@ -152,13 +152,15 @@ def split_stages(model: LLama, n_stages: int):
     return out
 
 
-def causalLLMLoss(logits, target, vocab_size=None, ignore_index=-100):  # noqa: N802 (reference name)
-    """Next-token CE: logits[:, :-1] vs target[:, 1:]. On the device every row of the [B, S, V]
-    logits goes to the fused kernel with the last position's label set to ``ignore_index`` (same
-    mean, no copy of the [B, S-1, V] slice)."""
+def causalLLMLoss(logits, target, vocab_size=None, ignore_index=-100, scale: float = 1.0):  # noqa: N802
+    """Next-token CE (reference name): logits[:, :-1] vs target[:, 1:]. On the device every row of
+    the [B, S, V] logits goes to the fused kernel with the last position's label set to
+    ``ignore_index`` (same mean, no copy of the [B, S-1, V] slice). ``scale`` (extension): a
+    constant factor such as 1 / micro-batches, folded into the kernel's normaliser."""
     if not logits.is_cuda:
-        return A.cross_entropy_vocab(logits[:, :-1].contiguous(), target[:, 1:].contiguous(), ignore_index)
+        return A.cross_entropy_vocab(logits[:, :-1].contiguous(), target[:, 1:].contiguous(), ignore_index,
+                                     scale)
     lab = torch.empty(target.shape, dtype=torch.int32, device=target.device)
     lab[:, :-1] = target[:, 1:]
     lab[:, -1] = ignore_index
-    return A.cross_entropy_vocab(logits, lab, ignore_index)
+    return A.cross_entropy_vocab(logits, lab, ignore_index, scale)

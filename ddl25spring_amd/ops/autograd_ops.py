@@ -31,6 +31,8 @@ _lib.register_signatures({
     "ddl_attn_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, vp],
     "ddl_ce_vocab_lse": [vp, vp, i32, i32, i32, vp, i32, vp, vp, vp],
     "ddl_ce_vocab_grad": [vp, vp, i32, i32, i32, vp, vp, vp, i32, vp, vp],
+    "ddl_ce_vocab_fused": [vp, vp, i32, i32, i32, vp, i32, vp, vp, vp],
+    "ddl_ce_vocab_scale": [vp, i64, vp, vp],
 })
 
 
@@ -350,13 +352,19 @@ def causal_attention(qkv, n_heads, head_dim):
 
 
 # ------------------------------------------------------------------------------- LM loss
+CE_FUSED_MAX_V = 32768  # == CE_RC * 256 * 8 in loss.hip
+
+
 class _VocabCE(torch.autograd.Function):
     """Mean token CE over the rows of bf16 logits [..., V] with int32 labels. No host sync (the
-    1/#valid normaliser is a device scalar) and the gradient is made in backward from the saved
-    logits and per-row log-sum-exp, already scaled by the upstream gradient (e.g. 1/micro-batches)."""
+    1/#valid normaliser is a device scalar). The forward makes the loss and the gradient at unit
+    upstream scale from one read of the logits (``ddl_ce_vocab_fused``, V <= 32768; wider
+    vocabularies take the lse-then-gradient pair); the backward rescales that
+    gradient in place by the upstream gradient only when it is not 1 (checked on the device). A
+    second backward through the same graph recomputes the gradient first."""
 
     @staticmethod
-    def forward(ctx, logits, labels, ignore_index):
+    def forward(ctx, logits, labels, ignore_index, scale):
         V = logits.shape[-1]
         lg = logits.reshape(-1, V)
         if not lg.is_contiguous():
@@ -364,33 +372,55 @@ class _VocabCE(torch.autograd.Function):
         R = lg.shape[0]
         lab = labels.reshape(-1)
         inv = (lab != ignore_index).sum(dtype=torch.float32).clamp_min_(1.0).reciprocal_().reshape(1)
+        if scale != 1.0:
+            inv.mul_(scale)
         loss = torch.zeros(1, dtype=torch.float32, device=lg.device)
-        lse = torch.empty(R, dtype=torch.float32, device=lg.device)
-        check(K().ddl_ce_vocab_lse(ptr(lg), ptr(lab), R, V, V, ptr(inv), int(ignore_index), ptr(loss),
-                                   ptr(lse), stream()), "ce_vocab_lse")
-        ctx.save_for_backward(lg, lab, lse, inv)
-        ctx.shape, ctx.ignore = logits.shape, int(ignore_index)
+        if V > CE_FUSED_MAX_V:
+            lse = torch.empty(R, dtype=torch.float32, device=lg.device)
+            check(K().ddl_ce_vocab_lse(ptr(lg), ptr(lab), R, V, V, ptr(inv), int(ignore_index), ptr(loss),
+                                       ptr(lse), stream()), "ce_vocab_lse")
+            d = None
+            ctx.lse = lse
+        else:
+            d = torch.empty_like(lg)
+            check(K().ddl_ce_vocab_fused(ptr(lg), ptr(lab), R, V, V, ptr(inv), int(ignore_index),
+                                         ptr(loss), ptr(d), stream()), "ce_vocab_fused")
+        ctx.save_for_backward(lg, lab, inv, d)
+        ctx.shape, ctx.ignore, ctx.used = logits.shape, int(ignore_index), False
         return loss[0]
 
     @staticmethod
     def backward(ctx, g):
-        lg, lab, lse, inv = ctx.saved_tensors
+        lg, lab, inv, d = ctx.saved_tensors
         R, V = lg.shape
+        if d is None:  # wide vocabulary: the gradient from the saved log-sum-exp, scaled by g
+            gg = g.detach().to(torch.float32).reshape(1).contiguous()
+            d = torch.empty_like(lg)
+            check(K().ddl_ce_vocab_grad(ptr(lg), ptr(lab), R, V, V, ptr(ctx.lse), ptr(inv), ptr(gg),
+                                        ctx.ignore, ptr(d), stream()), "ce_vocab_grad")
+            return d.view(ctx.shape), None, None, None
+        if ctx.used:  # the unit-scale gradient was already rescaled by an earlier backward
+            d = torch.empty_like(lg)
+            junk = torch.zeros(1, dtype=torch.float32, device=lg.device)
+            check(K().ddl_ce_vocab_fused(ptr(lg), ptr(lab), R, V, V, ptr(inv), ctx.ignore, ptr(junk),
+                                         ptr(d), stream()), "ce_vocab_fused")
+        ctx.used = True
         gg = g.detach().to(torch.float32).reshape(1).contiguous()
-        d = torch.empty_like(lg)
-        check(K().ddl_ce_vocab_grad(ptr(lg), ptr(lab), R, V, V, ptr(lse), ptr(inv), ptr(gg),
-                                    ctx.ignore, ptr(d), stream()), "ce_vocab_grad")
-        return d.view(ctx.shape), None, None
+        check(K().ddl_ce_vocab_scale(ptr(d), d.numel(), ptr(gg), stream()), "ce_vocab_scale")
+        return d.view(ctx.shape), None, None, None
 
 
-def cross_entropy_vocab(logits, targets, ignore_index=-100):
-    """Mean token cross-entropy; one fused kernel computes loss and d(logits)."""
+def cross_entropy_vocab(logits, targets, ignore_index=-100, scale: float = 1.0):
+    """``scale`` x mean token cross-entropy; one fused kernel computes loss and d(logits).
+    Pass a constant factor (e.g. 1 / micro-batches) as ``scale`` rather than multiplying the
+    returned loss: the gradient is then final in the forward pass and the backward has no
+    rescaling pass over the [rows, V] gradient."""
     if not logits.is_cuda:
-        return F.cross_entropy(logits.reshape(-1, logits.shape[-1]).float(), targets.reshape(-1).long(),
-                               ignore_index=ignore_index)
+        return scale * F.cross_entropy(logits.reshape(-1, logits.shape[-1]).float(),
+                                       targets.reshape(-1).long(), ignore_index=ignore_index)
     if logits.dtype != torch.bfloat16:
         logits = logits.to(torch.bfloat16)
-    return _VocabCE.apply(logits, targets.to(torch.int32).contiguous(), ignore_index)
+    return _VocabCE.apply(logits, targets.to(torch.int32).contiguous(), ignore_index, float(scale))
 
 
 # ===================================================================== image ops (NHWC, GANs)

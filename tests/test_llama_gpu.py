@@ -128,6 +128,24 @@ def test_vocab_cross_entropy(cuda):
     assert abs(a.item() - b.item()) < 2e-2
     a.backward(); b.backward()
     assert _rel(lc.grad, lh.grad) < 2e-2
+    # non-unit upstream gradient (the gradient made in forward is rescaled on the device), and a
+    # second backward through the same graph (recomputed, not rescaled twice)
+    for t in (lc, lh):
+        t.grad = None
+    a = A.cross_entropy_vocab(lc, tgt.to(cuda))
+    b = A.cross_entropy_vocab(lh, tgt)
+    (a * 0.25).backward(retain_graph=True); (b * 0.25).backward(retain_graph=True)
+    assert _rel(lc.grad, lh.grad) < 2e-2
+    (a * 0.5).backward(); (b * 0.5).backward()
+    assert _rel(lc.grad, lh.grad) < 2e-2
+    # a constant factor folded into the kernel (scale=) == scaling the loss
+    for t in (lc, lh):
+        t.grad = None
+    a = A.cross_entropy_vocab(lc, tgt.to(cuda), scale=0.25)
+    b = A.cross_entropy_vocab(lh, tgt) * 0.25
+    assert abs(a.item() - b.item()) < 1e-2
+    a.backward(); b.backward()
+    assert _rel(lc.grad, lh.grad) < 2e-2
 
 
 def test_llama_model_fwd_bwd_matches_fp32(cuda):
