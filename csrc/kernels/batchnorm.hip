@@ -152,6 +152,20 @@ static unsigned stream_blocks(long long M, int RPI, int G, int rows_per_thread) 
   return (unsigned)want;
 }
 
+// Grid of a striped reduce pass: every block ends with 2C fp32 atomics into the stripes, and with
+// wide channels the device-wide atomic rate, not HBM, bounds the pass (ResNet-50: a 2048-channel
+// reduce over 7x7 maps took 100 us in 784 blocks, 3.2M atomics, for 50 MB of input). So the
+// grid is also capped at ~512K atomics per launch; each block then sweeps more rows, 4 rows'
+// loads in flight per thread (REDUCE_UNROLL).
+static unsigned reduce_blocks(long long M, int RPI, int G, int C) {
+  unsigned b = stream_blocks(M, RPI, G, 16);
+  long long cap = (512LL * 1024) / (2LL * C * G);
+  if (cap < 8) cap = 8;
+  if (b > cap) b = (unsigned)cap;
+  return b;
+}
+constexpr int REDUCE_UNROLL = 4;
+
 // ---------------------------------------------------------------------------------------------
 // y = act(x*scale[c] + shift[c] + residual_term)     residual_term = r*rs[c]+rb[c] | r | 0
 // act: 0 none, 1 relu, 2 leaky(0.01), 3 leaky(0.2) (DCGAN)
@@ -254,21 +268,36 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
   load8f(rstd + (long long)g * C + cc * 8, r8);
   const long long base = (long long)g * M * C + cc * 8;
   if (active) {
-    for (long long p = (long long)blockIdx.x * RPI + row; p < M; p += (long long)gridDim.x * RPI) {
-      const long long e = base + p * C;
-      float d[8], xv[8];
-      unpack8(*(const i4v*)(dy + e), d);
-      unpack8(*(const i4v*)(x + e), xv);
-      if (ymask) {
-        float yv[8];
-        unpack8(*(const i4v*)(ymask + e), yv);
+    const long long stride = (long long)gridDim.x * RPI;
+    for (long long p0 = (long long)blockIdx.x * RPI + row; p0 < M; p0 += stride * REDUCE_UNROLL) {
+      i4v rd[REDUCE_UNROLL], rx[REDUCE_UNROLL], rm[REDUCE_UNROLL];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) if (!(yv[k] > 0.f)) d[k] = 0.f;
+      for (int u = 0; u < REDUCE_UNROLL; ++u) {  // all loads first: 4 rows in flight
+        const long long p = p0 + u * stride;
+        if (p < M) {
+          const long long e = base + p * C;
+          rd[u] = *(const i4v*)(dy + e);
+          rx[u] = *(const i4v*)(x + e);
+          if (ymask) rm[u] = *(const i4v*)(ymask + e);
+        }
       }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        s0[k] += d[k];
-        s1[k] += d[k] * (xv[k] - m8[k]) * r8[k];
+      for (int u = 0; u < REDUCE_UNROLL; ++u) {
+        if (p0 + u * stride >= M) break;
+        float d[8], xv[8];
+        unpack8(rd[u], d);
+        unpack8(rx[u], xv);
+        if (ymask) {
+          float yv[8];
+          unpack8(rm[u], yv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) if (!(yv[k] > 0.f)) d[k] = 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          s0[k] += d[k];
+          s1[k] += d[k] * (xv[k] - m8[k]) * r8[k];
+        }
       }
     }
   }
@@ -325,7 +354,7 @@ DDL_API int ddl_bn_bwd_reduce(const void* dy, const void* ymask, const void* x, 
                               hipStream_t s) {
   if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
   const int RPI = 256 / (C / 8);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(stream_blocks(M, RPI, G, 16), G), dim3(256), 0, s,
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(reduce_blocks(M, RPI, G, C), G), dim3(256), 0, s,
                      (const bf16_t*)dy, (const bf16_t*)ymask, (const bf16_t*)x, mean, rstd, part,
                      M, C);
   hipLaunchKernelGGL(bn_fold_kernel, dim3((G * C + 255) / 256), dim3(256), 0, s, part, sums, dgamma,
@@ -434,11 +463,20 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict_
   float s1[8] = {}, s2[8] = {};
   if (row < RPI) {
     const long long base = (long long)g * M * C + cc * 8;
-    for (long long p = (long long)blockIdx.x * RPI + row; p < M; p += (long long)gridDim.x * RPI) {
-      float v[8];
-      unpack8(*(const i4v*)(x + base + p * C), v);
+    const long long stride = (long long)gridDim.x * RPI;
+    for (long long p0 = (long long)blockIdx.x * RPI + row; p0 < M; p0 += stride * REDUCE_UNROLL) {
+      i4v rv[REDUCE_UNROLL];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) { s1[k] += v[k]; s2[k] += v[k] * v[k]; }
+      for (int u = 0; u < REDUCE_UNROLL; ++u)
+        if (p0 + u * stride < M) rv[u] = *(const i4v*)(x + base + (p0 + u * stride) * C);
+#pragma unroll
+      for (int u = 0; u < REDUCE_UNROLL; ++u) {
+        if (p0 + u * stride >= M) break;
+        float v[8];
+        unpack8(rv[u], v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { s1[k] += v[k]; s2[k] += v[k] * v[k]; }
+      }
     }
   }
 #pragma unroll
@@ -459,7 +497,7 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict_
 DDL_API int ddl_bn_stats(const void* x, float* stats, long long M, int C, int G, hipStream_t s) {
   if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
   const int RPI = 256 / (C / 8);
-  hipLaunchKernelGGL(bn_stats_kernel, dim3(stream_blocks(M, RPI, G, 16), G), dim3(256), 0, s,
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(reduce_blocks(M, RPI, G, C), G), dim3(256), 0, s,
                      (const bf16_t*)x, stats, M, C);
   return (int)hipGetLastError();
 }
@@ -588,7 +626,7 @@ DDL_API int ddl_bn_bwd_reduce_part(const void* dy, const void* ymask, const void
                                    const float* rstd, float* part, long long M, int C, int G, hipStream_t s) {
   if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
   const int RPI = 256 / (C / 8);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(stream_blocks(M, RPI, G, 16), G), dim3(256), 0, s,
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(reduce_blocks(M, RPI, G, C), G), dim3(256), 0, s,
                      (const bf16_t*)dy, (const bf16_t*)ymask, (const bf16_t*)x, mean, rstd, part, M, C);
   return (int)hipGetLastError();
 }
@@ -602,7 +640,7 @@ DDL_API int ddl_bn_backward(const void* dy, const void* ymask, const void* x, co
                             long long M, int C, int G, int do_reduce, hipStream_t s) {
   if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
   const int RPI = 256 / (C / 8);
-  if (do_reduce) hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(stream_blocks(M, RPI, G, 16), G), dim3(256), 0, s,
+  if (do_reduce) hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(reduce_blocks(M, RPI, G, C), G), dim3(256), 0, s,
                      (const bf16_t*)dy, (const bf16_t*)ymask, (const bf16_t*)x, mean, rstd, part,
                      M, C);
   hipLaunchKernelGGL(bn_fold_coef_kernel, dim3((C + 31) / 32, G), dim3(256), 0, s, part, dgamma,

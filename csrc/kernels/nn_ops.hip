@@ -355,20 +355,37 @@ __global__ __launch_bounds__(256) void avgpool_bwd_bn_kernel(
   for (int k = 0; k < 8; ++k) { m8[k] = mg[k]; r8[k] = rg[k]; }
   const float inv = 1.f / HW;
   if (row < RPI) {
-    for (long long p = (long long)blockIdx.x * RPI + row; p < M; p += (long long)gridDim.x * RPI) {
-      const long long e = ((long long)g * M + p) * C + cc * 8;
-      const long long n = p / HW;
-      float d[8], xv[8], cv[8];
-      unpack8(*(const i4v*)(dy + ((long long)g * N + n) * C + cc * 8), d);
-      unpack8(*(const i4v*)(x + e), xv);
-      unpack8(*(const i4v*)(c + e), cv);
+    constexpr int U = 4;  // 4 rows' loads in flight per thread
+    const long long stride = (long long)gridDim.x * RPI;
+    for (long long p0 = (long long)blockIdx.x * RPI + row; p0 < M; p0 += stride * U) {
+      i4v rd[U], rx[U], rc[U];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        d[k] = xv[k] > 0.f ? d[k] * inv : 0.f;
-        s0[k] += d[k];
-        s1[k] += d[k] * (cv[k] - m8[k]) * r8[k];
+      for (int u = 0; u < U; ++u) {
+        const long long p = p0 + u * stride;
+        if (p < M) {
+          const long long e = ((long long)g * M + p) * C + cc * 8;
+          rd[u] = *(const i4v*)(dy + ((long long)g * N + p / HW) * C + cc * 8);
+          rx[u] = *(const i4v*)(x + e);
+          rc[u] = *(const i4v*)(c + e);
+        }
       }
-      *(i4v*)(dx + e) = pack8(d);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long p = p0 + u * stride;
+        if (p >= M) break;
+        const long long e = ((long long)g * M + p) * C + cc * 8;
+        float d[8], xv[8], cv[8];
+        unpack8(rd[u], d);
+        unpack8(rx[u], xv);
+        unpack8(rc[u], cv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          d[k] = xv[k] > 0.f ? d[k] * inv : 0.f;
+          s0[k] += d[k];
+          s1[k] += d[k] * (cv[k] - m8[k]) * r8[k];
+        }
+        *(i4v*)(dx + e) = pack8(d);
+      }
     }
   }
 #pragma unroll
@@ -406,6 +423,9 @@ DDL_API int ddl_avgpool_bwd_bn(const void* dy, const void* x, const void* c, con
   const int RPI = 256 / (C / 8);
   long long want = ((long long)N * HW + RPI * 4 - 1) / (RPI * 4);
   long long cap = (2048 + G - 1) / G;
+  // each block ends with 2C atomics: keep ~512K per launch (batchnorm.hip reduce_blocks)
+  long long acap = (512LL * 1024) / (2LL * C * G);
+  if (cap > acap) cap = acap < 8 ? 8 : acap;
   if (want > cap) want = cap;
   hipLaunchKernelGGL(avgpool_bwd_bn_kernel, dim3((unsigned)(want < 1 ? 1 : want), G), dim3(256), 0, s,
                      (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)c, mean, rstd, (bf16_t*)dx,
