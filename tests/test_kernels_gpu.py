@@ -382,6 +382,11 @@ def test_prep_images_labels(cuda):
     a = Fn.prep_images(src, idx, mean, inv, 32, True, 1, labels=labels, labels_out=y)
     assert torch.equal(a, Fn.prep_images(src, idx, mean, inv, 32, True, 1))
     assert torch.equal(y, labels[idx.long()])
+    # the ImageNet-stem row kernel (7x7 / stride 2 im2col) gathers them too
+    y.zero_()
+    a = Fn.prep_images(src, idx, mean, inv, 160, 7, 3, 2, labels=labels, labels_out=y)
+    assert torch.equal(a, Fn.prep_images(src, idx, mean, inv, 160, 7, 3, 2))
+    assert torch.equal(y, labels[idx.long()])
 
 
 @pytest.mark.parametrize("geom", [ConvGeom(G=2, N=3, H=8, W=8, C=64, K=96, R=3, S=3, stride=1, pad=1),
