@@ -661,14 +661,16 @@ DDL_API int ddl_cast_bf16_f32(const void* x, float* y, long long n, hipStream_t 
 // ---------------------------------------------------------------------------------------------
 // general k x k / stride / pad max pool (ImageNet stem 3x3/2 p1); -inf padding like torch
 // am (optional): window-local argmax r*k+s per output element (uint8), consumed by the backward
+// I: index type (int when every element offset fits in 31 bits: no 64-bit division per item)
+template <typename I>
 __global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                    unsigned char* __restrict__ am, int NB,
                                    int H, int W, int C, int k, int st, int pd, int Ho, int Wo) {
   const int CC = C / 8;
-  const long long total = (long long)NB * Ho * Wo * CC;
-  GSTRIDE_LOOP(t, total) {
+  const I total = (I)NB * Ho * Wo * CC;
+  for (I t = blockIdx.x * (I)blockDim.x + threadIdx.x; t < total; t += (I)gridDim.x * blockDim.x) {
     const int cc = (int)(t % CC);
-    long long p = t / CC;
+    I p = t / CC;
     const int wo = (int)(p % Wo);
     p /= Wo;
     const int ho = (int)(p % Ho);
@@ -684,7 +686,7 @@ __global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restr
         const int iw = wo * st - pd + s2;
         if ((unsigned)iw >= (unsigned)W) continue;
         float v[8];
-        unpack8(*(const i4v*)(x + (((long long)n * H + ih) * W + iw) * C + cc * 8), v);
+        unpack8(*(const i4v*)(x + (((I)n * H + ih) * W + iw) * C + cc * 8), v);
 #pragma unroll
         for (int e = 0; e < 8; ++e)
           if (v[e] > m[e] || (v[e] != v[e] && m[e] == m[e])) { m[e] = v[e]; ai[e] = r * k + s2; }
@@ -702,15 +704,16 @@ __global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restr
 
 // backward from the saved argmax: each input pixel gathers dy of the (<= ceil(k/st)^2) windows
 // that contain it and chose it — one byte + one bf16 per window and channel, no recomputation
+template <typename I>
 __global__ void maxpool_bwd_am_kernel(const unsigned char* __restrict__ am,
                                       const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx,
                                       int NB, int H, int W, int C, int k, int st, int pd, int Ho,
                                       int Wo) {
   const int CC = C / 8;
-  const long long total = (long long)NB * H * W * CC;
-  GSTRIDE_LOOP(t, total) {
+  const I total = (I)NB * H * W * CC;
+  for (I t = blockIdx.x * (I)blockDim.x + threadIdx.x; t < total; t += (I)gridDim.x * blockDim.x) {
     const int cc = (int)(t % CC);
-    long long p = t / CC;
+    I p = t / CC;
     const int iw0 = (int)(p % W);
     p /= W;
     const int ih0 = (int)(p % H);
@@ -721,7 +724,7 @@ __global__ void maxpool_bwd_am_kernel(const unsigned char* __restrict__ am,
     for (int ho = ho_lo; ho <= ho_hi; ++ho)
       for (int wo = wo_lo; wo <= wo_hi; ++wo) {
         const int local = (ih0 - (ho * st - pd)) * k + (iw0 - (wo * st - pd));
-        const long long o = (((long long)n * Ho + ho) * Wo + wo) * C + cc * 8;
+        const I o = (((I)n * Ho + ho) * Wo + wo) * C + cc * 8;
         const unsigned long long a8 = *(const unsigned long long*)(am + o);
         float d[8];
         unpack8(*(const i4v*)(dy + o), d);
@@ -783,8 +786,12 @@ DDL_API int ddl_maxpool_fwd(const void* x, void* y, void* am, int NB, int H, int
   const int Ho = (H + 2 * pd - k) / st + 1, Wo = (W + 2 * pd - k) / st + 1;
   const long long total = (long long)NB * Ho * Wo * (C / 8);
   if (k > 15) return (int)hipErrorInvalidValue;  // argmax index must fit a byte
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s,
-                     (const bf16_t*)x, (bf16_t*)y, (unsigned char*)am, NB, H, W, C, k, st, pd, Ho, Wo);
+  if ((long long)NB * H * W * C < (1LL << 31) - 64)  // 32-bit offsets, one item per thread
+    hipLaunchKernelGGL(maxpool_fwd_kernel<int>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                       (const bf16_t*)x, (bf16_t*)y, (unsigned char*)am, NB, H, W, C, k, st, pd, Ho, Wo);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel<long long>, dim3(grid_for(total, 256)), dim3(256), 0, s,
+                       (const bf16_t*)x, (bf16_t*)y, (unsigned char*)am, NB, H, W, C, k, st, pd, Ho, Wo);
   return (int)hipGetLastError();
 }
 DDL_API int ddl_maxpool_bwd(const void* x, const void* dy, const void* am, void* dx, int NB, int H,
@@ -793,9 +800,14 @@ DDL_API int ddl_maxpool_bwd(const void* x, const void* dy, const void* am, void*
   const int Ho = (H + 2 * pd - k) / st + 1, Wo = (W + 2 * pd - k) / st + 1;
   const long long total = (long long)NB * H * W * (C / 8);
   if (am) {
-    hipLaunchKernelGGL(maxpool_bwd_am_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s,
-                       (const unsigned char*)am, (const bf16_t*)dy, (bf16_t*)dx, NB, H, W, C, k, st,
-                       pd, Ho, Wo);
+    if ((long long)NB * H * W * C < (1LL << 31) - 64)
+      hipLaunchKernelGGL(maxpool_bwd_am_kernel<int>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                         (const unsigned char*)am, (const bf16_t*)dy, (bf16_t*)dx, NB, H, W, C, k, st,
+                         pd, Ho, Wo);
+    else
+      hipLaunchKernelGGL(maxpool_bwd_am_kernel<long long>, dim3(grid_for(total, 256)), dim3(256), 0, s,
+                         (const unsigned char*)am, (const bf16_t*)dy, (bf16_t*)dx, NB, H, W, C, k, st,
+                         pd, Ho, Wo);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s,
