@@ -5,8 +5,9 @@ fallbacks, automatic halo / split-K), but the best tile moves with the client co
 1-8 clients per GPU the same ResNet-18 layer has a different winner (profiles/conv_halo_sweep_*,
 conv_wgrad_halo_r1.log; the FedAvg scaling runs put 8, 4, 2 and 1 clients on a GPU). So the first
 EAGER call of each (mode, shape, fused-epilogue) key times the heuristic and a short list of
-candidate tiles (streamed, halo-staged, halo WGRAD split counts) on scratch outputs, HIP events
-around a few back-to-back launches, and caches the fastest. Later calls — including the ones
+candidate tiles (streamed, halo-staged, halo WGRAD split counts) on scratch outputs, a few
+launches captured in a HIP graph and replayed (GPU time, not host launch cost), and caches the
+fastest. Later calls — including the ones
 captured into the training step's HIP graph — use the cached pick. A key first met during graph
 capture runs the heuristic (nothing is timed inside a capture).
 
@@ -73,15 +74,25 @@ def _key(mode, geom, flags):
             geom.pad, flags)
 
 
-def _time(run, cfg, sp, reps=4) -> float:
-    run(cfg, sp)  # warm (and validity: raises on an ineligible tile)
+def _time(run, cfg, sp, reps=8) -> float:
+    """GPU time per launch: ``reps`` launches captured in one HIP graph and replayed. Timing eager
+    launches measured the host instead on few-client shapes, whose kernels (5-25 us) are shorter
+    than the Python + launch cost of a call: the picks then varied run to run (a 1-client layer-1
+    forward drew a 128x256 tile at 25 us in one run, 64x256 at 19.5 us in another)."""
+    run(cfg, sp)  # warm (and validity: raises on an ineligible tile), outside the capture
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for _ in range(reps):
+            run(cfg, sp)
+    graph.replay()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
-    for _ in range(reps):
-        run(cfg, sp)
+    for _ in range(3):
+        graph.replay()
     b.record()
     b.synchronize()
-    return a.elapsed_time(b) / reps
+    return a.elapsed_time(b) / (3 * reps)
 
 
 def pick(mode: str, geom, flags: tuple, run, accumulate: bool = True):
