@@ -11,6 +11,12 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP kernels on device)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+    # under pytest-xdist, split the CPUs between the workers: the tabular nets' tiny CPU ops
+    # with every worker running all-core intra-op pools were up to 40x slower than serial
+    workers = int(os.environ.get("PYTEST_XDIST_WORKER_COUNT", "0") or 0)
+    if workers > 1:
+        import torch
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // workers))
 
 
 @pytest.fixture
