@@ -48,6 +48,10 @@ def candidates(mode: str, geom, accumulate: bool = True) -> list:
         out += [(_cfg(*t), 0) for t in _FD_TILES if red % t[2] == 0]
         out += [(_cfg(bp, bq, 32, ns, True), 0) for bp, bq, ns in _FD_HALO
                 if halo_eligible(geom, bq, ns) and red % 32 == 0]
+        if geom.R * geom.S * red >= 2304:  # deep reductions: split-K (+ its epilogue pass) too
+            out += [(None, s) for s in (2, 4, 8)]
+            if red % 64 == 0:
+                out += [(_cfg(64, 64, 64, 3), s) for s in (2, 4)]
     else:
         out += [(_cfg(*t), 0) for t in _WG_TILES if accumulate]
         if accumulate:  # the heuristic tile at explicit split-K depths (small grids: 1-2 clients)
