@@ -57,6 +57,9 @@ def candidates(mode: str, geom, accumulate: bool = True) -> list:
         if accumulate:  # the heuristic tile at explicit split-K depths (small grids: 1-2 clients)
             nk = geom.N * geom.P * geom.Q // 32
             out += [(None, s) for s in (4, 8, 16, 32, 64) if s <= max(1, nk // 8)]
+            # and the small tiles at explicit depths (few tiles per client: deep layers, 1 client)
+            out += [(_cfg(*t), s) for t in ((64, 64, 64, 3), (128, 64, 64, 3), (64, 128, 32, 4))
+                    for s in (8, 16, 32) if s <= max(1, nk // 8)]
         if accumulate and wgrad_halo_eligible(geom):
             tiles = (geom.K // 64) * (geom.C // 32) * geom.G
             nk = geom.N * geom.H * geom.W // 32
