@@ -214,6 +214,31 @@ def test_batchnorm(cuda):
     _close(sc2, sc_r, rel=1e-4); _close(sh2, sh_r, rel=1e-4)
 
 
+def test_bn_reduce_wide_channels(cuda):
+    """2048-channel reduces (ResNet-50's last stage): the grid is capped by the stripes' atomic
+    budget, so each block sweeps many rows (4 in flight per thread). Sums == fp32 references."""
+    G, N, H, W, C = 1, 4, 32, 32, 2048
+    x = _rand(G, N, H, W, C, dev=cuda) + 0.3
+    dy = _rand(G, N, H, W, C, dev=cuda)
+    y = _rand(G, N, H, W, C, dev=cuda)
+    xf = x.float().reshape(G, -1, C)
+    st = Fn.bn_stats(x)
+    _close(st.sum(1), torch.stack([xf.sum(1), (xf * xf).sum(1)], 1).cpu(), rel=1e-3)
+    mu = torch.randn(G, C, device=cuda) * 0.1
+    rs = torch.rand(G, C, device=cuda) + 0.5
+    dg = torch.zeros(G, C, device=cuda); db = torch.zeros(G, C, device=cuda)
+    sums = Fn.bn_bwd_reduce(dy, y, x, mu, rs, dg, db)
+    dg_r = torch.zeros(G, C); db_r = torch.zeros(G, C)
+    sums_r = ref.bn_bwd_reduce(dy.cpu(), y.cpu(), x.cpu(), mu.cpu(), rs.cpu(), dg_r, db_r)
+    _close(sums, sums_r, rel=2e-3)
+    # pool backward with the BN reduce at the same width
+    dp = _rand(G, N, C, dev=cuda)
+    dx, part = Fn.avgpool_bwd_bn(dp, x, (y, mu, rs))
+    dx_r, part_r = Fn.avgpool_bwd_bn(dp.cpu(), x.cpu(), (y.cpu(), mu.cpu(), rs.cpu()))
+    _close(dx, dx_r, rel=1e-2)
+    _close(part.sum(1), part_r.sum(1), rel=2e-3)
+
+
 def test_bn_dual_finalize_and_backward(cuda):
     """bn_finalize2 / bn_backward2 (a block's output BN and its shortcut's BN in one launch each)
     == the single-BN kernels, including the running statistics and d(gamma) / d(beta)."""
