@@ -22,6 +22,7 @@ import torch
 from . import workspace as ws
 
 ENABLED = os.environ.get("DDL_CONV_AUTOTUNE", "1") != "0"
+EAGER_TIMING = os.environ.get("DDL_TUNE_EAGER", "0") == "1"
 _CACHE: dict = {}
 
 _FD_TILES = [(64, 128, 32, 4), (128, 128, 32, 3), (128, 128, 64, 2), (128, 256, 32, 2),
@@ -87,6 +88,14 @@ def _time(run, cfg, sp, reps=8) -> float:
     than the Python + launch cost of a call: the picks then varied run to run (a 1-client layer-1
     forward drew a 128x256 tile at 25 us in one run, 64x256 at 19.5 us in another)."""
     run(cfg, sp)  # warm (and validity: raises on an ineligible tile), outside the capture
+    if EAGER_TIMING:  # the round-1 method, kept for A/B
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(4):
+            run(cfg, sp)
+        b.record()
+        b.synchronize()
+        return a.elapsed_time(b) / 4
     torch.cuda.synchronize()
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
