@@ -21,6 +21,7 @@ from ..data.text import SPTokenizer, TinyStories
 from ..models.llama import LLama, causalLLMLoss, split_stages
 from ..parallel.dp import GradBucketer, average_weights, broadcast_parameters
 from ..parallel.pipeline import PipelineStage, grid_ranks
+from ..runtime.graphs import CAPTURE_MODE
 
 
 @dataclass
@@ -129,7 +130,7 @@ def train_llm(cfg: LLMConfig, ctx, log=print, warmup: int = 0) -> dict:
                     body(sx)
             torch.cuda.current_stream().wait_stream(side)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
                 out = body(sx)
             for t, v in zip((opt.data, opt.m, opt.v, opt.t_dev), snap):
                 t.copy_(v)

@@ -17,6 +17,7 @@ import torch
 
 from .. import optim
 from ..data.split import plan_epoch
+from ..runtime.graphs import CAPTURE_MODE
 
 
 class LocalTrainer:
@@ -88,7 +89,7 @@ class LocalTrainer:
         # frozen first_step=False inside the graph is exact for every step of a round
         assert opt.dampening == 0.0
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, capture_error_mode=CAPTURE_MODE):
             for i in range(nsteps):
                 loss = self._step(plan[i], 0, G)
             if tl is not None:

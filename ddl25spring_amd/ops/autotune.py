@@ -20,6 +20,7 @@ import os
 import torch
 
 from . import workspace as ws
+from ..runtime.graphs import CAPTURE_MODE
 
 ENABLED = os.environ.get("DDL_CONV_AUTOTUNE", "1") != "0"
 EAGER_TIMING = os.environ.get("DDL_TUNE_EAGER", "0") == "1"
@@ -98,7 +99,7 @@ def _time(run, cfg, sp, reps=8) -> float:
         return a.elapsed_time(b) / 4
     torch.cuda.synchronize()
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
+    with torch.cuda.graph(graph, capture_error_mode=CAPTURE_MODE):
         for _ in range(reps):
             run(cfg, sp)
     graph.replay()

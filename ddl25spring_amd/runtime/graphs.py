@@ -19,6 +19,12 @@ from __future__ import annotations
 
 import torch
 
+# Capture mode of every HIP graph the framework records: errors only on unsafe calls of the
+# capturing thread. Under "global" (torch's default) an unsafe call on ANY thread fails the
+# capture, e.g. a collective library's watchdog thread polling its work events while a
+# multi-rank run (bench.py over RCCL) captures its first round.
+CAPTURE_MODE = "thread_local"
+
 
 class CapturedStep:
     def __init__(self, fn, warmup: int = 2, enabled: bool = True):
@@ -42,7 +48,7 @@ class CapturedStep:
             return out
         if self.graph is None:
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
+            with torch.cuda.graph(self.graph, capture_error_mode=CAPTURE_MODE):
                 self.out = self.fn()
         self.calls += 1
         self.graph.replay()
