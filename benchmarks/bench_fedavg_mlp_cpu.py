@@ -20,6 +20,10 @@ def main():
     from ddl25spring_amd.models import mnist_mlp
     from ddl25spring_amd.runtime import dist as rdist
     ctx = rdist.init(backend="gloo", device="cpu")
+    # torchrun exports OMP_NUM_THREADS=1 to every rank; give each rank its share of the cores
+    import os
+    import torch
+    torch.set_num_threads(max(1, (os.cpu_count() or 1) // ctx.world))
     train = load_images("mnist", True, args.train_size)
     parts = split(2, True, 10, labels=train.labels)
     fa = FedAvg(mnist_mlp, DeviceImageDataset(train, "cpu"), parts, lr=0.01, batch_size=100,

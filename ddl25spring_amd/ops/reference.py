@@ -23,8 +23,24 @@ def nchw_to_nhwc(x: torch.Tensor) -> torch.Tensor:
     return x.permute(0, 2, 3, 1)
 
 
+def _is_gemm(geom) -> bool:
+    """1x1 / stride 1 / no padding (every Linear layer): the conv is a plain GEMM over pixels."""
+    return geom.R == 1 and geom.S == 1 and geom.stride == 1 and geom.pad == 0
+
+
 def conv_fwd(x, w, geom, bias=None, relu=False, stats=None):
     G = geom.G
+    if _is_gemm(geom):  # one batched matmul over the client groups (the CPU MLP path)
+        y = torch.bmm(x.float().reshape(G, -1, geom.C), w.float().reshape(G, geom.K, geom.C).transpose(1, 2))
+        if bias is not None:
+            y = y + bias.float().reshape(G, 1, geom.K)
+        if relu:
+            y = y.clamp_min(0)
+        if stats is not None:
+            st = stats[:, 0] if stats.dim() == 4 else stats
+            st[:, 0] += y.sum(1)
+            st[:, 1] += (y * y).sum(1)
+        return _bf(y).reshape(G, geom.N, geom.P, geom.Q, geom.K)
     outs = []
     for g in range(G):
         xi = nhwc_to_nchw(x[g].float())
@@ -45,6 +61,15 @@ def conv_fwd(x, w, geom, bias=None, relu=False, stats=None):
 
 
 def conv_dgrad(dy, w, geom, residual=None, mask=None):
+    if _is_gemm(geom):
+        G = geom.G
+        dx = torch.bmm(dy.float().reshape(G, -1, geom.K), w.float().reshape(G, geom.K, geom.C))
+        dx = dx.reshape(G, geom.N, geom.H, geom.W, geom.C)
+        if residual is not None:
+            dx = dx + residual.float()
+        if mask is not None:
+            dx = dx * (mask.float() > 0)
+        return _bf(dx).contiguous()
     outs = []
     for g in range(geom.G):
         dyi = nhwc_to_nchw(dy[g].float())
@@ -61,6 +86,15 @@ def conv_dgrad(dy, w, geom, residual=None, mask=None):
 
 
 def conv_wgrad(dy, x, geom, dw, accumulate=True):
+    if _is_gemm(geom):
+        G = geom.G
+        gw = torch.bmm(dy.float().reshape(G, -1, geom.K).transpose(1, 2), x.float().reshape(G, -1, geom.C))
+        gw = gw.reshape(G, geom.K, 1, 1, geom.C)
+        if accumulate:
+            dw += gw
+        else:
+            dw.copy_(gw)
+        return
     for g in range(geom.G):
         dyi = nhwc_to_nchw(dy[g].float())
         xi = nhwc_to_nchw(x[g].float())
