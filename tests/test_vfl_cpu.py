@@ -156,6 +156,9 @@ def _vae_models():
 
 def _vfl_worker(rank, world, port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    # one intra-op thread on both sides: Adam turns float-reduction-order noise on (near-)zero
+    # gradients into full +-lr steps, so the reductions must run in the same order
+    torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from ddl25spring_amd.vfl import SplitNNParty, SplitNNServer, VAEParty, VAEServer
     bottoms, top, xs, y = _splitnn_models()
@@ -184,6 +187,15 @@ def _vfl_worker(rank, world, port, out_dir):
 
 
 def test_distributed_vfl_matches_single_process():
+    nthreads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        _check_distributed_vfl()
+    finally:
+        torch.set_num_threads(nthreads)
+
+
+def _check_distributed_vfl():
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_vfl_worker, args=(3, 29877, d), nprocs=3, join=True)
         res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(3)]
@@ -225,6 +237,9 @@ def test_distributed_vfl_matches_single_process():
 
 def _active_worker(rank, world, port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    # one intra-op thread on both sides: Adam turns float-reduction-order noise on (near-)zero
+    # gradients into full +-lr steps, so the reductions must run in the same order
+    torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from ddl25spring_amd.vfl import SplitNNParty, SplitNNServer
     bottoms, top, xs, y = _splitnn_models()
