@@ -74,6 +74,10 @@ struct ConvArgs {
   // the gradient of a 1x1 / stride-2 projection shortcut, computed without the 3/4 zero pixels.
   long long res_gs;
   int res_sub;
+  // WGRAD: every dW contribution is multiplied by gscale before it is added. gscale = -lr with
+  // `out` = the fp32 master weights applies a plain SGD step inside the backward ("direct SGD",
+  // fl/local.py): no gradient buffer to zero or re-read for the conv weights.
+  float gscale;
 };
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
@@ -918,6 +922,7 @@ __device__ __forceinline__ void conv_body(const ConvArgs& a, char* smem, int lin
   } else {  // WGRAD: dW[p=k][q=rsc] fp32
     float* O = (float*)a.out + (long long)g * a.out_gs;
     const bool atomic = a.accumulate || gy > 1;
+    const float gs = a.gscale;
 #pragma unroll
     for (int ti = 0; ti < TP; ++ti) {
 #pragma unroll
@@ -930,8 +935,8 @@ __device__ __forceinline__ void conv_body(const ConvArgs& a, char* smem, int lin
           const int p = p0 + wp * WP + ti * 16 + lp + e;
           if (p < Pd && q < Qd) {
             float* dst = O + (long long)p * Qd + q;
-            if (atomic) atomicAdd(dst, acc[ti][tj][e]);
-            else *dst = acc[ti][tj][e];
+            if (atomic) atomicAdd(dst, gs * acc[ti][tj][e]);
+            else *dst = gs * acc[ti][tj][e];
           }
         }
       }

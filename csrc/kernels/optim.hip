@@ -107,5 +107,44 @@ DDL_API int ddl_adam(const AdamArgs* a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// Plain SGD (no momentum / weight decay) over rows [rows][P] whose first Pd columns were already
+// updated inside the backward (conv WGRAD atomics of -lr * dW straight into the master weights,
+// ConvArgs::gscale): those columns only refresh the bf16 shadow (6 B/param instead of the 14 B of
+// sgd_kernel, and no zero-fill of their gradients). Columns >= Pd (BatchNorm, classifier head) take
+// the ordinary step and have their gradient zeroed for the next step in the same pass.
+struct SGDDirectArgs {
+  float* p; float* g; bf16_t* shadow;
+  long long rows, P, Pd;
+  float lr, grad_scale;
+};
+
+__global__ __launch_bounds__(256) void sgd_direct_kernel(SGDDirectArgs a) {
+  const long long n4 = a.rows * a.P / 4;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < n4;
+       t += (long long)gridDim.x * blockDim.x) {
+    const long long e = t * 4;
+    const long long col = e % a.P;
+    float4 pv = *(const float4*)(a.p + e);
+    if (col >= a.Pd) {
+      const float4 gv = *(const float4*)(a.g + e);
+      const float s = a.lr * a.grad_scale;
+      pv.x -= s * gv.x; pv.y -= s * gv.y; pv.z -= s * gv.z; pv.w -= s * gv.w;
+      *(float4*)(a.p + e) = pv;
+      *(float4*)(a.g + e) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    i2v o;
+    o[0] = (int)pack_bf2(pv.x, pv.y);
+    o[1] = (int)pack_bf2(pv.z, pv.w);
+    *(i2v*)(a.shadow + e) = o;
+  }
+}
+
+DDL_API int ddl_sgd_direct(const SGDDirectArgs* a, hipStream_t s) {
+  if (a->P % 4 || a->Pd % 4 || a->Pd > a->P) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(sgd_direct_kernel, dim3(grid_for(a->rows * a->P / 4, 256)), dim3(256), 0, s, *a);
+  return (int)hipGetLastError();
+}
+
+DDL_API int ddl_sgd_direct_args_size() { return (int)sizeof(SGDDirectArgs); }
 DDL_API int ddl_sgd_args_size() { return (int)sizeof(SGDArgs); }
 DDL_API int ddl_adam_args_size() { return (int)sizeof(AdamArgs); }

@@ -12,6 +12,8 @@ DataLoader and copied host<->device every round). Here:
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -20,16 +22,26 @@ from ..data.split import plan_epoch
 from ..runtime.graphs import CAPTURE_MODE
 
 
+# Direct SGD (default on the GPU for plain SGD): the conv weights' WGRAD launches add -lr * dW
+# straight into the fp32 master weights (ParamStore.direct_update), so a step skips zero-filling
+# and re-reading their gradients and its optimizer launch only refreshes their bf16 shadow.
+# DDL_DIRECT_SGD=0 keeps gradient buffer + fused SGD launch.
+DIRECT_SGD = os.environ.get("DDL_DIRECT_SGD", "1") != "0"
+
+
 class LocalTrainer:
     def __init__(self, net, data, lr: float, batch_size: int, momentum: float = 0.0,
                  weight_decay: float = 0.0, planner: str = "native", use_graph: bool | None = None,
-                 label_transform=None):
+                 label_transform=None, direct: bool | None = None):
         self.net, self.data = net, data
         self.B = batch_size
         self.opt = optim.SGD(net, lr=lr, momentum=momentum, weight_decay=weight_decay)
         self.planner = planner
         dev = net.device
         self.use_graph = (dev.type == "cuda") if use_graph is None else (use_graph and dev.type == "cuda")
+        eligible = momentum == 0.0 and weight_decay == 0.0 and net.store.Pd > 0 \
+            and getattr(net, "grad_hook", None) is None
+        self.direct = eligible and (DIRECT_SGD and dev.type == "cuda" if direct is None else direct)
         self.label_transform = label_transform  # callable(y [G,B], g0, g1) -> y (attacks); with a
         # ``graph_key`` attribute it is pure device ops and may be captured in the round graph
         self._graphs: dict = {}
@@ -42,9 +54,14 @@ class LocalTrainer:
         if self.label_transform is not None:
             y = self.label_transform(y, g0, g1)
         with st.select(g0, g1):
-            st.grad[g0:g1].zero_()
-            loss, _ = net.train_step(x, y)
-            self.opt.select(g0, g1).step()
+            if self.direct:  # the previous step_direct left the non-conv gradients zeroed
+                with st.direct_update(self.opt.lr):
+                    loss, _ = net.train_step(x, y)
+                self.opt.select(g0, g1).step_direct()
+            else:
+                st.grad[g0:g1].zero_()
+                loss, _ = net.train_step(x, y)
+                self.opt.select(g0, g1).step()
         return loss
 
     # ---------------------------------------------------------------- graph-captured round
@@ -111,6 +128,8 @@ class LocalTrainer:
         if G == 0:
             return 0
         self.opt.reset_state()
+        if self.direct:
+            self.net.store.grad[:G].zero_()  # direct steps keep it zero from here on
         sizes = {len(s) for s in slot_indices}
         samples = 0
         for ep in range(epochs):

@@ -107,7 +107,8 @@ class ConvUnit(Layer):
             w = torch.empty(cout_t, cin_t, k, k)
             init_w(w, gen)
             t[:cout_t, :, :, :cin_t] = w.permute(0, 2, 3, 1)
-        self.w = store.add(p + ".weight", shape, winit)
+        # conv weights (not Linear ones: a fused classifier head writes those) take direct SGD
+        self.w = store.add(p + ".weight", shape, winit, direct=not self.linear)
         if self.bias:
             binit = uniform_bias_(self.fan_in)
 

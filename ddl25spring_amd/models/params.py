@@ -35,6 +35,7 @@ class Spec:
     buffer: bool = False
     offset: int = 0
     numel: int = 0
+    direct: bool = False  # gradient comes only from conv WGRAD launches (direct-SGD eligible)
 
 
 def kaiming_uniform_(fan_in: int, a: float = math.sqrt(5)):
@@ -76,9 +77,12 @@ class ParamStore:
         self.data = self.grad = self.shadow = self.buffers = None
         self.device = torch.device("cpu")
         self._shadow_version = -1
+        self.Pd = 0              # columns [0, Pd): the direct-eligible params (laid out first)
+        self.direct_mode = False
+        self._direct_lr = 0.0
 
     # ---------------------------------------------------------------- declaration
-    def add(self, name: str, shape, init, buffer: bool = False) -> str:
+    def add(self, name: str, shape, init, buffer: bool = False, direct: bool = False) -> str:
         if name in self.specs:
             raise KeyError(f"duplicate parameter {name}")
         shape = tuple(int(s) for s in shape)
@@ -90,13 +94,27 @@ class ParamStore:
         else:
             off = self.P
             self.P += (n + 15) // 16 * 16
-        self.specs[name] = Spec(name, shape, init, buffer, off, n)
+        self.specs[name] = Spec(name, shape, init, buffer, off, n, direct and not buffer)
         return name
+
+    def _layout(self):
+        """Direct-eligible params first ([0, Pd)), the rest after, each in declaration order (the
+        init RNG draws in declaration order whatever the layout)."""
+        off = 0
+        for want in (True, False):
+            for s in self.specs.values():
+                if not s.buffer and s.direct == want:
+                    s.offset = off
+                    off += (s.numel + 15) // 16 * 16
+            if want:
+                self.Pd = off
+        assert off == self.P
 
     # ---------------------------------------------------------------- materialise
     def materialize(self, device, seed: int = 0, generator: torch.Generator | None = None):
         device = torch.device(device)
         self.device = device
+        self._layout()
         G = self.G
         gen = generator if generator is not None else torch.Generator().manual_seed(seed)
         data = torch.zeros(G, max(self.P, 16), dtype=torch.float32)
@@ -153,7 +171,31 @@ class ParamStore:
         return self._view(self.data, self.specs[name])
 
     def grad_of(self, name):
-        return self._view(self.grad, self.specs[name])
+        s = self.specs[name]
+        if self.direct_mode and s.direct:
+            v = self._view(self.data, s)
+            v._ddl_wscale = -self._direct_lr  # read by Fn.wgrad_scale: the WGRAD adds -lr * dW
+            return v
+        return self._view(self.grad, s)
+
+    class _Direct:
+        def __init__(self, store, lr):
+            self.store, self.lr = store, float(lr)
+
+        def __enter__(self):
+            st = self.store
+            self.prev = (st.direct_mode, st._direct_lr)
+            st.direct_mode, st._direct_lr = True, self.lr
+            return st
+
+        def __exit__(self, *a):
+            self.store.direct_mode, self.store._direct_lr = self.prev
+
+    def direct_update(self, lr: float):
+        """Context: the conv weights' (``Spec.direct``) WGRAD launches add ``-lr * dW`` straight into
+        the fp32 master weights instead of a zeroed gradient buffer — a plain SGD step (no momentum /
+        weight decay) fused into the backward. Finish the step with ``optim.SGD.step_direct``."""
+        return ParamStore._Direct(self, lr)
 
     def shadow_of(self, name):
         return self._view(self.shadow, self.specs[name])

@@ -43,7 +43,7 @@ class ConvArgs(ctypes.Structure):
                 ("S", i32), ("P", i32), ("Q", i32), ("stride", i32), ("pad", i32),
                 ("relu", i32), ("accumulate", i32), ("split_k", i32), ("stats_stripes", i32),
                 ("bn_x", vp), ("bn_mean", vp), ("bn_rstd", vp), ("partial", vp), ("partial_cap", i64),
-                ("mask_scale", vp), ("mask_shift", vp), ("res_gs", i64), ("res_sub", i32)]
+                ("mask_scale", vp), ("mask_shift", vp), ("res_gs", i64), ("res_sub", i32), ("gscale", f32)]
 
 
 class BNArgs(ctypes.Structure):
@@ -70,6 +70,11 @@ class SGDArgs(ctypes.Structure):
     _fields_ = [("p", vp), ("g", vp), ("mom", vp), ("shadow", vp), ("n", i64), ("lr", f32),
                 ("wd", f32), ("momentum", f32), ("dampening", f32), ("grad_scale", f32),
                 ("nesterov", i32), ("first_step", i32)]
+
+
+class SGDDirectArgs(ctypes.Structure):
+    _fields_ = [("p", vp), ("g", vp), ("shadow", vp), ("rows", i64), ("P", i64), ("Pd", i64),
+                ("lr", f32), ("grad_scale", f32)]
 
 
 class AdamArgs(ctypes.Structure):
@@ -121,6 +126,7 @@ _SIGS = {
     "ddl_head_train": [ctypes.POINTER(HeadArgs), vp],
     # optim.hip
     "ddl_sgd": [ctypes.POINTER(SGDArgs), vp],
+    "ddl_sgd_direct": [ctypes.POINTER(SGDDirectArgs), vp],
     "ddl_adam": [ctypes.POINTER(AdamArgs), vp],
     # aggregate.hip
     "ddl_weighted_sum": [vp, i64, vp, i32, i64, vp, i32, vp],
@@ -169,6 +175,7 @@ def kernels():
                                    ("BNBwdArgs", "ddl_bn_bwd_args_size", BNBwdArgs),
                                    ("HeadArgs", "ddl_head_args_size", HeadArgs),
                                    ("SGDArgs", "ddl_sgd_args_size", SGDArgs),
+                                   ("SGDDirectArgs", "ddl_sgd_direct_args_size", SGDDirectArgs),
                                    ("AdamArgs", "ddl_adam_args_size", AdamArgs)):
             f = getattr(lib, size_fn)
             f.restype = ctypes.c_int

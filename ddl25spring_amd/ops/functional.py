@@ -127,6 +127,7 @@ def _conv_args(geom: ConvGeom, device=None, split_k: int = 0, partial: bool = Fa
             if pw is not None:
                 a.partial, a.partial_cap = pw.data_ptr(), pw.numel()
     a.split_k = split_k
+    a.gscale = 1.0
     for k, v in kw.items():
         setattr(a, k, v)
     a.G, a.N, a.H, a.W, a.C, a.K = geom.G, geom.N, geom.H, geom.W, geom.C, geom.K
@@ -279,9 +280,20 @@ def _dgrad_args(dy, w, geom, dx, residual, mask, bn, mask_bn, split_k, residual_
     return a, part
 
 
+def wgrad_scale(dw) -> float:
+    """Scale of every WGRAD contribution into ``dw`` (ConvArgs::gscale): 1, or -lr for a view of the
+    fp32 master weights handed out by ``ParamStore.grad_of`` under ``direct_update`` (the backward
+    itself then applies the plain SGD step to those weights)."""
+    return getattr(dw, "_ddl_wscale", 1.0)
+
+
 def _wgrad_args(dy, x, geom, dw, accumulate, splits):
+    gscale = wgrad_scale(dw)
+    if gscale != 1.0 and not accumulate:
+        raise ValueError("a scaled WGRAD must accumulate (it adds into the master weights)")
     return _conv_args(geom, dy.device, 1 if not accumulate else int(splits), x=ptr(x), dy=ptr(dy),
-                      out=ptr(dw), x_gs=_gs(x), dy_gs=_gs(dy), out_gs=_gs(dw), accumulate=int(accumulate))
+                      out=ptr(dw), x_gs=_gs(x), dy_gs=_gs(dy), out_gs=_gs(dw), accumulate=int(accumulate),
+                      gscale=gscale)
 
 
 def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0, _tune=True):
@@ -289,7 +301,7 @@ def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0, _tun
     cfg = conv_cfg(bp, bq, bk, stages) (0: tuned default); splits = split-K slices (0: auto).
     Inside ``wgrad_overlap`` the launch goes to the side stream (see there)."""
     if not dy.is_cuda:
-        ref.conv_wgrad(dy, x, geom, dw, accumulate)
+        ref.conv_wgrad(dy, x, geom, dw, accumulate, wgrad_scale(dw))
         return dw
     _check_inner(dy, "dy"); _check_inner(x, "x"); _check_inner(dw, "dw")
     if _tune and cfg == 0 and splits == 0 and autotune.ENABLED:
@@ -1058,6 +1070,22 @@ def sgd_step(p, g, mom, shadow, lr, wd=0.0, momentum=0.0, dampening=0.0, nestero
     a.lr, a.wd, a.momentum, a.dampening, a.grad_scale = lr, wd, momentum, dampening, grad_scale
     a.nesterov, a.first_step = int(nesterov), int(first_step)
     check(_lib.kernels().ddl_sgd(ctypes.byref(a), stream()), "sgd")
+
+
+def sgd_direct_step(p, g, shadow, Pd: int, lr: float, grad_scale: float = 1.0):
+    """Finish a direct-SGD step over rows p/g/shadow [rows, P]: columns [0, Pd) (the conv weights,
+    already stepped by the scaled WGRAD) only refresh the bf16 shadow; columns >= Pd take
+    ``p -= lr * grad_scale * g`` and get their gradient zeroed. One launch."""
+    if not p.is_cuda:
+        ref.sgd_direct(p, g, shadow, Pd, lr, grad_scale)
+        return
+    assert p.dim() == 2 and p.is_contiguous() and g.is_contiguous() and shadow.is_contiguous()
+    assert p.shape == g.shape == shadow.shape and p.shape[1] % 4 == 0 and Pd % 4 == 0
+    a = _lib.SGDDirectArgs()
+    a.p, a.g, a.shadow = ptr(p), ptr(g), ptr(shadow)
+    a.rows, a.P, a.Pd = p.shape[0], p.shape[1], Pd
+    a.lr, a.grad_scale = lr, grad_scale
+    check(_lib.kernels().ddl_sgd_direct(ctypes.byref(a), stream()), "sgd_direct")
 
 
 def adam_step(p, g, m, v, shadow, lr, beta1, beta2, eps, wd, step, decoupled, grad_scale=1.0,

@@ -85,11 +85,13 @@ def conv_dgrad(dy, w, geom, residual=None, mask=None):
     return _bf(torch.stack(outs)).contiguous()
 
 
-def conv_wgrad(dy, x, geom, dw, accumulate=True):
+def conv_wgrad(dy, x, geom, dw, accumulate=True, scale=1.0):
     if _is_gemm(geom):
         G = geom.G
         gw = torch.bmm(dy.float().reshape(G, -1, geom.K).transpose(1, 2), x.float().reshape(G, -1, geom.C))
         gw = gw.reshape(G, geom.K, 1, 1, geom.C)
+        if scale != 1.0:
+            gw = gw * scale
         if accumulate:
             dw += gw
         else:
@@ -101,6 +103,8 @@ def conv_wgrad(dy, x, geom, dw, accumulate=True):
         gw = torch.nn.grad.conv2d_weight(xi, (geom.K, geom.C, geom.R, geom.S), dyi, geom.stride,
                                          geom.pad)
         gw = gw.permute(0, 2, 3, 1)  # [K, R, S, C]
+        if scale != 1.0:
+            gw = gw * scale
         if accumulate:
             dw[g] += gw
         else:
@@ -303,6 +307,15 @@ def sgd(p, g, mom, shadow, lr, wd, momentum, dampening, nesterov, first_step, gr
             mom.mul_(momentum).add_((1 - dampening) * d)
         d = d + momentum * mom if nesterov else mom
     p.sub_(lr * d)
+    if shadow is not None:
+        shadow.copy_(p.to(shadow.dtype))
+
+
+def sgd_direct(p, g, shadow, Pd, lr, grad_scale=1.0):
+    """Columns [0, Pd) were updated inside the backward: shadow refresh only; the rest take a
+    plain SGD step and have their gradient zeroed (optim.hip sgd_direct_kernel)."""
+    p[:, Pd:].sub_(lr * grad_scale * g[:, Pd:])
+    g[:, Pd:].zero_()
     if shadow is not None:
         shadow.copy_(p.to(shadow.dtype))
 

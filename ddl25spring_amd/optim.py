@@ -62,6 +62,17 @@ class SGD(_Base):
         st._shadow_version = st.data._version
         self.steps += 1
 
+    def step_direct(self, grad_scale: float = 1.0):
+        """Finish a step whose conv-weight part the backward already applied
+        (``ParamStore.direct_update``): shadow refresh for those, plain SGD + gradient zeroing for
+        the rest, in one launch. Only for momentum- and weight-decay-free SGD."""
+        assert self.mom is None and self.weight_decay == 0.0
+        st = self.store
+        Fn.sgd_direct_step(self._rows(st.data), self._rows(st.grad), self._rows(st.shadow), st.Pd,
+                           self.lr, grad_scale)
+        st._shadow_version = st.data._version
+        self.steps += 1
+
     def reset_state(self):
         self.steps = 0
         if self.mom is not None:

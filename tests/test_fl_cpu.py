@@ -282,3 +282,34 @@ def test_checkpoint_resume_under_gaussian_attack(fp32):
         b = FedAvg(mnist_mlp, data, parts, attack=GaussianNoise([1], sigma=0.1, seed=9), **kw)
         ckpt.run_with_checkpoints(b, 3, path)
     assert torch.equal(b.w_global, ref.w_global)
+
+
+@pytest.mark.parametrize("model", ["mnist_cnn", "resnet_tiny"])
+def test_direct_sgd_matches_gradient_sgd(fp32, model):
+    """Direct SGD (conv WGRAD adds -lr*dW straight into the master weights, then one launch
+    refreshes the shadow and steps the non-conv params) == zero grads + backward + fused SGD."""
+    from ddl25spring_amd.fl.local import LocalTrainer
+    from ddl25spring_amd.models import mnist_cnn
+    from ddl25spring_amd.models.resnet import BasicBlock, _resnet
+    if model == "mnist_cnn":
+        arr, data = _data(120)
+        make = mnist_cnn
+    else:
+        arr = synthetic_images("cifar10", 48, seed=0)
+        data = DeviceImageDataset(arr, "cpu")
+        make = lambda groups: _resnet(BasicBlock, (1, 1, 0, 0), 10, groups, "cifar")  # noqa: E731
+    parts = split(2, True, 10, labels=arr.labels)
+    out = []
+    for direct in (False, True):
+        net = make(groups=2).to("cpu", seed=3)
+        data.set_input_spec(net.input_spec)
+        assert 0 < net.store.Pd < net.store.P
+        tr = LocalTrainer(net, data, 0.05, 8, use_graph=False, direct=direct)
+        assert tr.direct == direct
+        tr.run([np.asarray(p) for p in parts], [11, 12], epochs=1)
+        out.append((net.store.data.clone(), net.store.shadow.clone(), net.store.grad.clone()))
+    (w0, s0, g0), (w1, s1, g1) = out
+    assert torch.allclose(w0, w1, atol=1e-5, rtol=1e-4), (w0 - w1).abs().max()
+    assert torch.allclose(s1, w1.to(s1.dtype))
+    Pd = net.store.Pd
+    assert torch.count_nonzero(g1[:, Pd:]) == 0  # non-conv grads left zeroed for the next step
