@@ -3,7 +3,7 @@ import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-marker = sys.argv[2] if len(sys.argv) > 2 else "sgd_kernel"
+marker = sys.argv[2] if len(sys.argv) > 2 else "sgd_"
 idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
 a, b = idx[-3], idx[-2]
 tot = 0.0
