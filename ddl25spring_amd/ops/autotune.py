@@ -23,6 +23,7 @@ from . import workspace as ws
 from ..runtime.graphs import CAPTURE_MODE
 
 ENABLED = os.environ.get("DDL_CONV_AUTOTUNE", "1") != "0"
+LOG = os.environ.get("DDL_TUNE_LOG", "0") == "1"  # print every candidate's time (stderr)
 EAGER_TIMING = os.environ.get("DDL_TUNE_EAGER", "0") == "1"
 _CACHE: dict = {}
 
@@ -131,6 +132,9 @@ def pick(mode: str, geom, flags: tuple, run, accumulate: bool = True):
                 t = _time(run, cfg, sp)
             except KernelError:
                 continue
+            if LOG:
+                import sys
+                print(f"[tune] {key} cfg={cfg} splits={sp} {t * 1e3:.1f} us", file=sys.stderr)
             if t < best_t * 0.97 or (cfg is None and t < best_t):  # ties keep the heuristic
                 best, best_t = (cfg, sp), t
     finally:

@@ -12,6 +12,12 @@ run resnet50 300 python benchmarks/bench_resnet50_dp.py --steps 10 --warmup 3
 run llm 300 python benchmarks/bench_llm.py --steps 20 --warmup 3
 run vflgan 300 python benchmarks/bench_vfl_gan.py
 run byz 300 python benchmarks/bench_byzantine.py
-run prof8 300 rocprofv3 --kernel-trace --stats -d $out/prof8 -o run -- python bench.py --steps 2 --warmup 1
-run prof1 300 rocprofv3 --kernel-trace --stats -d $out/prof1 -o run -- python bench.py --clients 1 --train-size 6250 --steps 3 --warmup 1
+run prof8 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof8 -o run -- python bench.py --steps 2 --warmup 1
+run prof1 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof1 -o run -- python bench.py --clients 1 --train-size 6250 --steps 3 --warmup 1
+# keep the kernel statistics and their summaries; the per-dispatch traces would overflow gpurun_out
+for p in prof8 prof1; do
+  f=$(find $out/$p -name '*kernel_stats.csv' | head -1)
+  [ -n "$f" ] && python scripts/prof_summary.py "$f" 30 > $out/${p}_summary.txt && cp "$f" $out/${p}_kernel_stats.csv
+  rm -rf $out/$p
+done
 echo ALLDONE
