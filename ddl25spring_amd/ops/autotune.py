@@ -31,6 +31,7 @@ _FD_TILES = [(64, 128, 32, 4), (128, 128, 32, 3), (128, 128, 64, 2), (128, 256, 
              (48, 256, 64, 2), (64, 128, 64, 3), (64, 64, 64, 3), (128, 64, 64, 3), (48, 256, 32, 4),
              (256, 128, 32, 3)]
 _FD_HALO = [(48, 256, 4), (48, 128, 4), (128, 128, 4)]
+WIDE_SPLIT = os.environ.get("DDL_TUNE_WIDE_SPLIT", "1") != "0"
 # WGRAD re-fetches dy once per column tile and x once per (row tile, tap): the 256-wide tiles
 # halve one of the two on the deep layers (512 x 4608 outputs)
 _WG_TILES = [(128, 128, 32, 3), (64, 128, 32, 4), (64, 64, 64, 3), (128, 64, 64, 3), (128, 128, 64, 2),
@@ -55,6 +56,12 @@ def candidates(mode: str, geom, accumulate: bool = True) -> list:
             out += [(None, s) for s in (2, 4, 8)]
             if red % 64 == 0:
                 out += [(_cfg(64, 64, 64, 3), s) for s in (2, 4)]
+                # wide tiles at split-K depths: on one client's 4x4 / 8x8 layers the 64x64 tiles
+                # re-read every weight slab once per 64-pixel column through L2 (layer 4: 236 MB
+                # per conv); 128-wide tiles halve that, split-K restores the workgroup count
+                if WIDE_SPLIT and geom.G * geom.N * geom.P * geom.Q <= 6400:
+                    out += [(_cfg(*t), s) for t in ((128, 128, 64, 2), (128, 64, 64, 3), (64, 128, 64, 3))
+                            for s in (2, 4, 8)]
     else:
         out += [(_cfg(*t), 0) for t in _WG_TILES if accumulate]
         if accumulate:  # the heuristic tile at explicit split-K depths (small grids: 1-2 clients)
