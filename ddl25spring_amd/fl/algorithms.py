@@ -94,7 +94,8 @@ class FederatedBase:
               "b_global": self.b_global.detach().cpu().clone(),
               "round_idx": self.round_idx, "rng": self.rng.bit_generator.state,
               "fail_rng": self.fail_rng.bit_generator.state, "dropped": self.dropped,
-              "algorithm": self.algorithm, "N": self.N, "K": self.K, "seed": self.seed}
+              "algorithm": self.algorithm, "N": self.N, "K": self.K, "seed": self.seed,
+              "param_layout": self.net.store.param_layout()}
         for name in ("g_global",):
             if hasattr(self, name):
                 sd[name] = getattr(self, name).detach().cpu().clone()
@@ -106,10 +107,16 @@ class FederatedBase:
         if (sd["algorithm"], sd["N"], sd["K"]) != (self.algorithm, self.N, self.K):
             raise ValueError("checkpoint is for a different federation "
                              f"{(sd['algorithm'], sd['N'], sd['K'])}")
-        self.w_global.copy_(sd["w_global"].to(self.dev))
+        # flat rows are remapped by parameter name when the writer used another layout (checkpoints
+        # without "param_layout" predate the direct-first layout: declaration order)
+        st = self.net.store
+        src = sd.get("param_layout") or st.param_layout(declaration_order=True)
+        fix = (lambda t: t) if [list(x) for x in src] == st.param_layout() else \
+            (lambda t: st.remap_flat(t, src))
+        self.w_global.copy_(fix(sd["w_global"]).to(self.dev))
         self.b_global.copy_(sd["b_global"].to(self.dev))
         if "g_global" in sd and hasattr(self, "g_global"):
-            self.g_global.copy_(sd["g_global"].to(self.dev))
+            self.g_global.copy_(fix(sd["g_global"]).to(self.dev))
         self.round_idx = int(sd["round_idx"])
         self.rng.bit_generator.state = sd["rng"]
         self.fail_rng.bit_generator.state = sd["fail_rng"]

@@ -36,6 +36,7 @@ class Spec:
     offset: int = 0
     numel: int = 0
     direct: bool = False  # gradient comes only from conv WGRAD launches (direct-SGD eligible)
+    decl_offset: int = 0  # offset in declaration order (the flat layout before direct-first)
 
 
 def kaiming_uniform_(fan_in: int, a: float = math.sqrt(5)):
@@ -94,8 +95,24 @@ class ParamStore:
         else:
             off = self.P
             self.P += (n + 15) // 16 * 16
-        self.specs[name] = Spec(name, shape, init, buffer, off, n, direct and not buffer)
+        self.specs[name] = Spec(name, shape, init, buffer, off, n, direct and not buffer, off)
         return name
+
+    def param_layout(self, declaration_order: bool = False) -> list:
+        """[[name, offset, numel], ...] of the trainable params in the flat ``data`` row (or in the
+        declaration-order layout that flat checkpoints written before the direct-first layout use)."""
+        return [[n, s.decl_offset if declaration_order else s.offset, s.numel]
+                for n, s in self.specs.items() if not s.buffer]
+
+    def remap_flat(self, flat: torch.Tensor, layout: list) -> torch.Tensor:
+        """A flat parameter row written with ``layout`` ([[name, offset, numel], ...]) in this
+        store's layout (by name)."""
+        out = torch.zeros(max(self.P, 16), dtype=flat.dtype, device=flat.device)
+        for name, off, n in layout:
+            s = self.specs[name]
+            assert s.numel == n and not s.buffer, name
+            out[s.offset:s.offset + n] = flat[off:off + n]
+        return out
 
     def _layout(self):
         """Direct-eligible params first ([0, Pd)), the rest after, each in declaration order (the

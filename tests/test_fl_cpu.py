@@ -313,3 +313,28 @@ def test_direct_sgd_matches_gradient_sgd(fp32, model):
     assert torch.allclose(s1, w1.to(s1.dtype))
     Pd = net.store.Pd
     assert torch.count_nonzero(g1[:, Pd:]) == 0  # non-conv grads left zeroed for the next step
+
+
+def test_checkpoint_layout_remap(fp32):
+    """Flat checkpoints are remapped by parameter name: a checkpoint in the declaration-order
+    layout (written before conv weights were laid out first, no "param_layout" key) resumes to the
+    same model."""
+    from ddl25spring_amd.models import mnist_cnn
+    arr, data = _data(200)
+    parts = split(2, True, 10, labels=arr.labels)
+    kw = dict(lr=0.05, batch_size=50, client_fraction=1.0, seed=4)
+    fa = FedAvg(mnist_cnn, data, parts, **kw)
+    fa.run(1)
+    st = fa.net.store
+    assert st.param_layout() != st.param_layout(declaration_order=True)
+    sd = fa.state_dict()
+    old = dict(sd)
+    del old["param_layout"]
+    decl = torch.zeros_like(sd["w_global"])
+    for name, off, n in st.param_layout(declaration_order=True):
+        decl[off:off + n] = sd["w_global"][st.specs[name].offset:st.specs[name].offset + n]
+    old["w_global"] = decl
+    for ck in (sd, old):
+        fb = FedAvg(mnist_cnn, data, parts, **kw)
+        fb.load_state_dict(ck)
+        assert torch.equal(fb.w_global, fa.w_global)
