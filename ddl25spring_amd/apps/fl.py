@@ -29,6 +29,9 @@ class FLConfig:
     attack: str | None = None      # label_flip | sign_flip | gaussian | free_rider
     malicious: int = 0             # number of malicious clients (ids 0..malicious-1)
     dropout: float = 0.0
+    stragglers: float = 0.0        # probability a sampled client is slow
+    straggler_slowdown: float = 4.0
+    deadline: float | None = None  # drop clients slower than this (x nominal mean-shard time)
     train_size: int | None = None
     test_size: int | None = None
     checkpoint: str | None = None
@@ -51,7 +54,8 @@ def build_server(cfg: FLConfig, ctx):
     kw = dict(lr=cfg.lr, client_fraction=cfg.client_fraction, seed=cfg.seed,
               test_data=DeviceImageDataset(test, ctx.device), aggregator=cfg.aggregator,
               agg_kwargs={"trim": cfg.trim, "f": cfg.krum_f}, attack=attack, ctx=ctx,
-              dropout=cfg.dropout)
+              dropout=cfg.dropout, stragglers=cfg.stragglers,
+              straggler_slowdown=cfg.straggler_slowdown, deadline=cfg.deadline)
     if algo is FedAvg:
         kw.update(batch_size=cfg.batch_size, local_epochs=cfg.local_epochs)
     return algo(model_fn, DeviceImageDataset(train, ctx.device), parts, **kw)

@@ -39,7 +39,8 @@ class FederatedBase:
                  aggregator="mean", attack=None, ctx=None, momentum: float = 0.0,
                  weight_decay: float = 0.0, planner: str = "native", use_graph=None,
                  init_fn=None, eval_every: int = 1, eval_limit: int | None = None, name=None,
-                 agg_kwargs=None, dropout: float = 0.0):
+                 agg_kwargs=None, dropout: float = 0.0, stragglers: float = 0.0,
+                 straggler_slowdown: float = 4.0, deadline: float | None = None):
         self.ctx = ctx or rdist.context()
         self.dev = self.ctx.device
         self.data = train_data
@@ -76,6 +77,17 @@ class FederatedBase:
         self.dropout = dropout
         self.fail_rng = np.random.default_rng([seed, 0xD20])
         self.dropped: list[list[int]] = []
+        # [NS] stragglers: each sampled client is independently slow with probability
+        # ``stragglers`` (its local round takes ``straggler_slowdown`` x the nominal time of its
+        # shard, n_k * E samples at unit speed). With a ``deadline`` (in nominal times of the mean
+        # shard) the server aggregates only the clients that report in time, the synchronous-FL
+        # policy of dropping stragglers; ``sim_time`` records each round's simulated duration
+        # (slowest reporting client), the reference's "parallel wall time = max over clients"
+        # (hfl_complete.py:294,296) under heterogeneous client speed.
+        self.stragglers, self.slowdown, self.deadline = stragglers, straggler_slowdown, deadline
+        self.strag_rng = np.random.default_rng([seed, 0x57A6])
+        self.straggled: list[list[int]] = []
+        self.sim_time: list[float] = []
         self.timer = PhaseTimer(self.dev)  # download / local_train / aggregate (HIP events + roctx)
 
     def _sample(self):
@@ -84,6 +96,15 @@ class FederatedBase:
             alive = self.fail_rng.random(len(chosen)) >= self.dropout
             self.dropped.append([int(c) for c in chosen[~alive]])
             chosen = chosen[alive]
+        if self.stragglers > 0:
+            slow = self.strag_rng.random(len(chosen)) < self.stragglers
+            mean_n = float(np.mean(self.counts))
+            t = np.array([self.counts[int(c)] / mean_n for c in chosen]) * \
+                np.where(slow, self.slowdown, 1.0)
+            late = t > self.deadline if self.deadline is not None else np.zeros(len(chosen), bool)
+            self.straggled.append([int(c) for c in chosen[late]])
+            self.sim_time.append(float(t[~late].max()) if (~late).any() else 0.0)
+            chosen = chosen[~late]
         return chosen
 
     # ------------------------------------------------------------------ checkpoint / resume
@@ -94,6 +115,8 @@ class FederatedBase:
               "b_global": self.b_global.detach().cpu().clone(),
               "round_idx": self.round_idx, "rng": self.rng.bit_generator.state,
               "fail_rng": self.fail_rng.bit_generator.state, "dropped": self.dropped,
+              "strag_rng": self.strag_rng.bit_generator.state, "straggled": self.straggled,
+              "sim_time": self.sim_time,
               "algorithm": self.algorithm, "N": self.N, "K": self.K, "seed": self.seed,
               "param_layout": self.net.store.param_layout()}
         for name in ("g_global",):
@@ -121,6 +144,10 @@ class FederatedBase:
         self.rng.bit_generator.state = sd["rng"]
         self.fail_rng.bit_generator.state = sd["fail_rng"]
         self.dropped = [list(d) for d in sd["dropped"]]
+        if "strag_rng" in sd:
+            self.strag_rng.bit_generator.state = sd["strag_rng"]
+            self.straggled = [list(d) for d in sd["straggled"]]
+            self.sim_time = list(sd["sim_time"])
         if self.attack is not None and "attack" in sd:
             self.attack.load_state_dict(sd["attack"])
 

@@ -338,3 +338,29 @@ def test_checkpoint_layout_remap(fp32):
         fb = FedAvg(mnist_cnn, data, parts, **kw)
         fb.load_state_dict(ck)
         assert torch.equal(fb.w_global, fa.w_global)
+
+
+def test_stragglers_deadline_policy(fp32):
+    """Straggler injection: without a deadline every sampled client reports and the simulated round
+    time is the slowest one (straggler_slowdown x nominal); with a deadline below the slowdown the
+    stragglers are dropped from aggregation, on their own RNG stream (client sampling unchanged),
+    and the state resumes exactly."""
+    arr, data = _data(300)
+    parts = split(6, True, 10, labels=arr.labels)
+    kw = dict(lr=0.05, batch_size=50, client_fraction=1.0, seed=4)
+    base = FedAvg(mnist_mlp, data, parts, **kw)
+    slow = FedAvg(mnist_mlp, data, parts, stragglers=0.5, straggler_slowdown=4.0, **kw)
+    cut = FedAvg(mnist_mlp, data, parts, stragglers=0.5, straggler_slowdown=4.0, deadline=2.0, **kw)
+    for fa in (base, slow, cut):
+        fa.run(3)
+    assert torch.equal(base.w_global, slow.w_global)  # no deadline: same aggregation
+    assert slow.straggled == [[], [], []] and max(slow.sim_time) == pytest.approx(4.0)
+    n_late = sum(len(s) for s in cut.straggled)
+    assert n_late > 0 and max(cut.sim_time) == pytest.approx(1.0)
+    assert not torch.equal(base.w_global, cut.w_global)
+    again = FedAvg(mnist_mlp, data, parts, stragglers=0.5, straggler_slowdown=4.0, deadline=2.0, **kw)
+    again.run(2)
+    resumed = FedAvg(mnist_mlp, data, parts, stragglers=0.5, straggler_slowdown=4.0, deadline=2.0, **kw)
+    resumed.load_state_dict(again.state_dict())
+    resumed.run(1)
+    assert resumed.straggled == cut.straggled and torch.equal(resumed.w_global, cut.w_global)
