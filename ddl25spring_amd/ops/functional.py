@@ -300,6 +300,8 @@ def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0, _tun
     """dw[G,K,R,S,C] (+)= sum over pixels dy (x) x  — fp32, split-K with atomics.
     cfg = conv_cfg(bp, bq, bk, stages) (0: tuned default); splits = split-K slices (0: auto).
     Inside ``wgrad_overlap`` the launch goes to the side stream (see there)."""
+    if not accumulate and wgrad_scale(dw) != 1.0:
+        raise ValueError("a scaled WGRAD must accumulate (it adds into the master weights)")
     if not dy.is_cuda:
         ref.conv_wgrad(dy, x, geom, dw, accumulate, wgrad_scale(dw))
         return dw
