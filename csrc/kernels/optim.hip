@@ -107,14 +107,15 @@ DDL_API int ddl_adam(const AdamArgs* a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-// Plain SGD (no momentum / weight decay) over rows [rows][P] whose first Pd columns were already
-// updated inside the backward (conv WGRAD atomics of -lr * dW straight into the master weights,
-// ConvArgs::gscale): those columns only refresh the bf16 shadow (6 B/param instead of the 14 B of
-// sgd_kernel, and no zero-fill of their gradients). Columns >= Pd (BatchNorm, classifier head) take
-// the ordinary step and have their gradient zeroed for the next step in the same pass.
+// Plain SGD (no momentum / weight decay) over rows [rows][P] whose direct-eligible columns were
+// already updated inside the backward (conv WGRAD atomics of -lr * dW straight into the master
+// weights, ConvArgs::gscale): those columns only refresh the bf16 shadow (6 B/param instead of the
+// 14 B of sgd_kernel, and no zero-fill of their gradients). dmap[col / 16] marks them (parameters
+// start and pad to 16-element boundaries). The other columns (BatchNorm, classifier head, biases)
+// take the ordinary step and have their gradient zeroed for the next step in the same pass.
 struct SGDDirectArgs {
-  float* p; float* g; bf16_t* shadow;
-  long long rows, P, Pd;
+  float* p; float* g; bf16_t* shadow; const unsigned char* dmap;
+  long long rows, P;
   float lr, grad_scale;
 };
 
@@ -125,7 +126,7 @@ __global__ __launch_bounds__(256) void sgd_direct_kernel(SGDDirectArgs a) {
     const long long e = t * 4;
     const long long col = e % a.P;
     float4 pv = *(const float4*)(a.p + e);
-    if (col >= a.Pd) {
+    if (!a.dmap[col >> 4]) {
       const float4 gv = *(const float4*)(a.g + e);
       const float s = a.lr * a.grad_scale;
       pv.x -= s * gv.x; pv.y -= s * gv.y; pv.z -= s * gv.z; pv.w -= s * gv.w;
@@ -140,7 +141,7 @@ __global__ __launch_bounds__(256) void sgd_direct_kernel(SGDDirectArgs a) {
 }
 
 DDL_API int ddl_sgd_direct(const SGDDirectArgs* a, hipStream_t s) {
-  if (a->P % 4 || a->Pd % 4 || a->Pd > a->P) return (int)hipErrorInvalidValue;
+  if (a->P % 16) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(sgd_direct_kernel, dim3(grid_for(a->rows * a->P / 4, 256)), dim3(256), 0, s, *a);
   return (int)hipGetLastError();
 }

@@ -130,10 +130,9 @@ class FederatedBase:
         if (sd["algorithm"], sd["N"], sd["K"]) != (self.algorithm, self.N, self.K):
             raise ValueError("checkpoint is for a different federation "
                              f"{(sd['algorithm'], sd['N'], sd['K'])}")
-        # flat rows are remapped by parameter name when the writer used another layout (checkpoints
-        # without "param_layout" predate the direct-first layout: declaration order)
+        # flat rows are remapped by parameter name when the writer used another layout
         st = self.net.store
-        src = sd.get("param_layout") or st.param_layout(declaration_order=True)
+        src = sd.get("param_layout") or st.param_layout()
         fix = (lambda t: t) if [list(x) for x in src] == st.param_layout() else \
             (lambda t: st.remap_flat(t, src))
         self.w_global.copy_(fix(sd["w_global"]).to(self.dev))

@@ -39,7 +39,7 @@ class LocalTrainer:
         self.planner = planner
         dev = net.device
         self.use_graph = (dev.type == "cuda") if use_graph is None else (use_graph and dev.type == "cuda")
-        eligible = momentum == 0.0 and weight_decay == 0.0 and net.store.Pd > 0 \
+        eligible = momentum == 0.0 and weight_decay == 0.0 and net.store.n_direct > 0 \
             and getattr(net, "grad_hook", None) is None
         self.direct = eligible and (DIRECT_SGD and dev.type == "cuda" if direct is None else direct)
         self.label_transform = label_transform  # callable(y [G,B], g0, g1) -> y (attacks); with a

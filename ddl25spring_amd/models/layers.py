@@ -107,8 +107,10 @@ class ConvUnit(Layer):
             w = torch.empty(cout_t, cin_t, k, k)
             init_w(w, gen)
             t[:cout_t, :, :, :cin_t] = w.permute(0, 2, 3, 1)
-        # conv weights (not Linear ones: a fused classifier head writes those) take direct SGD
-        self.w = store.add(p + ".weight", shape, winit, direct=not self.linear)
+        # every conv weight takes direct SGD; Linear weights unless Net marked the layer a fused
+        # classifier head (its weight gradient comes from Fn.head_train, not a WGRAD launch)
+        self.w = store.add(p + ".weight", shape, winit,
+                           direct=not self.linear or getattr(self, "direct_w", False))
         if self.bias:
             binit = uniform_bias_(self.fan_in)
 

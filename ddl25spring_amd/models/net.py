@@ -28,6 +28,12 @@ class Net:
         self.input_spec = input_spec or {}
         self.name = name
         self.store = ParamStore(groups)
+        # direct-SGD eligibility of Linear weights: all but a classifier head after a global
+        # average pool, whose weight gradient the fused head kernel (Fn.head_train) writes
+        for i, layer in enumerate(layers):
+            if isinstance(layer, ConvUnit) and layer.linear:
+                head = i == len(layers) - 1 and i > 0 and layers[i - 1].name == "avgpool"
+                layer.direct_w = not head
         for i, layer in enumerate(layers):
             layer.declare(self.store, getattr(layer, "pname", f"{i}.{layer.name}"))
         self._plan_fusions()

@@ -36,7 +36,7 @@ class Spec:
     offset: int = 0
     numel: int = 0
     direct: bool = False  # gradient comes only from conv WGRAD launches (direct-SGD eligible)
-    decl_offset: int = 0  # offset in declaration order (the flat layout before direct-first)
+
 
 
 def kaiming_uniform_(fan_in: int, a: float = math.sqrt(5)):
@@ -78,7 +78,8 @@ class ParamStore:
         self.data = self.grad = self.shadow = self.buffers = None
         self.device = torch.device("cpu")
         self._shadow_version = -1
-        self.Pd = 0              # columns [0, Pd): the direct-eligible params (laid out first)
+        self.direct_map = None   # uint8 [P/16]: chunks of direct-SGD-eligible params
+        self.n_direct = 0
         self.direct_mode = False
         self._direct_lr = 0.0
 
@@ -95,14 +96,12 @@ class ParamStore:
         else:
             off = self.P
             self.P += (n + 15) // 16 * 16
-        self.specs[name] = Spec(name, shape, init, buffer, off, n, direct and not buffer, off)
+        self.specs[name] = Spec(name, shape, init, buffer, off, n, direct and not buffer)
         return name
 
-    def param_layout(self, declaration_order: bool = False) -> list:
-        """[[name, offset, numel], ...] of the trainable params in the flat ``data`` row (or in the
-        declaration-order layout that flat checkpoints written before the direct-first layout use)."""
-        return [[n, s.decl_offset if declaration_order else s.offset, s.numel]
-                for n, s in self.specs.items() if not s.buffer]
+    def param_layout(self) -> list:
+        """[[name, offset, numel], ...] of the trainable params in the flat ``data`` row."""
+        return [[n, s.offset, s.numel] for n, s in self.specs.items() if not s.buffer]
 
     def remap_flat(self, flat: torch.Tensor, layout: list) -> torch.Tensor:
         """A flat parameter row written with ``layout`` ([[name, offset, numel], ...]) in this
@@ -114,24 +113,20 @@ class ParamStore:
             out[s.offset:s.offset + n] = flat[off:off + n]
         return out
 
-    def _layout(self):
-        """Direct-eligible params first ([0, Pd)), the rest after, each in declaration order (the
-        init RNG draws in declaration order whatever the layout)."""
-        off = 0
-        for want in (True, False):
-            for s in self.specs.values():
-                if not s.buffer and s.direct == want:
-                    s.offset = off
-                    off += (s.numel + 15) // 16 * 16
-            if want:
-                self.Pd = off
-        assert off == self.P
+    def _direct_map(self):
+        """uint8 [P/16]: 1 on the 16-column chunks of direct-eligible params (every spec starts on
+        a 16-element boundary and pads to one), read by the direct-SGD finishing launch."""
+        m = torch.zeros(max(self.P, 16) // 16, dtype=torch.uint8)
+        for s in self.specs.values():
+            if s.direct and not s.buffer:
+                m[s.offset // 16:(s.offset + s.numel + 15) // 16] = 1
+        self.n_direct = int(m.sum()) * 16
+        return m
 
     # ---------------------------------------------------------------- materialise
     def materialize(self, device, seed: int = 0, generator: torch.Generator | None = None):
         device = torch.device(device)
         self.device = device
-        self._layout()
         G = self.G
         gen = generator if generator is not None else torch.Generator().manual_seed(seed)
         data = torch.zeros(G, max(self.P, 16), dtype=torch.float32)
@@ -143,6 +138,7 @@ class ParamStore:
             tgt = bufs if s.buffer else data
             tgt[:, s.offset:s.offset + s.numel] = t.reshape(1, -1)
         self.data = data.to(device)
+        self.direct_map = self._direct_map().to(device)
         self.buffers = bufs.to(device)
         self.grad = torch.zeros_like(self.data)
         sdt = torch.bfloat16 if device.type != "cpu" else CPU_SHADOW_DTYPE

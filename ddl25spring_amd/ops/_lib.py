@@ -73,7 +73,7 @@ class SGDArgs(ctypes.Structure):
 
 
 class SGDDirectArgs(ctypes.Structure):
-    _fields_ = [("p", vp), ("g", vp), ("shadow", vp), ("rows", i64), ("P", i64), ("Pd", i64),
+    _fields_ = [("p", vp), ("g", vp), ("shadow", vp), ("dmap", vp), ("rows", i64), ("P", i64),
                 ("lr", f32), ("grad_scale", f32)]
 
 

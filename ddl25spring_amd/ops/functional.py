@@ -1074,18 +1074,20 @@ def sgd_step(p, g, mom, shadow, lr, wd=0.0, momentum=0.0, dampening=0.0, nestero
     check(_lib.kernels().ddl_sgd(ctypes.byref(a), stream()), "sgd")
 
 
-def sgd_direct_step(p, g, shadow, Pd: int, lr: float, grad_scale: float = 1.0):
-    """Finish a direct-SGD step over rows p/g/shadow [rows, P]: columns [0, Pd) (the conv weights,
-    already stepped by the scaled WGRAD) only refresh the bf16 shadow; columns >= Pd take
-    ``p -= lr * grad_scale * g`` and get their gradient zeroed. One launch."""
+def sgd_direct_step(p, g, shadow, dmap, lr: float, grad_scale: float = 1.0):
+    """Finish a direct-SGD step over rows p/g/shadow [rows, P]: the columns ``dmap`` (uint8 per
+    16 columns) marks — conv / Linear weights, already stepped by the scaled WGRAD — only refresh
+    the bf16 shadow; the others take ``p -= lr * grad_scale * g`` and get their gradient zeroed.
+    One launch."""
     if not p.is_cuda:
-        ref.sgd_direct(p, g, shadow, Pd, lr, grad_scale)
+        ref.sgd_direct(p, g, shadow, dmap, lr, grad_scale)
         return
     assert p.dim() == 2 and p.is_contiguous() and g.is_contiguous() and shadow.is_contiguous()
-    assert p.shape == g.shape == shadow.shape and p.shape[1] % 4 == 0 and Pd % 4 == 0
+    assert p.shape == g.shape == shadow.shape and p.shape[1] % 16 == 0
+    assert dmap.dtype == torch.uint8 and dmap.numel() == p.shape[1] // 16 and dmap.is_cuda
     a = _lib.SGDDirectArgs()
-    a.p, a.g, a.shadow = ptr(p), ptr(g), ptr(shadow)
-    a.rows, a.P, a.Pd = p.shape[0], p.shape[1], Pd
+    a.p, a.g, a.shadow, a.dmap = ptr(p), ptr(g), ptr(shadow), ptr(dmap)
+    a.rows, a.P = p.shape[0], p.shape[1]
     a.lr, a.grad_scale = lr, grad_scale
     check(_lib.kernels().ddl_sgd_direct(ctypes.byref(a), stream()), "sgd_direct")
 

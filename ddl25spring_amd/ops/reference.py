@@ -311,11 +311,12 @@ def sgd(p, g, mom, shadow, lr, wd, momentum, dampening, nesterov, first_step, gr
         shadow.copy_(p.to(shadow.dtype))
 
 
-def sgd_direct(p, g, shadow, Pd, lr, grad_scale=1.0):
-    """Columns [0, Pd) were updated inside the backward: shadow refresh only; the rest take a
-    plain SGD step and have their gradient zeroed (optim.hip sgd_direct_kernel)."""
-    p[:, Pd:].sub_(lr * grad_scale * g[:, Pd:])
-    g[:, Pd:].zero_()
+def sgd_direct(p, g, shadow, dmap, lr, grad_scale=1.0):
+    """Columns marked in ``dmap`` (per 16) were updated inside the backward: shadow refresh only;
+    the rest take a plain SGD step and have their gradient zeroed (optim.hip sgd_direct_kernel)."""
+    rest = (dmap == 0).repeat_interleave(16).to(p.device)
+    p[:, rest] -= lr * grad_scale * g[:, rest]
+    g[:, rest] = 0
     if shadow is not None:
         shadow.copy_(p.to(shadow.dtype))
 

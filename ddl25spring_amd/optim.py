@@ -68,8 +68,8 @@ class SGD(_Base):
         the rest, in one launch. Only for momentum- and weight-decay-free SGD."""
         assert self.mom is None and self.weight_decay == 0.0
         st = self.store
-        Fn.sgd_direct_step(self._rows(st.data), self._rows(st.grad), self._rows(st.shadow), st.Pd,
-                           self.lr, grad_scale)
+        Fn.sgd_direct_step(self._rows(st.data), self._rows(st.grad), self._rows(st.shadow),
+                           st.direct_map, self.lr, grad_scale)
         st._shadow_version = st.data._version
         self.steps += 1
 

@@ -303,7 +303,10 @@ def test_direct_sgd_matches_gradient_sgd(fp32, model):
     for direct in (False, True):
         net = make(groups=2).to("cpu", seed=3)
         data.set_input_spec(net.input_spec)
-        assert 0 < net.store.Pd < net.store.P
+        assert 0 < net.store.n_direct < net.store.P
+        # flat layout stays in declaration order (the DP bucketer and flat checkpoints rely on it)
+        offs = [o for _, o, _ in net.store.param_layout()]
+        assert offs == sorted(offs)
         tr = LocalTrainer(net, data, 0.05, 8, use_graph=False, direct=direct)
         assert tr.direct == direct
         tr.run([np.asarray(p) for p in parts], [11, 12], epochs=1)
@@ -311,14 +314,14 @@ def test_direct_sgd_matches_gradient_sgd(fp32, model):
     (w0, s0, g0), (w1, s1, g1) = out
     assert torch.allclose(w0, w1, atol=1e-5, rtol=1e-4), (w0 - w1).abs().max()
     assert torch.allclose(s1, w1.to(s1.dtype))
-    Pd = net.store.Pd
-    assert torch.count_nonzero(g1[:, Pd:]) == 0  # non-conv grads left zeroed for the next step
+    rest = (net.store.direct_map == 0).repeat_interleave(16)
+    assert torch.count_nonzero(g1[:, rest]) == 0  # non-direct grads left zeroed for the next step
 
 
 def test_checkpoint_layout_remap(fp32):
-    """Flat checkpoints are remapped by parameter name: a checkpoint in the declaration-order
-    layout (written before conv weights were laid out first, no "param_layout" key) resumes to the
-    same model."""
+    """Flat checkpoints carry their parameter layout and are remapped by name: a checkpoint whose
+    flat rows use another layout (here: the parameters in reverse order) resumes to the same
+    model."""
     from ddl25spring_amd.models import mnist_cnn
     arr, data = _data(200)
     parts = split(2, True, 10, labels=arr.labels)
@@ -326,15 +329,15 @@ def test_checkpoint_layout_remap(fp32):
     fa = FedAvg(mnist_cnn, data, parts, **kw)
     fa.run(1)
     st = fa.net.store
-    assert st.param_layout() != st.param_layout(declaration_order=True)
     sd = fa.state_dict()
-    old = dict(sd)
-    del old["param_layout"]
-    decl = torch.zeros_like(sd["w_global"])
-    for name, off, n in st.param_layout(declaration_order=True):
-        decl[off:off + n] = sd["w_global"][st.specs[name].offset:st.specs[name].offset + n]
-    old["w_global"] = decl
-    for ck in (sd, old):
+    other = dict(sd)
+    flat, layout, off = torch.zeros_like(sd["w_global"]), [], 0
+    for name, o, n in reversed(st.param_layout()):
+        flat[off:off + n] = sd["w_global"][o:o + n]
+        layout.append([name, off, n])
+        off += (n + 15) // 16 * 16
+    other["w_global"], other["param_layout"] = flat, layout
+    for ck in (sd, other):
         fb = FedAvg(mnist_cnn, data, parts, **kw)
         fb.load_state_dict(ck)
         assert torch.equal(fb.w_global, fa.w_global)
