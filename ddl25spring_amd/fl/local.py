@@ -22,7 +22,7 @@ from ..data.split import plan_epoch
 from ..runtime.graphs import CAPTURE_MODE
 
 
-# Direct SGD (default on the GPU for plain SGD): the conv weights' WGRAD launches add -lr * dW
+# Direct SGD (default on the GPU for plain SGD): the conv / Linear weights' WGRAD launches add -lr * dW
 # straight into the fp32 master weights (ParamStore.direct_update), so a step skips zero-filling
 # and re-reading their gradients and its optimizer launch only refreshes their bf16 shadow.
 # DDL_DIRECT_SGD=0 keeps gradient buffer + fused SGD launch.
@@ -54,7 +54,7 @@ class LocalTrainer:
         if self.label_transform is not None:
             y = self.label_transform(y, g0, g1)
         with st.select(g0, g1):
-            if self.direct:  # the previous step_direct left the non-conv gradients zeroed
+            if self.direct:  # the previous step_direct left the other gradients zeroed
                 with st.direct_update(self.opt.lr):
                     loss, _ = net.train_step(x, y)
                 self.opt.select(g0, g1).step_direct()

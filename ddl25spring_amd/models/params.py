@@ -35,8 +35,7 @@ class Spec:
     buffer: bool = False
     offset: int = 0
     numel: int = 0
-    direct: bool = False  # gradient comes only from conv WGRAD launches (direct-SGD eligible)
-
+    direct: bool = False  # gradient comes only from WGRAD launches (direct-SGD eligible)
 
 
 def kaiming_uniform_(fan_in: int, a: float = math.sqrt(5)):
