@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--train-size", type=int, default=50000)
     ap.add_argument("--model", default="resnet18")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--sync-rounds", action="store_true",
+                    help="synchronise host and device around every timed round (A/B)")
     ap.add_argument("--eval", action="store_true", help="also report test accuracy (untimed)")
     ap.add_argument("--backend", default=None,
                     help="collective backend (default: nccl = RCCL on GPUs); gloo lets several "
@@ -66,6 +68,9 @@ def main():
 
     for _ in range(args.warmup):
         fl.round()
+    # timed rounds without per-round host <-> device syncs: the host plans and enqueues round r+1
+    # while the GPU runs round r (FederatedBase.sync_rounds); the work per round is unchanged
+    fl.sync_rounds = args.sync_rounds
     ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -76,6 +81,9 @@ def main():
     ctx.barrier()
     torch.cuda.synchronize()
     elapsed = ctx.max_scalar(time.perf_counter() - t0)
+    if not fl.sync_rounds:
+        samples = int(ctx.sum_scalar(samples))  # round() returned this rank's samples
+        fl.sync_rounds = True
     ms_per_round = 1000.0 * elapsed / args.steps
     samples_per_s = samples / elapsed
     rounds_per_s = args.steps / elapsed

@@ -89,6 +89,12 @@ class FederatedBase:
         self.straggled: list[list[int]] = []
         self.sim_time: list[float] = []
         self.timer = PhaseTimer(self.dev)  # download / local_train / aggregate (HIP events + roctx)
+        # sync_rounds=False: FedAvg rounds run without any host <-> device synchronisation (no
+        # per-round wall time; round() returns dt = 0 and this rank's sample count), so the host
+        # samples, plans and enqueues round r+1 while the GPU still executes round r. For
+        # throughput runs (bench.py); run() keeps the reference's per-round timing.
+        self.sync_rounds = True
+        self._coeff_cache: dict = {}
 
     def _sample(self):
         chosen = self.rng.choice(self.N, self.K, replace=False)
@@ -227,8 +233,20 @@ class FedAvg(FederatedBase):
         self.trainer.use_graph = self._graph_default and (lt is None or hasattr(lt, "graph_key"))
         return self.trainer
 
+    def _coeffs(self, mine, total):
+        """Device tensor of the n_k / n weights of my clients; cached per (clients, total), since
+        building it from a host list is a blocking copy."""
+        key = (tuple(mine), total)
+        t = self._coeff_cache.get(key)
+        if t is None:
+            t = torch.tensor([self.counts[c] / total for c in mine], dtype=torch.float32, device=self.dev)
+            if len(self._coeff_cache) < 256:
+                self._coeff_cache[key] = t
+        return t
+
     def round(self):
-        _sync(self.dev)
+        if self.sync_rounds:
+            _sync(self.dev)
         t0 = time.perf_counter()
         chosen = self._sample()
         if len(chosen) == 0:  # every sampled client dropped out: the server model stays
@@ -257,14 +275,15 @@ class FedAvg(FederatedBase):
         st = self.net.store
         if self.attack is not None and G:
             self.attack.poison_updates(st.data[:G], self.w_global, mine)
-        coeffs = torch.tensor([self.counts[c] / total for c in mine], dtype=torch.float32,
-                              device=self.dev)
+        coeffs = self._coeffs(mine, total)
         with self.timer("aggregate"):
             self._aggregate(st.data[:G], coeffs, counts)
             self._mean_buffers(G, coeffs)
+        self.round_idx += 1
+        if not self.sync_rounds:
+            return 0.0, samples
         _sync(self.dev)
         dt = self.ctx.max_scalar(time.perf_counter() - t0)
-        self.round_idx += 1
         samples = int(self.ctx.sum_scalar(samples))
         return dt, samples
 

@@ -46,6 +46,11 @@ class LocalTrainer:
         # ``graph_key`` attribute it is pure device ops and may be captured in the round graph
         self._graphs: dict = {}
         self.last_loss = None
+        # double-buffered pinned staging of the round's batch plan: the host->device copy is then
+        # truly asynchronous, so with FederatedBase.sync_rounds off the host plans and enqueues
+        # round r+1 while the GPU still runs round r
+        self._pinned: dict = {}
+        self._pin_slot = 0
 
     # ---------------------------------------------------------------- one step (eager)
     def _step(self, idx, g0: int, g1: int):
@@ -165,11 +170,29 @@ class LocalTrainer:
                 out[s, g, :len(chunk)] = chunk
         return out
 
+    def _upload(self, plan: np.ndarray, dev) -> torch.Tensor:
+        if dev.type != "cuda":
+            return torch.from_numpy(plan).to(dev)
+        slots = self._pinned.get(plan.shape)
+        if slots is None:
+            slots = [[torch.empty(plan.shape, dtype=torch.int32, pin_memory=True), None] for _ in range(2)]
+            self._pinned[plan.shape] = slots
+        self._pin_slot ^= 1
+        buf, ev = slots[self._pin_slot]
+        if ev is not None:
+            ev.synchronize()  # the copy that last read this buffer (two uploads ago) is done
+        buf.numpy()[...] = plan
+        out = buf.to(dev, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        slots[self._pin_slot][1] = ev
+        return out
+
     def _run_plan(self, plan: np.ndarray, g0: int, g1: int) -> int:
         dev = self.net.device
         steps = plan.shape[0]
         full = (plan >= 0).all(axis=(1, 2))
-        plan_dev = torch.from_numpy(plan).to(dev, non_blocking=True)
+        plan_dev = self._upload(np.ascontiguousarray(plan, dtype=np.int32), dev)
         samples = 0
         G = g1 - g0
         s = 0

@@ -367,3 +367,18 @@ def test_stragglers_deadline_policy(fp32):
     resumed.load_state_dict(again.state_dict())
     resumed.run(1)
     assert resumed.straggled == cut.straggled and torch.equal(resumed.w_global, cut.w_global)
+
+
+def test_unsynchronised_rounds_match(fp32):
+    """sync_rounds=False (no host <-> device sync inside a round, the throughput mode of bench.py)
+    trains exactly as the synchronised rounds; round() then reports this rank's samples."""
+    arr, data = _data(300)
+    parts = split(6, True, 10, labels=arr.labels)
+    kw = dict(lr=0.05, batch_size=50, client_fraction=0.5, seed=4)
+    a, b = FedAvg(mnist_mlp, data, parts, **kw), FedAvg(mnist_mlp, data, parts, **kw)
+    b.sync_rounds = False
+    for _ in range(3):
+        _, sa = a.round()
+        dt, sb = b.round()
+        assert dt == 0.0 and sa == sb
+    assert torch.equal(a.w_global, b.w_global)
