@@ -130,11 +130,13 @@ def test_direct_sgd_equals_gradient_sgd(cuda, model, monkeypatch):
 
 def test_unsynchronised_rounds_match_on_device(cuda):
     """Rounds enqueued back to back without host <-> device syncs (pinned, double-buffered plan
-    uploads; bench.py's timed mode) train as the synchronised rounds (MnistCnn: rounding level)."""
+    uploads; bench.py's timed mode) train as the synchronised rounds. Same kernels in the same
+    order, so the only difference is fp32-atomic order, which bf16 shadow flips amplify over the
+    rounds: checked against the spread of two synchronised runs."""
     arr = synthetic_images("mnist", 800, seed=0)
     parts = split(4, True, 3, labels=arr.labels)
     ws = []
-    for sync in (True, False):
+    for sync in (True, False, True):
         fa = FedAvg(mnist_cnn, DeviceImageDataset(arr, cuda), parts, lr=0.05, batch_size=50,
                     client_fraction=1.0, seed=3, ctx=_ctx(cuda), eval_every=0)
         w0 = fa.w_global.clone()
@@ -146,4 +148,5 @@ def test_unsynchronised_rounds_match_on_device(cuda):
         torch.cuda.synchronize()
         ws.append(fa.w_global.clone())
     step = (ws[0] - w0).norm()
-    assert ((ws[0] - ws[1]).norm() / step).item() < 1e-2
+    noise = ((ws[0] - ws[2]).norm() / step).item()
+    assert ((ws[0] - ws[1]).norm() / step).item() < 2 * noise + 1e-2
