@@ -27,6 +27,11 @@ from ..runtime.graphs import CAPTURE_MODE
 # and re-reading their gradients and its optimizer launch only refreshes their bf16 shadow.
 # DDL_DIRECT_SGD=0 keeps gradient buffer + fused SGD launch.
 DIRECT_SGD = os.environ.get("DDL_DIRECT_SGD", "1") != "0"
+# Instances of each captured round graph, replayed alternately: ROCm's graph launch waits for the
+# same executable's previous launch to finish before it submits the ~7,000 kernel nodes, which left
+# the GPU idle ~1 ms at every round boundary even with the host rounds ahead (sync_rounds off);
+# with two instances (DDL_ROUND_GRAPHS=2) the host can submit round r+1 while round r runs.
+ROUND_GRAPHS = max(1, int(os.environ.get("DDL_ROUND_GRAPHS", "1")))
 
 
 class LocalTrainer:
@@ -45,6 +50,7 @@ class LocalTrainer:
         self.label_transform = label_transform  # callable(y [G,B], g0, g1) -> y (attacks); with a
         # ``graph_key`` attribute it is pure device ops and may be captured in the round graph
         self._graphs: dict = {}
+        self._next: dict = {}
         self.last_loss = None
         # double-buffered pinned staging of the round's batch plan: the host->device copy is then
         # truly asynchronous, so with FederatedBase.sync_rounds off the host plans and enqueues
@@ -79,10 +85,14 @@ class LocalTrainer:
         ran eagerly every round, ~130 host-side launches."""
         key = (G, self.B, nsteps, None if tail is None else tail.shape[-1],
                getattr(self.label_transform, "graph_key", None))
-        ent = self._graphs.get(key)
-        if ent is None:
-            ent = self._capture(plan_dev, nsteps, G, tail)
-            self._graphs[key] = ent
+        ents = self._graphs.get(key)
+        if ents is None:
+            n = ROUND_GRAPHS if self.net.device.type == "cuda" else 1
+            ents = [self._capture(plan_dev, nsteps, G, tail) for _ in range(n)]
+            self._graphs[key] = ents
+            self._next[key] = 0
+        ent = ents[self._next[key]]
+        self._next[key] = (self._next[key] + 1) % len(ents)
         ent["plan"].copy_(plan_dev[:nsteps])
         if tail is not None:
             ent["tail"].copy_(tail)
