@@ -4,7 +4,7 @@ set -o pipefail
 export TMPDIR=/tmp
 out=gpurun_out/rg2
 mkdir -p $out
-timeout -k 10 300 python -u -m pytest tests/test_fl_gpu.py tests/test_multirank_gpu.py tests/test_graphs_gpu.py -x -q --timeout 120 --timeout-method thread > $out/tests.log 2>&1 || { tail -30 $out/tests.log; exit 1; }
+DDL_ROUND_GRAPHS=2 timeout -k 10 300 python -u -m pytest tests/test_fl_gpu.py tests/test_multirank_gpu.py tests/test_graphs_gpu.py -x -q --timeout 120 --timeout-method thread > $out/tests.log 2>&1 || { tail -30 $out/tests.log; exit 1; }
 tail -1 $out/tests.log
 b() { local name=$1; shift; timeout -k 10 300 "$@" > $out/$name.log 2>&1 || { tail -5 $out/$name.log; exit 1; }; echo "$name: $(grep -o '"value": [0-9.]*' $out/$name.log)"; }
 for rep in 1 2; do
