@@ -9,7 +9,12 @@ spread over N GPUs, i.e. strong scaling: at N=1 the 8 clients run client-batched
 each GPU is one client.
 
 Data: synthetic CIFAR-10-shaped uint8 images (learnable class templates), random-init weights.
-Compute dtype bf16 (MFMA), fp32 master weights / grads / BN statistics / aggregation.
+Precision (``--precision``, default fp32 = the reference's, lab/tutorial_1a/hfl_complete.py:39-80):
+  fp32 — activations, weights, gradients and BN in fp32 end to end on the exact-fp32 MFMA
+         (conv_f32.hip / bn_f32.hip); the step is bitwise deterministic, so the JSON line also
+         carries a sha256 of the final server weights (``w_global_sha256``);
+  bf16 — bf16 MFMA operands / activations with fp32 master weights, grads, BN statistics and
+         aggregation (conv_igemm.hip), the faster non-reference-precision mode.
 
     python bench.py --gpus 1 --steps 3 --warmup 1
     torchrun --nproc-per-node 8 bench.py --gpus 8 ...
@@ -17,6 +22,7 @@ Compute dtype bf16 (MFMA), fp32 master weights / grads / BN statistics / aggrega
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -25,6 +31,11 @@ import time
 import torch
 
 METRIC = "FedAvg rounds/sec + local samples/sec, ResNet-18 CIFAR-10-shape, 8 clients"
+# the reference publishes no throughput; the number to beat is the reference's own FedAvg
+# loop (hfl_complete.py FedAvgServer: per-client nn.Module replicas, host-staged weights, fp32) on
+# the same config, timed on one MI355X with stock PyTorch-ROCm (benchmarks/bench_reference_eager.py
+# --variant faithful; profiles/reference_eager_r3.jsonl).
+REFERENCE_SAMPLES_PER_S = {"fp32": 2680.0}
 
 
 def main():
@@ -45,12 +56,16 @@ def main():
     ap.add_argument("--backend", default=None,
                     help="collective backend (default: nccl = RCCL on GPUs); gloo lets several "
                          "ranks share one GPU for a functional rehearsal")
+    ap.add_argument("--precision", default="fp32", choices=("fp32", "bf16"),
+                    help="compute precision (fp32 = the reference's; bf16 = bf16 MFMA / activations)")
     args = ap.parse_args()
 
     from ddl25spring_amd.runtime import dist as rdist
     ctx = rdist.init(backend=args.backend)
     if ctx.device.type != "cuda":
         print("bench.py needs a GPU", file=sys.stderr)
+        rdist.shutdown()
+        sys.exit(2)
     from ddl25spring_amd.data.images import DeviceImageDataset, synthetic_images
     from ddl25spring_amd.data.split import split
     from ddl25spring_amd.fl.algorithms import FedAvg
@@ -61,7 +76,10 @@ def main():
     dtrain = DeviceImageDataset(train, ctx.device)
     dtest = DeviceImageDataset(test, ctx.device) if test is not None else None
     parts = split(args.clients, True, 10, labels=train.labels)
-    model_fn = {"resnet18": resnet18_cifar}[args.model]
+    base_fn = {"resnet18": resnet18_cifar}[args.model]
+
+    def model_fn(groups):
+        return base_fn(10, groups=groups, precision=args.precision)
     fl = FedAvg(model_fn, dtrain, parts, lr=args.lr, batch_size=args.batch,
                 local_epochs=args.epochs, client_fraction=1.0, seed=10, test_data=dtest,
                 use_graph=not args.no_graph, eval_every=0)
@@ -88,6 +106,8 @@ def main():
     samples_per_s = samples / elapsed
     rounds_per_s = args.steps / elapsed
     acc = fl.test() if args.eval else None
+    w_hash = hashlib.sha256(fl.w_global.detach().cpu().numpy().tobytes()).hexdigest()
+    ref = REFERENCE_SAMPLES_PER_S.get(args.precision)
     if ctx.is_main:
         out = {
             "metric": METRIC,
@@ -99,9 +119,12 @@ def main():
             "ms_per_step": round(ms_per_round, 3),
             "higher_is_better": True,
             "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "bf16",
+            "vs_baseline": round(samples_per_s / ref, 2) if ref else None,
+            "baseline": ({"value": ref, "unit": "samples/s", "what": "reference FedAvg loop (hfl_complete.py), "
+                          "stock PyTorch-ROCm fp32, 1x MI355X"} if ref else None),
+            "dtype": args.precision,
             "data": "synthetic",
+            "w_global_sha256": w_hash,
             "rounds_per_sec": round(rounds_per_s, 4),
             "local_samples_per_round": samples // max(args.steps, 1),
             "config": {"model": "resnet18-cifar10", "global_batch": args.batch * args.clients,

@@ -79,7 +79,7 @@ def main():
     gcfg = GANConfig(clients=2, local_steps=args.local_steps, batch_size=args.gan_batch,
                      train_size=10000)
     data = client_images(gcfg, dev)
-    fg = FederatedGAN(data, ctx=ctx if ctx.world > 1 else None, local_steps=args.local_steps,
+    fg = FederatedGAN(data, ctx=ctx, local_steps=args.local_steps,
                       batch_size=args.gan_batch, device=dev)
     dt_g = timed(ctx, lambda: fg.run(1), args.steps, args.warmup)
     imgs = 2 * 2 * args.local_steps * args.gan_batch * args.steps  # 2 clients x (real + fake)

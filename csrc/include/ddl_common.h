@@ -1,7 +1,9 @@
 // Common device helpers for the ddl25spring_amd HIP kernels (gfx950 / CDNA4 only).
 //
 // Conventions used by every kernel in csrc/kernels:
-//   * activations are NHWC bf16 with a leading "group" (= simulated FL client) dimension:
+//   * activations are NHWC bf16 (or fp32 in the reference-precision mode: conv_f32.hip,
+//     bn_f32.hip and the `_f32` twins of the memory-bound launchers) with a leading "group"
+//     (= simulated FL client) dimension:
 //     x[g][n][h][w][c]; every launch covers all groups through blockIdx.z (client-batched
 //     execution, one launch for all clients resident on the GPU).
 //   * master weights / grads / optimizer state are fp32 flat buffers [G][P]; the kernels
@@ -64,6 +66,23 @@ __device__ __forceinline__ i4v pack8(const float* f) {
   for (int i = 0; i < 4; ++i) v[i] = (int)pack_bf2(f[2 * i], f[2 * i + 1]);
   return v;
 }
+
+// 8 consecutive activations <-> 8 floats, for kernels templated on the activation type
+// (bf16 storage: one 16-B access; fp32 storage — the reference-precision mode: two).
+__device__ __forceinline__ void ld8(const bf16_t* p, float* v) { unpack8(*(const i4v*)p, v); }
+__device__ __forceinline__ void ld8(const float* p, float* v) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void st8(bf16_t* p, const float* v) { *(i4v*)p = pack8(v); }
+__device__ __forceinline__ void st8(float* p, const float* v) {
+  *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+  *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ float ld1(const bf16_t* p) { return bf2f(*p); }
+__device__ __forceinline__ float ld1(const float* p) { return *p; }
+__device__ __forceinline__ void st1(bf16_t* p, float v) { *p = f2bf(v); }
+__device__ __forceinline__ void st1(float* p, float v) { *p = v; }
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

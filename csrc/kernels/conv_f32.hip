@@ -1,0 +1,748 @@
+// Reference-precision (fp32) implicit-GEMM convolution on CDNA4's exact-fp32 MFMA
+// (v_mfma_f32_16x16x4_f32: fp32 operands, fp32 accumulate, bitwise an fmaf chain), NHWC fp32.
+//
+// The reference trains every model in fp32 (stock nn.Conv2d / nn.Linear, reference
+// lab/tutorial_1a/hfl_complete.py:39-80); this is the kernel family behind the framework's fp32
+// precision mode, which the headline benchmark runs. Same three products as the bf16 family
+// (conv_igemm.hip), D[p][q] = sum_k Pop[p][k] * Qop[q][k]:
+//
+//   FWD   : y [q=(n,ho,wo)][p=k]    = sum_{(r,s,c)} W[k][(r,s,c)]    * X[pix(q,r,s)][c]
+//   DGRAD : dx[q=(n,h,w)][p=c]      = sum_{(r,s,k)} W[k][(r,s,c)]    * dY[pix'(q,r,s)][k]
+//   WGRAD : dW[p=k][q=(r,s,c)]     (+)= sum_{(n,ho,wo)} dY[pix][k]   * X[pix(r,s)][c]
+//
+// Design (fp32 MFMA issues at 1/16 of the bf16 rate, so the kernel is compute-bound from a much
+// lower arithmetic intensity and needs no LDS-DMA rings or halo staging):
+//   * 256-thread workgroup, 2x2 waves over a BP x BQ tile (64/128 each), 16-deep reduction steps;
+//     each wave owns (BP/2) x (BQ/2) as 16x16 MFMA tiles (up to 16 independent accumulators);
+//   * operands are register-prefetched one step ahead with 16-byte global loads and stored to a
+//     double-buffered LDS image [rows][16 floats] whose 16-B chunk c of row r sits at
+//     c ^ ((r >> 2) & 2): every fragment is ONE ds_read_b128 (4 reduction indices = the 4 MFMA
+//     sub-steps, the same permutation of k on both operands) and conflict-free for the b128 lane
+//     groups; MN-major sources (contiguous along p or q) are transposed 4 x KU in registers;
+//   * one barrier per step; XCD-aware block order (consecutive tiles of one split / phase /
+//     client share an XCD's L2);
+//   * operand-side BatchNorm: with in_scale/in_shift the X operand is relu(x * scale + shift) on
+//     in-image pixels (zero padding stays zero), so a BN+ReLU output that feeds only a conv is
+//     never materialised (FWD reads the BN input, WGRAD recomputes it);
+//   * DETERMINISTIC by construction — no floating-point atomics anywhere:
+//       - FWD BN statistics and the DGRAD epilogue's BN-backward reduce are written per q-tile into
+//         their own slot [G][slots][2][Pd] (plain stores, no zero-fill), folded in fixed order;
+//       - split-K (grids too small to fill 256 CUs) stores fp32 partial slices that a second
+//         kernel sums in slice order before the epilogue / the weight update;
+//       - WGRAD's (out = out + gscale * dW) has exactly one writer per element (gscale = -lr on
+//         the master weights is plain SGD fused into the backward).
+//   * stride-2 DGRAD runs as four sub-pixel phases (no MFMA on taps that miss every output);
+//     larger strides (none in the model zoo) run unphased with a per-tap divisibility test.
+#include "ddl_common.h"
+
+struct ConvF32Args {
+  const float* x;         // [G][N][H][W][C]                    (group stride x_gs)
+  const float* w;         // [G][K][R][S][C]                    (w_gs)
+  const float* dy;        // [G][N][P][Q][K]                    (dy_gs)
+  float* out;             // FWD y [G][N][P][Q][K] | DGRAD dx [G][N][H][W][C] | WGRAD dw like w (out_gs)
+  float* stats;           // FWD: [G][slots][2][K] (sum, sumsq) | DGRAD with bn_x: [G][slots][2][C]
+  const float* bias;      // FWD [G][K] (bias_gs)
+  const float* residual;  // FWD / DGRAD: added (layout of out; DGRAD res_sub 2: compact grid, res_gs)
+  const float* mask;      // DGRAD: dx *= (mask > 0) (layout of out)
+  const float* in_scale;  // X operand transform (FWD / WGRAD): [G][C] contiguous
+  const float* in_shift;
+  const float* bn_x;      // DGRAD BN-backward reduce: the preceding BN's input (layout of out)
+  const float* bn_mean;   // [G][C]
+  const float* bn_rstd;
+  const float* mask_scale;  // DGRAD: keep dx where bn_x * mask_scale + mask_shift > 0
+  const float* mask_shift;
+  float* partial;         // split-K workspace
+  long long partial_cap;  // floats at `partial`
+  long long x_gs, w_gs, dy_gs, out_gs, bias_gs, res_gs;
+  int G, N, H, W, C, K, R, S, P, Q, stride, pad;
+  int relu, accumulate, split_k, res_sub, in_relu;
+  int slots;              // stats / BN-reduce slots per group (filled by the launcher)
+  float gscale;           // WGRAD: out = (accumulate ? out : 0) + gscale * dW
+};
+
+enum { F_FWD = 0, F_DGRAD = 1, F_WGRAD = 2 };
+constexpr int FBK = 16;
+
+__device__ __forceinline__ int fswz(int row) { return (row >> 2) & 2; }
+__device__ __forceinline__ int lds_off(int row, int ch) { return row * 16 + ((ch ^ fswz(row)) << 2); }
+
+struct FDiv {
+  uint32_t m;
+  int s;
+};
+__host__ __device__ inline FDiv mk_fdiv(uint32_t d) {
+  FDiv f;
+  if (d <= 1) { f.m = 0; f.s = 0; return f; }
+  int l = 0;
+  while ((1u << l) < d) ++l;
+  f.m = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+  f.s = l;
+  return f;
+}
+__device__ __forceinline__ int fdv(int x, FDiv f) {
+  if (f.s == 0) return x;
+  const uint32_t t = __umulhi((uint32_t)x, f.m);
+  return (int)((t + (((uint32_t)x - t) >> 1)) >> (f.s - 1));
+}
+
+// Per-block problem geometry (shared by the main kernel and the split-K epilogue kernel).
+struct FGeo {
+  int Pd, Qd, Kr, nph, phase, split, nsplit, g, p0, q0, tq;
+  int pa, pb, Hs, Ws, r0, s0, Rn, Sn;
+};
+
+template <int MODE, int BP, int BQ>
+__device__ __forceinline__ FGeo fgeo(const ConvF32Args& a, int bx, int by, int g, int gy) {
+  FGeo o;
+  o.nph = (MODE == F_DGRAD && a.stride == 2) ? 4 : 1;
+  o.phase = by % o.nph;
+  o.split = by / o.nph;
+  o.nsplit = gy / o.nph;
+  o.g = g;
+  o.pa = o.pb = o.r0 = o.s0 = 0;
+  o.Hs = a.H; o.Ws = a.W; o.Rn = a.R; o.Sn = a.S;
+  if (MODE == F_FWD) {
+    o.Pd = a.K; o.Qd = a.N * a.P * a.Q; o.Kr = a.R * a.S * a.C;
+  } else if (MODE == F_DGRAD) {
+    o.Pd = a.C;
+    if (o.nph == 4) {
+      o.pa = o.phase >> 1; o.pb = o.phase & 1;
+      o.Hs = (a.H - o.pa + 1) >> 1; o.Ws = (a.W - o.pb + 1) >> 1;
+      o.r0 = (o.pa + a.pad) & 1; o.s0 = (o.pb + a.pad) & 1;
+      o.Rn = (a.R - o.r0 + 1) >> 1; o.Sn = (a.S - o.s0 + 1) >> 1;
+    }
+    o.Qd = a.N * o.Hs * o.Ws;
+    o.Kr = o.Rn * o.Sn * a.K;
+  } else {
+    o.Pd = a.K; o.Qd = a.R * a.S * a.C; o.Kr = a.N * a.P * a.Q;
+  }
+  const int ntp = (o.Pd + BP - 1) / BP;
+  o.p0 = (bx % ntp) * BP;
+  o.tq = bx / ntp;
+  o.q0 = o.tq * BQ;
+  return o;
+}
+
+// ------------------------------------------------------------------------------------ epilogue
+// acc[ti][tj][v] of this lane holds D[p][q], p = p0 + wp*WP + ti*16 + 4*(lane>>4) + v,
+// q = q0 + wq*WQ + tj*16 + (lane & 15).
+template <int MODE, int BP, int BQ>
+__device__ __forceinline__ void fepilogue(const ConvF32Args& a, const FGeo& o,
+                                          f4v (&acc)[BP / 32][BQ / 32], float* red) {
+  constexpr int WP = BP / 2, WQ = BQ / 2, TP = WP / 16, TQ = WQ / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wp = wid >> 1, wq = wid & 1;
+  const int g = o.g;
+  if constexpr (MODE == F_WGRAD) {
+    const int RSC = o.Qd;
+    float* outg = a.out + (long long)g * a.out_gs;
+#pragma unroll
+    for (int ti = 0; ti < TP; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < TQ; ++tj) {
+        const int q = o.q0 + wq * WQ + tj * 16 + (lane & 15);
+        if (q >= RSC) continue;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int p = o.p0 + wp * WP + ti * 16 + 4 * (lane >> 4) + v;
+          if (p >= o.Pd) continue;
+          float* d = outg + (long long)p * RSC + q;
+          const float base = a.accumulate ? *d : 0.f;
+          *d = base + a.gscale * acc[ti][tj][v];
+        }
+      }
+    return;
+  }
+  const bool want_stats = a.stats != nullptr;
+  const int Pd = o.Pd;
+  float* outg = a.out + (long long)g * a.out_gs;
+  float s0[TP][4], s1[TP][4];
+#pragma unroll
+  for (int ti = 0; ti < TP; ++ti)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) s0[ti][v] = s1[ti][v] = 0.f;
+
+  // per-p constants of this lane (4 consecutive channels per ti)
+  float bia[TP][4], bm[TP][4], br[TP][4], ms[TP][4], mh[TP][4];
+#pragma unroll
+  for (int ti = 0; ti < TP; ++ti) {
+    const int pb4 = o.p0 + wp * WP + ti * 16 + 4 * (lane >> 4);
+    const bool pv = pb4 < Pd;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      bia[ti][v] = (MODE == F_FWD && a.bias && pv) ? a.bias[(long long)g * a.bias_gs + pb4 + v] : 0.f;
+      bm[ti][v] = (MODE == F_DGRAD && a.bn_x && pv) ? a.bn_mean[(long long)g * Pd + pb4 + v] : 0.f;
+      br[ti][v] = (MODE == F_DGRAD && a.bn_x && pv) ? a.bn_rstd[(long long)g * Pd + pb4 + v] : 0.f;
+      ms[ti][v] = (MODE == F_DGRAD && a.mask_scale && pv) ? a.mask_scale[(long long)g * Pd + pb4 + v] : 0.f;
+      mh[ti][v] = (MODE == F_DGRAD && a.mask_scale && pv) ? a.mask_shift[(long long)g * Pd + pb4 + v] : 0.f;
+    }
+  }
+  const FDiv dpq = mk_fdiv((uint32_t)(o.Hs * o.Ws)), dq = mk_fdiv((uint32_t)o.Ws);
+#pragma unroll
+  for (int tj = 0; tj < TQ; ++tj) {
+    const int q = o.q0 + wq * WQ + tj * 16 + (lane & 15);
+    const bool qv = q < o.Qd;
+    long long pix = q;  // output / input pixel index of q (row of out)
+    int hh = 0, ww = 0, nn = 0;
+    if (MODE == F_DGRAD) {
+      nn = fdv(q, dpq);
+      const int rem = q - nn * o.Hs * o.Ws;
+      const int i = fdv(rem, dq), j = rem - i * o.Ws;
+      hh = o.nph == 4 ? 2 * i + o.pa : i;
+      ww = o.nph == 4 ? 2 * j + o.pb : j;
+      pix = ((long long)nn * a.H + hh) * a.W + ww;
+    }
+#pragma unroll
+    for (int ti = 0; ti < TP; ++ti) {
+      const int p = o.p0 + wp * WP + ti * 16 + 4 * (lane >> 4);
+      if (!qv || p >= Pd) continue;
+      const long long e = pix * Pd + p;
+      float v4[4] = {acc[ti][tj][0], acc[ti][tj][1], acc[ti][tj][2], acc[ti][tj][3]};
+      if (MODE == F_FWD) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) v4[v] += bia[ti][v];
+        if (a.residual) {
+          const float4 r = *(const float4*)(a.residual + (long long)g * a.out_gs + e);
+          v4[0] += r.x; v4[1] += r.y; v4[2] += r.z; v4[3] += r.w;
+        }
+        if (a.relu) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) v4[v] = fmaxf(v4[v], 0.f);
+        }
+        if (want_stats) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) { s0[ti][v] += v4[v]; s1[ti][v] += v4[v] * v4[v]; }
+        }
+      } else {  // DGRAD
+        if (a.residual) {
+          if (a.res_sub == 2) {
+            if (((hh | ww) & 1) == 0) {
+              const int Hc = (a.H + 1) >> 1, Wc = (a.W + 1) >> 1;
+              const long long re = (((long long)nn * Hc + (hh >> 1)) * Wc + (ww >> 1)) * Pd + p;
+              const float4 r = *(const float4*)(a.residual + (long long)g * a.res_gs + re);
+              v4[0] += r.x; v4[1] += r.y; v4[2] += r.z; v4[3] += r.w;
+            }
+          } else {
+            const float4 r = *(const float4*)(a.residual + (long long)g * a.out_gs + e);
+            v4[0] += r.x; v4[1] += r.y; v4[2] += r.z; v4[3] += r.w;
+          }
+        }
+        if (a.mask) {
+          const float4 m = *(const float4*)(a.mask + (long long)g * a.out_gs + e);
+          if (!(m.x > 0.f)) v4[0] = 0.f;
+          if (!(m.y > 0.f)) v4[1] = 0.f;
+          if (!(m.z > 0.f)) v4[2] = 0.f;
+          if (!(m.w > 0.f)) v4[3] = 0.f;
+        }
+        if (a.bn_x) {
+          const float4 xb = *(const float4*)(a.bn_x + (long long)g * a.out_gs + e);
+          const float xs[4] = {xb.x, xb.y, xb.z, xb.w};
+          if (a.mask_scale) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+              if (!(xs[v] * ms[ti][v] + mh[ti][v] > 0.f)) v4[v] = 0.f;
+          }
+          if (want_stats) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              s0[ti][v] += v4[v];
+              s1[ti][v] += v4[v] * ((xs[v] - bm[ti][v]) * br[ti][v]);
+            }
+          }
+        }
+      }
+      *(float4*)(outg + e) = make_float4(v4[0], v4[1], v4[2], v4[3]);
+    }
+  }
+  if (!want_stats || (MODE == F_DGRAD && !a.bn_x)) return;
+  // per-channel partial sums of this tile -> its own slot (fixed-order, no atomics)
+#pragma unroll
+  for (int ti = 0; ti < TP; ++ti)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      float x0 = s0[ti][v], x1 = s1[ti][v];
+#pragma unroll
+      for (int o2 = 1; o2 < 16; o2 <<= 1) {
+        x0 += __shfl_xor(x0, o2, 64);
+        x1 += __shfl_xor(x1, o2, 64);
+      }
+      if ((lane & 15) == 0) {
+        const int pl = wp * WP + ti * 16 + 4 * (lane >> 4) + v;
+        red[(wq * BP + pl) * 2] = x0;
+        red[(wq * BP + pl) * 2 + 1] = x1;
+      }
+    }
+  __syncthreads();
+  if (tid < BP && o.p0 + tid < Pd) {
+    const float t0 = red[tid * 2] + red[(BP + tid) * 2];
+    const float t1 = red[tid * 2 + 1] + red[(BP + tid) * 2 + 1];
+    const int slot = o.phase * (a.slots / o.nph) + o.tq;
+    float* st = a.stats + ((long long)g * a.slots + slot) * 2 * Pd + o.p0 + tid;
+    st[0] = t0;
+    st[Pd] = t1;
+  }
+}
+
+// zero stats slot of a tile that has no work (q0 beyond a smaller DGRAD phase)
+template <int MODE, int BP>
+__device__ __forceinline__ void fzero_slot(const ConvF32Args& a, const FGeo& o) {
+  if (MODE == F_WGRAD || !a.stats || (MODE == F_DGRAD && !a.bn_x)) return;
+  const int tid = threadIdx.x;
+  if (tid < BP && o.p0 + tid < o.Pd) {
+    const int slot = o.phase * (a.slots / o.nph) + o.tq;
+    float* st = a.stats + ((long long)o.g * a.slots + slot) * 2 * o.Pd + o.p0 + tid;
+    st[0] = 0.f;
+    st[o.Pd] = 0.f;
+  }
+}
+
+// ------------------------------------------------------------------------------------ main kernel
+template <int MODE, int BP, int BQ>
+__global__ __launch_bounds__(256, 2) void convf32_kernel(ConvF32Args a) {
+  constexpr int WP = BP / 2, WQ = BQ / 2, TP = WP / 16, TQ = WQ / 16;
+  constexpr int SP = BP * 16, SQ = BQ * 16;     // floats per operand image
+  constexpr int UPK = BP / 64, UQK = BQ / 64;    // K-major units (float4) per thread
+  constexpr int KUP = BP / 64, KUQ = BQ / 64;    // MN-major reductions per unit (4 rows x KU)
+  __shared__ float4 smem4[(2 * (SP + SQ)) / 4];
+  float* smem = (float*)smem4;
+  __shared__ float xform[2 * 512];               // in_scale | in_shift (C <= 512)
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wp = wid >> 1, wq = wid & 1;
+  const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+  const int lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int u = xcd_remap(lin, gx * gy * gz);
+  const int bx = u % gx, by = (u / gx) % gy, g = u / (gx * gy);
+  const FGeo o = fgeo<MODE, BP, BQ>(a, bx, by, g, gy);
+  const bool split_store = a.split_k > 1;
+  if (o.q0 >= o.Qd || o.p0 >= o.Pd) {
+    if (!split_store) fzero_slot<MODE, BP>(a, o);
+    return;
+  }
+  const int nk = (o.Kr + FBK - 1) / FBK;
+  const int per = (nk + o.nsplit - 1) / o.nsplit;
+  const int kt0 = o.split * per, kt1 = min(nk, kt0 + per);
+
+  const int H = a.H, W = a.W, C = a.C, K = a.K, S = a.S, P = a.P, Q = a.Q, st = a.stride, pd = a.pad;
+  const float* X = a.x + (long long)g * a.x_gs;
+  const float* Wt = a.w + (long long)g * a.w_gs;
+  const float* DY = a.dy + (long long)g * a.dy_gs;
+  const bool xf = (MODE != F_DGRAD) && a.in_scale != nullptr;
+  if (xf) {
+    for (int i = tid; i < C; i += 256) {
+      xform[i] = a.in_scale[(long long)g * C + i];
+      xform[512 + i] = a.in_shift[(long long)g * C + i];
+    }
+  }
+  const bool xrelu = a.in_relu != 0;
+
+  // ----------------------------------------------------------- per-thread operand bookkeeping
+  // P operand
+  int pk_row[UPK], pk_ch[UPK];  // FWD K-major units
+  int pm_rg = 0, pm_kp = 0;     // DGRAD / WGRAD MN-major unit
+  if constexpr (MODE == F_FWD) {
+#pragma unroll
+    for (int i = 0; i < UPK; ++i) {
+      const int uu = tid + 256 * i;
+      pk_row[i] = uu >> 2;
+      pk_ch[i] = uu & 3;
+    }
+  } else {
+    pm_kp = tid % (16 / KUP);
+    pm_rg = tid / (16 / KUP);
+  }
+  // Q operand
+  int qk_row[UQK], qk_ch[UQK], qk_n[UQK], qk_hb[UQK], qk_wb[UQK];
+  int qm_rg = 0, qm_kp = 0, qm_r = 0, qm_s = 0, qm_c = 0;
+  bool qm_ok = false;
+  float qm_sc[4] = {1.f, 1.f, 1.f, 1.f}, qm_sh[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (MODE != F_WGRAD) {
+    const FDiv dpq = mk_fdiv((uint32_t)(MODE == F_FWD ? P * Q : o.Hs * o.Ws));
+    const FDiv dq = mk_fdiv((uint32_t)(MODE == F_FWD ? Q : o.Ws));
+    const int PQ = MODE == F_FWD ? P * Q : o.Hs * o.Ws, QQ = MODE == F_FWD ? Q : o.Ws;
+#pragma unroll
+    for (int i = 0; i < UQK; ++i) {
+      const int uu = tid + 256 * i;
+      qk_row[i] = uu >> 2;
+      qk_ch[i] = uu & 3;
+      const int q = o.q0 + qk_row[i];
+      if (q < o.Qd) {
+        const int n = fdv(q, dpq), rem = q - n * PQ;
+        const int y = fdv(rem, dq), xq = rem - y * QQ;
+        qk_n[i] = n;
+        if (MODE == F_FWD) {
+          qk_hb[i] = y * st - pd;
+          qk_wb[i] = xq * st - pd;
+        } else {  // DGRAD: (h + pad, w + pad) of the input pixel
+          qk_hb[i] = (o.nph == 4 ? 2 * y + o.pa : y) + pd;
+          qk_wb[i] = (o.nph == 4 ? 2 * xq + o.pb : xq) + pd;
+        }
+      } else {
+        qk_n[i] = -1;
+        qk_hb[i] = qk_wb[i] = 0;
+      }
+    }
+  } else {
+    qm_kp = tid % (16 / KUQ);
+    qm_rg = tid / (16 / KUQ);
+    const int q = o.q0 + 4 * qm_rg;
+    qm_ok = q < o.Qd;
+    if (qm_ok) {
+      const int tap = q / C;
+      qm_c = q - tap * C;
+      qm_r = tap / S;
+      qm_s = tap - qm_r * S;
+    }
+  }
+  if (xf) __syncthreads();
+  if constexpr (MODE == F_WGRAD) {
+    if (xf && qm_ok) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) { qm_sc[v] = xform[qm_c + v]; qm_sh[v] = xform[512 + qm_c + v]; }
+    }
+  }
+  const FDiv dpix = mk_fdiv((uint32_t)(P * Q)), dpq1 = mk_fdiv((uint32_t)Q);
+
+  // ----------------------------------------------------------- global -> registers (step kt)
+  float4 rp[2], rq[2];
+  auto load_step = [&](int kt) {
+    const int kk0 = kt * FBK;
+    // P operand
+    if constexpr (MODE == F_FWD) {
+#pragma unroll
+      for (int i = 0; i < UPK; ++i) {
+        const int p = o.p0 + pk_row[i];
+        rp[i] = p < o.Pd ? *(const float4*)(Wt + (long long)p * o.Kr + kk0 + 4 * pk_ch[i])
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    } else if constexpr (MODE == F_DGRAD) {
+      const int tap = kk0 / K, k0 = kk0 - tap * K;
+      const int ir = tap / o.Sn, is = tap - ir * o.Sn;
+      const int r = o.r0 + (st == 2 ? 2 : 1) * ir, s = o.s0 + (st == 2 ? 2 : 1) * is;
+      const int c = o.p0 + 4 * pm_rg;
+#pragma unroll
+      for (int j = 0; j < KUP; ++j) {
+        const int k = k0 + pm_kp * KUP + j;
+        rp[j] = c < C ? *(const float4*)(Wt + (((long long)k * a.R + r) * S + s) * C + c)
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    } else {  // WGRAD: dY rows = channels k
+      const int kch = o.p0 + 4 * pm_rg;
+#pragma unroll
+      for (int j = 0; j < KUP; ++j) {
+        const int pix = kk0 + pm_kp * KUP + j;
+        rp[j] = (pix < o.Kr && kch < K) ? *(const float4*)(DY + (long long)pix * K + kch)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    // Q operand
+    if constexpr (MODE == F_FWD) {
+      const int tap = kk0 / C, c0 = kk0 - tap * C;
+      const int r = tap / S, s = tap - r * S;
+#pragma unroll
+      for (int i = 0; i < UQK; ++i) {
+        const int h = qk_hb[i] + r, w = qk_wb[i] + s;
+        const bool ok = qk_n[i] >= 0 && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+        const int c = c0 + 4 * qk_ch[i];
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ok) {
+          v = *(const float4*)(X + (((long long)qk_n[i] * H + h) * W + w) * C + c);
+          if (xf) {
+            v.x = v.x * xform[c] + xform[512 + c];
+            v.y = v.y * xform[c + 1] + xform[512 + c + 1];
+            v.z = v.z * xform[c + 2] + xform[512 + c + 2];
+            v.w = v.w * xform[c + 3] + xform[512 + c + 3];
+            if (xrelu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+          }
+        }
+        rq[i] = v;
+      }
+    } else if constexpr (MODE == F_DGRAD) {
+      const int tap = kk0 / K, k0 = kk0 - tap * K;
+      const int ir = tap / o.Sn, is = tap - ir * o.Sn;
+      const int r = o.r0 + (st == 2 ? 2 : 1) * ir, s = o.s0 + (st == 2 ? 2 : 1) * is;
+#pragma unroll
+      for (int i = 0; i < UQK; ++i) {
+        int ho = qk_hb[i] - r, wo = qk_wb[i] - s;
+        bool hit = true;
+        if (st == 2) {
+          ho >>= 1;  // exact: the phase's taps keep (h + pad - r) even
+          wo >>= 1;
+        } else if (st > 2) {  // unphased: only the taps that land on an output position
+          hit = ho >= 0 && wo >= 0 && ho % st == 0 && wo % st == 0;
+          ho /= st;
+          wo /= st;
+        }
+        const bool ok = hit && qk_n[i] >= 0 && (unsigned)ho < (unsigned)P && (unsigned)wo < (unsigned)Q;
+        rq[i] = ok ? *(const float4*)(DY + (((long long)qk_n[i] * P + ho) * Q + wo) * K + k0 + 4 * qk_ch[i])
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    } else {  // WGRAD: X rows = (r, s, c)
+#pragma unroll
+      for (int j = 0; j < KUQ; ++j) {
+        const int pix = kk0 + qm_kp * KUQ + j;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (qm_ok && pix < o.Kr) {
+          const int n = fdv(pix, dpix), rem = pix - n * P * Q;
+          const int ho = fdv(rem, dpq1), wo = rem - ho * Q;
+          const int h = ho * st - pd + qm_r, w = wo * st - pd + qm_s;
+          if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
+            v = *(const float4*)(X + (((long long)n * H + h) * W + w) * C + qm_c);
+            if (xf) {
+              v.x = v.x * qm_sc[0] + qm_sh[0];
+              v.y = v.y * qm_sc[1] + qm_sh[1];
+              v.z = v.z * qm_sc[2] + qm_sh[2];
+              v.w = v.w * qm_sc[3] + qm_sh[3];
+              if (xrelu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+            }
+          }
+        }
+        rq[j] = v;
+      }
+    }
+  };
+  // ----------------------------------------------------------- registers -> LDS image
+  auto store_mn = [&](float* img, int rg, int kp, int KU, const float4* v) {
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      const int row = 4 * rg + j4;
+      const int kk = kp * KU;
+      float* d = img + row * 16 + (((kk >> 2) ^ fswz(row)) << 2) + (kk & 3);
+      const float e0 = j4 == 0 ? v[0].x : j4 == 1 ? v[0].y : j4 == 2 ? v[0].z : v[0].w;
+      if (KU == 2) {
+        const float e1 = j4 == 0 ? v[1].x : j4 == 1 ? v[1].y : j4 == 2 ? v[1].z : v[1].w;
+        *(float2*)d = make_float2(e0, e1);
+      } else {
+        *d = e0;
+      }
+    }
+  };
+  auto store_step = [&](int buf) {
+    float* Ps = smem + buf * (SP + SQ);
+    float* Qs = Ps + SP;
+    if constexpr (MODE == F_FWD) {
+#pragma unroll
+      for (int i = 0; i < UPK; ++i) *(float4*)(Ps + lds_off(pk_row[i], pk_ch[i])) = rp[i];
+    } else {
+      store_mn(Ps, pm_rg, pm_kp, KUP, rp);
+    }
+    if constexpr (MODE != F_WGRAD) {
+#pragma unroll
+      for (int i = 0; i < UQK; ++i) *(float4*)(Qs + lds_off(qk_row[i], qk_ch[i])) = rq[i];
+    } else {
+      store_mn(Qs, qm_rg, qm_kp, KUQ, rq);
+    }
+  };
+
+  f4v acc[TP][TQ];
+#pragma unroll
+  for (int i = 0; i < TP; ++i)
+#pragma unroll
+    for (int j = 0; j < TQ; ++j) acc[i][j] = (f4v){0.f, 0.f, 0.f, 0.f};
+
+  if (kt0 < kt1) {
+    load_step(kt0);
+    store_step(0);
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int cur = (kt - kt0) & 1;
+      const bool more = kt + 1 < kt1;
+      if (more) load_step(kt + 1);
+      const float* Ps = smem + cur * (SP + SQ);
+      const float* Qs = Ps + SP;
+      float4 af[TP], bfr[TQ];
+#pragma unroll
+      for (int ti = 0; ti < TP; ++ti)
+        af[ti] = *(const float4*)(Ps + lds_off(wp * WP + ti * 16 + (lane & 15), lane >> 4));
+#pragma unroll
+      for (int tj = 0; tj < TQ; ++tj)
+        bfr[tj] = *(const float4*)(Qs + lds_off(wq * WQ + tj * 16 + (lane & 15), lane >> 4));
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int ti = 0; ti < TP; ++ti)
+#pragma unroll
+          for (int tj = 0; tj < TQ; ++tj) {
+            const float av = s4 == 0 ? af[ti].x : s4 == 1 ? af[ti].y : s4 == 2 ? af[ti].z : af[ti].w;
+            const float bv = s4 == 0 ? bfr[tj].x : s4 == 1 ? bfr[tj].y : s4 == 2 ? bfr[tj].z : bfr[tj].w;
+            acc[ti][tj] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[ti][tj], 0, 0, 0);
+          }
+      if (more) store_step(cur ^ 1);
+      __syncthreads();
+    }
+  }
+
+  if (split_store) {
+    // raw partial sums of this split slice: FWD / DGRAD [split][G][nph][Qd_max][Pd]; WGRAD [split][G][Pd][Qd]
+#pragma unroll
+    for (int ti = 0; ti < TP; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < TQ; ++tj) {
+        const int q = o.q0 + wq * WQ + tj * 16 + (lane & 15);
+        const int p = o.p0 + wp * WP + ti * 16 + 4 * (lane >> 4);
+        if (q >= o.Qd || p >= o.Pd) continue;
+        if constexpr (MODE == F_WGRAD) {
+          float* d = a.partial + ((long long)o.split * a.G + g) * o.Pd * o.Qd;
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            if (p + v < o.Pd) d[(long long)(p + v) * o.Qd + q] = acc[ti][tj][v];
+        } else {
+          const long long qmax = (long long)a.slots / o.nph * BQ;  // rows per phase (tile-padded)
+          float* d = a.partial + (((long long)o.split * a.G + g) * o.nph + o.phase) * qmax * o.Pd;
+          *(float4*)(d + (long long)q * o.Pd + p) = make_float4(acc[ti][tj][0], acc[ti][tj][1],
+                                                                acc[ti][tj][2], acc[ti][tj][3]);
+        }
+      }
+    return;
+  }
+  fepilogue<MODE, BP, BQ>(a, o, acc, smem);
+}
+
+// FWD / DGRAD split-K: sum the slices in slice order, then the same epilogue as the main kernel.
+template <int MODE, int BP, int BQ>
+__global__ __launch_bounds__(256) void convf32_splitk_epilogue(ConvF32Args a) {
+  constexpr int WP = BP / 2, WQ = BQ / 2, TP = WP / 16, TQ = WQ / 16;
+  __shared__ float red[2 * BP * 2];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wp = wid >> 1, wq = wid & 1;
+  const int nph = (MODE == F_DGRAD && a.stride == 2) ? 4 : 1;
+  const FGeo o = fgeo<MODE, BP, BQ>(a, blockIdx.x, blockIdx.y, blockIdx.z, nph * a.split_k);
+  if (o.q0 >= o.Qd || o.p0 >= o.Pd) {
+    fzero_slot<MODE, BP>(a, o);
+    return;
+  }
+  const long long qmax = (long long)a.slots / nph * BQ;
+  const long long slice = (long long)a.G * nph * qmax * o.Pd;
+  const float* base = a.partial + ((long long)o.g * nph + o.phase) * qmax * o.Pd;
+  f4v acc[TP][TQ];
+#pragma unroll
+  for (int ti = 0; ti < TP; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < TQ; ++tj) {
+      const int q = o.q0 + wq * WQ + tj * 16 + (lane & 15);
+      const int p = o.p0 + wp * WP + ti * 16 + 4 * (lane >> 4);
+      f4v s = (f4v){0.f, 0.f, 0.f, 0.f};
+      if (q < o.Qd && p < o.Pd) {
+        const float* src = base + (long long)q * o.Pd + p;
+        for (int k = 0; k < a.split_k; ++k) {
+          const float4 v = *(const float4*)(src + k * slice);
+          s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
+        }
+      }
+      acc[ti][tj] = s;
+    }
+  fepilogue<MODE, BP, BQ>(a, o, acc, red);
+}
+
+// WGRAD split-K: out = (accumulate ? out : 0) + gscale * sum_k partial[k] (slice order).
+__global__ __launch_bounds__(256) void convf32_wgrad_reduce(const float* __restrict__ part, float* out,
+                                                            long long out_gs, int G, long long n4,
+                                                            int splits, int accumulate, float gscale) {
+  const long long per = n4 * 4;
+  GSTRIDE_LOOP(t, (long long)G * n4) {
+    const long long g = t / n4, i = (t - g * n4) * 4;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* src = part + g * per + i;
+    for (int k = 0; k < splits; ++k) {
+      const float4 v = *(const float4*)(src + (long long)k * G * per);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    float* d = out + g * out_gs + i;
+    float4 b = accumulate ? *(const float4*)d : make_float4(0.f, 0.f, 0.f, 0.f);
+    b.x += gscale * s.x; b.y += gscale * s.y; b.z += gscale * s.z; b.w += gscale * s.w;
+    *(float4*)d = b;
+  }
+}
+
+// ------------------------------------------------------------------------------------ launchers
+static void fdims(const ConvF32Args& a, int mode, long long& Pd, long long& Qd, long long& Qmax, long long& Kr,
+                  int& nph) {
+  nph = (mode == F_DGRAD && a.stride == 2) ? 4 : 1;
+  if (mode == F_FWD) { Pd = a.K; Qd = Qmax = (long long)a.N * a.P * a.Q; Kr = (long long)a.R * a.S * a.C; }
+  else if (mode == F_DGRAD) {
+    Pd = a.C;
+    const int Hs = nph == 4 ? (a.H + 1) >> 1 : a.H, Ws = nph == 4 ? (a.W + 1) >> 1 : a.W;
+    Qd = Qmax = (long long)a.N * Hs * Ws;
+    Kr = (long long)a.R * a.S * a.K;
+  } else { Pd = a.K; Qd = Qmax = (long long)a.R * a.S * a.C; Kr = (long long)a.N * a.P * a.Q; }
+}
+
+// slots per group of the stats / BN-reduce buffer this launch writes (tile config cfg)
+DDL_API long long ddl_convf32_slots(const ConvF32Args* ap, int mode, int cfg) {
+  long long Pd, Qd, Qmax, Kr;
+  int nph;
+  fdims(*ap, mode, Pd, Qd, Qmax, Kr, nph);
+  const int bq = ((cfg >> 8) & 0xff) * 16;
+  if (bq <= 0) return -1;
+  return nph * ((Qmax + bq - 1) / bq);
+}
+
+// floats of split-K workspace a launch needs (0: none)
+DDL_API long long ddl_convf32_workspace(const ConvF32Args* ap, int mode, int cfg) {
+  if (ap->split_k <= 1) return 0;
+  long long Pd, Qd, Qmax, Kr;
+  int nph;
+  fdims(*ap, mode, Pd, Qd, Qmax, Kr, nph);
+  const int bq = ((cfg >> 8) & 0xff) * 16;
+  if (mode == F_WGRAD) return (long long)ap->split_k * ap->G * Pd * Qd;
+  const long long qm = (Qmax + bq - 1) / bq * bq;
+  return (long long)ap->split_k * ap->G * nph * qm * Pd;
+}
+
+template <int MODE, int BP, int BQ>
+static int launch_tile(ConvF32Args a, hipStream_t s) {
+  long long Pd, Qd, Qmax, Kr;
+  int nph;
+  fdims(a, MODE, Pd, Qd, Qmax, Kr, nph);
+  const long long ntp = (Pd + BP - 1) / BP, ntq = (Qmax + BQ - 1) / BQ;
+  a.slots = (int)(nph * ntq);
+  const int split = a.split_k < 1 ? 1 : a.split_k;
+  a.split_k = split;
+  if (split > 1) {
+    const long long need = MODE == F_WGRAD ? (long long)split * a.G * Pd * Qd
+                                           : (long long)split * a.G * nph * ntq * BQ * Pd;
+    if (!a.partial || need > a.partial_cap) return (int)hipErrorInvalidValue;
+  }
+  const dim3 grid((unsigned)(ntp * ntq), (unsigned)(nph * split), (unsigned)a.G);
+  hipLaunchKernelGGL((convf32_kernel<MODE, BP, BQ>), grid, dim3(256), 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || split == 1) return (int)e;
+  if (MODE == F_WGRAD) {
+    const long long n4 = Pd * Qd / 4;
+    hipLaunchKernelGGL(convf32_wgrad_reduce, dim3(grid_for((long long)a.G * n4, 256)), dim3(256), 0, s,
+                       (const float*)a.partial, a.out, a.out_gs, a.G, n4, split, a.accumulate, a.gscale);
+  } else {
+    hipLaunchKernelGGL((convf32_splitk_epilogue<MODE, BP, BQ>), dim3((unsigned)(ntp * ntq), nph, a.G),
+                       dim3(256), 0, s, a);
+  }
+  return (int)hipGetLastError();
+}
+
+template <int MODE>
+static int launch_mode(const ConvF32Args& a, int cfg, hipStream_t s) {
+  const int bp = (cfg & 0xff) * 16, bq = ((cfg >> 8) & 0xff) * 16;
+  if (bp == 64 && bq == 64) return launch_tile<MODE, 64, 64>(a, s);
+  if (bp == 64 && bq == 128) return launch_tile<MODE, 64, 128>(a, s);
+  if (bp == 128 && bq == 64) return launch_tile<MODE, 128, 64>(a, s);
+  if (bp == 128 && bq == 128) return launch_tile<MODE, 128, 128>(a, s);
+  return (int)hipErrorInvalidValue;
+}
+
+DDL_API int ddl_convf32(const ConvF32Args* ap, int mode, int cfg, hipStream_t s) {
+  const ConvF32Args& a = *ap;
+  if (a.G < 1 || a.N < 1 || a.C < 1 || a.K < 1 || a.stride < 1) return (int)hipErrorInvalidValue;
+  if (a.C > 512 && a.in_scale) return (int)hipErrorInvalidValue;
+  if (mode == F_FWD) {
+    if (a.C % 16 || a.K % 4) return (int)hipErrorInvalidValue;
+    return launch_mode<F_FWD>(a, cfg, s);
+  }
+  if (mode == F_DGRAD) {
+    if (a.K % 16 || a.C % 4) return (int)hipErrorInvalidValue;
+    return launch_mode<F_DGRAD>(a, cfg, s);
+  }
+  if (mode == F_WGRAD) {
+    if (a.C % 4 || a.K % 4) return (int)hipErrorInvalidValue;
+    if (!a.accumulate && a.gscale != 1.f) return (int)hipErrorInvalidValue;
+    return launch_mode<F_WGRAD>(a, cfg, s);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+DDL_API int ddl_convf32_args_size() { return (int)sizeof(ConvF32Args); }

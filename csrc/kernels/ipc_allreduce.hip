@@ -53,7 +53,10 @@ __device__ __forceinline__ float* ipc_data(char* base, unsigned epoch, long long
 
 // Block-level cross-rank barrier for (phase, this block): every wave drains its stores, one
 // lane per peer publishes `epoch` into that peer's signal word for (phase, block, my rank) and
-// polls my own word for (phase, block, peer).
+// polls my own word for (phase, block, peer) until it has reached `epoch`. The compare is
+// wrap-safe and monotonic (>=, not ==): back-to-back all-reduces without a host sync let a fast
+// peer overwrite its word with epoch+1 before a slow block here has seen epoch — which also
+// proves the peer passed this barrier.
 __device__ void ipc_barrier(const IpcArgs& a, int phase, unsigned epoch) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -64,7 +67,7 @@ __device__ void ipc_barrier(const IpcArgs& a, int phase, unsigned epoch) {
                        __HIP_MEMORY_SCOPE_SYSTEM);
     unsigned* mine = ipc_sig(a.base[a.rank], phase, blockIdx.x, t);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+    while ((int)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
       __builtin_amdgcn_s_sleep(2);
       if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout) {
         __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -13,20 +13,21 @@
 
 // logits [R][ld] bf16 with R = G*N rows; labels int32 [R] (hard) or targets fp32 [R][ncls] (soft)
 // loss[g] += scale * sum_rows_of_g loss_row ; dlogits = scale * (softmax*sum(t) - t) (0 for pad cols)
-__global__ __launch_bounds__(256) void ce_kernel(const bf16_t* __restrict__ logits,
+template <typename T>
+__global__ __launch_bounds__(256) void ce_kernel(const T* __restrict__ logits,
                                                  const int* __restrict__ labels,
                                                  const float* __restrict__ targets, int R, int N,
                                                  int ncls, int ld, float scale,
-                                                 float* __restrict__ loss, bf16_t* __restrict__ dlogits,
+                                                 float* __restrict__ loss, T* __restrict__ dlogits,
                                                  int* __restrict__ correct) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= R) return;
-  const bf16_t* z = logits + (long long)row * ld;
+  const T* z = logits + (long long)row * ld;
   float mx = -INFINITY;
   int amax = 0;
   for (int c = lane; c < ncls; c += 64) {
-    const float v = bf2f(z[c]);
+    const float v = ld1(z + c);
     if (v > mx) { mx = v; amax = c; }
   }
   // wave argmax (first max wins on ties, like torch.argmax)
@@ -37,7 +38,7 @@ __global__ __launch_bounds__(256) void ce_kernel(const bf16_t* __restrict__ logi
     if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
   }
   float se = 0.f;
-  for (int c = lane; c < ncls; c += 64) se += __expf(bf2f(z[c]) - mx);
+  for (int c = lane; c < ncls; c += 64) se += __expf(ld1(z + c) - mx);
   se = wave_sum(se);
   const float lse = mx + __logf(se);
   float lrow = 0.f, tsum = 1.f;
@@ -46,24 +47,24 @@ __global__ __launch_bounds__(256) void ce_kernel(const bf16_t* __restrict__ logi
     float ts = 0.f, l = 0.f;
     for (int c = lane; c < ncls; c += 64) {
       ts += t[c];
-      l += t[c] * (lse - bf2f(z[c]));
+      l += t[c] * (lse - ld1(z + c));
     }
     tsum = wave_sum(ts);
     lrow = wave_sum(l);
   } else {
     const int y = labels[row];
-    lrow = lse - bf2f(z[y]);
+    lrow = lse - ld1(z + y);
   }
   if (dlogits) {
-    bf16_t* dz = dlogits + (long long)row * ld;
+    T* dz = dlogits + (long long)row * ld;
     for (int c = lane; c < ld; c += 64) {
       float gv = 0.f;
       if (c < ncls) {
-        const float p = __expf(bf2f(z[c]) - lse);
+        const float p = __expf(ld1(z + c) - lse);
         const float tc = targets ? targets[(long long)row * ncls + c] : (c == labels[row] ? 1.f : 0.f);
         gv = scale * (p * tsum - tc);
       }
-      dz[c] = f2bf(gv);
+      st1(dz + c, gv);
     }
   }
   if (lane == 0) {
@@ -83,13 +84,24 @@ __global__ __launch_bounds__(256) void ce_kernel(const bf16_t* __restrict__ logi
   }
 }
 
+template <typename T>
+static int ce_fwd_bwd_impl(const void* logits, const int* labels, const float* targets, int R, int N, int ncls,
+                           int ld, float scale, float* loss, void* dlogits, int* correct, hipStream_t s) {
+  if (ncls > ld || N <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ce_kernel<T>, dim3((R + 3) / 4), dim3(256), 0, s, (const T*)logits, labels,
+                     targets, R, N, ncls, ld, scale, loss, (T*)dlogits, correct);
+  return (int)hipGetLastError();
+}
 DDL_API int ddl_ce_fwd_bwd(const void* logits, const int* labels, const float* targets, int R, int N,
                            int ncls, int ld, float scale, float* loss, void* dlogits, int* correct,
                            hipStream_t s) {
-  if (ncls > ld || N <= 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(ce_kernel, dim3((R + 3) / 4), dim3(256), 0, s, (const bf16_t*)logits, labels,
-                     targets, R, N, ncls, ld, scale, loss, (bf16_t*)dlogits, correct);
-  return (int)hipGetLastError();
+  return ce_fwd_bwd_impl<bf16_t>(logits, labels, targets, R, N, ncls, ld, scale, loss, dlogits, correct, s);
+}
+// fp32 logits / gradients (the reference-precision mode)
+DDL_API int ddl_ce_fwd_bwd_f32(const void* logits, const int* labels, const float* targets, int R, int N,
+                               int ncls, int ld, float scale, float* loss, void* dlogits, int* correct,
+                               hipStream_t s) {
+  return ce_fwd_bwd_impl<float>(logits, labels, targets, R, N, ncls, ld, scale, loss, dlogits, correct, s);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -23,9 +23,10 @@
 // (< k*k*Cs), rest 0 — the stem conv then runs as a 1x1 GEMM on MFMA.
 // Also gathers the labels (labels_out[b] = labels[idx[b]], nullable) so a training step's whole
 // batch materialisation is one launch.
+template <typename T>
 __global__ void prep_images_kernel(const uint8_t* __restrict__ src, const int* __restrict__ idx,
                                    const float* __restrict__ mean, const float* __restrict__ inv_std,
-                                   bf16_t* __restrict__ out, int nimg, int Hs, int Ws, int Cs,
+                                   T* __restrict__ out, int nimg, int Hs, int Ws, int Cs,
                                    int Ho, int Wo, int Cout, int im2col, int pad, int stride,
                                    const int* __restrict__ labels, int* __restrict__ labels_out) {
   const long long total = (long long)nimg * Ho * Wo * (Cout / 8);
@@ -56,7 +57,7 @@ __global__ void prep_images_kernel(const uint8_t* __restrict__ src, const int* _
       }
       v[k] = val;
     }
-    *(i4v*)(out + t * 8) = pack8(v);
+    st8(out + t * 8, v);
   }
 }
 
@@ -65,10 +66,10 @@ __global__ void prep_images_kernel(const uint8_t* __restrict__ src, const int* _
 // pixel's 64 B written as four 16-B stores. The generic kernel above decodes 64-bit indices and
 // re-gathers the neighbourhood per 8-channel chunk (ALU-bound: 57 us for the 8-client CIFAR
 // batch, ~1 TB/s of output).
-template <int K, int CS>
+template <int K, int CS, typename T>
 __global__ __launch_bounds__(256) void prep_stem32_kernel(
     const uint8_t* __restrict__ src, const int* __restrict__ idx, const float* __restrict__ mean,
-    const float* __restrict__ inv_std, bf16_t* __restrict__ out, int nimg, int Hs, int Ws, int Ho,
+    const float* __restrict__ inv_std, T* __restrict__ out, int nimg, int Hs, int Ws, int Ho,
     int Wo, int pad, int stride, const int* __restrict__ labels, int* __restrict__ labels_out) {
   static_assert(K * K * CS <= 32, "stem im2col fits 32 channels");
   const int hw = Ho * Wo;
@@ -99,19 +100,19 @@ __global__ __launch_bounds__(256) void prep_stem32_kernel(
       }
     }
   }
-  i4v* o = (i4v*)(out + (long long)pix * 32);
+  T* o = out + (long long)pix * 32;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) o[q] = pack8(v + 8 * q);
+  for (int q = 0; q < 4; ++q) st8(o + 8 * q, v + 8 * q);
 }
 
 // Fast path of a wider stem im2col (ImageNet 7x7x3 / stride 2 -> 147 of 160 channels): one
 // thread per (output pixel, 8-channel chunk) as the generic kernel, but 32-bit index math and
 // compile-time tap decoding (the generic kernel's 64-bit divisions made the 1 GB ResNet-50 batch
 // gather ALU-bound: 1.07 ms per step).
-template <int K, int CS>
+template <int K, int CS, typename T>
 __global__ __launch_bounds__(256) void prep_im2col_kernel(
     const uint8_t* __restrict__ src, const int* __restrict__ idx, const float* __restrict__ mean,
-    const float* __restrict__ inv_std, bf16_t* __restrict__ out, int nimg, int Hs, int Ws, int Ho,
+    const float* __restrict__ inv_std, T* __restrict__ out, int nimg, int Hs, int Ws, int Ho,
     int Wo, int nch, int pad, int stride, const int* __restrict__ labels, int* __restrict__ labels_out) {
   const int hw = Ho * Wo;
   const unsigned total = (unsigned)nimg * hw * nch;
@@ -137,7 +138,7 @@ __global__ __launch_bounds__(256) void prep_im2col_kernel(
       val = ((float)img[(ih * Ws + iw) * CS + c] * (1.f / 255.f) - mean[c]) * inv_std[c];
     v[k] = val;
   }
-  *(i4v*)(out + (long long)t * 8) = pack8(v);
+  st8(out + (long long)t * 8, v);
 }
 
 // ImageNet stem im2col, one block per (image, output row): the K input rows the row's windows
@@ -146,10 +147,10 @@ __global__ __launch_bounds__(256) void prep_im2col_kernel(
 // pixels' im2col rows (the block's output is one contiguous Wo x Cout run). The per-chunk kernel
 // above gathers its 8 bytes from 8 scattered taps of the uint8 image per thread: 667 us for a
 // batch of 256 at 224x224 (1 GB written at 1.5 TB/s).
-template <int K, int CS>
+template <int K, int CS, typename T>
 __global__ __launch_bounds__(256) void prep_im2col_row_kernel(
     const uint8_t* __restrict__ src, const int* __restrict__ idx, const float* __restrict__ mean,
-    const float* __restrict__ inv_std, bf16_t* __restrict__ out, int Hs, int Ws, int Ho, int Wo,
+    const float* __restrict__ inv_std, T* __restrict__ out, int Hs, int Ws, int Ho, int Wo,
     int nch, int pad, int stride, int Wl, const int* __restrict__ labels, int* __restrict__ labels_out) {
   extern __shared__ float rows[];  // [K][Wl][CS], column 0 = input column -pad
   const int b = blockIdx.y, h = blockIdx.x, tid = threadIdx.x;
@@ -171,7 +172,7 @@ __global__ __launch_bounds__(256) void prep_im2col_row_kernel(
     rows[t] = v;
   }
   __syncthreads();
-  bf16_t* o = out + ((long long)b * Ho + h) * Wo * nch * 8;
+  T* o = out + ((long long)b * Ho + h) * Wo * nch * 8;
   for (int q = tid; q < Wo * nch; q += 256) {
     const int px = q / nch, chunk = q - px * nch;
     const int wbase = px * stride;
@@ -183,11 +184,12 @@ __global__ __launch_bounds__(256) void prep_im2col_row_kernel(
       const int tr = tap / K, ts = tap - tr * K;
       v[k] = tap < K * K ? rows[(tr * Wl + wbase + ts) * CS + c] : 0.f;
     }
-    *(i4v*)(o + (long long)q * 8) = pack8(v);
+    st8(o + (long long)q * 8, v);
   }
 }
 
-DDL_API int ddl_prep_images(const void* src, const int* idx, const float* mean, const float* inv_std,
+template <typename T>
+static int prep_images_impl(const void* src, const int* idx, const float* mean, const float* inv_std,
                             void* out, int nimg, int Hs, int Ws, int Cs, int Cout, int im2col,
                             int pad, int stride, const int* labels, int* labels_out, hipStream_t s) {
   if (Cout % 8 || stride < 1) return (int)hipErrorInvalidValue;
@@ -199,35 +201,36 @@ DDL_API int ddl_prep_images(const void* src, const int* idx, const float* mean, 
   if (Cout == 32 && im2col == 3 && (Cs == 3 || Cs == 1) && pixels < (1LL << 31) - 256) {
     const dim3 grid((unsigned)((pixels + 255) / 256));
     if (Cs == 3)
-      hipLaunchKernelGGL((prep_stem32_kernel<3, 3>), grid, dim3(256), 0, s, (const uint8_t*)src, idx,
-                         mean, inv_std, (bf16_t*)out, nimg, Hs, Ws, Ho, Wo, pad, stride, labels, labels_out);
+      hipLaunchKernelGGL((prep_stem32_kernel<3, 3, T>), grid, dim3(256), 0, s, (const uint8_t*)src, idx,
+                         mean, inv_std, (T*)out, nimg, Hs, Ws, Ho, Wo, pad, stride, labels, labels_out);
     else
-      hipLaunchKernelGGL((prep_stem32_kernel<3, 1>), grid, dim3(256), 0, s, (const uint8_t*)src, idx,
-                         mean, inv_std, (bf16_t*)out, nimg, Hs, Ws, Ho, Wo, pad, stride, labels, labels_out);
+      hipLaunchKernelGGL((prep_stem32_kernel<3, 1, T>), grid, dim3(256), 0, s, (const uint8_t*)src, idx,
+                         mean, inv_std, (T*)out, nimg, Hs, Ws, Ho, Wo, pad, stride, labels, labels_out);
     return (int)hipGetLastError();
   }
   const long long total = (long long)nimg * Ho * Wo * (Cout / 8);
   const int Wl = (Wo - 1) * stride + im2col;  // input columns the row's windows span
   if (im2col == 7 && Cs == 3 && 7 * Wl * 3 * 4 <= 64 * 1024 && Ho < 65536) {
-    hipLaunchKernelGGL((prep_im2col_row_kernel<7, 3>), dim3(Ho, nimg), dim3(256), 7 * Wl * 3 * 4, s,
-                       (const uint8_t*)src, idx, mean, inv_std, (bf16_t*)out, Hs, Ws, Ho, Wo, Cout / 8,
+    hipLaunchKernelGGL((prep_im2col_row_kernel<7, 3, T>), dim3(Ho, nimg), dim3(256), 7 * Wl * 3 * 4, s,
+                       (const uint8_t*)src, idx, mean, inv_std, (T*)out, Hs, Ws, Ho, Wo, Cout / 8,
                        pad, stride, Wl, labels, labels_out);
     return (int)hipGetLastError();
   }
   if (im2col == 7 && Cs == 3 && total < (1LL << 31) - 256) {
-    hipLaunchKernelGGL((prep_im2col_kernel<7, 3>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
-                       (const uint8_t*)src, idx, mean, inv_std, (bf16_t*)out, nimg, Hs, Ws, Ho, Wo,
+    hipLaunchKernelGGL((prep_im2col_kernel<7, 3, T>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                       (const uint8_t*)src, idx, mean, inv_std, (T*)out, nimg, Hs, Ws, Ho, Wo,
                        Cout / 8, pad, stride, labels, labels_out);
     return (int)hipGetLastError();
   }
-  hipLaunchKernelGGL(prep_images_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s,
-                     (const uint8_t*)src, idx, mean, inv_std, (bf16_t*)out, nimg, Hs, Ws, Cs, Ho, Wo,
+  hipLaunchKernelGGL(prep_images_kernel<T>, dim3(grid_for(total, 256)), dim3(256), 0, s,
+                     (const uint8_t*)src, idx, mean, inv_std, (T*)out, nimg, Hs, Ws, Cs, Ho, Wo,
                      Cout, im2col, pad, stride, labels, labels_out);
   return (int)hipGetLastError();
 }
 
 // fp32 NCHW (already normalised) -> NHWC bf16, optionally im2col 3x3 (same rules as above)
-__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, bf16_t* __restrict__ out, int N,
+template <typename T>
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, T* __restrict__ out, int N,
                                     int Cs, int Hs, int Ws, int Ho, int Wo, int Cout, int im2col,
                                     int pad, int stride) {
   const long long total = (long long)N * Ho * Wo * (Cout / 8);
@@ -254,25 +257,27 @@ __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, bf16_t* __restr
       }
       v[k] = val;
     }
-    *(i4v*)(out + t * 8) = pack8(v);
+    st8(out + t * 8, v);
   }
 }
 
-DDL_API int ddl_nchw_to_nhwc(const float* x, void* out, int N, int Cs, int Hs, int Ws, int Cout,
+template <typename T>
+static int nchw_to_nhwc_impl(const float* x, void* out, int N, int Cs, int Hs, int Ws, int Cout,
                              int im2col, int pad, int stride, hipStream_t s) {
   if (Cout % 8 || stride < 1) return (int)hipErrorInvalidValue;
   if (im2col && im2col * im2col * Cs > Cout) return (int)hipErrorInvalidValue;
   const int Ho = im2col ? (Hs + 2 * pad - im2col) / stride + 1 : Hs;
   const int Wo = im2col ? (Ws + 2 * pad - im2col) / stride + 1 : Ws;
   const long long total = (long long)N * Ho * Wo * (Cout / 8);
-  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s, x,
-                     (bf16_t*)out, N, Cs, Hs, Ws, Ho, Wo, Cout, im2col, pad, stride);
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel<T>, dim3(grid_for(total, 256)), dim3(256), 0, s, x,
+                     (T*)out, N, Cs, Hs, Ws, Ho, Wo, Cout, im2col, pad, stride);
   return (int)hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
 // 2x2 stride-2 max pool over NHWC (NB = G*N images)
-__global__ void maxpool2_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int NB,
+template <typename T>
+__global__ void maxpool2_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int NB,
                                     int H, int W, int C) {
   const int Ho = H / 2, Wo = W / 2, CC = C / 8;
   const long long total = (long long)NB * Ho * Wo * CC;
@@ -283,24 +288,25 @@ __global__ void maxpool2_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __rest
     p /= Wo;
     const int ho = (int)(p % Ho);
     const int n = (int)(p / Ho);
-    const bf16_t* b = x + (((long long)n * H + 2 * ho) * W + 2 * wo) * C + cc * 8;
+    const T* b = x + (((long long)n * H + 2 * ho) * W + 2 * wo) * C + cc * 8;
     float m[8], v[8];
-    unpack8(*(const i4v*)b, m);
-    unpack8(*(const i4v*)(b + C), v);
+    ld8(b, m);
+    ld8(b + C, v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) m[k] = (v[k] > m[k] || v[k] != v[k]) ? v[k] : m[k];
-    unpack8(*(const i4v*)(b + (long long)W * C), v);
+    ld8(b + (long long)W * C, v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) m[k] = (v[k] > m[k] || v[k] != v[k]) ? v[k] : m[k];
-    unpack8(*(const i4v*)(b + (long long)W * C + C), v);
+    ld8(b + (long long)W * C + C, v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) m[k] = (v[k] > m[k] || v[k] != v[k]) ? v[k] : m[k];
-    *(i4v*)(y + t * 8) = pack8(m);
+    st8(y + t * 8, m);
   }
 }
 
-__global__ void maxpool2_bwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
-                                    bf16_t* __restrict__ dx, int NB, int H, int W, int C) {
+template <typename T>
+__global__ void maxpool2_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                    T* __restrict__ dx, int NB, int H, int W, int C) {
   const int Ho = H / 2, Wo = W / 2, CC = C / 8;
   const long long total = (long long)NB * Ho * Wo * CC;
   GSTRIDE_LOOP(t, total) {
@@ -314,8 +320,8 @@ __global__ void maxpool2_bwd_kernel(const bf16_t* __restrict__ x, const bf16_t* 
     const long long offs[4] = {o00, o00 + C, o00 + (long long)W * C, o00 + (long long)W * C + C};
     float v[4][8], d[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) unpack8(*(const i4v*)(x + offs[j]), v[j]);
-    unpack8(*(const i4v*)(dy + t * 8), d);
+    for (int j = 0; j < 4; ++j) ld8(x + offs[j], v[j]);
+    ld8(dy + t * 8, d);
     float out[4][8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -328,29 +334,32 @@ __global__ void maxpool2_bwd_kernel(const bf16_t* __restrict__ x, const bf16_t* 
       for (int j = 0; j < 4; ++j) out[j][k] = (j == am) ? d[k] : 0.f;
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) *(i4v*)(dx + offs[j]) = pack8(out[j]);
+    for (int j = 0; j < 4; ++j) st8(dx + offs[j], out[j]);
   }
 }
 
-DDL_API int ddl_maxpool2_fwd(const void* x, void* y, int NB, int H, int W, int C, hipStream_t s) {
+template <typename T>
+static int maxpool2_fwd_impl(const void* x, void* y, int NB, int H, int W, int C, hipStream_t s) {
   if (C % 8 || H % 2 || W % 2) return (int)hipErrorInvalidValue;
   const long long total = (long long)NB * (H / 2) * (W / 2) * (C / 8);
-  hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s,
-                     (const bf16_t*)x, (bf16_t*)y, NB, H, W, C);
+  hipLaunchKernelGGL(maxpool2_fwd_kernel<T>, dim3(grid_for(total, 256)), dim3(256), 0, s,
+                     (const T*)x, (T*)y, NB, H, W, C);
   return (int)hipGetLastError();
 }
-DDL_API int ddl_maxpool2_bwd(const void* x, const void* dy, void* dx, int NB, int H, int W, int C,
+template <typename T>
+static int maxpool2_bwd_impl(const void* x, const void* dy, void* dx, int NB, int H, int W, int C,
                              hipStream_t s) {
   if (C % 8 || H % 2 || W % 2) return (int)hipErrorInvalidValue;
   const long long total = (long long)NB * (H / 2) * (W / 2) * (C / 8);
-  hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s,
-                     (const bf16_t*)x, (const bf16_t*)dy, (bf16_t*)dx, NB, H, W, C);
+  hipLaunchKernelGGL(maxpool2_bwd_kernel<T>, dim3(grid_for(total, 256)), dim3(256), 0, s,
+                     (const T*)x, (const T*)dy, (T*)dx, NB, H, W, C);
   return (int)hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
 // global average pool: x [NB][HW][C] -> y [NB][C]; one thread per (image, 8-channel chunk)
-__global__ void avgpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int NB,
+template <typename T>
+__global__ void avgpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int NB,
                                    int HW, int C) {
   const int CC = C / 8;
   const long long total = (long long)NB * CC;
@@ -360,17 +369,18 @@ __global__ void avgpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restr
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int p = 0; p < HW; ++p) {
       float v[8];
-      unpack8(*(const i4v*)(x + (n * HW + p) * C + cc * 8), v);
+      ld8(x + (n * HW + p) * C + cc * 8, v);
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc[k] += v[k];
     }
     const float inv = 1.f / HW;
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] *= inv;
-    *(i4v*)(y + n * C + cc * 8) = pack8(acc);
+    st8(y + n * C + cc * 8, acc);
   }
 }
-__global__ void avgpool_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int NB,
+template <typename T>
+__global__ void avgpool_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int NB,
                                    int HW, int C) {
   const int CC = C / 8;
   const long long total = (long long)NB * HW * CC;
@@ -379,10 +389,10 @@ __global__ void avgpool_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __rest
     const int cc = (int)(t % CC);
     const long long n = t / CC / HW;
     float v[8];
-    unpack8(*(const i4v*)(dy + n * C + cc * 8), v);
+    ld8(dy + n * C + cc * 8, v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] *= inv;
-    *(i4v*)(dx + t * 8) = pack8(v);
+    st8(dx + t * 8, v);
   }
 }
 // Global-average-pool backward fused with the backward reduce of the BatchNorm that produced the
@@ -438,7 +448,7 @@ __global__ __launch_bounds__(256) void avgpool_bwd_bn_kernel(
           s0[k] += d[k];
           s1[k] += d[k] * (cv[k] - m8[k]) * r8[k];
         }
-        *(i4v*)(dx + e) = pack8(d);
+        st8(dx + e, d);
       }
     }
   }
@@ -487,16 +497,18 @@ DDL_API int ddl_avgpool_bwd_bn(const void* dy, const void* x, const void* c, con
   return (int)hipGetLastError();
 }
 
-DDL_API int ddl_avgpool_fwd(const void* x, void* y, int NB, int HW, int C, hipStream_t s) {
+template <typename T>
+static int avgpool_fwd_impl(const void* x, void* y, int NB, int HW, int C, hipStream_t s) {
   if (C % 8) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(grid_for((long long)NB * C / 8, 256)), dim3(256), 0,
-                     s, (const bf16_t*)x, (bf16_t*)y, NB, HW, C);
+  hipLaunchKernelGGL(avgpool_fwd_kernel<T>, dim3(grid_for((long long)NB * C / 8, 256)), dim3(256), 0,
+                     s, (const T*)x, (T*)y, NB, HW, C);
   return (int)hipGetLastError();
 }
-DDL_API int ddl_avgpool_bwd(const void* dy, void* dx, int NB, int HW, int C, hipStream_t s) {
+template <typename T>
+static int avgpool_bwd_impl(const void* dy, void* dx, int NB, int HW, int C, hipStream_t s) {
   if (C % 8) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for((long long)NB * HW * C / 8, 256)), dim3(256),
-                     0, s, (const bf16_t*)dy, (bf16_t*)dx, NB, HW, C);
+  hipLaunchKernelGGL(avgpool_bwd_kernel<T>, dim3(grid_for((long long)NB * HW * C / 8, 256)), dim3(256),
+                     0, s, (const T*)dy, (T*)dx, NB, HW, C);
   return (int)hipGetLastError();
 }
 
@@ -505,7 +517,8 @@ DDL_API int ddl_avgpool_bwd(const void* dy, void* dx, int NB, int HW, int C, hip
 // The Philox counter base = offset + *offset_dev (if given): a device-resident per-layer counter
 // advanced by ddl_u64_add after each backward, so a captured HIP graph draws a fresh mask on
 // every replay while forward and backward of one step share it.
-__global__ void dropout_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n,
+template <typename T>
+__global__ void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, long long n,
                                float p, unsigned long long seed, unsigned long long offset,
                                const unsigned long long* __restrict__ offset_dev) {
   if (offset_dev) offset += *offset_dev;
@@ -513,7 +526,7 @@ __global__ void dropout_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict_
   const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
   GSTRIDE_LOOP(t, n / 8) {
     float v[8];
-    unpack8(*(const i4v*)(x + t * 8), v);
+    ld8(x + t * 8, v);
     const unsigned long long ctr0 = offset + (unsigned long long)t * 2;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -523,15 +536,16 @@ __global__ void dropout_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict_
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[h * 4 + k] = (u32_to_unit(rr[k]) > p) ? v[h * 4 + k] * scale : 0.f;
     }
-    *(i4v*)(y + t * 8) = pack8(v);
+    st8(y + t * 8, v);
   }
 }
-DDL_API int ddl_dropout(const void* x, void* y, long long n, float p, unsigned long long seed,
+template <typename T>
+static int dropout_impl(const void* x, void* y, long long n, float p, unsigned long long seed,
                         unsigned long long offset, const unsigned long long* offset_dev,
                         hipStream_t s) {
   if (n % 8) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n / 8, 256)), dim3(256), 0, s, (const bf16_t*)x,
-                     (bf16_t*)y, n, p, seed, offset, offset_dev);
+  hipLaunchKernelGGL(dropout_kernel<T>, dim3(grid_for(n / 8, 256)), dim3(256), 0, s, (const T*)x,
+                     (T*)y, n, p, seed, offset, offset_dev);
   return (int)hipGetLastError();
 }
 
@@ -544,52 +558,57 @@ DDL_API int ddl_u64_add(unsigned long long* p, unsigned long long inc, hipStream
 // ---------------------------------------------------------------------------------------------
 // act fwd: 1 relu, 2 leaky(slope), 3 tanh, 4 sigmoid; act bwd: dx = dy * act'(y) computed from the
 // forward OUTPUT y (relu/leaky: sign preserved; tanh: 1-y^2; sigmoid: y(1-y))
-__global__ void act_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n,
+template <typename T>
+__global__ void act_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, long long n,
                                int act, float slope) {
   GSTRIDE_LOOP(t, n / 8) {
     float v[8];
-    unpack8(*(const i4v*)(x + t * 8), v);
+    ld8(x + t * 8, v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       if (act == 3) v[k] = tanhf(v[k]);
       else if (act == 4) v[k] = 1.f / (1.f + __expf(-v[k]));
       else v[k] = v[k] > 0.f ? v[k] : (act == 2 ? slope * v[k] : 0.f);
     }
-    *(i4v*)(y + t * 8) = pack8(v);
+    st8(y + t * 8, v);
   }
 }
-__global__ void act_bwd_kernel(const bf16_t* __restrict__ y, const bf16_t* __restrict__ dy,
-                               bf16_t* __restrict__ dx, long long n, int act, float slope) {
+template <typename T>
+__global__ void act_bwd_kernel(const T* __restrict__ y, const T* __restrict__ dy,
+                               T* __restrict__ dx, long long n, int act, float slope) {
   GSTRIDE_LOOP(t, n / 8) {
     float v[8], d[8];
-    unpack8(*(const i4v*)(y + t * 8), v);
-    unpack8(*(const i4v*)(dy + t * 8), d);
+    ld8(y + t * 8, v);
+    ld8(dy + t * 8, d);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       if (act == 3) d[k] *= 1.f - v[k] * v[k];
       else if (act == 4) d[k] *= v[k] * (1.f - v[k]);
       else d[k] = v[k] > 0.f ? d[k] : (act == 2 ? slope * d[k] : 0.f);
     }
-    *(i4v*)(dx + t * 8) = pack8(d);
+    st8(dx + t * 8, d);
   }
 }
-DDL_API int ddl_act_fwd(const void* x, void* y, long long n, int act, float slope, hipStream_t s) {
+template <typename T>
+static int act_fwd_impl(const void* x, void* y, long long n, int act, float slope, hipStream_t s) {
   if (n % 8) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(act_fwd_kernel, dim3(grid_for(n / 8, 256)), dim3(256), 0, s, (const bf16_t*)x,
-                     (bf16_t*)y, n, act, slope);
+  hipLaunchKernelGGL(act_fwd_kernel<T>, dim3(grid_for(n / 8, 256)), dim3(256), 0, s, (const T*)x,
+                     (T*)y, n, act, slope);
   return (int)hipGetLastError();
 }
-DDL_API int ddl_act_bwd(const void* y, const void* dy, void* dx, long long n, int act, float slope,
+template <typename T>
+static int act_bwd_impl(const void* y, const void* dy, void* dx, long long n, int act, float slope,
                         hipStream_t s) {
   if (n % 8) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(act_bwd_kernel, dim3(grid_for(n / 8, 256)), dim3(256), 0, s, (const bf16_t*)y,
-                     (const bf16_t*)dy, (bf16_t*)dx, n, act, slope);
+  hipLaunchKernelGGL(act_bwd_kernel<T>, dim3(grid_for(n / 8, 256)), dim3(256), 0, s, (const T*)y,
+                     (const T*)dy, (T*)dx, n, act, slope);
   return (int)hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
 // per-channel sum of x [G][M][C] bf16 -> out [G] (+g*gs) fp32 accumulate
-__global__ __launch_bounds__(256) void channel_sum_kernel(const bf16_t* __restrict__ x,
+template <typename T>
+__global__ __launch_bounds__(256) void channel_sum_kernel(const T* __restrict__ x,
                                                           float* __restrict__ out, long long gs,
                                                           long long M, int C) {
   __shared__ float red[256 * 9];
@@ -600,7 +619,7 @@ __global__ __launch_bounds__(256) void channel_sum_kernel(const bf16_t* __restri
   if (row < RPI) {
     for (long long p = (long long)blockIdx.x * RPI + row; p < M; p += (long long)gridDim.x * RPI) {
       float v[8];
-      unpack8(*(const i4v*)(x + ((long long)g * M + p) * C + cc * 8), v);
+      ld8(x + ((long long)g * M + p) * C + cc * 8, v);
 #pragma unroll
       for (int k = 0; k < 8; ++k) s[k] += v[k];
     }
@@ -617,15 +636,16 @@ __global__ __launch_bounds__(256) void channel_sum_kernel(const bf16_t* __restri
     for (int k = 0; k < 8; ++k) atomicAdd(out + (long long)g * gs + tid * 8 + k, t8[k]);
   }
 }
-DDL_API int ddl_channel_sum(const void* x, float* out, long long gs, long long M, int C, int G,
+template <typename T>
+static int channel_sum_impl(const void* x, float* out, long long gs, long long M, int C, int G,
                             hipStream_t s) {
   if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
   const int RPI = 256 / (C / 8);
   long long blocks = (M + (long long)RPI * 16 - 1) / ((long long)RPI * 16);
   if (blocks > 512) blocks = 512;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(channel_sum_kernel, dim3((unsigned)blocks, G), dim3(256), 0, s,
-                     (const bf16_t*)x, out, gs, M, C);
+  hipLaunchKernelGGL(channel_sum_kernel<T>, dim3((unsigned)blocks, G), dim3(256), 0, s,
+                     (const T*)x, out, gs, M, C);
   return (int)hipGetLastError();
 }
 
@@ -662,8 +682,8 @@ DDL_API int ddl_cast_bf16_f32(const void* x, float* y, long long n, hipStream_t 
 // general k x k / stride / pad max pool (ImageNet stem 3x3/2 p1); -inf padding like torch
 // am (optional): window-local argmax r*k+s per output element (uint8), consumed by the backward
 // I: index type (int when every element offset fits in 31 bits: no 64-bit division per item)
-template <typename I>
-__global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+template <typename I, typename T>
+__global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                    unsigned char* __restrict__ am, int NB,
                                    int H, int W, int C, int k, int st, int pd, int Ho, int Wo) {
   const int CC = C / 8;
@@ -686,13 +706,13 @@ __global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restr
         const int iw = wo * st - pd + s2;
         if ((unsigned)iw >= (unsigned)W) continue;
         float v[8];
-        unpack8(*(const i4v*)(x + (((I)n * H + ih) * W + iw) * C + cc * 8), v);
+        ld8(x + (((I)n * H + ih) * W + iw) * C + cc * 8, v);
 #pragma unroll
         for (int e = 0; e < 8; ++e)
           if (v[e] > m[e] || (v[e] != v[e] && m[e] == m[e])) { m[e] = v[e]; ai[e] = r * k + s2; }
       }
     }
-    *(i4v*)(y + t * 8) = pack8(m);
+    st8(y + t * 8, m);
     if (am) {
       unsigned long long packed = 0;
 #pragma unroll
@@ -704,9 +724,9 @@ __global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restr
 
 // backward from the saved argmax: each input pixel gathers dy of the (<= ceil(k/st)^2) windows
 // that contain it and chose it — one byte + one bf16 per window and channel, no recomputation
-template <typename I>
+template <typename I, typename T>
 __global__ void maxpool_bwd_am_kernel(const unsigned char* __restrict__ am,
-                                      const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx,
+                                      const T* __restrict__ dy, T* __restrict__ dx,
                                       int NB, int H, int W, int C, int k, int st, int pd, int Ho,
                                       int Wo) {
   const int CC = C / 8;
@@ -727,18 +747,19 @@ __global__ void maxpool_bwd_am_kernel(const unsigned char* __restrict__ am,
         const I o = (((I)n * Ho + ho) * Wo + wo) * C + cc * 8;
         const unsigned long long a8 = *(const unsigned long long*)(am + o);
         float d[8];
-        unpack8(*(const i4v*)(dy + o), d);
+        ld8(dy + o, d);
 #pragma unroll
         for (int e = 0; e < 8; ++e)
           if ((int)((a8 >> (8 * e)) & 0xff) == local) acc[e] += d[e];
       }
-    *(i4v*)(dx + t * 8) = pack8(acc);
+    st8(dx + t * 8, acc);
   }
 }
 // backward as a gather over the windows that contain each input pixel (no atomics): an input
 // element receives dy of every window whose (first) argmax it is.
-__global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
-                                   bf16_t* __restrict__ dx, int NB, int H, int W, int C, int k,
+template <typename T>
+__global__ void maxpool_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                   T* __restrict__ dx, int NB, int H, int W, int C, int k,
                                    int st, int pd, int Ho, int Wo) {
   const int CC = C / 8;
   const long long total = (long long)NB * H * W * CC;
@@ -765,52 +786,86 @@ __global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ x, const bf16_t* _
             const int iw = wo * st - pd + s2;
             if ((unsigned)iw >= (unsigned)W) continue;
             float v[8];
-            unpack8(*(const i4v*)(x + (((long long)n * H + ih) * W + iw) * C + cc * 8), v);
+            ld8(x + (((long long)n * H + ih) * W + iw) * C + cc * 8, v);
 #pragma unroll
             for (int e = 0; e < 8; ++e)
               if (v[e] > m[e] || (v[e] != v[e] && m[e] == m[e])) { m[e] = v[e]; am[e] = ih * W + iw; }
           }
         }
         float d[8];
-        unpack8(*(const i4v*)(dy + (((long long)n * Ho + ho) * Wo + wo) * C + cc * 8), d);
+        ld8(dy + (((long long)n * Ho + ho) * Wo + wo) * C + cc * 8, d);
 #pragma unroll
         for (int e = 0; e < 8; ++e)
           if (am[e] == ih0 * W + iw0) acc[e] += d[e];
       }
-    *(i4v*)(dx + t * 8) = pack8(acc);
+    st8(dx + t * 8, acc);
   }
 }
-DDL_API int ddl_maxpool_fwd(const void* x, void* y, void* am, int NB, int H, int W, int C, int k,
+template <typename T>
+static int maxpool_fwd_impl(const void* x, void* y, void* am, int NB, int H, int W, int C, int k,
                             int st, int pd, hipStream_t s) {
   if (C % 8) return (int)hipErrorInvalidValue;
   const int Ho = (H + 2 * pd - k) / st + 1, Wo = (W + 2 * pd - k) / st + 1;
   const long long total = (long long)NB * Ho * Wo * (C / 8);
   if (k > 15) return (int)hipErrorInvalidValue;  // argmax index must fit a byte
   if ((long long)NB * H * W * C < (1LL << 31) - 64)  // 32-bit offsets, one item per thread
-    hipLaunchKernelGGL(maxpool_fwd_kernel<int>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
-                       (const bf16_t*)x, (bf16_t*)y, (unsigned char*)am, NB, H, W, C, k, st, pd, Ho, Wo);
+    hipLaunchKernelGGL((maxpool_fwd_kernel<int, T>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                       (const T*)x, (T*)y, (unsigned char*)am, NB, H, W, C, k, st, pd, Ho, Wo);
   else
-    hipLaunchKernelGGL(maxpool_fwd_kernel<long long>, dim3(grid_for(total, 256)), dim3(256), 0, s,
-                       (const bf16_t*)x, (bf16_t*)y, (unsigned char*)am, NB, H, W, C, k, st, pd, Ho, Wo);
+    hipLaunchKernelGGL((maxpool_fwd_kernel<long long, T>), dim3(grid_for(total, 256)), dim3(256), 0, s,
+                       (const T*)x, (T*)y, (unsigned char*)am, NB, H, W, C, k, st, pd, Ho, Wo);
   return (int)hipGetLastError();
 }
-DDL_API int ddl_maxpool_bwd(const void* x, const void* dy, const void* am, void* dx, int NB, int H,
+template <typename T>
+static int maxpool_bwd_impl(const void* x, const void* dy, const void* am, void* dx, int NB, int H,
                             int W, int C, int k, int st, int pd, hipStream_t s) {
   if (C % 8) return (int)hipErrorInvalidValue;
   const int Ho = (H + 2 * pd - k) / st + 1, Wo = (W + 2 * pd - k) / st + 1;
   const long long total = (long long)NB * H * W * (C / 8);
   if (am) {
     if ((long long)NB * H * W * C < (1LL << 31) - 64)
-      hipLaunchKernelGGL(maxpool_bwd_am_kernel<int>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
-                         (const unsigned char*)am, (const bf16_t*)dy, (bf16_t*)dx, NB, H, W, C, k, st,
+      hipLaunchKernelGGL((maxpool_bwd_am_kernel<int, T>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                         (const unsigned char*)am, (const T*)dy, (T*)dx, NB, H, W, C, k, st,
                          pd, Ho, Wo);
     else
-      hipLaunchKernelGGL(maxpool_bwd_am_kernel<long long>, dim3(grid_for(total, 256)), dim3(256), 0, s,
-                         (const unsigned char*)am, (const bf16_t*)dy, (bf16_t*)dx, NB, H, W, C, k, st,
+      hipLaunchKernelGGL((maxpool_bwd_am_kernel<long long, T>), dim3(grid_for(total, 256)), dim3(256), 0, s,
+                         (const unsigned char*)am, (const T*)dy, (T*)dx, NB, H, W, C, k, st,
                          pd, Ho, Wo);
     return (int)hipGetLastError();
   }
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total, 256)), dim3(256), 0, s,
-                     (const bf16_t*)x, (const bf16_t*)dy, (bf16_t*)dx, NB, H, W, C, k, st, pd, Ho, Wo);
+  hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(grid_for(total, 256)), dim3(256), 0, s,
+                     (const T*)x, (const T*)dy, (T*)dx, NB, H, W, C, k, st, pd, Ho, Wo);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// exports: bf16 activations (ddl_x) and fp32 activations (ddl_x_f32, the reference-precision mode)
+#define NN_EXPORT(name, params, args)                                      \
+  DDL_API int ddl_##name params { return name##_impl<bf16_t> args; }       \
+  DDL_API int ddl_##name##_f32 params { return name##_impl<float> args; }
+NN_EXPORT(prep_images, (const void* src, const int* idx, const float* mean, const float* inv_std, void* out,
+                        int nimg, int Hs, int Ws, int Cs, int Cout, int im2col, int pad, int stride,
+                        const int* labels, int* labels_out, hipStream_t s),
+          (src, idx, mean, inv_std, out, nimg, Hs, Ws, Cs, Cout, im2col, pad, stride, labels, labels_out, s))
+NN_EXPORT(nchw_to_nhwc, (const float* x, void* out, int N, int Cs, int Hs, int Ws, int Cout, int im2col, int pad,
+                         int stride, hipStream_t s),
+          (x, out, N, Cs, Hs, Ws, Cout, im2col, pad, stride, s))
+NN_EXPORT(maxpool2_fwd, (const void* x, void* y, int NB, int H, int W, int C, hipStream_t s), (x, y, NB, H, W, C, s))
+NN_EXPORT(maxpool2_bwd, (const void* x, const void* dy, void* dx, int NB, int H, int W, int C, hipStream_t s),
+          (x, dy, dx, NB, H, W, C, s))
+NN_EXPORT(avgpool_fwd, (const void* x, void* y, int NB, int HW, int C, hipStream_t s), (x, y, NB, HW, C, s))
+NN_EXPORT(avgpool_bwd, (const void* dy, void* dx, int NB, int HW, int C, hipStream_t s), (dy, dx, NB, HW, C, s))
+NN_EXPORT(dropout, (const void* x, void* y, long long n, float p, unsigned long long seed, unsigned long long offset,
+                    const unsigned long long* offset_dev, hipStream_t s),
+          (x, y, n, p, seed, offset, offset_dev, s))
+NN_EXPORT(act_fwd, (const void* x, void* y, long long n, int act, float slope, hipStream_t s), (x, y, n, act, slope, s))
+NN_EXPORT(act_bwd, (const void* y, const void* dy, void* dx, long long n, int act, float slope, hipStream_t s),
+          (y, dy, dx, n, act, slope, s))
+NN_EXPORT(channel_sum, (const void* x, float* out, long long gs, long long M, int C, int G, hipStream_t s),
+          (x, out, gs, M, C, G, s))
+NN_EXPORT(maxpool_fwd, (const void* x, void* y, void* am, int NB, int H, int W, int C, int k, int st, int pd,
+                        hipStream_t s),
+          (x, y, am, NB, H, W, C, k, st, pd, s))
+NN_EXPORT(maxpool_bwd, (const void* x, const void* dy, const void* am, void* dx, int NB, int H, int W, int C, int k,
+                        int st, int pd, hipStream_t s),
+          (x, dy, am, dx, NB, H, W, C, k, st, pd, s))

@@ -125,14 +125,17 @@ __global__ __launch_bounds__(256) void sgd_direct_kernel(SGDDirectArgs a) {
        t += (long long)gridDim.x * blockDim.x) {
     const long long e = t * 4;
     const long long col = e % a.P;
+    const bool direct = a.dmap[col >> 4] != 0;
+    if (direct && !a.shadow) continue;  // fp32 mode: the WGRAD already stepped them, no shadow
     float4 pv = *(const float4*)(a.p + e);
-    if (!a.dmap[col >> 4]) {
+    if (!direct) {
       const float4 gv = *(const float4*)(a.g + e);
       const float s = a.lr * a.grad_scale;
       pv.x -= s * gv.x; pv.y -= s * gv.y; pv.z -= s * gv.z; pv.w -= s * gv.w;
       *(float4*)(a.p + e) = pv;
       *(float4*)(a.g + e) = make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    if (!a.shadow) continue;
     i2v o;
     o[0] = (int)pack_bf2(pv.x, pv.y);
     o[1] = (int)pack_bf2(pv.z, pv.w);

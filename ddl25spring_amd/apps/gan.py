@@ -20,6 +20,7 @@ class GANConfig:
     ndf: int = 64
     train_size: int = 50000
     seed: int = 0
+    save: str = ""  # rank 0 writes the final flat global (G | D | BN) weights here (torch.save)
 
 
 def client_images(cfg: GANConfig, device):
@@ -42,4 +43,6 @@ def run_gan(cfg: GANConfig, ctx, log=print):
     if log and ctx.rank == 0:
         for r, (ld, lg, t) in enumerate(zip(res.loss_d, res.loss_g, res.wall_time)):
             log(f"round {r + 1}: loss_D {ld:.3f} loss_G {lg:.3f} ({t:.2f}s)")
+    if cfg.save and ctx.rank == 0:
+        torch.save(fg._flat().detach().cpu(), cfg.save)
     return res

@@ -120,6 +120,7 @@ class DeviceImageDataset:
 
     def set_input_spec(self, spec: dict):
         self.spec = dict(spec)
+        self.dtype = torch.float32 if spec.get("dtype") == "fp32" else torch.bfloat16
         self.cpad = spec.get("cpad", 32)
         self.k = spec.get("stem_k", 0) if spec.get("im2col") else 0
         self.pad = spec.get("pad", 0)
@@ -130,21 +131,21 @@ class DeviceImageDataset:
         return self.labels.numel()
 
     def batch(self, idx: torch.Tensor, out: torch.Tensor | None = None):
-        """idx int32 [G, B] (device) -> (x [G, B, H', W', cpad] | [G, B, F] bf16, y int32 [G, B]).
-        One launch gathers images and labels."""
+        """idx int32 [G, B] (device) -> (x [G, B, H', W', cpad] | [G, B, F] in the spec's activation
+        dtype (bf16 / fp32), y int32 [G, B]). One launch gathers images and labels."""
         G, B = idx.shape
         y = torch.empty(G, B, dtype=torch.int32, device=self.device)
         kw = dict(labels=self.labels, labels_out=y)
         if self.flat:
-            x = Fn.prep_images(self.images, idx, self.mean, self.inv_std, 8, 0, 0, 1, **kw)
+            x = Fn.prep_images(self.images, idx, self.mean, self.inv_std, 8, 0, 0, 1, dtype=self.dtype, **kw)
             # [n, H, W, 8] -> keep the real channel(s), flatten, pad to cpad
             C = self.images.shape[-1]
             flat = x[..., :C].reshape(G, B, -1)
-            xo = torch.zeros(G, B, self.cpad, dtype=torch.bfloat16, device=self.device)
+            xo = torch.zeros(G, B, self.cpad, dtype=self.dtype, device=self.device)
             xo[..., :flat.shape[-1]] = flat
         else:
             x = Fn.prep_images(self.images, idx, self.mean, self.inv_std, self.cpad,
-                               self.k, self.pad, self.stride, out=out, **kw)
+                               self.k, self.pad, self.stride, out=out, dtype=self.dtype, **kw)
             xo = x.reshape(G, B, *x.shape[1:])
         return xo, y
 

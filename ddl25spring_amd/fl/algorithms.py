@@ -165,7 +165,7 @@ class FederatedBase:
     def _download(self, G):
         st = self.net.store
         if G:
-            Fn.broadcast_rows(self.w_global, st.data[:G], st.shadow[:G])
+            Fn.broadcast_rows(self.w_global, st.data[:G], None if st.shadow16 is None else st.shadow16[:G])
             Fn.broadcast_rows(self.b_global, st.buffers[:G])
             st._shadow_version = st.data._version
 
@@ -283,6 +283,7 @@ class FedAvg(FederatedBase):
         if not self.sync_rounds:
             return 0.0, samples
         _sync(self.dev)
+        self.ctx.check_comm()  # a peer-read all-reduce barrier timeout raises here, not silently
         dt = self.ctx.max_scalar(time.perf_counter() - t0)
         samples = int(self.ctx.sum_scalar(samples))
         return dt, samples

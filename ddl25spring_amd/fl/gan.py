@@ -3,9 +3,12 @@
 BASELINE config "federated DCGAN on 2xMI355X": each client trains a local (G, D) pair on its
 private image shard for ``local_steps`` Adam steps, then the server takes the n_k-weighted average
 of both networks (and of the BN running statistics), exactly as FedAvgServer does for classifiers
-(reference hfl_complete.py:336-390 is the aggregation template). One rank per GPU; clients are
-assigned round-robin to ranks; the weighted sums of all ranks meet in ONE all-reduce per round
-over a flat fp32 buffer (G params | D params | BN buffers).
+(reference hfl_complete.py:336-390 is the aggregation template). One rank per GPU; client c
+lives on rank c % world for the whole run (its Adam state stays there, like a real device); the
+weighted sums of all ranks meet in ONE all-reduce per round over a flat fp32 buffer
+(G params | D params | BN buffers). Batch indices AND generator noise of a client's round are
+drawn from that client's own seeded generator, so the result does not depend on how many ranks
+share the clients: W ranks reproduce the single-process run.
 
 Each client keeps its own Adam moments and step count across rounds (swapped in and out of the
 fused FlatAdam buffers), as a real client device would. On the GPU a client's ``local_steps``
@@ -48,7 +51,7 @@ class FederatedGAN:
                  use_graph: bool = True):
         self.ctx = ctx
         self.rank = ctx.rank if ctx else 0
-        self.world = ctx.world_size if ctx else 1
+        self.world = ctx.world if ctx else 1
         self.device = torch.device(device) if device is not None else client_data[0].device
         torch.manual_seed(seed)
         self.G = Generator(nz, ngf).to(self.device)
@@ -66,6 +69,7 @@ class FederatedGAN:
         self._state = {}  # client -> (mG, vG, tG, mD, vD, tD, tG_dev, tD_dev)
         self.use_graph = use_graph and self.device.type == "cuda"
         self._idx: dict = {}    # client -> static [local_steps, batch] device index buffer
+        self._z: dict = {}      # client -> static [local_steps, batch, nz] generator noise buffer
         self._graphs: dict = {}  # client -> CapturedStep over its local steps
 
     # ---------------------------------------------------------------------------------------
@@ -91,7 +95,11 @@ class FederatedGAN:
     def _swap_in(self, c):
         st = self._state.get(c)
         for opt, i in ((self.optG, 0), (self.optD, 3)):
-            if not hasattr(opt, "m"):
+            if not hasattr(opt, "m"):  # torch.optim.Adam (CPU): per-client state dicts
+                if st is None:
+                    opt.state.clear()
+                else:
+                    opt.load_state_dict(st[i])
                 continue
             if st is None:
                 opt.m.zero_(); opt.v.zero_(); opt.t = 0
@@ -103,16 +111,20 @@ class FederatedGAN:
                     opt.t_dev.copy_(st[6 + i // 3])
 
     def _swap_out(self, c):
-        if hasattr(self.optG, "m"):
+        if not hasattr(self.optG, "m"):
+            import copy
+            self._state[c] = (copy.deepcopy(self.optG.state_dict()), None, None,
+                              copy.deepcopy(self.optD.state_dict()), None, None)
+        else:
             tdev = [None if o.t_dev is None else o.t_dev.clone() for o in (self.optG, self.optD)]
             self._state[c] = (self.optG.m.clone(), self.optG.v.clone(), self.optG.t,
                               self.optD.m.clone(), self.optD.v.clone(), self.optD.t, *tdev)
 
     def _local_steps(self, c):
-        data, idx = self.data[c], self._idx[c]
+        data, idx, z = self.data[c], self._idx[c], self._z[c]
         ld = lg = None
         for i in range(self.local_steps):
-            ld, lg = self.trainer.step(data.index_select(0, idx[i]))
+            ld, lg = self.trainer.step(data.index_select(0, idx[i]), z=z[i])
         return ld, lg
 
     # ---------------------------------------------------------------------------------------
@@ -121,7 +133,7 @@ class FederatedGAN:
         for r in range(rounds):
             t0 = time.perf_counter()
             chosen = self.rng.choice(len(self.data), self.K, replace=False)
-            mine = chosen[self.rank::self.world]
+            mine = [c for c in chosen if c % self.world == self.rank]
             glob = self._flat()
             acc = torch.zeros_like(glob)
             wsum = self.n[chosen].sum()
@@ -133,9 +145,12 @@ class FederatedGAN:
                 data = self.data[int(c)]
                 idx = torch.stack([torch.randint(0, len(data), (self.batch_size,), generator=g)
                                    for _ in range(self.local_steps)])
+                z = torch.randn(self.local_steps, self.batch_size, self.G.nz, generator=g)
                 if int(c) not in self._idx:
                     self._idx[int(c)] = torch.empty_like(idx, device=data.device)
+                    self._z[int(c)] = torch.empty_like(z, device=data.device)
                 self._idx[int(c)].copy_(idx)
+                self._z[int(c)].copy_(z)
                 if self.use_graph:
                     if int(c) not in self._graphs:
                         self._graphs[int(c)] = CapturedStep(lambda c=int(c): self._local_steps(c), warmup=1)

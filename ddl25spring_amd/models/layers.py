@@ -146,7 +146,7 @@ class ConvUnit(Layer):
         g = self.geom(x4)
         w = st.shadow_of(self.w)
         if self.bn:
-            stats = Fn.stats_buffer(g.G, self.cout, x.device) if train else None
+            stats = Fn.stats_buffer(g.G, self.cout, x.device, like=x) if train else None
             c = Fn.conv_fwd(x4, w, g, stats=stats)
             count = g.N * g.P * g.Q
             sc, sh, mu, rs = Fn.bn_finalize(stats if train else Fn.stats_buffer(g.G, self.cout, x.device),

@@ -9,23 +9,29 @@
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
 
 from ..ops import functional as Fn
+from ..ops import reference as ref
 from ..ops.workspace import Workspace
 from .layers import RELU, ConvUnit, Dropout, Layer
-from .params import ParamStore
+from .params import PRECISIONS, ParamStore, default_precision
 
 
 class Net:
     def __init__(self, layers: list[Layer], groups: int = 1, num_classes: int | None = None,
-                 input_spec: dict | None = None, name: str = "net"):
+                 input_spec: dict | None = None, name: str = "net", precision: str | None = None):
         self.layers = layers
         self.G = groups
         self.num_classes = num_classes
-        self.input_spec = input_spec or {}
+        self.precision = precision or default_precision()
+        if self.precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {PRECISIONS}, got {self.precision!r}")
+        # the activation dtype travels with the input spec, so data loaders emit it
+        self.input_spec = dict(input_spec or {}, dtype=self.precision)
         self.name = name
         self.store = ParamStore(groups)
         # direct-SGD eligibility of Linear weights: all but a classifier head after a global
@@ -67,9 +73,19 @@ class Net:
             self.layers[0].needs_input_grad = False
 
     # ------------------------------------------------------------------ setup
+    @property
+    def act_dtype(self):
+        return torch.float32 if self.precision == "fp32" else torch.bfloat16
+
+    def _cpu_storage(self):
+        """CPU reference ops store activations in the net's precision."""
+        if self.device.type == "cpu" and self.precision == "fp32":
+            return ref.storage(torch.float32)
+        return contextlib.nullcontext()
+
     def to(self, device, seed: int = 0, generator=None):
         self.device = torch.device(device)
-        self.store.materialize(self.device, seed=seed, generator=generator)
+        self.store.materialize(self.device, seed=seed, generator=generator, fp32=self.precision == "fp32")
         for i, layer in enumerate(self.layers):
             layer.bind(self.store)
             if isinstance(layer, Dropout):  # deterministic per (net seed, position)
@@ -93,9 +109,10 @@ class Net:
         train = self.training if train is None else train
         self.store.ensure_shadow()
         ctxs = []
-        for layer in self.layers:
-            x, c = layer.forward(x, train)
-            ctxs.append(c)
+        with self._cpu_storage():
+            for layer in self.layers:
+                x, c = layer.forward(x, train)
+                ctxs.append(c)
         return x, ctxs
 
     grad_hook = None  # callable(layer_index) after each layer's weight grads are complete
@@ -108,7 +125,7 @@ class Net:
         took the last ones); ``part``: BN backward sums the caller's fused op left for the last of
         those layers."""
         n = len(ctxs)
-        with Fn.wgrad_overlap(self.device, self.overlap_wgrad) as ov:
+        with Fn.wgrad_overlap(self.device, self.overlap_wgrad) as ov, self._cpu_storage():
             for j, (layer, c) in enumerate(zip(reversed(self.layers[:n]), reversed(ctxs))):
                 i = n - 1 - j
                 kw = {"part": part} if part is not None else {}
@@ -135,18 +152,23 @@ class Net:
         if not hasattr(self, "_ws"):
             self._ws = Workspace()
         self._ws.begin(self.device)
+        self.store.ensure_shadow()  # the fused-head path runs layer.forward itself
         try:
-            head = self._fused_head(x, targets, ncls)
-            if head is not None:
-                return self._train_step_fused_head(x, labels, head, scale, with_correct)
-            logits, ctxs = self.forward_native(x, True)
-            N = logits.shape[1]
-            loss, dlogits, correct = Fn.cross_entropy(
-                logits, labels, targets, ncls=ncls or self.num_classes,
-                scale=(1.0 / N) if scale is None else scale, with_correct=with_correct)
-            self.backward_native(dlogits, ctxs)
+            with self._cpu_storage():
+                return self._train_step(x, labels, ncls, scale, targets, with_correct)
         finally:
             self._ws.end()
+
+    def _train_step(self, x, labels, ncls, scale, targets, with_correct):
+        head = self._fused_head(x, targets, ncls)
+        if head is not None:
+            return self._train_step_fused_head(x, labels, head, scale, with_correct)
+        logits, ctxs = self.forward_native(x, True)
+        N = logits.shape[1]
+        loss, dlogits, correct = Fn.cross_entropy(
+            logits, labels, targets, ncls=ncls or self.num_classes,
+            scale=(1.0 / N) if scale is None else scale, with_correct=with_correct)
+        self.backward_native(dlogits, ctxs)
         return loss, correct
 
     def _fused_head(self, x, targets, ncls):
@@ -158,16 +180,17 @@ class Net:
         if pool.name != "avgpool" or not isinstance(lin, ConvUnit) or not lin.linear or lin.bn or lin.act:
             return None
         ncls = ncls or self.num_classes or lin.cout
-        if not Fn.head_train_ok(lin.cin, ncls) or ncls > lin.cout:
+        if not Fn.head_train_ok(lin.cin, ncls, x.dtype) or ncls > lin.cout:
             return None
         return pool, lin, ncls
 
     def _train_step_fused_head(self, x, labels, head, scale, with_correct):
         pool, lin, ncls = head
         ctxs = []
-        for layer in self.layers[:-2]:
-            x, c = layer.forward(x, True)
-            ctxs.append(c)
+        with self._cpu_storage():
+            for layer in self.layers[:-2]:
+                x, c = layer.forward(x, True)
+                ctxs.append(c)
         st = self.store
         fuse = self.layers[-3].bn_out(ctxs[-1]) if pool.fuse_out_bn else None
         loss, correct, dx, part = Fn.head_train(
@@ -188,9 +211,10 @@ class Net:
 
     # ------------------------------------------------------------------ torch-compatible path
     def prepare_input(self, x: torch.Tensor) -> torch.Tensor:
-        """Accepts the native layout [G,N,...] bf16, or a torch-style fp32 batch (NCHW image /
-        [N, F] table) for G == 1, converting it with the kernels' input rules."""
-        if x.dtype == torch.bfloat16 and x.dim() >= 3 and x.shape[0] == self.G:
+        """Accepts the native layout [G,N,...] in the net's activation dtype, or a torch-style fp32
+        batch (NCHW image / [N, F] table) for G == 1, converting it with the kernels' input rules."""
+        dt = self.act_dtype
+        if x.dtype == dt and x.dim() >= 3 and x.shape[0] == self.G and (dt == torch.bfloat16 or x.dim() != 4):
             return x
         spec = self.input_spec
         if spec.get("flat") and x.dim() > 2:
@@ -198,12 +222,12 @@ class Net:
         if x.dim() == 4:  # NCHW images
             return Fn.nchw_to_nhwc(x.to(self.device), spec.get("cpad", 32),
                                    spec.get("stem_k", 0) if spec.get("im2col") else 0,
-                                   spec.get("pad", 0), spec.get("stem_stride", 1))
+                                   spec.get("pad", 0), spec.get("stem_stride", 1), dtype=dt)
         if x.dim() == 2:  # [N, F]
             F_ = x.shape[1]
             cp = spec.get("cpad", (F_ + 31) // 32 * 32)
-            out = torch.zeros(1, x.shape[0], cp, dtype=torch.bfloat16, device=self.device)
-            out[0, :, :F_] = x.to(self.device, torch.bfloat16)
+            out = torch.zeros(1, x.shape[0], cp, dtype=dt, device=self.device)
+            out[0, :, :F_] = x.to(self.device, dt)
             return out
         raise ValueError(f"unsupported input shape {tuple(x.shape)}")
 
@@ -273,9 +297,9 @@ class _NetFunction(torch.autograd.Function):
         (out,) = ctx.saved_tensors
         g = net.output_transform_backward(out, grad.float())
         G, N, ld = ctx.lshape
-        full = torch.zeros(G, N, ld, dtype=torch.bfloat16, device=g.device)
+        full = torch.zeros(G, N, ld, dtype=net.act_dtype, device=g.device)
         ncls = net.num_classes or ld
-        full[..., :ncls] = g.reshape(G, N, ncls).to(torch.bfloat16)
+        full[..., :ncls] = g.reshape(G, N, ncls).to(net.act_dtype)
         net.backward_native(full, ctx.ctxs)
         ctx.ctxs = None
         return None, None, None

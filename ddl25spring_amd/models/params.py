@@ -15,6 +15,7 @@ Consequences of this layout (the MI355X-first replacement for the reference's pe
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Callable
 
@@ -25,6 +26,24 @@ from ..ops import functional as Fn
 # Storage dtype of the weight shadow for CPU stores. bf16 mirrors the device numerics; tests flip
 # it (together with ops.reference._bf) to fp32 to check the fwd/bwd *logic* exactly.
 CPU_SHADOW_DTYPE = torch.bfloat16
+
+# Compute precision of native nets: "bf16" (bf16 MFMA operands and activations, fp32 master
+# weights / accumulation) or "fp32" (the reference's precision, lab/tutorial_1a/hfl_complete.py:
+# 39-80: fp32 activations and weights end to end on the exact-fp32 MFMA, conv_f32.hip; the
+# kernels read the fp32 master weights directly, there is no shadow). DDL_PRECISION sets the
+# default for nets built without an explicit precision.
+PRECISIONS = ("bf16", "fp32")
+_DEFAULT_PRECISION = [os.environ.get("DDL_PRECISION", "bf16")]
+
+
+def default_precision() -> str:
+    return _DEFAULT_PRECISION[0]
+
+
+def set_default_precision(p: str) -> None:
+    if p not in PRECISIONS:
+        raise ValueError(f"precision must be one of {PRECISIONS}, got {p!r}")
+    _DEFAULT_PRECISION[0] = p
 
 
 @dataclass
@@ -123,7 +142,9 @@ class ParamStore:
         return m
 
     # ---------------------------------------------------------------- materialise
-    def materialize(self, device, seed: int = 0, generator: torch.Generator | None = None):
+    def materialize(self, device, seed: int = 0, generator: torch.Generator | None = None,
+                    fp32: bool = False):
+        """fp32=True: the kernels read the fp32 master weights themselves (``shadow`` IS ``data``)."""
         device = torch.device(device)
         self.device = device
         G = self.G
@@ -140,13 +161,24 @@ class ParamStore:
         self.direct_map = self._direct_map().to(device)
         self.buffers = bufs.to(device)
         self.grad = torch.zeros_like(self.data)
-        sdt = torch.bfloat16 if device.type != "cpu" else CPU_SHADOW_DTYPE
-        self.shadow = torch.empty(self.data.shape, dtype=sdt, device=device)
+        if fp32:
+            self.shadow = self.data
+        else:
+            sdt = torch.bfloat16 if device.type != "cpu" else CPU_SHADOW_DTYPE
+            self.shadow = torch.empty(self.data.shape, dtype=sdt, device=device)
         self.sync_shadow()
         return self
 
+    @property
+    def shadow16(self):
+        """The separate bf16 weight shadow the optimizers refresh, or None when the kernels read
+        the fp32 master weights (fp32 precision)."""
+        return None if self.shadow is self.data else self.shadow
+
     def sync_shadow(self):
-        if self.shadow.dtype == torch.float32:
+        if self.shadow is self.data:
+            pass
+        elif self.shadow.dtype == torch.float32:
             self.shadow.copy_(self.data)
         else:
             Fn.to_bf16(self.data, self.shadow)

@@ -10,7 +10,10 @@ MI355X-first choices:
   * BatchNorm statistics come out of the conv epilogue; BN-apply fuses the residual join (identity
     or projected shortcut, whose own BN is folded into the same pass) and the ReLU;
   * backward of the residual join: the shortcut gradient is added inside the dgrad epilogue of
-    the block's first conv.
+    the block's first conv;
+  * fp32 precision (conv_f32.hip): a block's inner BN+ReLU outputs feed only the next conv, so
+    they are never stored — that conv applies relu(c * scale + shift) to its operand as it loads
+    it (``in_bn``), in the forward and again in its weight-gradient pass.
 """
 from __future__ import annotations
 
@@ -28,11 +31,11 @@ class _BNConv(ConvUnit):
     def __init__(self, cin, cout, k, stride, pad):
         super().__init__(cin, cout, k=k, stride=stride, pad=pad, bias=False, bn=True, act=None)
 
-    def conv_raw(self, x, train):
+    def conv_raw(self, x, train, in_bn=None):
         """The conv with its BN-statistics epilogue -> (c, stats | None, geom)."""
         g = self.geom(x)
-        stats = Fn.stats_buffer(g.G, self.cout, x.device) if train else None
-        return Fn.conv_fwd(x, self.store.shadow_of(self.w), g, stats=stats), stats, g
+        stats = Fn.stats_buffer(g.G, self.cout, x.device, like=x) if train else None
+        return Fn.conv_fwd(x, self.store.shadow_of(self.w), g, stats=stats, in_bn=in_bn), stats, g
 
     def bn_inputs(self, stats, g):
         st = self.store
@@ -44,8 +47,8 @@ class _BNConv(ConvUnit):
             stats = ws.zeros((g.G, 2, self.cout), self.store.data.device)
         return Fn.bn_finalize(*self.bn_inputs(stats, g), self.eps, self.momentum, training=train)
 
-    def conv_stats(self, x, train):
-        c, stats, g = self.conv_raw(x, train)
+    def conv_stats(self, x, train, in_bn=None):
+        c, stats, g = self.conv_raw(x, train, in_bn)
         sc, sh, mu, rs = self.finalize(stats, g, train)
         return c, sc, sh, mu, rs, g
 
@@ -59,18 +62,32 @@ class _BNConv(ConvUnit):
         return (c, mu, rs, st.param(self.gamma), st.grad_of(self.gamma), st.grad_of(self.beta), part)
 
 
-def _conv_pair_bn(main: _BNConv, y, down: _BNConv, x, train):
-    """A block's last conv (on y) and its projection shortcut (on the block input x), as one paired
-    launch where the tuner measured that faster, with both BatchNorms finalized in one launch -> (c, bn, g), (cs, bn_s, gs); bn = (scale, shift, mean, rstd)."""
+def _conv_pair_bn(main: _BNConv, y, down: _BNConv, x, train, in_bn=None):
+    """A block's last conv (on y, or on relu(y * scale + shift) with ``in_bn``) and its projection
+    shortcut (on the block input x), as one paired launch where the tuner measured that faster,
+    with both BatchNorms finalized in one launch -> (c, bn, g), (cs, bn_s, gs);
+    bn = (scale, shift, mean, rstd)."""
     g, gs = main.geom(y), down.geom(x)
-    st = Fn.stats_buffer(g.G, main.cout, y.device) if train else None
-    sts = Fn.stats_buffer(gs.G, down.cout, x.device) if train else None
-    c, cs = Fn.conv_fwd2(y, main.store.shadow_of(main.w), g, st, x, down.store.shadow_of(down.w), gs, sts)
+    st = Fn.stats_buffer(g.G, main.cout, y.device, like=y) if train else None
+    sts = Fn.stats_buffer(gs.G, down.cout, x.device, like=x) if train else None
+    if in_bn is not None:
+        c = Fn.conv_fwd(y, main.store.shadow_of(main.w), g, stats=st, in_bn=in_bn)
+        cs = Fn.conv_fwd(x, down.store.shadow_of(down.w), gs, stats=sts)
+    else:
+        c, cs = Fn.conv_fwd2(y, main.store.shadow_of(main.w), g, st, x, down.store.shadow_of(down.w), gs, sts)
     if train:
         bn, bns = Fn.bn_finalize2(main.bn_inputs(st, g), down.bn_inputs(sts, gs), main.eps, main.momentum)
     else:
         bn, bns = main.finalize(st, g, train), down.finalize(sts, gs, train)
     return (c, bn, g), (cs, bns, gs)
+
+
+def _inner_act(c, scale, shift):
+    """relu(BN(c)) feeding only the next conv: (activation, None), or in fp32 precision (c, (scale,
+    shift)) — the consumer applies it on the fly (operand-side BN), the activation is never stored."""
+    if Fn.F32.is_f32(c):
+        return c, (scale, shift)
+    return Fn.bn_apply(c, scale, shift, act=RELU), None
 
 
 class _ShortcutGrad:
@@ -130,23 +147,23 @@ class BasicBlock(_ShortcutGrad, Layer):
 
     def forward(self, x, train):
         c1, sc1, sh1, mu1, rs1, g1 = self.conv1.conv_stats(x, train)
-        a1 = Fn.bn_apply(c1, sc1, sh1, act=RELU)
+        a1, ib = _inner_act(c1, sc1, sh1)
         if self.down is not None:
             (c2, (sc2, sh2, mu2, rs2), g2), (cs, (scs, shs, mus, rss), gs) = \
-                _conv_pair_bn(self.conv2, a1, self.down, x, train)
+                _conv_pair_bn(self.conv2, a1, self.down, x, train, in_bn=ib)
             out = Fn.bn_apply(c2, sc2, sh2, r=cs, rscale=scs, rshift=shs, act=RELU)
             dctx = (cs, mus, rss, gs)
         else:
-            c2, sc2, sh2, mu2, rs2, g2 = self.conv2.conv_stats(a1, train)
+            c2, sc2, sh2, mu2, rs2, g2 = self.conv2.conv_stats(a1, train, in_bn=ib)
             out = Fn.bn_apply(c2, sc2, sh2, r=x, act=RELU)
             dctx = None
-        return out, (x, c1, a1, sc1, sh1, mu1, rs1, g1, c2, mu2, rs2, g2, out, dctx)
+        return out, (x, c1, a1, sc1, sh1, mu1, rs1, g1, c2, mu2, rs2, g2, out, dctx, ib)
 
     def bn_out(self, ctx):
         return (ctx[8], ctx[9], ctx[10])  # (c2, mu2, rs2): out = relu(bn2(c2) + shortcut)
 
     def backward(self, dout, ctx, part=None, fuse=None):
-        x, c1, a1, sc1, sh1, mu1, rs1, g1, c2, mu2, rs2, g2, out, dctx = ctx
+        x, c1, a1, sc1, sh1, mu1, rs1, g1, c2, mu2, rs2, g2, out, dctx, ib = ctx
         st = self.store
         dcs = None
         if part is not None and dctx is not None:  # output + shortcut BN backwards together
@@ -161,7 +178,7 @@ class BasicBlock(_ShortcutGrad, Layer):
         # dgrad epilogue applies bn1's ReLU mask (recomputed from c1: no read of a1) and reduces
         # bn1's backward sums (no reduce pass)
         da1, part1 = Fn.conv_dgrad_wgrad(dc2, st.shadow_of(self.conv2.w), a1, g2, st.grad_of(self.conv2.w),
-                                         bn=(c1, mu1, rs1), mask_bn=(sc1, sh1))
+                                         bn=(c1, mu1, rs1), mask_bn=(sc1, sh1), in_bn=ib)
         dc1 = self.conv1.bn_backward(da1, None, c1, mu1, rs1, part=part1)
         # with fuse: the producer's ReLU mask (x > 0) and BN reduce in this dgrad's epilogue
         return Fn.conv_dgrad_wgrad(dc1, st.shadow_of(self.conv1.w), x, g1, st.grad_of(self.conv1.w),
@@ -213,26 +230,27 @@ class Bottleneck(_ShortcutGrad, Layer):
 
     def forward(self, x, train):
         c1, sc1, sh1, mu1, rs1, g1 = self.conv1.conv_stats(x, train)
-        a1 = Fn.bn_apply(c1, sc1, sh1, act=RELU)
-        c2, sc2, sh2, mu2, rs2, g2 = self.conv2.conv_stats(a1, train)
-        a2 = Fn.bn_apply(c2, sc2, sh2, act=RELU)
+        a1, ib1 = _inner_act(c1, sc1, sh1)
+        c2, sc2, sh2, mu2, rs2, g2 = self.conv2.conv_stats(a1, train, in_bn=ib1)
+        a2, ib2 = _inner_act(c2, sc2, sh2)
         if self.down is not None:
             (c3, (sc3, sh3, mu3, rs3), g3), (cs, (scs, shs, mus, rss), gs) = \
-                _conv_pair_bn(self.conv3, a2, self.down, x, train)
+                _conv_pair_bn(self.conv3, a2, self.down, x, train, in_bn=ib2)
             out = Fn.bn_apply(c3, sc3, sh3, r=cs, rscale=scs, rshift=shs, act=RELU)
             dctx = (cs, mus, rss, gs)
         else:
-            c3, sc3, sh3, mu3, rs3, g3 = self.conv3.conv_stats(a2, train)
+            c3, sc3, sh3, mu3, rs3, g3 = self.conv3.conv_stats(a2, train, in_bn=ib2)
             out = Fn.bn_apply(c3, sc3, sh3, r=x, act=RELU)
             dctx = None
         return out, (x, (c1, a1, sc1, sh1, mu1, rs1, g1), (c2, a2, sc2, sh2, mu2, rs2, g2),
-                     (c3, mu3, rs3, g3), out, dctx)
+                     (c3, mu3, rs3, g3), out, dctx, (ib1, ib2))
 
     def bn_out(self, ctx):
         return ctx[3][:3]  # (c3, mu3, rs3): out = relu(bn3(c3) + shortcut)
 
     def backward(self, dout, ctx, part=None, fuse=None):
-        x, (c1, a1, sc1, sh1, mu1, rs1, g1), (c2, a2, sc2, sh2, mu2, rs2, g2), (c3, mu3, rs3, g3), out, dctx = ctx
+        x, (c1, a1, sc1, sh1, mu1, rs1, g1), (c2, a2, sc2, sh2, mu2, rs2, g2), (c3, mu3, rs3, g3), out, dctx, \
+            (ib1, ib2) = ctx
         st = self.store
         dcs = None
         if part is not None and dctx is not None:  # output + shortcut BN backwards together
@@ -244,10 +262,10 @@ class Bottleneck(_ShortcutGrad, Layer):
             dc3, dym = self.conv3.bn_backward(dout, out, c3, mu3, rs3, emit_dym=True)
         dres, rsub = self._shortcut_backward(dym, dctx, x, dcs) if dctx is not None else (dym, 1)
         da2, part2 = Fn.conv_dgrad_wgrad(dc3, st.shadow_of(self.conv3.w), a2, g3, st.grad_of(self.conv3.w),
-                                         bn=(c2, mu2, rs2), mask_bn=(sc2, sh2))
+                                         bn=(c2, mu2, rs2), mask_bn=(sc2, sh2), in_bn=ib2)
         dc2 = self.conv2.bn_backward(da2, None, c2, mu2, rs2, part=part2)
         da1, part1 = Fn.conv_dgrad_wgrad(dc2, st.shadow_of(self.conv2.w), a1, g2, st.grad_of(self.conv2.w),
-                                         bn=(c1, mu1, rs1), mask_bn=(sc1, sh1))
+                                         bn=(c1, mu1, rs1), mask_bn=(sc1, sh1), in_bn=ib1)
         dc1 = self.conv1.bn_backward(da1, None, c1, mu1, rs1, part=part1)
         return Fn.conv_dgrad_wgrad(dc1, st.shadow_of(self.conv1.w), x, g1, st.grad_of(self.conv1.w),
                                    residual=dres, mask=x if fuse is not None else None, bn=fuse,
@@ -287,7 +305,7 @@ class MaxPool3s2(Layer):
         return (G, N, (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1, C)
 
 
-def _resnet(block, layers, num_classes, groups, stem: str, in_ch=3) -> Net:
+def _resnet(block, layers, num_classes, groups, stem: str, in_ch=3, precision=None) -> Net:
     mods: list[Layer] = []
     if stem == "cifar":
         # im2col'd 3x3 stem: channel j = (r*3+s)*3 + c (27 real of 32), 1x1 conv on MFMA
@@ -320,19 +338,19 @@ def _resnet(block, layers, num_classes, groups, stem: str, in_ch=3) -> Net:
     fc.pname = "fc"
     mods.append(fc)
     net = Net(mods, groups=groups, num_classes=num_classes, input_spec=input_spec,
-              name=f"resnet{sum(layers) * (2 if block is BasicBlock else 3) + 2}")
+              name=f"resnet{sum(layers) * (2 if block is BasicBlock else 3) + 2}", precision=precision)
     return net
 
 
-def resnet18_cifar(num_classes=10, groups=1) -> Net:
+def resnet18_cifar(num_classes=10, groups=1, precision=None) -> Net:
     """ResNet-18, CIFAR variant (3x3 stem, no max-pool), 11.17M params."""
-    return _resnet(BasicBlock, (2, 2, 2, 2), num_classes, groups, "cifar")
+    return _resnet(BasicBlock, (2, 2, 2, 2), num_classes, groups, "cifar", precision=precision)
 
 
-def resnet50_imagenet(num_classes=1000, groups=1) -> Net:
+def resnet50_imagenet(num_classes=1000, groups=1, precision=None) -> Net:
     """ResNet-50, ImageNet variant (7x7/2 stem + 3x3/2 max-pool), 25.6M params."""
-    return _resnet(Bottleneck, (3, 4, 6, 3), num_classes, groups, "imagenet")
+    return _resnet(Bottleneck, (3, 4, 6, 3), num_classes, groups, "imagenet", precision=precision)
 
 
-def resnet18_imagenet(num_classes=1000, groups=1) -> Net:
-    return _resnet(BasicBlock, (2, 2, 2, 2), num_classes, groups, "imagenet")
+def resnet18_imagenet(num_classes=1000, groups=1, precision=None) -> Net:
+    return _resnet(BasicBlock, (2, 2, 2, 2), num_classes, groups, "imagenet", precision=precision)

@@ -66,6 +66,29 @@ class HeadArgs(ctypes.Structure):
                 ("HW", i32), ("C", i32), ("ncls", i32), ("S", i32), ("scale", f32)]
 
 
+class ConvF32Args(ctypes.Structure):  # conv_f32.hip
+    _fields_ = [("x", vp), ("w", vp), ("dy", vp), ("out", vp), ("stats", vp), ("bias", vp), ("residual", vp),
+                ("mask", vp), ("in_scale", vp), ("in_shift", vp), ("bn_x", vp), ("bn_mean", vp), ("bn_rstd", vp),
+                ("mask_scale", vp), ("mask_shift", vp), ("partial", vp), ("partial_cap", i64),
+                ("x_gs", i64), ("w_gs", i64), ("dy_gs", i64), ("out_gs", i64), ("bias_gs", i64), ("res_gs", i64),
+                ("G", i32), ("N", i32), ("H", i32), ("W", i32), ("C", i32), ("K", i32), ("R", i32), ("S", i32),
+                ("P", i32), ("Q", i32), ("stride", i32), ("pad", i32), ("relu", i32), ("accumulate", i32),
+                ("split_k", i32), ("res_sub", i32), ("in_relu", i32), ("slots", i32), ("gscale", f32)]
+
+
+class BNFBwdArgs(ctypes.Structure):  # bn_f32.hip
+    _fields_ = [("x", vp), ("mean", vp), ("rstd", vp), ("gamma", vp), ("dgamma", vp), ("dbeta", vp),
+                ("part", vp), ("coef", vp), ("dx", vp), ("gs_param", i64), ("slots", i32)]
+
+
+class HeadFArgs(ctypes.Structure):  # bn_f32.hip
+    _fields_ = [("x", vp), ("w", vp), ("b", vp), ("labels", vp), ("loss", vp), ("correct", vp),
+                ("dw", vp), ("db", vp), ("dx", vp), ("c", vp), ("mean", vp), ("rstd", vp), ("part", vp),
+                ("pooled", vp), ("dlog", vp), ("row_loss", vp), ("row_hit", vp),
+                ("w_gs", i64), ("b_gs", i64), ("dw_gs", i64), ("db_gs", i64), ("G", i32), ("N", i32),
+                ("HW", i32), ("C", i32), ("ncls", i32), ("scale", f32)]
+
+
 class SGDArgs(ctypes.Structure):
     _fields_ = [("p", vp), ("g", vp), ("mom", vp), ("shadow", vp), ("n", i64), ("lr", f32),
                 ("wd", f32), ("momentum", f32), ("dampening", f32), ("grad_scale", f32),
@@ -135,6 +158,28 @@ _SIGS = {
     "ddl_coord_select": [vp, i64, i32, i64, i32, i32, vp, vp],
 }
 
+# fp32-activation twins of the templated memory-bound launchers (nn_ops.hip): same signatures
+for _n in ("ddl_prep_images", "ddl_nchw_to_nhwc", "ddl_maxpool_fwd", "ddl_maxpool_bwd", "ddl_maxpool2_fwd",
+           "ddl_maxpool2_bwd", "ddl_avgpool_fwd", "ddl_avgpool_bwd", "ddl_dropout", "ddl_act_fwd", "ddl_act_bwd",
+           "ddl_channel_sum", "ddl_ce_fwd_bwd"):
+    _SIGS[_n + "_f32"] = _SIGS[_n]
+_SIGS.update({
+    # conv_f32.hip
+    "ddl_convf32": [ctypes.POINTER(ConvF32Args), i32, i32, vp],
+    "ddl_convf32_slots": [ctypes.POINTER(ConvF32Args), i32, i32],
+    "ddl_convf32_workspace": [ctypes.POINTER(ConvF32Args), i32, i32],
+    # bn_f32.hip
+    "ddl_bnf_finalize": [ctypes.POINTER(BNArgs), ctypes.POINTER(BNArgs), vp],
+    "ddl_bnf_apply": [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, vp],
+    "ddl_bnf_reduce_slots": [i64, i32, i32],
+    "ddl_bnf_reduce": [vp, vp, vp, vp, vp, vp, i64, i32, i32, vp],
+    "ddl_bnf_stats": [vp, vp, i64, i32, i32, vp],
+    "ddl_bnf_backward": [vp, vp, ctypes.POINTER(BNFBwdArgs), ctypes.POINTER(BNFBwdArgs), vp, i64, i32, i32, i32, vp],
+    "ddl_avgpoolf_bwd_bn": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp],
+    "ddl_headf_train": [ctypes.POINTER(HeadFArgs), vp],
+})
+_RESTYPES = {"ddl_convf32_slots": ctypes.c_longlong, "ddl_convf32_workspace": ctypes.c_longlong}
+
 _OPTIONAL_SIGS: dict[str, list] = {}
 
 
@@ -151,7 +196,7 @@ def _declare(lib, sigs) -> None:
         if fn is None:
             continue
         fn.argtypes = argt
-        fn.restype = ctypes.c_int
+        fn.restype = _RESTYPES.get(name, ctypes.c_int)
 
 
 def kernels_available() -> bool:
@@ -176,7 +221,11 @@ def kernels():
                                    ("HeadArgs", "ddl_head_args_size", HeadArgs),
                                    ("SGDArgs", "ddl_sgd_args_size", SGDArgs),
                                    ("SGDDirectArgs", "ddl_sgd_direct_args_size", SGDDirectArgs),
-                                   ("AdamArgs", "ddl_adam_args_size", AdamArgs)):
+                                   ("AdamArgs", "ddl_adam_args_size", AdamArgs),
+                                   ("ConvF32Args", "ddl_convf32_args_size", ConvF32Args),
+                                   ("BNArgs", "ddl_bnf_args_size", BNArgs),
+                                   ("BNFBwdArgs", "ddl_bnf_bwd_args_size", BNFBwdArgs),
+                                   ("HeadFArgs", "ddl_headf_args_size", HeadFArgs)):
             f = getattr(lib, size_fn)
             f.restype = ctypes.c_int
             if f() != ctypes.sizeof(cls):

@@ -375,7 +375,9 @@ class _VocabCE(torch.autograd.Function):
         if scale != 1.0:
             inv.mul_(scale)
         loss = torch.zeros(1, dtype=torch.float32, device=lg.device)
-        if V > CE_FUSED_MAX_V:
+        # the fused loss + gradient pass writes a [R, V] gradient: only worth it when one is needed
+        # (no_grad / eval forwards keep just the per-row log-sum-exp)
+        if V > CE_FUSED_MAX_V or not ctx.needs_input_grad[0]:
             lse = torch.empty(R, dtype=torch.float32, device=lg.device)
             check(K().ddl_ce_vocab_lse(ptr(lg), ptr(lab), R, V, V, ptr(inv), int(ignore_index), ptr(loss),
                                        ptr(lse), stream()), "ce_vocab_lse")

@@ -1,7 +1,8 @@
 """Tensor-level op API over the HIP kernels (device tensors) and the PyTorch reference (CPU).
 
 Layout contract (see csrc/include/ddl_common.h):
-  * activations: bf16, NHWC, leading client-group dim  ``[G, N, H, W, C]`` (or ``[G, N, C]``)
+  * activations: bf16, NHWC, leading client-group dim  ``[G, N, H, W, C]`` (or ``[G, N, C]``);
+    fp32 activations (the reference-precision mode) dispatch to ``ops.functional_f32``
   * weights: bf16 shadow views ``[G, K, R, S, C]`` whose group stride may be the flat-buffer
     stride (inner dims contiguous)
   * grads / master params / optimizer state: fp32 views of the same flat buffers
@@ -15,6 +16,7 @@ import torch
 
 from . import _lib
 from . import autotune
+from . import functional_f32 as F32
 from . import reference as ref
 from . import workspace as ws
 from ._lib import check, ptr, stream
@@ -144,17 +146,33 @@ def _check_inner(t: torch.Tensor, name: str) -> None:
 BN_STRIPES = 32  # == BN_NSTRIPE in batchnorm.hip
 
 
-def stats_buffer(G: int, C: int, device) -> torch.Tensor:
+def stats_buffer(G: int, C: int, device, like=None):
     """Zeroed BN statistics accumulator [G, BN_STRIPES, 2, C]: producers (conv epilogue, bn_stats)
-    spread their fp32 atomics over the stripes, bn_finalize folds them."""
+    spread their fp32 atomics over the stripes, bn_finalize folds them. For fp32 device activations
+    (``like``) a ``SlotStats`` the producing conv fills with its per-tile slots instead."""
+    if like is not None and F32.is_f32(like):
+        return F32.SlotStats()
     return ws.zeros((G, BN_STRIPES, 2, C), device)
 
 
+def _materialize_in_bn(x, in_bn):
+    """Operand-side BN (``in_bn=(scale, shift)``: the conv reads relu(x * scale + shift)) on the
+    paths without the fused operand transform: apply it as a pass."""
+    if in_bn is None:
+        return x
+    return bn_apply(x, in_bn[0], in_bn[1], act=1)
+
+
 def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out=None, cfg=0,
-             residual=None, split_k=0, _tune=True):
+             residual=None, split_k=0, _tune=True, in_bn=None):
     """y[G,N,P,Q,K] = conv(x[G,N,H,W,C], w[G,K,R,S,C]) (+bias)(+residual)(relu);
     stats ([G,S,2,K] from ``stats_buffer``, or [G,2,K]) += per-channel sum, sumsq of y.
-    split_k: 0 = automatic split-K for grids too small to fill the GPU, 1 = off, n = n slices."""
+    split_k: 0 = automatic split-K for grids too small to fill the GPU, 1 = off, n = n slices.
+    in_bn = (scale, shift): convolve relu(x * scale + shift) instead of x (fused in the fp32 kernel)."""
+    if F32.is_f32(x):
+        return F32.conv_fwd(x, w, geom, bias=bias, relu=relu, stats=stats, out=out, residual=residual,
+                            in_bn=in_bn, split_k=split_k)
+    x = _materialize_in_bn(x, in_bn)
     if not x.is_cuda:
         y = ref.conv_fwd(x, w, geom, bias, relu, stats)
         if residual is not None:
@@ -197,6 +215,9 @@ def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0,
     pixels (2i, 2j) only (a 1x1 / stride-2 shortcut's input gradient without its zero pixels)."""
     if mask_bn is not None:
         assert bn is not None and mask is None, "mask_bn recomputes the mask from bn's x"
+    if F32.is_f32(dy):
+        return F32.conv_dgrad(dy, w, geom, residual=residual, mask=mask, out=out, bn=bn, mask_bn=mask_bn,
+                              residual_sub=residual_sub, split_k=split_k)
     if not dy.is_cuda:
         if mask_bn is not None:
             sc, sh = mask_bn
@@ -296,12 +317,16 @@ def _wgrad_args(dy, x, geom, dw, accumulate, splits):
                       gscale=gscale)
 
 
-def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0, _tune=True):
-    """dw[G,K,R,S,C] (+)= sum over pixels dy (x) x  — fp32, split-K with atomics.
-    cfg = conv_cfg(bp, bq, bk, stages) (0: tuned default); splits = split-K slices (0: auto).
-    Inside ``wgrad_overlap`` the launch goes to the side stream (see there)."""
+def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0, _tune=True, in_bn=None):
+    """dw[G,K,R,S,C] (+)= sum over pixels dy (x) x  — fp32, split-K with atomics (fp32 activations:
+    deterministic slices). cfg = conv_cfg(bp, bq, bk, stages) (0: tuned default); splits = split-K
+    slices (0: auto). in_bn: as conv_fwd. Inside ``wgrad_overlap`` the launch goes to the side
+    stream (see there)."""
     if not accumulate and wgrad_scale(dw) != 1.0:
         raise ValueError("a scaled WGRAD must accumulate (it adds into the master weights)")
+    if F32.is_f32(dy):
+        return F32.conv_wgrad(dy, x, geom, dw, accumulate, wgrad_scale(dw), in_bn=in_bn, split_k=splits)
+    x = _materialize_in_bn(x, in_bn)
     if not dy.is_cuda:
         ref.conv_wgrad(dy, x, geom, dw, accumulate, wgrad_scale(dw))
         return dw
@@ -365,15 +390,18 @@ def conv_pair(dy, w, x, geom: ConvGeom, dw, dcfg: int, dsplit: int, wcfg: int, w
 
 
 def conv_dgrad_wgrad(dy, w, x, geom: ConvGeom, dw, residual=None, mask=None, bn=None, mask_bn=None,
-                     want_dx: bool = True, residual_sub: int = 1, dgeom: ConvGeom | None = None):
+                     want_dx: bool = True, residual_sub: int = 1, dgeom: ConvGeom | None = None, in_bn=None):
     """``conv_wgrad(dy, x, geom, dw)`` and (if want_dx) ``conv_dgrad(dy, w, dgeom or geom, residual,
     mask, bn=bn, mask_bn=mask_bn, residual_sub=...)`` — both read dy and are independent, so on
     the GPU they may run as ONE paired launch (whichever of paired / back-to-back the tuner
     measured faster for this shape). ``dgeom``: the DGRAD's own geometry (a stride-2 1x1
     shortcut's input gradient on the compact grid). Returns what conv_dgrad returns (None
-    without want_dx)."""
+    without want_dx). in_bn: the WGRAD's operand-side BN of x (as conv_fwd)."""
     dg = dgeom or geom
     dkw = dict(residual=residual, mask=mask, bn=bn, mask_bn=mask_bn, residual_sub=residual_sub)
+    if F32.is_f32(dy) or in_bn is not None:
+        conv_wgrad(dy, x, geom, dw, in_bn=in_bn)
+        return conv_dgrad(dy, w, dg, **dkw) if want_dx else None
     if not want_dx or not dy.is_cuda or not PAIR_ENABLED or _WGRAD_SIDE is not None \
             or not autotune.ENABLED:
         conv_wgrad(dy, x, geom, dw)
@@ -463,7 +491,7 @@ def conv_fwd2(xa, wa, ga: ConvGeom, stats_a, xb, wb, gb: ConvGeom, stats_b):
     downsample block's last conv (A) and its projection shortcut on the block input (B). On the
     GPU they may run as ONE paired launch (whichever of paired / back-to-back the pair tuner
     measured faster for these shapes)."""
-    if not xa.is_cuda or not PAIR_ENABLED or not PAIR_FWD_ENABLED or not autotune.ENABLED:
+    if not xa.is_cuda or F32.is_f32(xa) or not PAIR_ENABLED or not PAIR_FWD_ENABLED or not autotune.ENABLED:
         return conv_fwd(xa, wa, ga, stats=stats_a), conv_fwd(xb, wb, gb, stats=stats_b)
     _check_inner(xa, "xa"); _check_inner(wa, "wa"); _check_inner(xb, "xb"); _check_inner(wb, "wb")
     dev = xa.device
@@ -550,6 +578,11 @@ class wgrad_overlap:
 def bn_finalize(stats, gamma, beta, running_mean, running_var, count, eps=1e-5, momentum=0.1,
                 training=True):
     """-> (scale, shift, mean, rstd), each [G, C] fp32 contiguous."""
+    if isinstance(stats, F32.SlotStats):
+        G = stats.t.shape[0] if stats.t is not None else running_mean.shape[0]
+        C = stats.t.shape[-1] if stats.t is not None else running_mean.shape[-1]
+        return F32.bn_finalize_many([(stats, gamma, beta, running_mean, running_var, count, G, C)], eps, momentum,
+                                    training)[0]
     if not stats.is_cuda:
         return ref.bn_finalize(stats, gamma, beta, running_mean, running_var, count, eps, momentum,
                                training)
@@ -588,6 +621,9 @@ def bn_finalize2(bn_a, bn_b, eps=1e-5, momentum=0.1):
     """Training-mode bn_finalize of two independent BatchNorms in one launch (a residual block's
     output BN and its projected shortcut's BN). bn_* = (stats, gamma, beta, running_mean,
     running_var, count) -> ((scale, shift, mean, rstd), (scale, shift, mean, rstd))."""
+    if isinstance(bn_a[0], F32.SlotStats):
+        items = [(bn[0], *bn[1:], bn[0].t.shape[0], bn[0].t.shape[-1]) for bn in (bn_a, bn_b)]
+        return tuple(F32.bn_finalize_many(items, eps, momentum))
     if not bn_a[0].is_cuda:
         return (bn_finalize(*bn_a, eps, momentum), bn_finalize(*bn_b, eps, momentum))
     outs = []
@@ -604,6 +640,8 @@ def bn_bwd_reduce_part(dy, ymask, x, mean, rstd):
     """Striped BN backward reduce sums [G, BN_STRIPES, 2, C] (sum dy_m, sum dy_m * xhat) for
     ``bn_backward(..., part=)`` / ``bn_backward2``; dy_m = dy * (ymask > 0) (ymask nullable)."""
     G, C = x.shape[0], x.shape[-1]
+    if F32.is_f32(dy):
+        return F32.bn_bwd_reduce_part(dy, ymask, x, mean, rstd)
     if not dy.is_cuda:
         sums = ref.bn_bwd_reduce(dy, ymask, x, mean, rstd)
         part = torch.zeros(G, BN_STRIPES, 2, C)
@@ -620,6 +658,8 @@ def bn_backward2(dy, bn_a, bn_b):
     """Two BatchNorm backwards sharing the already-masked input gradient dy (a block's output BN and
     its shortcut's BN): one fold launch for both and one apply pass that reads dy once.
     bn_* = (x, mean, rstd, gamma, dgamma, dbeta, part) -> (dx_a, dx_b)."""
+    if F32.is_f32(dy):
+        return F32.bn_backward2(dy, bn_a, bn_b)
     if not dy.is_cuda:
         return tuple(bn_backward(dy, None, bn[0], bn[1], bn[2], bn[3], bn[4], bn[5], part=bn[6])
                      for bn in (bn_a, bn_b))
@@ -637,6 +677,7 @@ def bn_backward2(dy, bn_a, bn_b):
         t.x, t.mean, t.rstd, t.gamma = ptr(x), ptr(mean), ptr(rstd), ptr(gamma)
         t.dgamma, t.dbeta, t.part, t.coef, t.dx, t.gs_param = ptr(dgamma), ptr(dbeta), ptr(part), \
             ptr(coef), ptr(dx), gs
+        t._keep = coef  # outside a step's arena the scratch must outlive the launch
         args.append(t)
         outs.append(dx)
     check(_lib.kernels().ddl_bn_backward2(ptr(dy), ctypes.byref(args[0]), ctypes.byref(args[1]),
@@ -645,6 +686,8 @@ def bn_backward2(dy, bn_a, bn_b):
 
 
 def bn_apply(x, scale, shift, r=None, rscale=None, rshift=None, act=0, out=None):
+    if F32.is_f32(x):
+        return F32.bn_apply(x, scale, shift, r, rscale, rshift, act, out)
     if not x.is_cuda:
         y = ref.bn_apply(x, scale, shift, r, rscale, rshift, act)
         if out is not None:
@@ -663,6 +706,9 @@ def bn_apply(x, scale, shift, r=None, rscale=None, rshift=None, act=0, out=None)
 def bn_stats(x, stats=None):
     """stats [G, BN_STRIPES, 2, C] fp32 (+)= per-channel (sum, sum of squares) of x [G, ..., C]."""
     G, C = x.shape[0], x.shape[-1]
+    if F32.is_f32(x):
+        assert stats is None, "fp32 statistics are returned as a new SlotStats"
+        return F32.bn_stats(x)
     if stats is None:
         stats = stats_buffer(G, C, x.device)
     if not x.is_cuda:
@@ -676,6 +722,7 @@ def bn_stats(x, stats=None):
 
 def bn_bwd_reduce(dy, ymask, x, mean, rstd, dgamma=None, dbeta=None):
     """-> sums [G, 2, C] = (sum dy_m, sum dy_m*xhat); also accumulates into dgamma/dbeta views."""
+    assert not F32.is_f32(dy), "fp32 activations: use bn_backward / bn_bwd_reduce_part"
     if not dy.is_cuda:
         return ref.bn_bwd_reduce(dy, ymask, x, mean, rstd, dgamma, dbeta)
     G, C = x.shape[0], x.shape[-1]
@@ -694,6 +741,8 @@ def bn_backward(dy, ymask, x, mean, rstd, gamma, dgamma=None, dbeta=None, emit_d
     d(gamma), d(beta) into the given [G, C] views. -> dx (, dy_m if emit_dym).
     ``part``: the striped reduce sums already produced by dy's producer (``conv_dgrad(bn=...)``,
     which also applied the mask) — the reduce pass is skipped (two launches)."""
+    if F32.is_f32(dy):
+        return F32.bn_backward(dy, ymask, x, mean, rstd, gamma, dgamma, dbeta, emit_dym, part)
     if not dy.is_cuda:
         if part is not None:
             sums = part.sum(1)
@@ -724,6 +773,7 @@ def bn_backward(dy, ymask, x, mean, rstd, gamma, dgamma=None, dbeta=None, emit_d
 
 
 def bn_bwd_apply(dy, ymask, x, mean, rstd, gamma, sums, emit_dym=False):
+    assert not F32.is_f32(dy), "fp32 activations: use bn_backward"
     if not dy.is_cuda:
         return ref.bn_bwd_apply(dy, ymask, x, mean, rstd, gamma, sums, emit_dym)
     G, C = x.shape[0], x.shape[-1]
@@ -738,12 +788,21 @@ def bn_bwd_apply(dy, ymask, x, mean, rstd, gamma, sums, emit_dym=False):
 
 
 # ----------------------------------------------------------------------------- elementwise
+def _k(name: str, t: torch.Tensor):
+    """The launcher for t's activation dtype: ``name`` (bf16) or its ``_f32`` twin."""
+    lib = _lib.kernels()
+    if t.dtype == torch.float32:
+        return getattr(lib, name + "_f32")
+    assert t.dtype == torch.bfloat16, f"{name}: unsupported activation dtype {t.dtype}"
+    return getattr(lib, name)
+
+
 def maxpool2_fwd(x):
     if not x.is_cuda:
         return ref.maxpool2_fwd(x)
     G, N, H, W, C = x.shape
     y = torch.empty(G, N, H // 2, W // 2, C, dtype=x.dtype, device=x.device)
-    check(_lib.kernels().ddl_maxpool2_fwd(ptr(x), ptr(y), G * N, H, W, C, stream()), "maxpool2_fwd")
+    check(_k("ddl_maxpool2_fwd", x)(ptr(x), ptr(y), G * N, H, W, C, stream()), "maxpool2_fwd")
     return y
 
 
@@ -752,7 +811,7 @@ def maxpool2_bwd(x, dy):
         return ref.maxpool2_bwd(x, dy)
     G, N, H, W, C = x.shape
     dx = torch.empty_like(x)
-    check(_lib.kernels().ddl_maxpool2_bwd(ptr(x), ptr(dy), ptr(dx), G * N, H, W, C, stream()),
+    check(_k("ddl_maxpool2_bwd", x)(ptr(x), ptr(dy), ptr(dx), G * N, H, W, C, stream()),
           "maxpool2_bwd")
     return dx
 
@@ -762,7 +821,7 @@ def avgpool_fwd(x):
         return ref.avgpool_fwd(x)
     G, N, H, W, C = x.shape
     y = torch.empty(G, N, C, dtype=x.dtype, device=x.device)
-    check(_lib.kernels().ddl_avgpool_fwd(ptr(x), ptr(y), G * N, H * W, C, stream()), "avgpool_fwd")
+    check(_k("ddl_avgpool_fwd", x)(ptr(x), ptr(y), G * N, H * W, C, stream()), "avgpool_fwd")
     return y
 
 
@@ -771,7 +830,7 @@ def avgpool_bwd(dy, H, W):
         return ref.avgpool_bwd(dy, H, W)
     G, N, C = dy.shape
     dx = torch.empty(G, N, H, W, C, dtype=dy.dtype, device=dy.device)
-    check(_lib.kernels().ddl_avgpool_bwd(ptr(dy), ptr(dx), G * N, H * W, C, stream()), "avgpool_bwd")
+    check(_k("ddl_avgpool_bwd", dy)(ptr(dy), ptr(dx), G * N, H * W, C, stream()), "avgpool_bwd")
     return dx
 
 
@@ -779,6 +838,8 @@ def avgpool_bwd_bn(dy, x, bn):
     """Global-average-pool backward for a pooled input x = relu(BN(c) [+ r]) fused with that BN's
     backward reduce: -> (dx = dy/HW * (x > 0), part [G, BN_STRIPES, 2, C] with (sum dx,
     sum dx * (c - mean) * rstd)) for ``bn_backward(..., part=part)``. bn = (c, mean, rstd)."""
+    if F32.is_f32(x):
+        return F32.avgpool_bwd_bn(dy, x, bn)
     c, mean, rstd = bn
     G, N, H, W, C = x.shape
     if not dy.is_cuda:
@@ -806,7 +867,7 @@ def dropout(x, p, seed, offset, offset_dev=None):
         extra = int(offset_dev.item()) if offset_dev is not None else 0
         return ref.dropout(x, p, seed, offset + extra)
     y = torch.empty_like(x)
-    check(_lib.kernels().ddl_dropout(ptr(x), ptr(y), x.numel(), float(p), int(seed), int(offset),
+    check(_k("ddl_dropout", x)(ptr(x), ptr(y), x.numel(), float(p), int(seed), int(offset),
                                      ptr(offset_dev), stream()), "dropout")
     return y
 
@@ -827,7 +888,7 @@ def act_fwd(x, act: int, slope=0.01):
     if not x.is_cuda:
         return ref.act_fwd(x, act, slope)
     y = torch.empty_like(x)
-    check(_lib.kernels().ddl_act_fwd(ptr(x), ptr(y), x.numel(), act, float(slope), stream()), "act_fwd")
+    check(_k("ddl_act_fwd", x)(ptr(x), ptr(y), x.numel(), act, float(slope), stream()), "act_fwd")
     return y
 
 
@@ -835,7 +896,7 @@ def act_bwd(y, dy, act: int, slope=0.01):
     if not y.is_cuda:
         return ref.act_bwd(y, dy, act, slope)
     dx = torch.empty_like(dy)
-    check(_lib.kernels().ddl_act_bwd(ptr(y), ptr(dy), ptr(dx), y.numel(), act, float(slope),
+    check(_k("ddl_act_bwd", y)(ptr(y), ptr(dy), ptr(dx), y.numel(), act, float(slope),
                                      stream()), "act_bwd")
     return dx
 
@@ -846,7 +907,7 @@ def channel_sum(x, out):
         ref.channel_sum(x, out)
         return out
     G, C = x.shape[0], x.shape[-1]
-    check(_lib.kernels().ddl_channel_sum(ptr(x), ptr(out), _gs(out), x[0].numel() // C, C, G,
+    check(_k("ddl_channel_sum", x)(ptr(x), ptr(out), _gs(out), x[0].numel() // C, C, G,
                                          stream()), "channel_sum")
     return out
 
@@ -871,7 +932,7 @@ def _stem_out(H, W, k, pad, stride):
     return (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
 
 
-def _im2col_cpu(xf, k, pad, stride, cpad):
+def _im2col_cpu(xf, k, pad, stride, cpad, dtype=torch.bfloat16):
     N, C, H, W = xf.shape
     Ho, Wo = _stem_out(H, W, k, pad, stride)
     if k:
@@ -881,46 +942,48 @@ def _im2col_cpu(xf, k, pad, stride, cpad):
         cols = xf.permute(0, 2, 3, 1)
     out = torch.zeros(1, N, Ho, Wo, cpad, dtype=torch.float32)
     out[0, ..., :cols.shape[-1]] = cols
-    return ref._bf(out)
+    return out if dtype == torch.float32 else ref._bf(out)
 
 
-def nchw_to_nhwc(x: torch.Tensor, cpad: int, im2col=0, pad: int = 0, stride: int = 1):
-    """fp32 NCHW -> bf16 NHWC [1, N, H', W', cpad]; ``im2col=k`` lays out the k x k / stride
-    patches of the stem conv as channels ((r*k+s)*C + c), so the stem runs as a 1x1 GEMM."""
+def nchw_to_nhwc(x: torch.Tensor, cpad: int, im2col=0, pad: int = 0, stride: int = 1,
+                 dtype=torch.bfloat16):
+    """fp32 NCHW -> NHWC [1, N, H', W', cpad] (bf16, or fp32 for the reference-precision mode);
+    ``im2col=k`` lays out the k x k / stride patches of the stem conv as channels
+    ((r*k+s)*C + c), so the stem runs as a 1x1 GEMM."""
     k = _im2col_k(im2col)
     N, C, H, W = x.shape
     Ho, Wo = _stem_out(H, W, k, pad, stride)
     if not x.is_cuda:
-        return _im2col_cpu(x.float(), k, pad, stride, cpad)
+        return _im2col_cpu(x.float(), k, pad, stride, cpad, dtype)
     xc = x.float().contiguous()
-    out = torch.empty(1, N, Ho, Wo, cpad, dtype=torch.bfloat16, device=x.device)
-    check(_lib.kernels().ddl_nchw_to_nhwc(ptr(xc), ptr(out), N, C, H, W, cpad, k, pad, stride,
+    out = torch.empty(1, N, Ho, Wo, cpad, dtype=dtype, device=x.device)
+    check(_k("ddl_nchw_to_nhwc", out)(ptr(xc), ptr(out), N, C, H, W, cpad, k, pad, stride,
                                           stream()), "nchw_to_nhwc")
     return out
 
 
 def prep_images(src_u8, idx, mean, inv_std, cpad, im2col=0, pad=0, stride=1, out=None,
-                labels=None, labels_out=None):
-    """Gather uint8 HWC samples by id, normalise, NHWC bf16 (channel-padded / stem-im2col).
-    labels / labels_out: also gather the int32 labels of the batch (same launch)."""
+                labels=None, labels_out=None, dtype=torch.bfloat16):
+    """Gather uint8 HWC samples by id, normalise, NHWC bf16 / fp32 (``dtype``; channel-padded /
+    stem-im2col). labels / labels_out: also gather the int32 labels of the batch (same launch)."""
     k = _im2col_k(im2col)
     n = idx.numel()
     Hs, Ws, Cs = src_u8.shape[1:]
     Ho, Wo = _stem_out(Hs, Ws, k, pad, stride)
     if out is None:
-        out = torch.empty(n, Ho, Wo, cpad, dtype=torch.bfloat16, device=src_u8.device)
+        out = torch.empty(n, Ho, Wo, cpad, dtype=dtype, device=src_u8.device)
     if not src_u8.is_cuda:
         ids = idx.long().reshape(-1)
         x = src_u8[ids].float() / 255.0
         x = (x - mean) * inv_std
-        out.copy_(_im2col_cpu(x.permute(0, 3, 1, 2), k, pad, stride, cpad)[0].reshape(out.shape))
+        out.copy_(_im2col_cpu(x.permute(0, 3, 1, 2), k, pad, stride, cpad, out.dtype)[0].reshape(out.shape))
         if labels is not None:
             labels_out.copy_(labels[ids].reshape(labels_out.shape))
         return out
     assert idx.dtype == torch.int32 and idx.is_contiguous()
     assert labels is None or (labels.dtype == torch.int32 and labels_out.dtype == torch.int32
                               and labels_out.numel() == n)
-    check(_lib.kernels().ddl_prep_images(ptr(src_u8), ptr(idx), ptr(mean), ptr(inv_std), ptr(out),
+    check(_k("ddl_prep_images", out)(ptr(src_u8), ptr(idx), ptr(mean), ptr(inv_std), ptr(out),
                                          n, Hs, Ws, Cs, cpad, k, pad, stride, ptr(labels),
                                          ptr(labels_out), stream()),
           "prep_images")
@@ -934,11 +997,11 @@ def maxpool_fwd(x, k, stride, pad, want_argmax=False):
     if not x.is_cuda:
         xi = x.float().reshape(G * N, H, W, C).permute(0, 3, 1, 2)
         y = torch.nn.functional.max_pool2d(xi, k, stride, pad)
-        y = y.permute(0, 2, 3, 1).reshape(G, N, Ho, Wo, C).to(torch.bfloat16).contiguous()
+        y = y.permute(0, 2, 3, 1).reshape(G, N, Ho, Wo, C).to(x.dtype).contiguous()
         return (y, None) if want_argmax else y
     y = torch.empty(G, N, Ho, Wo, C, dtype=x.dtype, device=x.device)
     am = torch.empty(G, N, Ho, Wo, C, dtype=torch.uint8, device=x.device) if want_argmax else None
-    check(_lib.kernels().ddl_maxpool_fwd(ptr(x), ptr(y), ptr(am), G * N, H, W, C, k, stride, pad,
+    check(_k("ddl_maxpool_fwd", x)(ptr(x), ptr(y), ptr(am), G * N, H, W, C, k, stride, pad,
                                          stream()), "maxpool_fwd")
     return (y, am) if want_argmax else y
 
@@ -951,9 +1014,9 @@ def maxpool_bwd(x, dy, k, stride, pad, argmax=None):
             y = torch.nn.functional.max_pool2d(xi, k, stride, pad)
             g = dy.float().reshape(G * N, *dy.shape[2:]).permute(0, 3, 1, 2)
             (dx,) = torch.autograd.grad(y, xi, g)
-        return dx.permute(0, 2, 3, 1).reshape(G, N, H, W, C).to(torch.bfloat16).contiguous()
+        return dx.permute(0, 2, 3, 1).reshape(G, N, H, W, C).to(x.dtype).contiguous()
     dx = torch.empty_like(x)
-    check(_lib.kernels().ddl_maxpool_bwd(ptr(x), ptr(dy), ptr(argmax), ptr(dx), G * N, H, W, C, k,
+    check(_k("ddl_maxpool_bwd", x)(ptr(x), ptr(dy), ptr(argmax), ptr(dx), G * N, H, W, C, k,
                                          stride, pad, stream()), "maxpool_bwd")
     return dx
 
@@ -973,7 +1036,7 @@ def cross_entropy(logits, labels=None, targets=None, ncls=None, scale=1.0, want_
     d = torch.empty_like(logits) if want_grad else None
     lab = labels.to(torch.int32).contiguous() if labels is not None else None
     tgt = targets.float().contiguous() if targets is not None else None
-    check(_lib.kernels().ddl_ce_fwd_bwd(ptr(logits), ptr(lab), ptr(tgt), G * N, N, ncls, ld,
+    check(_k("ddl_ce_fwd_bwd", logits)(ptr(logits), ptr(lab), ptr(tgt), G * N, N, ncls, ld,
                                         float(scale), ptr(loss), ptr(d), ptr(correct), stream()),
           "ce_fwd_bwd")
     return loss, d, correct
@@ -982,10 +1045,12 @@ def cross_entropy(logits, labels=None, targets=None, ncls=None, scale=1.0, want_
 HEAD_FUSED = __import__("os").environ.get("DDL_FUSED_HEAD", "1") != "0"
 
 
-def head_train_ok(C: int, ncls: int) -> bool:
+def head_train_ok(C: int, ncls: int, dtype=torch.bfloat16) -> bool:
     """Shapes the fused classifier head (``head_train``) takes: 8-channel chunks that tile a
     256-thread block, at most 64 classes (one lane per class), class rows of W that fit 32 KiB
-    of LDS."""
+    of LDS (fp32 activations: ``functional_f32.head_train_ok``)."""
+    if dtype == torch.float32:
+        return F32.head_train_ok(C, ncls)
     return C % 8 == 0 and 256 % (C // 8) == 0 and 1 <= ncls <= 64 and ncls * C * 2 <= 32 * 1024
 
 
@@ -997,6 +1062,8 @@ def head_train(x, w, b, labels, ncls: int, scale: float, dw, db, bn=None, with_c
     None, dw / db: fp32 gradient views of the same shapes. bn = (c, mean, rstd) of the BatchNorm
     whose relu output x is: dx is masked by (x > 0) and the BN's backward sums come back as part
     (as ``avgpool_bwd_bn``). -> (loss[G], correct[G] | None, dx bf16, part | None)."""
+    if F32.is_f32(x):
+        return F32.head_train(x, w, b, labels, ncls, scale, dw, db, bn=bn, with_correct=with_correct)
     G, N, H, W, C = x.shape
     HW = H * W
     Kp = w.shape[1]
@@ -1018,7 +1085,7 @@ def head_train(x, w, b, labels, ncls: int, scale: float, dw, db, bn=None, with_c
             db.reshape(G, Kp)[:, :ncls] += dl.sum(1)
         dp = torch.einsum("gnk,gkc->gnc", dl, w2[:, :ncls]) / HW
         if bn is None:
-            dx = dp[:, :, None, None, :].expand(G, N, H, W, C).to(torch.bfloat16).contiguous()
+            dx = dp[:, :, None, None, :].expand(G, N, H, W, C).to(x.dtype).contiguous()
             return loss, correct, dx, None
         dx, part = _head_pool_bwd_bn_ref(dp, x, bn)
         return loss, correct, dx, part
@@ -1051,7 +1118,7 @@ def _head_pool_bwd_bn_ref(dp, x, bn):
     c, mean, rstd = bn
     G, N, H, W, C = x.shape
     d = dp.reshape(G, N, 1, 1, C) * (x.float() > 0)
-    dx = d.to(torch.bfloat16).contiguous()
+    dx = d.to(x.dtype).contiguous()
     xh = (c.float() - mean.reshape(G, 1, 1, 1, C)) * rstd.reshape(G, 1, 1, 1, C)
     part = torch.zeros(G, BN_STRIPES, 2, C)
     df = dx.float()
@@ -1082,8 +1149,9 @@ def sgd_direct_step(p, g, shadow, dmap, lr: float, grad_scale: float = 1.0):
     if not p.is_cuda:
         ref.sgd_direct(p, g, shadow, dmap, lr, grad_scale)
         return
-    assert p.dim() == 2 and p.is_contiguous() and g.is_contiguous() and shadow.is_contiguous()
-    assert p.shape == g.shape == shadow.shape and p.shape[1] % 16 == 0
+    assert p.dim() == 2 and p.is_contiguous() and g.is_contiguous()
+    assert shadow is None or (shadow.is_contiguous() and shadow.shape == p.shape)
+    assert p.shape == g.shape and p.shape[1] % 16 == 0
     assert dmap.dtype == torch.uint8 and dmap.numel() == p.shape[1] // 16 and dmap.is_cuda
     a = _lib.SGDDirectArgs()
     a.p, a.g, a.shadow, a.dmap = ptr(p), ptr(g), ptr(shadow), ptr(dmap)

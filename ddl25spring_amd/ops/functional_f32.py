@@ -1,0 +1,365 @@
+"""Reference-precision (fp32) device ops: ctypes front-ends of conv_f32.hip and bn_f32.hip.
+
+``ops.functional`` dispatches here for CUDA tensors of dtype float32 (the fp32 precision mode, see
+``models.params.default_precision``); the op signatures and semantics are those of the bf16 ops,
+with three differences of representation:
+  * BN statistics and BN-backward partial sums are per-tile / per-block *slots* ``[G, S, 2, C]``
+    written with plain stores (S depends on the producer's launch), folded in a fixed order — the
+    whole fp32 step is deterministic, with no zero-fill launches;
+  * a conv's forward statistics buffer is a :class:`SlotStats` holder that the conv fills;
+  * ``in_bn=(scale, shift)``: the X operand of FWD / WGRAD is relu(x * scale + shift) computed on
+    the fly (operand-side BatchNorm), so a BN+ReLU output that only feeds a conv is never stored.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+
+import torch
+
+from . import _lib
+from . import workspace as ws
+from ._lib import check, ptr, stream
+
+F_FWD, F_DGRAD, F_WGRAD = 0, 1, 2
+# split-K workspace (floats) per device: partial slices of small-grid FWD / DGRAD / WGRAD
+WS_CAP = 1 << 26
+_WS: dict = {}
+# workgroups a launch should provide before split-K stops (256 CUs, ~2 resident per CU)
+TARGET_WG = int(os.environ.get("DDL_F32_TARGET_WG", "640"))
+
+
+def is_f32(t) -> bool:
+    return t is not None and t.is_cuda and t.dtype == torch.float32
+
+
+class SlotStats:
+    """Forward BN statistics of an fp32 conv: ``t`` = [G, slots, 2, C] once the conv has run."""
+    __slots__ = ("t",)
+
+    def __init__(self):
+        self.t = None
+
+
+def workspace(device) -> torch.Tensor | None:
+    key = str(device)
+    b = _WS.get(key)
+    if b is None:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        b = torch.empty(WS_CAP, dtype=torch.float32, device=device)
+        _WS[key] = b
+    return b
+
+
+def _dims(mode, g):
+    """(Pd, Qd, Kr, phases) of a launch (DGRAD stride 2: the largest phase)."""
+    if mode == F_FWD:
+        return g.K, g.N * g.P * g.Q, g.R * g.S * g.C, 1
+    if mode == F_DGRAD:
+        if g.stride == 2:
+            hs, wsz = (g.H + 1) // 2, (g.W + 1) // 2
+            rn, sn = (g.R + 1) // 2, (g.S + 1) // 2
+            return g.C, g.N * hs * wsz, rn * sn * g.K, 4
+        return g.C, g.N * g.H * g.W, g.R * g.S * g.K, 1
+    return g.K, g.R * g.S * g.C, g.N * g.P * g.Q, 1
+
+
+def cfg_of(bp: int, bq: int) -> int:
+    return (bp // 16) | ((bq // 16) << 8)
+
+
+_PLANS: dict = {}
+_OVERRIDE: dict = {}
+
+
+def set_plan(mode: int, geom, bp: int, bq: int, split: int) -> None:
+    """Pin a launch plan (tile BP x BQ, split-K slices) for one (mode, geometry) — the tuner."""
+    _OVERRIDE[(mode, geom)] = (cfg_of(bp, bq), int(split))
+    _PLANS.pop((mode, geom), None)
+
+
+def plan(mode: int, geom) -> tuple[int, int]:
+    """(cfg, split) heuristic: 128-wide tiles where the dimension allows, then split-K until the
+    grid has ~TARGET_WG workgroups (each slice keeping >= 8 reduction steps)."""
+    key = (mode, geom)
+    p = _PLANS.get(key)
+    if p is not None:
+        return p
+    p = _OVERRIDE.get(key)
+    if p is None:
+        Pd, Qd, Kr, nph = _dims(mode, geom)
+        bp = 128 if Pd > 64 else 64
+        bq = 128 if Qd > 64 else 64
+        tiles = -(-Pd // bp) * -(-Qd // bq) * nph * geom.G
+        nk = -(-Kr // 16)
+        split = 1
+        while tiles * split < TARGET_WG and nk >= split * 2 * 8 and split < 64:
+            split *= 2
+        p = (cfg_of(bp, bq), split)
+    _PLANS[key] = p
+    return p
+
+
+def _args(geom, **kw) -> _lib.ConvF32Args:
+    a = _lib.ConvF32Args()
+    a.gscale = 1.0
+    for k, v in kw.items():
+        setattr(a, k, v)
+    a.G, a.N, a.H, a.W, a.C, a.K = geom.G, geom.N, geom.H, geom.W, geom.C, geom.K
+    a.R, a.S, a.P, a.Q, a.stride, a.pad = geom.R, geom.S, geom.P, geom.Q, geom.stride, geom.pad
+    return a
+
+
+def _gs(t) -> int:
+    return 0 if t is None else t.stride(0)
+
+
+def _launch(a, mode: int, geom, device, split_k: int = 0) -> None:
+    lib = _lib.kernels()
+    cfg, split = plan(mode, geom)
+    if split_k:
+        split = split_k
+    a.split_k = split
+    if split > 1:
+        need = lib.ddl_convf32_workspace(ctypes.byref(a), mode, cfg)
+        buf = workspace(device)
+        if buf is None or need > buf.numel():
+            a.split_k = split = 1
+        else:
+            a.partial, a.partial_cap = buf.data_ptr(), buf.numel()
+    check(lib.ddl_convf32(ctypes.byref(a), mode, cfg, stream()), ("conv_fwd", "conv_dgrad", "conv_wgrad")[mode] + "_f32")
+
+
+def _slots(a, mode: int, geom) -> int:
+    cfg, _ = plan(mode, geom)
+    return int(_lib.kernels().ddl_convf32_slots(ctypes.byref(a), mode, cfg))
+
+
+def _xform(in_bn):
+    if in_bn is None:
+        return {}
+    sc, sh = in_bn
+    assert sc.is_contiguous() and sh.is_contiguous()
+    return dict(in_scale=ptr(sc), in_shift=ptr(sh), in_relu=1)
+
+
+def conv_fwd(x, w, geom, bias=None, relu=False, stats=None, out=None, residual=None, in_bn=None, split_k=0):
+    y = out if out is not None else torch.empty(geom.G, geom.N, geom.P, geom.Q, geom.K, dtype=torch.float32,
+                                                device=x.device)
+    if residual is not None and (residual.stride(0) != y.stride(0) or not residual.is_contiguous()):
+        residual = residual.contiguous()
+    a = _args(geom, x=ptr(x), w=ptr(w), out=ptr(y), bias=ptr(bias), residual=ptr(residual),
+              x_gs=_gs(x), w_gs=_gs(w), out_gs=_gs(y), bias_gs=_gs(bias), relu=int(bool(relu)), **_xform(in_bn))
+    if stats is not None:
+        st = torch.empty(geom.G, _slots(a, F_FWD, geom), 2, geom.K, dtype=torch.float32, device=x.device)
+        a.stats = ptr(st)
+        if isinstance(stats, SlotStats):
+            stats.t = st
+        else:
+            raise TypeError("fp32 conv statistics go to a SlotStats (Fn.stats_buffer(..., like=x))")
+    _launch(a, F_FWD, geom, x.device, split_k)
+    return y
+
+
+def conv_dgrad(dy, w, geom, residual=None, mask=None, out=None, bn=None, mask_bn=None, residual_sub=1,
+               split_k=0):
+    dx = out if out is not None else torch.empty(geom.G, geom.N, geom.H, geom.W, geom.C, dtype=torch.float32,
+                                                 device=dy.device)
+    kw = {}
+    if residual is not None:
+        if residual_sub == 2:
+            want = (geom.G, geom.N, (geom.H + 1) // 2, (geom.W + 1) // 2, geom.C)
+            assert tuple(residual.shape) == want, (tuple(residual.shape), want)
+            residual = residual.contiguous()
+            kw.update(res_sub=2, res_gs=residual.stride(0))
+        elif residual.stride(0) != dx.stride(0) or not residual.is_contiguous():
+            residual = residual.contiguous()
+    if mask is not None and (mask.stride(0) != dx.stride(0) or not mask.is_contiguous()):
+        mask = mask.contiguous()
+    if bn is not None:
+        x, mean, rstd = bn
+        assert x.is_contiguous() and x.stride(0) == dx.stride(0) and mean.is_contiguous() and rstd.is_contiguous()
+        kw.update(bn_x=ptr(x), bn_mean=ptr(mean), bn_rstd=ptr(rstd))
+        if mask_bn is not None:
+            sc, sh = mask_bn
+            assert sc.is_contiguous() and sh.is_contiguous() and sc.numel() == geom.G * geom.C
+            kw.update(mask_scale=ptr(sc), mask_shift=ptr(sh))
+    a = _args(geom, w=ptr(w), dy=ptr(dy), out=ptr(dx), residual=ptr(residual), mask=ptr(mask),
+              w_gs=_gs(w), dy_gs=_gs(dy), out_gs=_gs(dx), **kw)
+    part = None
+    if bn is not None:
+        part = torch.empty(geom.G, _slots(a, F_DGRAD, geom), 2, geom.C, dtype=torch.float32, device=dy.device)
+        a.stats = ptr(part)
+    _launch(a, F_DGRAD, geom, dy.device, split_k)
+    return dx if bn is None else (dx, part)
+
+
+def conv_wgrad(dy, x, geom, dw, accumulate=True, gscale=1.0, in_bn=None, split_k=0):
+    if not accumulate and gscale != 1.0:
+        raise ValueError("a scaled WGRAD must accumulate (it adds into the master weights)")
+    a = _args(geom, x=ptr(x), dy=ptr(dy), out=ptr(dw), x_gs=_gs(x), dy_gs=_gs(dy), out_gs=_gs(dw),
+              accumulate=int(bool(accumulate)), gscale=float(gscale), **_xform(in_bn))
+    _launch(a, F_WGRAD, geom, dy.device, split_k)
+    return dw
+
+
+# --------------------------------------------------------------------------------------- BN
+def _bnf_args(stats, gamma, beta, running_mean, running_var, count, eps, momentum, training, outs, G, C):
+    a = _lib.BNArgs()
+    a.stats, a.gamma, a.beta = ptr(stats), ptr(gamma), ptr(beta)
+    a.running_mean, a.running_var = ptr(running_mean), ptr(running_var)
+    a.scale, a.shift, a.mean, a.rstd = (ptr(outs[i]) for i in range(4))
+    a.gs_param = _gs(gamma) if gamma is not None else _gs(beta)
+    a.gs_buf = _gs(running_mean)
+    a.G, a.C, a.count = G, C, int(count)
+    a.eps, a.momentum, a.training = float(eps), float(momentum), int(training)
+    a.stripes = stats.shape[1] if stats is not None else 0
+    return a
+
+
+def bn_finalize_many(items, eps=1e-5, momentum=0.1, training=True):
+    """items: [(stats SlotStats | tensor | None, gamma, beta, running_mean, running_var, count, G, C), ...]
+    (one or two BatchNorms, one launch) -> [(scale, shift, mean, rstd), ...]."""
+    dev = items[0][1].device if items[0][1] is not None else items[0][3].device
+    args, outs = [], []
+    for stats, gamma, beta, rm, rv, count, G, C in items:
+        t = stats.t if isinstance(stats, SlotStats) else stats
+        if training:
+            assert t is not None and t.is_contiguous(), "fp32 BN statistics missing (conv not run?)"
+        o = torch.empty(4, G, C, dtype=torch.float32, device=dev)
+        args.append(_bnf_args(t if training else None, gamma, beta, rm, rv, count, eps, momentum, training, o, G, C))
+        outs.append(o)
+    b = ctypes.byref(args[1]) if len(args) > 1 else None
+    check(_lib.kernels().ddl_bnf_finalize(ctypes.byref(args[0]), b, stream()), "bn_finalize_f32")
+    return [(o[0], o[1], o[2], o[3]) for o in outs]
+
+
+def bn_apply(x, scale, shift, r=None, rscale=None, rshift=None, act=0, out=None):
+    assert x.is_contiguous() and (r is None or r.is_contiguous())
+    y = out if out is not None else torch.empty_like(x)
+    G, C = x.shape[0], x.shape[-1]
+    check(_lib.kernels().ddl_bnf_apply(ptr(x), ptr(scale), ptr(shift), ptr(r), ptr(rscale), ptr(rshift), ptr(y),
+                                       x[0].numel(), C, G, act, stream()), "bn_apply_f32")
+    return y
+
+
+def reduce_slots(M: int, C: int, G: int) -> int:
+    return int(_lib.kernels().ddl_bnf_reduce_slots(int(M), int(C), int(G)))
+
+
+def bn_bwd_reduce_part(dy, ymask, x, mean, rstd):
+    G, C = x.shape[0], x.shape[-1]
+    M = x[0].numel() // C
+    part = torch.empty(G, reduce_slots(M, C, G), 2, C, dtype=torch.float32, device=x.device)
+    check(_lib.kernels().ddl_bnf_reduce(ptr(dy), ptr(ymask), ptr(x), ptr(mean), ptr(rstd), ptr(part), M, C, G,
+                                        stream()), "bn_bwd_reduce_f32")
+    return part
+
+
+def bn_stats(x):
+    G, C = x.shape[0], x.shape[-1]
+    M = x[0].numel() // C
+    st = SlotStats()
+    st.t = torch.empty(G, reduce_slots(M, C, G), 2, C, dtype=torch.float32, device=x.device)
+    check(_lib.kernels().ddl_bnf_stats(ptr(x), ptr(st.t), M, C, G, stream()), "bn_stats_f32")
+    return st
+
+
+def _bwd_args(x, mean, rstd, gamma, dgamma, dbeta, part, dx):
+    G, C = x.shape[0], x.shape[-1]
+    t = _lib.BNFBwdArgs()
+    coef = ws.scratch((G, 3, C), x.device)
+    gs = _gs(gamma) if gamma is not None else 0
+    if dgamma is not None or dbeta is not None:
+        gd = _gs(dgamma) if dgamma is not None else _gs(dbeta)
+        assert gamma is None or gd == gs, "gamma and its gradient must share the group stride"
+        gs = gd
+    t.x, t.mean, t.rstd, t.gamma = ptr(x), ptr(mean), ptr(rstd), ptr(gamma)
+    t.dgamma, t.dbeta, t.part, t.coef, t.dx, t.gs_param = ptr(dgamma), ptr(dbeta), ptr(part), ptr(coef), ptr(dx), gs
+    t.slots = part.shape[1] if part is not None else 0
+    t._keep = coef  # the scratch must outlive the launch (its memory would be reused otherwise)
+    return t
+
+
+def bn_backward(dy, ymask, x, mean, rstd, gamma, dgamma=None, dbeta=None, emit_dym=False, part=None):
+    G, C = x.shape[0], x.shape[-1]
+    M = x[0].numel() // C
+    assert dy.is_contiguous() and x.is_contiguous()
+    do_reduce = part is None
+    if do_reduce:
+        part = torch.empty(G, reduce_slots(M, C, G), 2, C, dtype=torch.float32, device=x.device)
+    dx = torch.empty_like(x)
+    dym = torch.empty_like(x) if emit_dym else None
+    a = _bwd_args(x, mean, rstd, gamma, dgamma, dbeta, part, dx)
+    check(_lib.kernels().ddl_bnf_backward(ptr(dy), ptr(ymask), ctypes.byref(a), None, ptr(dym), M, C, G,
+                                          int(do_reduce), stream()), "bn_backward_f32")
+    return (dx, dym) if emit_dym else dx
+
+
+def bn_backward2(dy, bn_a, bn_b):
+    """bn_* = (x, mean, rstd, gamma, dgamma, dbeta, part) -> (dx_a, dx_b); dy already masked."""
+    xa = bn_a[0]
+    G, C = xa.shape[0], xa.shape[-1]
+    M = xa[0].numel() // C
+    assert bn_b[0].shape == xa.shape and dy.is_contiguous()
+    outs, args = [], []
+    for x, mean, rstd, gamma, dgamma, dbeta, part in (bn_a, bn_b):
+        dx = torch.empty_like(x)
+        args.append(_bwd_args(x, mean, rstd, gamma, dgamma, dbeta, part, dx))
+        outs.append(dx)
+    check(_lib.kernels().ddl_bnf_backward(ptr(dy), None, ctypes.byref(args[0]), ctypes.byref(args[1]), None, M, C,
+                                          G, 0, stream()), "bn_backward2_f32")
+    return outs[0], outs[1]
+
+
+def avgpool_bwd_bn(dy, x, bn):
+    c, mean, rstd = bn
+    G, N, H, W, C = x.shape
+    assert x.is_contiguous() and c.is_contiguous() and dy.is_contiguous()
+    dx = torch.empty_like(x)
+    part = torch.empty(G, reduce_slots(N * H * W, C, G), 2, C, dtype=torch.float32, device=x.device)
+    check(_lib.kernels().ddl_avgpoolf_bwd_bn(ptr(dy), ptr(x), ptr(c), ptr(mean), ptr(rstd), ptr(dx), ptr(part),
+                                             G, N, H * W, C, stream()), "avgpool_bwd_bn_f32")
+    return dx, part
+
+
+def head_train_ok(C: int, ncls: int) -> bool:
+    return C % 4 == 0 and C // 4 <= 256 and 256 % (C // 4) == 0 and 1 <= ncls <= 64 and \
+        (2 * C + 64 + 2048 + ncls * C) * 4 <= 64 * 1024
+
+
+def head_train(x, w, b, labels, ncls: int, scale: float, dw, db, bn=None, with_correct=False):
+    G, N, H, W, C = x.shape
+    dev = x.device
+    assert x.is_contiguous() and labels.is_contiguous() and head_train_ok(C, ncls)
+    loss = torch.empty(G, dtype=torch.float32, device=dev)
+    correct = torch.empty(G, dtype=torch.int32, device=dev) if with_correct else None
+    dx = torch.empty_like(x)
+    a = _lib.HeadFArgs()
+    a.x, a.w, a.b, a.labels = ptr(x), ptr(w), ptr(b), ptr(labels)
+    a.loss, a.correct, a.dw, a.db, a.dx = ptr(loss), ptr(correct), ptr(dw), ptr(db), ptr(dx)
+    a.w_gs, a.dw_gs = _gs(w), _gs(dw)
+    a.b_gs, a.db_gs = (_gs(b), _gs(db)) if b is not None else (0, 0)
+    part = None
+    if bn is not None:
+        c, mean, rstd = bn
+        assert c.is_contiguous() and mean.is_contiguous() and rstd.is_contiguous()
+        part = torch.empty(G, N, 2, C, dtype=torch.float32, device=dev)
+        a.c, a.mean, a.rstd, a.part = ptr(c), ptr(mean), ptr(rstd), ptr(part)
+    pooled = torch.empty(G, N, C, dtype=torch.float32, device=dev)
+    dlog = torch.empty(G, N, 64, dtype=torch.float32, device=dev)
+    rl = torch.empty(G, N, dtype=torch.float32, device=dev)
+    rh = torch.empty(G, N, dtype=torch.int32, device=dev)
+    a.pooled, a.dlog, a.row_loss, a.row_hit = ptr(pooled), ptr(dlog), ptr(rl), ptr(rh)
+    a.G, a.N, a.HW, a.C, a.ncls, a.scale = G, N, H * W, C, ncls, float(scale)
+    check(_lib.kernels().ddl_headf_train(ctypes.byref(a), stream()), "head_train_f32")
+    return loss, correct, dx, part
+
+
+def conv_flops(geom) -> int:
+    return 2 * geom.G * geom.N * geom.P * geom.Q * geom.K * geom.R * geom.S * geom.C
+
+
+__all__ = [n for n in dir() if not n.startswith("_") and n not in ("ctypes", "math", "os", "torch")]

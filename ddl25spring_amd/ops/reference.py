@@ -7,12 +7,27 @@ layout contract as the kernels: NHWC activations with a leading client-group dim
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 import torch.nn.functional as F
 
+# activation storage dtype of the CPU path: bf16 (mirrors the device numerics) or fp32 (a net in
+# the fp32 precision mode runs its CPU ops inside ``storage(torch.float32)``)
+_STORAGE = [torch.bfloat16]
+
 
 def _bf(t: torch.Tensor) -> torch.Tensor:
-    return t.to(torch.bfloat16)
+    return t.to(_STORAGE[-1])
+
+
+@contextlib.contextmanager
+def storage(dtype):
+    _STORAGE.append(dtype)
+    try:
+        yield
+    finally:
+        _STORAGE.pop()
 
 
 def nhwc_to_nchw(x: torch.Tensor) -> torch.Tensor:

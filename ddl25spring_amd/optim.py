@@ -43,6 +43,10 @@ class _Base:
         g0, g1 = self._g
         return t[g0:g1]
 
+    def _shadow_rows(self):
+        sh = self.store.shadow16
+        return None if sh is None else self._rows(sh)
+
 
 class SGD(_Base):
     def __init__(self, params, lr: float, momentum: float = 0.0, dampening: float = 0.0,
@@ -56,7 +60,7 @@ class SGD(_Base):
     def step(self, grad_scale: float = 1.0):
         st = self.store
         Fn.sgd_step(self._rows(st.data), self._rows(st.grad),
-                    None if self.mom is None else self._rows(self.mom), self._rows(st.shadow),
+                    None if self.mom is None else self._rows(self.mom), self._shadow_rows(),
                     self.lr, self.weight_decay, self.momentum, self.dampening, self.nesterov,
                     first_step=(self.steps == 0), grad_scale=grad_scale)
         st._shadow_version = st.data._version
@@ -65,10 +69,13 @@ class SGD(_Base):
     def step_direct(self, grad_scale: float = 1.0):
         """Finish a step whose conv-weight part the backward already applied
         (``ParamStore.direct_update``): shadow refresh for those, plain SGD + gradient zeroing for
-        the rest, in one launch. Only for momentum- and weight-decay-free SGD."""
+        the rest, in one launch. Only for momentum- and weight-decay-free SGD, unscaled gradients
+        (the WGRAD launches already added the unscaled ``-lr * dW``)."""
         assert self.mom is None and self.weight_decay == 0.0
+        if grad_scale != 1.0:
+            raise ValueError("step_direct: the direct columns were stepped unscaled inside the backward")
         st = self.store
-        Fn.sgd_direct_step(self._rows(st.data), self._rows(st.grad), self._rows(st.shadow),
+        Fn.sgd_direct_step(self._rows(st.data), self._rows(st.grad), self._shadow_rows(),
                            st.direct_map, self.lr, grad_scale)
         st._shadow_version = st.data._version
         self.steps += 1
@@ -94,7 +101,7 @@ class Adam(_Base):
         self.t += 1
         st = self.store
         Fn.adam_step(self._rows(st.data), self._rows(st.grad), self._rows(self.m), self._rows(self.v),
-                     self._rows(st.shadow), self.lr, self.betas[0], self.betas[1], self.eps,
+                     self._shadow_rows(), self.lr, self.betas[0], self.betas[1], self.eps,
                      self.weight_decay, self.t, self.decoupled, grad_scale)
         st._shadow_version = st.data._version
 

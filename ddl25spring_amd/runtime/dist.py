@@ -33,13 +33,15 @@ class DistContext:
 
     @property
     def is_distributed(self) -> bool:
-        return self.world > 1 and dist.is_initialized()
+        return (self.world > 1 or self.forced_pg) and dist.is_initialized()
 
     @property
     def is_main(self) -> bool:
         return self.rank == 0
 
     # ------------------------------------------------------------- collectives (no-ops at world 1)
+    forced_pg: bool = False     # a process group even at world 1 (RCCL code-path rehearsal)
+
     def all_reduce(self, t: torch.Tensor, op=None, group=None):
         if self.is_distributed:
             if (self.ipc is not None and group is None and op in (None, dist.ReduceOp.SUM)
@@ -68,6 +70,12 @@ class DistContext:
         else:
             out.copy_(t)
         return out
+
+    def check_comm(self):
+        """Surface a peer-read all-reduce barrier timeout (sticky device error word) as an exception;
+        called at round / sync boundaries (it synchronises the device)."""
+        if self.ipc is not None:
+            self.ipc.check()
 
     def barrier(self):
         if self.is_distributed:
@@ -117,6 +125,9 @@ def init(backend: str | None = None, device: str | None = None, rank: int | None
     local = int(os.environ.get("LOCAL_RANK", rank))
     want_gpu = device != "cpu" and (device is not None and device.startswith("cuda") or
                                     (device is None and torch.cuda.is_available()))
+    # DDL_FORCE_PG=1: create the process group even at world 1, so the collective code paths
+    # (init_process_group(device_id=), barrier(device_ids=), device scalars, bucket hooks) run
+    forced = os.environ.get("DDL_FORCE_PG", "0") == "1" and world == 1
     if want_gpu:
         ndev = torch.cuda.device_count()
         dev = torch.device("cuda", local % max(ndev, 1))
@@ -128,7 +139,7 @@ def init(backend: str | None = None, device: str | None = None, rank: int | None
             local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
             torch.set_num_threads(max(1, (os.cpu_count() or 1) // local_world))
     backend = backend or ("nccl" if dev.type == "cuda" else "gloo")
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or forced) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         kw = {}
@@ -136,7 +147,8 @@ def init(backend: str | None = None, device: str | None = None, rank: int | None
             kw["device_id"] = dev
         dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
-    _CTX = DistContext(rank, world, local, dev, backend if world > 1 else "none")
+    _CTX = DistContext(rank, world, local, dev, backend if (world > 1 or forced) else "none",
+                       forced_pg=forced)
     # peer-read all-reduce for small messages (runtime/ipc.py): one node, RCCL backend, opt-in
     # until measured against RCCL on a multi-GPU node (benchmarks/bench_comm.py)
     if (world > 1 and backend == "nccl" and os.environ.get("DDL_IPC_ALLREDUCE", "0") == "1"
@@ -154,7 +166,8 @@ def context() -> DistContext:
 def shutdown():
     global _CTX
     if _CTX is not None and _CTX.ipc is not None:
-        _CTX.ipc.close()
+        _CTX.ipc.check()
+        _CTX.ipc.close()  # collective: barrier before unmapping
     if dist.is_initialized():
         dist.destroy_process_group()
     _CTX = None

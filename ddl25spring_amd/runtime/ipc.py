@@ -126,8 +126,12 @@ class IpcAllReduce:
         if int(self.err.item()):
             raise RuntimeError("ipc all_reduce: a peer did not arrive within the barrier timeout")
 
-    def close(self):
+    def close(self, group=None):
+        """Collective: every rank's last kernel may still be reading MY buffer, so unmap and free only
+        after all ranks have drained their device (synchronize + barrier)."""
         torch.cuda.synchronize(self.device)
+        if self.world > 1 and dist.is_initialized():
+            dist.barrier(group=group)
         for p in self._opened:
             self.lib.ddl_ipc_close(p)
         self._opened = []

@@ -2,6 +2,8 @@
 plus a check that the in-tree HIP library is what ran."""
 from __future__ import annotations
 
+import os
+
 import torch
 
 
@@ -18,8 +20,10 @@ def run_smoke():
     train = synthetic_images("cifar10", 400, seed=0)
     data = DeviceImageDataset(train, ctx.device)
     parts = split(2, True, 0, labels=train.labels)
-    fl = FedAvg(resnet18_cifar, data, parts, lr=0.01, batch_size=50, local_epochs=1,
-                client_fraction=1.0, seed=0, eval_every=0, use_graph=True)
+    # the headline's reference-precision (fp32) path; DDL_SMOKE_PRECISION=bf16 for the bf16 one
+    prec = os.environ.get("DDL_SMOKE_PRECISION", "fp32")
+    fl = FedAvg(lambda groups: resnet18_cifar(10, groups=groups, precision=prec), data, parts, lr=0.01,
+                batch_size=50, local_epochs=1, client_fraction=1.0, seed=0, eval_every=0, use_graph=True)
     w0 = fl.w_global.clone()
     dt, samples = fl.round()
     torch.cuda.synchronize()
@@ -29,7 +33,7 @@ def run_smoke():
     assert delta > 0 and delta == delta, "weights did not move"
     libs = _lib.loaded_library_paths()
     assert any("libddl_kernels.so" in p for p in libs), libs
-    print(f"[smoke] resnet18 fedavg round ok: {samples} samples in {dt*1e3:.1f} ms, "
+    print(f"[smoke] resnet18 ({prec}) fedavg round ok: {samples} samples in {dt*1e3:.1f} ms, "
           f"loss={loss.tolist()}, max|dw|={delta:.3e}, native libs={libs}")
 
 
