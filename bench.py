@@ -58,7 +58,12 @@ def main():
                          "ranks share one GPU for a functional rehearsal")
     ap.add_argument("--precision", default="fp32", choices=("fp32", "bf16"),
                     help="compute precision (fp32 = the reference's; bf16 = bf16 MFMA / activations)")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="require a bitwise-reproducible run (the fp32 path: no float atomics; two runs "
+                         "print the same w_global_sha256)")
     args = ap.parse_args()
+    if args.deterministic and args.precision != "fp32":
+        ap.error("--deterministic needs --precision fp32 (the bf16 path reduces with float atomics)")
 
     from ddl25spring_amd.runtime import dist as rdist
     ctx = rdist.init(backend=args.backend)

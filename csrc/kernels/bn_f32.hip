@@ -681,3 +681,29 @@ DDL_API int ddl_headf_train(const HeadFArgs* ap, hipStream_t s) {
   hipLaunchKernelGGL(headf_wgrad_kernel, dim3((a.C + 63) / 64, a.G), dim3(256), 0, s, a);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// Deterministic per-channel column sum (bias gradients): out[g][c] (+ g * gs) += sum_m x[g][m][c]
+// via per-block slots (bnf_reduce_kernel<1>) and a fixed-order fold — the fp32 twin of
+// nn_ops.hip's atomic channel_sum.
+__global__ __launch_bounds__(256) void bnf_colsum_fold_kernel(const float* __restrict__ part, int S, float* out,
+                                                              long long gs, int C) {
+  __shared__ double red[8 * 64];
+  const int g = blockIdx.y, c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const bool valid = c < C;
+  double s0, s1;
+  slot_fold(part + (long long)g * S * 2 * C, S, C, c, valid, red, s0, s1);
+  if ((threadIdx.x >> 5) == 0 && valid) out[(long long)g * gs + c] += (float)s0;
+}
+
+// part: scratch [G][S][2][C], S = ddl_bnf_reduce_slots(M, C, G)
+DDL_API int ddl_bnf_channel_sum(const float* x, float* out, long long gs, float* part, long long M, int C, int G,
+                                hipStream_t s) {
+  const int S = ddl_bnf_reduce_slots(M, C, G);
+  if (S < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bnf_reduce_kernel<1>, dim3(S, G), dim3(256), 0, s, (const float*)nullptr,
+                     (const float*)nullptr, x, (const float*)nullptr, (const float*)nullptr, part, M, C);
+  hipLaunchKernelGGL(bnf_colsum_fold_kernel, dim3((C + 31) / 32, G), dim3(256), 0, s, (const float*)part, S, out,
+                     gs, C);
+  return (int)hipGetLastError();
+}

@@ -402,7 +402,23 @@ __global__ __launch_bounds__(256, 2) void convf32_kernel(ConvF32Args a) {
   const FDiv dpix = mk_fdiv((uint32_t)(P * Q)), dpq1 = mk_fdiv((uint32_t)Q);
 
   // ----------------------------------------------------------- global -> registers (step kt)
+  // Raw buffer loads through per-group descriptors: an invalid element (padding tap, tile
+  // overhang, past the last reduction index) gets an offset beyond the descriptor's range and
+  // reads as zero — no branches around the loads. The operand-side BN is applied at LDS-store
+  // time (after the step's MFMAs), so it never waits on the loads it transforms.
+  constexpr unsigned OOB = 0xFFFFFFF0u;
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)X, 0, (int)((long long)a.N * H * W * C * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)Wt, 0, (int)((long long)K * a.R * S * C * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)DY, 0, (int)((long long)a.N * P * Q * K * 4), 0x00020000);
+  auto bload = [&](const __amdgpu_buffer_rsrc_t& rs, unsigned off) -> float4 {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    return __builtin_bit_cast(float4, v);
+  };
   float4 rp[2], rq[2];
+  bool qv[2] = {false, false};  // Q units holding real (in-image) X data: the BN transform applies
   auto load_step = [&](int kt) {
     const int kk0 = kt * FBK;
     // P operand
@@ -410,8 +426,7 @@ __global__ __launch_bounds__(256, 2) void convf32_kernel(ConvF32Args a) {
 #pragma unroll
       for (int i = 0; i < UPK; ++i) {
         const int p = o.p0 + pk_row[i];
-        rp[i] = p < o.Pd ? *(const float4*)(Wt + (long long)p * o.Kr + kk0 + 4 * pk_ch[i])
-                         : make_float4(0.f, 0.f, 0.f, 0.f);
+        rp[i] = bload(rW, p < o.Pd ? (unsigned)(p * o.Kr + kk0 + 4 * pk_ch[i]) * 4u : OOB);
       }
     } else if constexpr (MODE == F_DGRAD) {
       const int tap = kk0 / K, k0 = kk0 - tap * K;
@@ -421,16 +436,14 @@ __global__ __launch_bounds__(256, 2) void convf32_kernel(ConvF32Args a) {
 #pragma unroll
       for (int j = 0; j < KUP; ++j) {
         const int k = k0 + pm_kp * KUP + j;
-        rp[j] = c < C ? *(const float4*)(Wt + (((long long)k * a.R + r) * S + s) * C + c)
-                      : make_float4(0.f, 0.f, 0.f, 0.f);
+        rp[j] = bload(rW, c < C ? (unsigned)(((k * a.R + r) * S + s) * C + c) * 4u : OOB);
       }
     } else {  // WGRAD: dY rows = channels k
       const int kch = o.p0 + 4 * pm_rg;
 #pragma unroll
       for (int j = 0; j < KUP; ++j) {
         const int pix = kk0 + pm_kp * KUP + j;
-        rp[j] = (pix < o.Kr && kch < K) ? *(const float4*)(DY + (long long)pix * K + kch)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+        rp[j] = bload(rD, (pix < o.Kr && kch < K) ? (unsigned)(pix * K + kch) * 4u : OOB);
       }
     }
     // Q operand
@@ -441,19 +454,8 @@ __global__ __launch_bounds__(256, 2) void convf32_kernel(ConvF32Args a) {
       for (int i = 0; i < UQK; ++i) {
         const int h = qk_hb[i] + r, w = qk_wb[i] + s;
         const bool ok = qk_n[i] >= 0 && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-        const int c = c0 + 4 * qk_ch[i];
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ok) {
-          v = *(const float4*)(X + (((long long)qk_n[i] * H + h) * W + w) * C + c);
-          if (xf) {
-            v.x = v.x * xform[c] + xform[512 + c];
-            v.y = v.y * xform[c + 1] + xform[512 + c + 1];
-            v.z = v.z * xform[c + 2] + xform[512 + c + 2];
-            v.w = v.w * xform[c + 3] + xform[512 + c + 3];
-            if (xrelu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
-          }
-        }
-        rq[i] = v;
+        qv[i] = ok;
+        rq[i] = bload(rX, ok ? (unsigned)(((qk_n[i] * H + h) * W + w) * C + c0 + 4 * qk_ch[i]) * 4u : OOB);
       }
     } else if constexpr (MODE == F_DGRAD) {
       const int tap = kk0 / K, k0 = kk0 - tap * K;
@@ -472,32 +474,29 @@ __global__ __launch_bounds__(256, 2) void convf32_kernel(ConvF32Args a) {
           wo /= st;
         }
         const bool ok = hit && qk_n[i] >= 0 && (unsigned)ho < (unsigned)P && (unsigned)wo < (unsigned)Q;
-        rq[i] = ok ? *(const float4*)(DY + (((long long)qk_n[i] * P + ho) * Q + wo) * K + k0 + 4 * qk_ch[i])
-                   : make_float4(0.f, 0.f, 0.f, 0.f);
+        rq[i] = bload(rD, ok ? (unsigned)(((qk_n[i] * P + ho) * Q + wo) * K + k0 + 4 * qk_ch[i]) * 4u : OOB);
       }
     } else {  // WGRAD: X rows = (r, s, c)
 #pragma unroll
       for (int j = 0; j < KUQ; ++j) {
         const int pix = kk0 + qm_kp * KUQ + j;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (qm_ok && pix < o.Kr) {
-          const int n = fdv(pix, dpix), rem = pix - n * P * Q;
-          const int ho = fdv(rem, dpq1), wo = rem - ho * Q;
-          const int h = ho * st - pd + qm_r, w = wo * st - pd + qm_s;
-          if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
-            v = *(const float4*)(X + (((long long)n * H + h) * W + w) * C + qm_c);
-            if (xf) {
-              v.x = v.x * qm_sc[0] + qm_sh[0];
-              v.y = v.y * qm_sc[1] + qm_sh[1];
-              v.z = v.z * qm_sc[2] + qm_sh[2];
-              v.w = v.w * qm_sc[3] + qm_sh[3];
-              if (xrelu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
-            }
-          }
-        }
-        rq[j] = v;
+        const int n = fdv(pix, dpix), rem = pix - n * P * Q;
+        const int ho = fdv(rem, dpq1), wo = rem - ho * Q;
+        const int h = ho * st - pd + qm_r, w = wo * st - pd + qm_s;
+        const bool ok = qm_ok && pix < o.Kr && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+        qv[j] = ok;
+        rq[j] = bload(rX, ok ? (unsigned)(((n * H + h) * W + w) * C + qm_c) * 4u : OOB);
       }
     }
+  };
+  // operand-side BN of the X operand (FWD / WGRAD): relu(x * scale + shift) on real pixels only
+  auto xform4 = [&](float4 v, const float* sc, const float* sh) {
+    v.x = v.x * sc[0] + sh[0];
+    v.y = v.y * sc[1] + sh[1];
+    v.z = v.z * sc[2] + sh[2];
+    v.w = v.w * sc[3] + sh[3];
+    if (xrelu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+    return v;
   };
   // ----------------------------------------------------------- registers -> LDS image
   auto store_mn = [&](float* img, int rg, int kp, int KU, const float4* v) {
@@ -515,7 +514,7 @@ __global__ __launch_bounds__(256, 2) void convf32_kernel(ConvF32Args a) {
       }
     }
   };
-  auto store_step = [&](int buf) {
+  auto store_step = [&](int buf, int kt) {
     float* Ps = smem + buf * (SP + SQ);
     float* Qs = Ps + SP;
     if constexpr (MODE == F_FWD) {
@@ -523,6 +522,22 @@ __global__ __launch_bounds__(256, 2) void convf32_kernel(ConvF32Args a) {
       for (int i = 0; i < UPK; ++i) *(float4*)(Ps + lds_off(pk_row[i], pk_ch[i])) = rp[i];
     } else {
       store_mn(Ps, pm_rg, pm_kp, KUP, rp);
+    }
+    if constexpr (MODE == F_FWD) {
+      if (xf) {
+        const int kk0 = kt * FBK, c0 = kk0 - (kk0 / C) * C;
+#pragma unroll
+        for (int i = 0; i < UQK; ++i) {
+          const int c = c0 + 4 * qk_ch[i];
+          if (qv[i]) rq[i] = xform4(rq[i], xform + c, xform + 512 + c);
+        }
+      }
+    } else if constexpr (MODE == F_WGRAD) {
+      if (xf) {
+#pragma unroll
+        for (int j = 0; j < KUQ; ++j)
+          if (qv[j]) rq[j] = xform4(rq[j], qm_sc, qm_sh);
+      }
     }
     if constexpr (MODE != F_WGRAD) {
 #pragma unroll
@@ -540,7 +555,7 @@ __global__ __launch_bounds__(256, 2) void convf32_kernel(ConvF32Args a) {
 
   if (kt0 < kt1) {
     load_step(kt0);
-    store_step(0);
+    store_step(0, kt0);
     __syncthreads();
     for (int kt = kt0; kt < kt1; ++kt) {
       const int cur = (kt - kt0) & 1;
@@ -565,7 +580,7 @@ __global__ __launch_bounds__(256, 2) void convf32_kernel(ConvF32Args a) {
             const float bv = s4 == 0 ? bfr[tj].x : s4 == 1 ? bfr[tj].y : s4 == 2 ? bfr[tj].z : bfr[tj].w;
             acc[ti][tj] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[ti][tj], 0, 0, 0);
           }
-      if (more) store_step(cur ^ 1);
+      if (more) store_step(cur ^ 1, kt + 1);
       __syncthreads();
     }
   }
@@ -729,6 +744,11 @@ DDL_API int ddl_convf32(const ConvF32Args* ap, int mode, int cfg, hipStream_t s)
   const ConvF32Args& a = *ap;
   if (a.G < 1 || a.N < 1 || a.C < 1 || a.K < 1 || a.stride < 1) return (int)hipErrorInvalidValue;
   if (a.C > 512 && a.in_scale) return (int)hipErrorInvalidValue;
+  // per-group operands are addressed with 32-bit byte offsets (buffer descriptors)
+  const long long lim = (1LL << 31) - 64;
+  if ((long long)a.N * a.H * a.W * a.C * 4 > lim || (long long)a.K * a.R * a.S * a.C * 4 > lim ||
+      (long long)a.N * a.P * a.Q * a.K * 4 > lim)
+    return (int)hipErrorInvalidValue;
   if (mode == F_FWD) {
     if (a.C % 16 || a.K % 4) return (int)hipErrorInvalidValue;
     return launch_mode<F_FWD>(a, cfg, s);

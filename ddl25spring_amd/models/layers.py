@@ -185,12 +185,14 @@ class ConvUnit(Layer):
                 dc = Fn.act_bwd(y, dy, self.act)
             if self.bias:
                 Fn.channel_sum(dc, st.grad_of(self.b))
+        # DGRAD before WGRAD: in fp32 precision the DGRAD reads the master weight itself, which a
+        # direct-SGD WGRAD (ParamStore.direct_update) steps in place
+        dx = None
+        if self.needs_input_grad:
+            dx = Fn.conv_dgrad(dc, st.shadow_of(self.w), g, mask=x4 if self.mask_input else None)
+            if self.linear:
+                dx = dx.reshape(g.G, g.N, self.cin)
         Fn.conv_wgrad(dc, x4, g, st.grad_of(self.w))
-        if not self.needs_input_grad:
-            return None
-        dx = Fn.conv_dgrad(dc, st.shadow_of(self.w), g, mask=x4 if self.mask_input else None)
-        if self.linear:
-            dx = dx.reshape(g.G, g.N, self.cin)
         return dx
 
     def flops(self, x_shape):

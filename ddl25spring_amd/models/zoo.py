@@ -26,7 +26,7 @@ class LogSoftmaxNet(Net):
         return grad - torch.exp(out) * grad.sum(-1, keepdim=True)
 
 
-def mnist_cnn(groups: int = 1) -> Net:
+def mnist_cnn(groups: int = 1, precision: str | None = None) -> Net:
     conv1 = ConvUnit(32, 32, k=1, stride=1, pad=0, bias=True, act="relu", cin_true=9, fan_in=9)
     conv1.pname = "conv1"
     conv2 = ConvUnit(32, 64, k=3, stride=1, pad=0, bias=True, act="relu")
@@ -38,7 +38,7 @@ def mnist_cnn(groups: int = 1) -> Net:
     layers = [conv1, conv2, MaxPool2(), Dropout(0.25), Flatten(), fc1, Dropout(0.5), fc2]
     return LogSoftmaxNet(layers, groups=groups, num_classes=10,
                          input_spec={"cpad": 32, "im2col": True, "stem_k": 3, "pad": 0},
-                         name="mnist_cnn")
+                         name="mnist_cnn", precision=precision)
 
 
 def mnist_cnn_mapping():
@@ -48,7 +48,7 @@ def mnist_cnn_mapping():
             ("fc2.weight", "fc2.weight", "linear", None), ("fc2.bias", "fc2.bias", "vec", None)]
 
 
-def mnist_mlp(groups: int = 1, hidden=(200, 200), num_classes: int = 10) -> Net:
+def mnist_mlp(groups: int = 1, hidden=(200, 200), num_classes: int = 10, precision: str | None = None) -> Net:
     dims = (784, *hidden, num_classes)
     layers = []
     for i, (a, b) in enumerate(zip(dims[:-1], dims[1:])):
@@ -58,7 +58,7 @@ def mnist_mlp(groups: int = 1, hidden=(200, 200), num_classes: int = 10) -> Net:
         lin.pname = f"layers.{i}"
         layers.append(lin)
     return Net(layers, groups=groups, num_classes=num_classes, input_spec={"cpad": 800, "flat": True},
-               name="mnist_mlp")
+               name="mnist_mlp", precision=precision)
 
 
 def mnist_mlp_mapping(n_layers=3):
@@ -69,7 +69,7 @@ def mnist_mlp_mapping(n_layers=3):
     return m
 
 
-def heart_disease_nn(groups: int = 1, in_features: int = 30) -> Net:
+def heart_disease_nn(groups: int = 1, in_features: int = 30, precision: str | None = None) -> Net:
     """30 -> 64 -> 128 -> 256 -> 2, LeakyReLU, Dropout(0.1) before the last layer."""
     l1 = Linear(in_features, 64, act="leaky_relu")
     l1.pname = "fc1"
@@ -79,7 +79,8 @@ def heart_disease_nn(groups: int = 1, in_features: int = 30) -> Net:
     l3.pname = "fc3"
     l4 = Linear(256, 2)
     l4.pname = "fc4"
-    return Net([l1, l2, l3, Dropout(0.1), l4], groups=groups, num_classes=2, name="heart_disease_nn")
+    return Net([l1, l2, l3, Dropout(0.1), l4], groups=groups, num_classes=2, name="heart_disease_nn",
+               precision=precision)
 
 
 def import_mnist_cnn(net: Net, module) -> None:

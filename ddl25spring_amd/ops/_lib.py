@@ -177,6 +177,7 @@ _SIGS.update({
     "ddl_bnf_backward": [vp, vp, ctypes.POINTER(BNFBwdArgs), ctypes.POINTER(BNFBwdArgs), vp, i64, i32, i32, i32, vp],
     "ddl_avgpoolf_bwd_bn": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp],
     "ddl_headf_train": [ctypes.POINTER(HeadFArgs), vp],
+    "ddl_bnf_channel_sum": [vp, vp, i64, vp, i64, i32, i32, vp],
 })
 _RESTYPES = {"ddl_convf32_slots": ctypes.c_longlong, "ddl_convf32_workspace": ctypes.c_longlong}
 

@@ -400,8 +400,10 @@ def conv_dgrad_wgrad(dy, w, x, geom: ConvGeom, dw, residual=None, mask=None, bn=
     dg = dgeom or geom
     dkw = dict(residual=residual, mask=mask, bn=bn, mask_bn=mask_bn, residual_sub=residual_sub)
     if F32.is_f32(dy) or in_bn is not None:
+        # DGRAD first: in fp32 ``w`` IS the master weight that a direct-SGD WGRAD steps in place
+        dx = conv_dgrad(dy, w, dg, **dkw) if want_dx else None
         conv_wgrad(dy, x, geom, dw, in_bn=in_bn)
-        return conv_dgrad(dy, w, dg, **dkw) if want_dx else None
+        return dx
     if not want_dx or not dy.is_cuda or not PAIR_ENABLED or _WGRAD_SIDE is not None \
             or not autotune.ENABLED:
         conv_wgrad(dy, x, geom, dw)
@@ -903,6 +905,8 @@ def act_bwd(y, dy, act: int, slope=0.01):
 
 def channel_sum(x, out):
     """out[G, C] (view, fp32) += sum over all but first/last dims of x."""
+    if F32.is_f32(x):
+        return F32.channel_sum(x.contiguous(), out)
     if not x.is_cuda:
         ref.channel_sum(x, out)
         return out

@@ -72,6 +72,23 @@ def cfg_of(bp: int, bq: int) -> int:
 
 _PLANS: dict = {}
 _OVERRIDE: dict = {}
+_MODE_NAMES = ("fwd", "dgrad", "wgrad")
+# measured best plans per (mode, geometry) (scripts/conv_f32_tune.py on an MI355X)
+_TUNED_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "f32_plans.json")
+_TUNED: dict | None = None
+
+
+def _tuned(mode: int, g):
+    global _TUNED
+    if _TUNED is None:
+        _TUNED = {}
+        if os.environ.get("DDL_F32_TUNED", "1") != "0" and os.path.exists(_TUNED_PATH):
+            import json
+            with open(_TUNED_PATH) as f:
+                _TUNED = json.load(f).get("plans", {})
+    key = f"{_MODE_NAMES[mode]}:{g.G},{g.N},{g.H},{g.W},{g.C},{g.K},{g.R},{g.S},{g.stride},{g.pad}"
+    p = _TUNED.get(key)
+    return None if p is None else (cfg_of(p[0], p[1]), int(p[2]))
 
 
 def set_plan(mode: int, geom, bp: int, bq: int, split: int) -> None:
@@ -87,7 +104,7 @@ def plan(mode: int, geom) -> tuple[int, int]:
     p = _PLANS.get(key)
     if p is not None:
         return p
-    p = _OVERRIDE.get(key)
+    p = _OVERRIDE.get(key) or _tuned(mode, geom)
     if p is None:
         Pd, Qd, Kr, nph = _dims(mode, geom)
         bp = 128 if Pd > 64 else 64
@@ -323,6 +340,17 @@ def avgpool_bwd_bn(dy, x, bn):
     check(_lib.kernels().ddl_avgpoolf_bwd_bn(ptr(dy), ptr(x), ptr(c), ptr(mean), ptr(rstd), ptr(dx), ptr(part),
                                              G, N, H * W, C, stream()), "avgpool_bwd_bn_f32")
     return dx, part
+
+
+def channel_sum(x, out):
+    """out[G, C] (view, fp32) += per-channel sum of x [G, ..., C]: slots + fixed-order fold."""
+    G, C = x.shape[0], x.shape[-1]
+    M = x[0].numel() // C
+    assert x.is_contiguous()
+    part = torch.empty(G, reduce_slots(M, C, G), 2, C, dtype=torch.float32, device=x.device)
+    check(_lib.kernels().ddl_bnf_channel_sum(ptr(x), ptr(out), _gs(out), ptr(part), M, C, G, stream()),
+          "channel_sum_f32")
+    return out
 
 
 def head_train_ok(C: int, ncls: int) -> bool:

@@ -1,0 +1,118 @@
+"""Offline tuner of the fp32 conv launch plans (tile BP x BQ, split-K) for the ResNet-18 CIFAR layers.
+
+For every conv geometry of ResNet-18 at the headline's client counts (G = 8, 4, 2, 1 clients of
+batch 100) and every mode (FWD / DGRAD / WGRAD) it times each candidate plan with HIP events and
+writes the best to ``ddl25spring_amd/ops/f32_plans.json`` (read by ``functional_f32.plan``), with
+the achieved TF/s against the 157.3 TF/s fp32-MFMA peak.
+
+    python scripts/conv_f32_tune.py --out gpurun_out/f32_plans.json [--groups 8 1]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+from ddl25spring_amd.ops import functional_f32 as F32  # noqa: E402
+from ddl25spring_amd.ops.functional import ConvGeom  # noqa: E402
+
+PEAK_TF = 157.3
+
+
+def resnet18_geoms(G: int, N: int):
+    gs = [ConvGeom(G, N, 32, 32, 32, 64, 1, 1, 1, 0)]  # im2col'd stem (1x1 on 32 channels)
+    cin, hw = 64, 32
+    for planes in (64, 128, 256, 512):
+        stride = 1 if planes == 64 else 2
+        ho = hw // stride
+        gs.append(ConvGeom(G, N, hw, hw, cin, planes, 3, 3, stride, 1))
+        gs.append(ConvGeom(G, N, ho, ho, planes, planes, 3, 3, 1, 1))
+        if stride != 1:
+            gs.append(ConvGeom(G, N, hw, hw, cin, planes, 1, 1, 2, 0))
+        cin, hw = planes, ho
+    return list(dict.fromkeys(gs))
+
+
+def timed(fn, reps):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default="gpurun_out/f32_plans.json")
+    ap.add_argument("--groups", type=int, nargs="*", default=[8, 1])
+    ap.add_argument("--batch", type=int, default=100)
+    ap.add_argument("--budget-s", type=float, default=240.0)
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    t_start = time.time()
+    plans, report = {}, []
+    for G in a.groups:
+        for g in resnet18_geoms(G, a.batch):
+            x = torch.randn(g.G, g.N, g.H, g.W, g.C, device=dev)
+            w = torch.randn(g.G, g.K, g.R, g.S, g.C, device=dev) * 0.05
+            dy = torch.randn(g.G, g.N, g.P, g.Q, g.K, device=dev)
+            dw = torch.zeros_like(w)
+            flops = 2 * g.G * g.N * g.P * g.Q * g.K * g.R * g.S * g.C
+            for mode, name in ((F32.F_FWD, "fwd"), (F32.F_DGRAD, "dgrad"), (F32.F_WGRAD, "wgrad")):
+                if mode == F32.F_DGRAD and g.C == 32:
+                    continue  # the stem needs no input gradient
+                F32._OVERRIDE.pop((mode, g), None)
+                F32._PLANS.pop((mode, g), None)
+                heur = F32.plan(mode, g)
+                run = {F32.F_FWD: lambda: F32.conv_fwd(x, w, g, stats=F32.SlotStats()),
+                       F32.F_DGRAD: lambda: F32.conv_dgrad(dy, w, g),
+                       F32.F_WGRAD: lambda: F32.conv_wgrad(dy, x, g, dw)}[mode]
+                res = []
+                for bp in (64, 128):
+                    for bq in (64, 128):
+                        for split in (1, 2, 4, 8, 16, 32):
+                            F32.set_plan(mode, g, bp, bq, split)
+                            try:
+                                ms = timed(run, 5)
+                            except Exception as e:  # noqa: BLE001 (e.g. workspace too small)
+                                print("skip", name, g, bp, bq, split, e, flush=True)
+                                continue
+                            res.append((ms, bp, bq, split))
+                F32._OVERRIDE.pop((mode, g), None)
+                F32._PLANS.pop((mode, g), None)
+                res.sort()
+                ms, bp, bq, split = res[0]
+                hms = next(r[0] for r in res if F32.cfg_of(r[1], r[2]) == heur[0] and r[3] == heur[1]) \
+                    if any(F32.cfg_of(r[1], r[2]) == heur[0] and r[3] == heur[1] for r in res) else None
+                key = f"{name}:{g.G},{g.N},{g.H},{g.W},{g.C},{g.K},{g.R},{g.S},{g.stride},{g.pad}"
+                plans[key] = [bp, bq, split]
+                row = dict(mode=name, G=g.G, N=g.N, H=g.H, C=g.C, K=g.K, R=g.R, stride=g.stride,
+                           best_ms=round(ms, 4), plan=[bp, bq, split], tflops=round(flops / ms / 1e9, 1),
+                           pct_peak=round(100 * flops / ms / 1e9 / PEAK_TF, 1),
+                           heuristic_ms=None if hms is None else round(hms, 4))
+                report.append(row)
+                print(json.dumps(row), flush=True)
+                if time.time() - t_start > a.budget_s:
+                    break
+            del x, w, dy, dw
+            if time.time() - t_start > a.budget_s:
+                print("budget reached", flush=True)
+                break
+    Path(a.out).parent.mkdir(parents=True, exist_ok=True)
+    Path(a.out).write_text(json.dumps({"plans": plans, "report": report}, indent=1))
+    print("wrote", a.out)
+
+
+if __name__ == "__main__":
+    main()

@@ -348,3 +348,88 @@ def test_fedavg_fp32_deterministic(cuda):
     h3, w3 = run(False)
     assert h1 == h2, "graph-replayed fp32 rounds differ run to run"
     assert h1 == h3, f"graph vs eager differ: max {(w1 - w3).abs().max().item()}"
+
+
+# ------------------------------------------------------------------------------ exactness of the engine
+def _fedavg(cuda, model, kind, n, clients, batch, **kw):
+    from ddl25spring_amd.data.images import DeviceImageDataset, synthetic_images
+    from ddl25spring_amd.data.split import split
+    from ddl25spring_amd.fl.algorithms import FedAvg
+    from ddl25spring_amd.models import mnist_cnn, resnet18_cifar
+    from ddl25spring_amd.runtime.dist import DistContext
+    arr = synthetic_images(kind, n, seed=0)
+    fn = {"resnet18": resnet18_cifar, "mnist_cnn": mnist_cnn}[model]
+    return FedAvg(lambda groups: fn(groups=groups, precision="fp32"), DeviceImageDataset(arr, cuda),
+                  split(clients, True, 3, labels=arr.labels), lr=0.05, batch_size=batch, client_fraction=1.0,
+                  seed=3, ctx=DistContext(device=cuda), eval_every=0, **kw)
+
+
+@pytest.mark.parametrize("model,kind,batch", [("mnist_cnn", "mnist", 60), ("resnet18", "cifar10", 50)])
+def test_fp32_graph_replay_equals_eager_exactly(cuda, model, kind, batch):
+    """fp32: graph-replayed rounds == eager rounds bit for bit (MnistCnn includes dropout, whose
+    Philox counter advances on the device; batch 60 leaves a short last step in the graph)."""
+    ws = []
+    for graph in (True, False):
+        fa = _fedavg(cuda, model, kind, 400, 2, batch, use_graph=graph)
+        for _ in range(2):
+            fa.round()
+        ws.append(fa.w_global.clone())
+    assert torch.equal(ws[0], ws[1]), (ws[0] - ws[1]).abs().max().item()
+
+
+@pytest.mark.parametrize("model,kind", [("mnist_cnn", "mnist"), ("resnet18", "cifar10")])
+def test_fp32_direct_sgd_equals_gradient_sgd_exactly(cuda, model, kind, monkeypatch):
+    """Direct SGD (WGRAD adds -lr * dW into the master weights) == zeroed grads + fused SGD step:
+    fl(p + fl(-lr * dW)) == fl(p - fl(lr * dW)), so in fp32 the two are bitwise equal."""
+    import ddl25spring_amd.fl.local as L
+    ws = []
+    for direct in (False, True):
+        monkeypatch.setattr(L, "DIRECT_SGD", direct)
+        fa = _fedavg(cuda, model, kind, 200, 2, 50, use_graph=True)
+        fa.round()
+        assert fa.trainer.direct == direct
+        st = fa.net.store
+        assert st.shadow is st.data and st.shadow16 is None  # fp32: the kernels read the master
+        ws.append(fa.w_global.clone())
+    assert torch.equal(ws[0], ws[1]), (ws[0] - ws[1]).abs().max().item()
+
+
+def test_fp32_unsynchronised_rounds_equal_exactly(cuda):
+    """bench.py's timed mode (rounds enqueued back to back, no host sync) == synchronised rounds."""
+    ws = []
+    for sync in (True, False):
+        fa = _fedavg(cuda, "resnet18", "cifar10", 400, 4, 50)
+        fa.round()
+        fa.sync_rounds = sync
+        for _ in range(2):
+            _, s = fa.round()
+            assert s == 400
+        torch.cuda.synchronize()
+        ws.append(fa.w_global.clone())
+    assert torch.equal(ws[0], ws[1])
+
+
+def test_fp32_mnist_cnn_step_matches_torch(cuda):
+    """The reference's own model (hfl_complete.py:39-64) in fp32 on the device vs torch float64:
+    conv+bias+ReLU, maxpool, Linear, log_softmax/NLL — dropout disabled for the comparison."""
+    from ddl25spring_amd.models import convert, mnist_cnn
+    from ddl25spring_amd.models.torch_ref import TorchMnistCnn
+    from ddl25spring_amd.models.zoo import mnist_cnn_mapping
+    torch.manual_seed(3)
+    tm = TorchMnistCnn()
+    net = mnist_cnn(precision="fp32").to(cuda)
+    convert.import_torch(net, tm, mnist_cnn_mapping())
+    for layer in net.layers:
+        if hasattr(layer, "p"):
+            layer.p = 0.0
+    tm = tm.double().eval()
+    x = torch.randn(12, 1, 28, 28)
+    y = torch.randint(0, 10, (12,))
+    net.store.zero_grad()
+    loss, _ = net.train_step(net.prepare_input(x.to(cuda)), y[None].to(cuda, torch.int32))
+    lt = F.nll_loss(tm(x.double()), y)
+    lt.backward()
+    assert abs(loss[0].item() - lt.item()) <= 1e-5 * abs(lt.item())
+    g = convert.export_torch(net, tm, mnist_cnn_mapping(), grads=True)
+    for name, p in tm.named_parameters():
+        assert _err(g[name], p.grad) <= 1e-4, name
