@@ -11,7 +11,10 @@ same config (ResNet-18, CIFAR-10 shape, 8 IID clients, B=100, E=1, lr=0.01, 50k 
     weights copied back to the host (:332); ``n_k``-weighted sum on the host (:370-378) and the
     average copied back to the device (:380-383). fp32, NCHW, MIOpen convs.
   * ``tuned`` — the same algorithm with the usual eager-PyTorch speedups and no host round trips:
-    data resident on the device, bf16 autocast, channels_last, aggregation on the device.
+    data resident on the device, bf16 autocast, channels_last, aggregation on the device;
+  * ``tuned_fp32`` — as ``tuned`` at the reference's precision (no autocast; MIOpen fp32 convs with
+    cudnn.benchmark): the strongest stock-PyTorch fp32 loop, the fair comparison for bench.py's
+    fp32 headline.
 
 Both use synthetic CIFAR-shaped tensors (pre-normalised) and random init (no network here).
 
@@ -43,9 +46,9 @@ def make_data(n, device, seed=0):
 class Client:
     """WeightClient (hfl_complete.py:316-332): own model replica + own shuffling loader."""
 
-    def __init__(self, x, y, idx, lr, B, E, device, tuned):
+    def __init__(self, x, y, idx, lr, B, E, device, tuned, amp=True):
         self.x, self.y, self.idx = x, y, idx
-        self.B, self.E, self.device, self.tuned = B, E, device, tuned
+        self.B, self.E, self.device, self.tuned, self.amp = B, E, device, tuned, amp
         self.model = torch_resnet18_cifar().to(device)
         if tuned:
             self.model = self.model.to(memory_format=torch.channels_last)
@@ -70,7 +73,7 @@ class Client:
                 self.opt.zero_grad()
                 if self.tuned:
                     xb = xb.contiguous(memory_format=torch.channels_last)
-                    with torch.autocast("cuda", dtype=torch.bfloat16):
+                    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.amp):
                         loss = F.cross_entropy(self.model(xb), yb)
                 else:
                     loss = F.cross_entropy(self.model(xb), yb)
@@ -85,7 +88,7 @@ class Client:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variant", choices=("faithful", "tuned"), default="faithful")
+    ap.add_argument("--variant", choices=("faithful", "tuned", "tuned_fp32"), default="faithful")
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--clients", type=int, default=8)
@@ -97,7 +100,8 @@ def main():
     from ddl25spring_amd.runtime import dist as rdist
     ctx = rdist.init()
     dev = ctx.device
-    tuned = args.variant == "tuned" and dev.type == "cuda"
+    tuned = args.variant in ("tuned", "tuned_fp32") and dev.type == "cuda"
+    amp = args.variant == "tuned"
     torch.backends.cudnn.benchmark = tuned
     torch.backends.cudnn.deterministic = not tuned  # hfl_complete.py:17
     x, y = make_data(args.train_size, dev if tuned else "cpu")
@@ -107,7 +111,7 @@ def main():
     mine = [c for c in range(args.clients) if c % ctx.world == ctx.rank]
     torch.manual_seed(10)
     server = torch_resnet18_cifar().to(dev)
-    clients = {c: Client(x, y, shards[c], args.lr, args.batch, args.epochs, dev, tuned) for c in mine}
+    clients = {c: Client(x, y, shards[c], args.lr, args.batch, args.epochs, dev, tuned, amp) for c in mine}
     sizes = torch.tensor([len(s) for s in shards], dtype=torch.float64)
     p = (sizes / sizes.sum()).tolist()
 
@@ -149,7 +153,7 @@ def main():
     emit(ctx, metric=METRIC + f" [reference-equivalent eager PyTorch, {args.variant}]",
          value=round(samples / dt, 1), unit="samples/s", n_gpus=ctx.world, steps=args.steps,
          warmup=args.warmup, ms_per_step=round(1e3 * dt / args.steps, 3), higher_is_better=True,
-         scaling="strong", vs_baseline=None, dtype="bf16-autocast" if tuned else "fp32",
+         scaling="strong", vs_baseline=None, dtype="bf16-autocast" if (tuned and amp) else "fp32",
          data="synthetic", rounds_per_sec=round(args.steps / dt, 4),
          config={"model": "resnet18-cifar10", "global_batch": args.batch * args.clients,
                  "seq_len": None, "parallelism": f"fedavg-{args.clients}clients-eager-w{ctx.world}",

@@ -21,6 +21,7 @@ from ..data.text import SPTokenizer, TinyStories
 from ..models.llama import LLama, causalLLMLoss, split_stages
 from ..parallel.dp import GradBucketer, average_weights, broadcast_parameters
 from ..parallel.pipeline import PipelineStage, grid_ranks
+from ..runtime.checkpoint import ShardedCheckpoint, load_optimizer_state, optimizer_state
 from ..runtime.graphs import CAPTURE_MODE
 
 
@@ -44,6 +45,17 @@ class LLMConfig:
     log_every: int = 10
     fused_adam: bool = True
     graph: bool = True  # dp = pp = 1 on a GPU: replay the whole step (fwd, bwd, Adam) as a HIP graph
+    ckpt_dir: str = ""  # sharded checkpoint directory (runtime/checkpoint.py); resumes if committed
+    ckpt_every: int = 0  # commit a checkpoint every N optimizer steps (0: only at the end)
+
+
+_RUN_FIELDS = ("vocab_size", "dmodel", "num_heads", "n_layers", "ctx_size", "batch_size",
+               "micro_batches", "dp", "pp", "dp_mode", "lr", "seed", "fused_adam")
+
+
+def _run_tag(cfg: "LLMConfig") -> str:
+    """What a checkpoint must agree on to be resumable (not iters / logging / schedule)."""
+    return ",".join(f"{k}={getattr(cfg, k)}" for k in _RUN_FIELDS)
 
 
 class _PinnedH2D:
@@ -70,7 +82,12 @@ class _PinnedH2D:
 
 
 def train_llm(cfg: LLMConfig, ctx, log=print, warmup: int = 0) -> dict:
-    """Runs ``warmup`` untimed + ``cfg.iters`` timed iterations; returns losses and throughput."""
+    """Runs ``warmup`` untimed + ``cfg.iters`` timed iterations; returns losses and throughput.
+
+    With ``cfg.ckpt_dir`` every rank checkpoints its own stage shard (weights, Adam moments, step)
+    every ``cfg.ckpt_every`` steps and at the end, and a restarted job resumes from the last
+    committed step: the token stream is re-positioned to that step, so a resumed run is
+    bit-identical to an uninterrupted one (tests/test_checkpoint_cpu.py)."""
     if ctx.world != cfg.dp * cfg.pp:
         raise ValueError(f"world {ctx.world} != dp {cfg.dp} x pp {cfg.pp}")
     dev = ctx.device
@@ -97,8 +114,17 @@ def train_llm(cfg: LLMConfig, ctx, log=print, warmup: int = 0) -> dict:
     act_dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
     ps = PipelineStage(mod, stage, cfg.pp, ranks=pipe_ranks, act_shape=(mb, cfg.ctx_size, cfg.dmodel),
                        act_dtype=act_dtype, device=dev) if cfg.pp > 1 else None
+    ckpt = ShardedCheckpoint(cfg.ckpt_dir, ctx, tag=_run_tag(cfg)) if cfg.ckpt_dir else None
+    done = 0  # optimizer steps already taken (warm-up steps included: they train too)
+    restored = ckpt.load() if ckpt is not None else None
+    if restored is not None:
+        done, st = restored
+        mod.load_state_dict(st["model"])
+        load_optimizer_state(opt, st["opt"])
+        if log:
+            log(f"[pipe {pipe} stage {stage}] resumed from step {done}")
     stream = iter(TinyStories(SPTokenizer(cfg.vocab_size), cfg.batch_size, cfg.ctx_size,
-                              skip=pipe * 3000, seed=1234 + cfg.seed))
+                              skip=pipe * 3000 + done, seed=1234 + cfg.seed))
     h2d = _PinnedH2D((cfg.batch_size, cfg.ctx_size), torch.int64, dev) if dev.type == "cuda" else None
     losses = []
 
@@ -175,23 +201,38 @@ def train_llm(cfg: LLMConfig, ctx, log=print, warmup: int = 0) -> dict:
                 opt.sync_shadow()
         return loss
 
-    for _ in range(warmup):
+    def save(n):
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        ckpt.save(n, {"model": mod.state_dict(), "opt": optimizer_state(opt)})
+
+    total = warmup + cfg.iters
+    while done < warmup:
         step()
+        done += 1
     if dev.type == "cuda":
         torch.cuda.synchronize()
     ctx.barrier()
     t0 = time.perf_counter()
-    for it in range(cfg.iters):
+    timed = total - done
+    while done < total:
+        it = done - warmup
         loss = step()
+        done += 1
         if loss is not None and (it % cfg.log_every == 0 or it == cfg.iters - 1):
             lv = float(loss)
             losses.append((it, lv))
             if log:
                 log(f"[pipe {pipe} stage {stage}] iter {it} loss {lv:.4f}")
+        if ckpt is not None and cfg.ckpt_every and done % cfg.ckpt_every == 0 and done < total:
+            save(done)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     ctx.barrier()
     dt = ctx.max_scalar(time.perf_counter() - t0)
-    tokens = cfg.dp * cfg.batch_size * cfg.ctx_size * cfg.iters
-    return {"losses": losses, "seconds": dt, "tokens_per_s": tokens / dt,
-            "ms_per_iter": 1e3 * dt / max(1, cfg.iters), "config": asdict(cfg)}
+    if ckpt is not None and (restored is None or restored[0] < total):
+        save(total)
+    tokens = cfg.dp * cfg.batch_size * cfg.ctx_size * timed
+    return {"losses": losses, "seconds": dt, "tokens_per_s": tokens / max(dt, 1e-9),
+            "ms_per_iter": 1e3 * dt / max(1, timed), "config": asdict(cfg),
+            "resumed_from": None if restored is None else restored[0]}

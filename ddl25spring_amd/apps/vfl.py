@@ -40,6 +40,7 @@ def _partition(cfg, df, X):
 def run_vfl(cfg: VFLConfig, ctx, log=print) -> dict:
     from ..data import heart as H
     from ..models import tabular as T
+    from ..optim import make_adam
     df, real = H.load_heart()
     torch.manual_seed(cfg.seed)
     np.random.seed(cfg.seed)
@@ -68,7 +69,7 @@ def run_vfl(cfg: VFLConfig, ctx, log=print) -> dict:
         Xtr, Xte, ytr, yte = H.centralized_split(df, scaler="standard")
         real_t = torch.cat([torch.tensor(Xtr), torch.tensor(ytr).float().view(-1, 1)], 1).to(dev)
         vae = T.Autoencoder(real_t.shape[1], 48, 32, 16).to(dev)
-        opt = torch.optim.Adam(vae.parameters(), lr=1e-3)
+        opt = make_adam(vae.parameters(), lr=1e-3)
         losses = vae.train_with_settings(cfg.epochs, cfg.batch_size, real_t, opt, T.customLoss(),
                                          zero_grad_per_batch=not cfg.parity)
         _, mu, logvar = vae(real_t)
@@ -86,7 +87,7 @@ def run_vfl(cfg: VFLConfig, ctx, log=print) -> dict:
         m = T.VFLVAE([T.ClientEncoder(len(p), cfg.latent) for p in parts],
                      T.ServerVAE(cfg.parties * cfg.latent, 48, 32, 16),
                      [T.ClientDecoder(cfg.latent, len(p)) for p in parts], cfg.latent).to(dev)
-        opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+        opt = make_adam(m.parameters(), lr=1e-3)
         losses = []
         for _ in range(cfg.epochs):
             opt.zero_grad()
@@ -94,7 +95,8 @@ def run_vfl(cfg: VFLConfig, ctx, log=print) -> dict:
             loss = T.combined_loss(xs, rc, lat, rcat, mu, lv)
             loss.backward()
             opt.step()
-            losses.append(loss.item())
+            losses.append(loss.detach())
+        losses = torch.stack(losses).tolist()  # one host read for the whole run
         out.update(first_loss=losses[0], final_loss=losses[-1])
     else:
         raise ValueError(cfg.task)

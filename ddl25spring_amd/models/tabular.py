@@ -16,7 +16,6 @@ runtime, their cut-layer tensors cross GPUs over RCCL (``ddl25spring_amd.vfl``).
 """
 from __future__ import annotations
 
-import copy
 
 import numpy as np
 import torch
@@ -24,6 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import tabular_ops as TO
+from ..optim import make_adam
 
 
 class FLinear(nn.Linear):
@@ -81,10 +81,16 @@ class HeartDiseaseNN(nn.Module):
 
 def train_centralized(net, Xtr, ytr, Xte, yte, epochs: int = 49, optimizer=None):
     """Full-batch training keeping a DEEP copy of the best-test-accuracy weights (fixes the
-    reference's aliasing ``best_params = net.state_dict()``, centralized.py:51,69-70 / SURVEY Q9)."""
-    opt = optimizer or torch.optim.AdamW(net.parameters())
+    reference's aliasing ``best_params = net.state_dict()``, centralized.py:51,69-70 / SURVEY Q9).
+
+    Sync-free: the best-epoch selection is a device-side ``torch.where`` over the state tensors
+    (no per-epoch ``.item()``); the history is read back once at the end."""
+    opt = optimizer or make_adam(net.parameters(), decoupled=True)
     crit = SoftCrossEntropy()
-    best, best_sd, hist = -1.0, None, []
+    dev = Xtr.device
+    best = torch.full((), -1.0, device=dev)
+    best_sd = {k: v.detach().clone() for k, v in net.state_dict().items()}
+    losses, accs = [], []
     for _ in range(1, epochs + 1):
         net.train()
         opt.zero_grad()
@@ -94,12 +100,16 @@ def train_centralized(net, Xtr, ytr, Xte, yte, epochs: int = 49, optimizer=None)
         opt.step()
         net.eval()  # the reference scores with dropout still active; we score the deterministic net
         with torch.no_grad():
-            acc = (net(Xte).argmax(1) == yte).float().mean().item()
-        hist.append((loss.item(), acc))
-        if acc > best:
-            best, best_sd = acc, copy.deepcopy(net.state_dict())
+            acc = (net(Xte).argmax(1) == yte).float().mean()
+            better = acc > best
+            for k, v in net.state_dict().items():
+                best_sd[k].copy_(torch.where(better, v, best_sd[k]))
+            best = torch.maximum(best, acc)
+        losses.append(loss.detach())
+        accs.append(acc)
     net.load_state_dict(best_sd)
-    return best, hist
+    hist = list(zip(torch.stack(losses).tolist(), torch.stack(accs).tolist()))
+    return float(best), hist
 
 
 class Autoencoder(nn.Module):
@@ -141,7 +151,7 @@ class Autoencoder(nn.Module):
             self.train()
             if not zero_grad_per_batch:
                 optimizer.zero_grad()
-            total = 0.0
+            total = torch.zeros((), device=real_data.device)
             for b in range(nb):
                 mb = real_data[b * batch_sz:(b + 1) * batch_sz]
                 if zero_grad_per_batch:
@@ -150,11 +160,11 @@ class Autoencoder(nn.Module):
                 loss = loss_fn(out, mb, mu, logvar)
                 loss.backward()
                 optimizer.step()
-                total += loss.item()
+                total += loss.detach()  # accumulated on the device: no per-batch host sync
             losses.append(total / nb)
             if log:
-                log(epoch, losses[-1])
-        return losses
+                log(epoch, float(losses[-1]))
+        return torch.stack(losses).tolist()
 
     @torch.no_grad()
     def sample(self, nr_samples, dims, logvar, mu, label_col: bool = True, eval_mode: bool = False):
@@ -228,9 +238,21 @@ class VFLNetwork(nn.Module):
         else:
             self.bottom_models = nn.ModuleList(local_models)
         self.top_model = TopModel(local_models, n_outs)
-        self.optimizer = torch.optim.AdamW(self.parameters(), lr=lr)
+        self.lr, self._opt = lr, None
         self.criterion = SoftCrossEntropy()
         self.num_cli = self.cli_features = None
+
+    @property
+    def optimizer(self):
+        """AdamW over the registered parameters (vfl.py:50), built on first use so it sees the
+        device the network was moved to: the fused FlatAdam on the GPU."""
+        if self._opt is None:
+            self._opt = make_adam(self.parameters(), lr=self.lr, decoupled=True)
+        return self._opt
+
+    @optimizer.setter
+    def optimizer(self, opt):
+        self._opt = opt
 
     def forward(self, xs):
         return self.top_model([m(x) for m, x in zip(self.bottom_models, xs)])
@@ -254,7 +276,10 @@ class VFLNetwork(nn.Module):
                 m.train()
             if not self.zero_grad_per_batch:
                 self.optimizer.zero_grad()
-            total, correct = 0.0, 0
+            # loss / correct accumulate on the device; the host reads them once (at the end, or
+            # per epoch only when a logger asks)
+            total = torch.zeros((), device=yt.device)
+            correct = torch.zeros((), dtype=torch.int64, device=yt.device)
             for b in range(nb):
                 sl = slice(b * batch_sz, (b + 1) * batch_sz)
                 if self.zero_grad_per_batch:
@@ -263,14 +288,15 @@ class VFLNetwork(nn.Module):
                 loss = self.criterion(outs, yt[sl])
                 loss.backward()
                 self.optimizer.step()
-                total += loss.item()
-                correct += (outs.argmax(1) == yt[sl].argmax(1)).sum().item()
-            hist.append((total / nb, correct / n))
+                total += loss.detach()
+                correct += (outs.argmax(1) == yt[sl].argmax(1)).sum()
+            hist.append(torch.stack([total / nb, correct / n]))
             if log_loss is not None:
-                log_loss(total / nb)
+                log_loss(float(hist[-1][0]))
             if verbose:
-                print(f"Epoch: {epoch} Train accuracy: {100 * correct / n:.2f}% Loss: {total / nb:.3f}")
-        return hist
+                l, a = hist[-1].tolist()
+                print(f"Epoch: {epoch} Train accuracy: {100 * a:.2f}% Loss: {l:.3f}")
+        return [tuple(h) for h in torch.stack(hist).tolist()]
 
     def test(self, x, y):
         xs, yt = self._tensors(x, y, self.cli_features)

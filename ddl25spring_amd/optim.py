@@ -204,3 +204,16 @@ class FlatAdamW(FlatAdam):
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.01):
         super().__init__(params, lr, betas, eps, weight_decay, decoupled=True)
+
+
+def make_adam(params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+              weight_decay: float | None = None, decoupled: bool = False):
+    """``torch.optim.Adam``/``AdamW`` semantics (AdamW's default weight_decay 0.01) for plain
+    ``nn.Module`` parameters: the fused single-launch ``FlatAdam`` when they live on the GPU,
+    ``torch.optim`` on the CPU (where the golden tests pin torch's exact arithmetic)."""
+    params = [p for p in params if p.requires_grad]
+    wd = (0.01 if decoupled else 0.0) if weight_decay is None else weight_decay
+    if params and params[0].is_cuda:
+        return FlatAdam(params, lr=lr, betas=betas, eps=eps, weight_decay=wd, decoupled=decoupled)
+    cls = torch.optim.AdamW if decoupled else torch.optim.Adam
+    return cls(params, lr=lr, betas=betas, eps=eps, weight_decay=wd)

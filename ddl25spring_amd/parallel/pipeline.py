@@ -6,7 +6,9 @@ Replaces the reference's hand-written per-rank send/recv choreographies
     matching sends/receives in a deadlock-free order;
   * activations / gradients stay on the GPU (RCCL ``send/recv`` over xGMI; the reference staged
     every message through host memory with ``.to("cpu")``);
-  * a posted comm group is issued as ONE ``batch_isend_irecv`` (grouped P2P);
+  * a posted comm group is issued as ONE ``batch_isend_irecv`` (grouped P2P); over gloo (ranks that
+    share a GPU, or CPU runs) device tensors are staged through host memory, since gloo's
+    point-to-point moves CPU tensors only;
   * the loss is divided by the number of micro-batches (gradient averaging by loss scaling, as
     intro_PP_1F1B_MB.py:99 does), so an iteration equals one full-batch step.
 """
@@ -27,6 +29,8 @@ class PipelineStage:
         self.act_shape, self.act_dtype = act_shape, act_dtype
         self.device = device or next(module.parameters()).device
         self.group = group
+        self.host_staged = torch.device(self.device).type == "cuda" and dist.is_initialized() and \
+            dist.get_backend(group) == "gloo"
 
     @property
     def is_first(self):
@@ -39,9 +43,23 @@ class PipelineStage:
     def _p2p(self, ops):
         if not ops:
             return
-        reqs = dist.batch_isend_irecv(ops)
-        for r in reqs:
+        if not self.host_staged:
+            for r in dist.batch_isend_irecv(ops):
+                r.wait()
+            return
+        staged, back = [], []
+        for op in ops:
+            t = op.tensor
+            if op.op is dist.isend:
+                h = t.detach().cpu()
+            else:
+                h = torch.empty(t.shape, dtype=t.dtype)
+                back.append((t, h))
+            staged.append(dist.P2POp(op.op, h, op.peer, op.group))
+        for r in dist.batch_isend_irecv(staged):
             r.wait()
+        for t, h in back:
+            t.copy_(h)
 
     def run(self, kind: str, n_micro: int, inputs=None, targets=None, loss_fn=None, grad_sync=None):
         """One training iteration (forward + backward of all micro-batches; no optimizer step).

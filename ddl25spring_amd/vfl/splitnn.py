@@ -23,6 +23,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops import tabular_ops as TO
+from ..optim import make_adam
 
 
 def _exchange(sends, recvs, group=None):
@@ -43,7 +44,7 @@ class SplitNNParty:
 
     def __init__(self, bottom: nn.Module, out_dim: int, server: int = 0, optimizer=None, group=None):
         self.bottom, self.out_dim, self.server, self.group = bottom, out_dim, server, group
-        self.opt = optimizer or torch.optim.AdamW(bottom.parameters())
+        self.opt = optimizer or make_adam(bottom.parameters(), decoupled=True)
 
     def train_step(self, x):
         self.opt.zero_grad()
@@ -76,7 +77,7 @@ class SplitNNServer:
         self.top, self.parties, self.out_dims, self.group = top, parties, out_dims, group
         self.local = local_bottom
         params = list(top.parameters()) + (list(local_bottom.parameters()) if local_bottom else [])
-        self.opt = optimizer or torch.optim.AdamW(params)
+        self.opt = optimizer or make_adam(params, decoupled=True)
         self.criterion = criterion or nn.CrossEntropyLoss()
 
     def _recv(self, b, like):
@@ -98,9 +99,9 @@ class SplitNNServer:
         self.opt.step()
         # grads go back after the server step: the parties only need them for their own update
         _exchange([(a.grad.contiguous(), p) for a, p in zip(acts, self.parties)], [], self.group)
-        correct = (out.argmax(1) == y.argmax(1)).sum().item() if y.dim() == 2 else \
-            (out.argmax(1) == y).sum().item()
-        return loss.item(), correct
+        lab = y.argmax(1) if y.dim() == 2 else y
+        # device scalars: the host never waits on a mini-batch (fit reads them once at the end)
+        return loss.detach(), (out.argmax(1) == lab).sum()
 
     @torch.no_grad()
     def infer(self, n, like, eval_mode: bool = True, x_local=None):
@@ -114,14 +115,17 @@ class SplitNNServer:
     def fit(self, y, epochs, batch_size, log=None, x_local=None):
         hist = []
         for e in range(epochs):
-            tot, cor, bl = 0.0, 0, _batches(len(y), batch_size)
+            tot = torch.zeros((), device=y.device)
+            cor = torch.zeros((), dtype=torch.int64, device=y.device)
+            bl = _batches(len(y), batch_size)
             for sl in bl:
                 l, c = self.train_step(y[sl], None if x_local is None else x_local[sl])
-                tot, cor = tot + l, cor + c
-            hist.append((tot / len(bl), cor / len(y)))
+                tot += l
+                cor += c
+            hist.append(torch.stack([tot / len(bl), cor / len(y)]))
             if log:
-                log(e, *hist[-1])
-        return hist
+                log(e, *hist[-1].tolist())
+        return [tuple(h) for h in torch.stack(hist).tolist()]
 
 
 # ------------------------------------------------------------------------------------ VFL-VAE
@@ -129,7 +133,7 @@ class VAEParty:
     def __init__(self, encoder, decoder, latent_dim, server: int = 0, optimizer=None, group=None):
         self.enc, self.dec, self.L, self.server, self.group = encoder, decoder, latent_dim, server, group
         params = list(encoder.parameters()) + list(decoder.parameters())
-        self.opt = optimizer or torch.optim.Adam(params, lr=1e-3)
+        self.opt = optimizer or make_adam(params, lr=1e-3)
         self.mse = nn.MSELoss(reduction="sum")
 
     def train_step(self, x):
@@ -152,7 +156,7 @@ class VAEParty:
 class VAEServer:
     def __init__(self, vae, parties, latent_dim, optimizer=None, group=None):
         self.vae, self.parties, self.L, self.group = vae, parties, latent_dim, group
-        self.opt = optimizer or torch.optim.Adam(vae.parameters(), lr=1e-3)
+        self.opt = optimizer or make_adam(vae.parameters(), lr=1e-3)
         self.mse = nn.MSELoss(reduction="sum")
 
     def train_step(self, n, like):
@@ -175,4 +179,4 @@ class VAEServer:
         self.opt.step()
         _exchange([(lat.grad[:, i * L:(i + 1) * L].contiguous(), p) for i, p in enumerate(self.parties)],
                   [], self.group)
-        return sloss.item() + sum(c.item() for c in closs)
+        return sloss.detach() + torch.cat(closs).sum()  # device scalar, no host sync

@@ -178,7 +178,7 @@ def _vfl_worker(rank, world, port, out_dir):
         else:
             node.train_step(vx[rank - 1])
     if rank == 0:
-        vres = [p.detach() for p in vae.parameters()] + [torch.tensor([loss])]
+        vres = [p.detach() for p in vae.parameters()] + [loss.reshape(1)]
     else:
         vres = [p.detach() for p in encs[rank - 1].parameters()] + \
                [p.detach() for p in decs[rank - 1].parameters()]
