@@ -35,7 +35,7 @@ METRIC = "FedAvg rounds/sec + local samples/sec, ResNet-18 CIFAR-10-shape, 8 cli
 # loop (hfl_complete.py FedAvgServer: per-client nn.Module replicas, host-staged weights, fp32) on
 # the same config, timed on one MI355X with stock PyTorch-ROCm (benchmarks/bench_reference_eager.py
 # --variant faithful; profiles/reference_eager_r3.jsonl).
-REFERENCE_SAMPLES_PER_S = {"fp32": 5707.8}
+REFERENCE_SAMPLES_PER_S = {"fp32": 5296.8}
 
 
 def main():

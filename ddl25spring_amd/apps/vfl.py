@@ -25,6 +25,8 @@ class VFLConfig:
     parity: bool = False        # reproduce the reference's quirks (Q5/Q6/Q8)
     seed: int = 42
     latent: int = 8
+    ckpt_dir: str = ""          # distributed split-NN: per-rank sharded checkpoint (resumes if committed)
+    ckpt_every: int = 0         # commit every N epochs (0: only at the end)
 
 
 def _partition(cfg, df, X):
@@ -118,15 +120,56 @@ def _distributed_splitnn(cfg, ctx, parts, Xtr, Ytr, Xte, Yte):
     dims = [2 * len(p) for p in parts]
     if ctx.rank == 0:
         y = torch.tensor(Ytr.values.astype(np.float32)).to(dev)
-        srv = SplitNNServer(top.to(dev), list(range(1, cfg.parties + 1)), dims)
-        hist = srv.fit(y, cfg.epochs, cfg.batch_size)
+        node = SplitNNServer(top.to(dev), list(range(1, cfg.parties + 1)), dims)
+    else:
+        i = ctx.rank - 1
+        x = torch.tensor(Xtr[parts[i]].values.astype(np.float32)).to(dev)
+        node = SplitNNParty(bottoms[i].to(dev), dims[i])
+    start, prior, on_epoch = _splitnn_checkpointing(cfg, ctx, node)
+    if ctx.rank == 0:
+        hist = prior + node.fit(y, cfg.epochs, cfg.batch_size, start_epoch=start, on_epoch=on_epoch)
         yte = torch.tensor(Yte.values.astype(np.float32)).to(dev)
-        out = srv.infer(len(yte), yte)
+        out = node.infer(len(yte), yte)
         acc = (out.argmax(1) == yte.argmax(1)).float().mean().item()
-        return {"train_loss": hist[-1][0], "train_accuracy": hist[-1][1], "test_accuracy": acc}
-    i = ctx.rank - 1
-    x = torch.tensor(Xtr[parts[i]].values.astype(np.float32)).to(dev)
-    party = SplitNNParty(bottoms[i].to(dev), dims[i])
-    party.fit(x, cfg.epochs, cfg.batch_size)
-    party.infer(torch.tensor(Xte[parts[i]].values.astype(np.float32)).to(dev))
+        return {"train_loss": hist[-1][0], "train_accuracy": hist[-1][1], "test_accuracy": acc,
+                "resumed_from": start or None}
+    node.fit(x, cfg.epochs, cfg.batch_size, start_epoch=start, on_epoch=on_epoch)
+    node.infer(torch.tensor(Xte[parts[i]].values.astype(np.float32)).to(dev))
     return {}
+
+
+def _splitnn_checkpointing(cfg, ctx, node):
+    """Per-rank shards (this rank's bottom or top model, its optimizer moments, its dropout RNG
+    stream, the server's epoch history) through runtime/checkpoint.py. Returns (first epoch to
+    run, history of the epochs already done, per-epoch hook)."""
+    if not cfg.ckpt_dir:
+        return 0, [], None
+    from ..runtime.checkpoint import ShardedCheckpoint, load_optimizer_state, optimizer_state
+    tag = f"splitnn,parties={cfg.parties},partition={cfg.partition},bs={cfg.batch_size},seed={cfg.seed}"
+    ck = ShardedCheckpoint(cfg.ckpt_dir, ctx, tag=tag)
+    cuda = ctx.device.type == "cuda"
+    start, prior = 0, []
+    got = ck.load()
+    if got is not None:
+        start, st = got
+        for k, m in node.modules().items():
+            m.load_state_dict(st["model"][k])
+        load_optimizer_state(node.opt, st["opt"])
+        torch.set_rng_state(st["rng"])
+        if cuda:
+            torch.cuda.set_rng_state(st["cuda_rng"])
+        prior = [tuple(h) for h in st["hist"]]
+
+    def save(e):
+        hist = prior + [tuple(h.tolist()) for h in getattr(node, "history", [])]
+        st = {"model": {k: m.state_dict() for k, m in node.modules().items()},
+              "opt": optimizer_state(node.opt), "rng": torch.get_rng_state(), "hist": hist}
+        if cuda:
+            st["cuda_rng"] = torch.cuda.get_rng_state()
+        ck.save(e, st)
+
+    def on_epoch(e):
+        if (cfg.ckpt_every and e % cfg.ckpt_every == 0) or e == cfg.epochs:
+            save(e)
+
+    return start, prior, on_epoch

@@ -138,6 +138,11 @@ def init(backend: str | None = None, device: str | None = None, rank: int | None
             # ranks sharing a host must split its cores, or their intra-op pools oversubscribe it
             local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
             torch.set_num_threads(max(1, (os.cpu_count() or 1) // local_world))
+    if backend is None and dev.type == "cuda" and world > 1 and \
+            int(os.environ.get("LOCAL_WORLD_SIZE", world)) > torch.cuda.device_count():
+        # more ranks than GPUs on this node (e.g. 2 VFL parties sharing one MI355X): RCCL refuses
+        # two ranks on one device, so those ranks talk over gloo (host-staged cut-layer tensors)
+        backend = "gloo"
     backend = backend or ("nccl" if dev.type == "cuda" else "gloo")
     if (world > 1 or forced) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

@@ -27,11 +27,20 @@ from ..optim import make_adam
 
 
 def _exchange(sends, recvs, group=None):
+    if not (sends or recvs):
+        return
+    staged = dist.get_backend(group) == "gloo" and any(t.is_cuda for t, _ in sends + recvs)
+    if staged:
+        # gloo P2P moves host memory only (ranks sharing one GPU): stage through the host
+        sends = [(t.cpu(), p) for t, p in sends]
+        dev_recvs, recvs = recvs, [(torch.empty(t.shape, dtype=t.dtype), p) for t, p in recvs]
     ops = [dist.P2POp(dist.isend, t, peer, group) for t, peer in sends]
     ops += [dist.P2POp(dist.irecv, t, peer, group) for t, peer in recvs]
-    if ops:
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
+    for w in dist.batch_isend_irecv(ops):
+        w.wait()
+    if staged:
+        for (d, _), (h, _) in zip(dev_recvs, recvs):
+            d.copy_(h)
 
 
 def _batches(n, bs):
@@ -61,10 +70,15 @@ class SplitNNParty:
         self.bottom.train(not eval_mode)
         _exchange([(self.bottom(x).contiguous(), self.server)], [], self.group)
 
-    def fit(self, x, epochs, batch_size):
-        for _ in range(epochs):
+    def fit(self, x, epochs, batch_size, start_epoch: int = 0, on_epoch=None):
+        for e in range(start_epoch, epochs):
             for sl in _batches(len(x), batch_size):
                 self.train_step(x[sl])
+            if on_epoch is not None:
+                on_epoch(e + 1)
+
+    def modules(self):
+        return {"bottom": self.bottom}
 
 
 class SplitNNServer:
@@ -112,9 +126,18 @@ class SplitNNServer:
             acts = [self.local(x_local)] + acts
         return self.top(acts)
 
-    def fit(self, y, epochs, batch_size, log=None, x_local=None):
+    def modules(self):
+        mods = {"top": self.top}
+        if self.local is not None:
+            mods["local"] = self.local
+        return mods
+
+    def fit(self, y, epochs, batch_size, log=None, x_local=None, start_epoch: int = 0, on_epoch=None):
+        """Epochs ``start_epoch`` .. ``epochs``-1; ``on_epoch(e)`` after each (checkpoint hook;
+        it sees the history so far as ``self.history``). Returns that history as floats."""
         hist = []
-        for e in range(epochs):
+        self.history = hist
+        for e in range(start_epoch, epochs):
             tot = torch.zeros((), device=y.device)
             cor = torch.zeros((), dtype=torch.int64, device=y.device)
             bl = _batches(len(y), batch_size)
@@ -125,7 +148,9 @@ class SplitNNServer:
             hist.append(torch.stack([tot / len(bl), cor / len(y)]))
             if log:
                 log(e, *hist[-1].tolist())
-        return [tuple(h) for h in torch.stack(hist).tolist()]
+            if on_epoch is not None:
+                on_epoch(e + 1)
+        return [tuple(h) for h in torch.stack(hist).tolist()] if hist else []
 
 
 # ------------------------------------------------------------------------------------ VFL-VAE

@@ -92,3 +92,37 @@ def test_checkpoint_rejects_mismatched_world(tmp_path):
     Ctx.world = 1
     with pytest.raises(ValueError, match="tag"):
         ShardedCheckpoint(str(tmp_path), Ctx(), tag="b").latest()
+
+
+def _vfl_worker(rank, world, port, cfg_kw, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    from ddl25spring_amd.apps.vfl import VFLConfig, run_vfl
+    from ddl25spring_amd.runtime import dist as rdist
+    ctx = rdist.init(backend="gloo", device="cpu")
+    res = run_vfl(VFLConfig(**cfg_kw), ctx, log=None)
+    res.pop("real_data", None)
+    torch.save(res, os.path.join(out, f"res{rank}.pt"))
+    rdist.shutdown()
+
+
+def test_splitnn_resume_is_bit_identical():
+    cfg = dict(task="splitnn", parties=2, partition="balanced", batch_size=64)
+    with tempfile.TemporaryDirectory() as d:
+        full, part = os.path.join(d, "full"), os.path.join(d, "part")
+
+        def run(port, kw, o):
+            os.makedirs(o, exist_ok=True)
+            mp.spawn(_vfl_worker, args=(3, port, dict(cfg, **kw), o), nprocs=3, join=True)
+            return torch.load(os.path.join(o, "res0.pt"), weights_only=True)
+
+        r_full = run(29981, dict(epochs=6, ckpt_dir=full), os.path.join(d, "o1"))
+        run(29982, dict(epochs=3, ckpt_dir=part), os.path.join(d, "o2"))
+        r_res = run(29983, dict(epochs=6, ckpt_dir=part), os.path.join(d, "o3"))
+        assert r_res["resumed_from"] == 3
+        a, b = _shards(full, 6, 3), _shards(part, 6, 3)
+        for r in range(3):
+            _assert_identical(a[r], b[r], f"rank{r}")
+        assert r_res["test_accuracy"] == r_full["test_accuracy"]
+        assert r_res["train_loss"] == r_full["train_loss"]

@@ -60,3 +60,36 @@ def test_bench_two_ranks_gloo(cuda):
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1 and '"n_gpus": 2' in lines[0], out.stdout[-2000:]
+
+
+def test_federated_gan_two_ranks_share_gpu(tmp_path):
+    """Federated DCGAN with one client per rank on the device: 2 ranks share the
+    GPU (auto gloo: more ranks than GPUs) and match the single-process run."""
+    from ddl25spring_amd.runtime.launch import launch
+    args = ["gan", "--clients", "2", "--rounds", "2", "--local-steps", "2", "--batch-size", "16",
+            "--train-size", "128", "--seed", "3"]
+    w1, w2 = tmp_path / "w1.pt", tmp_path / "w2.pt"
+    env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    subprocess.run([sys.executable, "-m", "ddl25spring_amd", *args, "--save", str(w1)], check=True,
+                   env=env, timeout=300, cwd=ROOT)
+    res = launch([sys.executable, "-m", "ddl25spring_amd", *args, "--save", str(w2)], world=2,
+                 log_dir=str(tmp_path / "logs"), timeout=300)
+    assert res["returncode"] == 0, res
+    a, b = torch.load(w1, weights_only=True), torch.load(w2, weights_only=True)
+    assert a.shape == b.shape and torch.isfinite(b).all()
+    # same clients, same data, same noise; the device kernels may sum in a different order
+    assert ((a - b).norm() / a.norm()).item() < 1e-3
+
+
+def test_vfl_gan_bench_two_ranks_share_gpu():
+    """benchmarks/bench_vfl_gan.py at world 2: rank 0 = active party + GAN client 0, rank 1 =
+    passive party + GAN client 1; cut-layer tensors host-staged over gloo."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", "29745",
+           os.path.join(ROOT, "benchmarks", "bench_vfl_gan.py"), "--steps", "2", "--warmup", "1",
+           "--local-steps", "4"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and '"n_gpus": 2' in lines[0], out.stdout[-2000:]
+    print(lines[0])
