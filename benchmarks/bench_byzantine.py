@@ -2,7 +2,9 @@
 label-flip + sign-flip attackers, 8 clients (ResNet-18, CIFAR-10 shape, the headline workload).
 
 Per aggregator: FedAvg rounds/s and the device time of the aggregation phase (coordinate-sharded
-all-to-all + bitonic selection / fp32-MFMA Gram kernels), optionally test accuracy (--eval).
+all-to-all + bitonic selection / fp32-MFMA Gram kernels) under attack, and the robustness itself:
+test accuracy after ``--acc-rounds`` rounds on the learnable synthetic CIFAR set, clean (no
+attacker) vs attacked, for every aggregator (``--no-eval`` skips the accuracy runs).
 """
 from __future__ import annotations
 
@@ -20,7 +22,9 @@ def main():
     ap.add_argument("--model", default="resnet18")
     ap.add_argument("--train-size", type=int, default=50000)
     ap.add_argument("--aggregators", default="mean,median,trimmed_mean,krum")
-    ap.add_argument("--eval", action="store_true")
+    ap.add_argument("--no-eval", dest="eval", action="store_false")
+    ap.add_argument("--acc-rounds", type=int, default=6, help="rounds before the accuracy test")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"])
     args = ap.parse_args()
     from ddl25spring_amd.data.images import DeviceImageDataset, load_images
     from ddl25spring_amd.data.split import split
@@ -30,21 +34,29 @@ def main():
     from ddl25spring_amd.runtime import dist as rdist
     ctx = rdist.init()
     kind = "cifar10" if args.model == "resnet18" else "mnist"
-    model_fn = resnet18_cifar if args.model == "resnet18" else mnist_cnn
     train = load_images(kind, True, args.train_size)
     test = load_images(kind, False, 2000)
     parts = split(8, True, 0, labels=train.labels)
     data, tdata = DeviceImageDataset(train, ctx.device), DeviceImageDataset(test, ctx.device)
     results = {}
+
+    def build(groups):
+        if args.model == "resnet18":
+            return resnet18_cifar(10, groups=groups, precision=args.precision)
+        return mnist_cnn(groups=groups, precision=args.precision)
+
+    def make(agg, attacked):
+        fa = FedAvg(build, data, parts,
+                    lr=0.01, batch_size=100, client_fraction=1.0, seed=0, test_data=tdata,
+                    aggregator=agg, agg_kwargs={"trim": 0.25, "f": 2}, ctx=ctx, eval_every=0)
+        if attacked:
+            # clients 0,1 flip labels (data poisoning), clients 2,3 flip (and scale) their update
+            # signs (model poisoning): 4 of 8 clients hostile
+            fa.attack = _Both(make_attack("sign_flip", [2, 3]), make_attack("label_flip", [0, 1]))
+        return fa
+
     for agg in args.aggregators.split(","):
-        # clients 0,1 flip labels, clients 2,3 flip (and scale) their update signs: 4 of 8 hostile
-        # for the data-poisoning pair, 2 of 8 model-poisoners
-        attack = make_attack("sign_flip", [2, 3])
-        fa = FedAvg(model_fn, data, parts, lr=0.01, batch_size=100, client_fraction=1.0, seed=0,
-                    test_data=tdata, aggregator=agg, agg_kwargs={"trim": 0.25, "f": 2},
-                    attack=attack, ctx=ctx, eval_every=0)
-        flip = make_attack("label_flip", [0, 1])
-        fa.attack = _Both(attack, flip)
+        fa = make(agg, True)
         for _ in range(args.warmup):
             fa.round()
         fa.timer.summary()
@@ -53,14 +65,24 @@ def main():
             dt, _ = fa.round()
             times.append(dt)
             agg_ms.append(fa.timer.summary().get("aggregate", float("nan")))
-        results[agg] = {"rounds_per_s": round(len(times) / sum(times), 4),
-                        "aggregate_ms": round(float(np.mean(agg_ms)), 3)}
+        res = {"rounds_per_s": round(len(times) / sum(times), 4),
+               "aggregate_ms": round(float(np.mean(agg_ms)), 3)}
         if args.eval:
-            results[agg]["test_accuracy"] = fa.test()
+            for _ in range(args.acc_rounds - args.warmup - args.steps):
+                fa.round()
+            res["test_accuracy_attacked"] = round(fa.test(), 4)
+            clean = make(agg, False)
+            for _ in range(args.acc_rounds):
+                clean.round()
+            res["test_accuracy_clean"] = round(clean.test(), 4)
+            del clean
+        results[agg] = res
+        del fa
     emit(ctx, metric="Byzantine-robust FedAvg rounds/s (8 clients, 2 label-flip + 2 sign-flip)",
          value=results.get("krum", next(iter(results.values())))["rounds_per_s"], unit="rounds/s",
          n_gpus=ctx.world, steps=args.steps, warmup=args.warmup, higher_is_better=True,
-         scaling="strong", vs_baseline=None, dtype="bf16", data="synthetic", per_aggregator=results,
+         scaling="strong", vs_baseline=None, dtype=args.precision, data="synthetic",
+         acc_rounds=args.acc_rounds if args.eval else None, per_aggregator=results,
          config={"model": f"{args.model}-{kind}", "global_batch": 800, "seq_len": None,
                  "parallelism": f"fedavg-8clients-dp{ctx.world}"})
     rdist.shutdown()

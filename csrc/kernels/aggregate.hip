@@ -7,9 +7,10 @@
 //   ddl_broadcast_rows : dst[g][i] = src[i] (+ bf16 shadow) — server -> client weight download
 //                        (hfl_complete.py:323-325) without leaving HBM.
 //   ddl_gram_f32       : G = (X - c)(X - c)^T on the exact-fp32 MFMA (v_mfma_f32_16x16x4_f32),
-//                        split over the coordinate axis — pairwise distances for Krum /
-//                        multi-Krum (Blanchard et al. 2017) [north-star, absent in reference].
-//   ddl_coord_select   : coordinate-wise median / trimmed mean over K client vectors by an
+//                        split over the coordinate axis, K <= 128 clients, deterministic —
+//                        pairwise distances for Krum / multi-Krum (Blanchard et al. 2017)
+//                        [north-star, absent in reference].
+//   ddl_coord_select   : coordinate-wise median / trimmed mean over K <= 128 client vectors by an
 //                        in-register bitonic sort per coordinate (Yin et al. 2018) [north-star].
 #include "ddl_common.h"
 
@@ -67,28 +68,42 @@ DDL_API int ddl_broadcast_rows(const float* src, float* dst, long long ld, int G
 
 // ---------------------------------------------------------------------------------------------
 // Gram on exact-fp32 MFMA. X [K][n] (row stride ld), optional center c [n] subtracted on load.
-// Block = 256 threads = 4 waves; the block owns a slice of the coordinate axis and computes
-// the full KP x KP partial Gram (KP = K rounded up to 16, <= 64) with 16x16 output tiles
-// distributed over the waves; partials are atomically added into out [K][K].
+// Block = 256 threads = 4 waves; the block owns a slice of the coordinate axis and computes the
+// upper-triangular 16x16 tiles of its partial KP x KP Gram (KP = K rounded up to 16, <= 128; the
+// Gram is symmetric, so only ti <= tj tiles: 36 instead of 64 at KP = 128), tiles dealt round-robin
+// over the waves. Partials go to a per-block slice of `part` with plain stores, and
+// gram_reduce_kernel sums the slices in block order: the K x K result is bit-reproducible (no
+// float atomics), which Krum's argsort of scores needs to pick the same clients on every run.
 // Staging: LDS tile [KP][CHUNK] fp32 with a +1 float pad per row (conflict-free column reads).
+constexpr int GRAM_CHUNK = 64;
+
+__host__ __device__ inline int gram_blocks_cap(int KP) { return KP <= 64 ? 1024 : 512; }
+
 template <int KP>
 __global__ __launch_bounds__(256) void gram_f32_kernel(const float* __restrict__ X, long long ld,
                                                        const float* __restrict__ center, int K,
-                                                       long long n, float* __restrict__ out) {
-  constexpr int CHUNK = 64;
-  constexpr int LDW = CHUNK + 1;
+                                                       long long n, float* __restrict__ part) {
+  constexpr int LDW = GRAM_CHUNK + 1;
   constexpr int NT = KP / 16;
-  constexpr int TILES = NT * NT;
+  constexpr int TILES = NT * (NT + 1) / 2;
   constexpr int TPW = (TILES + 3) / 4;  // tiles per wave
   __shared__ float tile[KP * LDW];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int ti_[TPW], tj_[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    int idx = wid + 4 * t, ti = 0;
+    while (ti < NT && idx >= NT - ti) { idx -= NT - ti; ++ti; }
+    ti_[t] = ti;            // ti == NT: this wave has no tile in slot t
+    tj_[t] = ti + idx;
+  }
   f4v acc[TPW];
 #pragma unroll
   for (int i = 0; i < TPW; ++i) acc[i] = (f4v){0.f, 0.f, 0.f, 0.f};
-  for (long long c0 = (long long)blockIdx.x * CHUNK; c0 < n; c0 += (long long)gridDim.x * CHUNK) {
+  for (long long c0 = (long long)blockIdx.x * GRAM_CHUNK; c0 < n; c0 += (long long)gridDim.x * GRAM_CHUNK) {
     __syncthreads();
-    for (int e = tid; e < KP * CHUNK; e += 256) {
-      const int r = e / CHUNK, c = e - r * CHUNK;
+    for (int e = tid; e < KP * GRAM_CHUNK; e += 256) {
+      const int r = e / GRAM_CHUNK, c = e - r * GRAM_CHUNK;
       const long long col = c0 + c;
       float v = 0.f;
       if (r < K && col < n) v = X[r * ld + col] - (center ? center[col] : 0.f);
@@ -97,46 +112,67 @@ __global__ __launch_bounds__(256) void gram_f32_kernel(const float* __restrict__
     __syncthreads();
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
-      const int tt = wid + 4 * t;
-      if (tt < TILES) {
-        const int ti = tt / NT, tj = tt - ti * NT;
+      if (ti_[t] < NT) {
+        const float* ra = tile + (ti_[t] * 16 + (lane & 15)) * LDW + (lane >> 4);
+        const float* rb = tile + (tj_[t] * 16 + (lane & 15)) * LDW + (lane >> 4);
 #pragma unroll
-        for (int k = 0; k < CHUNK; k += 4) {
+        for (int k = 0; k < GRAM_CHUNK; k += 4)
           // A[i][k] lane: i = lane&15, k = lane>>4 ; B[k][j] lane: j = lane&15, k = lane>>4
-          const float av = tile[(ti * 16 + (lane & 15)) * LDW + k + (lane >> 4)];
-          const float bv = tile[(tj * 16 + (lane & 15)) * LDW + k + (lane >> 4)];
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[t], 0, 0, 0);
-        }
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[k], rb[k], acc[t], 0, 0, 0);
       }
     }
   }
+  float* mine = part + (long long)blockIdx.x * KP * KP;
 #pragma unroll
   for (int t = 0; t < TPW; ++t) {
-    const int tt = wid + 4 * t;
-    if (tt < TILES) {
-      const int ti = tt / NT, tj = tt - ti * NT;
-      const int j = tj * 16 + (lane & 15);
+    if (ti_[t] < NT) {
+      const int j = tj_[t] * 16 + (lane & 15);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int i = ti * 16 + 4 * (lane >> 4) + e;
-        if (i < K && j < K) atomicAdd(out + i * K + j, acc[t][e]);
-      }
+      for (int e = 0; e < 4; ++e) mine[(ti_[t] * 16 + 4 * (lane >> 4) + e) * KP + j] = acc[t][e];
     }
   }
 }
 
+// out[i][j] = sum over blocks (in block order) of the stored tile holding (i, j) or (j, i)
+__global__ void gram_reduce_kernel(const float* __restrict__ part, int blocks, int K, int KP,
+                                   float* __restrict__ out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= K * K) return;
+  int i = e / K, j = e - (e / K) * K;
+  if ((i >> 4) > (j >> 4)) { const int t = i; i = j; j = t; }
+  const float* p = part + i * KP + j;
+  float s = 0.f;
+  for (int b = 0; b < blocks; ++b) s += p[(long long)b * KP * KP];
+  out[e] = s;
+}
+
+static int gram_kp(int K) { return K <= 16 ? 16 : K <= 32 ? 32 : K <= 48 ? 48 : K <= 64 ? 64 : K <= 96 ? 96 : 128; }
+
+static int gram_blocks(int K, long long n) {
+  return grid_for((n + GRAM_CHUNK - 1) / GRAM_CHUNK, 1, gram_blocks_cap(gram_kp(K)));
+}
+
+// floats of scratch `ddl_gram_f32` needs for K clients over n coordinates (0: K unsupported)
+DDL_API long long ddl_gram_f32_workspace(int K, long long n) {
+  if (K < 1 || K > 128 || n < 1) return 0;
+  const long long kp = gram_kp(K);
+  return (long long)gram_blocks(K, n) * kp * kp;
+}
+
 DDL_API int ddl_gram_f32(const float* X, long long ld, const float* center, int K, long long n,
-                         float* out, hipStream_t s) {
-  const long long chunks = (n + 63) / 64;
-  const int blocks = grid_for(chunks, 1, 1024);
+                         float* part, long long part_cap, float* out, hipStream_t s) {
+  if (K < 1 || K > 128 || n < 1 || part_cap < ddl_gram_f32_workspace(K, n)) return (int)hipErrorInvalidValue;
+  const int blocks = gram_blocks(K, n);
+  switch (gram_kp(K)) {
 #define GRAM_CASE(KP_) \
-  if (K <= KP_) { \
-    hipLaunchKernelGGL(gram_f32_kernel<KP_>, dim3(blocks), dim3(256), 0, s, X, ld, center, K, n, out); \
-    return (int)hipGetLastError(); \
-  }
-  GRAM_CASE(16) GRAM_CASE(32) GRAM_CASE(48) GRAM_CASE(64)
+    case KP_: hipLaunchKernelGGL(gram_f32_kernel<KP_>, dim3(blocks), dim3(256), 0, s, X, ld, center, K, n, part); break;
+    GRAM_CASE(16) GRAM_CASE(32) GRAM_CASE(48) GRAM_CASE(64) GRAM_CASE(96) GRAM_CASE(128)
 #undef GRAM_CASE
-  return (int)hipErrorInvalidValue;
+    default: return (int)hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3((K * K + 255) / 256), dim3(256), 0, s, part, blocks, K,
+                     gram_kp(K), out);
+  return (int)hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -161,15 +197,63 @@ __device__ __forceinline__ void bitonic_sort(float (&v)[KP]) {
   }
 }
 
-template <int KP>
-__global__ void coord_select_kernel(const float* __restrict__ X, long long ld, int K, long long n,
-                                    int mode, int trim, float* __restrict__ out) {
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n;
-       e += (long long)gridDim.x * blockDim.x) {
-    float v[KP];
+// ascending sort of a bitonic sequence (the half-cleaner cascade)
+template <int N>
+__device__ __forceinline__ void bitonic_merge(float (&v)[N]) {
 #pragma unroll
-    for (int i = 0; i < KP; ++i) v[i] = (i < K) ? X[i * ld + e] : INFINITY;
+  for (int j = N >> 1; j > 0; j >>= 1) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int l = i ^ j;
+      if (l > i) {
+        const float a = v[i], b = v[l];
+        v[i] = fminf(a, b);
+        v[l] = fmaxf(a, b);
+      }
+    }
+  }
+}
+
+// Register-resident sort of KP <= 128 values. Above 64 the network is split: two 64-sorts, one
+// cross compare (a[i] vs b[63-i] leaves every a <= every b, both halves bitonic) and two 64-merges,
+// so each unrolled loop nest stays small enough to be fully unrolled and the array never leaves
+// VGPRs (a single 128-wide network is only partially unrolled and falls back to scratch memory).
+template <int KP>
+__device__ __forceinline__ void sort_values(float (&v)[KP]) {
+  if constexpr (KP <= 64) {
     bitonic_sort<KP>(v);
+  } else {
+    constexpr int H = KP / 2;
+    float (&a)[H] = *reinterpret_cast<float (*)[H]>(v);
+    float (&b)[H] = *reinterpret_cast<float (*)[H]>(v + H);
+    bitonic_sort<H>(a);
+    bitonic_sort<H>(b);
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      const float x = a[i], y = b[H - 1 - i];
+      a[i] = fminf(x, y);
+      b[H - 1 - i] = fmaxf(x, y);
+    }
+    bitonic_merge<H>(a);
+    bitonic_merge<H>(b);
+  }
+}
+
+template <int KP>
+__global__ __launch_bounds__(256) void coord_select_kernel(const float* __restrict__ X, long long ld, int K, long long n,
+                                    int mode, int trim, float* __restrict__ out) {
+  // one coordinate per thread, no grid-stride loop: a loop would hoist the per-rank selection
+  // masks (loop-invariant) out of it and spill ~KP lane masks from the SGPR file
+  const long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (e < n) {
+    float v[KP];
+    const float* p = X + e;  // walk the rows by pointer increments: no per-row 64-bit offsets
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+      v[i] = (i < K) ? *p : INFINITY;
+      p += (i + 1 < K) ? ld : 0;
+    }
+    sort_values<KP>(v);
     float r;
     if (mode == 0) {
       const int a = (K - 1) / 2, b = K / 2;
@@ -194,13 +278,14 @@ __global__ void coord_select_kernel(const float* __restrict__ X, long long ld, i
 DDL_API int ddl_coord_select(const float* X, long long ld, int K, long long n, int mode, int trim,
                              float* out, hipStream_t s) {
   if (K < 1 || (mode == 1 && K - 2 * trim < 1)) return (int)hipErrorInvalidValue;
-  const int blocks = grid_for(n, 256);
+  const long long blocks = (n + 255) / 256;
+  if (blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
 #define SEL_CASE(KP_) \
   if (K <= KP_) { \
     hipLaunchKernelGGL(coord_select_kernel<KP_>, dim3(blocks), dim3(256), 0, s, X, ld, K, n, mode, trim, out); \
     return (int)hipGetLastError(); \
   }
-  SEL_CASE(8) SEL_CASE(16) SEL_CASE(32) SEL_CASE(64)
+  SEL_CASE(8) SEL_CASE(16) SEL_CASE(32) SEL_CASE(64) SEL_CASE(128)
 #undef SEL_CASE
   return (int)hipErrorInvalidValue;
 }

@@ -5,8 +5,9 @@
 //   ddl_rmsnorm_fwd/bwd   : one wave per row, rstd saved, gamma grad reduced per block then atomics
 //   ddl_swiglu_fwd/bwd    : h = silu(a) * b over the fused [a | b] projection
 //   ddl_add               : bf16 residual add
-//   ddl_attn_fwd/bwd      : causal flash attention on MFMA (16x16x16 bf16: head_dim 32/48/64/128
-//                           are all multiples of 16) with RoPE applied as q / k tiles are staged
+//   ddl_attn_fwd/bwd      : causal flash attention on the gfx950 16x16x32 bf16 MFMA (head_dim
+//                           32/48/64/128; a 16-dim remainder on 16x16x16) with RoPE applied as
+//                           q / k tiles are staged
 //                           (so RoPE costs no HBM pass), online softmax, log-sum-exp saved;
 //                           backward recomputes P in two kernels (dQ; dK+dV) and writes the
 //                           un-rotated gradients straight into the fused dQKV buffer.
@@ -289,24 +290,33 @@ DDL_API int ddl_add(const void* a, const void* b, void* y, long long n, hipStrea
 }
 
 // ---------------------------------------------------------------------------------------------
-// Causal attention on MFMA (v_mfma_f32_16x16x16_bf16, fp32 accumulate). qkv: [B][S][3][H][HD]
-// bf16 (the fused projection output), o / dout: [B][S][H][HD], lse / delta: [B][H][S] fp32, RoPE
-// tables cos/sin [S][HD/2] fp32 (interleaved pairs (2i, 2i+1)), applied as tiles are staged.
-// A workgroup owns 64 query rows (forward, dQ) or 64 key rows (dK/dV), each of its 4 waves 16 of
-// them. Every product is oriented so that the softmax-side tile an MFMA produces (accumulator:
-// lane l holds rows 4(l/16)+i of column l%16) is directly the B operand (lane l holds k-rows
-// 4(l/16)+j of column l%16) of the next MFMA:
+// Causal attention on gfx950's double-rate MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulate; a
+// head-dim remainder of 16, e.g. HD = 48 = 32 + 16, takes one v_mfma_f32_16x16x16_bf16).
+// qkv: [B][S][3][H][HD] bf16 (the fused projection output), o / dout: [B][S][H][HD], lse / delta:
+// [B][H][S] fp32, RoPE tables cos/sin [S][HD/2] fp32 (interleaved pairs (2i, 2i+1)), applied as
+// tiles are staged. A workgroup owns 64 query rows (forward, dQ) or 64 key rows (dK/dV), each of
+// its 4 waves 16 of them, and steps over the other side 32 rows at a time. Every product is
+// oriented so that the softmax-side tiles an MFMA produces are directly the B operand of the next:
 //   forward : S^T = K Q^T (keys x queries)  -> P^T   -> O^T  += V^T P^T
 //   dQ      : S^T = K Q^T, dP^T = V dO^T    -> dS^T  -> dQ^T += K^T dS^T
 //   dK, dV  : S = Q K^T,   dP = dO V^T      -> P, dS -> dV^T += dO^T P, dK^T += Q^T dS
-// so no computed tile is ever transposed; the staged K / V / Q / dO tiles are also written
-// transposed into LDS where they are A operands over the head dimension. Online softmax in the
-// exp2 domain; the backward recomputes P from the saved log-sum-exp (flash-attention 2).
-constexpr int AT = 64;  // rows per workgroup tile
+// A 32-row step computes two 16x16 score tiles (rows 0-15 and 16-31 of the step); lane l holds
+// rows 4(l/16)+i of the first and 16+4(l/16)+i of the second. The x32 MFMA sums over its k slots
+// in any order as long as A and B agree, so the B operand of the follow-on product is just the
+// 8 values the lane holds — k slot (g = l/16, j) := step row 4g+j (j < 4) or 16+4g+j-4 (j >= 4) —
+// and the A operand (a transposed V / K / dO / Q image in LDS) is read at those same rows: two
+// 8-byte reads per lane. No computed tile is ever transposed or shuffled through LDS.
+// Online softmax in the exp2 domain; the backward recomputes P from the saved log-sum-exp
+// (flash-attention 2).
+constexpr int AT = 64;   // rows per workgroup tile
+constexpr int AST = 32;  // rows per inner step (one x32 MFMA k-extent)
 constexpr float LOG2E = 1.4426950408889634f;
 
 __device__ __forceinline__ f4v mma16(s4v a, s4v b, f4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f4v mma32(s8v a, s8v b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ s4v bf4(float a, float b, float c, float d) {
   s4v r;
@@ -316,7 +326,12 @@ __device__ __forceinline__ s4v bf4(float a, float b, float c, float d) {
   r[3] = (short)f2bf(d);
   return r;
 }
-__device__ __forceinline__ s4v lds4(const bf16_t* p) { return *(const s4v*)p; }
+__device__ __forceinline__ s8v cat8(s4v a, s4v b) {
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ s8v bf8(const float* v) {
+  return cat8(bf4(v[0], v[1], v[2], v[3]), bf4(v[4], v[5], v[6], v[7]));
+}
 
 // dims d0..d0+3 (d0 % 4 == 0) of one row, RoPE-rotated when cs != nullptr
 __device__ __forceinline__ void row4(const bf16_t* row, const float* cs, const float* sn, int d0,
@@ -354,14 +369,20 @@ __device__ __forceinline__ void store4_unrot(bf16_t* dst, const float* cs, const
   *(i2v*)(dst + d0) = v;
 }
 
-// Stage rows r0..r0+63 (row t at src + t*rs) into LDS: row-major [64][HD+4] and/or transposed
-// [HD][64+4] (the padded strides keep the 8-byte fragment reads bank-conflict free); rows >= S
+// LDS images: row-major [64][HD+8] (16-byte aligned rows for the x32 A reads) and transposed
+// [HD][64+8] (8-byte reads at 4g and 16+4g of a step land on distinct bank pairs).
+template <int HD> struct AttnLds {
+  static constexpr int KP = HD + 8, VP = AT + 8;
+  static constexpr int D32 = HD / 32, R16 = (HD % 32) / 16, NT = HD / 16;
+};
+
+// Stage rows r0..r0+63 (row t at src + t*rs) into LDS (row-major and/or transposed); rows >= S
 // are zeros.
 template <int HD>
 __device__ __forceinline__ void stage_rows(const bf16_t* src, long long rs, int r0, int S,
                                            const float* rcos, const float* rsin, bf16_t* rm,
                                            bf16_t* tr) {
-  constexpr int C4 = HD / 4, KP = HD + 4, VP = AT + 4;
+  constexpr int C4 = HD / 4, KP = AttnLds<HD>::KP, VP = AttnLds<HD>::VP;
   for (int e = threadIdx.x; e < AT * C4; e += 256) {
     const int r = e / C4, d0 = (e - r * C4) * 4, t = r0 + r;
     float v[4] = {0.f, 0.f, 0.f, 0.f};
@@ -376,16 +397,46 @@ __device__ __forceinline__ void stage_rows(const bf16_t* src, long long rs, int 
   }
 }
 
-// this lane's B fragments of one row (dims 16t + 4(l/16) + j), zeros when !valid
+// One row's B fragments over the head dimension: x32 chunk c holds dims 32c + 8g + j, the x16
+// remainder dims 32*D32 + 4g + j; zeros when !valid.
+template <int HD> struct RowFrag {
+  s8v c[AttnLds<HD>::D32 > 0 ? AttnLds<HD>::D32 : 1];
+  s4v r;
+};
+
 template <int HD>
 __device__ __forceinline__ void row_frags(const bf16_t* row, const float* cs, const float* sn,
-                                          int lg, bool valid, s4v* f) {
+                                          int lg, bool valid, RowFrag<HD>& f) {
+  constexpr int D32 = AttnLds<HD>::D32;
 #pragma unroll
-  for (int t = 0; t < HD / 16; ++t) {
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    if (valid) row4(row, cs, sn, 16 * t + 4 * lg, v);
-    f[t] = bf4(v[0], v[1], v[2], v[3]);
+  for (int c = 0; c < D32; ++c) {
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (valid) {
+      row4(row, cs, sn, 32 * c + 8 * lg, v);
+      row4(row, cs, sn, 32 * c + 8 * lg + 4, v + 4);
+    }
+    f.c[c] = bf8(v);
   }
+  if constexpr (AttnLds<HD>::R16) {
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (valid) row4(row, cs, sn, 32 * D32 + 4 * lg, v);
+    f.r = bf4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+// acc += A(16 rows of a row-major LDS image, this lane's row at `arow`) . f over the head dim
+template <int HD>
+__device__ __forceinline__ f4v dot_hd(const bf16_t* arow, const RowFrag<HD>& f, int lg, f4v acc) {
+  constexpr int D32 = AttnLds<HD>::D32;
+#pragma unroll
+  for (int c = 0; c < D32; ++c) acc = mma32(*(const s8v*)(arow + 32 * c + 8 * lg), f.c[c], acc);
+  if constexpr (AttnLds<HD>::R16) acc = mma16(*(const s4v*)(arow + 32 * D32 + 4 * lg), f.r, acc);
+  return acc;
+}
+
+// A operand over a 32-row step from a transposed image row: k slots (g, j) -> rows 4g+j, 16+4g+j
+__device__ __forceinline__ s8v step_frag(const bf16_t* trow, int lg) {
+  return cat8(*(const s4v*)(trow + 4 * lg), *(const s4v*)(trow + 16 + 4 * lg));
 }
 
 template <int HD>
@@ -395,7 +446,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
                                                        const float* __restrict__ rcos,
                                                        const float* __restrict__ rsin, int S, int H,
                                                        float scale) {
-  constexpr int NT = HD / 16, KP = HD + 4, VP = AT + 4;
+  using L = AttnLds<HD>;
+  constexpr int NT = L::NT, KP = L::KP, VP = L::VP;
   __shared__ __attribute__((aligned(16))) bf16_t Ks[AT * KP];
   __shared__ __attribute__((aligned(16))) bf16_t Vt[HD * VP];
   const int b = blockIdx.z, h = blockIdx.y, qt = blockIdx.x;
@@ -405,7 +457,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
   const int q = qt * AT + wv * 16 + lq, qmax = qt * AT + wv * 16 + 15;
   const bool qv = q < S;
   const float sl2 = scale * LOG2E;
-  s4v qf[NT];
+  RowFrag<HD> qf;
   row_frags<HD>(base + (long long)q * rs, rcos + (long long)q * (HD / 2),
                 rsin + (long long)q * (HD / 2), lg, qv, qf);
   f4v acc[NT];
@@ -418,26 +470,25 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
     stage_rows<HD>(base + 2 * ro, rs, kt * AT, S, nullptr, nullptr, nullptr, Vt);
     __syncthreads();
 #pragma unroll
-    for (int ks = 0; ks < AT / 16; ++ks) {
-      const int key0 = kt * AT + ks * 16;
+    for (int ks = 0; ks < AT / AST; ++ks) {
+      const int key0 = kt * AT + ks * AST;
       if (key0 > qmax || key0 >= S) break;  // wave-uniform: the causal / sequence edge
-      f4v s = {0.f, 0.f, 0.f, 0.f};
+      const f4v s0 = dot_hd<HD>(Ks + (ks * AST + lq) * KP, qf, lg, f4v{0.f, 0.f, 0.f, 0.f});
+      const f4v s1 = dot_hd<HD>(Ks + (ks * AST + 16 + lq) * KP, qf, lg, f4v{0.f, 0.f, 0.f, 0.f});
+      float x[8], mx = -INFINITY;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) s = mma16(lds4(Ks + (ks * 16 + lq) * KP + 16 * t + 4 * lg), qf[t], s);
-      float x[4], mx = -INFINITY;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = key0 + 4 * lg + i;
-        x[i] = (key <= q && key < S) ? s[i] * sl2 : -INFINITY;
+      for (int i = 0; i < 8; ++i) {
+        const int key = key0 + (i < 4 ? 4 * lg + i : 16 + 4 * lg + i - 4);
+        x[i] = (key <= q && key < S) ? (i < 4 ? s0[i] : s1[i - 4]) * sl2 : -INFINITY;
         mx = fmaxf(mx, x[i]);
       }
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mn = fmaxf(m, mx);
       const float corr = (mn == -INFINITY) ? 1.f : exp2f(m - mn);
-      float p[4], ps = 0.f;
+      float p[8], ps = 0.f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < 8; ++i) {
         p[i] = (x[i] == -INFINITY) ? 0.f : exp2f(x[i] - mn);
         ps += p[i];
       }
@@ -445,11 +496,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
       ps += __shfl_xor(ps, 32, 64);
       l = l * corr + ps;
       m = mn;
-      const s4v pb = bf4(p[0], p[1], p[2], p[3]);
+      const s8v pb = bf8(p);
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         acc[t] *= corr;
-        acc[t] = mma16(lds4(Vt + (16 * t + lq) * VP + ks * 16 + 4 * lg), pb, acc[t]);
+        acc[t] = mma32(step_frag(Vt + (16 * t + lq) * VP + ks * AST, lg), pb, acc[t]);
       }
     }
   }
@@ -468,7 +519,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout,
     const float* __restrict__ lse, float* __restrict__ delta, bf16_t* __restrict__ dqkv,
     const float* __restrict__ rcos, const float* __restrict__ rsin, int S, int H, float scale) {
-  constexpr int NT = HD / 16, KP = HD + 4, VP = AT + 4;
+  using L = AttnLds<HD>;
+  constexpr int NT = L::NT, KP = L::KP, VP = L::VP;
   __shared__ __attribute__((aligned(16))) bf16_t Ks[AT * KP];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[AT * KP];
   __shared__ __attribute__((aligned(16))) bf16_t Kt[HD * VP];
@@ -481,20 +533,20 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
   const float sl2 = scale * LOG2E;
   const float* cs = rcos + (long long)q * (HD / 2);
   const float* sn = rsin + (long long)q * (HD / 2);
-  s4v qf[NT], df[NT];
+  RowFrag<HD> qf, df;
   row_frags<HD>(base + (long long)q * rs, cs, sn, lg, qv, qf);
   const bf16_t* orow = o + ((long long)b * S + q) * ro + h * HD;
   const bf16_t* drow = dout + ((long long)b * S + q) * ro + h * HD;
+  row_frags<HD>(drow, nullptr, nullptr, lg, qv, df);
   float dd = 0.f;
+  if (qv) {  // delta = rowsum(dO * O): this lane's quarter of the head dims, then the wave sum
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    float dv[4] = {0.f, 0.f, 0.f, 0.f}, ov[4] = {0.f, 0.f, 0.f, 0.f};
-    if (qv) {
-      row4(drow, nullptr, nullptr, 16 * t + 4 * lg, dv);
-      row4(orow, nullptr, nullptr, 16 * t + 4 * lg, ov);
+    for (int d0 = 4 * lg; d0 < HD; d0 += 16) {
+      float dv[4], ov[4];
+      row4(drow, nullptr, nullptr, d0, dv);
+      row4(orow, nullptr, nullptr, d0, ov);
+      dd += dv[0] * ov[0] + dv[1] * ov[1] + dv[2] * ov[2] + dv[3] * ov[3];
     }
-    df[t] = bf4(dv[0], dv[1], dv[2], dv[3]);
-    dd += dv[0] * ov[0] + dv[1] * ov[1] + dv[2] * ov[2] + dv[3] * ov[3];
   }
   dd += __shfl_xor(dd, 16, 64);
   dd += __shfl_xor(dd, 32, 64);
@@ -509,26 +561,26 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
     stage_rows<HD>(base + 2 * ro, rs, kt * AT, S, nullptr, nullptr, Vs, nullptr);
     __syncthreads();
 #pragma unroll
-    for (int ks = 0; ks < AT / 16; ++ks) {
-      const int key0 = kt * AT + ks * 16;
+    for (int ks = 0; ks < AT / AST; ++ks) {
+      const int key0 = kt * AT + ks * AST;
       if (key0 > qmax || key0 >= S) break;
-      f4v s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+      const f4v z = {0.f, 0.f, 0.f, 0.f};
+      const f4v s0 = dot_hd<HD>(Ks + (ks * AST + lq) * KP, qf, lg, z);
+      const f4v s1 = dot_hd<HD>(Ks + (ks * AST + 16 + lq) * KP, qf, lg, z);
+      const f4v p0 = dot_hd<HD>(Vs + (ks * AST + lq) * KP, df, lg, z);
+      const f4v p1 = dot_hd<HD>(Vs + (ks * AST + 16 + lq) * KP, df, lg, z);
+      float ds[8];
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        s = mma16(lds4(Ks + (ks * 16 + lq) * KP + 16 * t + 4 * lg), qf[t], s);
-        dp = mma16(lds4(Vs + (ks * 16 + lq) * KP + 16 * t + 4 * lg), df[t], dp);
+      for (int i = 0; i < 8; ++i) {
+        const int key = key0 + (i < 4 ? 4 * lg + i : 16 + 4 * lg + i - 4);
+        const float sv = i < 4 ? s0[i] : s1[i - 4], dp = i < 4 ? p0[i] : p1[i - 4];
+        const float pr = (qv && key <= q && key < S) ? exp2f(sv * sl2 - L2) : 0.f;
+        ds[i] = pr * (dp - dd) * scale;
       }
-      float ds[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = key0 + 4 * lg + i;
-        const float pr = (qv && key <= q && key < S) ? exp2f(s[i] * sl2 - L2) : 0.f;
-        ds[i] = pr * (dp[i] - dd) * scale;
-      }
-      const s4v db = bf4(ds[0], ds[1], ds[2], ds[3]);
+      const s8v db = bf8(ds);
 #pragma unroll
       for (int t = 0; t < NT; ++t)
-        acc[t] = mma16(lds4(Kt + (16 * t + lq) * VP + ks * 16 + 4 * lg), db, acc[t]);
+        acc[t] = mma32(step_frag(Kt + (16 * t + lq) * VP + ks * AST, lg), db, acc[t]);
     }
   }
   if (qv) {
@@ -544,7 +596,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, bf16_t* __restrict__ dqkv, const float* __restrict__ rcos,
     const float* __restrict__ rsin, int S, int H, float scale) {
-  constexpr int NT = HD / 16, KP = HD + 4, VP = AT + 4;
+  using L = AttnLds<HD>;
+  constexpr int NT = L::NT, KP = L::KP, VP = L::VP;
   __shared__ __attribute__((aligned(16))) bf16_t Qs[AT * KP];
   __shared__ __attribute__((aligned(16))) bf16_t Ds[AT * KP];
   __shared__ __attribute__((aligned(16))) bf16_t Qt[HD * VP];
@@ -560,7 +613,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
   const float sl2 = scale * LOG2E;
   const float* cs = rcos + (long long)key * (HD / 2);
   const float* sn = rsin + (long long)key * (HD / 2);
-  s4v kf[NT], vf[NT];
+  RowFrag<HD> kf, vf;
   row_frags<HD>(base + ro + (long long)key * rs, cs, sn, lg, kv, kf);
   row_frags<HD>(base + 2 * ro + (long long)key * rs, nullptr, nullptr, lg, kv, vf);
   f4v dk[NT], dv[NT];
@@ -577,28 +630,28 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
     }
     __syncthreads();
 #pragma unroll
-    for (int qs = 0; qs < AT / 16; ++qs) {
-      const int q0 = qt * AT + qs * 16;
+    for (int qs = 0; qs < AT / AST; ++qs) {
+      const int q0 = qt * AT + qs * AST;
       if (q0 >= S) break;
-      if (q0 + 15 < kmin) continue;  // every query of the subtile precedes every key of the wave
-      f4v s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+      if (q0 + AST - 1 < kmin) continue;  // every query of the step precedes every key of the wave
+      const f4v z = {0.f, 0.f, 0.f, 0.f};
+      const f4v s0 = dot_hd<HD>(Qs + (qs * AST + lq) * KP, kf, lg, z);
+      const f4v s1 = dot_hd<HD>(Qs + (qs * AST + 16 + lq) * KP, kf, lg, z);
+      const f4v d0 = dot_hd<HD>(Ds + (qs * AST + lq) * KP, vf, lg, z);
+      const f4v d1 = dot_hd<HD>(Ds + (qs * AST + 16 + lq) * KP, vf, lg, z);
+      float p[8], ds[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = qs * AST + (i < 4 ? 4 * lg + i : 16 + 4 * lg + i - 4), qi = qt * AT + r;
+        const float sv = i < 4 ? s0[i] : s1[i - 4], dp = i < 4 ? d0[i] : d1[i - 4];
+        p[i] = (kv && qi >= key && qi < S) ? exp2f(sv * sl2 - Ls[r]) : 0.f;
+        ds[i] = p[i] * (dp - Dl[r]) * scale;
+      }
+      const s8v pb = bf8(p), db = bf8(ds);
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        s = mma16(lds4(Qs + (qs * 16 + lq) * KP + 16 * t + 4 * lg), kf[t], s);
-        dp = mma16(lds4(Ds + (qs * 16 + lq) * KP + 16 * t + 4 * lg), vf[t], dp);
-      }
-      float p[4], ds[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = qs * 16 + 4 * lg + i, qi = qt * AT + r;
-        p[i] = (kv && qi >= key && qi < S) ? exp2f(s[i] * sl2 - Ls[r]) : 0.f;
-        ds[i] = p[i] * (dp[i] - Dl[r]) * scale;
-      }
-      const s4v pb = bf4(p[0], p[1], p[2], p[3]), db = bf4(ds[0], ds[1], ds[2], ds[3]);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        dv[t] = mma16(lds4(Dt + (16 * t + lq) * VP + qs * 16 + 4 * lg), pb, dv[t]);
-        dk[t] = mma16(lds4(Qt + (16 * t + lq) * VP + qs * 16 + 4 * lg), db, dk[t]);
+        dv[t] = mma32(step_frag(Dt + (16 * t + lq) * VP + qs * AST, lg), pb, dv[t]);
+        dk[t] = mma32(step_frag(Qt + (16 * t + lq) * VP + qs * AST, lg), db, dk[t]);
       }
     }
   }

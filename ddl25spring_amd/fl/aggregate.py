@@ -97,7 +97,7 @@ class Krum(_Sharded):
     def __call__(self, ctx, rows, counts, P):
         K = sum(counts)
         shard, S, Pp = self.shard(ctx, rows, counts)
-        gram = Fn.gram(shard) if K <= 64 else shard @ shard.t()
+        gram = Fn.gram(shard)
         ctx.all_reduce(gram)
         sq = torch.diagonal(gram)
         d2 = (sq[:, None] + sq[None, :] - 2 * gram).clamp_min(0)

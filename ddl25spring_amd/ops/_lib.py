@@ -154,7 +154,8 @@ _SIGS = {
     # aggregate.hip
     "ddl_weighted_sum": [vp, i64, vp, i32, i64, vp, i32, vp],
     "ddl_broadcast_rows": [vp, vp, i64, i32, i64, vp, i64, vp],
-    "ddl_gram_f32": [vp, i64, vp, i32, i64, vp, vp],
+    "ddl_gram_f32": [vp, i64, vp, i32, i64, vp, i64, vp, vp],
+    "ddl_gram_f32_workspace": [i32, i64],
     "ddl_coord_select": [vp, i64, i32, i64, i32, i32, vp, vp],
 }
 
@@ -179,7 +180,8 @@ _SIGS.update({
     "ddl_headf_train": [ctypes.POINTER(HeadFArgs), vp],
     "ddl_bnf_channel_sum": [vp, vp, i64, vp, i64, i32, i32, vp],
 })
-_RESTYPES = {"ddl_convf32_slots": ctypes.c_longlong, "ddl_convf32_workspace": ctypes.c_longlong}
+_RESTYPES = {"ddl_convf32_slots": ctypes.c_longlong, "ddl_convf32_workspace": ctypes.c_longlong,
+             "ddl_gram_f32_workspace": ctypes.c_longlong}
 
 _OPTIONAL_SIGS: dict[str, list] = {}
 

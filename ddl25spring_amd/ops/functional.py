@@ -1227,22 +1227,39 @@ def broadcast_rows(src, dst, shadow=None):
           "broadcast_rows")
 
 
+MAX_ROBUST_CLIENTS = 128  # K limit of the native Gram / coordinate-selection kernels
+
+
+def _robust_k(K, what):
+    if not 1 <= K <= MAX_ROBUST_CLIENTS:
+        raise ValueError(f"{what}: K={K} client rows; the native kernel takes 1..{MAX_ROBUST_CLIENTS} "
+                         "(shard the clients over more GPUs, or pre-aggregate buckets of clients)")
+
+
 def gram(X, center=None):
-    """(X - c)(X - c)^T for X [K, n] fp32 on the exact-fp32 MFMA (K <= 64)."""
+    """(X - c)(X - c)^T for X [K, n] fp32 (K <= 128) on the exact-fp32 MFMA; per-block partial
+    Grams summed in a fixed order, so the result is bit-reproducible."""
     if not X.is_cuda:
         return ref.gram(X, center)
-    K = X.shape[0]
-    out = torch.zeros(K, K, dtype=torch.float32, device=X.device)
-    check(_lib.kernels().ddl_gram_f32(ptr(X), X.stride(0), ptr(center), K, X.shape[1], ptr(out),
+    K, n = X.shape
+    _robust_k(K, "gram")
+    assert X.dtype == torch.float32 and X.stride(1) == 1
+    out = torch.empty(K, K, dtype=torch.float32, device=X.device)
+    cap = _lib.kernels().ddl_gram_f32_workspace(K, n)
+    part = torch.empty(max(cap, 1), dtype=torch.float32, device=X.device)
+    check(_lib.kernels().ddl_gram_f32(ptr(X), X.stride(0), ptr(center), K, n, ptr(part), cap, ptr(out),
                                       stream()), "gram_f32")
+    out._keep = part  # the scratch must outlive the (asynchronous) launches
     return out
 
 
 def coord_select(X, mode: str, trim: int = 0):
     """Coordinate-wise median ('median') or trimmed mean ('trimmed') over K rows of X [K, n]."""
     m = 0 if mode == "median" else 1
-    if not X.is_cuda or X.shape[0] > 64:
+    if not X.is_cuda:
         return ref.coord_select(X, m, trim)
+    _robust_k(X.shape[0], f"coord_select({mode})")
+    assert X.dtype == torch.float32 and X.stride(1) == 1
     out = torch.empty(X.shape[1], dtype=torch.float32, device=X.device)
     check(_lib.kernels().ddl_coord_select(ptr(X), X.stride(0), X.shape[0], X.shape[1], m, trim,
                                           ptr(out), stream()), "coord_select")

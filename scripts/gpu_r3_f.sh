@@ -20,4 +20,15 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_f32f -o ru
 tail -1 gpurun_out/r3f_prof.log
 db=$(ls gpurun_out/prof_f32f/*/run_results.db gpurun_out/prof_f32f/run_results.db 2>/dev/null | head -n 1 || true)
 [ -n "$db" ] && python scripts/prof_summary.py "$db" --top 40 > gpurun_out/r3f_prof_summary.txt
+timeout -k 10 300 python -u benchmarks/bench_llm.py --steps 30 --warmup 5 > gpurun_out/r3f_llm.log 2>&1 || { tail -20 gpurun_out/r3f_llm.log; exit 1; }
+tail -1 gpurun_out/r3f_llm.log
+mkdir -p gpurun_out/prof_llm
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_llm -o run -- python -u benchmarks/bench_llm.py --steps 10 --warmup 3 \
+  > gpurun_out/r3f_prof_llm.log 2>&1 || { tail -20 gpurun_out/r3f_prof_llm.log; exit 1; }
+db=$(ls gpurun_out/prof_llm/*/run_results.db gpurun_out/prof_llm/run_results.db 2>/dev/null | head -n 1 || true)
+[ -n "$db" ] && python scripts/prof_summary.py "$db" --top 40 > gpurun_out/r3f_prof_llm_summary.txt
+timeout -k 10 300 python -u bench.py --steps 12 --warmup 1 --eval > gpurun_out/r3f_bench_eval.log 2>&1 || { tail -20 gpurun_out/r3f_bench_eval.log; exit 1; }
+tail -1 gpurun_out/r3f_bench_eval.log
+timeout -k 10 600 python -u benchmarks/bench_byzantine.py --steps 2 --warmup 1 --acc-rounds 8 > gpurun_out/r3f_byz.log 2>&1 || { tail -20 gpurun_out/r3f_byz.log; exit 1; }
+tail -1 gpurun_out/r3f_byz.log
 exit 0

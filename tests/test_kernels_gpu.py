@@ -359,7 +359,7 @@ def test_aggregation(cuda):
     sh = torch.zeros(G, P + 7, dtype=torch.bfloat16, device=cuda)
     Fn.broadcast_rows(out, dst[:, :P], sh[:, :P])
     assert torch.equal(dst[:, :P], out.expand(G, P)) and dst[:, P:].abs().max() == 0
-    for K in (3, 8, 20, 33, 64):
+    for K in (3, 8, 20, 33, 64, 65, 100, 128):
         X = torch.randn(K, 20000, device=cuda)
         c = torch.randn(20000, device=cuda)
         _close(Fn.gram(X, c), ref.gram(X.cpu().double(), c.cpu().double()).float(), rel=1e-5)
@@ -367,6 +367,19 @@ def test_aggregation(cuda):
             if mode == "trimmed" and K - 2 * trim < 1:
                 continue
             _close(Fn.coord_select(X, mode, trim), ref.coord_select(X.cpu(), 0 if mode == "median" else 1, trim), rel=1e-6)
+
+
+def test_robust_kernels_deterministic_and_bounded(cuda):
+    """The Gram sums per-block partials in a fixed order (no float atomics): bit-identical across
+    calls, so Krum's argsort never flips between runs; K > 128 raises instead of falling back."""
+    X = torch.randn(100, 300_000, device=cuda)
+    g = [Fn.gram(X) for _ in range(3)]
+    assert torch.equal(g[0], g[1]) and torch.equal(g[0], g[2])
+    assert torch.equal(g[0], g[0].t())  # symmetric by construction (mirrored tiles)
+    with pytest.raises(ValueError, match="128"):
+        Fn.gram(torch.randn(129, 64, device=cuda))
+    with pytest.raises(ValueError, match="128"):
+        Fn.coord_select(torch.randn(129, 64, device=cuda), "median")
 
 
 def test_prep_images(cuda):

@@ -77,8 +77,11 @@ def test_federated_gan_two_ranks_share_gpu(tmp_path):
     assert res["returncode"] == 0, res
     a, b = torch.load(w1, weights_only=True), torch.load(w2, weights_only=True)
     assert a.shape == b.shape and torch.isfinite(b).all()
-    # same clients, same data, same noise; the device kernels may sum in a different order
-    assert ((a - b).norm() / a.norm()).item() < 1e-3
+    # same clients, same data, same noise. One process batches both clients (groups=2), each rank
+    # runs one (groups=1): different split-K / tile plans round the bf16 GEMMs differently, and 4
+    # Adam steps amplify that to ~1e-3 of the weights (measured 1.3e-3); a wrong client->rank
+    # assignment or noise stream gives O(1)
+    assert ((a - b).norm() / a.norm()).item() < 1e-2
 
 
 def test_vfl_gan_bench_two_ranks_share_gpu():
