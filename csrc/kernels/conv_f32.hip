@@ -1,5 +1,9 @@
-// Reference-precision (fp32) implicit-GEMM convolution on CDNA4's exact-fp32 MFMA
-// (v_mfma_f32_16x16x4_f32: fp32 operands, fp32 accumulate, bitwise an fmaf chain), NHWC fp32.
+// Reference-precision (fp32) implicit-GEMM convolution, NHWC fp32, in two product engines:
+//   * exact: CDNA4's fp32 MFMA (v_mfma_f32_16x16x4_f32: fp32 operands, fp32 accumulate, bitwise
+//     an fmaf chain);
+//   * X6: fp32 products as six bf16 piece products on the double-rate v_mfma_f32_16x16x32_bf16
+//     (exact 3-way operand split, dropped terms <= one fp32 rounding; see split3) — 2.7x fewer
+//     MFMA cycles per step, same loads / LDS images / epilogues / determinism.
 //
 // The reference trains every model in fp32 (stock nn.Conv2d / nn.Linear, reference
 // lab/tutorial_1a/hfl_complete.py:39-80); this is the kernel family behind the framework's fp32
@@ -295,8 +299,39 @@ __device__ __forceinline__ void fzero_slot(const ConvF32Args& a, const FGeo& o) 
   }
 }
 
+// ------------------------------------------------------------------------------------ X6 math
+// fp32 products on the bf16 MFMA (X6 = 1). Every fp32 operand value splits EXACTLY into three
+// bf16 pieces by truncation, x = xh + xm + xl (xh: the top 8 significand bits, xm the next 8, xl
+// the last 8 — each remainder is exact in fp32 and the last fits bf16 exactly). Of the nine piece
+// products the six down to 2^-16 relative are kept (hh, hm, mh, hl, lh, mm); the dropped ml, lm,
+// ll are <= 2^-24 relative, the size of one fp32 rounding, and every bf16 x bf16 product is exact
+// in the fp32 accumulator. A 16-deep reduction step becomes 16 k values x 6 piece pairs = 96 k
+// slots = three v_mfma_f32_16x16x32_bf16 instead of four v_mfma_f32_16x16x4_f32: lane group g
+// holds k values 4g..4g+3 (the same ds_read_b128 fragment as the exact path), slots j < 4 of an
+// MFMA take one piece pair and j >= 4 the next:
+//   MFMA 0: A (h | h)  B (h | m)      MFMA 1: A (m | h)  B (h | l)      MFMA 2: A (l | m)  B (h | m)
+// At 16 cycles per x32 bf16 MFMA vs 32 per x4 fp32 MFMA the step costs 48 instead of 128 MFMA
+// cycles per 16x16 tile; the split is 4 VALU ops per value on the fragments (shared across the
+// wave's tiles). Numerics match the exact fp32 MFMA path to fp32 rounding (tests/test_fp32_gpu.py).
+__device__ __forceinline__ void split3(float4 v, s4v& h, s4v& m, s4v& l) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t u = __float_as_uint(x[i]);
+    const float r1 = x[i] - __uint_as_float(u & 0xFFFF0000u);
+    const uint32_t um = __float_as_uint(r1);
+    const float r2 = r1 - __uint_as_float(um & 0xFFFF0000u);
+    h[i] = (short)(u >> 16);
+    m[i] = (short)(um >> 16);
+    l[i] = (short)(__float_as_uint(r2) >> 16);
+  }
+}
+__device__ __forceinline__ s8v cat44(s4v a, s4v b) {
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 // ------------------------------------------------------------------------------------ main kernel
-template <int MODE, int BP, int BQ>
+template <int MODE, int BP, int BQ, int X6>
 __global__ __launch_bounds__(256, 2) void convf32_kernel(ConvF32Args a) {
   constexpr int WP = BP / 2, WQ = BQ / 2, TP = WP / 16, TQ = WQ / 16;
   constexpr int SP = BP * 16, SQ = BQ * 16;     // floats per operand image
@@ -570,16 +605,34 @@ __global__ __launch_bounds__(256, 2) void convf32_kernel(ConvF32Args a) {
 #pragma unroll
       for (int tj = 0; tj < TQ; ++tj)
         bfr[tj] = *(const float4*)(Qs + lds_off(wq * WQ + tj * 16 + (lane & 15), lane >> 4));
+      if constexpr (X6) {
+        s4v ah[TP], am[TP], al[TP], bh[TQ], bm[TQ], bl[TQ];
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4)
+        for (int ti = 0; ti < TP; ++ti) split3(af[ti], ah[ti], am[ti], al[ti]);
+#pragma unroll
+        for (int tj = 0; tj < TQ; ++tj) split3(bfr[tj], bh[tj], bm[tj], bl[tj]);
 #pragma unroll
         for (int ti = 0; ti < TP; ++ti)
 #pragma unroll
           for (int tj = 0; tj < TQ; ++tj) {
-            const float av = s4 == 0 ? af[ti].x : s4 == 1 ? af[ti].y : s4 == 2 ? af[ti].z : af[ti].w;
-            const float bv = s4 == 0 ? bfr[tj].x : s4 == 1 ? bfr[tj].y : s4 == 2 ? bfr[tj].z : bfr[tj].w;
-            acc[ti][tj] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[ti][tj], 0, 0, 0);
+            f4v c = acc[ti][tj];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat44(ah[ti], ah[ti]), cat44(bh[tj], bm[tj]), c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat44(am[ti], ah[ti]), cat44(bh[tj], bl[tj]), c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat44(al[ti], am[ti]), cat44(bh[tj], bm[tj]), c, 0, 0, 0);
+            acc[ti][tj] = c;
           }
+      } else {
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+          for (int ti = 0; ti < TP; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < TQ; ++tj) {
+              const float av = s4 == 0 ? af[ti].x : s4 == 1 ? af[ti].y : s4 == 2 ? af[ti].z : af[ti].w;
+              const float bv = s4 == 0 ? bfr[tj].x : s4 == 1 ? bfr[tj].y : s4 == 2 ? bfr[tj].z : bfr[tj].w;
+              acc[ti][tj] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[ti][tj], 0, 0, 0);
+            }
+      }
       if (more) store_step(cur ^ 1, kt + 1);
       __syncthreads();
     }
@@ -701,7 +754,7 @@ DDL_API long long ddl_convf32_workspace(const ConvF32Args* ap, int mode, int cfg
   return (long long)ap->split_k * ap->G * nph * qm * Pd;
 }
 
-template <int MODE, int BP, int BQ>
+template <int MODE, int BP, int BQ, int X6>
 static int launch_tile(ConvF32Args a, hipStream_t s) {
   long long Pd, Qd, Qmax, Kr;
   int nph;
@@ -716,7 +769,7 @@ static int launch_tile(ConvF32Args a, hipStream_t s) {
     if (!a.partial || need > a.partial_cap) return (int)hipErrorInvalidValue;
   }
   const dim3 grid((unsigned)(ntp * ntq), (unsigned)(nph * split), (unsigned)a.G);
-  hipLaunchKernelGGL((convf32_kernel<MODE, BP, BQ>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((convf32_kernel<MODE, BP, BQ, X6>), grid, dim3(256), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || split == 1) return (int)e;
   if (MODE == F_WGRAD) {
@@ -730,14 +783,20 @@ static int launch_tile(ConvF32Args a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// cfg = bp/16 | (bq/16) << 8 | x6 << 16 (x6: fp32 products on the bf16 MFMA, see split3)
+template <int MODE, int X6>
+static int launch_math(const ConvF32Args& a, int bp, int bq, hipStream_t s) {
+  if (bp == 64 && bq == 64) return launch_tile<MODE, 64, 64, X6>(a, s);
+  if (bp == 64 && bq == 128) return launch_tile<MODE, 64, 128, X6>(a, s);
+  if (bp == 128 && bq == 64) return launch_tile<MODE, 128, 64, X6>(a, s);
+  if (bp == 128 && bq == 128) return launch_tile<MODE, 128, 128, X6>(a, s);
+  return (int)hipErrorInvalidValue;
+}
+
 template <int MODE>
 static int launch_mode(const ConvF32Args& a, int cfg, hipStream_t s) {
   const int bp = (cfg & 0xff) * 16, bq = ((cfg >> 8) & 0xff) * 16;
-  if (bp == 64 && bq == 64) return launch_tile<MODE, 64, 64>(a, s);
-  if (bp == 64 && bq == 128) return launch_tile<MODE, 64, 128>(a, s);
-  if (bp == 128 && bq == 64) return launch_tile<MODE, 128, 64>(a, s);
-  if (bp == 128 && bq == 128) return launch_tile<MODE, 128, 128>(a, s);
-  return (int)hipErrorInvalidValue;
+  return (cfg >> 16) & 1 ? launch_math<MODE, 1>(a, bp, bq, s) : launch_math<MODE, 0>(a, bp, bq, s);
 }
 
 DDL_API int ddl_convf32(const ConvF32Args* ap, int mode, int cfg, hipStream_t s) {

@@ -70,6 +70,32 @@ def cfg_of(bp: int, bq: int) -> int:
     return (bp // 16) | ((bq // 16) << 8)
 
 
+# Product engine of the fp32 convolutions (csrc/kernels/conv_f32.hip):
+#   "mfma32": exact fp32 MFMA (v_mfma_f32_16x16x4_f32);
+#   "x6"    : each fp32 operand split exactly into 3 bf16 pieces, the 6 piece products above one
+#             fp32 rounding on the double-rate bf16 MFMA (2.7x fewer MFMA cycles per step).
+MATHS = ("mfma32", "x6")
+_MATH = [os.environ.get("DDL_F32_MATH", "mfma32")]
+if _MATH[0] not in MATHS:
+    raise ValueError(f"DDL_F32_MATH={_MATH[0]!r}: expected one of {MATHS}")
+
+
+def math() -> str:
+    return _MATH[0]
+
+
+def set_math(name: str) -> None:
+    if name not in MATHS:
+        raise ValueError(f"fp32 conv math {name!r}: expected one of {MATHS}")
+    if name != _MATH[0]:
+        _MATH[0] = name
+        _PLANS.clear()  # plans are tuned per engine
+
+
+def _cfg(cfg: int) -> int:
+    return cfg | (1 << 16) if _MATH[0] == "x6" else cfg
+
+
 _PLANS: dict = {}
 _OVERRIDE: dict = {}
 _MODE_NAMES = ("fwd", "dgrad", "wgrad")
@@ -87,6 +113,8 @@ def _tuned(mode: int, g):
             with open(_TUNED_PATH) as f:
                 _TUNED = json.load(f).get("plans", {})
     key = f"{_MODE_NAMES[mode]}:{g.G},{g.N},{g.H},{g.W},{g.C},{g.K},{g.R},{g.S},{g.stride},{g.pad}"
+    if _MATH[0] != "mfma32":
+        key = f"{_MATH[0]}:{key}"
     p = _TUNED.get(key)
     return None if p is None else (cfg_of(p[0], p[1]), int(p[2]))
 
@@ -139,6 +167,7 @@ def _launch(a, mode: int, geom, device, split_k: int = 0) -> None:
     if split_k:
         split = split_k
     a.split_k = split
+    cfg = _cfg(cfg)
     if split > 1:
         need = lib.ddl_convf32_workspace(ctypes.byref(a), mode, cfg)
         buf = workspace(device)
@@ -151,7 +180,7 @@ def _launch(a, mode: int, geom, device, split_k: int = 0) -> None:
 
 def _slots(a, mode: int, geom) -> int:
     cfg, _ = plan(mode, geom)
-    return int(_lib.kernels().ddl_convf32_slots(ctypes.byref(a), mode, cfg))
+    return int(_lib.kernels().ddl_convf32_slots(ctypes.byref(a), mode, _cfg(cfg)))
 
 
 def _xform(in_bn):

@@ -58,7 +58,10 @@ def main():
     ap.add_argument("--groups", type=int, nargs="*", default=[8, 1])
     ap.add_argument("--batch", type=int, default=100)
     ap.add_argument("--budget-s", type=float, default=240.0)
+    ap.add_argument("--math", default="mfma32", choices=list(F32.MATHS))
     a = ap.parse_args()
+    F32.set_math(a.math)
+    prefix = "" if a.math == "mfma32" else f"{a.math}:"
     dev = torch.device("cuda")
     t_start = time.time()
     plans, report = {}, []
@@ -95,9 +98,9 @@ def main():
                 ms, bp, bq, split = res[0]
                 hms = next(r[0] for r in res if F32.cfg_of(r[1], r[2]) == heur[0] and r[3] == heur[1]) \
                     if any(F32.cfg_of(r[1], r[2]) == heur[0] and r[3] == heur[1] for r in res) else None
-                key = f"{name}:{g.G},{g.N},{g.H},{g.W},{g.C},{g.K},{g.R},{g.S},{g.stride},{g.pad}"
+                key = f"{prefix}{name}:{g.G},{g.N},{g.H},{g.W},{g.C},{g.K},{g.R},{g.S},{g.stride},{g.pad}"
                 plans[key] = [bp, bq, split]
-                row = dict(mode=name, G=g.G, N=g.N, H=g.H, C=g.C, K=g.K, R=g.R, stride=g.stride,
+                row = dict(math=a.math, mode=name, G=g.G, N=g.N, H=g.H, C=g.C, K=g.K, R=g.R, stride=g.stride,
                            best_ms=round(ms, 4), plan=[bp, bq, split], tflops=round(flops / ms / 1e9, 1),
                            pct_peak=round(100 * flops / ms / 1e9 / PEAK_TF, 1),
                            heuristic_ms=None if hms is None else round(hms, 4))

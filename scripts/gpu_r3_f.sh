@@ -3,13 +3,18 @@
 set -o pipefail
 mkdir -p gpurun_out/prof_f32f
 export PYTHONUNBUFFERED=1
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
   > gpurun_out/r3f_gputests.log 2>&1
 rc=$?
 tail -5 gpurun_out/r3f_gputests.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python -u bench.py --steps 5 --warmup 1 > gpurun_out/r3f_bench_fp32.log 2>&1 || { tail -20 gpurun_out/r3f_bench_fp32.log; exit 1; }
 tail -1 gpurun_out/r3f_bench_fp32.log
+DDL_F32_MATH=x6 timeout -k 10 400 python -u bench.py --steps 5 --warmup 1 > gpurun_out/r3f_bench_x6.log 2>&1 || { tail -20 gpurun_out/r3f_bench_x6.log; exit 1; }
+tail -1 gpurun_out/r3f_bench_x6.log
+timeout -k 10 400 python -u scripts/conv_f32_tune.py --math x6 --out gpurun_out/f32_plans_x6_g8.json --groups 8 --budget-s 300 \
+  > gpurun_out/r3f_tune_x6.log 2>&1 || { tail -5 gpurun_out/r3f_tune_x6.log; exit 1; }
+tail -2 gpurun_out/r3f_tune_x6.log
 timeout -k 10 400 python -u bench.py --steps 5 --warmup 1 --deterministic > gpurun_out/r3f_bench_det.log 2>&1 || { tail -20 gpurun_out/r3f_bench_det.log; exit 1; }
 tail -1 gpurun_out/r3f_bench_det.log
 timeout -k 10 400 python -u bench.py --steps 5 --warmup 1 --precision bf16 > gpurun_out/r3f_bench_bf16.log 2>&1 || { tail -20 gpurun_out/r3f_bench_bf16.log; exit 1; }

@@ -106,7 +106,8 @@ def test_robust_aggregation_k100_native(cuda, agg):
     # the plain mean is dragged to ~1.2x |ref| away; the coordinate rules keep a small trimming
     # bias (20 of the trimmed values per side are honest), Krum returns one honest client
     assert ((rows.mean(0) - ref).norm() / ref.norm()).item() > 1.0
-    assert ((out_gpu - ref).norm() / ref.norm()).item() < 0.3
+    # (Krum returns ONE honest client: its own noise, 0.05 * sqrt(P) / |ref| ~ 0.5, remains)
+    assert ((out_gpu - ref).norm() / ref.norm()).item() < (0.6 if agg == "krum" else 0.3)
     if agg == "krum":
         assert max(a.last_selected) < 80  # picked an honest client
 

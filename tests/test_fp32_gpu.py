@@ -19,6 +19,15 @@ from ddl25spring_amd.ops.functional import ConvGeom
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["mfma32", "x6"])
+def fmath(request):
+    """Both fp32 product engines: the exact fp32 MFMA and the 3-way-split bf16 MFMA (x6)."""
+    old = F32.math()
+    F32.set_math(request.param)
+    yield request.param
+    F32.set_math(old)
+
+
 def _err(a, b):
     a = a.double().cpu()
     b = b.double().cpu()
@@ -75,7 +84,7 @@ def _weights(geom, dev):
 
 
 @pytest.mark.parametrize("geom", GEOMS, ids=IDS)
-def test_conv_f32_fwd(cuda, geom):
+def test_conv_f32_fwd(cuda, geom, fmath):
     torch.manual_seed(0)
     x = torch.randn(geom.G, geom.N, geom.H, geom.W, geom.C, device=cuda)
     w = _weights(geom, cuda)
@@ -100,7 +109,7 @@ def test_conv_f32_fwd(cuda, geom):
 
 
 @pytest.mark.parametrize("geom", GEOMS, ids=IDS)
-def test_conv_f32_dgrad(cuda, geom):
+def test_conv_f32_dgrad(cuda, geom, fmath):
     torch.manual_seed(1)
     dy = torch.randn(geom.G, geom.N, geom.P, geom.Q, geom.K, device=cuda)
     w = _weights(geom, cuda)
@@ -128,7 +137,7 @@ def test_conv_f32_dgrad(cuda, geom):
 
 
 @pytest.mark.parametrize("stride", [1, 2])
-def test_conv_f32_dgrad_compact_residual(cuda, stride):
+def test_conv_f32_dgrad_compact_residual(cuda, stride, fmath):
     """residual_sub=2: a 1x1/2 shortcut's input gradient added on the (2i, 2j) pixels only (the
     downsample block's first 3x3 conv has stride 2: its DGRAD runs in sub-pixel phases)."""
     geom = ConvGeom(G=2, N=3, H=9, W=8, C=64, K=64, R=3, S=3, stride=stride, pad=1)
@@ -140,7 +149,7 @@ def test_conv_f32_dgrad_compact_residual(cuda, stride):
 
 
 @pytest.mark.parametrize("geom", GEOMS, ids=IDS)
-def test_conv_f32_wgrad(cuda, geom):
+def test_conv_f32_wgrad(cuda, geom, fmath):
     torch.manual_seed(2)
     x = torch.randn(geom.G, geom.N, geom.H, geom.W, geom.C, device=cuda)
     dy = torch.randn(geom.G, geom.N, geom.P, geom.Q, geom.K, device=cuda)
@@ -164,7 +173,7 @@ def test_conv_f32_wgrad(cuda, geom):
     _close(dw2, ref_wgrad(dy.cpu(), xa.cpu(), geom))
 
 
-def test_conv_f32_tiles_and_splits_deterministic(cuda):
+def test_conv_f32_tiles_and_splits_deterministic(cuda, fmath):
     """Every tile config x split-K count gives the same math; each is bitwise reproducible."""
     geom = ConvGeom(G=2, N=3, H=8, W=8, C=128, K=128, R=3, S=3, stride=2, pad=1)
     torch.manual_seed(3)
@@ -296,7 +305,7 @@ def _resnet_pair(cuda, G, seed=0):
     return tm, net, mapping, convert
 
 
-def test_resnet18_fp32_step_matches_torch(cuda):
+def test_resnet18_fp32_step_matches_torch(cuda, fmath):
     """One native fp32 ResNet-18 training step (all the fused kernels, fused head) vs torch autograd
     in float64: loss and every parameter gradient within 1e-4 (max-abs relative); also reports
     stock torch fp32 on the GPU for scale."""
@@ -324,7 +333,7 @@ def _hash(t):
     return hashlib.sha256(t.detach().cpu().numpy().tobytes()).hexdigest()
 
 
-def test_fedavg_fp32_deterministic(cuda):
+def test_fedavg_fp32_deterministic(cuda, fmath):
     """Two fresh FedAvg runs (ResNet-18, fp32, 2 clients, graph-replayed rounds) and an eager run
     produce bitwise-identical server weights: no atomics anywhere in the fp32 step."""
     from ddl25spring_amd.data.images import DeviceImageDataset, synthetic_images
@@ -409,7 +418,7 @@ def test_fp32_unsynchronised_rounds_equal_exactly(cuda):
     assert torch.equal(ws[0], ws[1])
 
 
-def test_fp32_mnist_cnn_step_matches_torch(cuda):
+def test_fp32_mnist_cnn_step_matches_torch(cuda, fmath):
     """The reference's own model (hfl_complete.py:39-64) in fp32 on the device vs torch float64:
     conv+bias+ReLU, maxpool, Linear, log_softmax/NLL — dropout disabled for the comparison."""
     from ddl25spring_amd.models import convert, mnist_cnn
