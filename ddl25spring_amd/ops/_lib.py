@@ -156,6 +156,7 @@ _SIGS = {
     "ddl_broadcast_rows": [vp, vp, i64, i32, i64, vp, i64, vp],
     "ddl_gram_f32": [vp, i64, vp, i32, i64, vp, i64, vp, vp],
     "ddl_gram_f32_workspace": [i32, i64],
+    "ddl_gemm_nt_bf16": [vp, vp, vp, i32, i32, i32, i64, vp],
     "ddl_coord_select": [vp, i64, i32, i64, i32, i32, vp, vp],
 }
 

@@ -70,11 +70,12 @@ def _grad_ready(p: torch.Tensor) -> None:
 
 # ------------------------------------------------------------------------------------- linear
 # A plain (no bias / residual epilogue) linear with a vocabulary-sized output runs its forward on
-# hipBLASLt (torch.matmul): on the LLaMA-288 LM head (8192 x 288 -> 32000, K = 288) it takes
-# 264 us against 389 us for the MFMA conv-GEMM, whose 9-step reduction leaves the 524 MB bf16
-# output write exposed; every block-sized linear is as fast or faster on the conv-GEMM, and so is
-# the LM head's backward (scripts/gemm_vs_blas.py, profiles/gemm_vs_blas_r2f.txt).
-BLAS_FWD_MIN_OUT = 8192
+# the dedicated wide-output GEMM (csrc/kernels/gemm_bf16.hip): on the LLaMA-288 LM head
+# (8192 x 288 -> 32000) the MFMA conv-GEMM takes 389 us (its 9-step reduction leaves the 524 MB
+# bf16 output write exposed) and hipBLASLt 264 us (scripts/gemm_vs_blas.py,
+# profiles/gemm_vs_blas_r2f.txt); every block-sized linear, and the LM head's backward, run on
+# the conv-GEMM.
+WIDE_FWD_MIN_OUT = 8192
 
 
 class _Linear(torch.autograd.Function):
@@ -87,8 +88,8 @@ class _Linear(torch.autograd.Function):
         geom = Fn.ConvGeom(1, T, 1, 1, C, Kout, 1, 1, 1, 0)
         wb = _bf16_weight(w).view(1, Kout, 1, 1, C)
         res = residual.reshape(1, T, 1, 1, Kout).contiguous() if residual is not None else None
-        if b is None and res is None and Kout >= BLAS_FWD_MIN_OUT:
-            y = torch.matmul(x2, wb.view(Kout, C).t())
+        if b is None and res is None and Kout >= WIDE_FWD_MIN_OUT and Fn.gemm_nt_ok(C, Kout):
+            y = Fn.gemm_nt_bf16(x2, wb.view(Kout, C))
         else:
             y = Fn.conv_fwd(x2.view(1, T, 1, 1, C), wb, geom,
                             bias=None if b is None else b.detach().view(1, Kout), residual=res)

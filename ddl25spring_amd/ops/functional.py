@@ -916,6 +916,26 @@ def channel_sum(x, out):
     return out
 
 
+def gemm_nt_bf16(x, w, out=None):
+    """y[T][V] = x[T][C] . w[V][C]^T, bf16 in / out, fp32 accumulate (csrc/kernels/gemm_bf16.hip:
+    the wide-output LM-head GEMM, C % 32 == 0, V % 8 == 0)."""
+    T, C = x.shape
+    V = w.shape[0]
+    if not x.is_cuda:
+        return (x.float() @ w.float().t()).to(x.dtype)
+    assert x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()
+    assert w.shape[1] == C
+    if out is None:
+        out = torch.empty(T, V, dtype=torch.bfloat16, device=x.device)
+    check(_lib.kernels().ddl_gemm_nt_bf16(ptr(x), ptr(w), ptr(out), T, V, C, out.stride(0), stream()),
+          "gemm_nt_bf16")
+    return out
+
+
+def gemm_nt_ok(C: int, V: int) -> bool:
+    return C % 32 == 0 and C >= 32 and V % 8 == 0
+
+
 def to_bf16(x32: torch.Tensor, out=None):
     out = out if out is not None else torch.empty(x32.shape, dtype=torch.bfloat16, device=x32.device)
     if not x32.is_cuda:

@@ -39,6 +39,8 @@ def main():
         r = {}
         r["ours fwd"] = timed(lambda: Fn.conv_fwd(x5, w5, g))
         r["blas fwd"] = timed(lambda: torch.matmul(x, w.t()))
+        if Fn.gemm_nt_ok(C, K):
+            r["ours wide fwd"] = timed(lambda: Fn.gemm_nt_bf16(x, w))
         r["ours dgrad+wgrad"] = timed(lambda: Fn.conv_dgrad_wgrad(dy5, w5, x5, g, dw))
         r["blas dx"] = timed(lambda: torch.matmul(dy, w))
         r["blas dw bf16"] = timed(lambda: torch.matmul(dy.t(), x))

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of one env switch (0 vs 1) on bench.py at 1 and 8 clients, after the GPU tests matching -k.
-#   gpurun -- bash scripts/gpu_ab.sh <tag> <ENV_VAR> "<pytest -k expr>"
+#   gpurun -- bash scripts/gpu/gpu_ab.sh <tag> <ENV_VAR> "<pytest -k expr>"
 set -o pipefail
 tag=${1:-ab}
 var=${2:-DDL_FUSED_HEAD}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Fused BN tails: GPU tests, then bench.py A/B (DDL_BN_FUSED_TAIL=0 vs auto) at 1, 2, 8 clients.
-#   gpurun --timeout 900 -- bash scripts/gpu_ab_bntail.sh <tag>
+#   gpurun --timeout 900 -- bash scripts/gpu/gpu_ab_bntail.sh <tag>
 set -o pipefail
 tag=${1:-bt}
 out=gpurun_out/$tag

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of the paired DGRAD+WGRAD launches: conv GPU tests, then bench.py at 1 and 8 clients per GPU
 # with pairing on (default) and off (DDL_CONV_PAIR=0).
-#   gpurun --timeout 900 -- bash scripts/gpu_ab_pair.sh
+#   gpurun --timeout 900 -- bash scripts/gpu/gpu_ab_pair.sh
 set -o pipefail
 out=gpurun_out/pair
 mkdir -p $out

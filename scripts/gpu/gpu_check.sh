@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun call: GPU tests, headline bench (8 clients and the per-GPU load of the N=8 run),
 # reference-equivalent eager baselines, and a rocprofv3 kernel-stats profile of bench.py.
-#   gpurun --timeout 1200 -- bash scripts/gpu_check.sh [tests|bench|prof|all]
+#   gpurun --timeout 1200 -- bash scripts/gpu/gpu_check.sh [tests|bench|prof|all]
 set -o pipefail
 what=${1:-all}
 out=gpurun_out

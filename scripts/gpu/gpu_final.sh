@@ -10,4 +10,4 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 grep smoke gpurun_out/final/smoke.log | cut -c1-200
 timeout -k 10 300 python bench.py > gpurun_out/final/bench_default.log 2>&1 || { tail -20 gpurun_out/final/bench_default.log; exit 1; }
 grep '^{' gpurun_out/final/bench_default.log | cut -c1-220
-bash scripts/gpu_all_bench.sh
+bash scripts/gpu/gpu_all_bench.sh

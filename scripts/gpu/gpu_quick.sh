@@ -1,6 +1,6 @@
 #!/bin/bash
 # Quick GPU iteration: full GPU test suite, then bench.py at 1, 2 and 8 clients per GPU.
-#   gpurun --timeout 900 -- bash scripts/gpu_quick.sh <tag>
+#   gpurun --timeout 900 -- bash scripts/gpu/gpu_quick.sh <tag>
 set -o pipefail
 tag=${1:-q}
 out=gpurun_out/$tag

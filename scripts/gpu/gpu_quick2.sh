@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU kernel tests matching a -k filter, then bench.py at 1, 2 and 8 clients (2 reps each).
-#   gpurun -- bash scripts/gpu_quick2.sh <tag> "<pytest -k expr>"
+#   gpurun -- bash scripts/gpu/gpu_quick2.sh <tag> "<pytest -k expr>"
 set -o pipefail
 tag=${1:-q2}
 kexpr=${2:-prep}

@@ -25,6 +25,8 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_f32f -o ru
 tail -1 gpurun_out/r3f_prof.log
 db=$(ls gpurun_out/prof_f32f/*/run_results.db gpurun_out/prof_f32f/run_results.db 2>/dev/null | head -n 1 || true)
 [ -n "$db" ] && python scripts/prof_summary.py "$db" --top 40 > gpurun_out/r3f_prof_summary.txt
+PYTHONPATH=. timeout -k 10 200 python -u scripts/gemm_vs_blas.py > gpurun_out/r3f_gemm.log 2>&1 || { tail -20 gpurun_out/r3f_gemm.log; exit 1; }
+cat gpurun_out/r3f_gemm.log
 timeout -k 10 300 python -u benchmarks/bench_llm.py --steps 30 --warmup 5 > gpurun_out/r3f_llm.log 2>&1 || { tail -20 gpurun_out/r3f_llm.log; exit 1; }
 tail -1 gpurun_out/r3f_llm.log
 mkdir -p gpurun_out/prof_llm

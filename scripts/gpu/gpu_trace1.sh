@@ -1,6 +1,6 @@
 #!/bin/bash
 # Per-launch kernel trace of one training step at 1 and 8 clients per GPU (csv kernel trace).
-#   gpurun --timeout 600 -- bash scripts/gpu_trace1.sh <tag>
+#   gpurun --timeout 600 -- bash scripts/gpu/gpu_trace1.sh <tag>
 set -o pipefail
 export TMPDIR=/tmp
 tag=${1:-t}

@@ -12,5 +12,5 @@ for rep in 1 2; do
     echo "4 clients tune_big_halo=$t: $(grep -o '"value": [0-9.]*' $out/b4_$t.log)"
   done
 done
-bash scripts/gpu_trace1.sh r2j > /dev/null 2>&1 || exit 1
+bash scripts/gpu/gpu_trace1.sh r2j > /dev/null 2>&1 || exit 1
 tail -n 1 gpurun_out/r2j/step_c1.txt gpurun_out/r2j/step_c8.txt

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes over the conv microbenchmark (one pass per counter group, each its own short run).
-#   bash scripts/pmc_conv.sh "8 1" "c64 c256"
+#   bash scripts/gpu/pmc_conv.sh "8 1" "c64 c256"
 set -o pipefail
 export TMPDIR=/tmp
 out=gpurun_out/pmc

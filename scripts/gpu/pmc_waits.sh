@@ -1,7 +1,7 @@
 #!/bin/bash
 # Wave-cycle breakdown (waiting / issue-stalled / issuing, MFMA busy) of the conv kernels of one
 # ResNet-18 layer, one PMC pass per counter group.
-#   bash scripts/pmc_waits.sh "8 1" "c64 c512"
+#   bash scripts/gpu/pmc_waits.sh "8 1" "c64 c512"
 set -o pipefail
 export TMPDIR=/tmp
 out=gpurun_out/pmcw

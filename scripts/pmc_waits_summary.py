@@ -1,4 +1,4 @@
-"""Summarise scripts/pmc_waits.sh: per conv kernel, the share of wave cycles spent waiting
+"""Summarise scripts/gpu/pmc_waits.sh: per conv kernel, the share of wave cycles spent waiting
 (s_waitcnt / barrier), issue-stalled, and issuing, plus MFMA busy per CU-cycle and LDS conflicts.
 usage: python scripts/pmc_waits_summary.py gpurun_out/pmcw"""
 import glob

@@ -117,7 +117,7 @@ def test_direct_sgd_equals_gradient_sgd(cuda, model, monkeypatch):
     """Direct SGD (the conv WGRAD launches add -lr * dW into the master weights; one launch then
     refreshes the shadow and steps BN / head params) == zeroed gradients + fused SGD, one
     graph-replayed local step. The two differ only by fp32 rounding (p + sum(-lr * partial) vs
-    p - lr * sum(partial)). MnistCnn: 2e-4 of the update (scripts/dbg_direct.py). ResNet-18: two
+    p - lr * sum(partial)). MnistCnn: 2e-4 of the update (measured with a one-off script, r2). ResNet-18: two
     identical gradient-SGD runs already differ by ~16% of one step's update (fp32-atomic order of
     the BN statistics, amplified through bf16 activations and the BN backward), and direct SGD
     sits at that same noise floor, so it is checked against a second gradient-SGD run."""

@@ -204,3 +204,21 @@ def test_llm_step_graph_replay_matches_eager(cuda):
     for a, b in zip(*curves):
         assert abs(a - b) < 2e-2 * abs(a), curves
     assert curves[1][-1] < curves[1][0]
+
+
+@pytest.mark.parametrize("T,C,V", [(8192, 288, 32000), (300, 96, 520), (77, 32, 8)])
+def test_wide_gemm_matches_fp32(cuda, T, C, V):
+    """The LM-head GEMM (gemm_bf16.hip) vs an fp32 torch matmul of the same bf16 operands,
+    including tile overhangs on both edges."""
+    from ddl25spring_amd.ops import functional as Fn
+    torch.manual_seed(3)
+    x = torch.randn(T, C, device=cuda).to(torch.bfloat16)
+    w = (torch.randn(V, C, device=cuda) * 0.05).to(torch.bfloat16)
+    y = Fn.gemm_nt_bf16(x, w)
+    ref = x.float() @ w.float().t()
+    err = ((y.float() - ref).abs().max() / ref.abs().max()).item()
+    assert err < 1e-2, err  # bf16 output rounding
+    # a padded output row stride (a strided logits view)
+    out = torch.full((T, V + 8), 7.0, device=cuda, dtype=torch.bfloat16)
+    Fn.gemm_nt_bf16(x, w, out=out[:, :V])
+    assert torch.equal(out[:, :V], y) and (out[:, V:] == 7.0).all()
