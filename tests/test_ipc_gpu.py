@@ -30,6 +30,13 @@ def _worker(rank, world, port, out, sizes, two_shot_bytes):
             x = torch.randn(n, generator=g).to(dev)
             ar.all_reduce(x)
             res[(rep, n)] = x.cpu()
+    # back-to-back calls without a host sync in between: a fast rank runs whole calls ahead of a
+    # slow one, so the barrier's epoch compare must be wrap-safe monotonic, not equality
+    xs = [torch.full((777 + 64 * i,), float((rank + 1) * (i + 1)), device=dev) for i in range(8)]
+    torch.cuda.synchronize()
+    for t in xs:
+        ar.all_reduce(t)
+    res["b2b"] = [t.cpu() for t in xs]
     # graph-captured calls replay with the device-resident epoch
     x = torch.full((4099,), float(rank + 1), device=dev)
     s = torch.cuda.Stream()
@@ -70,3 +77,5 @@ def test_ipc_allreduce_matches_sum(cuda, world, two_shot_bytes):
     tot = float(sum(range(1, world + 1)))
     for r in range(world):
         assert torch.equal(outs[r]["graph"], torch.full((4099,), tot))
+        for i, t in enumerate(outs[r]["b2b"]):
+            assert torch.equal(t, torch.full((777 + 64 * i,), tot * (i + 1))), (r, i)
