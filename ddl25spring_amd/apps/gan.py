@@ -21,6 +21,8 @@ class GANConfig:
     train_size: int = 50000
     seed: int = 0
     save: str = ""  # rank 0 writes the final flat global (G | D | BN) weights here (torch.save)
+    ckpt_dir: str = ""  # per-rank sharded checkpoint (runtime/checkpoint.py); resumes if committed
+    ckpt_every: int = 0  # commit every N rounds (0: only at the end)
 
 
 def client_images(cfg: GANConfig, device):
@@ -39,7 +41,26 @@ def run_gan(cfg: GANConfig, ctx, log=print):
     fg = FederatedGAN(data, ctx=ctx, ngf=cfg.ngf, ndf=cfg.ndf, lr=cfg.lr,
                       local_steps=cfg.local_steps, batch_size=cfg.batch_size,
                       client_fraction=cfg.client_fraction, seed=cfg.seed, device=ctx.device)
-    res = fg.run(cfg.rounds)
+    ckpt = None
+    if cfg.ckpt_dir:
+        from ..runtime.checkpoint import ShardedCheckpoint
+        tag = f"gan,clients={cfg.clients},C={cfg.client_fraction},bs={cfg.batch_size},ls={cfg.local_steps},seed={cfg.seed}"
+        ckpt = ShardedCheckpoint(cfg.ckpt_dir, ctx, tag=tag)
+        got = ckpt.load()
+        if got is not None:
+            fg.load_state_dict(got[1])
+    from ..fl.gan import GANRunResult
+    res = GANRunResult()
+    while fg.round_idx < cfg.rounds:
+        part = fg.run(1)
+        res.rounds += part.rounds
+        res.loss_d += part.loss_d
+        res.loss_g += part.loss_g
+        res.wall_time += part.wall_time
+        res.samples += part.samples
+        if ckpt is not None and ((cfg.ckpt_every and fg.round_idx % cfg.ckpt_every == 0)
+                                 or fg.round_idx == cfg.rounds):
+            ckpt.save(fg.round_idx, fg.state_dict())
     if log and ctx.rank == 0:
         for r, (ld, lg, t) in enumerate(zip(res.loss_d, res.loss_g, res.wall_time)):
             log(f"round {r + 1}: loss_D {ld:.3f} loss_G {lg:.3f} ({t:.2f}s)")

@@ -71,6 +71,7 @@ class FederatedGAN:
         self._idx: dict = {}    # client -> static [local_steps, batch] device index buffer
         self._z: dict = {}      # client -> static [local_steps, batch, nz] generator noise buffer
         self._graphs: dict = {}  # client -> CapturedStep over its local steps
+        self.round_idx = 0       # rounds done (seeds the per-round client generators)
 
     # ---------------------------------------------------------------------------------------
     def _global_tensors(self):
@@ -130,7 +131,8 @@ class FederatedGAN:
     # ---------------------------------------------------------------------------------------
     def run(self, rounds: int) -> GANRunResult:
         res = GANRunResult()
-        for r in range(rounds):
+        for _ in range(rounds):
+            r = self.round_idx
             t0 = time.perf_counter()
             chosen = self.rng.choice(len(self.data), self.K, replace=False)
             mine = [c for c in chosen if c % self.world == self.rank]
@@ -170,4 +172,34 @@ class FederatedGAN:
             res.loss_d.append(ld_sum / max(1, len(mine)))
             res.loss_g.append(lg_sum / max(1, len(mine)))
             res.rounds += 1
+            self.round_idx += 1
         return res
+
+    # --------------------------------------------------------------------------- checkpointing
+    def state_dict(self) -> dict:
+        """This rank's shard: the global (G | D | BN) weights and the sampling stream (identical on
+        every rank), and the Adam state of the clients that live on this rank."""
+        clients = {}
+        for c, st in self._state.items():
+            if hasattr(self.optG, "m"):
+                clients[int(c)] = {"mG": st[0], "vG": st[1], "tG": st[2], "mD": st[3], "vD": st[4],
+                                   "tD": st[5]}
+            else:
+                clients[int(c)] = {"G": st[0], "D": st[3]}
+        return {"flat": self._flat(), "round": self.round_idx,
+                "rng": self.rng.bit_generator.state, "clients": clients}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self._load_flat(sd["flat"].to(self.device))
+        self.round_idx = int(sd["round"])
+        self.rng.bit_generator.state = sd["rng"]
+        self._state = {}
+        for c, st in sd["clients"].items():
+            if "G" in st:
+                self._state[int(c)] = (st["G"], None, None, st["D"], None, None)
+                continue
+            dev = self.device
+            tdev = [torch.tensor([t], dtype=torch.int64, device=dev) if o.t_dev is not None else None
+                    for t, o in ((st["tG"], self.optG), (st["tD"], self.optD))]
+            self._state[int(c)] = (st["mG"].to(dev), st["vG"].to(dev), int(st["tG"]),
+                                   st["mD"].to(dev), st["vD"].to(dev), int(st["tD"]), *tdev)
