@@ -106,7 +106,9 @@ def train_llm(cfg: LLMConfig, ctx, log=print, warmup: int = 0) -> dict:
         opt = FlatAdam(mod.parameters(), lr=cfg.lr, fused=True, bf16_shadow=True)
     else:
         opt = torch.optim.Adam(mod.parameters(), lr=cfg.lr)
-    sync = GradBucketer(mod, ctx, group=dp_group, bucket_mb=cfg.bucket_mb) \
+    # DP-GA buckets are slices of FlatAdam's own flat gradient buffer (no second copy)
+    sync = GradBucketer(mod, ctx, group=dp_group, bucket_mb=cfg.bucket_mb,
+                        flat=opt if hasattr(opt, "offsets") else None) \
         if cfg.dp > 1 and cfg.dp_mode == "ga" else None
     if cfg.batch_size % cfg.micro_batches:
         raise ValueError("batch_size must be divisible by micro_batches")

@@ -50,7 +50,11 @@ class GradBucketer:
     """Overlapped, bucketed gradient all-reduce (mean over the DP group) for a torch module."""
 
     def __init__(self, module: torch.nn.Module, ctx, group=None, bucket_mb: float = 64.0,
-                 world: int | None = None):
+                 world: int | None = None, flat=None):
+        """``flat``: a ``FlatAdam`` over the module's parameters — its flat ``grad`` buffer IS the
+        bucket storage (buckets are contiguous slices of it in reverse parameter order), so the
+        all-reduced gradients are already where the fused Adam reads them: no second gradient
+        buffer and no per-parameter copy in ``step``."""
         self.ctx, self.group = ctx, group
         self.world = world or (dist.get_world_size(group) if ctx.is_distributed else 1)
         params = [p for p in module.parameters() if p.requires_grad]
@@ -59,14 +63,23 @@ class GradBucketer:
         nb = max(ids) + 1 if ids else 0
         self.buckets = []
         dev = params[0].device if params else torch.device("cpu")
+        if flat is not None:
+            off = {id(p): o for p, o in zip(flat.params, flat.offsets)}
+            if [id(p) for p in flat.params] != [id(p) for p in params]:
+                raise ValueError("GradBucketer(flat=...): the optimizer's parameters must be the module's")
         for b in range(nb):
             members = [p for p, i in zip(ready, ids) if i == b]
-            flat = torch.zeros(sum(p.numel() for p in members), dtype=torch.float32, device=dev)
-            off = 0
-            for p in members:
-                p.grad = flat[off:off + p.numel()].view_as(p)
-                off += p.numel()
-            self.buckets.append({"flat": flat, "members": members, "pending": len(members),
+            if flat is not None:
+                lo = min(off[id(p)] for p in members)
+                hi = max(off[id(p)] + p.numel() for p in members)
+                buf = flat.grad[lo:hi]  # contiguous: reverse order of consecutive parameters
+            else:
+                buf = torch.zeros(sum(p.numel() for p in members), dtype=torch.float32, device=dev)
+                o = 0
+                for p in members:
+                    p.grad = buf[o:o + p.numel()].view_as(p)
+                    o += p.numel()
+            self.buckets.append({"flat": buf, "members": members, "pending": len(members),
                                  "handle": None})
         self.owner = {}
         for bi, b in enumerate(self.buckets):

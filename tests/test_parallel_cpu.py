@@ -253,3 +253,41 @@ def test_native_dp_bucketer_equals_large_batch(monkeypatch):
         opt.step()
     assert torch.equal(w0, w1)
     assert torch.allclose(w0, net.store.data, atol=1e-5)
+
+
+def _flat_bucket_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    from ddl25spring_amd.optim import FlatAdam
+    from ddl25spring_amd.parallel.dp import GradBucketer
+    from ddl25spring_amd.runtime import dist as rdist
+    ctx = rdist.init(backend="gloo", device="cpu")
+    res = {}
+    for mode in ("own", "flat"):
+        torch.manual_seed(0)
+        model = LLama(**TINY)
+        opt = FlatAdam(model.parameters(), lr=1e-3)
+        bk = GradBucketer(model, ctx, bucket_mb=0.02, flat=opt if mode == "flat" else None)
+        torch.manual_seed(7 + rank)
+        x = torch.randint(0, TINY["vocab_size"], (2, TINY["ctx_size"]))
+        for _ in range(2):
+            bk.zero_grad()  # (FlatAdam.zero_grad would re-point the grads away from own buckets)
+            causalLLMLoss(model(x), x).backward()
+            bk.finish()
+            opt.step()
+        res[mode] = opt.data.clone()
+        if mode == "flat":  # the buckets ARE the optimizer's gradient buffer
+            assert all(b["flat"].data_ptr() >= opt.grad.data_ptr() for b in bk.buckets)
+    torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
+    rdist.shutdown()
+
+
+def test_grad_bucketer_on_flatadam_buffer_equals_own_buckets():
+    """DP-GA buckets as slices of FlatAdam's flat grad (no second buffer, no copy in step) give
+    bit-identical steps to separate bucket buffers, and replicas agree."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_flat_bucket_worker, args=(2, 29961, d), nprocs=2, join=True)
+        res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(2)]
+    for r in range(2):
+        assert torch.equal(res[r]["own"], res[r]["flat"])
+    assert torch.equal(res[0]["flat"], res[1]["flat"])
