@@ -615,11 +615,15 @@ __global__ __launch_bounds__(256, 2) void convf32_kernel(ConvF32Args a) {
         for (int ti = 0; ti < TP; ++ti)
 #pragma unroll
           for (int tj = 0; tj < TQ; ++tj) {
-            f4v c = acc[ti][tj];
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat44(ah[ti], ah[ti]), cat44(bh[tj], bm[tj]), c, 0, 0, 0);
+            // the step's 96 piece products from a zero accumulator, smallest terms first, then ONE
+            // IEEE add into the running sum: the bf16 MFMA's internal accumulation is not a
+            // round-to-nearest fp32 chain, and over a 10^5-deep WGRAD reduction its bias would
+            // reach 1e-3 relative; per step it stays at fp32-rounding level
+            f4v c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat44(al[ti], am[ti]), cat44(bh[tj], bm[tj]),
+                                                            (f4v){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat44(am[ti], ah[ti]), cat44(bh[tj], bl[tj]), c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat44(al[ti], am[ti]), cat44(bh[tj], bm[tj]), c, 0, 0, 0);
-            acc[ti][tj] = c;
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat44(ah[ti], ah[ti]), cat44(bh[tj], bm[tj]), c, 0, 0, 0);
+            acc[ti][tj] += c;
           }
       } else {
 #pragma unroll

@@ -6,8 +6,8 @@
 //   ddl_swiglu_fwd/bwd    : h = silu(a) * b over the fused [a | b] projection
 //   ddl_add               : bf16 residual add
 //   ddl_attn_fwd/bwd      : causal flash attention on the gfx950 16x16x32 bf16 MFMA (head_dim
-//                           32/48/64/128; a 16-dim remainder on 16x16x16) with RoPE applied as
-//                           q / k tiles are staged
+//                           32/48/64/128; a 16-dim remainder zero-padded to 32) with RoPE applied
+//                           as q / k tiles are staged
 //                           (so RoPE costs no HBM pass), online softmax, log-sum-exp saved;
 //                           backward recomputes P in two kernels (dQ; dK+dV) and writes the
 //                           un-rotated gradients straight into the fused dQKV buffer.
@@ -291,7 +291,7 @@ DDL_API int ddl_add(const void* a, const void* b, void* y, long long n, hipStrea
 
 // ---------------------------------------------------------------------------------------------
 // Causal attention on gfx950's double-rate MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulate; a
-// head-dim remainder of 16, e.g. HD = 48 = 32 + 16, takes one v_mfma_f32_16x16x16_bf16).
+// head-dim remainder of 16, e.g. HD = 48 = 32 + 16, is zero-padded to one more x32).
 // qkv: [B][S][3][H][HD] bf16 (the fused projection output), o / dout: [B][S][H][HD], lse / delta:
 // [B][H][S] fp32, RoPE tables cos/sin [S][HD/2] fp32 (interleaved pairs (2i, 2i+1)), applied as
 // tiles are staged. A workgroup owns 64 query rows (forward, dQ) or 64 key rows (dK/dV), each of
@@ -312,9 +312,6 @@ constexpr int AT = 64;   // rows per workgroup tile
 constexpr int AST = 32;  // rows per inner step (one x32 MFMA k-extent)
 constexpr float LOG2E = 1.4426950408889634f;
 
-__device__ __forceinline__ f4v mma16(s4v a, s4v b, f4v c) {
-  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
-}
 __device__ __forceinline__ f4v mma32(s8v a, s8v b, f4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -369,20 +366,24 @@ __device__ __forceinline__ void store4_unrot(bf16_t* dst, const float* cs, const
   *(i2v*)(dst + d0) = v;
 }
 
-// LDS images: row-major [64][HD+8] (16-byte aligned rows for the x32 A reads) and transposed
-// [HD][64+8] (8-byte reads at 4g and 16+4g of a step land on distinct bank pairs).
+// LDS images: row-major [64][HDP+8] with HDP = HD rounded up to 32 (16-byte aligned rows for the
+// x32 A reads; dims HD..HDP-1 are staged as zeros, so a head-dim remainder of 16 runs as one x32
+// MFMA with a zero upper half — the same cycles as a 16x16x16 on gfx950, and every head-dim
+// product is one MFMA shape) and transposed [HD][64+8] (8-byte reads at 4g and 16+4g of a step
+// land on distinct bank pairs).
 template <int HD> struct AttnLds {
-  static constexpr int KP = HD + 8, VP = AT + 8;
-  static constexpr int D32 = HD / 32, R16 = (HD % 32) / 16, NT = HD / 16;
+  static constexpr int HDP = (HD + 31) / 32 * 32;
+  static constexpr int KP = HDP + 8, VP = AT + 8;
+  static constexpr int D32 = HDP / 32, NT = HD / 16;
 };
 
 // Stage rows r0..r0+63 (row t at src + t*rs) into LDS (row-major and/or transposed); rows >= S
-// are zeros.
+// and the row-major image's dims HD..HDP-1 are zeros.
 template <int HD>
 __device__ __forceinline__ void stage_rows(const bf16_t* src, long long rs, int r0, int S,
                                            const float* rcos, const float* rsin, bf16_t* rm,
                                            bf16_t* tr) {
-  constexpr int C4 = HD / 4, KP = AttnLds<HD>::KP, VP = AttnLds<HD>::VP;
+  constexpr int C4 = HD / 4, KP = AttnLds<HD>::KP, VP = AttnLds<HD>::VP, HDP = AttnLds<HD>::HDP;
   for (int e = threadIdx.x; e < AT * C4; e += 256) {
     const int r = e / C4, d0 = (e - r * C4) * 4, t = r0 + r;
     float v[4] = {0.f, 0.f, 0.f, 0.f};
@@ -395,42 +396,41 @@ __device__ __forceinline__ void stage_rows(const bf16_t* src, long long rs, int 
       for (int k = 0; k < 4; ++k) tr[(d0 + k) * VP + r] = f2bf(v[k]);
     }
   }
+  if constexpr (HDP > HD) {
+    if (rm) {
+      constexpr int Z4 = (HDP - HD) / 4;
+      for (int e = threadIdx.x; e < AT * Z4; e += 256) {
+        const int r = e / Z4, d0 = HD + (e - r * Z4) * 4;
+        *(s4v*)(rm + r * KP + d0) = s4v{0, 0, 0, 0};
+      }
+    }
+  }
 }
 
-// One row's B fragments over the head dimension: x32 chunk c holds dims 32c + 8g + j, the x16
-// remainder dims 32*D32 + 4g + j; zeros when !valid.
+// One row's B fragments over the (zero-padded) head dimension: chunk c holds dims 32c + 8g + j;
+// zeros when !valid or past HD.
 template <int HD> struct RowFrag {
-  s8v c[AttnLds<HD>::D32 > 0 ? AttnLds<HD>::D32 : 1];
-  s4v r;
+  s8v c[AttnLds<HD>::D32];
 };
 
 template <int HD>
 __device__ __forceinline__ void row_frags(const bf16_t* row, const float* cs, const float* sn,
                                           int lg, bool valid, RowFrag<HD>& f) {
-  constexpr int D32 = AttnLds<HD>::D32;
 #pragma unroll
-  for (int c = 0; c < D32; ++c) {
+  for (int c = 0; c < AttnLds<HD>::D32; ++c) {
     float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (valid) {
-      row4(row, cs, sn, 32 * c + 8 * lg, v);
-      row4(row, cs, sn, 32 * c + 8 * lg + 4, v + 4);
-    }
+    const int d0 = 32 * c + 8 * lg;
+    if (valid && d0 < HD) row4(row, cs, sn, d0, v);
+    if (valid && d0 + 4 < HD) row4(row, cs, sn, d0 + 4, v + 4);
     f.c[c] = bf8(v);
-  }
-  if constexpr (AttnLds<HD>::R16) {
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    if (valid) row4(row, cs, sn, 32 * D32 + 4 * lg, v);
-    f.r = bf4(v[0], v[1], v[2], v[3]);
   }
 }
 
 // acc += A(16 rows of a row-major LDS image, this lane's row at `arow`) . f over the head dim
 template <int HD>
 __device__ __forceinline__ f4v dot_hd(const bf16_t* arow, const RowFrag<HD>& f, int lg, f4v acc) {
-  constexpr int D32 = AttnLds<HD>::D32;
 #pragma unroll
-  for (int c = 0; c < D32; ++c) acc = mma32(*(const s8v*)(arow + 32 * c + 8 * lg), f.c[c], acc);
-  if constexpr (AttnLds<HD>::R16) acc = mma16(*(const s4v*)(arow + 32 * D32 + 4 * lg), f.r, acc);
+  for (int c = 0; c < AttnLds<HD>::D32; ++c) acc = mma32(*(const s8v*)(arow + 32 * c + 8 * lg), f.c[c], acc);
   return acc;
 }
 
