@@ -112,6 +112,7 @@ def main():
     rounds_per_s = args.steps / elapsed
     acc = fl.test() if args.eval else None
     w_hash = hashlib.sha256(fl.w_global.detach().cpu().numpy().tobytes()).hexdigest()
+    from ddl25spring_amd.ops import functional_f32 as F32
     ref = REFERENCE_SAMPLES_PER_S.get(args.precision)
     if ctx.is_main:
         out = {
@@ -137,7 +138,8 @@ def main():
                        "clients": args.clients, "local_batch": args.batch,
                        "local_epochs": args.epochs, "lr": args.lr,
                        "samples_per_client": args.train_size // args.clients,
-                       "client_slots_per_gpu": fl.slots, "hip_graphs": not args.no_graph},
+                       "client_slots_per_gpu": fl.slots, "hip_graphs": not args.no_graph,
+                       "fp32_conv_math": F32.math() if args.precision == "fp32" else None},
         }
         if acc is not None:
             out["test_accuracy"] = acc
