@@ -49,7 +49,8 @@ def main():
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.reps
     fl = 2 * g.G * g.N * g.P * g.Q * g.K * g.R * g.S * g.C
-    print(f"{a.math} {a.mode} G={a.G} {a.layer}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF/s plan={F32.plan({"fwd": F32.F_FWD, "dgrad": F32.F_DGRAD, "wgrad": F32.F_WGRAD}[a.mode], g)}")
+    mode = {"fwd": F32.F_FWD, "dgrad": F32.F_DGRAD, "wgrad": F32.F_WGRAD}[a.mode]
+    print(f"{a.math} {a.mode} G={a.G} {a.layer}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF/s plan={F32.plan(mode, g)}")
 
 
 if __name__ == "__main__":
