@@ -305,14 +305,21 @@ __device__ __forceinline__ void fzero_slot(const ConvF32Args& a, const FGeo& o) 
 // the last 8 — each remainder is exact in fp32 and the last fits bf16 exactly). Of the nine piece
 // products the six down to 2^-16 relative are kept (hh, hm, mh, hl, lh, mm); the dropped ml, lm,
 // ll are <= 2^-24 relative, the size of one fp32 rounding, and every bf16 x bf16 product is exact
-// in the fp32 accumulator. A 16-deep reduction step becomes 16 k values x 6 piece pairs = 96 k
-// slots = three v_mfma_f32_16x16x32_bf16 instead of four v_mfma_f32_16x16x4_f32: lane group g
-// holds k values 4g..4g+3 (the same ds_read_b128 fragment as the exact path), slots j < 4 of an
-// MFMA take one piece pair and j >= 4 the next:
-//   MFMA 0: A (h | h)  B (h | m)      MFMA 1: A (m | h)  B (h | l)      MFMA 2: A (l | m)  B (h | m)
-// At 16 cycles per x32 bf16 MFMA vs 32 per x4 fp32 MFMA the step costs 48 instead of 128 MFMA
-// cycles per 16x16 tile; the split is 4 VALU ops per value on the fragments (shared across the
-// wave's tiles). Numerics match the exact fp32 MFMA path to fp32 rounding (tests/test_fp32_gpu.py).
+// in the fp32 accumulator.
+// The split happens ONCE, when a thread stores its loaded values to LDS: a 4-deep k chunk of a
+// row becomes 32 bytes, two 16-byte halves (h | m) and (l | h), so every MFMA operand is one
+// ds_read_b128 and the inner loop has no conversion work (splitting the fragments after the LDS
+// read instead cost 253 VALU instructions per step against 24 MFMAs: VALU-bound). A 16-deep
+// step is 16 k values x 6 piece pairs = three v_mfma_f32_16x16x32_bf16 per 16x16 tile (lane group
+// g = k values 4g..4g+3):
+//   A (l | h) . B (h | m) = lh + hm      A (h | m) . B (l | h) = hl + mh      A (h | m) . B (h | m) = hh + mm
+// 48 MFMA cycles per tile-step instead of 128 for four v_mfma_f32_16x16x4_f32. Each step's three
+// MFMAs start from a zero accumulator and are added to the running sum with one IEEE add: the bf16
+// MFMA's internal accumulation is not a round-to-nearest fp32 chain, and over a 10^5-deep WGRAD
+// reduction its bias would reach 1e-3 relative.
+// LDS image: row r holds 4 chunks x 8 dwords; chunk c's half h sits at dword
+//   r*32 + 8*(c ^ f(r&15)) + 4*(h ^ g(r&15)),  f = (b3 << 1) | (b1 ^ b2), g = b2 ^ b3  (bits of r)
+// which makes both halves' fragment reads conflict-free for the four ds_read_b128 lane groups.
 __device__ __forceinline__ void split3(float4 v, s4v& h, s4v& m, s4v& l) {
   const float x[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -326,15 +333,31 @@ __device__ __forceinline__ void split3(float4 v, s4v& h, s4v& m, s4v& l) {
     l[i] = (short)(__float_as_uint(r2) >> 16);
   }
 }
+__device__ __forceinline__ void split1(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
+  const uint32_t u = __float_as_uint(x);
+  const float r1 = x - __uint_as_float(u & 0xFFFF0000u);
+  const uint32_t um = __float_as_uint(r1);
+  const float r2 = r1 - __uint_as_float(um & 0xFFFF0000u);
+  h = (uint16_t)(u >> 16);
+  m = (uint16_t)(um >> 16);
+  l = (uint16_t)(__float_as_uint(r2) >> 16);
+}
 __device__ __forceinline__ s8v cat44(s4v a, s4v b) {
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ int x6_off(int row, int ch, int half) {  // dwords
+  const int r = row & 15;
+  const int f = (((r >> 3) & 1) << 1) | (((r >> 1) ^ (r >> 2)) & 1);
+  const int g = ((r >> 2) ^ (r >> 3)) & 1;
+  return row * 32 + 8 * (ch ^ f) + 4 * (half ^ g);
 }
 
 // ------------------------------------------------------------------------------------ main kernel
 template <int MODE, int BP, int BQ, int X6>
 __global__ __launch_bounds__(256, 2) void convf32_kernel(ConvF32Args a) {
   constexpr int WP = BP / 2, WQ = BQ / 2, TP = WP / 16, TQ = WQ / 16;
-  constexpr int SP = BP * 16, SQ = BQ * 16;     // floats per operand image
+  constexpr int RW = X6 ? 32 : 16;              // dwords per image row (X6: 3 bf16 pieces + dup)
+  constexpr int SP = BP * RW, SQ = BQ * RW;     // dwords per operand image
   constexpr int UPK = BP / 64, UQK = BQ / 64;    // K-major units (float4) per thread
   constexpr int KUP = BP / 64, KUQ = BQ / 64;    // MN-major reductions per unit (4 rows x KU)
   __shared__ float4 smem4[(2 * (SP + SQ)) / 4];
@@ -549,14 +572,51 @@ __global__ __launch_bounds__(256, 2) void convf32_kernel(ConvF32Args a) {
       }
     }
   };
+  // X6: registers -> split LDS image (see split3 / x6_off)
+  auto store_k6 = [&](float* img, int row, int ch, float4 v) {
+    s4v h, m, l;
+    split3(v, h, m, l);
+    *(s8v*)(img + x6_off(row, ch, 0)) = cat44(h, m);
+    *(s8v*)(img + x6_off(row, ch, 1)) = cat44(l, h);
+  };
+  auto store_mn6 = [&](float* img, int rg, int kp, int KU, const float4* v) {
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      const int row = 4 * rg + j4;
+      const int kk = kp * KU, ch = kk >> 2, pos = kk & 3;
+      uint16_t* h0 = (uint16_t*)(img + x6_off(row, ch, 0)) + pos;  // (h | m) half
+      uint16_t* h1 = (uint16_t*)(img + x6_off(row, ch, 1)) + pos;  // (l | h) half
+      const float e0 = j4 == 0 ? v[0].x : j4 == 1 ? v[0].y : j4 == 2 ? v[0].z : v[0].w;
+      uint16_t ah, am, al;
+      split1(e0, ah, am, al);
+      if (KU == 2) {
+        const float e1 = j4 == 0 ? v[1].x : j4 == 1 ? v[1].y : j4 == 2 ? v[1].z : v[1].w;
+        uint16_t bh, bm, bl;
+        split1(e1, bh, bm, bl);
+        *(uint32_t*)h0 = (uint32_t)ah | ((uint32_t)bh << 16);
+        *(uint32_t*)(h0 + 4) = (uint32_t)am | ((uint32_t)bm << 16);
+        *(uint32_t*)h1 = (uint32_t)al | ((uint32_t)bl << 16);
+        *(uint32_t*)(h1 + 4) = (uint32_t)ah | ((uint32_t)bh << 16);
+      } else {
+        h0[0] = ah;
+        h0[4] = am;
+        h1[0] = al;
+        h1[4] = ah;
+      }
+    }
+  };
   auto store_step = [&](int buf, int kt) {
     float* Ps = smem + buf * (SP + SQ);
     float* Qs = Ps + SP;
     if constexpr (MODE == F_FWD) {
 #pragma unroll
-      for (int i = 0; i < UPK; ++i) *(float4*)(Ps + lds_off(pk_row[i], pk_ch[i])) = rp[i];
+      for (int i = 0; i < UPK; ++i) {
+        if constexpr (X6) store_k6(Ps, pk_row[i], pk_ch[i], rp[i]);
+        else *(float4*)(Ps + lds_off(pk_row[i], pk_ch[i])) = rp[i];
+      }
     } else {
-      store_mn(Ps, pm_rg, pm_kp, KUP, rp);
+      if constexpr (X6) store_mn6(Ps, pm_rg, pm_kp, KUP, rp);
+      else store_mn(Ps, pm_rg, pm_kp, KUP, rp);
     }
     if constexpr (MODE == F_FWD) {
       if (xf) {
@@ -576,9 +636,13 @@ __global__ __launch_bounds__(256, 2) void convf32_kernel(ConvF32Args a) {
     }
     if constexpr (MODE != F_WGRAD) {
 #pragma unroll
-      for (int i = 0; i < UQK; ++i) *(float4*)(Qs + lds_off(qk_row[i], qk_ch[i])) = rq[i];
+      for (int i = 0; i < UQK; ++i) {
+        if constexpr (X6) store_k6(Qs, qk_row[i], qk_ch[i], rq[i]);
+        else *(float4*)(Qs + lds_off(qk_row[i], qk_ch[i])) = rq[i];
+      }
     } else {
-      store_mn(Qs, qm_rg, qm_kp, KUQ, rq);
+      if constexpr (X6) store_mn6(Qs, qm_rg, qm_kp, KUQ, rq);
+      else store_mn(Qs, qm_rg, qm_kp, KUQ, rq);
     }
   };
 
@@ -598,34 +662,37 @@ __global__ __launch_bounds__(256, 2) void convf32_kernel(ConvF32Args a) {
       if (more) load_step(kt + 1);
       const float* Ps = smem + cur * (SP + SQ);
       const float* Qs = Ps + SP;
-      float4 af[TP], bfr[TQ];
-#pragma unroll
-      for (int ti = 0; ti < TP; ++ti)
-        af[ti] = *(const float4*)(Ps + lds_off(wp * WP + ti * 16 + (lane & 15), lane >> 4));
-#pragma unroll
-      for (int tj = 0; tj < TQ; ++tj)
-        bfr[tj] = *(const float4*)(Qs + lds_off(wq * WQ + tj * 16 + (lane & 15), lane >> 4));
       if constexpr (X6) {
-        s4v ah[TP], am[TP], al[TP], bh[TQ], bm[TQ], bl[TQ];
+        s8v a0[TP], a1[TP], b0[TQ], b1[TQ];
 #pragma unroll
-        for (int ti = 0; ti < TP; ++ti) split3(af[ti], ah[ti], am[ti], al[ti]);
+        for (int ti = 0; ti < TP; ++ti) {
+          const int R = wp * WP + ti * 16 + (lane & 15);
+          a0[ti] = *(const s8v*)(Ps + x6_off(R, lane >> 4, 0));
+          a1[ti] = *(const s8v*)(Ps + x6_off(R, lane >> 4, 1));
+        }
 #pragma unroll
-        for (int tj = 0; tj < TQ; ++tj) split3(bfr[tj], bh[tj], bm[tj], bl[tj]);
+        for (int tj = 0; tj < TQ; ++tj) {
+          const int R = wq * WQ + tj * 16 + (lane & 15);
+          b0[tj] = *(const s8v*)(Qs + x6_off(R, lane >> 4, 0));
+          b1[tj] = *(const s8v*)(Qs + x6_off(R, lane >> 4, 1));
+        }
 #pragma unroll
         for (int ti = 0; ti < TP; ++ti)
 #pragma unroll
           for (int tj = 0; tj < TQ; ++tj) {
-            // the step's 96 piece products from a zero accumulator, smallest terms first, then ONE
-            // IEEE add into the running sum: the bf16 MFMA's internal accumulation is not a
-            // round-to-nearest fp32 chain, and over a 10^5-deep WGRAD reduction its bias would
-            // reach 1e-3 relative; per step it stays at fp32-rounding level
-            f4v c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat44(al[ti], am[ti]), cat44(bh[tj], bm[tj]),
-                                                            (f4v){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat44(am[ti], ah[ti]), cat44(bh[tj], bl[tj]), c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat44(ah[ti], ah[ti]), cat44(bh[tj], bm[tj]), c, 0, 0, 0);
+            f4v c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[ti], b0[tj], (f4v){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[ti], b1[tj], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[ti], b0[tj], c, 0, 0, 0);
             acc[ti][tj] += c;
           }
       } else {
+        float4 af[TP], bfr[TQ];
+#pragma unroll
+        for (int ti = 0; ti < TP; ++ti)
+          af[ti] = *(const float4*)(Ps + lds_off(wp * WP + ti * 16 + (lane & 15), lane >> 4));
+#pragma unroll
+        for (int tj = 0; tj < TQ; ++tj)
+          bfr[tj] = *(const float4*)(Qs + lds_off(wq * WQ + tj * 16 + (lane & 15), lane >> 4));
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
