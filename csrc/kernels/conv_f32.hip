@@ -354,7 +354,7 @@ __device__ __forceinline__ int x6_off(int row, int ch, int half) {  // dwords
 
 // ------------------------------------------------------------------------------------ main kernel
 template <int MODE, int BP, int BQ, int X6>
-__global__ __launch_bounds__(256, 2) void convf32_kernel(ConvF32Args a) {
+__global__ __launch_bounds__(256, (X6 && BP * BQ <= 64 * 128) ? 3 : 2) void convf32_kernel(ConvF32Args a) {
   constexpr int WP = BP / 2, WQ = BQ / 2, TP = WP / 16, TQ = WQ / 16;
   constexpr int RW = X6 ? 32 : 16;              // dwords per image row (X6: 3 bf16 pieces + dup)
   constexpr int SP = BP * RW, SQ = BQ * RW;     // dwords per operand image

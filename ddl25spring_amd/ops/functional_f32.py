@@ -75,7 +75,7 @@ def cfg_of(bp: int, bq: int) -> int:
 #   "x6"    : each fp32 operand split exactly into 3 bf16 pieces, the 6 piece products above one
 #             fp32 rounding on the double-rate bf16 MFMA (2.7x fewer MFMA cycles per step).
 MATHS = ("mfma32", "x6")
-_MATH = [os.environ.get("DDL_F32_MATH", "mfma32")]
+_MATH = [os.environ.get("DDL_F32_MATH", "x6")]
 if _MATH[0] not in MATHS:
     raise ValueError(f"DDL_F32_MATH={_MATH[0]!r}: expected one of {MATHS}")
 
