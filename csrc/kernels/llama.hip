@@ -378,22 +378,30 @@ template <int HD> struct AttnLds {
 };
 
 // Stage rows r0..r0+63 (row t at src + t*rs) into LDS (row-major and/or transposed); rows >= S
-// and the row-major image's dims HD..HDP-1 are zeros.
+// and the row-major image's dims HD..HDP-1 are zeros. A thread owns a 4-row x 4-dim block: four
+// 8-byte row reads, then (transposed image) a 4x4 register transpose and four 8-byte writes of 4
+// consecutive rows per dim — a quarter of the LDS write instructions of per-element stores.
 template <int HD>
 __device__ __forceinline__ void stage_rows(const bf16_t* src, long long rs, int r0, int S,
                                            const float* rcos, const float* rsin, bf16_t* rm,
                                            bf16_t* tr) {
   constexpr int C4 = HD / 4, KP = AttnLds<HD>::KP, VP = AttnLds<HD>::VP, HDP = AttnLds<HD>::HDP;
-  for (int e = threadIdx.x; e < AT * C4; e += 256) {
-    const int r = e / C4, d0 = (e - r * C4) * 4, t = r0 + r;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    if (t < S)
-      row4(src + (long long)t * rs, rcos ? rcos + (long long)t * (HD / 2) : nullptr,
-           rsin ? rsin + (long long)t * (HD / 2) : nullptr, d0, v);
-    if (rm) *(s4v*)(rm + r * KP + d0) = bf4(v[0], v[1], v[2], v[3]);
+  for (int e = threadIdx.x; e < (AT / 4) * C4; e += 256) {
+    const int rq = e / C4, d0 = (e - rq * C4) * 4, rb = 4 * rq;
+    float v[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = r0 + rb + j;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[j][k] = 0.f;
+      if (t < S)
+        row4(src + (long long)t * rs, rcos ? rcos + (long long)t * (HD / 2) : nullptr,
+             rsin ? rsin + (long long)t * (HD / 2) : nullptr, d0, v[j]);
+      if (rm) *(s4v*)(rm + (rb + j) * KP + d0) = bf4(v[j][0], v[j][1], v[j][2], v[j][3]);
+    }
     if (tr) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) tr[(d0 + k) * VP + r] = f2bf(v[k]);
+      for (int k = 0; k < 4; ++k) *(s4v*)(tr + (d0 + k) * VP + rb) = bf4(v[0][k], v[1][k], v[2][k], v[3][k]);
     }
   }
   if constexpr (HDP > HD) {
