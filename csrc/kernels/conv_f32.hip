@@ -475,9 +475,12 @@ __global__ __launch_bounds__(256, (X6 && BP * BQ <= 64 * 128) ? 3 : 2) void conv
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
     return __builtin_bit_cast(float4, v);
   };
-  float4 rp[2], rq[2];
-  bool qv[2] = {false, false};  // Q units holding real (in-image) X data: the BN transform applies
-  auto load_step = [&](int kt) {
+  // Two register sets (A, B) of prefetched operands: the loads of step kt + 2 are issued while
+  // step kt computes and step kt + 1 waits in the other set to be stored — two steps of MFMA work
+  // cover the load latency (one step of the X6 engine's MFMAs does not cover an L2 miss).
+  float4 rpA[2], rqA[2], rpB[2], rqB[2];
+  bool qvA[2] = {false, false}, qvB[2] = {false, false};  // Q units holding real (in-image) X data
+  auto load_step = [&](int kt, float4 (&rp)[2], float4 (&rq)[2], bool (&qv)[2]) {
     const int kk0 = kt * FBK;
     // P operand
     if constexpr (MODE == F_FWD) {
@@ -605,7 +608,7 @@ __global__ __launch_bounds__(256, (X6 && BP * BQ <= 64 * 128) ? 3 : 2) void conv
       }
     }
   };
-  auto store_step = [&](int buf, int kt) {
+  auto store_step = [&](int buf, int kt, float4 (&rp)[2], float4 (&rq)[2], const bool (&qv)[2]) {
     float* Ps = smem + buf * (SP + SQ);
     float* Qs = Ps + SP;
     if constexpr (MODE == F_FWD) {
@@ -652,60 +655,66 @@ __global__ __launch_bounds__(256, (X6 && BP * BQ <= 64 * 128) ? 3 : 2) void conv
 #pragma unroll
     for (int j = 0; j < TQ; ++j) acc[i][j] = (f4v){0.f, 0.f, 0.f, 0.f};
 
-  if (kt0 < kt1) {
-    load_step(kt0);
-    store_step(0, kt0);
-    __syncthreads();
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const int cur = (kt - kt0) & 1;
-      const bool more = kt + 1 < kt1;
-      if (more) load_step(kt + 1);
-      const float* Ps = smem + cur * (SP + SQ);
-      const float* Qs = Ps + SP;
-      if constexpr (X6) {
-        s8v a0[TP], a1[TP], b0[TQ], b1[TQ];
+  auto step = [&](int kt, float4 (&cp)[2], float4 (&cq)[2], bool (&cv)[2], float4 (&np)[2],
+                  float4 (&nq)[2], bool (&nv)[2]) {
+    // cp/cq/cv: step kt + 1 (loaded two iterations ago); np/nq/nv receive step kt + 2
+    const int cur = (kt - kt0) & 1;
+    if (kt + 2 < kt1) load_step(kt + 2, np, nq, nv);
+    const float* Ps = smem + cur * (SP + SQ);
+    const float* Qs = Ps + SP;
+    if constexpr (X6) {
+      s8v a0[TP], a1[TP], b0[TQ], b1[TQ];
 #pragma unroll
-        for (int ti = 0; ti < TP; ++ti) {
-          const int R = wp * WP + ti * 16 + (lane & 15);
-          a0[ti] = *(const s8v*)(Ps + x6_off(R, lane >> 4, 0));
-          a1[ti] = *(const s8v*)(Ps + x6_off(R, lane >> 4, 1));
-        }
+      for (int ti = 0; ti < TP; ++ti) {
+        const int R = wp * WP + ti * 16 + (lane & 15);
+        a0[ti] = *(const s8v*)(Ps + x6_off(R, lane >> 4, 0));
+        a1[ti] = *(const s8v*)(Ps + x6_off(R, lane >> 4, 1));
+      }
+#pragma unroll
+      for (int tj = 0; tj < TQ; ++tj) {
+        const int R = wq * WQ + tj * 16 + (lane & 15);
+        b0[tj] = *(const s8v*)(Qs + x6_off(R, lane >> 4, 0));
+        b1[tj] = *(const s8v*)(Qs + x6_off(R, lane >> 4, 1));
+      }
+#pragma unroll
+      for (int ti = 0; ti < TP; ++ti)
 #pragma unroll
         for (int tj = 0; tj < TQ; ++tj) {
-          const int R = wq * WQ + tj * 16 + (lane & 15);
-          b0[tj] = *(const s8v*)(Qs + x6_off(R, lane >> 4, 0));
-          b1[tj] = *(const s8v*)(Qs + x6_off(R, lane >> 4, 1));
+          f4v c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[ti], b0[tj], (f4v){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[ti], b1[tj], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[ti], b0[tj], c, 0, 0, 0);
+          acc[ti][tj] += c;
         }
+    } else {
+      float4 af[TP], bfr[TQ];
+#pragma unroll
+      for (int ti = 0; ti < TP; ++ti)
+        af[ti] = *(const float4*)(Ps + lds_off(wp * WP + ti * 16 + (lane & 15), lane >> 4));
+#pragma unroll
+      for (int tj = 0; tj < TQ; ++tj)
+        bfr[tj] = *(const float4*)(Qs + lds_off(wq * WQ + tj * 16 + (lane & 15), lane >> 4));
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
         for (int ti = 0; ti < TP; ++ti)
 #pragma unroll
           for (int tj = 0; tj < TQ; ++tj) {
-            f4v c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[ti], b0[tj], (f4v){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[ti], b1[tj], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[ti], b0[tj], c, 0, 0, 0);
-            acc[ti][tj] += c;
+            const float av = s4 == 0 ? af[ti].x : s4 == 1 ? af[ti].y : s4 == 2 ? af[ti].z : af[ti].w;
+            const float bv = s4 == 0 ? bfr[tj].x : s4 == 1 ? bfr[tj].y : s4 == 2 ? bfr[tj].z : bfr[tj].w;
+            acc[ti][tj] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[ti][tj], 0, 0, 0);
           }
-      } else {
-        float4 af[TP], bfr[TQ];
-#pragma unroll
-        for (int ti = 0; ti < TP; ++ti)
-          af[ti] = *(const float4*)(Ps + lds_off(wp * WP + ti * 16 + (lane & 15), lane >> 4));
-#pragma unroll
-        for (int tj = 0; tj < TQ; ++tj)
-          bfr[tj] = *(const float4*)(Qs + lds_off(wq * WQ + tj * 16 + (lane & 15), lane >> 4));
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-          for (int ti = 0; ti < TP; ++ti)
-#pragma unroll
-            for (int tj = 0; tj < TQ; ++tj) {
-              const float av = s4 == 0 ? af[ti].x : s4 == 1 ? af[ti].y : s4 == 2 ? af[ti].z : af[ti].w;
-              const float bv = s4 == 0 ? bfr[tj].x : s4 == 1 ? bfr[tj].y : s4 == 2 ? bfr[tj].z : bfr[tj].w;
-              acc[ti][tj] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[ti][tj], 0, 0, 0);
-            }
-      }
-      if (more) store_step(cur ^ 1, kt + 1);
-      __syncthreads();
+    }
+    if (kt + 1 < kt1) store_step(cur ^ 1, kt + 1, cp, cq, cv);
+    __syncthreads();
+  };
+  if (kt0 < kt1) {
+    load_step(kt0, rpA, rqA, qvA);
+    if (kt0 + 1 < kt1) load_step(kt0 + 1, rpB, rqB, qvB);
+    store_step(0, kt0, rpA, rqA, qvA);
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; kt += 2) {
+      step(kt, rpB, rqB, qvB, rpA, rqA, qvA);
+      if (kt + 1 < kt1) step(kt + 1, rpA, rqA, qvA, rpB, rqB, qvB);
     }
   }
 
