@@ -318,8 +318,10 @@ __device__ __forceinline__ void fzero_slot(const ConvF32Args& a, const FGeo& o) 
 // MFMA's internal accumulation is not a round-to-nearest fp32 chain, and over a 10^5-deep WGRAD
 // reduction its bias would reach 1e-3 relative.
 // LDS image: row r holds 4 chunks x 8 dwords; chunk c's half h sits at dword
-//   r*32 + 8*(c ^ f(r&15)) + 4*(h ^ g(r&15)),  f = (b3 << 1) | (b1 ^ b2), g = b2 ^ b3  (bits of r)
-// which makes both halves' fragment reads conflict-free for the four ds_read_b128 lane groups.
+//   r*32 + 8*(c ^ f(r)) + 4*(h ^ g(r)),  f = b1 << 1, g = b0 ^ b2  (bits of r)
+// which makes both halves' fragment reads conflict-free for the four ds_read_b128 lane groups AND
+// the K-major ds_write_b128 stores (8-lane groups = rows 2m, 2m+1 x 4 chunks) conflict-free (the
+// previous swizzle left those stores 2-way; found by exhaustive search over XOR-linear swizzles).
 __device__ __forceinline__ void split3(float4 v, s4v& h, s4v& m, s4v& l) {
   const float x[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -346,9 +348,8 @@ __device__ __forceinline__ s8v cat44(s4v a, s4v b) {
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 __device__ __forceinline__ int x6_off(int row, int ch, int half) {  // dwords
-  const int r = row & 15;
-  const int f = (((r >> 3) & 1) << 1) | (((r >> 1) ^ (r >> 2)) & 1);
-  const int g = ((r >> 2) ^ (r >> 3)) & 1;
+  const int f = row & 2;                     // (b1 << 1)
+  const int g = (row ^ (row >> 2)) & 1;      // b0 ^ b2
   return row * 32 + 8 * (ch ^ f) + 4 * (half ^ g);
 }
 
@@ -487,7 +488,12 @@ __global__ __launch_bounds__(256, (X6 && BP * BQ <= 64 * 128) ? 3 : 2) void conv
 #pragma unroll
       for (int i = 0; i < UPK; ++i) {
         const int p = o.p0 + pk_row[i];
+#ifdef X6_PROBE_W128
+        const int odd = pk_row[i] & 1;
+        rp[i] = bload(rW, p < o.Pd ? (unsigned)((p - odd) * o.Kr + kk0 + 16 * odd + 4 * pk_ch[i]) * 4u : OOB);
+#else
         rp[i] = bload(rW, p < o.Pd ? (unsigned)(p * o.Kr + kk0 + 4 * pk_ch[i]) * 4u : OOB);
+#endif
       }
     } else if constexpr (MODE == F_DGRAD) {
       const int tap = kk0 / K, k0 = kk0 - tap * K;
@@ -516,7 +522,12 @@ __global__ __launch_bounds__(256, (X6 && BP * BQ <= 64 * 128) ? 3 : 2) void conv
         const int h = qk_hb[i] + r, w = qk_wb[i] + s;
         const bool ok = qk_n[i] >= 0 && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
         qv[i] = ok;
+#ifdef X6_PROBE_W128
+        const int odd = qk_row[i] & 1;
+        rq[i] = bload(rX, ok ? (unsigned)(((qk_n[i] * H + h) * W + w - odd) * C + c0 + 16 * odd + 4 * qk_ch[i]) * 4u : OOB);
+#else
         rq[i] = bload(rX, ok ? (unsigned)(((qk_n[i] * H + h) * W + w) * C + c0 + 4 * qk_ch[i]) * 4u : OOB);
+#endif
       }
     } else if constexpr (MODE == F_DGRAD) {
       const int tap = kk0 / K, k0 = kk0 - tap * K;
@@ -683,7 +694,10 @@ __global__ __launch_bounds__(256, (X6 && BP * BQ <= 64 * 128) ? 3 : 2) void conv
           f4v c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[ti], b0[tj], (f4v){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[ti], b1[tj], c, 0, 0, 0);
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[ti], b0[tj], c, 0, 0, 0);
-          acc[ti][tj] += c;
+          // four scalar v_add_f32 (this file builds with -fno-slp-vectorize): a packed
+          // v_pk_add_f32 issued beside MFMAs costs more than two plain adds
+#pragma unroll
+          for (int v = 0; v < 4; ++v) acc[ti][tj][v] = acc[ti][tj][v] + c[v];
         }
     } else {
       float4 af[TP], bfr[TQ];

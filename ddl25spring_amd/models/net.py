@@ -116,9 +116,24 @@ class Net:
         return x, ctxs
 
     grad_hook = None  # callable(layer_index) after each layer's weight grads are complete
-    # weight grads on a side stream (Fn.wgrad_overlap), opt-in with DDL_WGRAD_OVERLAP=1: measured
-    # slower on the graph-replayed ResNet-18 step (1 client: 138 -> 152 ms per round)
-    overlap_wgrad = os.environ.get("DDL_WGRAD_OVERLAP", "0") != "0"
+    # Weight grads on a side stream (Fn.wgrad_overlap). DDL_WGRAD_OVERLAP=1 / 0 forces it; by default
+    # it is on for fp32 activations, where it was measured faster on the graph-replayed ResNet-18
+    # FedAvg step (1 client 17.97k -> 19.11k, 8 clients 33.9k -> 35.0k samples/s), and off for
+    # bf16, where it was measured slower (1 client: 138 -> 152 ms per round).
+    _OVERLAP_ENV = os.environ.get("DDL_WGRAD_OVERLAP", "auto")
+
+    @property
+    def overlap_wgrad(self) -> bool:
+        forced = self.__dict__.get("_overlap_forced")
+        if forced is not None:
+            return forced
+        if self._OVERLAP_ENV in ("0", "1"):
+            return self._OVERLAP_ENV == "1"
+        return self.act_dtype == torch.float32
+
+    @overlap_wgrad.setter
+    def overlap_wgrad(self, on: bool) -> None:
+        self.__dict__["_overlap_forced"] = bool(on)
 
     def backward_native(self, dy, ctxs, part=None):
         """Backward through the first len(ctxs) layers (all of them unless a fused head already

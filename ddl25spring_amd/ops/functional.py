@@ -325,7 +325,18 @@ def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0, _tun
     if not accumulate and wgrad_scale(dw) != 1.0:
         raise ValueError("a scaled WGRAD must accumulate (it adds into the master weights)")
     if F32.is_f32(dy):
-        return F32.conv_wgrad(dy, x, geom, dw, accumulate, wgrad_scale(dw), in_bn=in_bn, split_k=splits)
+        side = _WGRAD_SIDE
+        if side is None:
+            return F32.conv_wgrad(dy, x, geom, dw, accumulate, wgrad_scale(dw), in_bn=in_bn, split_k=splits)
+        # side stream: after everything queued so far (the DGRAD that reads the weights this
+        # direct-SGD WGRAD steps), concurrent with the rest of the backward; joined on exit of
+        # wgrad_overlap. Its split-K workspace is the side stream's own (functional_f32.workspace).
+        side.wait_stream(torch.cuda.current_stream())
+        for t in (dy, x) + (tuple(in_bn) if in_bn is not None else ()):
+            t.record_stream(side)
+        with torch.cuda.stream(side):
+            return F32.conv_wgrad(dy, x, geom, dw, accumulate, wgrad_scale(dw), in_bn=in_bn, split_k=splits,
+                                  ws_role="side")
     x = _materialize_in_bn(x, in_bn)
     if not dy.is_cuda:
         ref.conv_wgrad(dy, x, geom, dw, accumulate, wgrad_scale(dw))
@@ -541,8 +552,9 @@ class wgrad_overlap:
     (after an event on the main stream), so a layer's weight gradient can overlap the main
     stream's dgrad -> BN-backward chain of the layers below it (the two are independent: wgrad
     only accumulates into the fp32 grad buffer). Leaving the context joins the side stream back;
-    captured in a HIP graph this is a fork/join per layer. Opt-in (``Net.overlap_wgrad``): on the
-    graph-replayed ResNet-18 step the cross-queue synchronisation cost more than the overlap won.
+    captured in a HIP graph this is a fork/join per layer. ``Net.overlap_wgrad`` turns it on for
+    fp32 nets (measured faster) and off for bf16 ones (the cross-queue synchronisation cost more
+    than the overlap won on the graph-replayed bf16 ResNet-18 step).
     ``run_joined(fn)`` runs ``fn`` (e.g. a DP all-reduce hook) ordered after both streams."""
 
     def __init__(self, device, enabled: bool = True):

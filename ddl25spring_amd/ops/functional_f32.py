@@ -42,8 +42,10 @@ class SlotStats:
         self.t = None
 
 
-def workspace(device) -> torch.Tensor | None:
-    key = str(device)
+def workspace(device, role: str = "main") -> torch.Tensor | None:
+    # one per (device, role): a side-stream WGRAD (role "side", functional.wgrad_overlap) runs
+    # concurrently with the main stream's split-K launches
+    key = f"{device}:{role}"
     b = _WS.get(key)
     if b is None:
         if torch.cuda.is_current_stream_capturing():
@@ -161,7 +163,7 @@ def _gs(t) -> int:
     return 0 if t is None else t.stride(0)
 
 
-def _launch(a, mode: int, geom, device, split_k: int = 0) -> None:
+def _launch(a, mode: int, geom, device, split_k: int = 0, ws_role: str = "main") -> None:
     lib = _lib.kernels()
     cfg, split = plan(mode, geom)
     if split_k:
@@ -170,7 +172,7 @@ def _launch(a, mode: int, geom, device, split_k: int = 0) -> None:
     cfg = _cfg(cfg)
     if split > 1:
         need = lib.ddl_convf32_workspace(ctypes.byref(a), mode, cfg)
-        buf = workspace(device)
+        buf = workspace(device, ws_role)
         if buf is None or need > buf.numel():
             a.split_k = split = 1
         else:
@@ -242,12 +244,12 @@ def conv_dgrad(dy, w, geom, residual=None, mask=None, out=None, bn=None, mask_bn
     return dx if bn is None else (dx, part)
 
 
-def conv_wgrad(dy, x, geom, dw, accumulate=True, gscale=1.0, in_bn=None, split_k=0):
+def conv_wgrad(dy, x, geom, dw, accumulate=True, gscale=1.0, in_bn=None, split_k=0, ws_role="main"):
     if not accumulate and gscale != 1.0:
         raise ValueError("a scaled WGRAD must accumulate (it adds into the master weights)")
     a = _args(geom, x=ptr(x), dy=ptr(dy), out=ptr(dw), x_gs=_gs(x), dy_gs=_gs(dy), out_gs=_gs(dw),
               accumulate=int(bool(accumulate)), gscale=float(gscale), **_xform(in_bn))
-    _launch(a, F_WGRAD, geom, dy.device, split_k)
+    _launch(a, F_WGRAD, geom, dy.device, split_k, ws_role)
     return dw
 
 

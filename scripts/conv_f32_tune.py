@@ -39,6 +39,13 @@ def resnet18_geoms(G: int, N: int):
     return list(dict.fromkeys(gs))
 
 
+def workspace_need(mode, g, bp, bq, split) -> int:
+    import ctypes
+    a = F32._args(g)
+    a.split_k = split
+    return int(F32._lib.kernels().ddl_convf32_workspace(ctypes.byref(a), mode, F32._cfg(F32.cfg_of(bp, bq))))
+
+
 def timed(fn, reps):
     for _ in range(2):
         fn()
@@ -84,10 +91,12 @@ def main():
                 res = []
                 for bp in (64, 128):
                     for bq in (64, 128):
-                        for split in (1, 2, 4, 8, 16, 32):
+                        for split in ((1, 2, 4, 8, 16, 32, 64, 128) if G <= 2 else (1, 2, 4, 8, 16, 32)):
                             F32.set_plan(mode, g, bp, bq, split)
+                            if split > 1 and workspace_need(mode, g, bp, bq, split) > F32.WS_CAP:
+                                continue  # would silently run unsplit
                             try:
-                                ms = timed(run, 5)
+                                ms = timed(run, 10)
                             except Exception as e:  # noqa: BLE001 (e.g. workspace too small)
                                 print("skip", name, g, bp, bq, split, e, flush=True)
                                 continue
