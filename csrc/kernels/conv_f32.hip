@@ -39,6 +39,11 @@
 //     larger strides (none in the model zoo) run unphased with a per-tap divisibility test.
 #include "ddl_common.h"
 
+// operand prefetch depth in steps (register sets): 2 or 3
+#ifndef F32_PREFETCH
+#define F32_PREFETCH 2
+#endif
+
 struct ConvF32Args {
   const float* x;         // [G][N][H][W][C]                    (group stride x_gs)
   const float* w;         // [G][K][R][S][C]                    (w_gs)
@@ -476,11 +481,13 @@ __global__ __launch_bounds__(256, (X6 && BP * BQ <= 64 * 128) ? 3 : 2) void conv
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
     return __builtin_bit_cast(float4, v);
   };
-  // Two register sets (A, B) of prefetched operands: the loads of step kt + 2 are issued while
-  // step kt computes and step kt + 1 waits in the other set to be stored — two steps of MFMA work
-  // cover the load latency (one step of the X6 engine's MFMAs does not cover an L2 miss).
-  float4 rpA[2], rqA[2], rpB[2], rqB[2];
-  bool qvA[2] = {false, false}, qvB[2] = {false, false};  // Q units holding real (in-image) X data
+  // PF register sets of prefetched operands (PF = F32_PREFETCH, 2 or 3): the loads of step kt + PF
+  // are issued while step kt computes and steps kt + 1 .. kt + PF - 1 wait in the other sets to be
+  // stored — PF steps of MFMA work cover the load latency (one step of the X6 engine's MFMAs does
+  // not cover an L2 miss under load).
+  constexpr int PF = F32_PREFETCH;
+  float4 rpA[2], rqA[2], rpB[2], rqB[2], rpC[2], rqC[2];
+  bool qvA[2] = {false, false}, qvB[2] = {false, false}, qvC[2] = {false, false};  // real (in-image) X data
   auto load_step = [&](int kt, float4 (&rp)[2], float4 (&rq)[2], bool (&qv)[2]) {
     const int kk0 = kt * FBK;
     // P operand
@@ -488,12 +495,7 @@ __global__ __launch_bounds__(256, (X6 && BP * BQ <= 64 * 128) ? 3 : 2) void conv
 #pragma unroll
       for (int i = 0; i < UPK; ++i) {
         const int p = o.p0 + pk_row[i];
-#ifdef X6_PROBE_W128
-        const int odd = pk_row[i] & 1;
-        rp[i] = bload(rW, p < o.Pd ? (unsigned)((p - odd) * o.Kr + kk0 + 16 * odd + 4 * pk_ch[i]) * 4u : OOB);
-#else
         rp[i] = bload(rW, p < o.Pd ? (unsigned)(p * o.Kr + kk0 + 4 * pk_ch[i]) * 4u : OOB);
-#endif
       }
     } else if constexpr (MODE == F_DGRAD) {
       const int tap = kk0 / K, k0 = kk0 - tap * K;
@@ -522,12 +524,7 @@ __global__ __launch_bounds__(256, (X6 && BP * BQ <= 64 * 128) ? 3 : 2) void conv
         const int h = qk_hb[i] + r, w = qk_wb[i] + s;
         const bool ok = qk_n[i] >= 0 && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
         qv[i] = ok;
-#ifdef X6_PROBE_W128
-        const int odd = qk_row[i] & 1;
-        rq[i] = bload(rX, ok ? (unsigned)(((qk_n[i] * H + h) * W + w - odd) * C + c0 + 16 * odd + 4 * qk_ch[i]) * 4u : OOB);
-#else
         rq[i] = bload(rX, ok ? (unsigned)(((qk_n[i] * H + h) * W + w) * C + c0 + 4 * qk_ch[i]) * 4u : OOB);
-#endif
       }
     } else if constexpr (MODE == F_DGRAD) {
       const int tap = kk0 / K, k0 = kk0 - tap * K;
@@ -668,9 +665,9 @@ __global__ __launch_bounds__(256, (X6 && BP * BQ <= 64 * 128) ? 3 : 2) void conv
 
   auto step = [&](int kt, float4 (&cp)[2], float4 (&cq)[2], bool (&cv)[2], float4 (&np)[2],
                   float4 (&nq)[2], bool (&nv)[2]) {
-    // cp/cq/cv: step kt + 1 (loaded two iterations ago); np/nq/nv receive step kt + 2
+    // cp/cq/cv: step kt + 1 (loaded PF - 1 iterations ago); np/nq/nv receive step kt + PF
     const int cur = (kt - kt0) & 1;
-    if (kt + 2 < kt1) load_step(kt + 2, np, nq, nv);
+    if (kt + PF < kt1) load_step(kt + PF, np, nq, nv);
     const float* Ps = smem + cur * (SP + SQ);
     const float* Qs = Ps + SP;
     if constexpr (X6) {
@@ -724,11 +721,23 @@ __global__ __launch_bounds__(256, (X6 && BP * BQ <= 64 * 128) ? 3 : 2) void conv
   if (kt0 < kt1) {
     load_step(kt0, rpA, rqA, qvA);
     if (kt0 + 1 < kt1) load_step(kt0 + 1, rpB, rqB, qvB);
+    if constexpr (PF == 3) {
+      if (kt0 + 2 < kt1) load_step(kt0 + 2, rpC, rqC, qvC);
+    }
     store_step(0, kt0, rpA, rqA, qvA);
     __syncthreads();
-    for (int kt = kt0; kt < kt1; kt += 2) {
-      step(kt, rpB, rqB, qvB, rpA, rqA, qvA);
-      if (kt + 1 < kt1) step(kt + 1, rpA, rqA, qvA, rpB, rqB, qvB);
+    if constexpr (PF == 3) {
+      // set of step k = (k - kt0) % 3: A, B, C
+      for (int kt = kt0; kt < kt1; kt += 3) {
+        step(kt, rpB, rqB, qvB, rpA, rqA, qvA);
+        if (kt + 1 < kt1) step(kt + 1, rpC, rqC, qvC, rpB, rqB, qvB);
+        if (kt + 2 < kt1) step(kt + 2, rpA, rqA, qvA, rpC, rqC, qvC);
+      }
+    } else {
+      for (int kt = kt0; kt < kt1; kt += 2) {
+        step(kt, rpB, rqB, qvB, rpA, rqA, qvA);
+        if (kt + 1 < kt1) step(kt + 1, rpA, rqA, qvA, rpB, rqB, qvB);
+      }
     }
   }
 
