@@ -40,23 +40,25 @@ struct BNFArgs {  // same layout as BNArgs (batchnorm.hip); stats = [G][stripes]
   int training, stripes;
 };
 
-// Fixed-order fold of S slots of one group: thread (sg, cl) of a 256-thread block owning 32
-// channels sums slots sg, sg+8, ... in double; the 8 partials meet in LDS. Totals on sg == 0.
+// Fixed-order fold of S slots of one group: thread (sg, cl) of a FOLD_T-thread block owning 32
+// channels sums slots sg, sg+NSG, ... in double (NSG = FOLD_T / 32 slot groups); the NSG partials
+// meet in LDS and are added in group order. Totals on sg == 0. (A 1024-thread block keeps 32 slot
+// streams in flight per channel: the fold is latency-bound on its few blocks — 2 for C = 64 — and
+// ran ~10 us per launch with 8 groups at one client per GPU.)
+constexpr int FOLD_T = 1024, NSG = FOLD_T / 32;
 __device__ __forceinline__ void slot_fold(const float* __restrict__ base, int S, int C, int c, bool valid,
                                           double* red, double& t0, double& t1) {
   const int sg = threadIdx.x >> 5, cl = threadIdx.x & 31;
   double a0 = 0.0, a1 = 0.0;
   if (valid) {
     int k = sg;
-    for (; k + 24 < S; k += 32) {  // 4 slots' loads in flight
+    for (; k + NSG < S; k += 2 * NSG) {  // 2 slots' loads in flight per thread
       const float x0 = base[(long long)k * 2 * C + c], y0 = base[(long long)k * 2 * C + C + c];
-      const float x1 = base[(long long)(k + 8) * 2 * C + c], y1 = base[(long long)(k + 8) * 2 * C + C + c];
-      const float x2 = base[(long long)(k + 16) * 2 * C + c], y2 = base[(long long)(k + 16) * 2 * C + C + c];
-      const float x3 = base[(long long)(k + 24) * 2 * C + c], y3 = base[(long long)(k + 24) * 2 * C + C + c];
-      a0 += x0; a0 += x1; a0 += x2; a0 += x3;
-      a1 += y0; a1 += y1; a1 += y2; a1 += y3;
+      const float x1 = base[(long long)(k + NSG) * 2 * C + c], y1 = base[(long long)(k + NSG) * 2 * C + C + c];
+      a0 += x0; a0 += x1;
+      a1 += y0; a1 += y1;
     }
-    for (; k < S; k += 8) {
+    for (; k < S; k += NSG) {
       a0 += base[(long long)k * 2 * C + c];
       a1 += base[(long long)k * 2 * C + C + c];
     }
@@ -66,8 +68,8 @@ __device__ __forceinline__ void slot_fold(const float* __restrict__ base, int S,
   __syncthreads();
   t0 = t1 = 0.0;
   if (sg == 0) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
+#pragma unroll 8
+    for (int k = 0; k < NSG; ++k) {
       t0 += red[k * 64 + cl];
       t1 += red[k * 64 + 32 + cl];
     }
@@ -111,8 +113,8 @@ __device__ __forceinline__ void bnf_finalize_body(const BNFArgs& a, double* red)
   a.rstd[i] = rs;
 }
 
-__global__ __launch_bounds__(256) void bnf_finalize_kernel(BNFArgs a, BNFArgs b) {
-  __shared__ double red[8 * 64];
+__global__ __launch_bounds__(FOLD_T) void bnf_finalize_kernel(BNFArgs a, BNFArgs b) {
+  __shared__ double red[NSG * 64];
   bnf_finalize_body(blockIdx.z ? b : a, red);
 }
 
@@ -121,7 +123,7 @@ DDL_API int ddl_bnf_finalize(const BNFArgs* a, const BNFArgs* b, hipStream_t s) 
   const int nbn = b ? 2 : 1;
   if (b && (b->G != a->G || (b->training && b->stripes < 1))) return (int)hipErrorInvalidValue;
   const int C = (b && b->C > a->C) ? b->C : a->C;
-  hipLaunchKernelGGL(bnf_finalize_kernel, dim3((C + 31) / 32, a->G, nbn), dim3(256), 0, s, *a, b ? *b : *a);
+  hipLaunchKernelGGL(bnf_finalize_kernel, dim3((C + 31) / 32, a->G, nbn), dim3(FOLD_T), 0, s, *a, b ? *b : *a);
   return (int)hipGetLastError();
 }
 DDL_API int ddl_bnf_args_size() { return (int)sizeof(BNFArgs); }
@@ -341,8 +343,8 @@ __device__ __forceinline__ void bnf_fold_body(const BNFBwdArgs& t, long long M, 
   t.coef[(long long)g * 3 * C + 2 * C + c] = (float)(-A * s0 * invM - B * mu);
 }
 
-__global__ __launch_bounds__(256) void bnf_fold_kernel(BNFBwdArgs a, BNFBwdArgs b, long long M, int C) {
-  __shared__ double red[8 * 64];
+__global__ __launch_bounds__(FOLD_T) void bnf_fold_kernel(BNFBwdArgs a, BNFBwdArgs b, long long M, int C) {
+  __shared__ double red[NSG * 64];
   bnf_fold_body(blockIdx.z ? b : a, M, C, red);
 }
 
@@ -416,7 +418,7 @@ DDL_API int ddl_bnf_backward(const float* dy, const float* ymask, const BNFBwdAr
   if (a.slots < 1 || (bp && bp->slots < 1)) return (int)hipErrorInvalidValue;
   const int two = bp ? 1 : 0;
   const BNFBwdArgs b = bp ? *bp : a;
-  hipLaunchKernelGGL(bnf_fold_kernel, dim3((C + 31) / 32, G, 1 + two), dim3(256), 0, s, a, b, M, C);
+  hipLaunchKernelGGL(bnf_fold_kernel, dim3((C + 31) / 32, G, 1 + two), dim3(FOLD_T), 0, s, a, b, M, C);
   const int RPI = 256 / (C / 4);
   hipLaunchKernelGGL(bnf_bwd_apply_kernel, dim3(fstream_blocks(M, RPI, G, 4), G), dim3(256), 0, s, dy, ymask, a, b,
                      two, dym_out, M, C);
@@ -686,9 +688,9 @@ DDL_API int ddl_headf_train(const HeadFArgs* ap, hipStream_t s) {
 // Deterministic per-channel column sum (bias gradients): out[g][c] (+ g * gs) += sum_m x[g][m][c]
 // via per-block slots (bnf_reduce_kernel<1>) and a fixed-order fold — the fp32 twin of
 // nn_ops.hip's atomic channel_sum.
-__global__ __launch_bounds__(256) void bnf_colsum_fold_kernel(const float* __restrict__ part, int S, float* out,
-                                                              long long gs, int C) {
-  __shared__ double red[8 * 64];
+__global__ __launch_bounds__(FOLD_T) void bnf_colsum_fold_kernel(const float* __restrict__ part, int S, float* out,
+                                                                 long long gs, int C) {
+  __shared__ double red[NSG * 64];
   const int g = blockIdx.y, c = blockIdx.x * 32 + (threadIdx.x & 31);
   const bool valid = c < C;
   double s0, s1;
@@ -703,7 +705,7 @@ DDL_API int ddl_bnf_channel_sum(const float* x, float* out, long long gs, float*
   if (S < 1) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(bnf_reduce_kernel<1>, dim3(S, G), dim3(256), 0, s, (const float*)nullptr,
                      (const float*)nullptr, x, (const float*)nullptr, (const float*)nullptr, part, M, C);
-  hipLaunchKernelGGL(bnf_colsum_fold_kernel, dim3((C + 31) / 32, G), dim3(256), 0, s, (const float*)part, S, out,
+  hipLaunchKernelGGL(bnf_colsum_fold_kernel, dim3((C + 31) / 32, G), dim3(FOLD_T), 0, s, (const float*)part, S, out,
                      gs, C);
   return (int)hipGetLastError();
 }
