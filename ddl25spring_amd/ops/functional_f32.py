@@ -75,9 +75,12 @@ def cfg_of(bp: int, bq: int) -> int:
 # Product engine of the fp32 convolutions (csrc/kernels/conv_f32.hip):
 #   "mfma32": exact fp32 MFMA (v_mfma_f32_16x16x4_f32);
 #   "x6"    : each fp32 operand split exactly into 3 bf16 pieces, the 6 piece products above one
-#             fp32 rounding on the double-rate bf16 MFMA (2.7x fewer MFMA cycles per step).
-MATHS = ("mfma32", "x6")
-_MATH = [os.environ.get("DDL_F32_MATH", "x6")]
+#             fp32 rounding on the double-rate bf16 MFMA (2.7x fewer MFMA cycles per step);
+#   "auto"  : per (mode, geometry) whichever engine the tuner measured faster (plans keyed
+#             "auto:...", [bp, bq, split, engine]); untuned launches use X6. Both engines meet the
+#             same fp32 tolerances, so mixing them per layer changes only rounding-level detail.
+MATHS = ("mfma32", "x6", "auto")
+_MATH = [os.environ.get("DDL_F32_MATH", "auto")]
 if _MATH[0] not in MATHS:
     raise ValueError(f"DDL_F32_MATH={_MATH[0]!r}: expected one of {MATHS}")
 
@@ -94,8 +97,16 @@ def set_math(name: str) -> None:
         _PLANS.clear()  # plans are tuned per engine
 
 
+X6_BIT = 1 << 16
+
+
 def _cfg(cfg: int) -> int:
-    return cfg | (1 << 16) if _MATH[0] == "x6" else cfg
+    """Launch cfg with the engine bit: forced by a fixed engine; under "auto" the plan's own."""
+    if _MATH[0] == "x6":
+        return cfg | X6_BIT
+    if _MATH[0] == "mfma32":
+        return cfg & ~X6_BIT
+    return cfg
 
 
 _PLANS: dict = {}
@@ -115,15 +126,22 @@ def _tuned(mode: int, g):
             with open(_TUNED_PATH) as f:
                 _TUNED = json.load(f).get("plans", {})
     key = f"{_MODE_NAMES[mode]}:{g.G},{g.N},{g.H},{g.W},{g.C},{g.K},{g.R},{g.S},{g.stride},{g.pad}"
+    if _MATH[0] == "auto":
+        p = _TUNED.get(f"auto:{key}")
+        if p is not None:
+            return cfg_of(p[0], p[1]) | (X6_BIT if p[3] == "x6" else 0), int(p[2])
+        p = _TUNED.get(f"x6:{key}")
+        return None if p is None else (cfg_of(p[0], p[1]) | X6_BIT, int(p[2]))
     if _MATH[0] != "mfma32":
         key = f"{_MATH[0]}:{key}"
     p = _TUNED.get(key)
     return None if p is None else (cfg_of(p[0], p[1]), int(p[2]))
 
 
-def set_plan(mode: int, geom, bp: int, bq: int, split: int) -> None:
-    """Pin a launch plan (tile BP x BQ, split-K slices) for one (mode, geometry) — the tuner."""
-    _OVERRIDE[(mode, geom)] = (cfg_of(bp, bq), int(split))
+def set_plan(mode: int, geom, bp: int, bq: int, split: int, engine: str | None = None) -> None:
+    """Pin a launch plan (tile BP x BQ, split-K slices[, engine under "auto"]) for one (mode,
+    geometry) — the tuner."""
+    _OVERRIDE[(mode, geom)] = (cfg_of(bp, bq) | (X6_BIT if engine in (None, "x6") else 0), int(split))
     _PLANS.pop((mode, geom), None)
 
 
@@ -144,7 +162,7 @@ def plan(mode: int, geom) -> tuple[int, int]:
         split = 1
         while tiles * split < TARGET_WG and nk >= split * 2 * 8 and split < 64:
             split *= 2
-        p = (cfg_of(bp, bq), split)
+        p = (cfg_of(bp, bq) | X6_BIT, split)
     _PLANS[key] = p
     return p
 

@@ -69,6 +69,7 @@ def main():
     a = ap.parse_args()
     F32.set_math(a.math)
     prefix = "" if a.math == "mfma32" else f"{a.math}:"
+    engines = ("x6", "mfma32") if a.math == "auto" else (None,)
     dev = torch.device("cuda")
     t_start = time.time()
     plans, report = {}, []
@@ -89,28 +90,34 @@ def main():
                        F32.F_DGRAD: lambda: F32.conv_dgrad(dy, w, g),
                        F32.F_WGRAD: lambda: F32.conv_wgrad(dy, x, g, dw)}[mode]
                 res = []
-                for bp in (64, 128):
-                    for bq in (64, 128):
-                        for split in ((1, 2, 4, 8, 16, 32, 64, 128) if G <= 2 else (1, 2, 4, 8, 16, 32)):
-                            F32.set_plan(mode, g, bp, bq, split)
-                            if split > 1 and workspace_need(mode, g, bp, bq, split) > F32.WS_CAP:
-                                continue  # would silently run unsplit
-                            try:
-                                ms = timed(run, 10)
-                            except Exception as e:  # noqa: BLE001 (e.g. workspace too small)
-                                print("skip", name, g, bp, bq, split, e, flush=True)
-                                continue
-                            res.append((ms, bp, bq, split))
+                for eng in engines:
+                    for bp in (64, 128):
+                        for bq in (64, 128):
+                            for split in ((1, 2, 4, 8, 16, 32, 64, 128) if G <= 2 else (1, 2, 4, 8, 16, 32)):
+                                F32.set_plan(mode, g, bp, bq, split, eng)
+                                if split > 1 and workspace_need(mode, g, bp, bq, split) > F32.WS_CAP:
+                                    continue  # would silently run unsplit
+                                try:
+                                    ms = timed(run, 10)
+                                except Exception as e:  # noqa: BLE001 (e.g. workspace too small)
+                                    print("skip", name, g, bp, bq, split, e, flush=True)
+                                    continue
+                                res.append((ms, bp, bq, split, eng))
                 F32._OVERRIDE.pop((mode, g), None)
                 F32._PLANS.pop((mode, g), None)
-                res.sort()
-                ms, bp, bq, split = res[0]
-                hms = next(r[0] for r in res if F32.cfg_of(r[1], r[2]) == heur[0] and r[3] == heur[1]) \
-                    if any(F32.cfg_of(r[1], r[2]) == heur[0] and r[3] == heur[1] for r in res) else None
+                res.sort(key=lambda r: r[0])
+                ms, bp, bq, split, eng = res[0]
+                hcfg = heur[0] & ~F32.X6_BIT
+                hms = next((r[0] for r in res if F32.cfg_of(r[1], r[2]) == hcfg and r[3] == heur[1]
+                            and r[4] in (None, "x6")), None)
                 key = f"{prefix}{name}:{g.G},{g.N},{g.H},{g.W},{g.C},{g.K},{g.R},{g.S},{g.stride},{g.pad}"
-                plans[key] = [bp, bq, split]
+                plans[key] = [bp, bq, split] + ([eng] if eng else [])
+                best_other = None
+                if a.math == "auto":  # the other engine's best, for the report
+                    best_other = next((round(r[0], 4) for r in res if r[4] != eng), None)
                 row = dict(math=a.math, mode=name, G=g.G, N=g.N, H=g.H, C=g.C, K=g.K, R=g.R, stride=g.stride,
-                           best_ms=round(ms, 4), plan=[bp, bq, split], tflops=round(flops / ms / 1e9, 1),
+                           best_ms=round(ms, 4), plan=plans[key], other_engine_ms=best_other,
+                           tflops=round(flops / ms / 1e9, 1),
                            pct_peak=round(100 * flops / ms / 1e9 / PEAK_TF, 1),
                            heuristic_ms=None if hms is None else round(hms, 4))
                 report.append(row)

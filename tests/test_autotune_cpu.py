@@ -60,3 +60,29 @@ def test_pick_caches_and_respects_disable(monkeypatch):
     assert not calls
     monkeypatch.setitem(autotune._CACHE, autotune._key("fwd", g, (True,)), (123, 0))
     assert autotune.pick("fwd", g, (True,), lambda c, s: calls.append(c)) == (123, 0)
+
+
+def test_fp32_plans_engine_choice():
+    """fp32 conv plans: under "auto" a tuned plan carries its engine (X6 bit in the launch cfg),
+    an x6-only entry falls back to X6, and a fixed engine forces / clears the bit."""
+    from ddl25spring_amd.ops import functional_f32 as F32
+    from ddl25spring_amd.ops.functional import ConvGeom
+    g = ConvGeom(3, 7, 8, 8, 16, 16, 3, 3, 1, 1)
+    key = "fwd:3,7,8,8,16,16,3,3,1,1"
+    old_math, old_tuned = F32.math(), F32._TUNED
+    try:
+        F32._TUNED = {f"auto:{key}": [64, 128, 4, "mfma32"], f"x6:dgrad:3,7,8,8,16,16,3,3,1,1": [128, 64, 2]}
+        F32.set_math("auto")
+        F32._PLANS.clear()
+        cfg, split = F32.plan(F32.F_FWD, g)
+        assert (cfg, split) == (F32.cfg_of(64, 128), 4) and F32._cfg(cfg) & F32.X6_BIT == 0
+        cfg, split = F32.plan(F32.F_DGRAD, g)
+        assert (cfg, split) == (F32.cfg_of(128, 64) | F32.X6_BIT, 2)
+        F32.set_math("mfma32")
+        assert F32._cfg(F32.cfg_of(64, 64) | F32.X6_BIT) == F32.cfg_of(64, 64)
+        F32.set_math("x6")
+        assert F32._cfg(F32.cfg_of(64, 64)) & F32.X6_BIT
+    finally:
+        F32._TUNED = old_tuned
+        F32.set_math(old_math)
+        F32._PLANS.clear()

@@ -19,9 +19,10 @@ from ddl25spring_amd.ops.functional import ConvGeom
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["mfma32", "x6"])
+@pytest.fixture(params=["mfma32", "x6", "auto"])
 def fmath(request):
-    """Both fp32 product engines: the exact fp32 MFMA and the 3-way-split bf16 MFMA (x6)."""
+    """Both fp32 product engines — the exact fp32 MFMA and the 3-way-split bf16 MFMA (x6) — and
+    the default per-layer mix of the two (auto: the tuned plans pick the engine)."""
     old = F32.math()
     F32.set_math(request.param)
     yield request.param
