@@ -1,7 +1,8 @@
 """BASELINE config #3: data-parallel all-reduce SGD, ResNet-50 ImageNet-shape, one rank per GPU.
 
-Each rank: native ResNet-50 (MFMA implicit-GEMM convs, fused BN, bf16 activations, fp32 master
-weights) on its own synthetic 224x224x3 batch; gradients all-reduced over RCCL in layer-aligned
+Each rank: native ResNet-50 (MFMA implicit-GEMM convs, fused BN; fp32 activations and weights by
+default — the reference's precision — or --precision bf16: bf16 activations, fp32 master weights)
+on its own synthetic 224x224x3 batch; gradients all-reduced over RCCL in layer-aligned
 buckets launched from the backward pass (overlapped); SGD momentum 0.9, wd 1e-4. Weak scaling
 (fixed per-GPU batch). value = images/s over all GPUs.
 
@@ -25,6 +26,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--pool", type=int, default=1024, help="distinct synthetic images per rank")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--precision", default="fp32", choices=("fp32", "bf16"))
     args = ap.parse_args()
     from ddl25spring_amd.data.images import DeviceImageDataset, ImageArrays
     from ddl25spring_amd.models import resnet50_imagenet
@@ -36,7 +38,7 @@ def main():
     rng = np.random.default_rng(ctx.rank)
     arr = ImageArrays(rng.integers(0, 256, (args.pool, 224, 224, 3), dtype=np.uint8),
                       rng.integers(0, 1000, args.pool), "imagenet", True)
-    net = resnet50_imagenet(groups=1).to(dev, seed=0)
+    net = resnet50_imagenet(groups=1, precision=args.precision).to(dev, seed=0)
     ctx.broadcast(net.store.data, 0)
     ctx.broadcast(net.store.buffers, 0)
     net.store.sync_shadow()
@@ -66,7 +68,7 @@ def main():
     emit(ctx, metric="ResNet-50 DP all-reduce SGD images/s (ImageNet-shape)", value=round(ips, 1),
          unit="images/s", n_gpus=ctx.world, steps=args.steps, warmup=args.warmup,
          ms_per_step=round(1e3 * dt / args.steps, 3), higher_is_better=True, scaling="weak",
-         vs_baseline=None, dtype="bf16", data="synthetic",
+         vs_baseline=None, dtype=args.precision, data="synthetic",
          allreduce_busbw_GBps=None if busbw is None else round(busbw, 1),
          config={"model": "resnet50-imagenet", "global_batch": ctx.world * args.batch,
                  "seq_len": None, "parallelism": f"dp{ctx.world}", "per_gpu_batch": args.batch})

@@ -121,7 +121,10 @@ class LocalTrainer:
         # frozen first_step=False inside the graph is exact for every step of a round
         assert opt.dampening == 0.0
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, capture_error_mode=CAPTURE_MODE):
+        # DDL_GRAPH_PRIO=1: capture on a high-priority stream, so the step's critical path (the
+        # main stream) outranks the side-stream weight gradients (Fn.wgrad_overlap) it overlaps
+        cap = torch.cuda.Stream(priority=-1) if os.environ.get("DDL_GRAPH_PRIO", "0") == "1" else None
+        with torch.cuda.graph(graph, stream=cap, capture_error_mode=CAPTURE_MODE):
             for i in range(nsteps):
                 loss = self._step(plan[i], 0, G)
             if tl is not None:

@@ -443,3 +443,32 @@ def test_fp32_mnist_cnn_step_matches_torch(cuda, fmath):
     g = convert.export_torch(net, tm, mnist_cnn_mapping(), grads=True)
     for name, p in tm.named_parameters():
         assert _err(g[name], p.grad) <= 1e-4, name
+
+
+def test_resnet50_fp32_step_matches_torch(cuda):
+    """BASELINE config 3's model at the reference's precision: one native fp32 ResNet-50 training
+    step (bottleneck blocks, 7x7 im2col stem, max pool, 1x1 convs up to 2048 channels; default
+    engine mix) vs torch autograd in float64 on a small ImageNet-shaped batch: loss and every
+    parameter gradient within 1e-4 (max-abs relative)."""
+    from ddl25spring_amd.models import convert, resnet50_imagenet
+    from ddl25spring_amd.models.torch_ref import torch_resnet50_imagenet
+    torch.manual_seed(0)
+    tm = torch_resnet50_imagenet(1000)
+    net = resnet50_imagenet(1000, groups=1, precision="fp32").to(cuda)
+    mapping = convert.resnet_mapping(net)
+    convert.import_torch(net, tm, mapping)
+    torch.manual_seed(1)
+    x = torch.randn(2, 3, 112, 112)
+    y = torch.randint(0, 1000, (2,))
+    net.store.zero_grad()
+    xin = net.prepare_input(x.to(cuda))
+    assert xin.dtype == torch.float32
+    loss, _ = net.train_step(xin, y.view(1, -1).to(cuda, torch.int32))
+    t64 = tm.double()
+    lt = F.cross_entropy(t64(x.double()), y)
+    lt.backward()
+    assert abs(loss[0].item() - lt.item()) <= 1e-5 * abs(lt.item())
+    g = convert.export_torch(net, t64, mapping, group=0, grads=True)
+    for name, p in t64.named_parameters():
+        e = _err(g[name], p.grad)
+        assert e <= 1e-4, (name, e)
