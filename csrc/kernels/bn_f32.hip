@@ -23,7 +23,7 @@
 // variance) of the north-star ResNets; nn.AdaptiveAvgPool2d + nn.Linear + F.cross_entropy.
 #include "ddl_common.h"
 
-struct BNFArgs {  // same layout as BNArgs (batchnorm.hip); stats = [G][stripes][2][C] slots
+struct BNFArgs {  // BNArgs (batchnorm.hip) + tile_rows; stats = [G][stripes][2][C] slots
   const float* stats;
   const float* gamma;
   const float* beta;
@@ -38,6 +38,8 @@ struct BNFArgs {  // same layout as BNArgs (batchnorm.hip); stats = [G][stripes]
   long long count;
   float eps, momentum;
   int training, stripes;
+  int tile_rows;  // > 0: slot i holds (sum, M2 about its own mean) of min(tile_rows, count - i*tile_rows) rows
+  int pad_;
 };
 
 // Fixed-order fold of S slots of one group: thread (sg, cl) of a FOLD_T-thread block owning 32
@@ -76,6 +78,38 @@ __device__ __forceinline__ void slot_fold(const float* __restrict__ base, int S,
   }
 }
 
+// Chan's parallel merge of per-tile (sum, M2) slots, fixed order, in double: mean = sum S0 / M,
+// M2 = sum M2_i + sum (S0_i - n_i mean)^2 / n_i, n_i = min(rows, M - i * rows). Two slot passes.
+__device__ __forceinline__ void slot_fold_chan(const float* __restrict__ base, int S, int C, int c, bool valid,
+                                               double* red, long long M, int rows, double& mean, double& m2) {
+  double t0, t1;
+  slot_fold(base, S, C, c, valid, red, t0, t1);  // t0 = sum S0, t1 = sum M2 (on sg == 0)
+  const int sg = threadIdx.x >> 5, cl = threadIdx.x & 31;
+  __syncthreads();
+  if (sg == 0) red[cl] = t0 / (double)M;
+  __syncthreads();
+  const double mu = red[cl];
+  __syncthreads();
+  double a = 0.0;
+  if (valid) {
+    for (int k = sg; k < S; k += NSG) {
+      const long long rem = M - (long long)k * rows;
+      const double n = (double)(rem < rows ? rem : rows);
+      if (n <= 0.0) continue;
+      const double d = (double)base[(long long)k * 2 * C + c] - n * mu;
+      a += d * d / n;
+    }
+  }
+  red[sg * 64 + cl] = a;
+  __syncthreads();
+  double b = 0.0;
+  if (sg == 0) {
+    for (int k = 0; k < NSG; ++k) b += red[k * 64 + cl];
+  }
+  mean = mu;
+  m2 = t1 + b;
+}
+
 __device__ __forceinline__ void bnf_finalize_body(const BNFArgs& a, double* red) {
   const int g = blockIdx.y, c = blockIdx.x * 32 + (threadIdx.x & 31);
   const bool valid = c < a.C;
@@ -86,12 +120,21 @@ __device__ __forceinline__ void bnf_finalize_body(const BNFArgs& a, double* red)
   const float rm0 = rs_io ? a.running_mean[o] : 0.f, rv0 = rs_io ? a.running_var[o] : 0.f;
   float mean, var;
   if (a.training) {
-    double s1, s2;
-    slot_fold(a.stats + (long long)g * a.stripes * 2 * a.C, a.stripes, a.C, c, valid, red, s1, s2);
-    if (!lead) return;
     const double M = (double)a.count;
-    const double m = s1 / M;
-    double v = s2 / M - m * m;
+    double m, v;
+    if (a.tile_rows > 0) {
+      double m2;
+      slot_fold_chan(a.stats + (long long)g * a.stripes * 2 * a.C, a.stripes, a.C, c, valid, red, a.count,
+                     a.tile_rows, m, m2);
+      if (!lead) return;
+      v = m2 / M;
+    } else {
+      double s1, s2;
+      slot_fold(a.stats + (long long)g * a.stripes * 2 * a.C, a.stripes, a.C, c, valid, red, s1, s2);
+      if (!lead) return;
+      m = s1 / M;
+      v = s2 / M - m * m;
+    }
     if (v < 0) v = 0;
     mean = (float)m;
     var = (float)v;
@@ -128,6 +171,12 @@ DDL_API int ddl_bnf_finalize(const BNFArgs* a, const BNFArgs* b, hipStream_t s) 
 }
 DDL_API int ddl_bnf_args_size() { return (int)sizeof(BNFArgs); }
 
+// Channel tiling of the streaming passes: a 256-thread block covers RPI = 256 / TPR rows of
+// TPR = min(C/4, 256) float4 chunks; wider rows (C = 2048: ResNet-50's last stage) loop over
+// NCH = C / (4 * TPR) channel chunks of 1024 (each chunk's bytes are disjoint: no extra traffic).
+__device__ __host__ __forceinline__ int f_tpr(int C) { return (C >> 2) < 256 ? (C >> 2) : 256; }
+static inline bool f_chan_ok(int C) { return C % 4 == 0 && ((C >> 2) <= 256 || (C >> 2) % 256 == 0); }
+
 // blocks per group of a streaming pass
 static unsigned fstream_blocks(long long M, int RPI, int G, int rows_per_thread) {
   long long want = (M + (long long)RPI * rows_per_thread - 1) / ((long long)RPI * rows_per_thread);
@@ -161,9 +210,11 @@ __global__ __launch_bounds__(256) void bnf_apply_kernel(
     const float* __restrict__ r, const float* __restrict__ rscale, const float* __restrict__ rshift,
     float* __restrict__ y, long long M, int C, int act) {
   const int g = blockIdx.y;
-  const int TPR = C >> 2, RPI = 256 / TPR;
-  const int cc = threadIdx.x % TPR, row = threadIdx.x / TPR;
+  const int TPR = f_tpr(C), RPI = 256 / TPR, NCH = (C >> 2) / TPR;
+  const int row = threadIdx.x / TPR;
   if (row >= RPI) return;
+  for (int ch = 0; ch < NCH; ++ch) {
+  const int cc = threadIdx.x % TPR + ch * TPR;
   const float4 sc = ld4(scale + (long long)g * C + cc * 4), sh = ld4(shift + (long long)g * C + cc * 4);
   float4 rsc = make_float4(1.f, 1.f, 1.f, 1.f), rsh = make_float4(0.f, 0.f, 0.f, 0.f);
   if (rscale) {
@@ -194,14 +245,15 @@ __global__ __launch_bounds__(256) void bnf_apply_kernel(
       *(float4*)(y + base + p * C) = act4(v, act);
     }
   }
+  }
 }
 
 DDL_API int ddl_bnf_apply(const float* x, const float* scale, const float* shift, const float* r,
                           const float* rscale, const float* rshift, float* y, long long per_group, int C, int G,
                           int act, hipStream_t s) {
-  if (C % 4 || C / 4 > 256 || per_group % C) return (int)hipErrorInvalidValue;
+  if (!f_chan_ok(C) || per_group % C) return (int)hipErrorInvalidValue;
   const long long M = per_group / C;
-  const int RPI = 256 / (C / 4);
+  const int RPI = 256 / f_tpr(C);
   hipLaunchKernelGGL(bnf_apply_kernel, dim3(fstream_blocks(M, RPI, G, 4), G), dim3(256), 0, s, x, scale, shift, r,
                      rscale, rshift, y, M, C, act);
   return (int)hipGetLastError();
@@ -217,8 +269,11 @@ __global__ __launch_bounds__(256) void bnf_reduce_kernel(
     const float* __restrict__ mean, const float* __restrict__ rstd, float* __restrict__ part, long long M, int C) {
   __shared__ float red[256 * 8];
   const int g = blockIdx.y;
-  const int TPR = C >> 2, RPI = 256 / TPR;
-  const int tid = threadIdx.x, cc = tid % TPR, row = tid / TPR;
+  const int TPR = f_tpr(C), RPI = 256 / TPR, NCH = (C >> 2) / TPR;
+  const int tid = threadIdx.x, row = tid / TPR;
+  for (int ch = 0; ch < NCH; ++ch) {
+  const int cc = tid % TPR + ch * TPR;
+  if (ch) __syncthreads();  // the previous chunk's LDS fold is done
   float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
   if (row < RPI) {
     float4 m4 = s0, r4 = s0;
@@ -267,7 +322,7 @@ __global__ __launch_bounds__(256) void bnf_reduce_kernel(
   __syncthreads();
   if (row == 0) {
     for (int r = 1; r < RPI; ++r) {
-      const float* o = red + (r * TPR + cc) * 8;
+      const float* o = red + (r * TPR + tid % TPR) * 8;
       s0.x += o[0]; s0.y += o[1]; s0.z += o[2]; s0.w += o[3];
       s1.x += o[4]; s1.y += o[5]; s1.z += o[6]; s1.w += o[7];
     }
@@ -275,12 +330,13 @@ __global__ __launch_bounds__(256) void bnf_reduce_kernel(
     *(float4*)pg = s0;
     *(float4*)(pg + C) = s1;
   }
+  }
 }
 
 // slots (= blocks per group) of a reduce pass over M rows: a pure function of the shape
 DDL_API int ddl_bnf_reduce_slots(long long M, int C, int G) {
-  if (C % 4 || C / 4 > 256) return -1;
-  const int RPI = 256 / (C / 4);
+  if (!f_chan_ok(C)) return -1;
+  const int RPI = 256 / f_tpr(C);
   long long want = (M + (long long)RPI * 16 - 1) / ((long long)RPI * 16);
   long long cap = (2048 + G - 1) / G;
   if (cap > 256) cap = 256;
@@ -352,9 +408,11 @@ __global__ __launch_bounds__(256) void bnf_bwd_apply_kernel(
     const float* __restrict__ dy, const float* __restrict__ ymask, BNFBwdArgs a, BNFBwdArgs b, int two,
     float* __restrict__ dym_out, long long M, int C) {
   const int g = blockIdx.y;
-  const int TPR = C >> 2, RPI = 256 / TPR;
-  const int cc = threadIdx.x % TPR, row = threadIdx.x / TPR;
+  const int TPR = f_tpr(C), RPI = 256 / TPR, NCH = (C >> 2) / TPR;
+  const int row = threadIdx.x / TPR;
   if (row >= RPI) return;
+  for (int ch = 0; ch < NCH; ++ch) {
+  const int cc = threadIdx.x % TPR + ch * TPR;
   const float* ca = a.coef + (long long)g * 3 * C + cc * 4;
   const float4 Aa = ld4(ca), Ba = ld4(ca + C), Ca = ld4(ca + 2 * C);
   float4 Ab = Aa, Bb = Ba, Cb = Ca;
@@ -399,6 +457,7 @@ __global__ __launch_bounds__(256) void bnf_bwd_apply_kernel(
       }
     }
   }
+  }
 }
 
 DDL_API int ddl_bnf_bwd_args_size() { return (int)sizeof(BNFBwdArgs); }
@@ -408,7 +467,7 @@ DDL_API int ddl_bnf_bwd_args_size() { return (int)sizeof(BNFBwdArgs); }
 // holds `slots` complete partial sums from dy's producer.
 DDL_API int ddl_bnf_backward(const float* dy, const float* ymask, const BNFBwdArgs* ap, const BNFBwdArgs* bp,
                              float* dym_out, long long M, int C, int G, int do_reduce, hipStream_t s) {
-  if (C % 4 || C / 4 > 256) return (int)hipErrorInvalidValue;
+  if (!f_chan_ok(C)) return (int)hipErrorInvalidValue;
   BNFBwdArgs a = *ap;
   if (do_reduce) {
     a.slots = ddl_bnf_reduce_slots(M, C, G);
@@ -419,7 +478,7 @@ DDL_API int ddl_bnf_backward(const float* dy, const float* ymask, const BNFBwdAr
   const int two = bp ? 1 : 0;
   const BNFBwdArgs b = bp ? *bp : a;
   hipLaunchKernelGGL(bnf_fold_kernel, dim3((C + 31) / 32, G, 1 + two), dim3(FOLD_T), 0, s, a, b, M, C);
-  const int RPI = 256 / (C / 4);
+  const int RPI = 256 / f_tpr(C);
   hipLaunchKernelGGL(bnf_bwd_apply_kernel, dim3(fstream_blocks(M, RPI, G, 4), G), dim3(256), 0, s, dy, ymask, a, b,
                      two, dym_out, M, C);
   return (int)hipGetLastError();
@@ -434,11 +493,14 @@ __global__ __launch_bounds__(256) void avgpoolf_bwd_bn_kernel(
     float* __restrict__ part, int N, int HW, int C) {
   __shared__ float red[256 * 8];
   const int g = blockIdx.y;
-  const int TPR = C >> 2, RPI = 256 / TPR;
-  const int tid = threadIdx.x, cc = tid % TPR, row = tid / TPR;
+  const int TPR = f_tpr(C), RPI = 256 / TPR, NCH = (C >> 2) / TPR;
+  const int tid = threadIdx.x, row = tid / TPR;
   const long long M = (long long)N * HW;
-  float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
   const float inv = 1.f / HW;
+  for (int ch = 0; ch < NCH; ++ch) {
+  const int cc = tid % TPR + ch * TPR;
+  if (ch) __syncthreads();  // the previous chunk's LDS fold is done
+  float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
   if (row < RPI) {
     const float4 m4 = ld4(mean + (long long)g * C + cc * 4), r4 = ld4(rstd + (long long)g * C + cc * 4);
     const long long stride = (long long)gridDim.x * RPI;
@@ -476,13 +538,14 @@ __global__ __launch_bounds__(256) void avgpoolf_bwd_bn_kernel(
   __syncthreads();
   if (row == 0) {
     for (int r = 1; r < RPI; ++r) {
-      const float* o = red + (r * TPR + cc) * 8;
+      const float* o = red + (r * TPR + tid % TPR) * 8;
       s0.x += o[0]; s0.y += o[1]; s0.z += o[2]; s0.w += o[3];
       s1.x += o[4]; s1.y += o[5]; s1.z += o[6]; s1.w += o[7];
     }
     float* pg = part + ((long long)g * gridDim.x + blockIdx.x) * 2 * C + cc * 4;
     *(float4*)pg = s0;
     *(float4*)(pg + C) = s1;
+  }
   }
 }
 

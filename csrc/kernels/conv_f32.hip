@@ -219,7 +219,10 @@ __device__ __forceinline__ void fepilogue(const ConvF32Args& a, const FGeo& o,
         }
         if (want_stats) {
 #pragma unroll
-          for (int v = 0; v < 4; ++v) { s0[ti][v] += v4[v]; s1[ti][v] += v4[v] * v4[v]; }
+          for (int v = 0; v < 4; ++v) {
+            s0[ti][v] += v4[v];
+            acc[ti][tj][v] = v4[v];  // kept for the centred second pass below
+          }
         }
       } else {  // DGRAD
         if (a.residual) {
@@ -263,6 +266,62 @@ __device__ __forceinline__ void fepilogue(const ConvF32Args& a, const FGeo& o,
     }
   }
   if (!want_stats || (MODE == F_DGRAD && !a.bn_x)) return;
+  if constexpr (MODE == F_FWD) {
+    // Forward BN statistics of this tile as (sum, M2 = sum of squared deviations from the TILE
+    // mean): two passes over the register-resident outputs, merged across tiles in bnf_finalize
+    // with Chan's formula. A single-pass (sum, sum of squares) loses the variance to cancellation
+    // when |mean| >> std (deep layers of ResNet-50: 1e-5 relative error in rstd).
+    const int nq = min(BQ, o.Qd - o.q0);  // valid rows of this tile
+#pragma unroll
+    for (int ti = 0; ti < TP; ++ti)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float x0 = s0[ti][v];
+#pragma unroll
+        for (int o2 = 1; o2 < 16; o2 <<= 1) x0 += __shfl_xor(x0, o2, 64);
+        if ((lane & 15) == 0) red[(wq * BP + wp * WP + ti * 16 + 4 * (lane >> 4) + v) * 2] = x0;
+      }
+    __syncthreads();
+    float mu[TP][4];
+#pragma unroll
+    for (int ti = 0; ti < TP; ++ti)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int pl = wp * WP + ti * 16 + 4 * (lane >> 4) + v;
+        mu[ti][v] = (red[pl * 2] + red[(BP + pl) * 2]) / (float)nq;
+        s1[ti][v] = 0.f;
+      }
+#pragma unroll
+    for (int tj = 0; tj < TQ; ++tj) {
+      const bool qv = o.q0 + wq * WQ + tj * 16 + (lane & 15) < o.Qd;
+#pragma unroll
+      for (int ti = 0; ti < TP; ++ti) {
+        if (!qv || o.p0 + wp * WP + ti * 16 + 4 * (lane >> 4) >= Pd) continue;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const float d = acc[ti][tj][v] - mu[ti][v];
+          s1[ti][v] += d * d;
+        }
+      }
+    }
+#pragma unroll
+    for (int ti = 0; ti < TP; ++ti)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float x1 = s1[ti][v];
+#pragma unroll
+        for (int o2 = 1; o2 < 16; o2 <<= 1) x1 += __shfl_xor(x1, o2, 64);
+        if ((lane & 15) == 0) red[(wq * BP + wp * WP + ti * 16 + 4 * (lane >> 4) + v) * 2 + 1] = x1;
+      }
+    __syncthreads();
+    if (tid < BP && o.p0 + tid < Pd) {
+      const int slot = o.phase * (a.slots / o.nph) + o.tq;
+      float* st = a.stats + ((long long)g * a.slots + slot) * 2 * Pd + o.p0 + tid;
+      st[0] = red[tid * 2] + red[(BP + tid) * 2];
+      st[Pd] = red[tid * 2 + 1] + red[(BP + tid) * 2 + 1];
+    }
+    return;
+  }
   // per-channel partial sums of this tile -> its own slot (fixed-order, no atomics)
 #pragma unroll
   for (int ti = 0; ti < TP; ++ti)

@@ -53,6 +53,10 @@ class BNArgs(ctypes.Structure):
                 ("eps", f32), ("momentum", f32), ("training", i32), ("stripes", i32)]
 
 
+class BNFArgs(ctypes.Structure):  # bn_f32.hip: BNArgs + the per-tile centred-statistics row count
+    _fields_ = BNArgs._fields_ + [("tile_rows", i32), ("pad_", i32)]
+
+
 class BNBwdArgs(ctypes.Structure):
     _fields_ = [("x", vp), ("mean", vp), ("rstd", vp), ("gamma", vp), ("dgamma", vp), ("dbeta", vp),
                 ("part", vp), ("coef", vp), ("dx", vp), ("gs_param", i64)]
@@ -227,7 +231,7 @@ def kernels():
                                    ("SGDDirectArgs", "ddl_sgd_direct_args_size", SGDDirectArgs),
                                    ("AdamArgs", "ddl_adam_args_size", AdamArgs),
                                    ("ConvF32Args", "ddl_convf32_args_size", ConvF32Args),
-                                   ("BNArgs", "ddl_bnf_args_size", BNArgs),
+                                   ("BNFArgs", "ddl_bnf_args_size", BNFArgs),
                                    ("BNFBwdArgs", "ddl_bnf_bwd_args_size", BNFBwdArgs),
                                    ("HeadFArgs", "ddl_headf_args_size", HeadFArgs)):
             f = getattr(lib, size_fn)

@@ -35,11 +35,15 @@ def is_f32(t) -> bool:
 
 
 class SlotStats:
-    """Forward BN statistics of an fp32 conv: ``t`` = [G, slots, 2, C] once the conv has run."""
-    __slots__ = ("t",)
+    """Forward BN statistics of an fp32 conv: ``t`` = [G, slots, 2, C] once the conv has run.
+    ``rows`` > 0: slot i holds (sum, M2 about the slot's own mean) of min(rows, M - i*rows)
+    output rows (the conv epilogue's per-tile centred statistics, merged exactly in bn_finalize);
+    0: (sum, sum of squares) partials (bn_stats)."""
+    __slots__ = ("t", "rows")
 
     def __init__(self):
         self.t = None
+        self.rows = 0
 
 
 def workspace(device, role: str = "main") -> torch.Tensor | None:
@@ -223,6 +227,7 @@ def conv_fwd(x, w, geom, bias=None, relu=False, stats=None, out=None, residual=N
         a.stats = ptr(st)
         if isinstance(stats, SlotStats):
             stats.t = st
+            stats.rows = ((_cfg(plan(F_FWD, geom)[0]) >> 8) & 0xFF) * 16  # the tile's BQ
         else:
             raise TypeError("fp32 conv statistics go to a SlotStats (Fn.stats_buffer(..., like=x))")
     _launch(a, F_FWD, geom, x.device, split_k)
@@ -272,8 +277,10 @@ def conv_wgrad(dy, x, geom, dw, accumulate=True, gscale=1.0, in_bn=None, split_k
 
 
 # --------------------------------------------------------------------------------------- BN
-def _bnf_args(stats, gamma, beta, running_mean, running_var, count, eps, momentum, training, outs, G, C):
-    a = _lib.BNArgs()
+def _bnf_args(stats, gamma, beta, running_mean, running_var, count, eps, momentum, training, outs, G, C,
+              tile_rows=0):
+    a = _lib.BNFArgs()
+    a.tile_rows = int(tile_rows)
     a.stats, a.gamma, a.beta = ptr(stats), ptr(gamma), ptr(beta)
     a.running_mean, a.running_var = ptr(running_mean), ptr(running_var)
     a.scale, a.shift, a.mean, a.rstd = (ptr(outs[i]) for i in range(4))
@@ -292,10 +299,12 @@ def bn_finalize_many(items, eps=1e-5, momentum=0.1, training=True):
     args, outs = [], []
     for stats, gamma, beta, rm, rv, count, G, C in items:
         t = stats.t if isinstance(stats, SlotStats) else stats
+        rows = stats.rows if isinstance(stats, SlotStats) else 0
         if training:
             assert t is not None and t.is_contiguous(), "fp32 BN statistics missing (conv not run?)"
         o = torch.empty(4, G, C, dtype=torch.float32, device=dev)
-        args.append(_bnf_args(t if training else None, gamma, beta, rm, rv, count, eps, momentum, training, o, G, C))
+        args.append(_bnf_args(t if training else None, gamma, beta, rm, rv, count, eps, momentum, training, o, G, C,
+                              rows))
         outs.append(o)
     b = ctypes.byref(args[1]) if len(args) > 1 else None
     check(_lib.kernels().ddl_bnf_finalize(ctypes.byref(args[0]), b, stream()), "bn_finalize_f32")
