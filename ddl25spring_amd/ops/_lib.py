@@ -175,7 +175,7 @@ _SIGS.update({
     "ddl_convf32_slots": [ctypes.POINTER(ConvF32Args), i32, i32],
     "ddl_convf32_workspace": [ctypes.POINTER(ConvF32Args), i32, i32],
     # bn_f32.hip
-    "ddl_bnf_finalize": [ctypes.POINTER(BNArgs), ctypes.POINTER(BNArgs), vp],
+    "ddl_bnf_finalize": [ctypes.POINTER(BNFArgs), ctypes.POINTER(BNFArgs), vp],
     "ddl_bnf_apply": [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, vp],
     "ddl_bnf_reduce_slots": [i64, i32, i32],
     "ddl_bnf_reduce": [vp, vp, vp, vp, vp, vp, i64, i32, i32, vp],
