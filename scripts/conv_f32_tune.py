@@ -46,6 +46,24 @@ def workspace_need(mode, g, bp, bq, split) -> int:
     return int(F32._lib.kernels().ddl_convf32_workspace(ctypes.byref(a), mode, F32._cfg(F32.cfg_of(bp, bq))))
 
 
+def resnet50_geoms(G: int, N: int):
+    """ResNet-50 (ImageNet 224, torchvision v1.5 strides) conv geometries: im2col'd 7x7 stem (1x1 on
+    160 channels) and the bottleneck 1x1 / 3x3 / strided convs."""
+    gs = [ConvGeom(G, N, 112, 112, 160, 64, 1, 1, 1, 0)]
+    cin, hw = 64, 56
+    for planes, n in zip((64, 128, 256, 512), (3, 4, 6, 3)):
+        for b in range(n):
+            stride = 2 if (b == 0 and planes != 64) else 1
+            ho = hw // stride
+            gs.append(ConvGeom(G, N, hw, hw, cin, planes, 1, 1, 1, 0))
+            gs.append(ConvGeom(G, N, hw, hw, planes, planes, 3, 3, stride, 1))
+            gs.append(ConvGeom(G, N, ho, ho, planes, planes * 4, 1, 1, 1, 0))
+            if b == 0:
+                gs.append(ConvGeom(G, N, hw, hw, cin, planes * 4, 1, 1, stride, 0))
+            cin, hw = planes * 4, ho
+    return list(dict.fromkeys(gs))
+
+
 def timed(fn, reps):
     for _ in range(2):
         fn()
@@ -66,6 +84,7 @@ def main():
     ap.add_argument("--batch", type=int, default=100)
     ap.add_argument("--budget-s", type=float, default=240.0)
     ap.add_argument("--math", default="mfma32", choices=list(F32.MATHS))
+    ap.add_argument("--model", default="resnet18", choices=("resnet18", "resnet50"))
     a = ap.parse_args()
     F32.set_math(a.math)
     prefix = "" if a.math == "mfma32" else f"{a.math}:"
@@ -74,15 +93,15 @@ def main():
     t_start = time.time()
     plans, report = {}, []
     for G in a.groups:
-        for g in resnet18_geoms(G, a.batch):
+        for g in (resnet50_geoms if a.model == "resnet50" else resnet18_geoms)(G, a.batch):
             x = torch.randn(g.G, g.N, g.H, g.W, g.C, device=dev)
             w = torch.randn(g.G, g.K, g.R, g.S, g.C, device=dev) * 0.05
             dy = torch.randn(g.G, g.N, g.P, g.Q, g.K, device=dev)
             dw = torch.zeros_like(w)
             flops = 2 * g.G * g.N * g.P * g.Q * g.K * g.R * g.S * g.C
             for mode, name in ((F32.F_FWD, "fwd"), (F32.F_DGRAD, "dgrad"), (F32.F_WGRAD, "wgrad")):
-                if mode == F32.F_DGRAD and g.C == 32:
-                    continue  # the stem needs no input gradient
+                if mode == F32.F_DGRAD and g.C in (32, 160) and g.R == 1:
+                    continue  # the (im2col'd) stem needs no input gradient
                 F32._OVERRIDE.pop((mode, g), None)
                 F32._PLANS.pop((mode, g), None)
                 heur = F32.plan(mode, g)
@@ -93,7 +112,11 @@ def main():
                 for eng in engines:
                     for bp in (64, 128):
                         for bq in (64, 128):
+                            Pd, Qd, _, nph = F32._dims(mode, g)
+                            tiles = -(-Pd // bp) * -(-Qd // bq) * nph * g.G
                             for split in ((1, 2, 4, 8, 16, 32, 64, 128) if G <= 2 else (1, 2, 4, 8, 16, 32)):
+                                if split > 1 and tiles * split > 8192:
+                                    break  # the grid is already wide: deeper split-K only adds epilogue work
                                 F32.set_plan(mode, g, bp, bq, split, eng)
                                 if split > 1 and workspace_need(mode, g, bp, bq, split) > F32.WS_CAP:
                                     continue  # would silently run unsplit
