@@ -1,6 +1,6 @@
 """Reference-equivalent baseline for BASELINE config 3: stock PyTorch-ROCm ResNet-50 (torchvision v1.5
 layout, ``models/torch_ref.py``) training in fp32 on one GPU — SGD momentum 0.9, wd 1e-4, synthetic
-ImageNet-shaped batch, channels_last, cudnn.benchmark (MIOpen's own kernel search). The number the
+ImageNet-shaped batch, channels_last (MIOpen's default find; --benchmark for its exhaustive search). The number the
 native fp32 path (``bench_resnet50_dp.py``) is compared against.
 
     python benchmarks/bench_resnet50_torch.py --batch 256 --steps 8 --warmup 3
@@ -25,8 +25,17 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--benchmark", action="store_true", help="cudnn.benchmark (MIOpen exhaustive find: minutes)")
     a = ap.parse_args()
-    torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.benchmark = a.benchmark
+    import threading
+
+    def heartbeat():  # MIOpen's first-use kernel search / compilation runs for minutes without output
+        t0 = time.time()
+        while True:
+            time.sleep(30)
+            print(f"[heartbeat] {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=heartbeat, daemon=True).start()
     dev = torch.device("cuda")
     torch.manual_seed(0)
     m = torch_resnet50_imagenet(1000).to(dev).to(memory_format=torch.channels_last)
@@ -38,8 +47,10 @@ def main():
         opt.zero_grad(set_to_none=True)
         F.cross_entropy(m(x), y).backward()
         opt.step()
-    for _ in range(a.warmup):
+    for i in range(a.warmup):
         step()
+        torch.cuda.synchronize()
+        print(f"warmup step {i} done", file=sys.stderr, flush=True)  # MIOpen compiles kernels on first use
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
