@@ -332,8 +332,10 @@ def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0, _tun
         # direct-SGD WGRAD steps), concurrent with the rest of the backward; joined on exit of
         # wgrad_overlap. Its split-K workspace is the side stream's own (functional_f32.workspace).
         side.wait_stream(torch.cuda.current_stream())
-        for t in (dy, x) + (tuple(in_bn) if in_bn is not None else ()):
-            t.record_stream(side)
+        # keep the inputs alive until wgrad_overlap joins the side stream back (not record_stream:
+        # inside a graph capture the allocator can never retire a record_stream'd block, so every
+        # captured step would grow the graph's private pool — 226 GiB reserved for one 8-client round)
+        _SIDE_KEEP.extend((dy, x) + (tuple(in_bn) if in_bn is not None else ()))
         with torch.cuda.stream(side):
             return F32.conv_wgrad(dy, x, geom, dw, accumulate, wgrad_scale(dw), in_bn=in_bn, split_k=splits,
                                   ws_role="side")
@@ -368,6 +370,7 @@ def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0, _tun
 # ------------------------------------------------------------------- wgrad / dgrad overlap
 _WGRAD_SIDE: "torch.cuda.Stream | None" = None
 _SIDE_STREAMS: dict = {}
+_SIDE_KEEP: list = []  # fp32 side-stream WGRAD inputs, released when wgrad_overlap joins
 
 
 # Paired DGRAD + WGRAD of one conv in one launch (conv_igemm.hip ``ddl_conv_pair``). The pair
@@ -575,6 +578,7 @@ class wgrad_overlap:
         global _WGRAD_SIDE
         if _WGRAD_SIDE is not None and _WGRAD_SIDE is not self.prev:
             torch.cuda.current_stream().wait_stream(_WGRAD_SIDE)
+            _SIDE_KEEP.clear()  # joined: their memory may be reused in stream order
         _WGRAD_SIDE = self.prev
         return False
 
