@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 for C in 8 1; do
-  timeout -k 10 300 python -u scratch/mem_probe.py $C > gpurun_out/om_mem_$C.log 2>&1 || { tail -5 gpurun_out/om_mem_$C.log; exit 1; }
+  timeout -k 10 300 python -u scripts/mem_probe.py $C > gpurun_out/om_mem_$C.log 2>&1 || { tail -5 gpurun_out/om_mem_$C.log; exit 1; }
   tail -1 gpurun_out/om_mem_$C.log
 done
 timeout -k 10 600 python -u -m pytest tests/test_fp32_gpu.py tests/test_overlap_gpu.py -q -x --timeout 500 --timeout-method thread > gpurun_out/om_tests.log 2>&1 || { tail -30 gpurun_out/om_tests.log; exit 1; }
