@@ -37,331 +37,17 @@
 //         the master weights is plain SGD fused into the backward).
 //   * stride-2 DGRAD runs as four sub-pixel phases (no MFMA on taps that miss every output);
 //     larger strides (none in the model zoo) run unphased with a per-tap divisibility test.
-#include "ddl_common.h"
+#include "conv_f32_core.h"
 
 // operand prefetch depth in steps (register sets): 2 or 3
 #ifndef F32_PREFETCH
 #define F32_PREFETCH 2
 #endif
 
-struct ConvF32Args {
-  const float* x;         // [G][N][H][W][C]                    (group stride x_gs)
-  const float* w;         // [G][K][R][S][C]                    (w_gs)
-  const float* dy;        // [G][N][P][Q][K]                    (dy_gs)
-  float* out;             // FWD y [G][N][P][Q][K] | DGRAD dx [G][N][H][W][C] | WGRAD dw like w (out_gs)
-  float* stats;           // FWD: [G][slots][2][K] (sum, sumsq) | DGRAD with bn_x: [G][slots][2][C]
-  const float* bias;      // FWD [G][K] (bias_gs)
-  const float* residual;  // FWD / DGRAD: added (layout of out; DGRAD res_sub 2: compact grid, res_gs)
-  const float* mask;      // DGRAD: dx *= (mask > 0) (layout of out)
-  const float* in_scale;  // X operand transform (FWD / WGRAD): [G][C] contiguous
-  const float* in_shift;
-  const float* bn_x;      // DGRAD BN-backward reduce: the preceding BN's input (layout of out)
-  const float* bn_mean;   // [G][C]
-  const float* bn_rstd;
-  const float* mask_scale;  // DGRAD: keep dx where bn_x * mask_scale + mask_shift > 0
-  const float* mask_shift;
-  float* partial;         // split-K workspace
-  long long partial_cap;  // floats at `partial`
-  long long x_gs, w_gs, dy_gs, out_gs, bias_gs, res_gs;
-  int G, N, H, W, C, K, R, S, P, Q, stride, pad;
-  int relu, accumulate, split_k, res_sub, in_relu;
-  int slots;              // stats / BN-reduce slots per group (filled by the launcher)
-  float gscale;           // WGRAD: out = (accumulate ? out : 0) + gscale * dW
-};
-
-enum { F_FWD = 0, F_DGRAD = 1, F_WGRAD = 2 };
 constexpr int FBK = 16;
 
 __device__ __forceinline__ int fswz(int row) { return (row >> 2) & 2; }
 __device__ __forceinline__ int lds_off(int row, int ch) { return row * 16 + ((ch ^ fswz(row)) << 2); }
-
-struct FDiv {
-  uint32_t m;
-  int s;
-};
-__host__ __device__ inline FDiv mk_fdiv(uint32_t d) {
-  FDiv f;
-  if (d <= 1) { f.m = 0; f.s = 0; return f; }
-  int l = 0;
-  while ((1u << l) < d) ++l;
-  f.m = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
-  f.s = l;
-  return f;
-}
-__device__ __forceinline__ int fdv(int x, FDiv f) {
-  if (f.s == 0) return x;
-  const uint32_t t = __umulhi((uint32_t)x, f.m);
-  return (int)((t + (((uint32_t)x - t) >> 1)) >> (f.s - 1));
-}
-
-// Per-block problem geometry (shared by the main kernel and the split-K epilogue kernel).
-struct FGeo {
-  int Pd, Qd, Kr, nph, phase, split, nsplit, g, p0, q0, tq;
-  int pa, pb, Hs, Ws, r0, s0, Rn, Sn;
-};
-
-template <int MODE, int BP, int BQ>
-__device__ __forceinline__ FGeo fgeo(const ConvF32Args& a, int bx, int by, int g, int gy) {
-  FGeo o;
-  o.nph = (MODE == F_DGRAD && a.stride == 2) ? 4 : 1;
-  o.phase = by % o.nph;
-  o.split = by / o.nph;
-  o.nsplit = gy / o.nph;
-  o.g = g;
-  o.pa = o.pb = o.r0 = o.s0 = 0;
-  o.Hs = a.H; o.Ws = a.W; o.Rn = a.R; o.Sn = a.S;
-  if (MODE == F_FWD) {
-    o.Pd = a.K; o.Qd = a.N * a.P * a.Q; o.Kr = a.R * a.S * a.C;
-  } else if (MODE == F_DGRAD) {
-    o.Pd = a.C;
-    if (o.nph == 4) {
-      o.pa = o.phase >> 1; o.pb = o.phase & 1;
-      o.Hs = (a.H - o.pa + 1) >> 1; o.Ws = (a.W - o.pb + 1) >> 1;
-      o.r0 = (o.pa + a.pad) & 1; o.s0 = (o.pb + a.pad) & 1;
-      o.Rn = (a.R - o.r0 + 1) >> 1; o.Sn = (a.S - o.s0 + 1) >> 1;
-    }
-    o.Qd = a.N * o.Hs * o.Ws;
-    o.Kr = o.Rn * o.Sn * a.K;
-  } else {
-    o.Pd = a.K; o.Qd = a.R * a.S * a.C; o.Kr = a.N * a.P * a.Q;
-  }
-  const int ntp = (o.Pd + BP - 1) / BP;
-  o.p0 = (bx % ntp) * BP;
-  o.tq = bx / ntp;
-  o.q0 = o.tq * BQ;
-  return o;
-}
-
-// ------------------------------------------------------------------------------------ epilogue
-// acc[ti][tj][v] of this lane holds D[p][q], p = p0 + wp*WP + ti*16 + 4*(lane>>4) + v,
-// q = q0 + wq*WQ + tj*16 + (lane & 15).
-template <int MODE, int BP, int BQ>
-__device__ __forceinline__ void fepilogue(const ConvF32Args& a, const FGeo& o,
-                                          f4v (&acc)[BP / 32][BQ / 32], float* red) {
-  constexpr int WP = BP / 2, WQ = BQ / 2, TP = WP / 16, TQ = WQ / 16;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wp = wid >> 1, wq = wid & 1;
-  const int g = o.g;
-  if constexpr (MODE == F_WGRAD) {
-    const int RSC = o.Qd;
-    float* outg = a.out + (long long)g * a.out_gs;
-#pragma unroll
-    for (int ti = 0; ti < TP; ++ti)
-#pragma unroll
-      for (int tj = 0; tj < TQ; ++tj) {
-        const int q = o.q0 + wq * WQ + tj * 16 + (lane & 15);
-        if (q >= RSC) continue;
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int p = o.p0 + wp * WP + ti * 16 + 4 * (lane >> 4) + v;
-          if (p >= o.Pd) continue;
-          float* d = outg + (long long)p * RSC + q;
-          const float base = a.accumulate ? *d : 0.f;
-          *d = base + a.gscale * acc[ti][tj][v];
-        }
-      }
-    return;
-  }
-  const bool want_stats = a.stats != nullptr;
-  const int Pd = o.Pd;
-  float* outg = a.out + (long long)g * a.out_gs;
-  float s0[TP][4], s1[TP][4];
-#pragma unroll
-  for (int ti = 0; ti < TP; ++ti)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) s0[ti][v] = s1[ti][v] = 0.f;
-
-  // per-p constants of this lane (4 consecutive channels per ti)
-  float bia[TP][4], bm[TP][4], br[TP][4], ms[TP][4], mh[TP][4];
-#pragma unroll
-  for (int ti = 0; ti < TP; ++ti) {
-    const int pb4 = o.p0 + wp * WP + ti * 16 + 4 * (lane >> 4);
-    const bool pv = pb4 < Pd;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      bia[ti][v] = (MODE == F_FWD && a.bias && pv) ? a.bias[(long long)g * a.bias_gs + pb4 + v] : 0.f;
-      bm[ti][v] = (MODE == F_DGRAD && a.bn_x && pv) ? a.bn_mean[(long long)g * Pd + pb4 + v] : 0.f;
-      br[ti][v] = (MODE == F_DGRAD && a.bn_x && pv) ? a.bn_rstd[(long long)g * Pd + pb4 + v] : 0.f;
-      ms[ti][v] = (MODE == F_DGRAD && a.mask_scale && pv) ? a.mask_scale[(long long)g * Pd + pb4 + v] : 0.f;
-      mh[ti][v] = (MODE == F_DGRAD && a.mask_scale && pv) ? a.mask_shift[(long long)g * Pd + pb4 + v] : 0.f;
-    }
-  }
-  const FDiv dpq = mk_fdiv((uint32_t)(o.Hs * o.Ws)), dq = mk_fdiv((uint32_t)o.Ws);
-#pragma unroll
-  for (int tj = 0; tj < TQ; ++tj) {
-    const int q = o.q0 + wq * WQ + tj * 16 + (lane & 15);
-    const bool qv = q < o.Qd;
-    long long pix = q;  // output / input pixel index of q (row of out)
-    int hh = 0, ww = 0, nn = 0;
-    if (MODE == F_DGRAD) {
-      nn = fdv(q, dpq);
-      const int rem = q - nn * o.Hs * o.Ws;
-      const int i = fdv(rem, dq), j = rem - i * o.Ws;
-      hh = o.nph == 4 ? 2 * i + o.pa : i;
-      ww = o.nph == 4 ? 2 * j + o.pb : j;
-      pix = ((long long)nn * a.H + hh) * a.W + ww;
-    }
-#pragma unroll
-    for (int ti = 0; ti < TP; ++ti) {
-      const int p = o.p0 + wp * WP + ti * 16 + 4 * (lane >> 4);
-      if (!qv || p >= Pd) continue;
-      const long long e = pix * Pd + p;
-      float v4[4] = {acc[ti][tj][0], acc[ti][tj][1], acc[ti][tj][2], acc[ti][tj][3]};
-      if (MODE == F_FWD) {
-#pragma unroll
-        for (int v = 0; v < 4; ++v) v4[v] += bia[ti][v];
-        if (a.residual) {
-          const float4 r = *(const float4*)(a.residual + (long long)g * a.out_gs + e);
-          v4[0] += r.x; v4[1] += r.y; v4[2] += r.z; v4[3] += r.w;
-        }
-        if (a.relu) {
-#pragma unroll
-          for (int v = 0; v < 4; ++v) v4[v] = fmaxf(v4[v], 0.f);
-        }
-        if (want_stats) {
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            s0[ti][v] += v4[v];
-            acc[ti][tj][v] = v4[v];  // kept for the centred second pass below
-          }
-        }
-      } else {  // DGRAD
-        if (a.residual) {
-          if (a.res_sub == 2) {
-            if (((hh | ww) & 1) == 0) {
-              const int Hc = (a.H + 1) >> 1, Wc = (a.W + 1) >> 1;
-              const long long re = (((long long)nn * Hc + (hh >> 1)) * Wc + (ww >> 1)) * Pd + p;
-              const float4 r = *(const float4*)(a.residual + (long long)g * a.res_gs + re);
-              v4[0] += r.x; v4[1] += r.y; v4[2] += r.z; v4[3] += r.w;
-            }
-          } else {
-            const float4 r = *(const float4*)(a.residual + (long long)g * a.out_gs + e);
-            v4[0] += r.x; v4[1] += r.y; v4[2] += r.z; v4[3] += r.w;
-          }
-        }
-        if (a.mask) {
-          const float4 m = *(const float4*)(a.mask + (long long)g * a.out_gs + e);
-          if (!(m.x > 0.f)) v4[0] = 0.f;
-          if (!(m.y > 0.f)) v4[1] = 0.f;
-          if (!(m.z > 0.f)) v4[2] = 0.f;
-          if (!(m.w > 0.f)) v4[3] = 0.f;
-        }
-        if (a.bn_x) {
-          const float4 xb = *(const float4*)(a.bn_x + (long long)g * a.out_gs + e);
-          const float xs[4] = {xb.x, xb.y, xb.z, xb.w};
-          if (a.mask_scale) {
-#pragma unroll
-            for (int v = 0; v < 4; ++v)
-              if (!(xs[v] * ms[ti][v] + mh[ti][v] > 0.f)) v4[v] = 0.f;
-          }
-          if (want_stats) {
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-              s0[ti][v] += v4[v];
-              s1[ti][v] += v4[v] * ((xs[v] - bm[ti][v]) * br[ti][v]);
-            }
-          }
-        }
-      }
-      *(float4*)(outg + e) = make_float4(v4[0], v4[1], v4[2], v4[3]);
-    }
-  }
-  if (!want_stats || (MODE == F_DGRAD && !a.bn_x)) return;
-  if constexpr (MODE == F_FWD) {
-    // Forward BN statistics of this tile as (sum, M2 = sum of squared deviations from the TILE
-    // mean): two passes over the register-resident outputs, merged across tiles in bnf_finalize
-    // with Chan's formula. A single-pass (sum, sum of squares) loses the variance to cancellation
-    // when |mean| >> std (deep layers of ResNet-50: 1e-5 relative error in rstd).
-    const int nq = min(BQ, o.Qd - o.q0);  // valid rows of this tile
-#pragma unroll
-    for (int ti = 0; ti < TP; ++ti)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        float x0 = s0[ti][v];
-#pragma unroll
-        for (int o2 = 1; o2 < 16; o2 <<= 1) x0 += __shfl_xor(x0, o2, 64);
-        if ((lane & 15) == 0) red[(wq * BP + wp * WP + ti * 16 + 4 * (lane >> 4) + v) * 2] = x0;
-      }
-    __syncthreads();
-    float mu[TP][4];
-#pragma unroll
-    for (int ti = 0; ti < TP; ++ti)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int pl = wp * WP + ti * 16 + 4 * (lane >> 4) + v;
-        mu[ti][v] = (red[pl * 2] + red[(BP + pl) * 2]) / (float)nq;
-        s1[ti][v] = 0.f;
-      }
-#pragma unroll
-    for (int tj = 0; tj < TQ; ++tj) {
-      const bool qv = o.q0 + wq * WQ + tj * 16 + (lane & 15) < o.Qd;
-#pragma unroll
-      for (int ti = 0; ti < TP; ++ti) {
-        if (!qv || o.p0 + wp * WP + ti * 16 + 4 * (lane >> 4) >= Pd) continue;
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const float d = acc[ti][tj][v] - mu[ti][v];
-          s1[ti][v] += d * d;
-        }
-      }
-    }
-#pragma unroll
-    for (int ti = 0; ti < TP; ++ti)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        float x1 = s1[ti][v];
-#pragma unroll
-        for (int o2 = 1; o2 < 16; o2 <<= 1) x1 += __shfl_xor(x1, o2, 64);
-        if ((lane & 15) == 0) red[(wq * BP + wp * WP + ti * 16 + 4 * (lane >> 4) + v) * 2 + 1] = x1;
-      }
-    __syncthreads();
-    if (tid < BP && o.p0 + tid < Pd) {
-      const int slot = o.phase * (a.slots / o.nph) + o.tq;
-      float* st = a.stats + ((long long)g * a.slots + slot) * 2 * Pd + o.p0 + tid;
-      st[0] = red[tid * 2] + red[(BP + tid) * 2];
-      st[Pd] = red[tid * 2 + 1] + red[(BP + tid) * 2 + 1];
-    }
-    return;
-  }
-  // per-channel partial sums of this tile -> its own slot (fixed-order, no atomics)
-#pragma unroll
-  for (int ti = 0; ti < TP; ++ti)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      float x0 = s0[ti][v], x1 = s1[ti][v];
-#pragma unroll
-      for (int o2 = 1; o2 < 16; o2 <<= 1) {
-        x0 += __shfl_xor(x0, o2, 64);
-        x1 += __shfl_xor(x1, o2, 64);
-      }
-      if ((lane & 15) == 0) {
-        const int pl = wp * WP + ti * 16 + 4 * (lane >> 4) + v;
-        red[(wq * BP + pl) * 2] = x0;
-        red[(wq * BP + pl) * 2 + 1] = x1;
-      }
-    }
-  __syncthreads();
-  if (tid < BP && o.p0 + tid < Pd) {
-    const float t0 = red[tid * 2] + red[(BP + tid) * 2];
-    const float t1 = red[tid * 2 + 1] + red[(BP + tid) * 2 + 1];
-    const int slot = o.phase * (a.slots / o.nph) + o.tq;
-    float* st = a.stats + ((long long)g * a.slots + slot) * 2 * Pd + o.p0 + tid;
-    st[0] = t0;
-    st[Pd] = t1;
-  }
-}
-
-// zero stats slot of a tile that has no work (q0 beyond a smaller DGRAD phase)
-template <int MODE, int BP>
-__device__ __forceinline__ void fzero_slot(const ConvF32Args& a, const FGeo& o) {
-  if (MODE == F_WGRAD || !a.stats || (MODE == F_DGRAD && !a.bn_x)) return;
-  const int tid = threadIdx.x;
-  if (tid < BP && o.p0 + tid < o.Pd) {
-    const int slot = o.phase * (a.slots / o.nph) + o.tq;
-    float* st = a.stats + ((long long)o.g * a.slots + slot) * 2 * o.Pd + o.p0 + tid;
-    st[0] = 0.f;
-    st[o.Pd] = 0.f;
-  }
-}
 
 // ------------------------------------------------------------------------------------ X6 math
 // fp32 products on the bf16 MFMA (X6 = 1). Every fp32 operand value splits EXACTLY into three
@@ -386,31 +72,6 @@ __device__ __forceinline__ void fzero_slot(const ConvF32Args& a, const FGeo& o) 
 // which makes both halves' fragment reads conflict-free for the four ds_read_b128 lane groups AND
 // the K-major ds_write_b128 stores (8-lane groups = rows 2m, 2m+1 x 4 chunks) conflict-free (the
 // previous swizzle left those stores 2-way; found by exhaustive search over XOR-linear swizzles).
-__device__ __forceinline__ void split3(float4 v, s4v& h, s4v& m, s4v& l) {
-  const float x[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t u = __float_as_uint(x[i]);
-    const float r1 = x[i] - __uint_as_float(u & 0xFFFF0000u);
-    const uint32_t um = __float_as_uint(r1);
-    const float r2 = r1 - __uint_as_float(um & 0xFFFF0000u);
-    h[i] = (short)(u >> 16);
-    m[i] = (short)(um >> 16);
-    l[i] = (short)(__float_as_uint(r2) >> 16);
-  }
-}
-__device__ __forceinline__ void split1(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
-  const uint32_t u = __float_as_uint(x);
-  const float r1 = x - __uint_as_float(u & 0xFFFF0000u);
-  const uint32_t um = __float_as_uint(r1);
-  const float r2 = r1 - __uint_as_float(um & 0xFFFF0000u);
-  h = (uint16_t)(u >> 16);
-  m = (uint16_t)(um >> 16);
-  l = (uint16_t)(__float_as_uint(r2) >> 16);
-}
-__device__ __forceinline__ s8v cat44(s4v a, s4v b) {
-  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
-}
 __device__ __forceinline__ int x6_off(int row, int ch, int half) {  // dwords
   const int f = row & 2;                     // (b1 << 1)
   const int g = (row ^ (row >> 2)) & 1;      // b0 ^ b2
@@ -823,42 +484,7 @@ __global__ __launch_bounds__(256, (X6 && BP * BQ <= 64 * 128) ? 3 : 2) void conv
       }
     return;
   }
-  fepilogue<MODE, BP, BQ>(a, o, acc, smem);
-}
-
-// FWD / DGRAD split-K: sum the slices in slice order, then the same epilogue as the main kernel.
-template <int MODE, int BP, int BQ>
-__global__ __launch_bounds__(256) void convf32_splitk_epilogue(ConvF32Args a) {
-  constexpr int WP = BP / 2, WQ = BQ / 2, TP = WP / 16, TQ = WQ / 16;
-  __shared__ float red[2 * BP * 2];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wp = wid >> 1, wq = wid & 1;
-  const int nph = (MODE == F_DGRAD && a.stride == 2) ? 4 : 1;
-  const FGeo o = fgeo<MODE, BP, BQ>(a, blockIdx.x, blockIdx.y, blockIdx.z, nph * a.split_k);
-  if (o.q0 >= o.Qd || o.p0 >= o.Pd) {
-    fzero_slot<MODE, BP>(a, o);
-    return;
-  }
-  const long long qmax = (long long)a.slots / nph * BQ;
-  const long long slice = (long long)a.G * nph * qmax * o.Pd;
-  const float* base = a.partial + ((long long)o.g * nph + o.phase) * qmax * o.Pd;
-  f4v acc[TP][TQ];
-#pragma unroll
-  for (int ti = 0; ti < TP; ++ti)
-#pragma unroll
-    for (int tj = 0; tj < TQ; ++tj) {
-      const int q = o.q0 + wq * WQ + tj * 16 + (lane & 15);
-      const int p = o.p0 + wp * WP + ti * 16 + 4 * (lane >> 4);
-      f4v s = (f4v){0.f, 0.f, 0.f, 0.f};
-      if (q < o.Qd && p < o.Pd) {
-        const float* src = base + (long long)q * o.Pd + p;
-        for (int k = 0; k < a.split_k; ++k) {
-          const float4 v = *(const float4*)(src + k * slice);
-          s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
-        }
-      }
-      acc[ti][tj] = s;
-    }
-  fepilogue<MODE, BP, BQ>(a, o, acc, red);
+  fepi<MODE, BP, BQ, Lay16<BP, BQ>>(a, o, acc, smem);
 }
 
 // WGRAD split-K: out = (accumulate ? out : 0) + gscale * sum_k partial[k] (slice order).

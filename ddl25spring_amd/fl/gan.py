@@ -143,7 +143,8 @@ class FederatedGAN:
             for c in mine:
                 self._load_flat(glob)
                 self._swap_in(int(c))
-                g = torch.Generator(device="cpu").manual_seed(self.seed + int(c) + 1 + r * self.K)
+                # round stride = all clients (not K): no two (round, client) pairs share a stream
+                g = torch.Generator(device="cpu").manual_seed(self.seed + int(c) + 1 + r * len(self.data))
                 data = self.data[int(c)]
                 idx = torch.stack([torch.randint(0, len(data), (self.batch_size,), generator=g)
                                    for _ in range(self.local_steps)])

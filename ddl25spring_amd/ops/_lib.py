@@ -77,7 +77,8 @@ class ConvF32Args(ctypes.Structure):  # conv_f32.hip
                 ("x_gs", i64), ("w_gs", i64), ("dy_gs", i64), ("out_gs", i64), ("bias_gs", i64), ("res_gs", i64),
                 ("G", i32), ("N", i32), ("H", i32), ("W", i32), ("C", i32), ("K", i32), ("R", i32), ("S", i32),
                 ("P", i32), ("Q", i32), ("stride", i32), ("pad", i32), ("relu", i32), ("accumulate", i32),
-                ("split_k", i32), ("res_sub", i32), ("in_relu", i32), ("slots", i32), ("gscale", f32)]
+                ("split_k", i32), ("res_sub", i32), ("in_relu", i32), ("slots", i32), ("gscale", f32),
+                ("wsplit", vp), ("ws_gs", i64)]
 
 
 class BNFBwdArgs(ctypes.Structure):  # bn_f32.hip
@@ -174,6 +175,11 @@ _SIGS.update({
     "ddl_convf32": [ctypes.POINTER(ConvF32Args), i32, i32, vp],
     "ddl_convf32_slots": [ctypes.POINTER(ConvF32Args), i32, i32],
     "ddl_convf32_workspace": [ctypes.POINTER(ConvF32Args), i32, i32],
+    # conv_x6h.hip
+    "ddl_x6h": [ctypes.POINTER(ConvF32Args), i32, i32, vp],
+    "ddl_x6h_ok": [ctypes.POINTER(ConvF32Args), i32, i32],
+    "ddl_x6h_workspace": [ctypes.POINTER(ConvF32Args), i32, i32],
+    "ddl_x6_split_weights": [vp, vp, i32, i32, i32, i32, i32, i64, i64, i32, vp],
     # bn_f32.hip
     "ddl_bnf_finalize": [ctypes.POINTER(BNFArgs), ctypes.POINTER(BNFArgs), vp],
     "ddl_bnf_apply": [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, vp],
@@ -186,6 +192,7 @@ _SIGS.update({
     "ddl_bnf_channel_sum": [vp, vp, i64, vp, i64, i32, i32, vp],
 })
 _RESTYPES = {"ddl_convf32_slots": ctypes.c_longlong, "ddl_convf32_workspace": ctypes.c_longlong,
+             "ddl_x6h_workspace": ctypes.c_longlong,
              "ddl_gram_f32_workspace": ctypes.c_longlong}
 
 _OPTIONAL_SIGS: dict[str, list] = {}

@@ -335,7 +335,7 @@ def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0, _tun
         # keep the inputs alive until wgrad_overlap joins the side stream back (not record_stream:
         # inside a graph capture the allocator can never retire a record_stream'd block, so every
         # captured step would grow the graph's private pool — 226 GiB reserved for one 8-client round)
-        _SIDE_KEEP.extend((dy, x) + (tuple(in_bn) if in_bn is not None else ()))
+        _side_keep(side, (dy, x) + (tuple(in_bn) if in_bn is not None else ()))
         with torch.cuda.stream(side):
             return F32.conv_wgrad(dy, x, geom, dw, accumulate, wgrad_scale(dw), in_bn=in_bn, split_k=splits,
                                   ws_role="side")
@@ -360,8 +360,7 @@ def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0, _tun
         check(_lib.kernels().ddl_conv_wgrad(ctypes.byref(a), cfg, stream()), "conv_wgrad")
         return dw
     side.wait_stream(torch.cuda.current_stream())
-    dy.record_stream(side)
-    x.record_stream(side)
+    _side_keep(side, (dy, x))  # as the fp32 branch: no record_stream (graph-pool growth)
     with torch.cuda.stream(side):
         check(_lib.kernels().ddl_conv_wgrad(ctypes.byref(a), cfg, stream()), "conv_wgrad")
     return dw
@@ -370,7 +369,12 @@ def conv_wgrad(dy, x, geom: ConvGeom, dw, accumulate=True, cfg=0, splits=0, _tun
 # ------------------------------------------------------------------- wgrad / dgrad overlap
 _WGRAD_SIDE: "torch.cuda.Stream | None" = None
 _SIDE_STREAMS: dict = {}
-_SIDE_KEEP: list = []  # fp32 side-stream WGRAD inputs, released when wgrad_overlap joins
+# side-stream WGRAD inputs per side stream, released when wgrad_overlap joins THAT stream back
+_SIDE_KEEP: dict = {}
+
+
+def _side_keep(side, tensors) -> None:
+    _SIDE_KEEP.setdefault(side.cuda_stream, []).extend(tensors)
 
 
 # Paired DGRAD + WGRAD of one conv in one launch (conv_igemm.hip ``ddl_conv_pair``). The pair
@@ -578,7 +582,9 @@ class wgrad_overlap:
         global _WGRAD_SIDE
         if _WGRAD_SIDE is not None and _WGRAD_SIDE is not self.prev:
             torch.cuda.current_stream().wait_stream(_WGRAD_SIDE)
-            _SIDE_KEEP.clear()  # joined: their memory may be reused in stream order
+            # joined: this side stream's inputs may be reused in stream order (other devices'
+            # side streams, not joined here, keep theirs)
+            _SIDE_KEEP.pop(_WGRAD_SIDE.cuda_stream, None)
         _WGRAD_SIDE = self.prev
         return False
 
@@ -1278,6 +1284,8 @@ def gram(X, center=None):
     if not X.is_cuda:
         return ref.gram(X, center)
     K, n = X.shape
+    if K > MAX_ROBUST_CLIENTS:
+        return _gram_blocked(X, center)
     _robust_k(K, "gram")
     assert X.dtype == torch.float32 and X.stride(1) == 1
     out = torch.empty(K, K, dtype=torch.float32, device=X.device)
@@ -1286,6 +1294,28 @@ def gram(X, center=None):
     check(_lib.kernels().ddl_gram_f32(ptr(X), X.stride(0), ptr(center), K, n, ptr(part), cap, ptr(out),
                                       stream()), "gram_f32")
     out._keep = part  # the scratch must outlive the (asynchronous) launches
+    return out
+
+
+def _gram_blocked(X, center=None):
+    """Gram of K > MAX_ROBUST_CLIENTS rows: the native Gram of every pair of row blocks stacked
+    ([A; B], <= MAX_ROBUST_CLIENTS rows) yields A A^T, A B^T and B B^T; each output block comes from
+    one fixed-order native reduction, so the result stays bit-reproducible."""
+    K = X.shape[0]
+    bs = MAX_ROBUST_CLIENTS // 2
+    nb = -(-K // bs)
+    out = torch.empty(K, K, dtype=torch.float32, device=X.device)
+    for i in range(nb):
+        a0, a1 = i * bs, min(K, (i + 1) * bs)
+        for j in range(i, nb):
+            b0, b1 = j * bs, min(K, (j + 1) * bs)
+            if i == j:
+                out[a0:a1, a0:a1] = gram(X[a0:a1].contiguous(), center)
+                continue
+            gp = gram(torch.cat([X[a0:a1], X[b0:b1]]), center)
+            na = a1 - a0
+            out[a0:a1, b0:b1] = gp[:na, na:]
+            out[b0:b1, a0:a1] = gp[na:, :na]
     return out
 
 

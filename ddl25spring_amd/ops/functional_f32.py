@@ -46,17 +46,28 @@ class SlotStats:
         self.rows = 0
 
 
-def workspace(device, role: str = "main") -> torch.Tensor | None:
-    # one per (device, role): a side-stream WGRAD (role "side", functional.wgrad_overlap) runs
-    # concurrently with the main stream's split-K launches
+def workspace(device, role: str = "main") -> torch.Tensor:
+    """The split-K workspace of (device, role): a side-stream WGRAD (role "side",
+    functional.wgrad_overlap) runs concurrently with the main stream's split-K launches. Both
+    roles are allocated on the first (eager) call; a first call inside a HIP-graph capture raises
+    rather than silently dropping to split 1 (which would change the reduction order, so a
+    captured step would no longer match the eager one bit for bit)."""
     key = f"{device}:{role}"
     b = _WS.get(key)
     if b is None:
         if torch.cuda.is_current_stream_capturing():
-            return None
-        b = torch.empty(WS_CAP, dtype=torch.float32, device=device)
-        _WS[key] = b
+            raise RuntimeError("fp32 split-K workspace first requested inside a graph capture: run one eager "
+                               "step (or functional_f32.ensure_workspace) before capturing")
+        ensure_workspace(device)
+        b = _WS[key]
     return b
+
+
+def ensure_workspace(device) -> None:
+    for role in ("main", "side"):
+        key = f"{device}:{role}"
+        if key not in _WS:
+            _WS[key] = torch.empty(WS_CAP, dtype=torch.float32, device=device)
 
 
 def _dims(mode, g):
@@ -102,6 +113,40 @@ def set_math(name: str) -> None:
 
 
 X6_BIT = 1 << 16
+# conv_x6h.hip: the halo-staged X6 kernel (FWD / stride-1 DGRAD of "same" 3x3 and 1x1 convs, 128-pixel
+# tiles, pre-split weights). DDL_F32_HALO=0 keeps every launch on conv_f32.hip.
+HALO_BIT = 1 << 17
+_HALO = [os.environ.get("DDL_F32_HALO", "1") != "0"]
+HALO_HPMAX = 288
+
+
+def set_halo(on: bool) -> None:
+    if bool(on) != _HALO[0]:
+        _HALO[0] = bool(on)
+        _PLANS.clear()
+
+
+def halo_ok(mode: int, g) -> bool:
+    """Mirror of conv_x6h.hip x6h_geo: can the halo kernel run this (mode, geometry)?"""
+    if mode not in (F_FWD, F_DGRAD) or g.stride != 1 or g.R != g.S or g.R not in (1, 3) or g.pad != (g.R - 1) // 2:
+        return False
+    if g.P != g.H or g.Q != g.W:
+        return False
+    OH, OW = g.P, g.Q
+    if OW < 4 or OW > 128 or OW & (OW - 1):
+        return False
+    TR = 128 // OW
+    if TR <= OH:
+        if OH % TR:
+            return False
+        SR = TR
+    else:
+        if TR % OH:
+            return False
+        SR = OH
+    HP = (TR // SR) * (SR + g.R - 1) * (OW + g.S - 1)
+    SC, Pd = (g.C, g.K) if mode == F_FWD else (g.K, g.C)
+    return HP <= HALO_HPMAX and SC % 16 == 0 and Pd % 4 == 0
 
 
 def _cfg(cfg: int) -> int:
@@ -143,9 +188,15 @@ def _tuned(mode: int, g):
 
 
 def set_plan(mode: int, geom, bp: int, bq: int, split: int, engine: str | None = None) -> None:
-    """Pin a launch plan (tile BP x BQ, split-K slices[, engine under "auto"]) for one (mode,
-    geometry) — the tuner."""
-    _OVERRIDE[(mode, geom)] = (cfg_of(bp, bq) | (X6_BIT if engine in (None, "x6") else 0), int(split))
+    """Pin a launch plan (tile BP x BQ, split-K slices[, engine under "auto": "x6", "mfma32", or
+    "x6h" = the halo kernel, BQ 128]) for one (mode, geometry) — the tuner and the tests."""
+    bits = {None: X6_BIT, "x6": X6_BIT, "x6h": X6_BIT | HALO_BIT, "mfma32": 0}[engine]
+    _OVERRIDE[(mode, geom)] = (cfg_of(bp, bq) | bits, int(split))
+    _PLANS.pop((mode, geom), None)
+
+
+def clear_plan(mode: int, geom) -> None:
+    _OVERRIDE.pop((mode, geom), None)
     _PLANS.pop((mode, geom), None)
 
 
@@ -156,7 +207,11 @@ def plan(mode: int, geom) -> tuple[int, int]:
     p = _PLANS.get(key)
     if p is not None:
         return p
-    p = _OVERRIDE.get(key) or _tuned(mode, geom)
+    p = _OVERRIDE.get(key)
+    if p is None and _HALO[0] and _MATH[0] != "mfma32" and halo_ok(mode, geom):
+        p = _halo_plan(mode, geom)
+    if p is None:
+        p = _tuned(mode, geom)
     if p is None:
         Pd, Qd, Kr, nph = _dims(mode, geom)
         bp = 128 if Pd > 64 else 64
@@ -169,6 +224,20 @@ def plan(mode: int, geom) -> tuple[int, int]:
         p = (cfg_of(bp, bq) | X6_BIT, split)
     _PLANS[key] = p
     return p
+
+
+def _halo_plan(mode: int, geom) -> tuple[int, int]:
+    """Halo kernel: BP 128 where the output channels allow, 128-pixel tiles, split-K over the
+    16-channel chunks until ~TARGET_WG workgroups (each slice keeping >= 4 chunks)."""
+    Pd, Qd, _, _ = _dims(mode, geom)
+    SC = geom.C if mode == F_FWD else geom.K
+    bp = 128 if Pd > 64 else 64
+    tiles = -(-Pd // bp) * -(-Qd // 128) * geom.G
+    nch = SC // 16
+    split = 1
+    while tiles * split < TARGET_WG and nch >= split * 2 * 4 and split < 32:
+        split *= 2
+    return cfg_of(bp, 128) | X6_BIT | HALO_BIT, split
 
 
 def _args(geom, **kw) -> _lib.ConvF32Args:
@@ -192,14 +261,33 @@ def _launch(a, mode: int, geom, device, split_k: int = 0, ws_role: str = "main")
         split = split_k
     a.split_k = split
     cfg = _cfg(cfg)
+    if cfg & HALO_BIT and not halo_ok(mode, geom):
+        cfg &= ~HALO_BIT
     if split > 1:
         need = lib.ddl_convf32_workspace(ctypes.byref(a), mode, cfg)
         buf = workspace(device, ws_role)
-        if buf is None or need > buf.numel():
-            a.split_k = split = 1
+        if need > buf.numel():
+            a.split_k = split = 1  # plan-determined (same choice eager and captured)
         else:
             a.partial, a.partial_cap = buf.data_ptr(), buf.numel()
-    check(lib.ddl_convf32(ctypes.byref(a), mode, cfg, stream()), ("conv_fwd", "conv_dgrad", "conv_wgrad")[mode] + "_f32")
+    name = ("conv_fwd", "conv_dgrad", "conv_wgrad")[mode] + "_f32"
+    if cfg & HALO_BIT:
+        ws_buf = split_weights(a, mode, geom, device)
+        a.wsplit, a.ws_gs = ws_buf.data_ptr(), ws_buf.stride(0)
+        check(lib.ddl_x6h(ctypes.byref(a), mode, cfg & ~HALO_BIT, stream()), name + "_halo")
+        return
+    check(lib.ddl_convf32(ctypes.byref(a), mode, cfg, stream()), name)
+
+
+def split_weights(a, mode: int, geom, device) -> torch.Tensor:
+    """The X6 operand image of the launch's weights (8 bytes per element): FWD layout [G][K][R][S][C],
+    DGRAD layout [G][C][R][S][K]. Rebuilt from the fp32 weights for every launch (the fused-SGD
+    WGRAD updates them in place), into a stream-ordered temporary."""
+    T = geom.R * geom.S
+    out = torch.empty(geom.G, geom.K * T * geom.C * 2, dtype=torch.float32, device=device)
+    check(_lib.kernels().ddl_x6_split_weights(a.w, out.data_ptr(), geom.G, geom.K, T, geom.C, 0 if mode == F_FWD else 1,
+                                              a.w_gs, out.stride(0) * 4, 0, stream()), "x6_split_weights")
+    return out
 
 
 def _slots(a, mode: int, geom) -> int:

@@ -170,12 +170,20 @@ def context() -> DistContext:
 
 def shutdown():
     global _CTX
-    if _CTX is not None and _CTX.ipc is not None:
-        _CTX.ipc.check()
-        _CTX.ipc.close()  # collective: barrier before unmapping
-    if dist.is_initialized():
-        dist.destroy_process_group()
-    _CTX = None
+    err = None
+    try:
+        if _CTX is not None and _CTX.ipc is not None:
+            try:
+                _CTX.ipc.check()
+            except Exception as e:  # raised after the collective teardown: peers must not wait on us
+                err = e
+            _CTX.ipc.close()  # collective: barrier before unmapping
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        _CTX = None
+    if err is not None:
+        raise err
 
 
 def set_context(ctx: DistContext | None):

@@ -26,8 +26,10 @@ def main():
     ap.add_argument("--N", type=int, default=100)
     ap.add_argument("--layer", default="c64", choices=list(LAYERS))
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--halo", type=int, default=1, help="0: never the halo kernel (conv_x6h.hip)")
     a = ap.parse_args()
     F32.set_math(a.math)
+    F32.set_halo(bool(a.halo))
     H, C, K, R, st = LAYERS[a.layer]
     g = ConvGeom(a.G, a.N, H, H, C, K, R, R, st, (R - 1) // 2)
     dev = torch.device("cuda")
@@ -50,7 +52,8 @@ def main():
     ms = e0.elapsed_time(e1) / a.reps
     fl = 2 * g.G * g.N * g.P * g.Q * g.K * g.R * g.S * g.C
     mode = {"fwd": F32.F_FWD, "dgrad": F32.F_DGRAD, "wgrad": F32.F_WGRAD}[a.mode]
-    print(f"{a.math} {a.mode} G={a.G} {a.layer}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF/s plan={F32.plan(mode, g)}")
+    print(f"{a.math} halo={a.halo} {a.mode} G={a.G} {a.layer}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF/s "
+          f"plan={F32.plan(mode, g)}")
 
 
 if __name__ == "__main__":

@@ -1,0 +1,172 @@
+"""Halo-staged X6 fp32 convolution (csrc/kernels/conv_x6h.hip): FWD and stride-1 DGRAD against a
+float64 PyTorch oracle, every fused epilogue, every tile geometry class (rows of one image, whole
+images per tile, a partial last tile) and split-K; plus bitwise run-to-run determinism.
+
+The reference's convs are stock fp32 nn.Conv2d (lab/tutorial_1a/hfl_complete.py:43-53); the
+tolerance is the fp32 one of tests/test_fp32_gpu.py (1e-5 of the result's max-abs).
+"""
+import pytest
+import torch
+
+from ddl25spring_amd.ops import functional as Fn
+from ddl25spring_amd.ops import functional_f32 as F32
+from ddl25spring_amd.ops.functional import ConvGeom
+
+from test_fp32_gpu import _close, _weights, ref_dgrad, ref_fwd
+
+pytestmark = pytest.mark.gpu
+
+GEOMS = [
+    ConvGeom(G=2, N=5, H=32, W=32, C=64, K=64, R=3, S=3, stride=1, pad=1),    # 4 rows of one image
+    ConvGeom(G=1, N=3, H=16, W=16, C=128, K=128, R=3, S=3, stride=1, pad=1),  # 8 rows
+    ConvGeom(G=2, N=5, H=8, W=8, C=256, K=256, R=3, S=3, stride=1, pad=1),    # 2 images, partial tile
+    ConvGeom(G=1, N=11, H=4, W=4, C=512, K=192, R=3, S=3, stride=1, pad=1),   # 8 images, partial tile
+    ConvGeom(G=2, N=3, H=32, W=32, C=32, K=64, R=1, S=1, stride=1, pad=0),    # 1x1 (the im2col stem)
+    ConvGeom(G=1, N=2, H=8, W=8, C=48, K=36, R=3, S=3, stride=1, pad=1),      # odd channel counts
+]
+IDS = [f"{g.C}x{g.K}_{g.H}x{g.W}_{g.R}n{g.N}" for g in GEOMS]
+
+
+@pytest.fixture(autouse=True)
+def _x6():
+    old = F32.math()
+    F32.set_math("x6")
+    yield
+    F32.set_math(old)
+
+
+def _pin(mode, g, split):
+    Pd = g.K if mode == F32.F_FWD else g.C
+    F32.set_plan(mode, g, 128 if Pd > 64 else 64, 128, split, "x6h")
+
+
+@pytest.mark.parametrize("split", [1, 2])
+@pytest.mark.parametrize("geom", GEOMS, ids=IDS)
+def test_x6h_fwd(cuda, geom, split):
+    if geom.C % 16:
+        pytest.skip("halo FWD needs C % 16 == 0")
+    assert F32.halo_ok(F32.F_FWD, geom)
+    _pin(F32.F_FWD, geom, split)
+    try:
+        torch.manual_seed(0)
+        x = torch.randn(geom.G, geom.N, geom.H, geom.W, geom.C, device=cuda)
+        w = _weights(geom, cuda)
+        st = F32.SlotStats()
+        y = Fn.conv_fwd(x, w, geom, stats=st)
+        yr = ref_fwd(x.cpu(), w.cpu(), geom)
+        _close(y, yr)
+        t = st.t.double().cpu()
+        yf = yr.reshape(geom.G, -1, geom.K)
+        rows = st.rows
+        assert rows == 128 and t.shape[1] == -(-yf.shape[1] // rows)
+        for i in range(t.shape[1]):
+            blk = yf[:, i * rows:(i + 1) * rows]
+            _close(t[:, i, 0], blk.sum(1))
+            _close(t[:, i, 1], ((blk - blk.mean(1, keepdim=True)) ** 2).sum(1))
+        bias = torch.randn(geom.G, geom.K, device=cuda)
+        res = torch.randn(geom.G, geom.N, geom.P, geom.Q, geom.K, device=cuda)
+        y2 = Fn.conv_fwd(x, w, geom, bias=bias, relu=True, residual=res)
+        _close(y2, (yr + bias.cpu().double()[:, None, None, None] + res.cpu().double()).clamp_min(0))
+        sc = torch.rand(geom.G, geom.C, device=cuda) + 0.5
+        sh = torch.randn(geom.G, geom.C, device=cuda) * 0.3
+        y3 = Fn.conv_fwd(x, w, geom, in_bn=(sc, sh))
+        xa = (x.double() * sc.double()[:, None, None, None] + sh.double()[:, None, None, None]).clamp_min(0)
+        _close(y3, ref_fwd(xa.cpu(), w.cpu(), geom))
+        # bitwise run-to-run
+        assert torch.equal(Fn.conv_fwd(x, w, geom, in_bn=(sc, sh)), y3)
+    finally:
+        F32.clear_plan(F32.F_FWD, geom)
+
+
+@pytest.mark.parametrize("split", [1, 2])
+@pytest.mark.parametrize("geom", GEOMS, ids=IDS)
+def test_x6h_dgrad(cuda, geom, split):
+    if geom.K % 16:
+        pytest.skip("halo DGRAD needs K % 16 == 0")
+    assert F32.halo_ok(F32.F_DGRAD, geom)
+    _pin(F32.F_DGRAD, geom, split)
+    try:
+        torch.manual_seed(1)
+        dy = torch.randn(geom.G, geom.N, geom.P, geom.Q, geom.K, device=cuda)
+        w = _weights(geom, cuda)
+        dxr = ref_dgrad(dy.cpu(), w.cpu(), geom)
+        d1 = Fn.conv_dgrad(dy, w, geom)
+        _close(d1, dxr)
+        res = torch.randn(geom.G, geom.N, geom.H, geom.W, geom.C, device=cuda)
+        mask = torch.randn(geom.G, geom.N, geom.H, geom.W, geom.C, device=cuda)
+        d2 = Fn.conv_dgrad(dy, w, geom, residual=res, mask=mask)
+        _close(d2, (dxr + res.cpu().double()) * (mask.cpu() > 0))
+        bx = torch.randn(geom.G, geom.N, geom.H, geom.W, geom.C, device=cuda)
+        mean = torch.randn(geom.G, geom.C, device=cuda) * 0.1
+        rstd = torch.rand(geom.G, geom.C, device=cuda) + 0.5
+        sc = torch.rand(geom.G, geom.C, device=cuda) + 0.5
+        sh = torch.randn(geom.G, geom.C, device=cuda) * 0.2
+        d3, part = Fn.conv_dgrad(dy, w, geom, bn=(bx, mean, rstd), mask_bn=(sc, sh))
+        b = lambda t: t.cpu().double()[:, None, None, None]  # noqa: E731
+        keep = (bx.cpu().double() * b(sc) + b(sh)) > 0
+        want = dxr * keep
+        _close(d3, want)
+        xhat = (bx.cpu().double() - b(mean)) * b(rstd)
+        p = part.double().cpu().sum(1)
+        _close(p[:, 0], want.sum((1, 2, 3)))
+        _close(p[:, 1], (want * xhat).sum((1, 2, 3)))
+        assert torch.equal(Fn.conv_dgrad(dy, w, geom), d1)
+    finally:
+        F32.clear_plan(F32.F_DGRAD, geom)
+
+
+def test_x6h_split_weights(cuda):
+    """The pre-split weight image reconstructs the fp32 weights exactly (h + m + l == w)."""
+    from ddl25spring_amd.ops import _lib
+    g = ConvGeom(G=2, N=1, H=8, W=8, C=32, K=48, R=3, S=3, stride=1, pad=1)
+    w = _weights(g, cuda)
+    a = F32._args(g, w=w.data_ptr(), w_gs=w.stride(0))
+    for mode in (F32.F_FWD, F32.F_DGRAD):
+        img = F32.split_weights(a, mode, g, cuda)
+        torch.cuda.synchronize()
+        raw = img.view(torch.int16).view(g.G, -1, 2, 8)  # per 4-chunk: (h0..h3 m0..m3)(l0..l3 h0..h3)
+        bf = lambda t: (t.to(torch.int32) << 16).view(torch.float32)  # noqa: E731
+        h, m, l_ = raw[:, :, 0, :4], raw[:, :, 0, 4:], raw[:, :, 1, :4]
+        assert torch.equal(raw[:, :, 1, 4:], h)
+        rec = (bf(h).double() + bf(m).double() + bf(l_).double()).reshape(g.G, -1)
+        want = w if mode == F32.F_FWD else w.permute(0, 4, 2, 3, 1)  # DGRAD: [G][C][R][S][K]
+        assert torch.equal(rec, want.reshape(g.G, -1).double()), _lib
+
+
+def test_split_workspace_capture(cuda):
+    """A split-K launch first requested inside a graph capture raises (no silent split-1 fallback);
+    after ensure_workspace the captured launch equals the eager one bit for bit."""
+    g = ConvGeom(G=1, N=3, H=4, W=4, C=512, K=512, R=3, S=3, stride=1, pad=1)
+    _pin(F32.F_FWD, g, 4)
+    try:
+        x = torch.randn(g.G, g.N, g.H, g.W, g.C, device=cuda)
+        w = _weights(g, cuda)
+        saved = dict(F32._WS)
+        F32._WS.clear()
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            graph = torch.cuda.CUDAGraph()
+            with pytest.raises(RuntimeError, match="graph capture"):
+                with torch.cuda.graph(graph, stream=s):
+                    Fn.conv_fwd(x, w, g)
+        torch.cuda.synchronize()
+        F32._WS.update(saved)
+        F32.ensure_workspace(cuda)
+        eager = Fn.conv_fwd(x, w, g)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            y = Fn.conv_fwd(x, w, g)
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(y, eager)
+    finally:
+        F32.clear_plan(F32.F_FWD, g)
+
+
+def test_gram_blocked_k129(cuda):
+    """Krum's Gram for K > 128 clients: blocked native Grams, float64-close and bit-reproducible."""
+    X = torch.randn(129, 4096, device=cuda)
+    G1 = Fn.gram(X)
+    ref = (X.double() @ X.double().t()).cpu()
+    _close(G1, ref)
+    assert torch.equal(Fn.gram(X), G1)
