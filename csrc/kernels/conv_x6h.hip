@@ -28,14 +28,21 @@
 // bf16 MFMA's own accumulation is not round-to-nearest, see conv_f32.hip), plain stores only.
 #include "conv_f32_core.h"
 
-namespace {
-
 constexpr int BQH = 128;    // output pixels per tile
 constexpr int HSTR = 144;   // halo image bytes per pixel: 16 channels x 8 B + 16 B pad (bank spread)
 constexpr int PSTR = 128;   // weight image bytes per row (16 channels x 8 B, 16-B granule XOR swizzle)
-constexpr int HPMAX = 288;  // halo pixels per tile (4 x 4 images: 8 x 6 x 6)
-constexpr unsigned OOB = 0xFFFFFFF0u;
+constexpr int HBSMALL = 32768;  // halo image bytes, OW >= 8 (2 workgroups per CU at BP 128: 48 + 32 KiB)
+constexpr int HBLARGE = 45056;  // OW = 4 (8 image segments of 6 x 6 pixels)
+constexpr int NWB = 3;      // weight images in the LDS ring (DMA runs two steps ahead)
+// Out-of-range buffer offset: any per-step scalar offset added to it stays >= the descriptor's
+// num_records (< 2^31), so the load returns zeros without a per-step select.
+constexpr unsigned OOB = 0x80000000u;
 
+// Halo image layout: pixel (segment sg, row hi, col hj) at sg * SEGB + hi * ROWB + hj * HSTR bytes.
+// HSTR = 9 quads (16 B) per pixel spreads the pixels of one row over the 16 bank quads; ROWB and
+// SEGB are padded (host: halo_layout) so that the 16 lanes of every ds_read_b128 group — which
+// span 1..8 output rows of the tile depending on OW — land on distinct bank quads (conflict-free
+// for OW = 4, 16, 32; one 2-way pair for OW = 8 inside the 32 KiB budget).
 struct HaloGeo {
   int lgW;      // log2 OW (output pixels per row)
   int SR;       // output rows per image segment of the tile
@@ -44,27 +51,46 @@ struct HaloGeo {
   int OH;       // output rows per image
   int SH, SW, SC;  // source (X for FWD, dY for DGRAD) height, width, channels
   int Pd;       // output channels (K for FWD, C for DGRAD)
+  int ROWB, SEGB, HBYTES;  // halo row / segment strides, image bytes
 };
 
 typedef float f16v __attribute__((ext_vector_type(16)));
 
-__device__ __forceinline__ float4 bload4(const __amdgpu_buffer_rsrc_t& rs, unsigned off) {
-  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+template <int N>
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// Workgroup barrier WITHOUT the release fence of __syncthreads (which waits for every outstanding
+// vector-memory op, the in-flight weight DMA included): callers order LDS themselves (counted
+// vmcnt for the DMA pieces, lgkmcnt(0) after ds_writes that other waves read).
+__device__ __forceinline__ void cta_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void wait_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// One LDS-DMA piece (16 B per lane to lds + 16 * lane). Kept out of the kernel body: with the
+// address-space cast inline in a __global__ template, the host pass silently drops the kernel's
+// launch stub (the library then fails to load).
+__device__ __forceinline__ void dma16(const __amdgpu_buffer_rsrc_t& rs, char* lds, unsigned off, unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds, 16, off, soff, 0, 0);
 }
 
-template <int MODE, int BP, int RS>
+__device__ __forceinline__ float4 bload4(const __amdgpu_buffer_rsrc_t& rs, unsigned off, unsigned soff) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, soff, 0));
+}
+
+template <int MODE, int BP, int RS, int HB>
 __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo hg) {
   constexpr int T = RS * RS;                 // taps
   constexpr int PD = (RS - 1) / 2;           // pad
   constexpr int WP = BP / 2, TI = WP / 32, TJ = 2;
   constexpr int UP = BP / 32;                // weight LDS-DMA pieces (1 KiB) per wave per step
-  constexpr int NUH = (HPMAX * 4 + 255) / 256;  // halo units (pixel x 4-channel chunk) per thread
+  constexpr int HPM = HB == HBSMALL ? 208 : 288;   // halo pixel capacity (host-checked)
+  constexpr int NUH = (HPM * 4 + 255) / 256;  // halo units (pixel x 4-channel chunk) per thread
   constexpr int PIMG = BP * PSTR;            // bytes per weight image
   constexpr bool XF_OK = MODE == F_FWD;
-  __shared__ __attribute__((aligned(16))) char smem[2 * PIMG + HPMAX * HSTR];
-  __shared__ float xform[XF_OK ? 1024 : 1];
+  __shared__ __attribute__((aligned(16))) char smem[NWB * PIMG + HB];
   char* const pimg = smem;
-  char* const himg = smem + 2 * PIMG;
+  char* const himg = smem + NWB * PIMG;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wp = wid >> 1, wq = wid & 1;
   const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
@@ -82,16 +108,11 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
   const int per = (ncc + o.nsplit - 1) / o.nsplit;
   const int cc0 = o.split * per, cc1 = min(ncc, cc0 + per);
 
+  // operand-side BN (FWD): every halo unit of this thread covers the same 4 channels of a chunk,
+  // channels cc * 16 + 4 * (tid & 3) .. + 3: scale / shift loaded with the chunk's halo
   const bool xf = XF_OK && a.in_scale != nullptr;
-  if constexpr (XF_OK) {
-    if (xf) {
-      for (int i = tid; i < SC; i += 256) {
-        xform[i] = a.in_scale[(long long)g * SC + i];
-        xform[512 + i] = a.in_shift[(long long)g * SC + i];
-      }
-    }
-  }
   const bool xrelu = a.in_relu != 0;
+  float4 xsc = make_float4(1.f, 1.f, 1.f, 1.f), xsh = make_float4(0.f, 0.f, 0.f, 0.f);
 
   // ---------------------------------------------------------------- buffer descriptors
   const float* src = MODE == F_FWD ? a.x + (long long)g * a.x_gs : a.dy + (long long)g * a.dy_gs;
@@ -122,13 +143,20 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
       const int sr = r0 + hi - PD, sc = hj - PD;
       if (n < a.N && (unsigned)sr < (unsigned)hg.SH && (unsigned)sc < (unsigned)hg.SW)
         hoff[i] = (unsigned)((((long long)n * hg.SH + sr) * hg.SW + sc) * SC + ch * 4) * 4u;
-      hlds[i] = hp * HSTR + ch * 32;
+      hlds[i] = seg * hg.SEGB + hi * hg.ROWB + hj * HSTR + ch * 32;
     }
   }
   float4 hreg[NUH];
   auto halo_load = [&](int cc) {
 #pragma unroll
-    for (int i = 0; i < NUH; ++i) hreg[i] = bload4(rS, hoff[i] == OOB ? OOB : hoff[i] + (unsigned)cc * 64u);
+    for (int i = 0; i < NUH; ++i) hreg[i] = bload4(rS, hoff[i], (unsigned)cc * 64u);
+    if constexpr (XF_OK) {
+      if (xf) {
+        const long long c = (long long)g * SC + cc * 16 + 4 * (tid & 3);
+        xsc = *(const float4*)(a.in_scale + c);
+        xsh = *(const float4*)(a.in_shift + c);
+      }
+    }
   };
   auto halo_store = [&](int cc) {
 #pragma unroll
@@ -137,11 +165,10 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
       float4 v = hreg[i];
       if constexpr (XF_OK) {
         if (xf && hoff[i] != OOB) {  // operand-side BN + ReLU on real pixels (padding stays 0)
-          const int c = cc * 16 + ((tid + 256 * i) & 3) * 4;
-          v.x = v.x * xform[c] + xform[512 + c];
-          v.y = v.y * xform[c + 1] + xform[512 + c + 1];
-          v.z = v.z * xform[c + 2] + xform[512 + c + 2];
-          v.w = v.w * xform[c + 3] + xform[512 + c + 3];
+          v.x = v.x * xsc.x + xsh.x;
+          v.y = v.y * xsc.y + xsh.y;
+          v.z = v.z * xsc.z + xsh.z;
+          v.w = v.w * xsc.w + xsh.w;
           if (xrelu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
         }
       }
@@ -167,12 +194,9 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
   }
   auto wload = [&](int buf, int cc, int t) {
     const int wtap = MODE == F_FWD ? t : T - 1 - t;  // DGRAD: the flipped kernel
-    const unsigned add = (unsigned)(wtap * SC * 8 + cc * 128);
+    const unsigned add = (unsigned)(wtap * SC * 8 + cc * 128);  // wave-uniform: the scalar offset
 #pragma unroll
-    for (int i = 0; i < UP; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rW, (__attribute__((address_space(3))) void*)(pimg + buf * PIMG + (wsc + 4 * i) * 1024), 16,
-          woff[i] == OOB ? OOB : woff[i] + add, 0, 0, 0);
+    for (int i = 0; i < UP; ++i) dma16(rW, pimg + buf * PIMG + (wsc + 4 * i) * 1024, woff[i], add);
   };
 
   // ---------------------------------------------------------------- fragment addressing
@@ -193,22 +217,39 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
     const int ql = wq * 64 + tj * 32 + (lane & 31);
     const int jj = ql & ((1 << hg.lgW) - 1), rowl = ql >> hg.lgW;
     const int seg = rowl / hg.SR, ii = rowl - seg * hg.SR;
-    boff[tj] = ((seg * hg.HR + ii) * hg.HC + jj) * HSTR + hh * 32;
+    boff[tj] = seg * hg.SEGB + ii * hg.ROWB + jj * HSTR + hh * 32;
   }
 
-  f16v acc[TI][TJ];
+  // acc: the running sums (IEEE adds); cacc: one 16-channel chunk's MFMA chains (T taps x 6 MFMAs
+  // accumulated inside the MFMA, whose internal accumulation is not round-to-nearest: bounded to
+  // T * 6 <= 54 steps — <= ~2e-6 relative — before each IEEE add into acc)
+  f16v acc[TI][TJ], cacc[TI][TJ];
 #pragma unroll
   for (int ti = 0; ti < TI; ++ti)
 #pragma unroll
-    for (int tj = 0; tj < TJ; ++tj) acc[ti][tj] = (f16v){};
+    for (int tj = 0; tj < TJ; ++tj) acc[ti][tj] = cacc[ti][tj] = (f16v){};
+  auto flush = [&]() {
+#pragma unroll
+    for (int ti = 0; ti < TI; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj) {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[ti][tj][v] = acc[ti][tj][v] + cacc[ti][tj][v];
+        cacc[ti][tj] = (f16v){};
+      }
+  };
 
   const int k0 = cc0 * T, k1 = cc1 * T;
   constexpr int HT = T >= 3 ? T - 3 : 0;  // tap at which the next chunk's halo loads are issued
 
+  int bdr[RS][TJ];  // halo fragment bases per tap row
+#pragma unroll
+  for (int dr = 0; dr < RS; ++dr)
+#pragma unroll
+    for (int tj = 0; tj < TJ; ++tj) bdr[dr][tj] = boff[tj] + dr * hg.ROWB;
   auto compute = [&](int buf, int t) {
     const char* P = pimg + buf * PIMG;
     const int dr = t / RS, ds = t - dr * RS;
-    const int tapoff = (dr * hg.HC + ds) * HSTR;
     s8v a_hm[TI][2], a_lh[TI][2], b_hm[TJ][2], b_lh[TJ][2];
 #pragma unroll
     for (int ti = 0; ti < TI; ++ti)
@@ -221,7 +262,7 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
     for (int tj = 0; tj < TJ; ++tj)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const char* hb = himg + boff[tj] + tapoff + j * 64;
+        const char* hb = himg + bdr[dr][tj] + ds * HSTR + j * 64;
         b_hm[tj][j] = *(const s8v*)hb;
         b_lh[tj][j] = *(const s8v*)(hb + 16);
       }
@@ -229,38 +270,83 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
     for (int ti = 0; ti < TI; ++ti)
 #pragma unroll
       for (int tj = 0; tj < TJ; ++tj) {
-        f16v c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_lh[ti][0], b_hm[tj][0], (f16v){}, 0, 0, 0);
+        f16v c = cacc[ti][tj];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_lh[ti][0], b_hm[tj][0], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_hm[ti][0], b_lh[tj][0], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_hm[ti][0], b_hm[tj][0], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_lh[ti][1], b_hm[tj][1], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_hm[ti][1], b_lh[tj][1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_hm[ti][1], b_hm[tj][1], c, 0, 0, 0);
-#pragma unroll
-        for (int v = 0; v < 16; ++v) acc[ti][tj][v] = acc[ti][tj][v] + c[v];
+        cacc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_hm[ti][1], b_hm[tj][1], c, 0, 0, 0);
       }
   };
 
   if (k0 < k1) {
-    // prologue: halo of chunk cc0 and the weights of step k0
-    wload(0, cc0, 0);
-    halo_load(cc0);
-    halo_store(cc0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int cc = cc0, t = 0;
+    // Weight images: a ring of NWB = 3; the DMA of step k + 2 is issued at step k into slot
+    // (k + 2) % 3, whose last reader (step k - 1) is past the barrier. vmcnt counts in issue order
+    // (DMA pieces and the halo register loads together): at the end of step k, step k + 1's pieces
+    // must have landed while step k + 2's (UP) and — between issue (tap HT) and use (chunk end) —
+    // the next chunk's halo loads (NUH, +2 for the BN constants) may still fly.
+    constexpr int NHL = NUH + (XF_OK ? 2 : 0);
+    auto step_of = [&](int kk, int& c, int& tt) { c = kk / T; tt = kk - c * T; };
+    {
+      int c1_, t1_;
+      wload(0, cc0, 0);
+      halo_load(cc0);
+      if (k0 + 1 < k1) { step_of(k0 + 1, c1_, t1_); wload(1, c1_, t1_); }
+      halo_store(cc0);
+      wait_vm<0>();
+      wait_lds();
+      cta_barrier();
+    }
+    if constexpr (T % 3 == 0) {
+      // taps unrolled: slot (tap % 3), DMA targets, halo timing and vmcnt counts are constants
+      for (int cc = cc0; cc < cc1; ++cc) {
+        const bool more = cc + 1 < cc1;
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          if (t + 2 < T) wload((t + 2) % 3, cc, t + 2);
+          else if (more) wload((t + 2) % 3, cc + 1, t + 2 - T);
+          if (t == HT && more) halo_load(cc + 1);
+          compute(t % 3, t);
+          if (t == T - 1) flush();
+          if (!more && t + 2 >= T) wait_vm<0>();
+          else if (more && (t == HT || t == HT + 1) && HT + 1 < T - 1) wait_vm<UP + NHL>();
+          else wait_vm<UP>();
+          cta_barrier();
+          if (t == T - 1 && more) {  // chunk boundary: every wave is done with this chunk's halo
+            halo_store(cc + 1);
+            wait_lds();
+            cta_barrier();
+          }
+        }
+      }
+    } else {
+    int cc = cc0, t = 0, slot = 0;
     for (int k = k0; k < k1; ++k) {
-      const int buf = (k - k0) & 1;
-      // step k + 1's weights into the other buffer (its last reader, step k - 1, is past the barrier)
-      if (k + 1 < k1) wload(buf ^ 1, t == T - 1 ? cc + 1 : cc, t == T - 1 ? 0 : t + 1);
-      if (t == HT && cc + 1 < cc1) halo_load(cc + 1);
-      compute(buf, t);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      const bool issue2 = k + 2 < k1;
+      if (issue2) {
+        int c2, t2;
+        step_of(k + 2, c2, t2);
+        wload(slot == 0 ? 2 : slot - 1, c2, t2);  // (slot + 2) % 3
+      }
+      const bool hl = t == HT && cc + 1 < cc1;
+      if (hl) halo_load(cc + 1);
+      compute(slot, t);
+      if (t == T - 1) flush();
+      // retire step k + 1's pieces (and, at the chunk's last tap, the halo loads)
+      const bool halo_fly = (HT < T - 1) && cc + 1 < cc1 && (t == HT || t == HT + 1);
+      if (!issue2) wait_vm<0>();
+      else if (halo_fly) wait_vm<UP + NHL>();
+      else wait_vm<UP>();
+      cta_barrier();
       if (t == T - 1 && k + 1 < k1) {  // chunk boundary: every wave is done with this chunk's halo
         halo_store(cc + 1);
-        __syncthreads();
+        wait_lds();
+        cta_barrier();
       }
       if (++t == T) { t = 0; ++cc; }
+      slot = slot == 2 ? 0 : slot + 1;
+    }
     }
   }
 
@@ -323,7 +409,50 @@ __global__ __launch_bounds__(256) void x6_split_weights_kernel(const float* __re
   }
 }
 
-bool x6h_geo(const ConvF32Args& a, int mode, int bp, HaloGeo& h, int& rs) {
+// Halo row / segment strides (in 16-B quads): the fewest bank conflicts of the fragment reads
+// (the 4 ds_read_b128 lane groups of a 32x32x16 B operand: lane l reads tile pixel l & 31, chunk
+// half l >> 5), then the fewest bytes; within HBSMALL when any candidate fits.
+static void halo_layout(HaloGeo& h) {
+  static const int grp[2][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+                                 {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31}};
+  const int OW = 1 << h.lgW, nseg = h.HP / (h.HR * h.HC);
+  int best[4] = {1 << 30, 1 << 30, 0, 0};  // worst, total, rq, sq
+  bool best_fit = false;
+  for (int rq = 9 * h.HC; rq < 9 * h.HC + 16; ++rq)
+    for (int sq = h.HR * rq; sq < h.HR * rq + 16; ++sq) {
+      int worst = 0, tot = 0;
+      for (int hh = 0; hh < 2; ++hh)
+        for (int gi = 0; gi < 2; ++gi) {
+          int cnt[16] = {0};
+          for (int e = 0; e < 16; ++e) {
+            const int q = grp[gi][e], row = q / OW, col = q % OW;
+            const int seg = row / h.SR, ri = row % h.SR;
+            ++cnt[(seg * sq + ri * rq + 9 * col + 2 * hh) & 15];
+          }
+          int m = 0;
+          for (int c = 0; c < 16; ++c) m = cnt[c] > m ? cnt[c] : m;
+          worst = m > worst ? m : worst;
+          tot += m;
+        }
+      const int bytes = nseg * sq * 16;
+      const bool fit = bytes <= HBSMALL;
+      const int bbytes = nseg * best[3] * 16;
+      bool better;
+      if (fit != best_fit) better = fit;
+      else if (worst != best[0]) better = worst < best[0];
+      else if (tot != best[1]) better = tot < best[1];
+      else better = bytes < bbytes;
+      if (better) {
+        best[0] = worst; best[1] = tot; best[2] = rq; best[3] = sq;
+        best_fit = fit;
+      }
+    }
+  h.ROWB = best[2] * 16;
+  h.SEGB = best[3] * 16;
+  h.HBYTES = nseg * h.SEGB;
+}
+
+static bool x6h_geo(const ConvF32Args& a, int mode, int bp, HaloGeo& h, int& rs) {
   if (mode != F_FWD && mode != F_DGRAD) return false;
   if (bp != 64 && bp != 128) return false;
   if (a.stride != 1 || a.R != a.S || (a.R != 1 && a.R != 3) || a.pad != (a.R - 1) / 2) return false;
@@ -352,16 +481,17 @@ bool x6h_geo(const ConvF32Args& a, int mode, int bp, HaloGeo& h, int& rs) {
   h.SW = a.W;
   h.SC = mode == F_FWD ? a.C : a.K;
   h.Pd = mode == F_FWD ? a.K : a.C;
-  if (h.HP > HPMAX || h.SC % 16 || h.Pd % 4) return false;
-  if (mode == F_FWD && a.in_scale && a.C > 512) return false;
+  if (h.HP > 288 || h.SC % 16 || h.Pd % 4) return false;
   if (mode == F_DGRAD && a.in_scale) return false;
   const long long lim = (1LL << 31) - 64;
   if ((long long)a.N * a.H * a.W * h.SC * 4 > lim || (long long)h.Pd * a.R * a.S * h.SC * 8 > lim) return false;
+  halo_layout(h);
+  if (h.HBYTES > HBLARGE || (h.HBYTES > HBSMALL && h.HP > 288) || (h.HBYTES <= HBSMALL && h.HP > 208)) return false;
   return true;
 }
 
-template <int MODE, int BP, int RS>
-int launch_x6h(ConvF32Args a, const HaloGeo& h, hipStream_t s) {
+template <int MODE, int BP, int RS, int HB>
+static int launch_x6h(ConvF32Args a, const HaloGeo& h, hipStream_t s) {
   const long long Pd = h.Pd, Qd = (long long)a.N * a.P * a.Q;
   const long long ntp = (Pd + BP - 1) / BP, ntq = (Qd + BQH - 1) / BQH;
   a.slots = (int)ntq;
@@ -372,7 +502,7 @@ int launch_x6h(ConvF32Args a, const HaloGeo& h, hipStream_t s) {
     if (!a.partial || need > a.partial_cap) return (int)hipErrorInvalidValue;
   }
   const dim3 grid((unsigned)(ntp * ntq), (unsigned)split, (unsigned)a.G);
-  hipLaunchKernelGGL((convx6h_kernel<MODE, BP, RS>), grid, dim3(256), 0, s, a, h);
+  hipLaunchKernelGGL((convx6h_kernel<MODE, BP, RS, HB>), grid, dim3(256), 0, s, a, h);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || split == 1) return (int)e;
   hipLaunchKernelGGL((convf32_splitk_epilogue<MODE, BP, BQH>), dim3((unsigned)(ntp * ntq), 1, a.G), dim3(256), 0,
@@ -380,13 +510,16 @@ int launch_x6h(ConvF32Args a, const HaloGeo& h, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-template <int MODE>
-int dispatch_x6h(const ConvF32Args& a, int bp, int rs, const HaloGeo& h, hipStream_t s) {
-  if (rs == 3) return bp == 128 ? launch_x6h<MODE, 128, 3>(a, h, s) : launch_x6h<MODE, 64, 3>(a, h, s);
-  return bp == 128 ? launch_x6h<MODE, 128, 1>(a, h, s) : launch_x6h<MODE, 64, 1>(a, h, s);
+template <int MODE, int HB>
+static int dispatch_hb(const ConvF32Args& a, int bp, int rs, const HaloGeo& h, hipStream_t s) {
+  if (rs == 3) return bp == 128 ? launch_x6h<MODE, 128, 3, HB>(a, h, s) : launch_x6h<MODE, 64, 3, HB>(a, h, s);
+  return bp == 128 ? launch_x6h<MODE, 128, 1, HB>(a, h, s) : launch_x6h<MODE, 64, 1, HB>(a, h, s);
 }
-
-}  // namespace
+template <int MODE>
+static int dispatch_x6h(const ConvF32Args& a, int bp, int rs, const HaloGeo& h, hipStream_t s) {
+  return h.HBYTES <= HBSMALL ? dispatch_hb<MODE, HBSMALL>(a, bp, rs, h, s)
+                             : dispatch_hb<MODE, HBLARGE>(a, bp, rs, h, s);
+}
 
 // Can the halo kernel run this (mode, geometry) with BP = (cfg & 0xff) * 16?
 DDL_API int ddl_x6h_ok(const ConvF32Args* ap, int mode, int cfg) {

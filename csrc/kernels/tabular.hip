@@ -177,7 +177,7 @@ __global__ __launch_bounds__(256) void bn1d_bwd_kernel(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ x,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
     float* __restrict__ dx, float* __restrict__ dgamma, float* __restrict__ dbeta, int M, int C,
-    int act, float slope) {
+    int act, float slope, int training) {
   __shared__ float red[8 * 32];
   const int c = blockIdx.x * 32 + (threadIdx.x & 31), rg = threadIdx.x >> 5;
   const bool ok = c < C;
@@ -203,21 +203,23 @@ __global__ __launch_bounds__(256) void bn1d_bwd_kernel(
     const long long o = (long long)m * C + c;
     const float g = dy[o] * act_grad_from_out(y[o], act, slope);
     const float xh = (x[o] - mu) * rs;
-    dx[o] = ga * rs * (g - s0 * invM - xh * s1 * invM);
+    // eval mode (running statistics): the normalisation is a fixed affine map
+    dx[o] = training ? ga * rs * (g - s0 * invM - xh * s1 * invM) : ga * rs * g;
   }
 }
 
 DDL_API int ddl_bn1d_bwd(const float* dy, const float* y, const float* x, const float* mean,
                          const float* rstd, const float* gamma, float* dx, float* dgamma,
-                         float* dbeta, int M, int C, int act, float slope, hipStream_t s) {
+                         float* dbeta, int M, int C, int act, float slope, int training, hipStream_t s) {
   hipLaunchKernelGGL(bn1d_bwd_kernel, dim3((C + 31) / 32), dim3(256), 0, s, dy, y, x, mean, rstd,
-                     gamma, dx, dgamma, dbeta, M, C, act, slope);
+                     gamma, dx, dgamma, dbeta, M, C, act, slope, training);
   return (int)hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
-// Softmax CE on fp32 logits [M][C] (C <= 64): one wave per row. targets: probabilities [M][C]
-// (the VFL float one-hot) or labels [M] (int). loss (fp32 scalar) += mean; dlogits = (p - t) / M
+// Softmax CE on fp32 logits [M][C]: one wave per row, each lane over columns lane, lane + 64, ...
+// targets: probabilities [M][C] (the VFL float one-hot) or labels [M] (int).
+// loss (fp32 scalar) += mean; dlogits = (p * sum(t) - t) / M
 __global__ __launch_bounds__(256) void ce_f32_kernel(const float* __restrict__ logits,
                                                      const float* __restrict__ targets,
                                                      const int* __restrict__ labels, int M, int C,
@@ -226,22 +228,34 @@ __global__ __launch_bounds__(256) void ce_f32_kernel(const float* __restrict__ l
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
-  const float v = lane < C ? logits[(long long)row * C + lane] : -INFINITY;
-  const float mx = wave_max(v);
-  const float e = lane < C ? __expf(v - mx) : 0.f;
-  const float se = wave_sum(e);
+  const float* lg = logits + (long long)row * C;
+  float mx = -INFINITY;
+  for (int c = lane; c < C; c += 64) mx = fmaxf(mx, lg[c]);
+  mx = wave_max(mx);
+  float se = 0.f, tsum = 0.f, tl = 0.f;
+  for (int c = lane; c < C; c += 64) {
+    const float v = lg[c];
+    se += __expf(v - mx);
+    const float t = targets ? targets[(long long)row * C + c] : (labels[row] == c ? 1.f : 0.f);
+    tsum += t;
+    tl += t * v;
+  }
+  se = wave_sum(se);
+  tsum = wave_sum(tsum);
+  tl = wave_sum(tl);
   const float lse = mx + __logf(se);
-  float t = 0.f;
-  if (lane < C) t = targets ? targets[(long long)row * C + lane] : (labels[row] == lane ? 1.f : 0.f);
-  const float l = wave_sum(lane < C ? t * (lse - v) : 0.f);
-  const float tsum = wave_sum(t);  // cross-lane ops stay outside divergent code
-  if (lane < C && dlogits) dlogits[(long long)row * C + lane] = (e / se * tsum - t) / (float)M;
-  if (lane == 0) atomicAdd(loss, l / (float)M);
+  if (dlogits) {
+    for (int c = lane; c < C; c += 64) {
+      const float t = targets ? targets[(long long)row * C + c] : (labels[row] == c ? 1.f : 0.f);
+      dlogits[(long long)row * C + c] = (__expf(lg[c] - mx) / se * tsum - t) / (float)M;
+    }
+  }
+  if (lane == 0) atomicAdd(loss, (tsum * lse - tl) / (float)M);
 }
 
 DDL_API int ddl_ce_f32(const float* logits, const float* targets, const int* labels, int M, int C,
                        float* loss, float* dlogits, hipStream_t s) {
-  if (C > 64) return (int)hipErrorInvalidValue;
+  if (C < 1) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(ce_f32_kernel, dim3((M + 3) / 4), dim3(256), 0, s, logits, targets, labels, M,
                      C, loss, dlogits);
   return (int)hipGetLastError();

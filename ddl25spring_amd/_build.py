@@ -56,6 +56,16 @@ def _jobs() -> int:
     return max(1, min(16, os.cpu_count() or 4))
 
 
+def _check_undefined(lib: Path) -> None:
+    """A kernel whose host stub was never emitted (e.g. a template in an anonymous namespace)
+    links fine and fails only at dlopen on the GPU box: refuse such a library here."""
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    res = subprocess.run([nm, "-u", "-D", str(lib)], capture_output=True, text=True)
+    bad = [ln.split()[-1] for ln in res.stdout.splitlines() if "__device_stub__" in ln]
+    if bad:
+        raise RuntimeError(f"{lib.name}: undefined kernel stubs (would fail at load): {bad[:5]}")
+
+
 def build_kernels(force: bool = False, verbose: bool = False) -> Path:
     srcs = sorted((CSRC / "kernels").glob("*.hip"))
     headers = list((CSRC / "include").glob("*.h"))
@@ -81,6 +91,7 @@ def build_kernels(force: bool = False, verbose: bool = False) -> Path:
             print(f"[build] link {KERNEL_LIB.name}", flush=True)
         tmp = KERNEL_LIB.with_suffix(".so.tmp")
         _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)])
+        _check_undefined(tmp)
         os.replace(tmp, KERNEL_LIB)
     return KERNEL_LIB
 

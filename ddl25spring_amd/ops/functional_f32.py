@@ -231,7 +231,9 @@ def _halo_plan(mode: int, geom) -> tuple[int, int]:
     16-channel chunks until ~TARGET_WG workgroups (each slice keeping >= 4 chunks)."""
     Pd, Qd, _, _ = _dims(mode, geom)
     SC = geom.C if mode == F_FWD else geom.K
-    bp = 128 if Pd > 64 else 64
+    # BP 128 where the channels allow, except 4x4 images: their 8-image halo (43 KiB) with a BP 128
+    # weight ring would leave one workgroup per CU
+    bp = 128 if Pd > 64 and geom.Q > 4 else 64
     tiles = -(-Pd // bp) * -(-Qd // 128) * geom.G
     nch = SC // 16
     split = 1
@@ -273,7 +275,7 @@ def _launch(a, mode: int, geom, device, split_k: int = 0, ws_role: str = "main")
     name = ("conv_fwd", "conv_dgrad", "conv_wgrad")[mode] + "_f32"
     if cfg & HALO_BIT:
         ws_buf = split_weights(a, mode, geom, device)
-        a.wsplit, a.ws_gs = ws_buf.data_ptr(), ws_buf.stride(0)
+        a.wsplit, a.ws_gs = ws_buf.data_ptr(), ws_buf.stride(0) * 4  # bytes
         check(lib.ddl_x6h(ctypes.byref(a), mode, cfg & ~HALO_BIT, stream()), name + "_halo")
         return
     check(lib.ddl_convf32(ctypes.byref(a), mode, cfg, stream()), name)

@@ -30,7 +30,7 @@ _lib.register_signatures({
     "ddl_gemm_f32": [ctypes.POINTER(GemmF32Args), vp],
     "ddl_bias_act_bwd": [vp, vp, vp, vp, i32, i32, i32, f32, vp],
     "ddl_bn1d_fwd": [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, i32, f32, vp],
-    "ddl_bn1d_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, vp],
+    "ddl_bn1d_bwd": [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, i32, vp],
     "ddl_ce_f32": [vp, vp, vp, i32, i32, vp, vp, vp],
     "ddl_reparam": [vp, vp, vp, vp, i64, u64, u64, vp],
 })
@@ -115,7 +115,7 @@ class _BN1dAct(torch.autograd.Function):
                                ptr(rstd), M, C, int(training), float(momentum), float(eps), act,
                                float(slope), stream()), "bn1d_fwd")
         ctx.save_for_backward(x2, y, mean, rstd, gamma)
-        ctx.act, ctx.slope = act, slope
+        ctx.act, ctx.slope, ctx.training = act, slope, int(bool(training))
         return y
 
     @staticmethod
@@ -127,7 +127,7 @@ class _BN1dAct(torch.autograd.Function):
         db = torch.zeros_like(dg)
         check(K().ddl_bn1d_bwd(ptr(dy.contiguous().float()), ptr(y), ptr(x2), ptr(mean), ptr(rstd),
                                ptr(gamma), ptr(dx), ptr(dg), ptr(db), M, C, ctx.act, ctx.slope,
-                               stream()), "bn1d_bwd")
+                               ctx.training, stream()), "bn1d_bwd")
         return dx, dg, db, None, None, None, None, None, None, None
 
 
@@ -137,9 +137,7 @@ def batch_norm1d_act(x, gamma, beta, running_mean, running_var, training, moment
     if not x.is_cuda:
         y = F.batch_norm(x, running_mean, running_var, gamma, beta, training, momentum, eps)
         return _act_torch(y, code, slope)
-    if not training:  # eval: an affine map per channel (autograd through torch is fine here)
-        y = (x - running_mean) * torch.rsqrt(running_var + eps) * gamma + beta
-        return _act_torch(y, code, slope)
+    # eval mode runs the same native kernels with the running statistics (fixed affine backward)
     return _BN1dAct.apply(x, gamma, beta, running_mean, running_var, training, momentum, eps,
                           code, slope)
 
@@ -167,7 +165,7 @@ class _CE(torch.autograd.Function):
 
 def cross_entropy(logits, target):
     """nn.CrossEntropyLoss (mean) with hard labels or probability targets (vfl.py:51,79)."""
-    if not logits.is_cuda or logits.shape[1] > 64:
+    if not logits.is_cuda:
         return F.cross_entropy(logits, target)
     return _CE.apply(logits, target)
 

@@ -24,7 +24,11 @@ def _run(nproc, args, d):
     cmd = [sys.executable, "-m", "ddl25spring_amd", "--device", "cpu"] + args
     res = launch(cmd, nproc, log_dir=d, timeout=240)
     logs = [open(os.path.join(d, f"out{r}.txt")).read() for r in range(nproc)]
-    assert res["returncode"] == 0, logs
+    if res["returncode"] != 0:
+        # the full log of every rank (the abort reason of a dead rank is usually at its end)
+        for r, lg in enumerate(logs):
+            sys.stderr.write(f"===== rank {r} =====\n{lg}\n")
+        raise AssertionError(f"launcher result {res}; rank logs on stderr")
     return logs
 
 

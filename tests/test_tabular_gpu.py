@@ -49,8 +49,28 @@ def test_bn1d(cuda, act):
     yc.backward(g.to(cuda)); yh.backward(g)
     for a, b in ((xc, xh), (gc, gh), (bc, bh)):
         assert _rel(a.grad, b.grad) < 1e-4
-    ye = TO.batch_norm1d_act(xc, gc, bc, rmc, rvc, False, act=act)
-    assert _rel(ye, TO.batch_norm1d_act(xh, gh, bh, rmh, rvh, False, act=act)) < 1e-5
+    # eval mode: the native kernels with the running statistics, forward AND backward
+    xc2, xh2 = _pair(x, cuda)
+    gc.grad = gh.grad = bc.grad = bh.grad = None
+    ye = TO.batch_norm1d_act(xc2, gc, bc, rmc, rvc, False, act=act)
+    yeh = TO.batch_norm1d_act(xh2, gh, bh, rmh, rvh, False, act=act)
+    assert _rel(ye, yeh) < 1e-5
+    ye.backward(g.to(cuda)); yeh.backward(g)
+    for a, b in ((xc2, xh2), (gc, gh), (bc, bh)):
+        assert _rel(a.grad, b.grad) < 1e-5
+
+
+@pytest.mark.parametrize("C", [2, 10, 64, 65, 100, 1000])
+def test_cross_entropy_any_width(cuda, C):
+    """No torch fallback above 64 classes: the native CE loops over columns."""
+    torch.manual_seed(3)
+    lg = torch.randn(37, C) * 2
+    for tgt in (F.softmax(torch.randn(37, C), 1), torch.randint(0, C, (37,))):
+        lc, lh = _pair(lg, cuda)
+        a, b = TO.cross_entropy(lc, tgt.to(cuda)), F.cross_entropy(lh, tgt)
+        assert abs(a.item() - b.item()) < 1e-5 * max(1.0, abs(b.item()))
+        a.backward(); b.backward()
+        assert _rel(lc.grad, lh.grad) < 1e-5
 
 
 def test_losses_and_reparam(cuda):
