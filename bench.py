@@ -10,8 +10,12 @@ each GPU is one client.
 
 Data: synthetic CIFAR-10-shaped uint8 images (learnable class templates), random-init weights.
 Precision (``--precision``, default fp32 = the reference's, lab/tutorial_1a/hfl_complete.py:39-80):
-  fp32 — activations, weights, gradients and BN in fp32 end to end on the exact-fp32 MFMA
-         (conv_f32.hip / bn_f32.hip); the step is bitwise deterministic, so the JSON line also
+  fp32 — activations, weights, gradients and BN in fp32 end to end (bn_f32.hip). The convs run
+         the X6 engine by default (``fp32_conv_math`` "auto"): every fp32 operand split exactly
+         into three bf16 pieces, the six piece products above one fp32 rounding on the bf16 MFMA
+         (conv_x6h.hip: halo-staged FWD / stride-1 DGRAD; conv_f32.hip: the rest), or the exact
+         fp32 MFMA where the tuner measured that faster; both meet the fp32 tolerances of
+         tests/test_fp32_gpu.py. The step is bitwise deterministic, so the JSON line also
          carries a sha256 of the final server weights (``w_global_sha256``);
   bf16 — bf16 MFMA operands / activations with fp32 master weights, grads, BN statistics and
          aggregation (conv_igemm.hip), the faster non-reference-precision mode.

@@ -34,6 +34,14 @@ constexpr int PSTR = 128;   // weight image bytes per row (16 channels x 8 B, 16
 constexpr int HBSMALL = 32768;  // halo image bytes, OW >= 8 (2 workgroups per CU at BP 128: 48 + 32 KiB)
 constexpr int HBLARGE = 45056;  // OW = 4 (8 image segments of 6 x 6 pixels)
 constexpr int NWB = 3;      // weight images in the LDS ring (DMA runs two steps ahead)
+// MFMA-chain length between IEEE adds: 1 = one tap (6 MFMAs), 0 = one 16-channel chunk (T x 6).
+// The bf16 MFMA's internal accumulation is biased (not round-to-nearest): chains of 54 left a
+// ~3e-6 relative SYSTEMATIC error in the conv outputs, which a BatchNorm backward's sums over
+// 16k pixels (sum dy: heavy cancellation) amplified to 1e-2 (scripts/debug_r18_grads.py: ResNet-18
+// layer1 bn1.bias / conv1.weight gradients vs float64). Chains of 6: every gradient <= 5e-6.
+#ifndef X6H_STEP_ADD
+#define X6H_STEP_ADD 1
+#endif
 // Out-of-range buffer offset: any per-step scalar offset added to it stays >= the descriptor's
 // num_records (< 2^31), so the load returns zeros without a per-step select.
 constexpr unsigned OOB = 0x80000000u;
@@ -220,9 +228,7 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
     boff[tj] = seg * hg.SEGB + ii * hg.ROWB + jj * HSTR + hh * 32;
   }
 
-  // acc: the running sums (IEEE adds); cacc: one 16-channel chunk's MFMA chains (T taps x 6 MFMAs
-  // accumulated inside the MFMA, whose internal accumulation is not round-to-nearest: bounded to
-  // T * 6 <= 54 steps — <= ~2e-6 relative — before each IEEE add into acc)
+  // acc: the running sums (IEEE adds); cacc: the MFMA chains between two adds (X6H_STEP_ADD)
   f16v acc[TI][TJ], cacc[TI][TJ];
 #pragma unroll
   for (int ti = 0; ti < TI; ++ti)
@@ -285,8 +291,7 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
     // (k + 2) % 3, whose last reader (step k - 1) is past the barrier. vmcnt counts in issue order
     // (DMA pieces and the halo register loads together): at the end of step k, step k + 1's pieces
     // must have landed while step k + 2's (UP) and — between issue (tap HT) and use (chunk end) —
-    // the next chunk's halo loads (NUH, +2 for the BN constants) may still fly.
-    constexpr int NHL = NUH + (XF_OK ? 2 : 0);
+    // the next chunk's halo loads (NUH, +2 for the BN constants with xf) may still fly.
     auto step_of = [&](int kk, int& c, int& tt) { c = kk / T; tt = kk - c * T; };
     {
       int c1_, t1_;
@@ -308,10 +313,13 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
           else if (more) wload((t + 2) % 3, cc + 1, t + 2 - T);
           if (t == HT && more) halo_load(cc + 1);
           compute(t % 3, t);
-          if (t == T - 1) flush();
+          if (X6H_STEP_ADD || t == T - 1) flush();
+          // (the BN-constant loads of the halo exist only with xf: the count must match exactly)
           if (!more && t + 2 >= T) wait_vm<0>();
-          else if (more && (t == HT || t == HT + 1) && HT + 1 < T - 1) wait_vm<UP + NHL>();
-          else wait_vm<UP>();
+          else if (more && (t == HT || t == HT + 1) && HT + 1 < T - 1) {
+            if (xf) wait_vm<UP + NUH + 2>();
+            else wait_vm<UP + NUH>();
+          } else wait_vm<UP>();
           cta_barrier();
           if (t == T - 1 && more) {  // chunk boundary: every wave is done with this chunk's halo
             halo_store(cc + 1);
@@ -332,12 +340,14 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
       const bool hl = t == HT && cc + 1 < cc1;
       if (hl) halo_load(cc + 1);
       compute(slot, t);
-      if (t == T - 1) flush();
+      if (X6H_STEP_ADD || t == T - 1) flush();
       // retire step k + 1's pieces (and, at the chunk's last tap, the halo loads)
       const bool halo_fly = (HT < T - 1) && cc + 1 < cc1 && (t == HT || t == HT + 1);
       if (!issue2) wait_vm<0>();
-      else if (halo_fly) wait_vm<UP + NHL>();
-      else wait_vm<UP>();
+      else if (halo_fly) {
+        if (xf) wait_vm<UP + NUH + 2>();
+        else wait_vm<UP + NUH>();
+      } else wait_vm<UP>();
       cta_barrier();
       if (t == T - 1 && k + 1 < k1) {  // chunk boundary: every wave is done with this chunk's halo
         halo_store(cc + 1);

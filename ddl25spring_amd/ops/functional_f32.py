@@ -126,14 +126,17 @@ def set_halo(on: bool) -> None:
         _PLANS.clear()
 
 
-def halo_ok(mode: int, g) -> bool:
-    """Mirror of conv_x6h.hip x6h_geo: can the halo kernel run this (mode, geometry)?"""
+def halo_ok(mode: int, g, auto: bool = False) -> bool:
+    """Mirror of conv_x6h.hip x6h_geo: can the halo kernel run this (mode, geometry)? ``auto``: is it
+    also the default choice there (explicit plans may pin it where it is not)?"""
     if mode not in (F_FWD, F_DGRAD) or g.stride != 1 or g.R != g.S or g.R not in (1, 3) or g.pad != (g.R - 1) // 2:
         return False
     if g.P != g.H or g.Q != g.W:
         return False
     OH, OW = g.P, g.Q
     if OW < 4 or OW > 128 or OW & (OW - 1):
+        return False
+    if auto and OW < 8:  # 8 images per tile: measured slower than conv_f32.hip (profiles/x6h_layers_r4.txt)
         return False
     TR = 128 // OW
     if TR <= OH:
@@ -208,7 +211,7 @@ def plan(mode: int, geom) -> tuple[int, int]:
     if p is not None:
         return p
     p = _OVERRIDE.get(key)
-    if p is None and _HALO[0] and _MATH[0] != "mfma32" and halo_ok(mode, geom):
+    if p is None and _HALO[0] and _MATH[0] != "mfma32" and halo_ok(mode, geom, auto=True):
         p = _halo_plan(mode, geom)
     if p is None:
         p = _tuned(mode, geom)

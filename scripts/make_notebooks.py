@@ -127,6 +127,171 @@ pd.DataFrame(rows)'''),
     ])
 
 
+# ------------------------------------------------------------------------------ tutorial 1a (template)
+def tutorial_1a_template():
+    """The exercise version of tutorial 1a: the reference template's nine `# TODO` cells
+    (lab/tutorial_1a/horizontal-federated-learning.ipynb) as stubs to fill
+    in, each checked against the framework's solution (compat.hfl_complete) once implemented."""
+    return notebook([
+        md("""
+# Tutorial 1a (exercise) — horizontal federated learning
+
+The exercise form of `tutorial_1a_horizontal_fl.ipynb`: the nine building blocks of FedSGD /
+FedAvg are left as `# TODO` stubs with the reference's names and signatures. Fill them in with
+plain PyTorch; the last cell runs every server whose pieces are implemented, compares the client
+split with the framework's solution (`ddl25spring_amd.compat.hfl_complete`, the client-batched
+native engine) and lists the pieces still missing. Data is the learnable MNIST-shaped stand-in
+unless `DDL_DATA_ROOT` holds MNIST.
+"""),
+        code(SETUP),
+        code("""import numpy as np
+import torch.nn.functional as F
+from torch.utils.data import DataLoader, Subset
+from ddl25spring_amd.compat import hfl_complete as solution
+from ddl25spring_amd.compat.hfl_complete import RunResult, configure
+from ddl25spring_amd.models.torch_ref import TorchMnistCnn as MnistCnn  # a plain nn.Module CNN
+if QUICK:
+    configure(n_train=2000, n_test=400)
+train_dataset, test_loader = solution.train_dataset, solution.test_loader
+device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+TODO = NotImplementedError"""),
+        md("## 1. The local epoch and the client split"),
+        code("""def train_epoch(model, loader, optimizer):
+    # TODO: model.train(); for every (x, y) batch moved to `device`: zero_grad, forward,
+    #       F.nll_loss, backward, optimizer.step()
+    raise TODO("train_epoch")
+
+
+def split(nr_clients, iid, seed):
+    # TODO: rng = np.random.default_rng(seed); IID: rng.permutation of all indices cut into
+    #       nr_clients parts; non-IID: sort by label, cut into 2 * nr_clients shards, shuffle the
+    #       shard ids, give every client two shards. Return [Subset(train_dataset, idx), ...]
+    raise TODO("split")"""),
+        md("## 2. Clients and servers"),
+        code("""class Client:
+    def __init__(self, client_data, batch_size):
+        self.model = MnistCnn().to(device)
+        self.generator = torch.Generator()
+        self.loader = DataLoader(client_data, batch_size=batch_size, shuffle=True, generator=self.generator)
+
+    def update(self, weights, seed):
+        raise NotImplementedError
+
+
+class Server:
+    def __init__(self, lr, batch_size, seed):
+        self.lr, self.batch_size, self.seed = lr, batch_size, seed
+        torch.manual_seed(seed)
+        self.model = MnistCnn().to(device)
+
+    def run(self, nr_rounds):
+        raise NotImplementedError
+
+    def test(self):
+        # TODO: eval mode, no_grad, one pass over test_loader, argmax, return 100 * correct / total
+        raise TODO("Server.test")
+
+
+class CentralizedServer(Server):
+    def __init__(self, lr, batch_size, seed):
+        super().__init__(lr, batch_size, seed)
+        self.optimizer = torch.optim.SGD(self.model.parameters(), lr=lr)
+        self.generator = torch.Generator()
+        self.loader = DataLoader(train_dataset, batch_size=batch_size, shuffle=True, generator=self.generator)
+
+    def run(self, nr_rounds):
+        # TODO: per round (one epoch): generator.manual_seed(seed + epoch + 1), train_epoch, then
+        #       append wall time, message count 0 and self.test() to
+        #       RunResult("Centralized", 1, 1, batch_size, 1, lr, seed)
+        raise TODO("CentralizedServer.run")
+
+
+class DecentralizedServer(Server):
+    def __init__(self, lr, batch_size, client_subsets, client_fraction, seed):
+        super().__init__(lr, batch_size, seed)
+        self.nr_clients = len(client_subsets)
+        self.client_fraction = client_fraction
+        self.client_sample_counts = [len(s) for s in client_subsets]
+        # TODO: self.nr_clients_per_round = max(1, round(client_fraction * nr_clients));
+        #       self.rng = np.random.default_rng(seed)
+        raise TODO("DecentralizedServer.__init__")
+
+
+class GradientClient(Client):
+    def __init__(self, client_data):
+        super().__init__(client_data, len(client_data))
+
+    def update(self, weights, seed):
+        # TODO: copy `weights` into the model, zero the grads, one full-batch forward/backward
+        #       (nll_loss), return [p.grad.detach().cpu().clone() for p in parameters]
+        raise TODO("GradientClient.update")
+
+
+class FedSgdGradientServer(DecentralizedServer):
+    def __init__(self, lr, client_subsets, client_fraction, seed):
+        super().__init__(lr, -1, client_subsets, client_fraction, seed)
+        self.clients = [GradientClient(s) for s in client_subsets]
+        self.optimizer = torch.optim.SGD(self.model.parameters(), lr=lr)
+
+    def run(self, nr_rounds):
+        # TODO: per round: sample K clients without replacement (self.rng), client seed
+        #       seed + idx + 1 + round * K, weight each client's gradients by n_k / sum(n_k), sum
+        #       them, set .grad and take one SGD step; message_count 2 * (round + 1) * K
+        raise TODO("FedSgdGradientServer.run")
+
+
+class WeightClient(Client):
+    def __init__(self, client_data, lr, batch_size, nr_epochs):
+        super().__init__(client_data, batch_size)
+        self.optimizer = torch.optim.SGD(self.model.parameters(), lr=lr)
+        self.nr_epochs = nr_epochs
+
+    def update(self, weights, seed):
+        # TODO: copy `weights` in, generator.manual_seed(seed), nr_epochs x train_epoch,
+        #       return [p.detach().cpu().clone() for p in parameters]
+        raise TODO("WeightClient.update")
+
+
+class FedAvgServer(DecentralizedServer):
+    def __init__(self, lr, batch_size, client_subsets, client_fraction, nr_local_epochs, seed):
+        super().__init__(lr, batch_size, client_subsets, client_fraction, seed)
+        self.clients = [WeightClient(s, lr, batch_size, nr_local_epochs) for s in client_subsets]
+        self.nr_local_epochs = nr_local_epochs
+
+    def run(self, nr_rounds):
+        # TODO: as FedSGD, but average the returned WEIGHTS (n_k-weighted) into the server model
+        raise TODO("FedAvgServer.run")"""),
+        md("## 3. Run what is implemented"),
+        code("""N, ROUNDS = (10, 1) if QUICK else (100, 5)
+status = []
+
+
+def attempt(name, fn):
+    try:
+        out = fn()
+        status.append((name, "implemented"))
+        return out
+    except NotImplementedError as e:
+        status.append((name, f"TODO ({e})"))
+        return None
+
+
+subsets = attempt("split", lambda: split(N, True, 42))
+ref = solution.split(N, True, 42)
+if subsets is not None:
+    assert [len(s) for s in subsets] == [len(s) for s in ref], "split: client sizes differ from the solution"
+else:
+    subsets = [Subset(train_dataset, list(s.indices)) for s in ref]
+for name, make in [("CentralizedServer", lambda: CentralizedServer(0.5, 1024, 42)),
+                   ("FedSgdGradientServer", lambda: FedSgdGradientServer(0.02, subsets, 0.2, 42)),
+                   ("FedAvgServer", lambda: FedAvgServer(0.02, 200, subsets, 0.2, 1, 42))]:
+    res = attempt(name, lambda: make().run(ROUNDS))
+    if res is not None:
+        print(name, "test accuracy per round:", res.test_accuracy)
+pd.DataFrame(status, columns=["piece", "status"])"""),
+    ])
+
+
 # ------------------------------------------------------------------------------ homework 1
 def homework_1():
     return notebook([
@@ -349,6 +514,7 @@ curve.iloc[[0, len(curve) // 2, -1]]'''),
 
 NOTEBOOKS = {
     "tutorial_1a_horizontal_fl.ipynb": tutorial_1a,
+    "tutorial_1a_horizontal_fl_template.ipynb": tutorial_1a_template,
     "homework_1.ipynb": homework_1,
     "lab_vfl.ipynb": lab_vfl,
     "homework_2.ipynb": homework_2,

@@ -20,7 +20,7 @@ GEOMS = [
     ConvGeom(G=2, N=5, H=32, W=32, C=64, K=64, R=3, S=3, stride=1, pad=1),    # 4 rows of one image
     ConvGeom(G=1, N=3, H=16, W=16, C=128, K=128, R=3, S=3, stride=1, pad=1),  # 8 rows
     ConvGeom(G=2, N=5, H=8, W=8, C=256, K=256, R=3, S=3, stride=1, pad=1),    # 2 images, partial tile
-    ConvGeom(G=1, N=11, H=4, W=4, C=512, K=192, R=3, S=3, stride=1, pad=1),   # 8 images, partial tile
+    ConvGeom(G=1, N=11, H=4, W=4, C=512, K=192, R=3, S=3, stride=1, pad=1),   # 8 images (explicit plan)
     ConvGeom(G=2, N=3, H=32, W=32, C=32, K=64, R=1, S=1, stride=1, pad=0),    # 1x1 (the im2col stem)
     ConvGeom(G=1, N=2, H=8, W=8, C=48, K=36, R=3, S=3, stride=1, pad=1),      # odd channel counts
 ]
@@ -170,3 +170,54 @@ def test_gram_blocked_k129(cuda):
     ref = (X.double() @ X.double().t()).cpu()
     _close(G1, ref)
     assert torch.equal(Fn.gram(X), G1)
+
+
+NET = [ConvGeom(G=2, N=16, H=h, W=h, C=c, K=c, R=3, S=3, stride=1, pad=1) for h, c in
+       ((32, 64), (16, 128), (8, 256), (4, 512))] + [ConvGeom(G=2, N=16, H=32, W=32, C=32, K=64, R=1, S=1, stride=1,
+                                                               pad=0)]
+
+
+@pytest.mark.parametrize("geom", NET, ids=[f"c{g.C}k{g.K}_{g.H}_r{g.R}" for g in NET])
+def test_x6h_network_shapes_auto_plan(cuda, geom):
+    """The ResNet-18 (CIFAR) stride-1 layers at a small batch with the DEFAULT plan (halo where
+    eligible, its split-K choice) and the fused epilogues the network uses together: FWD with
+    operand-side BN + statistics; DGRAD with residual + ReLU mask + the producer BN's reduce, and
+    with the recomputed-mask BN reduce. Run twice: bitwise equal."""
+    torch.manual_seed(5)
+    x = torch.randn(geom.G, geom.N, geom.H, geom.W, geom.C, device=cuda)
+    w = _weights(geom, cuda)
+    sc = torch.rand(geom.G, geom.C, device=cuda) + 0.5
+    sh = torch.randn(geom.G, geom.C, device=cuda) * 0.3
+    st = F32.SlotStats()
+    y = Fn.conv_fwd(x, w, geom, stats=st, in_bn=(sc, sh))
+    xa = (x.double() * sc.double()[:, None, None, None] + sh.double()[:, None, None, None]).clamp_min(0)
+    yr = ref_fwd(xa.cpu(), w.cpu(), geom)
+    _close(y, yr)
+    tot = st.t.double().cpu()[:, :, 0].sum(1)
+    _close(tot, yr.reshape(geom.G, -1, geom.K).sum(1))
+    st2 = F32.SlotStats()
+    assert torch.equal(Fn.conv_fwd(x, w, geom, stats=st2, in_bn=(sc, sh)), y) and torch.equal(st2.t, st.t)
+    if geom.R == 1:
+        return
+    dy = torch.randn(geom.G, geom.N, geom.P, geom.Q, geom.K, device=cuda)
+    dxr = ref_dgrad(dy.cpu(), w.cpu(), geom)
+    res = torch.randn(geom.G, geom.N, geom.H, geom.W, geom.C, device=cuda)
+    mask = torch.randn(geom.G, geom.N, geom.H, geom.W, geom.C, device=cuda)
+    bx = torch.randn(geom.G, geom.N, geom.H, geom.W, geom.C, device=cuda)
+    mean = torch.randn(geom.G, geom.C, device=cuda) * 0.1
+    rstd = torch.rand(geom.G, geom.C, device=cuda) + 0.5
+    d1, part = Fn.conv_dgrad(dy, w, geom, residual=res, mask=mask, bn=(bx, mean, rstd))
+    want = (dxr + res.cpu().double()) * (mask.cpu() > 0)
+    _close(d1, want)
+    b = lambda t: t.cpu().double()[:, None, None, None]  # noqa: E731
+    xhat = (bx.cpu().double() - b(mean)) * b(rstd)
+    p = part.double().cpu().sum(1)
+    _close(p[:, 0], want.sum((1, 2, 3)))
+    _close(p[:, 1], (want * xhat).sum((1, 2, 3)))
+    d1b, part_b = Fn.conv_dgrad(dy, w, geom, residual=res, mask=mask, bn=(bx, mean, rstd))
+    assert torch.equal(d1b, d1) and torch.equal(part_b, part)
+    sc2 = torch.rand(geom.G, geom.C, device=cuda) + 0.5
+    sh2 = torch.randn(geom.G, geom.C, device=cuda) * 0.2
+    d2, part2 = Fn.conv_dgrad(dy, w, geom, bn=(bx, mean, rstd), mask_bn=(sc2, sh2))
+    keep = (bx.cpu().double() * b(sc2) + b(sh2)) > 0
+    _close(d2, dxr * keep)
