@@ -29,25 +29,27 @@
 #include "conv_f32_core.h"
 
 constexpr int BQH = 128;    // output pixels per tile
-constexpr int HSTR = 144;   // halo image bytes per pixel: 16 channels x 8 B + 16 B pad (bank spread)
-constexpr int PSTR = 128;   // weight image bytes per row (16 channels x 8 B, 16-B granule XOR swizzle)
+// Operand images are PLANAR per 16-channel chunk: [h0..h15 | m0..m15 | l0..l15] (3 x 32 B), one
+// plane per bf16 piece of the exact split, padded to 7 x 16 B so consecutive rows / pixels rotate
+// over the 16 bank quads (7 is odd).
+constexpr int HSTR = 112;   // halo image bytes per pixel
+constexpr int PSTR = 112;   // weight image bytes per row
+constexpr int PQ = 7;       // quads per pixel / row
 constexpr int HBSMALL = 32768;  // halo image bytes, OW >= 8 (2 workgroups per CU at BP 128: 48 + 32 KiB)
 constexpr int HBLARGE = 45056;  // OW = 4 (8 image segments of 6 x 6 pixels)
 constexpr int NWB = 3;      // weight images in the LDS ring (DMA runs two steps ahead)
-// MFMA-chain length between IEEE adds: 1 = one tap (6 MFMAs), 0 = one 16-channel chunk (T x 6).
-// The bf16 MFMA's internal accumulation is biased (not round-to-nearest): chains of 54 left a
-// ~3e-6 relative SYSTEMATIC error in the conv outputs, which a BatchNorm backward's sums over
-// 16k pixels (sum dy: heavy cancellation) amplified to 1e-2 (scripts/debug_r18_grads.py: ResNet-18
-// layer1 bn1.bias / conv1.weight gradients vs float64). Chains of 6: every gradient <= 5e-6.
-#ifndef X6H_STEP_ADD
-#define X6H_STEP_ADD 1
-#endif
+// Precision note: the bf16 MFMA's internal accumulation is biased (not round-to-nearest). Long
+// chains into one accumulator (one per 16-channel chunk = 54 MFMAs) left a ~3e-6 relative
+// SYSTEMATIC error in the conv outputs, which a BatchNorm backward's sum over 16k pixels (heavy
+// cancellation) amplified to 1e-2 (scripts/debug_r18_grads.py, ResNet-18 layer1 bn1.bias). Here
+// each 16-channel step is one chain whose value is large for exactly one accumulation (hh last),
+// then one IEEE add — the rounding pattern of conv_f32.hip's X6 engine.
 // Out-of-range buffer offset: any per-step scalar offset added to it stays >= the descriptor's
 // num_records (< 2^31), so the load returns zeros without a per-step select.
 constexpr unsigned OOB = 0x80000000u;
 
 // Halo image layout: pixel (segment sg, row hi, col hj) at sg * SEGB + hi * ROWB + hj * HSTR bytes.
-// HSTR = 9 quads (16 B) per pixel spreads the pixels of one row over the 16 bank quads; ROWB and
+// HSTR = 7 quads (16 B) per pixel spreads the pixels of one row over the 16 bank quads; ROWB and
 // SEGB are padded (host: halo_layout) so that the 16 lanes of every ds_read_b128 group — which
 // span 1..8 output rows of the tile depending on OW — land on distinct bank quads (conflict-free
 // for OW = 4, 16, 32; one 2-way pair for OW = 8 inside the 32 KiB budget).
@@ -94,7 +96,7 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
   constexpr int UP = BP / 32;                // weight LDS-DMA pieces (1 KiB) per wave per step
   constexpr int HPM = HB == HBSMALL ? 208 : 288;   // halo pixel capacity (host-checked)
   constexpr int NUH = (HPM * 4 + 255) / 256;  // halo units (pixel x 4-channel chunk) per thread
-  constexpr int PIMG = BP * PSTR;            // bytes per weight image
+  constexpr int PIMG = BP * 128;             // bytes per weight image slot (BP * 112 used)
   constexpr bool XF_OK = MODE == F_FWD;
   __shared__ __attribute__((aligned(16))) char smem[NWB * PIMG + HB];
   char* const pimg = smem;
@@ -128,7 +130,7 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
   const __amdgpu_buffer_rsrc_t rS = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, (int)src_bytes, 0x00020000);
   const char* wsp = (const char*)a.wsplit + (long long)g * a.ws_gs;
   const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)wsp, 0, (int)((long long)Pd * T * SC * 8), 0x00020000);
+      (void*)wsp, 0, (int)((long long)Pd * T * SC * 6), 0x00020000);
 
   // ---------------------------------------------------------------- halo bookkeeping
   // unit i of this thread: halo pixel hp = uu >> 2, 4-channel chunk ch = uu & 3
@@ -151,7 +153,7 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
       const int sr = r0 + hi - PD, sc = hj - PD;
       if (n < a.N && (unsigned)sr < (unsigned)hg.SH && (unsigned)sc < (unsigned)hg.SW)
         hoff[i] = (unsigned)((((long long)n * hg.SH + sr) * hg.SW + sc) * SC + ch * 4) * 4u;
-      hlds[i] = seg * hg.SEGB + hi * hg.ROWB + hj * HSTR + ch * 32;
+      hlds[i] = seg * hg.SEGB + hi * hg.ROWB + hj * HSTR + ch * 8;
     }
   }
   float4 hreg[NUH];
@@ -182,68 +184,52 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
       }
       s4v h, m, l;
       split3(v, h, m, l);
-      *(s8v*)(himg + hlds[i]) = cat44(h, m);
-      *(s8v*)(himg + hlds[i] + 16) = cat44(l, h);
+      *(s4v*)(himg + hlds[i]) = h;
+      *(s4v*)(himg + hlds[i] + 32) = m;
+      *(s4v*)(himg + hlds[i] + 64) = l;
     }
   };
 
   // ---------------------------------------------------------------- weight (P operand) staging
   // LDS-DMA (buffer_load ... lds, 1 KiB per wave-instruction, lane-linear destination): piece i of
-  // wave wsc covers image bytes (wsc + 4 i) KiB = rows 8 (wsc + 4 i) .. +7; a lane fetches the
-  // logical granule that the XOR swizzle places at its destination (gl = physical ^ swizzle).
+  // wave wsc covers image bytes (wsc + 4 i) KiB, i.e. 16-B granule L = 64 (wsc + 4 i) + lane =
+  // row L / 7, granule L % 7 (6 = the pad: nothing to fetch). The global source (pre-split
+  // weights) holds the same 96 B per (row, tap, 16-channel chunk).
   const int wsc = __builtin_amdgcn_readfirstlane(wid);
   unsigned woff[UP];
 #pragma unroll
   for (int i = 0; i < UP; ++i) {
-    const int row = (wsc + 4 * i) * 8 + (lane >> 3);
-    const int gl = (lane & 7) ^ ((row >> 1) & 7);
+    const int L = (wsc + 4 * i) * 64 + lane;
+    const int row = L / PQ, gr = L - row * PQ;
     const int p = o.p0 + row;
-    woff[i] = p < Pd ? (unsigned)((long long)p * T * SC * 8 + gl * 16) : OOB;
+    woff[i] = (row < BP && gr < 6 && p < Pd) ? (unsigned)((long long)p * T * SC * 6 + gr * 16) : OOB;
   }
   auto wload = [&](int buf, int cc, int t) {
     const int wtap = MODE == F_FWD ? t : T - 1 - t;  // DGRAD: the flipped kernel
-    const unsigned add = (unsigned)(wtap * SC * 8 + cc * 128);  // wave-uniform: the scalar offset
+    const unsigned add = (unsigned)(wtap * SC * 6 + cc * 96);  // wave-uniform: the scalar offset
 #pragma unroll
     for (int i = 0; i < UP; ++i) dma16(rW, pimg + buf * PIMG + (wsc + 4 * i) * 1024, woff[i], add);
   };
 
   // ---------------------------------------------------------------- fragment addressing
-  const int hh = lane >> 5;  // lane half: reduction values 4 * hh .. of each 8-deep k-group
-  int aoff[TI][4];           // weight image byte offsets per (ti, granule pair index 2j + half)
+  const int hh = lane >> 5;  // lane half: channels 8 hh .. 8 hh + 7 of the 16-channel chunk
+  int aoff[TI];              // weight image byte offset of the h plane (m: +32, l: +64)
 #pragma unroll
-  for (int ti = 0; ti < TI; ++ti) {
-    const int row = wp * WP + ti * 32 + (lane & 31), sw = (row >> 1) & 7;
-#pragma unroll
-    for (int jh = 0; jh < 4; ++jh) {  // jh = 2 * j + half
-      const int gl = 4 * (jh >> 1) + 2 * hh + (jh & 1);
-      aoff[ti][jh] = row * PSTR + 16 * (gl ^ sw);
-    }
-  }
+  for (int ti = 0; ti < TI; ++ti) aoff[ti] = (wp * WP + ti * 32 + (lane & 31)) * PSTR + hh * 16;
   int boff[TJ];  // halo image byte offsets of tap (0, 0)
 #pragma unroll
   for (int tj = 0; tj < TJ; ++tj) {
     const int ql = wq * 64 + tj * 32 + (lane & 31);
     const int jj = ql & ((1 << hg.lgW) - 1), rowl = ql >> hg.lgW;
     const int seg = rowl / hg.SR, ii = rowl - seg * hg.SR;
-    boff[tj] = seg * hg.SEGB + ii * hg.ROWB + jj * HSTR + hh * 32;
+    boff[tj] = seg * hg.SEGB + ii * hg.ROWB + jj * HSTR + hh * 16;
   }
 
-  // acc: the running sums (IEEE adds); cacc: the MFMA chains between two adds (X6H_STEP_ADD)
-  f16v acc[TI][TJ], cacc[TI][TJ];
+  f16v acc[TI][TJ];  // running sums: one IEEE add per 16-channel step
 #pragma unroll
   for (int ti = 0; ti < TI; ++ti)
 #pragma unroll
-    for (int tj = 0; tj < TJ; ++tj) acc[ti][tj] = cacc[ti][tj] = (f16v){};
-  auto flush = [&]() {
-#pragma unroll
-    for (int ti = 0; ti < TI; ++ti)
-#pragma unroll
-      for (int tj = 0; tj < TJ; ++tj) {
-#pragma unroll
-        for (int v = 0; v < 16; ++v) acc[ti][tj][v] = acc[ti][tj][v] + cacc[ti][tj][v];
-        cacc[ti][tj] = (f16v){};
-      }
-  };
+    for (int tj = 0; tj < TJ; ++tj) acc[ti][tj] = (f16v){};
 
   const int k0 = cc0 * T, k1 = cc1 * T;
   constexpr int HT = T >= 3 ? T - 3 : 0;  // tap at which the next chunk's halo loads are issued
@@ -256,33 +242,38 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
   auto compute = [&](int buf, int t) {
     const char* P = pimg + buf * PIMG;
     const int dr = t / RS, ds = t - dr * RS;
-    s8v a_hm[TI][2], a_lh[TI][2], b_hm[TJ][2], b_lh[TJ][2];
+    // one 16-channel step: A (weights) and B (activations) as three piece vectors each; the six
+    // piece products in ONE chain, the five small ones first and hh last, so the chain's value is
+    // large for exactly one (biased, non-round-to-nearest) MFMA accumulation before the IEEE add
+    s8v ah[TI], am[TI], al[TI], bh[TJ], bm[TJ], bl[TJ];
 #pragma unroll
-    for (int ti = 0; ti < TI; ++ti)
+    for (int ti = 0; ti < TI; ++ti) {
+      ah[ti] = *(const s8v*)(P + aoff[ti]);
+      am[ti] = *(const s8v*)(P + aoff[ti] + 32);
+      al[ti] = *(const s8v*)(P + aoff[ti] + 64);
+    }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        a_hm[ti][j] = *(const s8v*)(P + aoff[ti][2 * j]);
-        a_lh[ti][j] = *(const s8v*)(P + aoff[ti][2 * j + 1]);
-      }
-#pragma unroll
-    for (int tj = 0; tj < TJ; ++tj)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const char* hb = himg + bdr[dr][tj] + ds * HSTR + j * 64;
-        b_hm[tj][j] = *(const s8v*)hb;
-        b_lh[tj][j] = *(const s8v*)(hb + 16);
-      }
+    for (int tj = 0; tj < TJ; ++tj) {
+      const char* hb = himg + bdr[dr][tj] + ds * HSTR;
+      bh[tj] = *(const s8v*)hb;
+      bm[tj] = *(const s8v*)(hb + 32);
+      bl[tj] = *(const s8v*)(hb + 64);
+    }
 #pragma unroll
     for (int ti = 0; ti < TI; ++ti)
 #pragma unroll
       for (int tj = 0; tj < TJ; ++tj) {
-        f16v c = cacc[ti][tj];
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_lh[ti][0], b_hm[tj][0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_hm[ti][0], b_lh[tj][0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_hm[ti][0], b_hm[tj][0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_lh[ti][1], b_hm[tj][1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_hm[ti][1], b_lh[tj][1], c, 0, 0, 0);
-        cacc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_hm[ti][1], b_hm[tj][1], c, 0, 0, 0);
+        f16v c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ti], bh[tj], (f16v){}, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ti], bl[tj], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[ti], bm[tj], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ti], bm[tj], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[ti], bh[tj], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ti], bh[tj], c, 0, 0, 0);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[ti][tj][v] = acc[ti][tj][v] + c[v];
+        // pin the adds to this step: otherwise they sink past the unrolled taps' barriers and
+        // every step's chain result lives (in scratch) until the end of the chunk
+        asm volatile("" : "+v"(acc[ti][tj]));
       }
   };
 
@@ -313,7 +304,9 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
           else if (more) wload((t + 2) % 3, cc + 1, t + 2 - T);
           if (t == HT && more) halo_load(cc + 1);
           compute(t % 3, t);
-          if (X6H_STEP_ADD || t == T - 1) flush();
+          // keep each step's MFMAs and adds inside the step: moved across the barrier into the next
+          // step they pile up two steps' operands and chains and spill
+          __builtin_amdgcn_sched_barrier(0);
           // (the BN-constant loads of the halo exist only with xf: the count must match exactly)
           if (!more && t + 2 >= T) wait_vm<0>();
           else if (more && (t == HT || t == HT + 1) && HT + 1 < T - 1) {
@@ -340,7 +333,6 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
       const bool hl = t == HT && cc + 1 < cc1;
       if (hl) halo_load(cc + 1);
       compute(slot, t);
-      if (X6H_STEP_ADD || t == T - 1) flush();
       // retire step k + 1's pieces (and, at the chunk's last tap, the halo loads)
       const bool halo_fly = (HT < T - 1) && cc + 1 < cc1 && (t == HT || t == HT + 1);
       if (!issue2) wait_vm<0>();
@@ -388,34 +380,42 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
   fepi<MODE, BP, BQH, Lay32<BP, BQH>>(a, o, quad, (float*)smem);
 }
 
-// Pre-split weights: FWD layout [G][K][T][C] (chunks of 4 input channels), DGRAD layout [G][C][T][K]
-// (chunks of 4 output channels), 8 bytes per element: per 4-chunk (h0..h3 | m0..m3)(l0..l3 | h0..h3).
+// Pre-split weights: FWD layout [G][K][T][C] (16-channel chunks of the input channels), DGRAD
+// layout [G][C][T][K] (16-channel chunks of the output channels), 6 bytes per element: per chunk
+// the three bf16 planes [h0..h15 | m0..m15 | l0..l15] (the LDS operand image row of conv_x6h).
 __global__ __launch_bounds__(256) void x6_split_weights_kernel(const float* __restrict__ w, char* out, int G, int K,
                                                                int T, int C, int layout, long long w_gs,
                                                                long long o_gs) {
-  const long long per = (long long)K * T * C / 4;  // 4-chunks per group
+  const long long per = (long long)K * T * C / 16;  // 16-chunks per group
   GSTRIDE_LOOP(t, (long long)G * per) {
     const long long g = t / per, e = t - g * per;
-    float4 v;
-    long long dst;
-    if (layout == 0) {  // element (k, tap, c..c+3): contiguous in w
-      v = *(const float4*)(w + g * w_gs + e * 4);
-      dst = e * 4;
-    } else {  // element (c, tap, k..k+3): w[k + i][tap][c]
-      const int K4 = K / 4;
-      const long long ct = e / K4;
-      const int k = (int)(e - ct * K4) * 4;
+    const float* wg = w + g * w_gs;
+    float v[16];
+    if (layout == 0) {  // chunk (k, tap, c..c+15): contiguous in w
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float4 f = *(const float4*)(wg + e * 16 + 4 * i);
+        v[4 * i] = f.x; v[4 * i + 1] = f.y; v[4 * i + 2] = f.z; v[4 * i + 3] = f.w;
+      }
+    } else {  // chunk (c, tap, k..k+15): w[k + i][tap][c]
+      const int K16 = K / 16;
+      const long long ct = e / K16;
+      const int k = (int)(e - ct * K16) * 16;
       const int c = (int)(ct / T), tap = (int)(ct - (long long)c * T);
-      const float* s = w + g * w_gs + ((long long)k * T + tap) * C + c;
+      const float* s = wg + ((long long)k * T + tap) * C + c;
       const long long ks = (long long)T * C;
-      v = make_float4(s[0], s[ks], s[2 * ks], s[3 * ks]);
-      dst = ((long long)c * T + tap) * K + k;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = s[i * ks];
     }
-    s4v h, m, l;
-    split3(v, h, m, l);
-    char* d = out + g * o_gs + dst * 8;
-    *(s8v*)d = cat44(h, m);
-    *(s8v*)(d + 16) = cat44(l, h);
+    char* d = out + g * o_gs + e * 96;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      s4v h, m, l;
+      split3(make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]), h, m, l);
+      *(s4v*)(d + 8 * q) = h;
+      *(s4v*)(d + 32 + 8 * q) = m;
+      *(s4v*)(d + 64 + 8 * q) = l;
+    }
   }
 }
 
@@ -428,7 +428,7 @@ static void halo_layout(HaloGeo& h) {
   const int OW = 1 << h.lgW, nseg = h.HP / (h.HR * h.HC);
   int best[4] = {1 << 30, 1 << 30, 0, 0};  // worst, total, rq, sq
   bool best_fit = false;
-  for (int rq = 9 * h.HC; rq < 9 * h.HC + 16; ++rq)
+  for (int rq = PQ * h.HC; rq < PQ * h.HC + 16; ++rq)
     for (int sq = h.HR * rq; sq < h.HR * rq + 16; ++sq) {
       int worst = 0, tot = 0;
       for (int hh = 0; hh < 2; ++hh)
@@ -437,7 +437,7 @@ static void halo_layout(HaloGeo& h) {
           for (int e = 0; e < 16; ++e) {
             const int q = grp[gi][e], row = q / OW, col = q % OW;
             const int seg = row / h.SR, ri = row % h.SR;
-            ++cnt[(seg * sq + ri * rq + 9 * col + 2 * hh) & 15];
+            ++cnt[(seg * sq + ri * rq + PQ * col + hh) & 15];
           }
           int m = 0;
           for (int c = 0; c < 16; ++c) m = cnt[c] > m ? cnt[c] : m;
@@ -494,7 +494,7 @@ static bool x6h_geo(const ConvF32Args& a, int mode, int bp, HaloGeo& h, int& rs)
   if (h.HP > 288 || h.SC % 16 || h.Pd % 4) return false;
   if (mode == F_DGRAD && a.in_scale) return false;
   const long long lim = (1LL << 31) - 64;
-  if ((long long)a.N * a.H * a.W * h.SC * 4 > lim || (long long)h.Pd * a.R * a.S * h.SC * 8 > lim) return false;
+  if ((long long)a.N * a.H * a.W * h.SC * 4 > lim || (long long)h.Pd * a.R * a.S * h.SC * 6 > lim) return false;
   halo_layout(h);
   if (h.HBYTES > HBLARGE || (h.HBYTES > HBSMALL && h.HP > 288) || (h.HBYTES <= HBSMALL && h.HP > 208)) return false;
   return true;
@@ -548,12 +548,12 @@ DDL_API int ddl_x6h(const ConvF32Args* ap, int mode, int cfg, hipStream_t s) {
   return mode == F_FWD ? dispatch_x6h<F_FWD>(a, bp, rs, h, s) : dispatch_x6h<F_DGRAD>(a, bp, rs, h, s);
 }
 
-// w [G][K][T][C] fp32 (group stride w_gs floats) -> out (group stride o_gs bytes, >= K*T*C*8)
+// w [G][K][T][C] fp32 (group stride w_gs floats) -> out (group stride o_gs bytes, >= K*T*C*6)
 DDL_API int ddl_x6_split_weights(const float* w, void* out, int G, int K, int T, int C, int layout,
                                  long long w_gs, long long o_gs, int pad_, hipStream_t s) {
   (void)pad_;
-  if (G < 1 || K < 1 || T < 1 || C < 1 || (layout == 0 ? C % 4 : K % 4) || (w_gs % 4)) return (int)hipErrorInvalidValue;
-  const long long work = (long long)G * K * T * C / 4;
+  if (G < 1 || K < 1 || T < 1 || C < 1 || (layout == 0 ? C % 16 : K % 16) || (w_gs % 4)) return (int)hipErrorInvalidValue;
+  const long long work = (long long)G * K * T * C / 16;
   hipLaunchKernelGGL(x6_split_weights_kernel, dim3(grid_for(work, 256)), dim3(256), 0, s, w, (char*)out, G, K, T,
                      C, layout, w_gs, o_gs);
   return (int)hipGetLastError();

@@ -278,20 +278,21 @@ def _launch(a, mode: int, geom, device, split_k: int = 0, ws_role: str = "main")
     name = ("conv_fwd", "conv_dgrad", "conv_wgrad")[mode] + "_f32"
     if cfg & HALO_BIT:
         ws_buf = split_weights(a, mode, geom, device)
-        a.wsplit, a.ws_gs = ws_buf.data_ptr(), ws_buf.stride(0) * 4  # bytes
+        a.wsplit, a.ws_gs = ws_buf.data_ptr(), ws_buf.stride(0)  # bytes
         check(lib.ddl_x6h(ctypes.byref(a), mode, cfg & ~HALO_BIT, stream()), name + "_halo")
         return
     check(lib.ddl_convf32(ctypes.byref(a), mode, cfg, stream()), name)
 
 
 def split_weights(a, mode: int, geom, device) -> torch.Tensor:
-    """The X6 operand image of the launch's weights (8 bytes per element): FWD layout [G][K][R][S][C],
-    DGRAD layout [G][C][R][S][K]. Rebuilt from the fp32 weights for every launch (the fused-SGD
-    WGRAD updates them in place), into a stream-ordered temporary."""
+    """The X6 operand image of the launch's weights (6 bytes per element: three bf16 planes per 16
+    channels): FWD layout [G][K][R][S][C], DGRAD layout [G][C][R][S][K]. Rebuilt from the fp32
+    weights for every launch (the fused-SGD WGRAD updates them in place), into a stream-ordered
+    temporary."""
     T = geom.R * geom.S
-    out = torch.empty(geom.G, geom.K * T * geom.C * 2, dtype=torch.float32, device=device)
+    out = torch.empty(geom.G, geom.K * T * geom.C * 6, dtype=torch.uint8, device=device)
     check(_lib.kernels().ddl_x6_split_weights(a.w, out.data_ptr(), geom.G, geom.K, T, geom.C, 0 if mode == F_FWD else 1,
-                                              a.w_gs, out.stride(0) * 4, 0, stream()), "x6_split_weights")
+                                              a.w_gs, out.stride(0), 0, stream()), "x6_split_weights")
     return out
 
 

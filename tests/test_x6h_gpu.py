@@ -116,21 +116,19 @@ def test_x6h_dgrad(cuda, geom, split):
 
 
 def test_x6h_split_weights(cuda):
-    """The pre-split weight image reconstructs the fp32 weights exactly (h + m + l == w)."""
-    from ddl25spring_amd.ops import _lib
+    """The pre-split weight image reconstructs the fp32 weights exactly (h + m + l == w): per
+    16-channel chunk three bf16 planes [h0..h15 | m0..m15 | l0..l15]."""
     g = ConvGeom(G=2, N=1, H=8, W=8, C=32, K=48, R=3, S=3, stride=1, pad=1)
     w = _weights(g, cuda)
     a = F32._args(g, w=w.data_ptr(), w_gs=w.stride(0))
     for mode in (F32.F_FWD, F32.F_DGRAD):
         img = F32.split_weights(a, mode, g, cuda)
         torch.cuda.synchronize()
-        raw = img.view(torch.int16).view(g.G, -1, 2, 8)  # per 4-chunk: (h0..h3 m0..m3)(l0..l3 h0..h3)
-        bf = lambda t: (t.to(torch.int32) << 16).view(torch.float32)  # noqa: E731
-        h, m, l_ = raw[:, :, 0, :4], raw[:, :, 0, 4:], raw[:, :, 1, :4]
-        assert torch.equal(raw[:, :, 1, 4:], h)
-        rec = (bf(h).double() + bf(m).double() + bf(l_).double()).reshape(g.G, -1)
+        planes = img.view(torch.int16).view(g.G, -1, 3, 16)
+        bf = lambda t: (t.to(torch.int32) << 16).view(torch.float32).double()  # noqa: E731
+        rec = (bf(planes[:, :, 0]) + bf(planes[:, :, 1]) + bf(planes[:, :, 2])).reshape(g.G, -1)
         want = w if mode == F32.F_FWD else w.permute(0, 4, 2, 3, 1)  # DGRAD: [G][C][R][S][K]
-        assert torch.equal(rec, want.reshape(g.G, -1).double()), _lib
+        assert torch.equal(rec, want.reshape(g.G, -1).double())
 
 
 def test_split_workspace_capture(cuda):
