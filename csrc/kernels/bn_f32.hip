@@ -375,6 +375,8 @@ struct BNFBwdArgs {  // same layout as BNBwdArgs (batchnorm.hip) + the slot coun
   float* dx;
   long long gs_param;
   int slots;
+  int pad0_;
+  double* fold_ws;  // two-level fold: per-slot-block partials [S / FB_SB][2][C] (null: one-level fold)
 };
 
 __device__ __forceinline__ void bnf_fold_body(const BNFBwdArgs& t, long long M, int C, double* red) {
@@ -402,6 +404,82 @@ __device__ __forceinline__ void bnf_fold_body(const BNFBwdArgs& t, long long M, 
 __global__ __launch_bounds__(FOLD_T) void bnf_fold_kernel(BNFBwdArgs a, BNFBwdArgs b, long long M, int C) {
   __shared__ double red[NSG * 64];
   bnf_fold_body(blockIdx.z ? b : a, M, C, red);
+}
+
+// Two-level fixed-order fold for many slots (the fp32 step at 8 clients: S = 800 per BN). Level 1:
+// 256-thread blocks (8 slot streams x 32 channels) each reduce FB_SB consecutive slots, all 2 x 8
+// loads of a thread in flight at once, into a double partial per block; level 2 adds the partials in
+// block order and derives the coefficients. Both levels are small blocks that fit beside the
+// side-stream WGRAD's resident workgroups (the one-level fold's 1024-thread blocks waited for a
+// whole CU to drain: ~100 us per fold inside the overlapped backward).
+constexpr int FB_SG = 8, FB_SB = 64;
+
+__global__ __launch_bounds__(256) void bnf_fold_part_kernel(BNFBwdArgs a, BNFBwdArgs b, int C, int nb) {
+  const BNFBwdArgs& t = blockIdx.z ? b : a;
+  __shared__ double red[FB_SG * 64];
+  const int g = blockIdx.y, cg = blockIdx.x / nb, sb = blockIdx.x - cg * nb;
+  const int sg = threadIdx.x >> 5, cl = threadIdx.x & 31, c = cg * 32 + cl;
+  const int S = t.slots;
+  const float* base = t.part + (long long)g * S * 2 * C;
+  constexpr int PER = FB_SB / FB_SG;
+  float x0[PER], x1[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int k = sb * FB_SB + sg + j * FB_SG;
+    const bool ok = c < C && k < S;
+    x0[j] = ok ? base[(long long)k * 2 * C + c] : 0.f;
+    x1[j] = ok ? base[(long long)k * 2 * C + C + c] : 0.f;
+  }
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    a0 += x0[j];
+    a1 += x1[j];
+  }
+  red[sg * 64 + cl] = a0;
+  red[sg * 64 + 32 + cl] = a1;
+  __syncthreads();
+  if (sg == 0 && c < C) {
+    double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < FB_SG; ++k) {
+      t0 += red[k * 64 + cl];
+      t1 += red[k * 64 + 32 + cl];
+    }
+    double* w = t.fold_ws + ((long long)g * nb + sb) * 2 * C;
+    w[c] = t0;
+    w[C + c] = t1;
+  }
+}
+
+__global__ __launch_bounds__(256) void bnf_fold_fin_kernel(BNFBwdArgs a, BNFBwdArgs b, long long M, int C, int nb) {
+  const BNFBwdArgs& t = blockIdx.z ? b : a;
+  const int g = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double s0 = 0.0, s1 = 0.0;
+  const double* w = t.fold_ws + (long long)g * nb * 2 * C;
+  for (int k = 0; k < nb; ++k) {
+    s0 += w[(long long)k * 2 * C + c];
+    s1 += w[(long long)k * 2 * C + C + c];
+  }
+  const int i = g * C + c;
+  const long long po = (long long)g * t.gs_param + c;
+  const float mu = t.mean[i], rs = t.rstd[i];
+  const float ga = t.gamma ? t.gamma[po] : 1.f;
+  if (t.dbeta) t.dbeta[po] = t.dbeta[po] + (float)s0;
+  if (t.dgamma) t.dgamma[po] = t.dgamma[po] + (float)s1;
+  const double invM = 1.0 / (double)M;
+  const double A = (double)ga * rs;
+  const double B = -A * rs * s1 * invM;
+  t.coef[(long long)g * 3 * C + c] = (float)A;
+  t.coef[(long long)g * 3 * C + C + c] = (float)B;
+  t.coef[(long long)g * 3 * C + 2 * C + c] = (float)(-A * s0 * invM - B * mu);
+}
+
+// doubles of fold workspace a BN backward with S slots needs (two-level fold)
+DDL_API long long ddl_bnf_fold_ws(int S, int C, int G) {
+  const int nb = (S + FB_SB - 1) / FB_SB;
+  return (long long)G * nb * 2 * C;
 }
 
 __global__ __launch_bounds__(256) void bnf_bwd_apply_kernel(
@@ -477,7 +555,15 @@ DDL_API int ddl_bnf_backward(const float* dy, const float* ymask, const BNFBwdAr
   if (a.slots < 1 || (bp && bp->slots < 1)) return (int)hipErrorInvalidValue;
   const int two = bp ? 1 : 0;
   const BNFBwdArgs b = bp ? *bp : a;
-  hipLaunchKernelGGL(bnf_fold_kernel, dim3((C + 31) / 32, G, 1 + two), dim3(FOLD_T), 0, s, a, b, M, C);
+  if (a.fold_ws && (!two || b.fold_ws)) {
+    // one grid for both BNs: nb of the larger; blocks past a BN's own slots add exact zeros
+    const int sm = two && b.slots > a.slots ? b.slots : a.slots;
+    const int nb = (sm + FB_SB - 1) / FB_SB;
+    hipLaunchKernelGGL(bnf_fold_part_kernel, dim3((C + 31) / 32 * nb, G, 1 + two), dim3(256), 0, s, a, b, C, nb);
+    hipLaunchKernelGGL(bnf_fold_fin_kernel, dim3((C + 255) / 256, G, 1 + two), dim3(256), 0, s, a, b, M, C, nb);
+  } else {
+    hipLaunchKernelGGL(bnf_fold_kernel, dim3((C + 31) / 32, G, 1 + two), dim3(FOLD_T), 0, s, a, b, M, C);
+  }
   const int RPI = 256 / f_tpr(C);
   hipLaunchKernelGGL(bnf_bwd_apply_kernel, dim3(fstream_blocks(M, RPI, G, 4), G), dim3(256), 0, s, dy, ymask, a, b,
                      two, dym_out, M, C);

@@ -83,7 +83,8 @@ class ConvF32Args(ctypes.Structure):  # conv_f32.hip
 
 class BNFBwdArgs(ctypes.Structure):  # bn_f32.hip
     _fields_ = [("x", vp), ("mean", vp), ("rstd", vp), ("gamma", vp), ("dgamma", vp), ("dbeta", vp),
-                ("part", vp), ("coef", vp), ("dx", vp), ("gs_param", i64), ("slots", i32)]
+                ("part", vp), ("coef", vp), ("dx", vp), ("gs_param", i64), ("slots", i32), ("pad0_", i32),
+                ("fold_ws", vp)]
 
 
 class HeadFArgs(ctypes.Structure):  # bn_f32.hip
@@ -190,9 +191,10 @@ _SIGS.update({
     "ddl_avgpoolf_bwd_bn": [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp],
     "ddl_headf_train": [ctypes.POINTER(HeadFArgs), vp],
     "ddl_bnf_channel_sum": [vp, vp, i64, vp, i64, i32, i32, vp],
+    "ddl_bnf_fold_ws": [i32, i32, i32],
 })
 _RESTYPES = {"ddl_convf32_slots": ctypes.c_longlong, "ddl_convf32_workspace": ctypes.c_longlong,
-             "ddl_x6h_workspace": ctypes.c_longlong,
+             "ddl_x6h_workspace": ctypes.c_longlong, "ddl_bnf_fold_ws": ctypes.c_longlong,
              "ddl_gram_f32_workspace": ctypes.c_longlong}
 
 _OPTIONAL_SIGS: dict[str, list] = {}

@@ -436,7 +436,8 @@ def bn_stats(x):
     return st
 
 
-def _bwd_args(x, mean, rstd, gamma, dgamma, dbeta, part, dx):
+def _bwd_args(x, mean, rstd, gamma, dgamma, dbeta, part, dx, fold_slots: int = 0):
+    """fold_slots: size the two-level fold's workspace for this many slots (0: part's own)."""
     G, C = x.shape[0], x.shape[-1]
     t = _lib.BNFBwdArgs()
     coef = ws.scratch((G, 3, C), x.device)
@@ -448,8 +449,17 @@ def _bwd_args(x, mean, rstd, gamma, dgamma, dbeta, part, dx):
     t.x, t.mean, t.rstd, t.gamma = ptr(x), ptr(mean), ptr(rstd), ptr(gamma)
     t.dgamma, t.dbeta, t.part, t.coef, t.dx, t.gs_param = ptr(dgamma), ptr(dbeta), ptr(part), ptr(coef), ptr(dx), gs
     t.slots = part.shape[1] if part is not None else 0
-    t._keep = coef  # the scratch must outlive the launch (its memory would be reused otherwise)
+    S = max(fold_slots, t.slots)
+    fws = None
+    if FOLD2[0] and S > 0:
+        fws = torch.empty(int(_lib.kernels().ddl_bnf_fold_ws(S, C, G)), dtype=torch.float64, device=x.device)
+        t.fold_ws = fws.data_ptr()
+    t._keep = (coef, fws)  # scratch that must outlive the launch (its memory would be reused otherwise)
     return t
+
+
+# BN-backward coefficient fold: two small-block levels (DDL_F32_FOLD2=0: the one-level fold)
+FOLD2 = [os.environ.get("DDL_F32_FOLD2", "1") != "0"]
 
 
 def bn_backward(dy, ymask, x, mean, rstd, gamma, dgamma=None, dbeta=None, emit_dym=False, part=None):
@@ -474,9 +484,10 @@ def bn_backward2(dy, bn_a, bn_b):
     M = xa[0].numel() // C
     assert bn_b[0].shape == xa.shape and dy.is_contiguous()
     outs, args = [], []
+    smax = max(bn_a[6].shape[1], bn_b[6].shape[1])
     for x, mean, rstd, gamma, dgamma, dbeta, part in (bn_a, bn_b):
         dx = torch.empty_like(x)
-        args.append(_bwd_args(x, mean, rstd, gamma, dgamma, dbeta, part, dx))
+        args.append(_bwd_args(x, mean, rstd, gamma, dgamma, dbeta, part, dx, fold_slots=smax))
         outs.append(dx)
     check(_lib.kernels().ddl_bnf_backward(ptr(dy), None, ctypes.byref(args[0]), ctypes.byref(args[1]), None, M, C,
                                           G, 0, stream()), "bn_backward2_f32")
