@@ -145,6 +145,10 @@ def main():
                        "client_slots_per_gpu": fl.slots, "hip_graphs": not args.no_graph,
                        "fp32_conv_math": F32.math() if args.precision == "fp32" else None},
         }
+        if ctx.world > 1:  # which all-reduce path the round's weight reduce took (runtime/dist.py policy)
+            wb = fl.w_global.numel() * 4
+            out["allreduce"] = {"weights_bytes": wb, "path": rdist.allreduce_path(ctx, wb),
+                                "backend": ctx.backend, **ctx.ipc_policy}
         if acc is not None:
             out["test_accuracy"] = acc
         print(json.dumps(out), flush=True)

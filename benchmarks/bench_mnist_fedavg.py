@@ -12,7 +12,10 @@ B=100, lr=0.01, seed 10; 600 samples per client).
 
 Synthetic MNIST-shaped uint8 images (learnable class templates), random init.
 
-    python benchmarks/bench_mnist_fedavg.py --variant native --steps 10 --warmup 2
+    python benchmarks/bench_mnist_fedavg.py --variant native --steps 10 --warmup 2 [--precision bf16]
+
+The native variant defaults to fp32 (the reference's precision); ``--precision bf16`` is the
+labelled faster mode.
 """
 from __future__ import annotations
 
@@ -34,7 +37,9 @@ def run_native(args, ctx):
     from ddl25spring_amd.models import mnist_cnn
     train = synthetic_images("mnist", args.train_size, seed=0)
     parts = split(args.clients, True, 10, labels=train.labels)
-    fl = FedAvg(mnist_cnn, DeviceImageDataset(train, ctx.device), parts, lr=args.lr,
+    def model(groups=1):
+        return mnist_cnn(groups, precision=args.precision)
+    fl = FedAvg(model, DeviceImageDataset(train, ctx.device), parts, lr=args.lr,
                 batch_size=args.batch, local_epochs=args.epochs, client_fraction=args.fraction,
                 seed=10, eval_every=0)
     for _ in range(args.warmup):
@@ -127,6 +132,8 @@ def main():
     ap.add_argument("--epochs", type=int, default=1)
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--train-size", type=int, default=60000)
+    ap.add_argument("--precision", choices=("fp32", "bf16"), default="fp32",
+                    help="native variant: fp32 = the reference's precision (default), bf16 = bf16 MFMA")
     args = ap.parse_args()
     from ddl25spring_amd.runtime import dist as rdist
     ctx = rdist.init()
@@ -136,7 +143,7 @@ def main():
     emit(ctx, metric=METRIC, variant=args.variant, value=round(samples / dt, 1), unit="samples/s",
          rounds_per_sec=round(args.steps / dt, 3), n_gpus=ctx.world, steps=args.steps,
          warmup=args.warmup, ms_per_step=round(1e3 * dt / args.steps, 3), higher_is_better=True,
-         dtype="bf16" if args.variant == "native" else "fp32", data="synthetic",
+         dtype=args.precision if args.variant == "native" else "fp32", data="synthetic",
          config={"model": "mnist_cnn", "clients": args.clients, "client_fraction": args.fraction,
                  "local_batch": args.batch, "local_epochs": args.epochs, "lr": args.lr})
     rdist.shutdown()

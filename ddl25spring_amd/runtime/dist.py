@@ -29,7 +29,8 @@ class DistContext:
     backend: str = "none"
     groups: dict = field(default_factory=dict)
     ipc: object = None          # runtime.ipc.IpcAllReduce (peer-read all-reduce) when enabled
-    ipc_max_bytes: int = 0
+    ipc_max_bytes: int = 0      # SUM all-reduces of fp32 tensors up to this size take the peer-read path
+    ipc_policy: dict = field(default_factory=dict)  # how ipc_max_bytes was chosen (probe table)
 
     @property
     def is_distributed(self) -> bool:
@@ -154,14 +155,85 @@ def init(backend: str | None = None, device: str | None = None, rank: int | None
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
     _CTX = DistContext(rank, world, local, dev, backend if (world > 1 or forced) else "none",
                        forced_pg=forced)
-    # peer-read all-reduce for small messages (runtime/ipc.py): one node, RCCL backend, opt-in
-    # until measured against RCCL on a multi-GPU node (benchmarks/bench_comm.py)
-    if (world > 1 and backend == "nccl" and os.environ.get("DDL_IPC_ALLREDUCE", "0") == "1"
+    # peer-read all-reduce for small messages (runtime/ipc.py): one node, RCCL
+    # backend. DDL_IPC_ALLREDUCE: "auto" (default) probes both paths once here and keeps the
+    # peer-read kernel below the measured crossover; "1" forces it up to DDL_IPC_MAX_BYTES; "0" off.
+    mode = os.environ.get("DDL_IPC_ALLREDUCE", "auto")
+    if (world > 1 and backend == "nccl" and mode != "0"
             and int(os.environ.get("LOCAL_WORLD_SIZE", world)) == world and world <= 8):
-        from .ipc import IpcAllReduce
-        _CTX.ipc_max_bytes = int(os.environ.get("DDL_IPC_MAX_BYTES", str(8 << 20)))
-        _CTX.ipc = IpcAllReduce(rank, world, dev, capacity=_CTX.ipc_max_bytes)
+        cap = int(os.environ.get("DDL_IPC_MAX_BYTES", str(8 << 20)))
+        try:
+            from .ipc import IpcAllReduce
+            _CTX.ipc = IpcAllReduce(rank, world, dev, capacity=cap)
+            _CTX.ipc_max_bytes = cap
+            _CTX.ipc_policy = {"mode": "forced", "ipc_threshold_bytes": cap}
+        except Exception as e:  # no peer mapping on this node: RCCL for everything
+            _CTX.ipc, _CTX.ipc_max_bytes = None, 0
+            _CTX.ipc_policy = {"mode": mode, "ipc_threshold_bytes": 0, "error": str(e)[:200]}
+        if _CTX.ipc is not None and mode == "auto":
+            probe_ipc_threshold(_CTX)
     return _CTX
+
+
+PROBE_SIZES = (16 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20, 8 << 20)
+
+
+def probe_ipc_threshold(ctx: DistContext, sizes=PROBE_SIZES, iters: int = 5) -> int:
+    """Time the peer-read all-reduce against the process group's all-reduce (RCCL) at each size on
+    every rank, take the slowest rank per (path, size) and keep the peer-read path up to the largest
+    size below which it always won. Sets ctx.ipc_max_bytes / ctx.ipc_policy (identical on every
+    rank: the decision is made on all-reduced timings) and releases the peer buffers when the
+    crossover is 0. Returns the threshold in bytes."""
+    sizes = [s for s in sizes if s <= ctx.ipc.cap]
+    dev = ctx.device
+    times = torch.zeros(2, len(sizes), dtype=torch.float64, device=dev)
+    try:
+        for j, nb in enumerate(sizes):
+            x = torch.ones(nb // 4, dtype=torch.float32, device=dev)
+            for path in (0, 1):
+                run = (lambda: ctx.ipc.all_reduce(x)) if path == 0 else (lambda: dist.all_reduce(x))
+                for _ in range(2):
+                    run()
+                torch.cuda.synchronize(dev)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(iters):
+                    run()
+                e1.record()
+                e1.synchronize()
+                times[path, j] = e0.elapsed_time(e1) / iters
+        ctx.ipc.check()
+        ok = True
+    except Exception as e:  # a peer timed out / the kernel refused: RCCL for everything
+        ok = False
+        err = str(e)[:200]
+    flag = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    dist.all_reduce(times, op=dist.ReduceOp.MAX)
+    thr = 0
+    if flag.item() == 0.0:
+        for j, nb in enumerate(sizes):
+            if times[0, j] < times[1, j]:
+                thr = nb
+            else:
+                break
+    ctx.ipc_max_bytes = thr
+    ctx.ipc_policy = {"mode": "auto", "ipc_threshold_bytes": thr,
+                      "probe_ms": {str(nb): {"ipc": round(float(times[0, j]), 4), "rccl": round(float(times[1, j]), 4)}
+                                   for j, nb in enumerate(sizes)}}
+    if flag.item() != 0.0:
+        ctx.ipc_policy["error"] = err if not ok else "a peer failed the probe"
+    if thr == 0:
+        ctx.ipc.close()
+        ctx.ipc = None
+    return thr
+
+
+def allreduce_path(ctx: DistContext, nbytes: int) -> str:
+    """Which path a SUM all-reduce of ``nbytes`` fp32 takes under the context's policy."""
+    if not ctx.is_distributed:
+        return "none"
+    return "ipc" if ctx.ipc is not None and nbytes <= ctx.ipc_max_bytes else ctx.backend
 
 
 def context() -> DistContext:

@@ -79,3 +79,42 @@ def test_ipc_allreduce_matches_sum(cuda, world, two_shot_bytes):
         assert torch.equal(outs[r]["graph"], torch.full((4099,), tot))
         for i, t in enumerate(outs[r]["b2b"]):
             assert torch.equal(t, torch.full((777 + 64 * i,), tot * (i + 1))), (r, i)
+
+
+def _policy_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from ddl25spring_amd.runtime import dist as rdist
+    from ddl25spring_amd.runtime.ipc import IpcAllReduce
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    ctx = rdist.DistContext(rank, world, rank, dev, "gloo")
+    ctx.ipc = IpcAllReduce(rank, world, dev, capacity=1 << 20, nblocks=8, timeout_s=10.0)
+    thr = rdist.probe_ipc_threshold(ctx, sizes=(16 << 10, 256 << 10, 1 << 20), iters=2)
+    x = torch.full((50000,), float(rank + 1), device=dev)  # 200 KB: either path, per the policy
+    ctx.all_reduce(x)
+    torch.save({"thr": thr, "policy": ctx.ipc_policy, "x": x.cpu(),
+                "path": rdist.allreduce_path(ctx, x.numel() * 4)}, os.path.join(out, f"p{rank}.pt"))
+    dist.barrier()
+    if ctx.ipc is not None:
+        ctx.ipc.close()
+    dist.destroy_process_group()
+
+
+def test_ipc_threshold_probe_agrees_across_ranks(cuda):
+    """The peer-read vs process-group all-reduce crossover probe (runtime/dist.py): every rank
+    takes the same decision from the all-reduced timings, and the policy's all_reduce sums
+    correctly on whichever path it chose (2 ranks sharing the GPU; gloo stands in for RCCL)."""
+    from ddl25spring_amd.runtime.launch import free_port
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_policy_worker, args=(world, free_port(), d), nprocs=world, join=True,
+                           start_method="spawn")
+        res = [torch.load(os.path.join(d, f"p{r}.pt"), weights_only=True) for r in range(world)]
+    assert res[0]["thr"] == res[1]["thr"] and res[0]["thr"] in (0, 16 << 10, 256 << 10, 1 << 20)
+    assert res[0]["policy"]["probe_ms"] == res[1]["policy"]["probe_ms"]
+    for r in res:
+        assert torch.equal(r["x"], torch.full((50000,), 3.0))
+        assert r["path"] == ("ipc" if r["thr"] >= 200000 else "gloo")
