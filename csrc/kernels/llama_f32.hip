@@ -1,0 +1,685 @@
+// Reference-precision (fp32) kernels of the tiny-LLaMA path (reference lab/tutorial_1b: simplellm
+// LLama trained in fp32 — stock modules, Adam, no autocast, intro_PP_1F1B_MB.py:16-46,
+// intro_DP_GA.py:16-31). The projections, FFN and LM head run as 1x1 convolutions on the X6 /
+// exact-fp32 conv engine (conv_f32.hip); this file holds the rest of the block, fp32 in and out:
+//
+//   ddl_embf_fwd / bwd    row gather; the backward is DETERMINISTIC: one wave per vocabulary row
+//                         scans the token ids (staged in LDS) and adds the matching dY rows in token
+//                         order (no float atomics; untouched rows are not written)
+//   ddl_rmsf_fwd / bwd    one wave per row (rstd saved); d(gamma) partials per block, folded in a
+//                         fixed block order by ddl_rmsf_fold (accumulates into the grad)
+//   ddl_swiglu_f32_*      h = silu(a) * b over the fused [a | b] projection
+//   ddl_attnf_fwd         causal attention with interleaved RoPE applied as K / Q are staged; four
+//                         lanes per query row split the head dimension (dot products finish with
+//                         two DPP quad exchanges), online softmax in the exp2 domain, log2-sum-exp
+//                         saved
+//   ddl_attnf_bwd_dq      recomputes P from the saved lse; delta = rowsum(dO * O) computed here
+//   ddl_attnf_bwd_dkdv    one workgroup per 64 keys sweeps the later query tiles (no atomics);
+//                         both backward kernels write the un-rotated gradients straight into the
+//                         fused dQKV buffer
+//   ddl_cevf_rows / fold  vocabulary cross-entropy: per-row loss + d(logits) at unit scale from
+//                         one block per row, row losses folded in a fixed order
+//   ddl_scale_f32         x *= *g unless *g == 1 (device scalar: no host sync)
+#include "ddl_common.h"
+
+// ---------------------------------------------------------------------------------------------
+// sum over the 4 lanes of a quad (DPP quad_perm, no LDS traffic); every lane gets the same bits
+__device__ __forceinline__ float quad_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));  // [1,0,3,2]
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true));  // [2,3,0,1]
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// embedding
+__global__ void embf_fwd_kernel(const int* __restrict__ idx, const float* __restrict__ w,
+                                float* __restrict__ y, int T, int D) {
+  const long long n = (long long)T * D;
+  GSTRIDE_LOOP(e, n) {
+    const int t = (int)(e / D), d = (int)(e - (long long)t * D);
+    y[e] = w[(long long)idx[t] * D + d];
+  }
+}
+
+// Block = 4 waves x EMB_RPW vocabulary rows each; the token ids go through LDS in chunks.
+constexpr int EMB_RPW = 4, EMB_CHUNK = 4096, EMB_MAXK = 16;  // D <= 64 * EMB_MAXK
+__global__ __launch_bounds__(256) void embf_bwd_kernel(const int* __restrict__ idx,
+                                                       const float* __restrict__ dy,
+                                                       float* __restrict__ dw, int T, int D, int V,
+                                                       int pad_idx) {
+  __shared__ int sid[EMB_CHUNK];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int v0 = (blockIdx.x * 4 + wv) * EMB_RPW;
+  float acc[EMB_RPW][EMB_MAXK];
+  bool hit[EMB_RPW];
+#pragma unroll
+  for (int r = 0; r < EMB_RPW; ++r) {
+    hit[r] = false;
+#pragma unroll
+    for (int k = 0; k < EMB_MAXK; ++k) acc[r][k] = 0.f;
+  }
+  const int nk = (D + 63) / 64;
+  for (int c0 = 0; c0 < T; c0 += EMB_CHUNK) {
+    const int cn = min(EMB_CHUNK, T - c0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < cn; i += 256) sid[i] = idx[c0 + i];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < EMB_RPW; ++r) {
+      const int v = v0 + r;
+      if (v >= V || v == pad_idx) continue;
+      for (int i0 = 0; i0 < cn; i0 += 64) {
+        const int i = i0 + lane;
+        unsigned long long m = __ballot(i < cn && sid[i] == v);
+        while (m) {
+          const int t = c0 + i0 + __builtin_ctzll(m);
+          m &= m - 1;
+          hit[r] = true;
+          const float* src = dy + (long long)t * D;
+#pragma unroll
+          for (int k = 0; k < EMB_MAXK; ++k)
+            if (k < nk && lane + 64 * k < D) acc[r][k] += src[lane + 64 * k];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < EMB_RPW; ++r) {
+    const int v = v0 + r;
+    if (!hit[r] || v >= V) continue;
+    float* dst = dw + (long long)v * D;
+#pragma unroll
+    for (int k = 0; k < EMB_MAXK; ++k)
+      if (k < nk && lane + 64 * k < D) dst[lane + 64 * k] += acc[r][k];
+  }
+}
+
+DDL_API int ddl_embf_fwd(const int* idx, const float* w, float* y, int T, int D, hipStream_t s) {
+  if (T < 1 || D < 1) return 0;
+  hipLaunchKernelGGL(embf_fwd_kernel, dim3(grid_for((long long)T * D, 256)), dim3(256), 0, s, idx, w, y, T, D);
+  return (int)hipGetLastError();
+}
+
+DDL_API int ddl_embf_bwd(const int* idx, const float* dy, float* dw, int T, int D, int V, int pad_idx,
+                         hipStream_t s) {
+  if (D > 64 * EMB_MAXK || D < 1) return (int)hipErrorInvalidValue;
+  if (T < 1) return 0;
+  const int rows_per_block = 4 * EMB_RPW;
+  hipLaunchKernelGGL(embf_bwd_kernel, dim3((V + rows_per_block - 1) / rows_per_block), dim3(256), 0, s, idx, dy,
+                     dw, T, D, V, pad_idx);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// RMSNorm: y = x * rstd * g, rstd = 1 / sqrt(mean(x^2) + eps). One wave per row; a lane keeps its
+// float4 slices of the row in registers (D % 4 == 0, D <= 256 * RMS_MAXV).
+constexpr int RMS_MAXV = 8;
+__global__ __launch_bounds__(256) void rmsf_fwd_kernel(const float* __restrict__ x, const float* __restrict__ g,
+                                                       float* __restrict__ y, float* __restrict__ rstd, int T,
+                                                       int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= T) return;
+  const int D4 = D / 4;
+  const float4* xr = (const float4*)(x + (long long)row * D);
+  float4 v[RMS_MAXV];
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < RMS_MAXV; ++k) {
+    const int c = lane + 64 * k;
+    v[k] = c < D4 ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+  }
+  ss = wave_sum(ss);
+  const float r = 1.f / sqrtf(ss / (float)D + eps);
+  if (lane == 0) rstd[row] = r;
+  float4* yr = (float4*)(y + (long long)row * D);
+  const float4* g4 = (const float4*)g;
+#pragma unroll
+  for (int k = 0; k < RMS_MAXV; ++k) {
+    const int c = lane + 64 * k;
+    if (c < D4) {
+      const float4 gg = g4[c];
+      yr[c] = make_float4(v[k].x * r * gg.x, v[k].y * r * gg.y, v[k].z * r * gg.z, v[k].w * r * gg.w);
+    }
+  }
+}
+
+// dx = r*g*dy - x * r^3 * sum(g*dy*x) / D (+ dres);  part[block][d] = sum over the block's rows of
+// dy*x*r (fixed row order per wave, waves combined in a fixed order).
+__global__ __launch_bounds__(256) void rmsf_bwd_kernel(const float* __restrict__ x, const float* __restrict__ g,
+                                                       const float* __restrict__ rstd,
+                                                       const float* __restrict__ dy,
+                                                       const float* __restrict__ dres, float* __restrict__ dx,
+                                                       float* __restrict__ part, int T, int D, int rows_per_block) {
+  __shared__ float4 sdg[4][64 * RMS_MAXV];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int D4 = D / 4;
+  const float4* g4 = (const float4*)g;
+  float4 dg[RMS_MAXV], gg[RMS_MAXV];
+#pragma unroll
+  for (int k = 0; k < RMS_MAXV; ++k) {
+    const int c = lane + 64 * k;
+    dg[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    gg[k] = c < D4 ? g4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(T, r0 + rows_per_block);
+  for (int row = r0 + wv; row < r1; row += 4) {
+    const float4* xr = (const float4*)(x + (long long)row * D);
+    const float4* dr = (const float4*)(dy + (long long)row * D);
+    const float r = rstd[row];
+    float4 xv[RMS_MAXV], dv[RMS_MAXV];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < RMS_MAXV; ++k) {
+      const int c = lane + 64 * k;
+      xv[k] = c < D4 ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+      dv[k] = c < D4 ? dr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+      s += gg[k].x * dv[k].x * xv[k].x + gg[k].y * dv[k].y * xv[k].y + gg[k].z * dv[k].z * xv[k].z +
+           gg[k].w * dv[k].w * xv[k].w;
+    }
+    s = wave_sum(s);
+    const float c3 = r * r * r * s / (float)D;
+    float4* out = (float4*)(dx + (long long)row * D);
+    const float4* rs = dres ? (const float4*)(dres + (long long)row * D) : nullptr;
+#pragma unroll
+    for (int k = 0; k < RMS_MAXV; ++k) {
+      const int c = lane + 64 * k;
+      if (c >= D4) continue;
+      float4 o = make_float4(r * gg[k].x * dv[k].x - xv[k].x * c3, r * gg[k].y * dv[k].y - xv[k].y * c3,
+                             r * gg[k].z * dv[k].z - xv[k].z * c3, r * gg[k].w * dv[k].w - xv[k].w * c3);
+      if (rs) {
+        const float4 q = rs[c];
+        o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+      }
+      out[c] = o;
+      dg[k].x += dv[k].x * xv[k].x * r; dg[k].y += dv[k].y * xv[k].y * r;
+      dg[k].z += dv[k].z * xv[k].z * r; dg[k].w += dv[k].w * xv[k].w * r;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < RMS_MAXV; ++k) sdg[wv][lane + 64 * k] = dg[k];
+  __syncthreads();
+  float4* p = (float4*)(part + (long long)blockIdx.x * D);
+  for (int c = threadIdx.x; c < D4; c += 256) {
+    float4 a = sdg[0][c];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+      const float4 b = sdg[w][c];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    p[c] = a;
+  }
+}
+
+__global__ void rmsf_fold_kernel(const float* __restrict__ part, float* __restrict__ dg, int nb, int D,
+                                 int accumulate) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= D) return;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += part[(long long)b * D + d];
+  dg[d] = accumulate ? dg[d] + s : s;
+}
+
+DDL_API int ddl_rmsf_fwd(const float* x, const float* g, float* y, float* rstd, int T, int D, float eps,
+                         hipStream_t s) {
+  if (D % 4 || D > 256 * RMS_MAXV) return (int)hipErrorInvalidValue;
+  if (T < 1) return 0;
+  hipLaunchKernelGGL(rmsf_fwd_kernel, dim3((T + 3) / 4), dim3(256), 0, s, x, g, y, rstd, T, D, eps);
+  return (int)hipGetLastError();
+}
+
+// blocks of the backward grid for T rows (the d(gamma) partial buffer holds nb x D floats)
+DDL_API int ddl_rmsf_blocks(int T) {
+  const int rpb = T <= 1024 ? 4 : ((T + 255) / 256 + 3) / 4 * 4;
+  return (T + rpb - 1) / rpb;
+}
+
+DDL_API int ddl_rmsf_bwd(const float* x, const float* g, const float* rstd, const float* dy, const float* dres,
+                         float* dx, float* part, float* dg, int accumulate, int T, int D, hipStream_t s) {
+  if (D % 4 || D > 256 * RMS_MAXV) return (int)hipErrorInvalidValue;
+  if (T < 1) return 0;
+  const int nb = ddl_rmsf_blocks(T);
+  const int rpb = (T + nb - 1) / nb;
+  hipLaunchKernelGGL(rmsf_bwd_kernel, dim3(nb), dim3(256), 0, s, x, g, rstd, dy, dres, dx, part, T, D, rpb);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !dg) return (int)e;
+  hipLaunchKernelGGL(rmsf_fold_kernel, dim3((D + 255) / 256), dim3(256), 0, s, part, dg, nb, D, accumulate);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// SwiGLU over ab [T][2F] = [a | b]  ->  h [T][F]
+__device__ __forceinline__ float sigm(float a) { return 1.f / (1.f + expf(-a)); }
+
+__global__ void swiglu_f32_fwd_kernel(const float* __restrict__ ab, float* __restrict__ h, int T, int F) {
+  const long long n = (long long)T * F;
+  GSTRIDE_LOOP(e, n) {
+    const long long t = e / F, f = e - t * F;
+    const float a = ab[t * 2 * F + f], b = ab[t * 2 * F + F + f];
+    h[e] = a * sigm(a) * b;
+  }
+}
+
+__global__ void swiglu_f32_bwd_kernel(const float* __restrict__ ab, const float* __restrict__ dh,
+                                      float* __restrict__ dab, int T, int F) {
+  const long long n = (long long)T * F;
+  GSTRIDE_LOOP(e, n) {
+    const long long t = e / F, f = e - t * F;
+    const float a = ab[t * 2 * F + f], b = ab[t * 2 * F + F + f], d = dh[e];
+    const float sg = sigm(a), si = a * sg;
+    dab[t * 2 * F + f] = d * b * sg * (1.f + a * (1.f - sg));
+    dab[t * 2 * F + F + f] = d * si;
+  }
+}
+
+DDL_API int ddl_swiglu_f32_fwd(const float* ab, float* h, int T, int F, hipStream_t s) {
+  if (T < 1 || F < 1) return 0;
+  hipLaunchKernelGGL(swiglu_f32_fwd_kernel, dim3(grid_for((long long)T * F, 256)), dim3(256), 0, s, ab, h, T, F);
+  return (int)hipGetLastError();
+}
+
+DDL_API int ddl_swiglu_f32_bwd(const float* ab, const float* dh, float* dab, int T, int F, hipStream_t s) {
+  if (T < 1 || F < 1) return 0;
+  hipLaunchKernelGGL(swiglu_f32_bwd_kernel, dim3(grid_for((long long)T * F, 256)), dim3(256), 0, s, ab, dh, dab,
+                     T, F);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Causal attention, fp32. qkv [B][S][3][H][HD], o / dO [B][S][H][HD], lse / delta [B][H][S]
+// (lse in the log2 domain of the scaled scores), cos / sin [S][HD/2] (interleaved pairs).
+// A workgroup owns 64 rows of one (b, h); lane quad (4 consecutive lanes) owns one row, lane
+// j of the quad the head dims [j*DPT, (j+1)*DPT), DPT = HD / 4 (even: whole RoPE pairs, and a
+// multiple of 4: float4 loads). The other side of each product is staged 64 rows at a time in LDS
+// (RoPE applied while staging) and read by all quads of a wave at the same row: a broadcast.
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr int ATT_R = 64;
+
+template <int DPT>
+__device__ __forceinline__ void load_slice(const float* p, float (&v)[DPT]) {
+#pragma unroll
+  for (int m = 0; m < DPT; m += 4) {
+    const float4 f = *(const float4*)(p + m);
+    v[m] = f.x; v[m + 1] = f.y; v[m + 2] = f.z; v[m + 3] = f.w;
+  }
+}
+template <int DPT>
+__device__ __forceinline__ void store_slice(float* p, const float (&v)[DPT]) {
+#pragma unroll
+  for (int m = 0; m < DPT; m += 4) *(float4*)(p + m) = make_float4(v[m], v[m + 1], v[m + 2], v[m + 3]);
+}
+// rotate dims d0.. of a row at position pos in place (dir = +1 forward, -1 inverse: the gradient)
+template <int DPT>
+__device__ __forceinline__ void rope_slice(float (&v)[DPT], const float* cs, const float* sn, int d0, int dir) {
+#pragma unroll
+  for (int m = 0; m < DPT; m += 2) {
+    const float c = cs[(d0 + m) >> 1], s = dir * sn[(d0 + m) >> 1];
+    const float a = v[m], b = v[m + 1];
+    v[m] = a * c - b * s;
+    v[m + 1] = a * s + b * c;
+  }
+}
+
+// Stage rows r0..r0+63 of one (b, h) into LDS img[64][HD] (rows >= S zero), optionally rotated.
+template <int HD>
+__device__ __forceinline__ void stage_rows(float* img, const float* base, long long rstride, int r0, int S,
+                                           const float* cosb, const float* sinb, bool rope) {
+  constexpr int N4 = ATT_R * HD / 4;
+  for (int e = threadIdx.x; e < N4; e += 256) {
+    const int r = e / (HD / 4), d = (e - r * (HD / 4)) * 4;
+    const int row = r0 + r;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row < S) {
+      v = *(const float4*)(base + row * rstride + d);
+      if (rope) {
+        const float* cs = cosb + (long long)row * (HD / 2) + d / 2;
+        const float* sn = sinb + (long long)row * (HD / 2) + d / 2;
+        const float a0 = v.x * cs[0] - v.y * sn[0], a1 = v.x * sn[0] + v.y * cs[0];
+        const float b0 = v.z * cs[1] - v.w * sn[1], b1 = v.z * sn[1] + v.w * cs[1];
+        v = make_float4(a0, a1, b0, b1);
+      }
+    }
+    *(float4*)(img + r * HD + d) = v;
+  }
+}
+
+template <int HD>
+__device__ __forceinline__ float dot_lds(const float (&q)[HD / 4], const float* row) {
+  float s = 0.f;
+#pragma unroll
+  for (int m = 0; m < HD / 4; m += 4) {
+    const float4 k = *(const float4*)(row + m);
+    s += q[m] * k.x + q[m + 1] * k.y + q[m + 2] * k.z + q[m + 3] * k.w;
+  }
+  return quad_sum(s);
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void attnf_fwd_kernel(const float* __restrict__ qkv, float* __restrict__ o,
+                                                        float* __restrict__ lse, const float* __restrict__ cosb,
+                                                        const float* __restrict__ sinb, int S, int H,
+                                                        float sl2) {
+  constexpr int DPT = HD / 4;
+  __shared__ float Ks[ATT_R * HD], Vs[ATT_R * HD];
+  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int qr = threadIdx.x >> 2, part = threadIdx.x & 3, d0 = part * DPT;
+  const int i = qb * ATT_R + qr;
+  const long long rs = 3LL * H * HD;  // qkv row stride
+  const float* qbase = qkv + (long long)b * S * rs + (long long)h * HD;
+  const float* kbase = qbase + (long long)H * HD;
+  const float* vbase = qbase + 2LL * H * HD;
+  float q[DPT], acc[DPT];
+#pragma unroll
+  for (int m = 0; m < DPT; ++m) acc[m] = 0.f;
+  const int iq = min(i, S - 1);
+  load_slice<DPT>(qbase + iq * rs + d0, q);
+  rope_slice<DPT>(q, cosb + (long long)iq * (HD / 2), sinb + (long long)iq * (HD / 2), d0, 1);
+  float mx = -INFINITY, l = 0.f;
+  for (int kt = 0; kt <= qb; ++kt) {
+    __syncthreads();
+    stage_rows<HD>(Ks, kbase, rs, kt * ATT_R, S, cosb, sinb, true);
+    stage_rows<HD>(Vs, vbase, rs, kt * ATT_R, S, cosb, sinb, false);
+    __syncthreads();
+    float sc[ATT_R];
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < ATT_R; ++j) {
+      const int key = kt * ATT_R + j;
+      const float d = dot_lds<HD>(q, Ks + j * HD + d0) * sl2;
+      sc[j] = (key <= i && key < S) ? d : -INFINITY;
+      tmax = fmaxf(tmax, sc[j]);
+    }
+    const float nm = fmaxf(mx, tmax);
+    if (nm == -INFINITY) continue;  // row fully masked in this tile (padding rows only)
+    const float corr = exp2f(mx - nm);
+    l *= corr;
+#pragma unroll
+    for (int m = 0; m < DPT; ++m) acc[m] *= corr;
+#pragma unroll
+    for (int j = 0; j < ATT_R; ++j) {
+      const float p = exp2f(sc[j] - nm);
+      l += p;
+      const float* vr = Vs + j * HD + d0;
+#pragma unroll
+      for (int m = 0; m < DPT; m += 4) {
+        const float4 v = *(const float4*)(vr + m);
+        acc[m] += p * v.x; acc[m + 1] += p * v.y; acc[m + 2] += p * v.z; acc[m + 3] += p * v.w;
+      }
+    }
+    mx = nm;
+  }
+  if (i >= S) return;
+  const float inv = 1.f / l;
+#pragma unroll
+  for (int m = 0; m < DPT; ++m) acc[m] *= inv;
+  store_slice<DPT>(o + ((long long)(b * S + i) * H + h) * HD + d0, acc);
+  if (part == 0) lse[((long long)b * H + h) * S + i] = mx + log2f(l);
+}
+
+// dQ (and delta): per query row, over the key tiles 0..qb
+template <int HD>
+__global__ __launch_bounds__(256) void attnf_bwd_dq_kernel(const float* __restrict__ qkv, const float* __restrict__ o,
+                                                           const float* __restrict__ dout,
+                                                           const float* __restrict__ lse, float* __restrict__ delta,
+                                                           float* __restrict__ dqkv, const float* __restrict__ cosb,
+                                                           const float* __restrict__ sinb, int S, int H, float sl2,
+                                                           float scale) {
+  constexpr int DPT = HD / 4;
+  __shared__ float Ks[ATT_R * HD], Vs[ATT_R * HD];
+  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int qr = threadIdx.x >> 2, part = threadIdx.x & 3, d0 = part * DPT;
+  const int i = qb * ATT_R + qr, iq = min(i, S - 1);
+  const long long rs = 3LL * H * HD;
+  const float* qbase = qkv + (long long)b * S * rs + (long long)h * HD;
+  const float* kbase = qbase + (long long)H * HD;
+  const float* vbase = qbase + 2LL * H * HD;
+  const long long orow = ((long long)(b * S + iq) * H + h) * HD + d0;
+  float q[DPT], dO[DPT], ov[DPT], dq[DPT];
+  load_slice<DPT>(qbase + iq * rs + d0, q);
+  rope_slice<DPT>(q, cosb + (long long)iq * (HD / 2), sinb + (long long)iq * (HD / 2), d0, 1);
+  load_slice<DPT>(dout + orow, dO);
+  load_slice<DPT>(o + orow, ov);
+  float dl = 0.f;
+#pragma unroll
+  for (int m = 0; m < DPT; ++m) {
+    dl += dO[m] * ov[m];
+    dq[m] = 0.f;
+  }
+  dl = quad_sum(dl);
+  const long long li = ((long long)b * H + h) * S + iq;
+  const float L = lse[li];
+  if (part == 0 && i < S) delta[li] = dl;
+  for (int kt = 0; kt <= qb; ++kt) {
+    __syncthreads();
+    stage_rows<HD>(Ks, kbase, rs, kt * ATT_R, S, cosb, sinb, true);
+    stage_rows<HD>(Vs, vbase, rs, kt * ATT_R, S, cosb, sinb, false);
+    __syncthreads();
+#pragma unroll 4
+    for (int j = 0; j < ATT_R; ++j) {
+      const int key = kt * ATT_R + j;
+      const float* kr = Ks + j * HD + d0;
+      const float s = dot_lds<HD>(q, kr) * sl2;
+      const float dp = dot_lds<HD>(dO, Vs + j * HD + d0);
+      const float p = (key <= i && key < S) ? exp2f(s - L) : 0.f;
+      const float ds = p * (dp - dl);
+#pragma unroll
+      for (int m = 0; m < DPT; m += 4) {
+        const float4 k = *(const float4*)(kr + m);
+        dq[m] += ds * k.x; dq[m + 1] += ds * k.y; dq[m + 2] += ds * k.z; dq[m + 3] += ds * k.w;
+      }
+    }
+  }
+  if (i >= S) return;
+#pragma unroll
+  for (int m = 0; m < DPT; ++m) dq[m] *= scale;
+  rope_slice<DPT>(dq, cosb + (long long)i * (HD / 2), sinb + (long long)i * (HD / 2), d0, -1);
+  store_slice<DPT>(dqkv + (long long)(b * S + i) * rs + (long long)h * HD + d0, dq);
+}
+
+// dK, dV: per key row, over the query tiles kb..end (causal: queries >= key)
+template <int HD>
+__global__ __launch_bounds__(256) void attnf_bwd_dkdv_kernel(const float* __restrict__ qkv,
+                                                             const float* __restrict__ dout,
+                                                             const float* __restrict__ lse,
+                                                             const float* __restrict__ delta,
+                                                             float* __restrict__ dqkv, const float* __restrict__ cosb,
+                                                             const float* __restrict__ sinb, int S, int H, float sl2,
+                                                             float scale) {
+  constexpr int DPT = HD / 4;
+  __shared__ float Qs[ATT_R * HD], Ds[ATT_R * HD], Ls[ATT_R], Dl[ATT_R];
+  const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int kr_ = threadIdx.x >> 2, part = threadIdx.x & 3, d0 = part * DPT;
+  const int j = kb * ATT_R + kr_, jk = min(j, S - 1);
+  const long long rs = 3LL * H * HD;
+  const float* qbase = qkv + (long long)b * S * rs + (long long)h * HD;
+  const float* kbase = qbase + (long long)H * HD;
+  const float* vbase = qbase + 2LL * H * HD;
+  const float* obase = dout + (long long)b * S * H * HD + (long long)h * HD;
+  const long long lrow = ((long long)b * H + h) * S;
+  float k[DPT], v[DPT], dk[DPT], dv[DPT];
+  load_slice<DPT>(kbase + jk * rs + d0, k);
+  rope_slice<DPT>(k, cosb + (long long)jk * (HD / 2), sinb + (long long)jk * (HD / 2), d0, 1);
+  load_slice<DPT>(vbase + jk * rs + d0, v);
+#pragma unroll
+  for (int m = 0; m < DPT; ++m) dk[m] = dv[m] = 0.f;
+  const int nqt = (S + ATT_R - 1) / ATT_R;
+  for (int qt = kb; qt < nqt; ++qt) {
+    __syncthreads();
+    stage_rows<HD>(Qs, qbase, rs, qt * ATT_R, S, cosb, sinb, true);
+    stage_rows<HD>(Ds, obase, (long long)H * HD, qt * ATT_R, S, cosb, sinb, false);
+    if (threadIdx.x < ATT_R) {
+      const int qi = qt * ATT_R + threadIdx.x;
+      Ls[threadIdx.x] = qi < S ? lse[lrow + qi] : 0.f;
+      Dl[threadIdx.x] = qi < S ? delta[lrow + qi] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int r = 0; r < ATT_R; ++r) {
+      const int qi = qt * ATT_R + r;
+      const float* qr = Qs + r * HD + d0;
+      const float* dr = Ds + r * HD + d0;
+      const float s = dot_lds<HD>(k, qr) * sl2;
+      const float dp = dot_lds<HD>(v, dr);
+      const float p = (qi >= j && qi < S) ? exp2f(s - Ls[r]) : 0.f;
+      const float ds = p * (dp - Dl[r]);
+#pragma unroll
+      for (int m = 0; m < DPT; m += 4) {
+        const float4 qq = *(const float4*)(qr + m);
+        const float4 dd = *(const float4*)(dr + m);
+        dk[m] += ds * qq.x; dk[m + 1] += ds * qq.y; dk[m + 2] += ds * qq.z; dk[m + 3] += ds * qq.w;
+        dv[m] += p * dd.x; dv[m + 1] += p * dd.y; dv[m + 2] += p * dd.z; dv[m + 3] += p * dd.w;
+      }
+    }
+  }
+  if (j >= S) return;
+#pragma unroll
+  for (int m = 0; m < DPT; ++m) dk[m] *= scale;
+  rope_slice<DPT>(dk, cosb + (long long)j * (HD / 2), sinb + (long long)j * (HD / 2), d0, -1);
+  float* dst = dqkv + (long long)(b * S + j) * rs + (long long)h * HD + d0;
+  store_slice<DPT>(dst + (long long)H * HD, dk);
+  store_slice<DPT>(dst + 2LL * H * HD, dv);
+}
+
+#define ATT_HD_SWITCH(HDV, CALL) \
+  switch (HDV) {                 \
+    case 16: CALL(16); break;    \
+    case 32: CALL(32); break;    \
+    case 48: CALL(48); break;    \
+    case 64: CALL(64); break;    \
+    case 96: CALL(96); break;    \
+    case 128: CALL(128); break;  \
+    default: return (int)hipErrorInvalidValue; \
+  }
+
+DDL_API int ddl_attnf_fwd(const float* qkv, float* o, float* lse, const float* cosb, const float* sinb, int B, int S,
+                          int H, int HD, float scale, hipStream_t s) {
+  if (B < 1 || S < 1 || H < 1) return 0;
+  const dim3 grid((S + ATT_R - 1) / ATT_R, H, B);
+  const float sl2 = scale * LOG2E;
+#define ATT_FWD(D) hipLaunchKernelGGL(attnf_fwd_kernel<D>, grid, dim3(256), 0, s, qkv, o, lse, cosb, sinb, S, H, sl2)
+  ATT_HD_SWITCH(HD, ATT_FWD)
+#undef ATT_FWD
+  return (int)hipGetLastError();
+}
+
+DDL_API int ddl_attnf_bwd(const float* qkv, const float* o, const float* dout, const float* lse, float* delta,
+                          float* dqkv, const float* cosb, const float* sinb, int B, int S, int H, int HD, float scale,
+                          hipStream_t s) {
+  if (B < 1 || S < 1 || H < 1) return 0;
+  const dim3 grid((S + ATT_R - 1) / ATT_R, H, B);
+  const float sl2 = scale * LOG2E;
+#define ATT_DQ(D)                                                                                                 \
+  hipLaunchKernelGGL(attnf_bwd_dq_kernel<D>, grid, dim3(256), 0, s, qkv, o, dout, lse, delta, dqkv, cosb, sinb, S, \
+                     H, sl2, scale)
+  ATT_HD_SWITCH(HD, ATT_DQ)
+#undef ATT_DQ
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+#define ATT_DKV(D)                                                                                             \
+  hipLaunchKernelGGL(attnf_bwd_dkdv_kernel<D>, grid, dim3(256), 0, s, qkv, dout, lse, delta, dqkv, cosb, sinb, \
+                     S, H, sl2, scale)
+  ATT_HD_SWITCH(HD, ATT_DKV)
+#undef ATT_DKV
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Vocabulary cross-entropy, fp32 logits [R][V] (row stride ld), int32 labels. One block per row:
+// pass 1 online max / sum-exp, pass 2 d = (softmax - onehot) * (*inv); rowloss[r] = lse - z[label]
+// (0 for ignored rows, whose gradient row is zero).
+__device__ __forceinline__ void block_maxsum(float& m, float& s, float* sm) {
+  // merge (m, s) pairs: wave level, then the 4 waves in a fixed order
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o), s2 = __shfl_xor(s, o);
+    const float nm = fmaxf(m, m2);
+    s = (nm == -INFINITY) ? 0.f : s * exp2f(m - nm) + s2 * exp2f(m2 - nm);
+    m = nm;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) { sm[w] = m; sm[4 + w] = s; }
+  __syncthreads();
+  m = sm[0]; s = sm[4];
+  for (int k = 1; k < 4; ++k) {
+    const float m2 = sm[k], s2 = sm[4 + k], nm = fmaxf(m, m2);
+    s = (nm == -INFINITY) ? 0.f : s * exp2f(m - nm) + s2 * exp2f(m2 - nm);
+    m = nm;
+  }
+}
+
+__global__ __launch_bounds__(256) void cevf_rows_kernel(const float* __restrict__ z, const int* __restrict__ labels,
+                                                        int V, long long ld, const float* __restrict__ inv,
+                                                        int ignore_index, float* __restrict__ rowloss,
+                                                        float* __restrict__ dz, long long ldd) {
+  __shared__ float sm[8];
+  const int row = blockIdx.x;
+  const float* zr = z + row * ld;
+  const int lab = labels[row];
+  float m = -INFINITY, s = 0.f;
+  const bool vec = (V % 4 == 0) && (ld % 4 == 0);
+  if (vec) {
+    for (int c = threadIdx.x; c < V / 4; c += 256) {
+      const float4 v = ((const float4*)zr)[c];
+      const float x[4] = {v.x * LOG2E, v.y * LOG2E, v.z * LOG2E, v.w * LOG2E};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float nm = fmaxf(m, x[k]);
+        s = s * exp2f(m - nm) + exp2f(x[k] - nm);
+        m = nm;
+      }
+    }
+  } else {
+    for (int c = threadIdx.x; c < V; c += 256) {
+      const float x = zr[c] * LOG2E, nm = fmaxf(m, x);
+      s = s * exp2f(m - nm) + exp2f(x - nm);
+      m = nm;
+    }
+  }
+  block_maxsum(m, s, sm);
+  const float lse2 = m + log2f(s);  // log2 domain
+  const bool valid = lab != ignore_index && lab >= 0 && lab < V;
+  if (threadIdx.x == 0) rowloss[row] = valid ? (lse2 / LOG2E - zr[lab]) : 0.f;
+  if (!dz) return;
+  const float k = valid ? *inv : 0.f;
+  float* dr = dz + row * ldd;
+  for (int c = threadIdx.x; c < V; c += 256) {
+    const float p = exp2f(zr[c] * LOG2E - lse2);
+    dr[c] = (p - (c == lab ? 1.f : 0.f)) * k;
+  }
+}
+
+__global__ __launch_bounds__(256) void cevf_fold_kernel(const float* __restrict__ rowloss, int R,
+                                                        const float* __restrict__ inv, float* __restrict__ loss) {
+  __shared__ float sm[4];
+  float s = 0.f;
+  for (int r = threadIdx.x; r < R; r += 256) s += rowloss[r];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) loss[0] = (((sm[0] + sm[1]) + sm[2]) + sm[3]) * (*inv);
+}
+
+DDL_API int ddl_cevf(const float* z, const int* labels, int R, int V, long long ld, const float* inv,
+                     int ignore_index, float* rowloss, float* loss, float* dz, long long ldd, hipStream_t s) {
+  if (R < 1 || V < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(cevf_rows_kernel, dim3(R), dim3(256), 0, s, z, labels, V, ld, inv, ignore_index, rowloss, dz,
+                     ldd);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(cevf_fold_kernel, dim3(1), dim3(256), 0, s, rowloss, R, inv, loss);
+  return (int)hipGetLastError();
+}
+
+__global__ void scale_f32_kernel(float* __restrict__ x, long long n, const float* __restrict__ g) {
+  const float s = *g;
+  if (s == 1.f) return;
+  GSTRIDE_LOOP(i, n) x[i] *= s;
+}
+
+DDL_API int ddl_scale_f32(float* x, long long n, const float* g, hipStream_t s) {
+  if (n < 1) return 0;
+  hipLaunchKernelGGL(scale_f32_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, x, n, g);
+  return (int)hipGetLastError();
+}

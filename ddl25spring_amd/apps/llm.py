@@ -12,6 +12,7 @@ messages; stage weights start identical across pipelines (seeded init + broadcas
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import asdict, dataclass
 
@@ -20,7 +21,7 @@ import torch
 from ..data.text import SPTokenizer, TinyStories
 from ..models.llama import LLama, causalLLMLoss, split_stages
 from ..parallel.dp import GradBucketer, average_weights, broadcast_parameters
-from ..parallel.pipeline import PipelineStage, grid_ranks
+from ..parallel.pipeline import PipelineStage, grid_ranks, pipeline_links
 from ..runtime.checkpoint import ShardedCheckpoint, load_optimizer_state, optimizer_state
 from ..runtime.graphs import CAPTURE_MODE
 
@@ -47,10 +48,13 @@ class LLMConfig:
     graph: bool = True  # dp = pp = 1 on a GPU: replay the whole step (fwd, bwd, Adam) as a HIP graph
     ckpt_dir: str = ""  # sharded checkpoint directory (runtime/checkpoint.py); resumes if committed
     ckpt_every: int = 0  # commit a checkpoint every N optimizer steps (0: only at the end)
+    # "fp32": the reference's precision (fp32 activations, stage messages and math; deterministic
+    # kernels) — the default; "bf16": bf16 activations / MFMA operands with fp32 master weights
+    precision: str = "fp32"
 
 
 _RUN_FIELDS = ("vocab_size", "dmodel", "num_heads", "n_layers", "ctx_size", "batch_size",
-               "micro_batches", "dp", "pp", "dp_mode", "lr", "seed", "fused_adam")
+               "micro_batches", "dp", "pp", "dp_mode", "lr", "seed", "fused_adam", "precision")
 
 
 def _run_tag(cfg: "LLMConfig") -> str:
@@ -95,15 +99,16 @@ def train_llm(cfg: LLMConfig, ctx, log=print, warmup: int = 0) -> dict:
     dp_group = ctx.new_groups("dp", [[p * cfg.pp + s for p in range(cfg.dp)] for s in range(cfg.pp)])
     torch.manual_seed(cfg.seed)
     full = LLama(vocab_size=cfg.vocab_size, dmodel=cfg.dmodel, num_heads=cfg.num_heads,
-                 n_layers=cfg.n_layers, ctx_size=cfg.ctx_size)
+                 n_layers=cfg.n_layers, ctx_size=cfg.ctx_size, precision=cfg.precision)
     mod = split_stages(full, cfg.pp)[stage].to(dev)
     if cfg.dp > 1:
         broadcast_parameters(mod, ctx, src=stage, group=dp_group)  # pipeline 0's stage s is rank s
     if dev.type == "cuda" and cfg.fused_adam:
         from ..optim import FlatAdam
-        # one fused Adam launch that also refreshes the bf16 weight shadow the GEMMs read;
-        # weight grads accumulate straight into the flat grad buffer (or the DP buckets)
-        opt = FlatAdam(mod.parameters(), lr=cfg.lr, fused=True, bf16_shadow=True)
+        # one fused Adam launch (bf16: also refreshes the bf16 weight shadow the GEMMs read; fp32:
+        # the kernels read the master weights); weight grads accumulate straight into the flat
+        # grad buffer (or the DP buckets)
+        opt = FlatAdam(mod.parameters(), lr=cfg.lr, fused=True, bf16_shadow=cfg.precision == "bf16")
     else:
         opt = torch.optim.Adam(mod.parameters(), lr=cfg.lr)
     # DP-GA buckets are slices of FlatAdam's own flat gradient buffer (no second copy)
@@ -113,9 +118,14 @@ def train_llm(cfg: LLMConfig, ctx, log=print, warmup: int = 0) -> dict:
     if cfg.batch_size % cfg.micro_batches:
         raise ValueError("batch_size must be divisible by micro_batches")
     mb = cfg.batch_size // cfg.micro_batches
-    act_dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
+    # stage messages in the compute precision (the reference ships fp32 micro-batch activations,
+    # intro_PP_1F1B_MB.py:57)
+    act_dtype = torch.bfloat16 if dev.type == "cuda" and cfg.precision == "bf16" else torch.float32
+    # per-link communicators: asynchronous P2P overlapped with compute (DDL_PP_ASYNC=0: blocking)
+    links = pipeline_links(cfg.dp, cfg.pp) if (cfg.pp > 1 and ctx.is_distributed
+                                               and os.environ.get("DDL_PP_ASYNC", "1") != "0") else None
     ps = PipelineStage(mod, stage, cfg.pp, ranks=pipe_ranks, act_shape=(mb, cfg.ctx_size, cfg.dmodel),
-                       act_dtype=act_dtype, device=dev) if cfg.pp > 1 else None
+                       act_dtype=act_dtype, device=dev, links=links) if cfg.pp > 1 else None
     ckpt = ShardedCheckpoint(cfg.ckpt_dir, ctx, tag=_run_tag(cfg)) if cfg.ckpt_dir else None
     done = 0  # optimizer steps already taken (warm-up steps included: they train too)
     restored = ckpt.load() if ckpt is not None else None

@@ -59,6 +59,8 @@ class Generator(nn.Module):
         N = z.shape[0]
         if z.shape[1] != self.nz_pad:
             z = torch.cat([z, z.new_zeros(N, self.nz_pad - z.shape[1])], 1)
+        if z.is_cuda:
+            z = z.to(torch.bfloat16)  # bf16 device path (fp32 activations would select the fp32 linear)
         h = A.linear(z, self.proj).view(N, 4, 4, 4 * self.ngf)
         h = self.bn0(h, "relu")
         h = self.bn1(A.conv_transpose2d(h, self.up1, 2, 1), "relu")      # 8x8

@@ -10,6 +10,12 @@ interleaved RoPE -> out-proj (+residual, fused in the GEMM epilogue) -> RMSNorm 
 SwiGLU FFN (hidden = 8/3 d rounded to 32) -> w2 (+residual) ; final RMSNorm and an untied LM head.
 Loss-curve comparisons with the reference are therefore trend-level.
 
+Precision (extension): ``precision="fp32"`` (default: the reference trains this model in fp32,
+lab/tutorial_1b/PP/1F1B/intro_PP_1F1B_MB.py:16-46) makes the embedding emit fp32 activations, so
+every op downstream runs the reference-precision kernels (ops/llama_f32.py: linears on the X6 /
+exact-fp32 conv engine, fp32 attention / RMSNorm / SwiGLU / CE, all deterministic);
+``precision="bf16"`` is the bf16-MFMA fast path. On CPU everything is fp32 either way.
+
 Stage 0's ``embed`` runs the embedding AND the stage's blocks (the reference's rank 0 only calls
 ``embed``, so whether its blocks ran was simplellm-dependent).
 """
@@ -58,10 +64,21 @@ class CausalLLama:
     """Marker type, as passed to ``LLama(CausalLLama, ...)`` in the reference."""
 
 
+PRECISIONS = ("fp32", "bf16")
+
+
+def _act_dtype(precision: str):
+    if precision not in PRECISIONS:
+        raise ValueError(f"LLaMA precision must be one of {PRECISIONS}, got {precision!r}")
+    return torch.float32 if precision == "fp32" else torch.bfloat16
+
+
 class _Base(nn.Module):
-    def __init__(self, dmodel, num_heads, n_layers, ctx_size, device=None, ffn_hidden=None):
+    def __init__(self, dmodel, num_heads, n_layers, ctx_size, device=None, ffn_hidden=None, precision="fp32"):
         super().__init__()
         self.dmodel, self.ctx_size = dmodel, ctx_size
+        self.precision = precision
+        self.act_dtype = _act_dtype(precision)
         self.layers = nn.ModuleList(Block(dmodel, num_heads, ffn_hidden) for _ in range(n_layers))
         if device is not None:
             self.to(device)
@@ -74,22 +91,23 @@ class _Base(nn.Module):
 
 class LLamaFirstStage(_Base):
     def __init__(self, vocab_size, dmodel=288, num_heads=6, device=None, n_layers=2, ctx_size=256,
-                 padding_idx=None, ffn_hidden=None):
-        super().__init__(dmodel, num_heads, n_layers, ctx_size, None, ffn_hidden)
+                 padding_idx=None, ffn_hidden=None, precision="fp32"):
+        super().__init__(dmodel, num_heads, n_layers, ctx_size, None, ffn_hidden, precision)
         self.vocab_size, self.padding_idx = vocab_size, padding_idx
         self.emb = nn.Parameter(torch.randn(vocab_size, dmodel) * 0.02)
         if device is not None:
             self.to(device)
 
     def embed(self, x):
-        return self.run_layers(A.embedding(x, self.emb, self.padding_idx))
+        return self.run_layers(A.embedding(x, self.emb, self.padding_idx, dtype=self.act_dtype))
 
     forward = embed
 
 
 class LLamaStage(_Base):
-    def __init__(self, dmodel=288, num_heads=6, device=None, n_layers=2, ctx_size=256, ffn_hidden=None):
-        super().__init__(dmodel, num_heads, n_layers, ctx_size, device, ffn_hidden)
+    def __init__(self, dmodel=288, num_heads=6, device=None, n_layers=2, ctx_size=256, ffn_hidden=None,
+                 precision="fp32"):
+        super().__init__(dmodel, num_heads, n_layers, ctx_size, device, ffn_hidden, precision)
 
     def forward(self, x):
         return self.run_layers(x)
@@ -97,8 +115,8 @@ class LLamaStage(_Base):
 
 class LLamaLastStage(_Base):
     def __init__(self, vocab_size, dmodel=288, num_heads=6, device=None, n_layers=2, ctx_size=256,
-                 ffn_hidden=None):
-        super().__init__(dmodel, num_heads, n_layers, ctx_size, None, ffn_hidden)
+                 ffn_hidden=None, precision="fp32"):
+        super().__init__(dmodel, num_heads, n_layers, ctx_size, None, ffn_hidden, precision)
         self.vocab_size = vocab_size
         self.norm = nn.Parameter(torch.ones(dmodel))
         self.head = nn.Parameter(torch.randn(vocab_size, dmodel) * 0.02)
@@ -113,12 +131,14 @@ class LLama(nn.Module):
     """Whole model (reference primer/intro.py:17-18): first stage + last stage, n_layers total."""
 
     def __init__(self, kind=CausalLLama, vocab_size=32000, dmodel=288, num_heads=6, device=None,
-                 n_layers=6, ctx_size=256, padding_idx=None, ffn_hidden=None):
+                 n_layers=6, ctx_size=256, padding_idx=None, ffn_hidden=None, precision="fp32"):
         super().__init__()
         n0 = n_layers // 2
+        self.precision = precision
         self.first = LLamaFirstStage(vocab_size, dmodel, num_heads, None, n0, ctx_size, padding_idx,
-                                     ffn_hidden)
-        self.last = LLamaLastStage(vocab_size, dmodel, num_heads, None, n_layers - n0, ctx_size, ffn_hidden)
+                                     ffn_hidden, precision)
+        self.last = LLamaLastStage(vocab_size, dmodel, num_heads, None, n_layers - n0, ctx_size, ffn_hidden,
+                                   precision)
         if device is not None:
             self.to(device)
 
@@ -146,6 +166,7 @@ def split_stages(model: LLama, n_stages: int):
             st = LLamaStage.__new__(LLamaStage)
             nn.Module.__init__(st)
         st.layers = nn.ModuleList(mine)
+        st.precision, st.act_dtype = model.precision, _act_dtype(model.precision)
         if n_stages == 1:
             st = model
         out.append(st)

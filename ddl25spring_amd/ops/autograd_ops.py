@@ -1,9 +1,10 @@
 """Autograd-composable ops for ``torch.nn.Module`` models (LLaMA stages, tabular nets, GANs).
 
 On device tensors every op below is a HIP kernel (MFMA implicit-GEMM for the linears, the fused
-LLaMA kernels of csrc/kernels/llama.hip, fused CE over the vocabulary); activations are bf16,
-parameters stay fp32 ``nn.Parameter`` (cast to a bf16 shadow per forward) and weight gradients are
-fp32. On CPU tensors the same functions run plain PyTorch fp32 ops, so module code is written once
+LLaMA kernels of csrc/kernels/llama.hip, fused CE over the vocabulary). The activation dtype picks
+the precision: bf16 activations run the bf16-MFMA kernels (parameters stay fp32 ``nn.Parameter``,
+cast to a bf16 shadow per forward); fp32 activations (the reference's precision) run
+ops/llama_f32.py (csrc/kernels/llama_f32.hip + the fp32 conv engine). Weight gradients are fp32. On CPU tensors the same functions run plain PyTorch fp32 ops, so module code is written once
 and is testable without a GPU.
 """
 from __future__ import annotations
@@ -15,6 +16,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from . import functional as Fn
+from . import llama_f32 as L32
 from ._lib import check, ptr, stream
 
 vp, i32, i64, f32 = _lib.vp, _lib.i32, _lib.i64, _lib.f32
@@ -128,11 +130,19 @@ class _Linear(torch.autograd.Function):
         return dx, dw, db, dres
 
 
+def _f32(x) -> bool:
+    """fp32 device activations take the reference-precision kernels (ops/llama_f32.py)."""
+    return x.dtype == torch.float32
+
+
 def linear(x, w, b=None, residual=None):
-    """y = x @ w.T (+ b) (+ residual). Device: one MFMA GEMM with the bias / residual in its epilogue."""
+    """y = x @ w.T (+ b) (+ residual). Device: one MFMA GEMM with the bias / residual in its epilogue
+    (bf16 activations: bf16 MFMA; fp32 activations: the X6 / exact-fp32 conv engine)."""
     if not x.is_cuda:
         y = F.linear(x, w, b)
         return y + residual if residual is not None else y
+    if _f32(x):
+        return L32.LinearF32.apply(x, w, b, None if residual is None else residual.float())
     if x.dtype != torch.bfloat16:
         x = x.to(torch.bfloat16)
     if residual is not None and residual.dtype != torch.bfloat16:
@@ -185,6 +195,8 @@ class _RMSNorm(torch.autograd.Function):
 def rmsnorm(x, g, eps=1e-6):
     if not x.is_cuda:
         return x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + eps) * g
+    if _f32(x):
+        return L32.RMSNormF32.apply(x, g, eps, False)
     return _RMSNorm.apply(x.to(torch.bfloat16), g, eps, False)
 
 
@@ -193,6 +205,8 @@ def rmsnorm_fork(x, g, eps=1e-6):
     is summed into dx by the RMSNorm backward kernel."""
     if not x.is_cuda:
         return rmsnorm(x, g, eps), x
+    if _f32(x):
+        return L32.RMSNormF32.apply(x, g, eps, True)
     return _RMSNorm.apply(x.to(torch.bfloat16), g, eps, True)
 
 
@@ -224,6 +238,8 @@ def swiglu(ab):
     if not ab.is_cuda:
         a, b = ab.chunk(2, -1)
         return F.silu(a) * b
+    if _f32(ab):
+        return L32.SwiGLUF32.apply(ab)
     return _SwiGLU.apply(ab.to(torch.bfloat16))
 
 
@@ -256,9 +272,13 @@ class _Embedding(torch.autograd.Function):
         return None, dw, None
 
 
-def embedding(idx, w, padding_idx=None):
+def embedding(idx, w, padding_idx=None, dtype=None):
+    """Row gather; on the device the output dtype is ``dtype`` (default bf16): float32 selects the
+    reference-precision path for everything downstream."""
     if not w.is_cuda:
         return F.embedding(idx, w, padding_idx)
+    if dtype == torch.float32:
+        return L32.EmbeddingF32.apply(idx, w, padding_idx)
     return _Embedding.apply(idx, w, padding_idx)
 
 
@@ -349,6 +369,8 @@ def causal_attention(qkv, n_heads, head_dim):
     """Causal multi-head attention with RoPE on q, k. qkv: [B, S, 3*H*hd] -> [B, S, H*hd]."""
     if not qkv.is_cuda:
         return attention_ref(qkv, n_heads, head_dim)
+    if _f32(qkv):
+        return L32.AttentionF32.apply(qkv, n_heads, head_dim)
     return _Attention.apply(qkv.to(torch.bfloat16), n_heads, head_dim)
 
 
@@ -419,8 +441,12 @@ def cross_entropy_vocab(logits, targets, ignore_index=-100, scale: float = 1.0):
     returned loss: the gradient is then final in the forward pass and the backward has no
     rescaling pass over the [rows, V] gradient."""
     if not logits.is_cuda:
-        return scale * F.cross_entropy(logits.reshape(-1, logits.shape[-1]).float(),
-                                       targets.reshape(-1).long(), ignore_index=ignore_index)
+        lg = logits.reshape(-1, logits.shape[-1])
+        if lg.dtype not in (torch.float32, torch.float64):
+            lg = lg.float()
+        return scale * F.cross_entropy(lg, targets.reshape(-1).long(), ignore_index=ignore_index)
+    if _f32(logits):
+        return L32.VocabCEF32.apply(logits, targets.to(torch.int32).contiguous(), ignore_index, float(scale))
     if logits.dtype != torch.bfloat16:
         logits = logits.to(torch.bfloat16)
     return _VocabCE.apply(logits, targets.to(torch.int32).contiguous(), ignore_index, float(scale))

@@ -6,9 +6,18 @@ Replaces the reference's hand-written per-rank send/recv choreographies
     matching sends/receives in a deadlock-free order;
   * activations / gradients stay on the GPU (RCCL ``send/recv`` over xGMI; the reference staged
     every message through host memory with ``.to("cpu")``);
-  * a posted comm group is issued as ONE ``batch_isend_irecv`` (grouped P2P); over gloo (ranks that
-    share a GPU, or CPU runs) device tensors are staged through host memory, since gloo's
-    point-to-point moves CPU tensors only;
+  * with per-link communicators (``pipeline_links``: one process group per DIRECTED stage link,
+    activations s -> s+1 and gradients s+1 -> s apart) the P2P is asynchronous and overlaps
+    compute: the receives of the next comm step are posted BEFORE the current compute step, sends
+    are posted right after the compute that produced them, and a stage waits for a received tensor
+    only when a compute step consumes it (``work.wait()``: on RCCL a device-side stream wait, the
+    host keeps queueing). Each link's stream carries one direction between one pair of ranks in
+    schedule order, so posting receives early cannot create a send/recv cycle on a shared stream;
+    the link communicators are initialised up front in one global order (no lazy-init rendezvous
+    inside the schedule). Without links the legacy path posts each comm group as ONE blocking
+    ``batch_isend_irecv``;
+  * over gloo (ranks that share a GPU, or CPU runs) device tensors are staged through host memory,
+    since gloo's point-to-point moves CPU tensors only;
   * the loss is divided by the number of micro-batches (gradient averaging by loss scaling, as
     intro_PP_1F1B_MB.py:99 does), so an iteration equals one full-batch step.
 """
@@ -22,8 +31,10 @@ from . import schedule as S
 
 class PipelineStage:
     def __init__(self, module: torch.nn.Module, stage: int, n_stages: int, ranks: list[int] | None = None,
-                 act_shape=None, act_dtype=None, device=None, group=None):
-        """``ranks[s]`` = global rank of stage s in this pipeline (default: range(n_stages))."""
+                 act_shape=None, act_dtype=None, device=None, group=None, links: dict | None = None):
+        """``ranks[s]`` = global rank of stage s in this pipeline (default: range(n_stages)).
+        ``links``: ``pipeline_links(...)`` (every rank's dict, built collectively) -> asynchronous,
+        compute-overlapped P2P; None -> blocking grouped P2P on ``group``."""
         self.module, self.stage, self.S = module, stage, n_stages
         self.ranks = ranks or list(range(n_stages))
         self.act_shape, self.act_dtype = act_shape, act_dtype
@@ -31,6 +42,13 @@ class PipelineStage:
         self.group = group
         self.host_staged = torch.device(self.device).type == "cuda" and dist.is_initialized() and \
             dist.get_backend(group) == "gloo"
+        self.links = None
+        if links is not None and dist.is_initialized():
+            me = self.ranks[stage]
+            self.links = {k: g for k, g in links.items() if me in k}
+            self.link_host_staged = torch.device(self.device).type == "cuda" and any(
+                dist.get_backend(g) == "gloo" for g in self.links.values())
+            _warm_links(links, me, self.device)
 
     @property
     def is_first(self):
@@ -68,6 +86,8 @@ class PipelineStage:
         grad_sync: optional DP bucketer; its all-reduces only fire on the stage's LAST backward
         (earlier micro-batches accumulate under ``no_sync``).
         Returns the summed (already 1/M-scaled) loss on the last stage, else None."""
+        if self.links is not None:
+            return self._run_async(kind, n_micro, inputs, targets, loss_fn, grad_sync)
         import contextlib
         acts = S.make(kind, self.S, n_micro)
         prog = S.stage_program(acts, self.stage)
@@ -93,6 +113,87 @@ class PipelineStage:
                     x_in[a.mb] = buf.requires_grad_(True)
                 else:
                     grads_in[a.mb] = buf
+        return total
+
+    # ------------------------------------------------------------------ asynchronous (per-link) P2P
+    def _link(self, op: int, peer_stage: int):
+        me, peer = self.ranks[self.stage], self.ranks[peer_stage]
+        return self.links[(me, peer) if op in (S.SEND_ACT, S.SEND_GRAD) else (peer, me)], peer
+
+    def _post_recv(self, a, pending):
+        if (a.op, a.mb) in pending:
+            return
+        g, peer = self._link(a.op, a.peer)
+        buf = torch.empty(self.act_shape, dtype=self.act_dtype,
+                          device="cpu" if self.link_host_staged else self.device)
+        pending[(a.op, a.mb)] = (dist.irecv(buf, peer, group=g), buf)
+
+    def _take(self, pending, op, mb):
+        work, buf = pending.pop((op, mb))
+        work.wait()  # RCCL: the current stream waits for the receive; the host does not block
+        return buf.to(self.device) if self.link_host_staged else buf
+
+    def _post_send(self, a, t, sends):
+        g, peer = self._link(a.op, a.peer)
+        t = t.detach().contiguous()
+        if self.link_host_staged:
+            t = t.cpu()
+        sends.append((dist.isend(t, peer, group=g), t))  # keep the tensor alive until completion
+
+    def _run_async(self, kind, n_micro, inputs, targets, loss_fn, grad_sync):
+        import contextlib
+        prog = S.stage_program(S.make(kind, self.S, n_micro), self.stage)
+        last_bwd = max(i for i, st in enumerate(prog) if st[0].op == S.BWD)
+        pending, sends = {}, []
+        x_in, y_out = {}, {}
+        total = None
+        for si, step in enumerate(prog):
+            a0 = step[0]
+            if a0.op not in (S.FWD, S.BWD):  # a comm step: receives (unless posted early), then sends
+                for a in step:
+                    if a.op in (S.RECV_ACT, S.RECV_GRAD):
+                        self._post_recv(a, pending)
+                for a in step:
+                    if a.op == S.SEND_ACT:
+                        self._post_send(a, y_out[a.mb], sends)
+                    elif a.op == S.SEND_GRAD:
+                        self._post_send(a, x_in.pop(a.mb).grad, sends)
+                continue
+            # post the receives of the comm steps that follow BEFORE this compute step
+            j = si + 1
+            while j < len(prog) and prog[j][0].op not in (S.FWD, S.BWD):
+                for a in prog[j]:
+                    if a.op in (S.RECV_ACT, S.RECV_GRAD):
+                        self._post_recv(a, pending)
+                j += 1
+            sync_ctx = contextlib.nullcontext()
+            if grad_sync is not None and a0.op == S.BWD and si != last_bwd:
+                sync_ctx = grad_sync.no_sync()
+            with sync_ctx:
+                if a0.op == S.FWD:
+                    if self.is_first:
+                        inp = inputs[a0.mb]
+                    else:
+                        inp = self._take(pending, S.RECV_ACT, a0.mb).requires_grad_(True)
+                        x_in[a0.mb] = inp
+                    out = self.module(inp)
+                    if self.is_last:
+                        l = loss_fn(out, targets[a0.mb]) / n_micro
+                        y_out[a0.mb] = l
+                        total = l.detach() if total is None else total + l.detach()
+                    else:
+                        y_out[a0.mb] = out
+                else:
+                    out = y_out.pop(a0.mb)
+                    if self.is_last:
+                        out.backward()
+                    else:
+                        out.backward(self._take(pending, S.RECV_GRAD, a0.mb))
+                    if self.is_first:
+                        x_in.pop(a0.mb, None)
+        for work, _ in sends:
+            work.wait()
+        assert not pending, f"unconsumed receives {sorted(pending)}"
         return total
 
     def _exec_step(self, step, ops, posted, x_in, y_out, grads_in, inputs, targets, loss_fn, n_micro):
@@ -130,6 +231,36 @@ class PipelineStage:
                     buf = torch.empty(self.act_shape, dtype=self.act_dtype, device=self.device)
                     ops.append(dist.P2POp(dist.irecv, buf, peer, self.group))
                     posted.append((a, buf))
+
+
+def pipeline_links(dp: int, pp: int) -> dict | None:
+    """One process group per DIRECTED stage link of every pipeline of a dp x pp grid (rank =
+    pipe * pp + stage): key (src, dst) -> group of {src, dst}; activations flow (s, s+1),
+    gradients (s+1, s). Collective: every rank must call it, in the same program order."""
+    if not dist.is_initialized() or pp < 2:
+        return None
+    links = {}
+    for pipe in range(dp):
+        for s in range(pp - 1):
+            a, b = pipe * pp + s, pipe * pp + s + 1
+            links[(a, b)] = dist.new_group([a, b])
+            links[(b, a)] = dist.new_group([a, b])
+    return links
+
+
+def _warm_links(links: dict, me: int, device) -> None:
+    """Initialise my link communicators in one global order (a blocking 1-element exchange per
+    link), so no lazy communicator rendezvous happens inside the asynchronous schedule."""
+    for (src, dst) in sorted(links):
+        if me not in (src, dst):
+            continue
+        g = links[(src, dst)]
+        dev = "cpu" if dist.get_backend(g) == "gloo" else device
+        t = torch.zeros(1, dtype=torch.float32, device=dev)
+        if me == src:
+            dist.send(t, dst, group=g)
+        else:
+            dist.recv(t, src, group=g)
 
 
 def grid_ranks(rank: int, dp: int, pp: int):

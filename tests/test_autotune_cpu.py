@@ -74,6 +74,10 @@ def test_fp32_plans_engine_choice():
         F32._TUNED = {f"auto:{key}": [64, 128, 4, "mfma32"], f"x6:dgrad:3,7,8,8,16,16,3,3,1,1": [128, 64, 2]}
         F32.set_math("auto")
         F32._PLANS.clear()
+        # a halo-eligible geometry (stride-1 "same" 3x3, OW 8) takes the halo X6 kernel first
+        cfg, split = F32.plan(F32.F_FWD, g)
+        assert cfg & F32.HALO_BIT and cfg & F32.X6_BIT
+        F32.set_halo(False)
         cfg, split = F32.plan(F32.F_FWD, g)
         assert (cfg, split) == (F32.cfg_of(64, 128), 4) and F32._cfg(cfg) & F32.X6_BIT == 0
         cfg, split = F32.plan(F32.F_DGRAD, g)
@@ -85,4 +89,5 @@ def test_fp32_plans_engine_choice():
     finally:
         F32._TUNED = old_tuned
         F32.set_math(old_math)
+        F32.set_halo(True)
         F32._PLANS.clear()

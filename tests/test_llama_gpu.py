@@ -1,5 +1,7 @@
-"""LLaMA HIP ops (linear / rmsnorm / swiglu / embedding / fused RoPE attention / vocab CE) vs the
-fp32 PyTorch reference of the same op, and a whole-model fwd+bwd check."""
+"""bf16 LLaMA HIP ops (linear / rmsnorm / swiglu / embedding / fused RoPE attention / vocab CE) vs
+the fp32 PyTorch reference of the same op, and a whole-model fwd+bwd check. The device inputs are
+bf16: the activation dtype selects the kernels, fp32 activations run the reference-precision path
+(tests/test_llama_f32_gpu.py)."""
 import pytest
 import torch
 
@@ -14,8 +16,11 @@ def _rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-def _pair(t, cuda):
-    c = t.detach().clone().to(cuda).requires_grad_(True)
+BF = torch.bfloat16
+
+
+def _pair(t, cuda, dtype=torch.float32):
+    c = t.detach().clone().to(cuda, dtype).requires_grad_(True)
     h = t.detach().clone().float().requires_grad_(True)
     return c, h
 
@@ -27,7 +32,7 @@ def test_rmsnorm_backward_shapes(cuda, T, D):
     torch.manual_seed(1)
     x = torch.randn(T, D)
     gam = torch.rand(D) + 0.5
-    xc, xh = _pair(x, cuda); gc, gh = _pair(gam, cuda)
+    xc, xh = _pair(x, cuda, BF); gc, gh = _pair(gam, cuda)
     yc, yh = A.rmsnorm(xc, gc), A.rmsnorm(xh, gh)
     assert _rel(yc, yh) < 1e-2
     g = torch.randn_like(yh)
@@ -43,7 +48,7 @@ def test_rmsnorm_fork_sums_residual_gradient(cuda):
     x = torch.randn(4, 64, 288)
     gam = torch.rand(288) + 0.5
     w = torch.randn(288, 288) * 0.05
-    xc, xh = _pair(x, cuda); gc, gh = _pair(gam, cuda)
+    xc, xh = _pair(x, cuda, BF); gc, gh = _pair(gam, cuda)
     hc, rc = A.rmsnorm_fork(xc, gc)
     hh, rh = A.rmsnorm_fork(xh, gh)
     assert _rel(rc, xh) < 1e-2
@@ -53,7 +58,7 @@ def test_rmsnorm_fork_sums_residual_gradient(cuda):
     yc.backward(g.to(cuda)); yh.backward(g)
     assert _rel(xc.grad, xh.grad) < 2e-2 and _rel(gc.grad, gh.grad) < 2e-2
     # residual output unused: the fork's second gradient is None
-    xc2 = x.detach().clone().to(cuda).requires_grad_(True)
+    xc2 = x.detach().clone().to(cuda, BF).requires_grad_(True)
     h2, _ = A.rmsnorm_fork(xc2, gc.detach())
     h2.float().sum().backward()
     xr = x.detach().clone().requires_grad_(True)
@@ -67,7 +72,7 @@ def test_linear_rmsnorm_swiglu_embedding(cuda):
     w = torch.randn(160, 96) * 0.1
     b = torch.randn(160)
     r = torch.randn(2, 37, 160)
-    xc, xh = _pair(x, cuda); wc, wh = _pair(w, cuda); bc, bh = _pair(b, cuda); rc, rh = _pair(r, cuda)
+    xc, xh = _pair(x, cuda, BF); wc, wh = _pair(w, cuda); bc, bh = _pair(b, cuda); rc, rh = _pair(r, cuda, BF)
     yc = A.linear(xc, wc, bc, residual=rc)
     yh = A.linear(xh, wh, bh, residual=rh)
     assert _rel(yc, yh) < 1e-2
@@ -77,7 +82,7 @@ def test_linear_rmsnorm_swiglu_embedding(cuda):
         assert _rel(a_.grad, b_.grad) < 2e-2
     # rmsnorm
     gam = torch.rand(96) + 0.5
-    xc, xh = _pair(x, cuda); gc, gh = _pair(gam, cuda)
+    xc, xh = _pair(x, cuda, BF); gc, gh = _pair(gam, cuda)
     yc, yh = A.rmsnorm(xc, gc), A.rmsnorm(xh, gh)
     assert _rel(yc, yh) < 1e-2
     g = torch.randn_like(yh)
@@ -85,7 +90,7 @@ def test_linear_rmsnorm_swiglu_embedding(cuda):
     assert _rel(xc.grad, xh.grad) < 2e-2 and _rel(gc.grad, gh.grad) < 2e-2
     # swiglu
     ab = torch.randn(2, 37, 128)
-    ac, ah = _pair(ab, cuda)
+    ac, ah = _pair(ab, cuda, BF)
     yc, yh = A.swiglu(ac), A.swiglu(ah)
     assert _rel(yc, yh) < 1e-2
     g = torch.randn_like(yh)
@@ -106,7 +111,7 @@ def test_linear_rmsnorm_swiglu_embedding(cuda):
 def test_fused_rope_attention(cuda, B, S, H, hd):
     torch.manual_seed(1)
     qkv = torch.randn(B, S, 3 * H * hd)
-    qc, qh = _pair(qkv, cuda)
+    qc, qh = _pair(qkv, cuda, BF)
     oc = A.causal_attention(qc, H, hd)
     oh = A.causal_attention(qh, H, hd)
     assert _rel(oc, oh) < 1e-2
@@ -122,7 +127,7 @@ def test_vocab_cross_entropy(cuda):
     logits = torch.randn(3, 17, 32000) * 2
     tgt = torch.randint(0, 32000, (3, 17))
     tgt[0, 3] = -100
-    lc, lh = _pair(logits, cuda)
+    lc, lh = _pair(logits, cuda, BF)
     a = A.cross_entropy_vocab(lc, tgt.to(cuda))
     b = A.cross_entropy_vocab(lh, tgt)
     assert abs(a.item() - b.item()) < 2e-2
@@ -153,7 +158,7 @@ def test_llama_model_fwd_bwd_matches_fp32(cuda):
     torch.manual_seed(0)
     mh = LLama(**cfg)
     torch.manual_seed(0)
-    mc = LLama(**cfg).to(cuda)
+    mc = LLama(**cfg, precision="bf16").to(cuda)
     x = torch.randint(0, 512, (2, 64))
     lh = causalLLMLoss(mh(x), x)
     lc = causalLLMLoss(mc(x.to(cuda)), x.to(cuda))
@@ -172,7 +177,7 @@ def test_fused_grad_accumulation_and_bf16_shadow(cuda):
     models, opts = [], []
     for fused in (False, True):
         torch.manual_seed(0)
-        m = LLama(**cfg).to(cuda)
+        m = LLama(**cfg, precision="bf16").to(cuda)
         models.append(m)
         opts.append(FlatAdam(m.parameters(), lr=1e-3, fused=fused, bf16_shadow=fused))
     torch.manual_seed(1)
@@ -197,7 +202,7 @@ def test_llm_step_graph_replay_matches_eager(cuda):
     curves = []
     for graph in (False, True):
         cfg = LLMConfig(vocab_size=1024, dmodel=96, num_heads=2, n_layers=2, ctx_size=64, batch_size=8,
-                        micro_batches=4, iters=6, log_every=1, graph=graph)
+                        micro_batches=4, iters=6, log_every=1, graph=graph, precision="bf16")
         out = train_llm(cfg, DistContext(device=cuda), log=None)
         curves.append([v for _, v in out["losses"]])
     assert len(curves[0]) == 6

@@ -62,10 +62,11 @@ def _ref_grads(seed, x):
     return loss.item(), {n: p.grad.clone() for n, p in model.named_parameters()}
 
 
-def _pp_worker(rank, world, port, kind, out_dir, micro):
+def _pp_worker(rank, world, port, kind, out_dir, micro, use_links=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from ddl25spring_amd.parallel.pipeline import PipelineStage
+    from ddl25spring_amd.parallel.pipeline import PipelineStage, pipeline_links
+    links = pipeline_links(1, world) if use_links else None
     torch.manual_seed(0)
     model = LLama(**TINY)
     names = {id(p): n for n, p in model.named_parameters()}
@@ -74,7 +75,7 @@ def _pp_worker(rank, world, port, kind, out_dir, micro):
     x = torch.randint(0, TINY["vocab_size"], (6, TINY["ctx_size"]))
     mbs = list(torch.chunk(x, micro))
     ps = PipelineStage(stage_mod, rank, world, act_shape=(6 // micro, TINY["ctx_size"], TINY["dmodel"]),
-                       act_dtype=torch.float32, device=torch.device("cpu"))
+                       act_dtype=torch.float32, device=torch.device("cpu"), links=links)
     loss = ps.run(kind, micro, inputs=mbs, targets=mbs, loss_fn=lambda o, t: causalLLMLoss(o, t))
     grads = {names[id(p)]: p.grad.clone() for p in stage_mod.parameters() if p.grad is not None}
     torch.save({"loss": None if loss is None else loss.item(), "grads": grads},
@@ -82,9 +83,13 @@ def _pp_worker(rank, world, port, kind, out_dir, micro):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind,world,micro", [("gpipe", 3, 3), ("1f1b", 3, 3), ("1f1b", 2, 6),
-                                              ("naive", 2, 1)])
-def test_pipeline_matches_single_process(kind, world, micro):
+@pytest.mark.parametrize("kind,world,micro,use_links", [("gpipe", 3, 3, False), ("1f1b", 3, 3, False),
+                                                        ("1f1b", 2, 6, False), ("naive", 2, 1, False),
+                                                        ("1f1b", 3, 3, True), ("gpipe", 3, 3, True),
+                                                        ("1f1b", 2, 6, True), ("naive", 3, 2, True)])
+def test_pipeline_matches_single_process(kind, world, micro, use_links):
+    """Blocking grouped P2P and the asynchronous per-link executor (receives posted before the
+    preceding compute step) both reproduce the single-process gradients."""
     torch.manual_seed(123)
     x = torch.randint(0, TINY["vocab_size"], (6, TINY["ctx_size"]))
     # full-batch reference equals mean of micro-batch losses when micro-batches are equal-sized
@@ -94,8 +99,8 @@ def test_pipeline_matches_single_process(kind, world, micro):
     loss_ref.backward()
     ref = {n: p.grad for n, p in model.named_parameters()}
     with tempfile.TemporaryDirectory() as d:
-        port = 29700 + hash((kind, world, micro)) % 200
-        mp.spawn(_pp_worker, args=(world, port, kind, d, micro), nprocs=world, join=True)
+        port = 29700 + hash((kind, world, micro, use_links)) % 200
+        mp.spawn(_pp_worker, args=(world, port, kind, d, micro, use_links), nprocs=world, join=True)
         res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
     assert abs(res[-1]["loss"] - loss_ref.item()) < 1e-5
     seen = set()
@@ -158,13 +163,14 @@ def _grid_worker(rank, world, port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     from ddl25spring_amd.parallel.dp import GradBucketer
-    from ddl25spring_amd.parallel.pipeline import PipelineStage, grid_ranks
+    from ddl25spring_amd.parallel.pipeline import PipelineStage, grid_ranks, pipeline_links
     from ddl25spring_amd.runtime import dist as rdist
     ctx = rdist.init(backend="gloo", device="cpu")
     dp, pp = 2, 2
     pipe, stage, pipe_ranks, dp_ranks = grid_ranks(rank, dp, pp)
     # collective creation of every DP group, in the same order on all ranks (fixes SURVEY Q2)
     dp_group = ctx.new_groups("dp", [[p * pp + s for p in range(dp)] for s in range(pp)])
+    links = pipeline_links(dp, pp)  # collective: every rank, same order
     torch.manual_seed(0)
     model = LLama(**TINY)
     mod = split_stages(model, pp)[stage]
@@ -174,7 +180,7 @@ def _grid_worker(rank, world, port, out_dir):
     data = torch.randint(0, TINY["vocab_size"], (8, TINY["ctx_size"]))
     mine = data[pipe * 4:(pipe + 1) * 4]
     ps = PipelineStage(mod, stage, pp, ranks=pipe_ranks, act_shape=(2, TINY["ctx_size"], TINY["dmodel"]),
-                       act_dtype=torch.float32, device=torch.device("cpu"))
+                       act_dtype=torch.float32, device=torch.device("cpu"), links=links)
     losses = []
     for it in range(3):
         bk.zero_grad()
