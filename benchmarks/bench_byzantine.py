@@ -1,8 +1,11 @@
 """BASELINE config #4: Byzantine-robust FL — Krum / trimmed-mean / coordinate-median under
 label-flip + sign-flip attackers, 8 clients (ResNet-18, CIFAR-10 shape, the headline workload).
 
-Per aggregator: FedAvg rounds/s and the device time of the aggregation phase (coordinate-sharded
-all-to-all + bitonic selection / fp32-MFMA Gram kernels) under attack, and the robustness itself:
+Per aggregator: FedAvg rounds/s under attack over ``--steps`` (default 10) UNSYNCHRONISED rounds
+(the host enqueues round r+1 while the GPU runs round r, as bench.py's headline does; one device
+sync brackets the timed span), the device time of the aggregation phase (coordinate-sharded
+all-to-all + bitonic selection / fp32-MFMA Gram kernels) from two extra synchronised rounds, the
+same rounds/s of the CLEAN mean run (no attacker) as the yardstick, and the robustness itself:
 test accuracy after ``--acc-rounds`` rounds on the learnable synthetic CIFAR set, clean (no
 attacker) vs attacked, for every aggregator (``--no-eval`` skips the accuracy runs).
 """
@@ -17,13 +20,14 @@ from _common import emit
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", type=int, default=2, help="timed rounds per aggregator")
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10, help="timed (unsynchronised) rounds per aggregator")
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--model", default="resnet18")
     ap.add_argument("--train-size", type=int, default=50000)
     ap.add_argument("--aggregators", default="mean,median,trimmed_mean,krum")
     ap.add_argument("--no-eval", dest="eval", action="store_false")
-    ap.add_argument("--acc-rounds", type=int, default=6, help="rounds before the accuracy test")
+    ap.add_argument("--acc-rounds", type=int, default=16,
+                    help="rounds before the accuracy test (at least the timed run's rounds)")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"])
     args = ap.parse_args()
     from ddl25spring_amd.data.images import DeviceImageDataset, load_images
@@ -55,24 +59,52 @@ def main():
             fa.attack = _Both(make_attack("sign_flip", [2, 3]), make_attack("label_flip", [0, 1]))
         return fa
 
-    for agg in args.aggregators.split(","):
-        fa = make(agg, True)
+    import time
+
+    import torch
+
+    def timed(fa):
+        """rounds/s over args.steps unsynchronised rounds (max over ranks), then the aggregation
+        phase's device time from 2 synchronised rounds."""
         for _ in range(args.warmup):
             fa.round()
-        fa.timer.summary()
-        times, agg_ms = [], []
+        fa.sync_rounds = False
+        if ctx.device.type == "cuda":
+            torch.cuda.synchronize()
+        ctx.barrier()
+        t0 = time.perf_counter()
         for _ in range(args.steps):
-            dt, _ = fa.round()
-            times.append(dt)
+            fa.round()
+        if ctx.device.type == "cuda":
+            torch.cuda.synchronize()
+        ctx.barrier()
+        dt = ctx.max_scalar(time.perf_counter() - t0)
+        fa.sync_rounds = True
+        fa.timer.summary()
+        agg_ms = []
+        for _ in range(2):
+            fa.round()
             agg_ms.append(fa.timer.summary().get("aggregate", float("nan")))
-        res = {"rounds_per_s": round(len(times) / sum(times), 4),
-               "aggregate_ms": round(float(np.mean(agg_ms)), 3)}
+        return args.steps / dt, float(np.mean(agg_ms))
+
+    clean_rps = None
+    if "mean" in args.aggregators.split(","):
+        fa = make("mean", False)
+        clean_rps, _ = timed(fa)
+        del fa
+    for agg in args.aggregators.split(","):
+        fa = make(agg, True)
+        rps, agg_ms = timed(fa)
+        res = {"rounds_per_s": round(rps, 4), "aggregate_ms": round(agg_ms, 3)}
+        if clean_rps:
+            res["vs_clean_mean"] = round(rps / clean_rps, 4)
         if args.eval:
-            for _ in range(args.acc_rounds - args.warmup - args.steps):
+            total = max(args.acc_rounds, fa.round_idx)
+            while fa.round_idx < total:
                 fa.round()
             res["test_accuracy_attacked"] = round(fa.test(), 4)
             clean = make(agg, False)
-            for _ in range(args.acc_rounds):
+            for _ in range(total):
                 clean.round()
             res["test_accuracy_clean"] = round(clean.test(), 4)
             del clean
@@ -82,7 +114,9 @@ def main():
          value=results.get("krum", next(iter(results.values())))["rounds_per_s"], unit="rounds/s",
          n_gpus=ctx.world, steps=args.steps, warmup=args.warmup, higher_is_better=True,
          scaling="strong", vs_baseline=None, dtype=args.precision, data="synthetic",
-         acc_rounds=args.acc_rounds if args.eval else None, per_aggregator=results,
+         acc_rounds=max(args.acc_rounds, args.warmup + args.steps + 2) if args.eval else None,
+         per_aggregator=results,
+         clean_mean_rounds_per_s=None if clean_rps is None else round(clean_rps, 4),
          config={"model": f"{args.model}-{kind}", "global_batch": 800, "seq_len": None,
                  "parallelism": f"fedavg-8clients-dp{ctx.world}"})
     rdist.shutdown()

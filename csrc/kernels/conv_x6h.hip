@@ -445,7 +445,9 @@ static void halo_layout(HaloGeo& h) {
           tot += m;
         }
       const int bytes = nseg * sq * 16;
-      const bool fit = bytes <= HBSMALL;
+      if (bytes > HBLARGE) continue;
+      // the small-LDS instance also holds fewer halo units per thread (HPM 208, convx6h_kernel)
+      const bool fit = bytes <= HBSMALL && h.HP <= 208;
       const int bbytes = nseg * best[3] * 16;
       bool better;
       if (fit != best_fit) better = fit;
@@ -459,7 +461,7 @@ static void halo_layout(HaloGeo& h) {
     }
   h.ROWB = best[2] * 16;
   h.SEGB = best[3] * 16;
-  h.HBYTES = nseg * h.SEGB;
+  h.HBYTES = best[3] ? nseg * h.SEGB : (1 << 30);  // no candidate fits: x6h_geo refuses
 }
 
 static bool x6h_geo(const ConvF32Args& a, int mode, int bp, HaloGeo& h, int& rs) {

@@ -42,11 +42,17 @@ class LabelFlip(Attack):
     def __init__(self, malicious):
         super().__init__(malicious)
         self._masks: dict = {}
+        self._pinned: list = []  # sources of in-flight mask copies (bounded: trimmed below)
+
+    def _trim(self):
+        if len(self._pinned) > 64:
+            del self._pinned[:32]  # copies enqueued 32+ rounds ago have long completed
 
     def label_transform_for(self, slot_clients, num_classes):
         bad = [i for i, c in enumerate(slot_clients) if c in self.malicious]
         if not bad:
             return None
+        self._trim()
         n = len(slot_clients)
         mask_cpu = torch.zeros(n, dtype=torch.bool)
         mask_cpu[bad] = True
@@ -57,7 +63,14 @@ class LabelFlip(Attack):
             if key not in self._masks:
                 self._masks[key] = torch.zeros(n, dtype=torch.bool, device=device)
             if key not in fresh:
-                self._masks[key].copy_(mask_cpu)
+                src = mask_cpu
+                if self._masks[key].is_cuda:
+                    # pinned + non-blocking: a pageable copy would make the host wait for the GPU
+                    # to drain, serialising rounds that otherwise run unsynchronised (the source
+                    # is never written again, so the in-flight copy is safe)
+                    src = mask_cpu.pin_memory()
+                    self._pinned.append(src)
+                self._masks[key].copy_(src, non_blocking=True)
                 fresh.add(key)
             return self._masks[key]
 

@@ -173,3 +173,44 @@ def test_unsynchronised_rounds_match_on_device(cuda):
     step = (ws[0] - w0).norm()
     noise = ((ws[0] - ws[2]).norm() / step).item()
     assert ((ws[0] - ws[1]).norm() / step).item() < 2 * noise + 1e-2
+
+
+class _BothAttacks:
+    """label flip for some clients + sign flip for others (benchmarks/bench_byzantine.py)."""
+
+    def __init__(self, model_attack, data_attack):
+        self.m, self.d = model_attack, data_attack
+
+    def label_transform_for(self, mine, ncls):
+        return self.d.label_transform_for(mine, ncls)
+
+    def skip_training(self, c):
+        return False
+
+    def poison_updates(self, rows, w_global, mine):
+        self.m.poison_updates(rows, w_global, mine)
+
+
+@pytest.mark.parametrize("agg", ["mean", "median"])
+def test_attacked_fp32_graph_unsynced_equals_eager_bitwise(cuda, agg):
+    """The Byzantine bench's configuration at fp32 (deterministic kernels, BN included): label-flip
+    + sign-flip attackers, rounds replayed from the captured round graph AND enqueued without host
+    syncs give exactly the eager synchronised rounds' server model."""
+    import functools
+    from ddl25spring_amd.fl.attacks import make_attack
+    from ddl25spring_amd.models import resnet18_cifar
+    arr = synthetic_images("cifar10", 400, seed=0)
+    parts = split(4, True, 3, labels=arr.labels)
+    ws = []
+    for graph, sync in ((False, True), (True, False)):
+        fa = FedAvg(functools.partial(resnet18_cifar, precision="fp32"), DeviceImageDataset(arr, cuda), parts,
+                    lr=0.02, batch_size=50, client_fraction=1.0, seed=3, ctx=_ctx(cuda), use_graph=graph,
+                    eval_every=0, aggregator=agg,
+                    attack=_BothAttacks(make_attack("sign_flip", [2]), make_attack("label_flip", [0])))
+        fa.sync_rounds = sync
+        for _ in range(3):
+            fa.round()
+        torch.cuda.synchronize()
+        ws.append(fa.w_global.clone())
+    assert torch.isfinite(ws[0]).all()
+    assert torch.equal(ws[0], ws[1])

@@ -51,6 +51,60 @@ def test_two_ranks_one_gpu_match_single_process(cuda):
     assert ((ws[0].to(cuda) - single.w_global).norm() / upd).item() < 2e-2
 
 
+def _worker_r18(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DDL_F32_TARGET_WG="1",
+                      DDL_F32_TUNED="0")
+    from ddl25spring_amd.runtime import dist as rdist
+    ctx = rdist.init(backend="gloo", device="cuda")
+    fa = _r18_fedavg(ctx)
+    fa.round()
+    fa.round()
+    torch.save(fa.w_global.cpu(), os.path.join(out, f"w{rank}.pt"))
+    rdist.shutdown()
+
+
+def _r18_fedavg(ctx):
+    import functools
+    from ddl25spring_amd.models import resnet18_cifar
+    arr = synthetic_images("cifar10", 400, seed=0)
+    parts = split(2, True, 1, labels=arr.labels)
+    return FedAvg(functools.partial(resnet18_cifar, precision="fp32"), DeviceImageDataset(arr, ctx.device),
+                  parts, lr=0.05, batch_size=50, client_fraction=1.0, seed=1, ctx=ctx, eval_every=0)
+
+
+def test_fp32_resnet18_two_ranks_match_single_process(cuda):
+    """The headline workload's multi-rank path at the reference's precision:
+    2 gloo ranks share the GPU, one client slot each, vs one process holding both clients. With
+    split-K pinned off and the tuned-plan table off (DDL_F32_TARGET_WG=1, DDL_F32_TUNED=0, so a
+    client's kernels run the same tiles at G=1 and G=2) the only difference left is the aggregation's rounding (fused multiply-add over the
+    process's clients vs a per-rank product then the all-reduce add): <= 1e-6 relative after two
+    rounds, and both ranks hold the identical server model (same w_global sha256)."""
+    import hashlib
+    from ddl25spring_amd.ops import functional_f32 as F32
+    old, old_tuned = F32.TARGET_WG, F32._TUNED
+    F32.TARGET_WG, F32._TUNED = 1, {}
+    F32._PLANS.clear()
+    try:
+        single = _r18_fedavg(DistContext(device=cuda))
+        w0 = single.w_global.clone()
+        single.round()
+        single.round()
+    finally:
+        F32.TARGET_WG, F32._TUNED = old, old_tuned
+        F32._PLANS.clear()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker_r18, args=(2, 29737, d), nprocs=2, join=True)
+        ws = [torch.load(os.path.join(d, f"w{r}.pt"), weights_only=True) for r in range(2)]
+    shas = [hashlib.sha256(w.numpy().tobytes()).hexdigest() for w in ws]
+    assert shas[0] == shas[1]
+    ref = single.w_global.cpu()
+    rel_w = ((ws[0] - ref).norm() / ref.norm()).item()
+    rel_upd = ((ws[0] - ref).norm() / (ref - w0.cpu()).norm()).item()
+    print(f"fp32 ResNet-18 2-rank vs 1-process: rel(w) {rel_w:.2e}, rel(update) {rel_upd:.2e}")
+    assert rel_w <= 1e-6 and rel_upd < 1e-4, (rel_w, rel_upd)
+
+
 def test_bench_two_ranks_gloo(cuda):
     """bench.py end to end with world 2 (the driver's torchrun path, gloo instead of RCCL)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
