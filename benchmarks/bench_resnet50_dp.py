@@ -25,7 +25,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--pool", type=int, default=1024, help="distinct synthetic images per rank")
-    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--bucket-mb", type=float, default=25.0,
+                    help="bucket ceiling: layer-aligned buckets close at 0.64x (16-25 MB by default)")
     ap.add_argument("--precision", default="fp32", choices=("fp32", "bf16"))
     args = ap.parse_args()
     from ddl25spring_amd.data.images import DeviceImageDataset, ImageArrays
@@ -70,6 +71,7 @@ def main():
          ms_per_step=round(1e3 * dt / args.steps, 3), higher_is_better=True, scaling="weak",
          vs_baseline=None, dtype=args.precision, data="synthetic",
          allreduce_busbw_GBps=None if busbw is None else round(busbw, 1),
+         buckets_mb=[round((hi - lo) * 4 / 2 ** 20, 2) for lo, hi in bk.bounds],
          config={"model": "resnet50-imagenet", "global_batch": ctx.world * args.batch,
                  "seq_len": None, "parallelism": f"dp{ctx.world}", "per_gpu_batch": args.batch})
     rdist.shutdown()

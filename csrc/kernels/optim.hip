@@ -75,19 +75,30 @@ struct AdamArgs {
   // optional device step counter (advanced by ddl_u64_add before the launch): the bias corrections
   // are then computed on the device, so a captured HIP graph stays exact on every replay
   const unsigned long long* step_dev;
+  // > 0: the buffers are rows of row_len elements (client slots of a client-batched model), each
+  // with its OWN device step counter step_dev[row] (clients that joined different numbers of
+  // rounds keep their own bias correction)
+  long long row_len;
 };
 
 __global__ void adam_kernel(AdamArgs a) {
   float bc1 = a.bc1, bc2 = a.bc2;
-  if (a.step_dev) {
+  if (a.step_dev && a.row_len <= 0) {
     const float t = (float)*a.step_dev;
     bc1 = 1.f - powf(a.beta1, t);
     bc2 = 1.f - powf(a.beta2, t);
   }
-  const float sbc2 = sqrtf(bc2);
-  const float step = a.lr / bc1;
+  float sbc2 = sqrtf(bc2);
+  float step = a.lr / bc1;
+  long long row = -1;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < a.n;
        e += (long long)gridDim.x * blockDim.x) {
+    if (a.row_len > 0 && e / a.row_len != row) {
+      row = e / a.row_len;
+      const float t = (float)a.step_dev[row];
+      sbc2 = sqrtf(1.f - powf(a.beta2, t));
+      step = a.lr / (1.f - powf(a.beta1, t));
+    }
     float p = a.p[e];
     float g = a.g[e] * a.grad_scale;
     if (a.decoupled) p *= (1.f - a.lr * a.wd);
@@ -103,6 +114,7 @@ __global__ void adam_kernel(AdamArgs a) {
 }
 
 DDL_API int ddl_adam(const AdamArgs* a, hipStream_t s) {
+  if (a->row_len > 0 && !a->step_dev) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(a->n, 256)), dim3(256), 0, s, *a);
   return (int)hipGetLastError();
 }

@@ -10,22 +10,39 @@ weighted sums of all ranks meet in ONE all-reduce per round over a flat fp32 buf
 drawn from that client's own seeded generator, so the result does not depend on how many ranks
 share the clients: W ranks reproduce the single-process run.
 
-Each client keeps its own Adam moments and step count across rounds (swapped in and out of the
-fused FlatAdam buffers), as a real client device would. On the GPU a client's ``local_steps``
-steps replay from one HIP graph per client (``runtime.graphs.CapturedStep``): the batch indices
-of the round are drawn on the host from the client's seeded generator as before and uploaded into
-a static buffer the graph reads.
+Each client keeps its own Adam moments and step count across rounds, as a real client device
+would.
+
+Client-batched engine (``batched``, the default on the GPU): all of a rank's clients of the round
+train TOGETHER — G and D hold S client slots ([S, ...] slot tensors, models.dcgan.Grouped*), every
+layer of every client is ONE grouped launch (ops/grouped.py), one SlotAdam launch steps all slots
+with per-client step counters, and the round's ``local_steps`` steps of all slots replay from ONE
+HIP graph per slot count. Batch indices / noise are drawn per client from the same seeded
+generators as the sequential engine (so both engines train the same clients on the same data),
+uploaded once per round; download, weighted aggregation and the all-reduce stay on the device over
+the flat (G | D | BN) buffers, with one host sync per round (wall time and the loss log). Adam state
+stays in its slot while the slot keeps its client (client_fraction 1: never copied).
+
+Sequential engine (``batched=False``; the CPU default): one client after another through a single
+(G, D) pair, its Adam state swapped in and out of the fused FlatAdam buffers; on the GPU each
+client's steps replay from one HIP graph per client.
 """
 from __future__ import annotations
 
+import math
 import time
+import warnings
 from dataclasses import dataclass, field
 
 import numpy as np
 import torch
 
-from ..models.dcgan import Discriminator, GANTrainer, Generator
+from ..models.dcgan import (Discriminator, GANTrainer, Generator, GroupedDiscriminator, GroupedGANTrainer,
+                            GroupedGenerator)
 from ..runtime.graphs import CapturedStep
+
+# the slot tensors' gradients are strided rows of SlotAdam's [S, P] buffer (CPU autograd path)
+warnings.filterwarnings("ignore", message="grad and param do not obey the gradient layout contract")
 
 
 @dataclass
@@ -44,11 +61,25 @@ def _flat_buffers(mods):
     return [b for m in mods for b in m.buffers() if b.dtype.is_floating_point]
 
 
+def _row_params(row, mod, slot_opt):
+    """Inverse of _param_row: the parameters of a SlotAdam row, concatenated without gaps."""
+    return torch.cat([row[off:off + p.numel()] for p, off in
+                      zip([p for p in mod.parameters() if p.requires_grad], slot_opt.offsets)])
+
+
+def _param_row(mod, slot_opt):
+    """A single module's parameters in a SlotAdam row layout (CPU torch.optim path)."""
+    row = torch.zeros(slot_opt.P, dtype=torch.float32, device=slot_opt.data.device)
+    for p, off in zip([p for p in mod.parameters() if p.requires_grad], slot_opt.offsets):
+        row[off:off + p.numel()] = p.detach().reshape(-1)
+    return row
+
+
 class FederatedGAN:
     def __init__(self, client_data: list[torch.Tensor], ctx=None, nz: int = 100, ngf: int = 64,
                  ndf: int = 64, lr: float = 2e-4, betas=(0.5, 0.999), local_steps: int = 10,
                  batch_size: int = 64, client_fraction: float = 1.0, seed: int = 0, device=None,
-                 use_graph: bool = True):
+                 use_graph: bool = True, batched: bool | None = None):
         self.ctx = ctx
         self.rank = ctx.rank if ctx else 0
         self.world = ctx.world if ctx else 1
@@ -72,6 +103,9 @@ class FederatedGAN:
         self._z: dict = {}      # client -> static [local_steps, batch, nz] generator noise buffer
         self._graphs: dict = {}  # client -> CapturedStep over its local steps
         self.round_idx = 0       # rounds done (seeds the per-round client generators)
+        self.batched = (self.device.type == "cuda") if batched is None else bool(batched)
+        if self.batched:
+            self._init_batched(lr, betas)
 
     # ---------------------------------------------------------------------------------------
     def _global_tensors(self):
@@ -128,9 +162,172 @@ class FederatedGAN:
             ld, lg = self.trainer.step(data.index_select(0, idx[i]), z=z[i])
         return ld, lg
 
+    # ------------------------------------------------------------------ client-batched engine
+    def _init_batched(self, lr, betas):
+        S = self.S = math.ceil(self.K / self.world)
+        self.gG = GroupedGenerator(self.G, S).to(self.device)
+        self.gD = GroupedDiscriminator(self.D, S).to(self.device)
+        self.gtr = GroupedGANTrainer(self.gG, self.gD, S, lr, tuple(betas))
+        # this rank's clients (client c lives on rank c % world) in one device tensor: a slot's batch
+        # is a row gather with the client's offset folded into the uploaded indices
+        self._mine_all = [c for c in range(len(self.data)) if c % self.world == self.rank]
+        self._off = {}
+        off = 0
+        for c in self._mine_all:
+            self._off[c] = off
+            off += len(self.data[c])
+        self._cat = torch.cat([self.data[c] for c in self._mine_all]) if self._mine_all else None
+        self._slot_clients = [None] * S
+        self._bidx: dict = {}
+        self._bz: dict = {}
+        self._bgraphs: dict = {}
+        self._gbufs = _flat_buffers([self.gG, self.gD])
+        self._bufs = _flat_buffers([self.G, self.D])
+
+    def _row_global(self, row, mod, slot_opt):
+        """A slot-row vector in ``_flat``'s layout: the FlatAdam buffer itself on the device (same
+        aligned layout), the gap-free parameter concatenation with torch.optim on the CPU."""
+        opt = self.optG if mod is self.G else self.optD
+        return row if hasattr(opt, "data") else _row_params(row, mod, slot_opt)
+
+    def _slot_state_out(self, i):
+        """Slot i's Adam state -> its client's entry of ``_state`` (the sequential engine's format)."""
+        c = self._slot_clients[i]
+        if c is None:
+            return
+        oG, oD = self.gtr.optG, self.gtr.optD
+        tdev = [None if o.t_dev is None else o.t_dev[i:i + 1].clone() for o in (oG, oD)]
+        self._state[c] = (oG.m[i].clone(), oG.v[i].clone(), oG.t[i], oD.m[i].clone(), oD.v[i].clone(), oD.t[i],
+                          *tdev)
+
+    def _assign_slots(self, mine):
+        """Slot order for this round's clients: a client already resident in one of the first
+        len(mine) slots stays there (its Adam state is not copied); the others fill the free ones.
+        Every displaced slot's state is written back BEFORE any slot loads (a client may move)."""
+        G = len(mine)
+        order = [None] * G
+        rest = []
+        for c in mine:
+            i = self._slot_clients.index(c) if c in self._slot_clients else -1
+            if 0 <= i < G:
+                order[i] = c
+            else:
+                rest.append(c)
+        free = [i for i in range(G) if order[i] is None]
+        for i, c in zip(free, rest):
+            order[i] = c
+        for i in range(self.S):
+            cur = self._slot_clients[i]
+            if cur is not None and (i >= G or order[i] != cur):
+                self._slot_state_out(i)
+                self._slot_clients[i] = None
+        for i, c in enumerate(order):
+            self._slot_state_in(i, c)
+        return order
+
+    def _slot_state_in(self, i, c):
+        if self._slot_clients[i] == c:
+            return  # the slot still holds this client's state
+        st = self._state.get(c)
+        for o, j in ((self.gtr.optG, 0), (self.gtr.optD, 3)):
+            if st is None:
+                o.m[i].zero_(); o.v[i].zero_(); o.t[i] = 0
+                if o.t_dev is not None:
+                    o.t_dev[i].zero_()
+            else:
+                o.m[i].copy_(st[j]); o.v[i].copy_(st[j + 1]); o.t[i] = st[j + 2]
+                if o.t_dev is not None:
+                    o.t_dev[i:i + 1].copy_(st[6 + j // 3])
+        self._slot_clients[i] = c
+
+    def flush_slots(self):
+        """Write every slot's Adam state back to ``_state`` (checkpointing)."""
+        if not self.batched:
+            return
+        for i in range(self.S):
+            self._slot_state_out(i)
+        for o, j in ((self.gtr.optG, 2), (self.gtr.optD, 5)):
+            if o.t_dev is not None:  # graph replays advance only the device counters
+                for c, st in list(self._state.items()):
+                    if st[6 + j // 3] is not None:
+                        self._state[c] = tuple(int(st[6 + j // 3].item()) if k == j else v for k, v in enumerate(st))
+
+    def _batched_local(self, G):
+        idx, z = self._bidx[G], self._bz[G]
+        B = self.batch_size
+        ld = lg = None
+        for i in range(self.local_steps):
+            real = self._cat.index_select(0, idx[i]).view(G, B, *self._cat.shape[1:])
+            ld, lg = self.gtr.step(real, z[i])
+        return ld, lg
+
+    def _round_batched(self, res):
+        r = self.round_idx
+        t0 = time.perf_counter()
+        chosen = self.rng.choice(len(self.data), self.K, replace=False)
+        mine = [int(c) for c in chosen if c % self.world == self.rank]
+        G = len(mine)
+        wsum = self.n[chosen].sum()
+        oG, oD = self.gtr.optG, self.gtr.optD
+        if G:
+            with torch.no_grad():  # download the global model into the slots in use
+                oG.data[:G].copy_(self.optG.data if hasattr(self.optG, "data") else _param_row(self.G, oG))
+                oD.data[:G].copy_(self.optD.data if hasattr(self.optD, "data") else _param_row(self.D, oD))
+                for gb, b in zip(self._gbufs, self._bufs):
+                    gb[:G].copy_(b)
+            oG.sync_shadow()
+            oD.sync_shadow()
+            mine = self._assign_slots(mine)
+            B, nz = self.batch_size, self.G.nz
+            idx = torch.empty(self.local_steps, G * B, dtype=torch.int64)
+            z = torch.empty(self.local_steps, G, B, nz)
+            for i, c in enumerate(mine):
+                # the sequential engine's per-(round, client) stream: same batches, same noise
+                g = torch.Generator(device="cpu").manual_seed(self.seed + c + 1 + r * len(self.data))
+                n_c = len(self.data[c])
+                idx[:, i * B:(i + 1) * B] = torch.stack([torch.randint(0, n_c, (B,), generator=g)
+                                                         for _ in range(self.local_steps)]) + self._off[c]
+                z[:, i] = torch.randn(self.local_steps, B, nz, generator=g)
+            if G not in self._bidx:
+                self._bidx[G] = torch.empty_like(idx, device=self.device)
+                self._bz[G] = torch.empty_like(z, device=self.device)
+            self._bidx[G].copy_(idx, non_blocking=False)
+            self._bz[G].copy_(z, non_blocking=False)
+            if self.use_graph:
+                if G not in self._bgraphs:
+                    self._bgraphs[G] = CapturedStep(lambda G=G: self._batched_local(G), warmup=1)
+                ld, lg = self._bgraphs[G]()
+            else:
+                ld, lg = self._batched_local(G)
+            res.samples += self.batch_size * self.local_steps * G
+            coef = torch.tensor(self.n[mine] / wsum, dtype=torch.float32, device=self.device).view(G, 1)
+            with torch.no_grad():
+                parts = [self._row_global((coef * oG.data[:G]).sum(0), self.G, oG),
+                         self._row_global((coef * oD.data[:G]).sum(0), self.D, oD)]
+                parts += [(coef.view(G, *([1] * (gb.dim() - 1))) * gb[:G]).sum(0).reshape(-1) for gb in self._gbufs]
+                acc = torch.cat(parts)
+        else:
+            acc = torch.zeros_like(self._flat())
+            ld = lg = None
+        if self.ctx and self.world > 1:
+            self.ctx.all_reduce(acc)
+        self._load_flat(acc)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
+        res.wall_time.append(time.perf_counter() - t0)
+        # the grouped losses are sums over the slots' own mean losses: / G = the clients' mean
+        res.loss_d.append(float(ld) / G if G else 0.0)
+        res.loss_g.append(float(lg) / G if G else 0.0)
+        res.rounds += 1
+        self.round_idx += 1
+
     # ---------------------------------------------------------------------------------------
     def run(self, rounds: int) -> GANRunResult:
         res = GANRunResult()
+        if self.batched:
+            for _ in range(rounds):
+                self._round_batched(res)
+            return res
         for _ in range(rounds):
             r = self.round_idx
             t0 = time.perf_counter()
@@ -180,9 +377,10 @@ class FederatedGAN:
     def state_dict(self) -> dict:
         """This rank's shard: the global (G | D | BN) weights and the sampling stream (identical on
         every rank), and the Adam state of the clients that live on this rank."""
+        self.flush_slots()
         clients = {}
         for c, st in self._state.items():
-            if hasattr(self.optG, "m"):
+            if self.batched or hasattr(self.optG, "m"):
                 clients[int(c)] = {"mG": st[0], "vG": st[1], "tG": st[2], "mD": st[3], "vD": st[4],
                                    "tD": st[5]}
             else:
@@ -195,12 +393,15 @@ class FederatedGAN:
         self.round_idx = int(sd["round"])
         self.rng.bit_generator.state = sd["rng"]
         self._state = {}
+        if self.batched:
+            self._slot_clients = [None] * self.S  # slots reload their clients from _state
         for c, st in sd["clients"].items():
             if "G" in st:
                 self._state[int(c)] = (st["G"], None, None, st["D"], None, None)
                 continue
             dev = self.device
-            tdev = [torch.tensor([t], dtype=torch.int64, device=dev) if o.t_dev is not None else None
-                    for t, o in ((st["tG"], self.optG), (st["tD"], self.optD))]
+            opts = (self.gtr.optG, self.gtr.optD) if self.batched else (self.optG, self.optD)
+            tdev = [torch.tensor([t], dtype=torch.int64, device=dev) if getattr(o, "t_dev", None) is not None
+                    else None for t, o in zip((st["tG"], st["tD"]), opts)]
             self._state[int(c)] = (st["mG"].to(dev), st["vG"].to(dev), int(st["tG"]),
                                    st["mD"].to(dev), st["vD"].to(dev), int(st["tD"]), *tdev)

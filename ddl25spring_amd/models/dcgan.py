@@ -135,3 +135,103 @@ class GANTrainer:
         lossG.backward()
         self.optG.step()
         return lossD.detach(), lossG.detach()
+
+
+# ------------------------------------------------------------------------- client-batched
+def _slots(t: torch.Tensor, S: int) -> torch.Tensor:
+    return t.detach().unsqueeze(0).repeat(S, *([1] * t.dim())).clone()
+
+
+class _GBN(nn.Module):
+    def __init__(self, bn: _BN, S: int):
+        super().__init__()
+        self.weight = nn.Parameter(_slots(bn.weight, S))
+        self.bias = nn.Parameter(_slots(bn.bias, S))
+        self.register_buffer("running_mean", _slots(bn.running_mean, S))
+        self.register_buffer("running_var", _slots(bn.running_var, S))
+
+    def forward(self, x, act, stats=None):
+        from ..ops import grouped as Gp
+        return Gp.batch_norm_act(x, self.weight, self.bias, self.running_mean, self.running_var, self.training,
+                                 act=act, stats=stats)
+
+
+class GroupedGenerator(nn.Module):
+    """S client copies of a Generator as slot tensors [S, ...]: z [G, N, nz] -> [G, N, 32, 32, nc_pad]
+    for the first G slots, every layer one client-batched launch (ops/grouped.py). Parameter and
+    buffer order match ``Generator``, so a slot row has a single generator's flat layout."""
+
+    def __init__(self, gen: Generator, S: int):
+        super().__init__()
+        self.nz, self.nz_pad, self.nc, self.nc_pad, self.ngf = gen.nz, gen.nz_pad, gen.nc, gen.nc_pad, gen.ngf
+        self.proj = nn.Parameter(_slots(gen.proj, S))
+        self.bn0 = _GBN(gen.bn0, S)
+        self.up1 = nn.Parameter(_slots(gen.up1, S))
+        self.bn1 = _GBN(gen.bn1, S)
+        self.up2 = nn.Parameter(_slots(gen.up2, S))
+        self.bn2 = _GBN(gen.bn2, S)
+        self.up3 = nn.Parameter(_slots(gen.up3, S))
+
+    def forward(self, z):
+        from ..ops import grouped as Gp
+        G, N = z.shape[:2]
+        if z.shape[2] != self.nz_pad:
+            z = torch.cat([z, z.new_zeros(G, N, self.nz_pad - z.shape[2])], 2)
+        h = Gp.linear(z, self.proj).view(G, N, 4, 4, 4 * self.ngf)
+        h = self.bn0(h, "relu")
+        h = self.bn1(Gp.conv_transpose2d(h, self.up1, 2, 1), "relu")
+        h = self.bn2(Gp.conv_transpose2d(h, self.up2, 2, 1), "relu")
+        return A.activation(Gp.conv_transpose2d(h, self.up3, 2, 1), "tanh")
+
+
+class GroupedDiscriminator(nn.Module):
+    """S client copies of a Discriminator: [G, N, 32, 32, nc_pad] -> logits [G, N, 32]."""
+
+    def __init__(self, disc: Discriminator, S: int):
+        super().__init__()
+        self.nc, self.nc_pad, self.ndf = disc.nc, disc.nc_pad, disc.ndf
+        self.c0 = nn.Parameter(_slots(disc.c0, S))
+        self.c1 = nn.Parameter(_slots(disc.c1, S))
+        self.bn1 = _GBN(disc.bn1, S)
+        self.c2 = nn.Parameter(_slots(disc.c2, S))
+        self.bn2 = _GBN(disc.bn2, S)
+        self.head = nn.Parameter(_slots(disc.head, S))
+
+    def forward(self, x):
+        from ..ops import grouped as Gp
+        G, N = x.shape[:2]
+        h = A.activation(Gp.conv2d(x, self.c0, 2, 1), "leaky_relu")
+        y, st = Gp.conv2d(h, self.c1, 2, 1, with_stats=True)
+        h = self.bn1(y, "leaky_relu", st)
+        y, st = Gp.conv2d(h, self.c2, 2, 1, with_stats=True)
+        h = self.bn2(y, "leaky_relu", st)
+        return Gp.linear(h.reshape(G, N, -1), self.head)
+
+
+class GroupedGANTrainer:
+    """One (D, G) step pair for the first G client slots at once: per-client non-saturating losses
+    (the grouped BCE sums each client's own mean), SlotAdam per network (one launch each, per-client
+    step counters)."""
+
+    def __init__(self, gen: GroupedGenerator, disc: GroupedDiscriminator, S: int, lr: float = 2e-4,
+                 betas=(0.5, 0.999)):
+        from ..optim import SlotAdam
+        self.G, self.D = gen, disc
+        cuda = gen.proj.is_cuda
+        self.optG = SlotAdam(gen.parameters(), S, lr=lr, betas=betas, bf16_shadow=cuda)
+        self.optD = SlotAdam(disc.parameters(), S, lr=lr, betas=betas, bf16_shadow=cuda)
+
+    def step(self, real, z):
+        """real [G, N, 32, 32, nc_pad], z [G, N, nz] -> (sum of the clients' D losses, of G losses)."""
+        from ..ops import grouped as Gp
+        G = real.shape[0]
+        self.optD.zero_grad()
+        fake = self.G(z)
+        lossD = Gp.bce_with_logits(self.D(real), 1.0) + Gp.bce_with_logits(self.D(fake.detach()), 0.0)
+        lossD.backward()
+        self.optD.step(G)
+        self.optG.zero_grad()
+        lossG = Gp.bce_with_logits(self.D(fake), 1.0)
+        lossG.backward()
+        self.optG.step(G)
+        return lossD.detach(), lossG.detach()

@@ -110,7 +110,7 @@ class AdamArgs(ctypes.Structure):
     _fields_ = [("p", vp), ("g", vp), ("m", vp), ("v", vp), ("shadow", vp), ("n", i64),
                 ("lr", f32), ("beta1", f32), ("beta2", f32), ("eps", f32), ("wd", f32),
                 ("grad_scale", f32), ("bc1", f32), ("bc2", f32), ("decoupled", i32),
-                ("amsgrad_unused", i32), ("step_dev", vp)]
+                ("amsgrad_unused", i32), ("step_dev", vp), ("row_len", i64)]
 
 
 _SIGS = {

@@ -1207,10 +1207,18 @@ def sgd_direct_step(p, g, shadow, dmap, lr: float, grad_scale: float = 1.0):
 
 
 def adam_step(p, g, m, v, shadow, lr, beta1, beta2, eps, wd, step, decoupled, grad_scale=1.0,
-              step_dev=None):
+              step_dev=None, row_len: int = 0):
     """One fused Adam/AdamW pass over flat buffers. ``step_dev`` (int64 [1] on the device, already
-    advanced to this step) makes the bias correction device-side (HIP-graph capturable)."""
+    advanced to this step) makes the bias correction device-side (HIP-graph capturable).
+    ``row_len`` > 0: the buffers are rows of that many elements with one step counter each
+    (``step_dev`` [rows]; ``step`` is then a per-row host list on the CPU path)."""
     if not p.is_cuda:
+        if row_len > 0:
+            for r, t in enumerate(step):
+                sl = slice(r * row_len, (r + 1) * row_len)
+                ref.adam(p[sl], g[sl], m[sl], v[sl], None if shadow is None else shadow[sl], lr, beta1, beta2,
+                         eps, wd, t, decoupled, grad_scale)
+            return
         ref.adam(p, g, m, v, shadow, lr, beta1, beta2, eps, wd, step, decoupled, grad_scale)
         return
     a = _lib.AdamArgs()
@@ -1218,8 +1226,12 @@ def adam_step(p, g, m, v, shadow, lr, beta1, beta2, eps, wd, step, decoupled, gr
     a.n = p.numel()
     a.lr, a.beta1, a.beta2, a.eps, a.wd, a.grad_scale = lr, beta1, beta2, eps, wd, grad_scale
     a.bc1, a.bc2 = 1 - beta1 ** step, 1 - beta2 ** step
+    if row_len > 0:
+        a.bc1 = a.bc2 = 1.0
+        assert step_dev is not None and step_dev.numel() * row_len == p.numel()
     a.decoupled = int(decoupled)
     a.step_dev = ptr(step_dev)
+    a.row_len = int(row_len)
     check(_lib.kernels().ddl_adam(ctypes.byref(a), stream()), "adam")
 
 

@@ -200,6 +200,69 @@ class FlatAdam:
                      step_dev=self.t_dev)
 
 
+class SlotAdam:
+    """Adam for CLIENT-BATCHED ``nn.Module`` parameters: every parameter is [S, *shape] (slot s =
+    one client's copy). Storage is slot-major ``data[S, P]`` (a row = one client's whole model, the
+    parameters are strided views of it, rows aligned like ``FlatAdam``'s flat buffer so a row has
+    exactly a single-client FlatAdam's layout), and each row has its own device step counter, so
+    clients that joined different numbers of rounds keep their own bias correction while ONE fused
+    launch steps the first ``rows`` slots (csrc/kernels/optim.hip adam_kernel, row_len > 0).
+    Backward accumulates weight gradients straight into the slot rows (``_ddl_fuse_grad``,
+    ops/grouped.py). ``bf16_shadow``: a bf16 image of the rows, refreshed by the same launch, is
+    what the bf16 MFMA ops read."""
+
+    def __init__(self, params, slots: int, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0, bf16_shadow: bool = False):
+        self.params = [p for p in params if p.requires_grad]
+        S = self.S = slots
+        dev = self.params[0].device
+        self.offsets, n = [], 0
+        for p in self.params:
+            if p.shape[0] != S:
+                raise ValueError(f"SlotAdam: parameter of shape {tuple(p.shape)} is not [{S}, ...]")
+            self.offsets.append(n)
+            n += (p[0].numel() + 63) // 64 * 64
+        self.P = n
+        self.data = torch.zeros(S, n, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros_like(self.data)
+        self.m = torch.zeros_like(self.data)
+        self.v = torch.zeros_like(self.data)
+        self.shadow = torch.empty(S, n, dtype=torch.bfloat16, device=dev) \
+            if bf16_shadow and dev.type == "cuda" else None
+        with torch.no_grad():
+            for p, off in zip(self.params, self.offsets):
+                k = p[0].numel()
+                self.data[:, off:off + k].copy_(p.detach().reshape(S, k))
+                p.data = self.data[:, off:off + k].view(p.shape)
+                p.grad = self.grad[:, off:off + k].view(p.shape)
+                p._ddl_fuse_grad = True
+                if self.shadow is not None:
+                    p._ddl_bf16 = self.shadow[:, off:off + k].view(p.shape)
+        self.sync_shadow()
+        self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
+        self.t = [0] * S  # host step counts (CPU path; the device path reads t_dev)
+        self.t_dev = torch.zeros(S, dtype=torch.int64, device=dev) if dev.type == "cuda" else None
+
+    def sync_shadow(self):
+        if self.shadow is not None:
+            Fn.to_bf16(self.data, out=self.shadow)
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    @torch.no_grad()
+    def step(self, rows: int | None = None):
+        r = self.S if rows is None else rows
+        for i in range(r):
+            self.t[i] += 1
+        if self.t_dev is not None:
+            self.t_dev[:r].add_(1)
+        Fn.adam_step(self.data[:r].reshape(-1), self.grad[:r].reshape(-1), self.m[:r].reshape(-1),
+                     self.v[:r].reshape(-1), None if self.shadow is None else self.shadow[:r].reshape(-1),
+                     self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay, self.t[:r], False,
+                     step_dev=None if self.t_dev is None else self.t_dev[:r], row_len=self.P)
+
+
 class FlatAdamW(FlatAdam):
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.01):

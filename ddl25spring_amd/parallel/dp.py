@@ -133,7 +133,11 @@ class GradBucketer:
 class NativeGradBucketer:
     """Bucketed, backward-overlapped all-reduce of a native Net's flat ``store.grad``."""
 
-    def __init__(self, net, ctx, group=None, bucket_mb: float = 64.0):
+    def __init__(self, net, ctx, group=None, bucket_mb: float = 25.0):
+        """Buckets of whole layers, closed once they reach 0.64 x ``bucket_mb`` walking backward (so
+        with layers under ~9 MB, ResNet-50's largest, the default gives 16-25 MB buckets: few
+        enough for per-call overheads, small enough that the first all-reduce starts early in
+        the backward and the last one after the final layer is short)."""
         self.net, self.ctx, self.group = net, ctx, group
         self.world = dist.get_world_size(group) if ctx.is_distributed else 1
         st = net.store
@@ -148,7 +152,7 @@ class NativeGradBucketer:
             else:
                 spans.append(None)
         self.spans = spans
-        cap = int(bucket_mb * 2 ** 20) // 4
+        cap = int(0.64 * bucket_mb * 2 ** 20) // 4
         # buckets cut at layer boundaries, walking backward (ready order)
         self.bounds = []
         hi_open, acc = None, 0

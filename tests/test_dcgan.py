@@ -115,3 +115,66 @@ def test_federated_gan_cpu_and_fedavg_identity():
     fg1.run(1)
     assert not torch.equal(before, fg1._flat())
 
+
+
+@pytest.mark.parametrize("fraction,nclients", [(1.0, 3), (0.5, 4)])
+def test_batched_gan_engine_matches_sequential_cpu(fraction, nclients):
+    """Client-batched engine (all of a rank's clients in grouped launches, SlotAdam with per-client
+    step counters, slot-resident Adam state) vs the sequential per-client engine: same clients,
+    batches and noise, so the same model up to Adam rounding (torch.optim.Adam vs the fused
+    formula); with client_fraction 0.5 clients move between slots across rounds."""
+    from ddl25spring_amd.fl.gan import FederatedGAN
+    torch.manual_seed(0)
+    data = [to_nhwc_padded(torch.rand(40, 3, 32, 32) * 2 - 1) for _ in range(nclients)]
+    out = []
+    for batched in (False, True):
+        fg = FederatedGAN(data, ngf=32, ndf=32, local_steps=2, batch_size=8, seed=1, device="cpu",
+                          client_fraction=fraction, batched=batched)
+        res = fg.run(3)
+        assert res.samples == 3 * fg.K * 2 * 8
+        out.append((fg._flat().clone(), res.loss_d, fg))
+    a, b = out[0][0], out[1][0]
+    assert ((a - b).norm() / a.norm()).item() < 1e-4
+    assert np.allclose(out[0][1], out[1][1], rtol=1e-4)
+    # every client's Adam state (incl. step count) is the sequential engine's
+    fs, fb = out[0][2], out[1][2]
+    fb.flush_slots()
+    assert set(fs._state) == set(fb._state)
+    for c in fs._state:
+        assert fb._state[c][2] == fs._state[c][0]["state"][0]["step"].item()
+
+
+def test_batched_gan_checkpoint_resume_cpu():
+    """state_dict flushes the slot-resident Adam state: a resumed batched run equals an
+    uninterrupted one."""
+    from ddl25spring_amd.fl.gan import FederatedGAN
+    torch.manual_seed(0)
+    data = [to_nhwc_padded(torch.rand(32, 3, 32, 32) * 2 - 1) for _ in range(4)]
+    kw = dict(ngf=32, ndf=32, local_steps=2, batch_size=8, seed=5, device="cpu", client_fraction=0.5, batched=True)
+    full = FederatedGAN(data, **kw)
+    full.run(4)
+    part = FederatedGAN(data, **kw)
+    part.run(2)
+    sd = part.state_dict()
+    resumed = FederatedGAN(data, **kw)
+    resumed.load_state_dict(sd)
+    resumed.run(2)
+    assert torch.equal(full._flat(), resumed._flat())
+
+
+@pytest.mark.gpu
+def test_batched_gan_engine_matches_sequential_gpu(cuda):
+    """On the device: the client-batched engine (one grouped launch per layer for all clients, one
+    graph replay per round) vs the sequential engine, bf16 tolerance (grouped vs per-client tile
+    plans round the bf16 GEMMs differently)."""
+    from ddl25spring_amd.fl.gan import FederatedGAN
+    torch.manual_seed(0)
+    data = [to_nhwc_padded(torch.rand(64, 3, 32, 32) * 2 - 1).to(cuda) for _ in range(3)]
+    flats = []
+    for batched in (False, True):
+        fg = FederatedGAN(data, ngf=32, ndf=32, local_steps=2, batch_size=16, seed=1, device=cuda, batched=batched)
+        w0 = fg._flat().clone()
+        fg.run(2)
+        flats.append(fg._flat().clone())
+    upd = (flats[0] - w0).norm()
+    assert ((flats[1] - flats[0]).norm() / upd).item() < 5e-2

@@ -44,16 +44,21 @@ def test_captured_step_matches_eager(cuda):
     assert abs(lg.item() - le.item()) < 1e-4
 
 
-def test_federated_gan_graphs_keep_client_adam_state(cuda):
+@pytest.mark.parametrize("batched", [False, True])
+def test_federated_gan_graphs_keep_client_adam_state(cuda, batched):
     """Two clients, three rounds (eager, capture, replay): finite losses, and each client's
-    restored device step counter continues from its own count (3 rounds x 2 local steps)."""
+    restored device step counter continues from its own count (3 rounds x 2 local steps). The
+    client-batched engine runs a round's 2 clients as ONE graph replay."""
     from ddl25spring_amd.fl.gan import FederatedGAN
     from ddl25spring_amd.models.dcgan import to_nhwc_padded
     torch.manual_seed(0)
     data = [to_nhwc_padded(torch.rand(48, 3, 32, 32) * 2 - 1).to(cuda) for _ in range(2)]
-    fg = FederatedGAN(data, ngf=32, ndf=32, local_steps=2, batch_size=8, seed=1, device=cuda)
+    fg = FederatedGAN(data, ngf=32, ndf=32, local_steps=2, batch_size=8, seed=1, device=cuda, batched=batched)
     assert fg.use_graph
     res = fg.run(3)
+    fg.flush_slots()
+    if batched:
+        assert list(fg._bgraphs) == [2] and fg._bgraphs[2].calls == 3 and fg._bgraphs[2].graph is not None
     assert res.rounds == 3 and res.samples == 3 * 2 * 2 * 8
     assert all(torch.isfinite(torch.tensor(res.loss_d))) and all(torch.isfinite(torch.tensor(res.loss_g)))
     for c in (0, 1):
