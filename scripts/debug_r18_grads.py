@@ -15,22 +15,37 @@ from test_fp32_gpu import _err, _resnet_pair  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--halo", type=int, default=1)
 ap.add_argument("--math", default="x6")
+ap.add_argument("--groups", type=int, default=2)
+ap.add_argument("--batch", type=int, default=16)
+ap.add_argument("--target-wg", type=int, default=0)
+ap.add_argument("--quiet", action="store_true", help="only the worst error and the BAD parameters")
 a = ap.parse_args()
+if a.target_wg:
+    F32.TARGET_WG = a.target_wg
 F32.set_math(a.math)
 F32.set_halo(bool(a.halo))
 cuda = torch.device("cuda")
-tm, net, mapping, convert = _resnet_pair(cuda, G=2)
+G = a.groups
+tm, net, mapping, convert = _resnet_pair(cuda, G=G)
 torch.manual_seed(1)
-x = torch.randn(16, 3, 32, 32)
-y = torch.randint(0, 10, (16,))
+x = torch.randn(a.batch, 3, 32, 32)
+y = torch.randint(0, 10, (a.batch,))
 net.store.zero_grad()
 xin = net.prepare_input(x.to(cuda))
-loss, _ = net.train_step(torch.cat([xin, xin]), torch.stack([y, y]).to(cuda, torch.int32))
+loss, _ = net.train_step(torch.cat([xin] * G), torch.stack([y] * G).to(cuda, torch.int32))
 t64 = tm.double()
 lt = F.cross_entropy(t64(x.double()), y)
 lt.backward()
-print(f"halo={a.halo} math={a.math} loss {loss[0].item():.8f} ref {lt.item():.8f}")
-g = convert.export_torch(net, t64, mapping, group=0, grads=True)
-for name, p in t64.named_parameters():
-    e = _err(g[name], p.grad)
-    print(f"  {name:40s} {e:.2e} {'BAD' if e > 1e-4 else ''}")
+print(f"G={G} B={a.batch} twg={a.target_wg} halo={a.halo} math={a.math} loss {loss[0].item():.8f} "
+      f"ref {lt.item():.8f}")
+for grp in range(G):
+    g = convert.export_torch(net, t64, mapping, group=grp, grads=True)
+    worst, bad = 0.0, []
+    for name, p in t64.named_parameters():
+        e = _err(g[name], p.grad)
+        worst = max(worst, e)
+        if e > 1e-4:
+            bad.append(f"{name}:{e:.1e}")
+        if not a.quiet:
+            print(f"  {name:40s} {e:.2e} {'BAD' if e > 1e-4 else ''}")
+    print(f"  group {grp}: worst {worst:.2e}; {len(bad)} bad: {' '.join(bad[:12])}")
