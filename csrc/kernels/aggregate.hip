@@ -22,16 +22,20 @@ __global__ void weighted_sum_kernel(const float* __restrict__ src, long long ld,
     const long long e = t * 4;
     if (e + 4 <= n && (ld % 4) == 0) {
       float4 acc = accumulate ? *(const float4*)(out + e) : make_float4(0, 0, 0, 0);
+      // products rounded, then added in client order (no fused multiply-add): the same bits as
+      // clients spread over ranks (each rank's product, then the all-reduce add) for 2 ranks, and
+      // the reference's sum of n_k/n-scaled state dicts (hfl_complete.py:370-378)
       for (int g = 0; g < G; ++g) {
         const float c = coeff[g];
         const float4 v = *(const float4*)(src + g * ld + e);
-        acc.x += c * v.x; acc.y += c * v.y; acc.z += c * v.z; acc.w += c * v.w;
+        acc.x = __fadd_rn(acc.x, __fmul_rn(c, v.x)); acc.y = __fadd_rn(acc.y, __fmul_rn(c, v.y));
+        acc.z = __fadd_rn(acc.z, __fmul_rn(c, v.z)); acc.w = __fadd_rn(acc.w, __fmul_rn(c, v.w));
       }
       *(float4*)(out + e) = acc;
     } else {
       for (long long k = e; k < min(n, e + 4); ++k) {
         float acc = accumulate ? out[k] : 0.f;
-        for (int g = 0; g < G; ++g) acc += coeff[g] * src[g * ld + k];
+        for (int g = 0; g < G; ++g) acc = __fadd_rn(acc, __fmul_rn(coeff[g], src[g * ld + k]));
         out[k] = acc;
       }
     }
