@@ -38,6 +38,13 @@ struct ConvF32Args {
   // [G][K][R][S][C] or DGRAD layout [G][C][R][S][K], 8 bytes per element (group stride ws_gs bytes)
   const void* wsplit;
   long long ws_gs;
+  // DGRAD (conv_x6h): the dY operand is the BN backward of the following BN, applied on the fly:
+  // dY' = A[k] * dy + B[k] * dyb_x + C[k] with dyb_coef [G][3][K] (A | B | C) and dyb_x the BN's
+  // input (layout of dy); dyb_out (nullable) receives dY' (each element written once: the first
+  // P tile, core halo pixels) for the same layer's WGRAD
+  const float* dyb_x;
+  const float* dyb_coef;
+  float* dyb_out;
 };
 
 enum { F_FWD = 0, F_DGRAD = 1, F_WGRAD = 2 };

@@ -564,9 +564,38 @@ DDL_API int ddl_bnf_backward(const float* dy, const float* ymask, const BNFBwdAr
   } else {
     hipLaunchKernelGGL(bnf_fold_kernel, dim3((C + 31) / 32, G, 1 + two), dim3(FOLD_T), 0, s, a, b, M, C);
   }
+  // coefficient-only mode (a.dx == null): the consumer applies A * dy + B * x + C itself (the halo
+  // DGRAD's operand transform, conv_x6h.hip dyb_*), no apply pass
+  if (!a.dx && (!two || !b.dx) && !dym_out) return (int)hipGetLastError();
   const int RPI = 256 / f_tpr(C);
   hipLaunchKernelGGL(bnf_bwd_apply_kernel, dim3(fstream_blocks(M, RPI, G, 4), G), dim3(256), 0, s, dy, ymask, a, b,
                      two, dym_out, M, C);
+  return (int)hipGetLastError();
+}
+
+// out = A * dy + B * x + C per channel (coef [G][3][C]): the BN backward's apply from folded
+// coefficients, for a consumer that cannot apply it on the fly
+__global__ __launch_bounds__(256) void bnf_coef_apply_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                             const float* __restrict__ coef, float* __restrict__ out,
+                                                             long long M, int C) {
+  const int g = blockIdx.y, C4 = C >> 2;
+  const long long n4 = M * C4;
+  const float* cf = coef + (long long)g * 3 * C;
+  const long long base = (long long)g * M * C;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < n4; t += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(t % C4) * 4;
+    const float4 d = ld4(dy + base + t * 4), v = ld4(x + base + t * 4);
+    const float4 A = ld4(cf + c), B = ld4(cf + C + c), K = ld4(cf + 2 * C + c);
+    *(float4*)(out + base + t * 4) = make_float4(A.x * d.x + B.x * v.x + K.x, A.y * d.y + B.y * v.y + K.y,
+                                                 A.z * d.z + B.z * v.z + K.z, A.w * d.w + B.w * v.w + K.w);
+  }
+}
+
+DDL_API int ddl_bnf_coef_apply(const float* dy, const float* x, const float* coef, float* out, long long M, int C,
+                               int G, hipStream_t s) {
+  if (C % 4 || G < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bnf_coef_apply_kernel, dim3(grid_for(M * C / 4, 256, 4096), G), dim3(256), 0, s, dy, x, coef, out,
+                     M, C);
   return (int)hipGetLastError();
 }
 

@@ -98,6 +98,7 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
   constexpr int NUH = (HPM * 4 + 255) / 256;  // halo units (pixel x 4-channel chunk) per thread
   constexpr int PIMG = BP * 128;             // bytes per weight image slot (BP * 112 used)
   constexpr bool XF_OK = MODE == F_FWD;
+  constexpr bool DYB_OK = MODE == F_DGRAD;
   __shared__ __attribute__((aligned(16))) char smem[NWB * PIMG + HB];
   char* const pimg = smem;
   char* const himg = smem + NWB * PIMG;
@@ -123,11 +124,19 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
   const bool xf = XF_OK && a.in_scale != nullptr;
   const bool xrelu = a.in_relu != 0;
   float4 xsc = make_float4(1.f, 1.f, 1.f, 1.f), xsh = make_float4(0.f, 0.f, 0.f, 0.f);
+  // DGRAD: dY operand = the following BN's backward, A * dy + B * x_bn + C (per channel); the
+  // first P tile also writes it out (dyb_out) for the layer's WGRAD
+  const bool dyb = DYB_OK && a.dyb_coef != nullptr;
+  const bool dyb_w = dyb && a.dyb_out != nullptr && o.p0 == 0;
+  float4 dA = xsc, dB = xsh, dC = xsh;
 
   // ---------------------------------------------------------------- buffer descriptors
   const float* src = MODE == F_FWD ? a.x + (long long)g * a.x_gs : a.dy + (long long)g * a.dy_gs;
   const long long src_bytes = (long long)a.N * hg.SH * hg.SW * SC * 4;
   const __amdgpu_buffer_rsrc_t rS = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, (int)src_bytes, 0x00020000);
+  const float* srcx = dyb ? a.dyb_x + (long long)g * a.dy_gs : src;
+  const __amdgpu_buffer_rsrc_t rXb = __builtin_amdgcn_make_buffer_rsrc((void*)srcx, 0, (int)src_bytes, 0x00020000);
+  float* dyo = dyb_w ? a.dyb_out + (long long)g * a.dy_gs : nullptr;
   const char* wsp = (const char*)a.wsplit + (long long)g * a.ws_gs;
   const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(
       (void*)wsp, 0, (int)((long long)Pd * T * SC * 6), 0x00020000);
@@ -138,6 +147,7 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
   const int t0 = o.q0 >> hg.lgW;  // first output row (over n, oh) of the tile
   unsigned hoff[NUH];             // source byte offset at chunk 0 (OOB: padding / beyond N)
   int hlds[NUH];                  // LDS byte offset of the unit (-1: no unit)
+  unsigned own = 0;               // bit i: unit i is one of the tile's own (core) pixels
 #pragma unroll
   for (int i = 0; i < NUH; ++i) {
     const int uu = tid + 256 * i;
@@ -153,13 +163,25 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
       const int sr = r0 + hi - PD, sc = hj - PD;
       if (n < a.N && (unsigned)sr < (unsigned)hg.SH && (unsigned)sc < (unsigned)hg.SW)
         hoff[i] = (unsigned)((((long long)n * hg.SH + sr) * hg.SW + sc) * SC + ch * 4) * 4u;
+      if (hoff[i] != OOB && hi >= PD && hi < PD + hg.SR && hj >= PD && hj < PD + (1 << hg.lgW)) own |= 1u << i;
       hlds[i] = seg * hg.SEGB + hi * hg.ROWB + hj * HSTR + ch * 8;
     }
   }
   float4 hreg[NUH];
+  float4 hxb[DYB_OK ? NUH : 1];
   auto halo_load = [&](int cc) {
 #pragma unroll
     for (int i = 0; i < NUH; ++i) hreg[i] = bload4(rS, hoff[i], (unsigned)cc * 64u);
+    if constexpr (DYB_OK) {
+      if (dyb) {
+#pragma unroll
+        for (int i = 0; i < NUH; ++i) hxb[i] = bload4(rXb, hoff[i], (unsigned)cc * 64u);
+        const float* cf = a.dyb_coef + (long long)g * 3 * SC + cc * 16 + 4 * (tid & 3);
+        dA = *(const float4*)cf;
+        dB = *(const float4*)(cf + SC);
+        dC = *(const float4*)(cf + 2 * SC);
+      }
+    }
     if constexpr (XF_OK) {
       if (xf) {
         const long long c = (long long)g * SC + cc * 16 + 4 * (tid & 3);
@@ -180,6 +202,16 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
           v.z = v.z * xsc.z + xsh.z;
           v.w = v.w * xsc.w + xsh.w;
           if (xrelu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+        }
+      }
+      if constexpr (DYB_OK) {
+        if (dyb && hoff[i] != OOB) {  // BN backward of dY on real pixels (padding stays 0)
+          const float4 xb = hxb[i];
+          v.x = dA.x * v.x + dB.x * xb.x + dC.x;
+          v.y = dA.y * v.y + dB.y * xb.y + dC.y;
+          v.z = dA.z * v.z + dB.z * xb.z + dC.z;
+          v.w = dA.w * v.w + dB.w * xb.w + dC.w;
+          if (dyb_w && ((own >> i) & 1u)) *(float4*)(dyo + (hoff[i] + (unsigned)cc * 64u) / 4u) = v;
         }
       }
       s4v h, m, l;
@@ -282,7 +314,8 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
     // (k + 2) % 3, whose last reader (step k - 1) is past the barrier. vmcnt counts in issue order
     // (DMA pieces and the halo register loads together): at the end of step k, step k + 1's pieces
     // must have landed while step k + 2's (UP) and — between issue (tap HT) and use (chunk end) —
-    // the next chunk's halo loads (NUH, +2 for the BN constants with xf) may still fly.
+    // the next chunk's halo loads (NUH, +2 for the BN constants with xf; 2 NUH + 3 with the dY
+    // BN-backward transform: dy, x_bn and the A | B | C constants) may still fly.
     auto step_of = [&](int kk, int& c, int& tt) { c = kk / T; tt = kk - c * T; };
     {
       int c1_, t1_;
@@ -307,10 +340,12 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
           // keep each step's MFMAs and adds inside the step: moved across the barrier into the next
           // step they pile up two steps' operands and chains and spill
           __builtin_amdgcn_sched_barrier(0);
-          // (the BN-constant loads of the halo exist only with xf: the count must match exactly)
+          // (the BN-constant / x_bn loads of the halo exist only with xf / dyb: the counts must match
+          // exactly — a larger count than issued would let a weight piece still be in flight)
           if (!more && t + 2 >= T) wait_vm<0>();
           else if (more && (t == HT || t == HT + 1) && HT + 1 < T - 1) {
-            if (xf) wait_vm<UP + NUH + 2>();
+            if (dyb) wait_vm<UP + 2 * NUH + 3>();
+            else if (xf) wait_vm<UP + NUH + 2>();
             else wait_vm<UP + NUH>();
           } else wait_vm<UP>();
           cta_barrier();
@@ -337,7 +372,8 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
       const bool halo_fly = (HT < T - 1) && cc + 1 < cc1 && (t == HT || t == HT + 1);
       if (!issue2) wait_vm<0>();
       else if (halo_fly) {
-        if (xf) wait_vm<UP + NUH + 2>();
+        if (dyb) wait_vm<UP + 2 * NUH + 3>();
+        else if (xf) wait_vm<UP + NUH + 2>();
         else wait_vm<UP + NUH>();
       } else wait_vm<UP>();
       cta_barrier();

@@ -57,6 +57,12 @@ class _BNConv(ConvUnit):
         return Fn.bn_backward(dy, ymask, c, mu, rs, st.param(self.gamma), st.grad_of(self.gamma),
                               st.grad_of(self.beta), emit_dym=emit_dym, part=part)
 
+    def bn_backward_coef(self, dy, c, mu, rs, part):
+        """fp32: this BN's backward without the apply pass -> (c, coef) for conv_dgrad_wgrad(dy_bn=)."""
+        st = self.store
+        return c, Fn.F32.bn_backward_coef(dy, c, mu, rs, st.param(self.gamma), st.grad_of(self.gamma),
+                                          st.grad_of(self.beta), part=part)
+
     def bn_bwd_inputs(self, c, mu, rs, part):
         st = self.store
         return (c, mu, rs, st.param(self.gamma), st.grad_of(self.gamma), st.grad_of(self.beta), part)
@@ -90,7 +96,19 @@ def _inner_act(c, scale, shift):
     return Fn.bn_apply(c, scale, shift, act=RELU), None
 
 
+def _bn_fold(t) -> bool:
+    """fp32 activations: BN backwards hand their coefficients to the consuming DGRAD (applied as
+    the halo kernel stages dY) instead of running an apply pass (DDL_F32_BNFOLD=0: apply pass)."""
+    return Fn.F32.is_f32(t) and Fn.F32.BNFOLD[0]
+
+
 class _ShortcutGrad:
+    def _inner_bn_backward(self, conv, d, c, mu, rs, part, fold):
+        """An inner BN's backward -> (operand for the conv's DGRAD/WGRAD, dy_bn or None)."""
+        if fold:
+            return d, conv.bn_backward_coef(d, c, mu, rs, part)
+        return conv.bn_backward(d, None, c, mu, rs, part=part), None
+
     def _out_and_shortcut_bn_backward(self, main: _BNConv, dout, c, mu, rs, part, dctx):
         """The block's output BN and its shortcut's BN both take the (masked) block output gradient:
         the shortcut's reduce, then ONE fold launch and ONE apply pass for both (bn_backward2).
@@ -166,11 +184,17 @@ class BasicBlock(_ShortcutGrad, Layer):
         x, c1, a1, sc1, sh1, mu1, rs1, g1, c2, mu2, rs2, g2, out, dctx, ib = ctx
         st = self.store
         dcs = None
+        fold = _bn_fold(dout)
+        dyb2 = None
         if part is not None and dctx is not None:  # output + shortcut BN backwards together
             (dc2, dcs), dym = self._out_and_shortcut_bn_backward(self.conv2, dout, c2, mu2, rs2, part,
                                                                  dctx), dout
         elif part is not None:  # dout arrives masked by (out > 0) with bn2's reduce sums
-            dc2, dym = self.conv2.bn_backward(dout, None, c2, mu2, rs2, part=part), dout
+            if fold:
+                dc2, dyb2 = dout, self.conv2.bn_backward_coef(dout, c2, mu2, rs2, part)
+            else:
+                dc2 = self.conv2.bn_backward(dout, None, c2, mu2, rs2, part=part)
+            dym = dout
         else:
             dc2, dym = self.conv2.bn_backward(dout, out, c2, mu2, rs2, emit_dym=True)
         # every conv's DGRAD and WGRAD read the same dY: one (possibly paired) launch each
@@ -178,12 +202,12 @@ class BasicBlock(_ShortcutGrad, Layer):
         # dgrad epilogue applies bn1's ReLU mask (recomputed from c1: no read of a1) and reduces
         # bn1's backward sums (no reduce pass)
         da1, part1 = Fn.conv_dgrad_wgrad(dc2, st.shadow_of(self.conv2.w), a1, g2, st.grad_of(self.conv2.w),
-                                         bn=(c1, mu1, rs1), mask_bn=(sc1, sh1), in_bn=ib)
-        dc1 = self.conv1.bn_backward(da1, None, c1, mu1, rs1, part=part1)
+                                         bn=(c1, mu1, rs1), mask_bn=(sc1, sh1), in_bn=ib, dy_bn=dyb2)
+        dc1, dyb1 = self._inner_bn_backward(self.conv1, da1, c1, mu1, rs1, part1, fold)
         # with fuse: the producer's ReLU mask (x > 0) and BN reduce in this dgrad's epilogue
         return Fn.conv_dgrad_wgrad(dc1, st.shadow_of(self.conv1.w), x, g1, st.grad_of(self.conv1.w),
                                    residual=dres, mask=x if fuse is not None else None, bn=fuse,
-                                   want_dx=self.needs_input_grad, residual_sub=rsub)
+                                   want_dx=self.needs_input_grad, residual_sub=rsub, dy_bn=dyb1)
 
     def flops(self, s):
         G, N, H, W, _ = s
@@ -253,23 +277,29 @@ class Bottleneck(_ShortcutGrad, Layer):
             (ib1, ib2) = ctx
         st = self.store
         dcs = None
+        fold = _bn_fold(dout)
+        dyb3 = None
         if part is not None and dctx is not None:  # output + shortcut BN backwards together
             (dc3, dcs), dym = self._out_and_shortcut_bn_backward(self.conv3, dout, c3, mu3, rs3, part,
                                                                  dctx), dout
         elif part is not None:  # dout arrives masked by (out > 0) with bn3's reduce sums
-            dc3, dym = self.conv3.bn_backward(dout, None, c3, mu3, rs3, part=part), dout
+            if fold:
+                dc3, dyb3 = dout, self.conv3.bn_backward_coef(dout, c3, mu3, rs3, part)
+            else:
+                dc3 = self.conv3.bn_backward(dout, None, c3, mu3, rs3, part=part)
+            dym = dout
         else:
             dc3, dym = self.conv3.bn_backward(dout, out, c3, mu3, rs3, emit_dym=True)
         dres, rsub = self._shortcut_backward(dym, dctx, x, dcs) if dctx is not None else (dym, 1)
         da2, part2 = Fn.conv_dgrad_wgrad(dc3, st.shadow_of(self.conv3.w), a2, g3, st.grad_of(self.conv3.w),
-                                         bn=(c2, mu2, rs2), mask_bn=(sc2, sh2), in_bn=ib2)
-        dc2 = self.conv2.bn_backward(da2, None, c2, mu2, rs2, part=part2)
+                                         bn=(c2, mu2, rs2), mask_bn=(sc2, sh2), in_bn=ib2, dy_bn=dyb3)
+        dc2, dyb2 = self._inner_bn_backward(self.conv2, da2, c2, mu2, rs2, part2, fold)
         da1, part1 = Fn.conv_dgrad_wgrad(dc2, st.shadow_of(self.conv2.w), a1, g2, st.grad_of(self.conv2.w),
-                                         bn=(c1, mu1, rs1), mask_bn=(sc1, sh1), in_bn=ib1)
-        dc1 = self.conv1.bn_backward(da1, None, c1, mu1, rs1, part=part1)
+                                         bn=(c1, mu1, rs1), mask_bn=(sc1, sh1), in_bn=ib1, dy_bn=dyb2)
+        dc1, dyb1 = self._inner_bn_backward(self.conv1, da1, c1, mu1, rs1, part1, fold)
         return Fn.conv_dgrad_wgrad(dc1, st.shadow_of(self.conv1.w), x, g1, st.grad_of(self.conv1.w),
                                    residual=dres, mask=x if fuse is not None else None, bn=fuse,
-                                   want_dx=self.needs_input_grad, residual_sub=rsub)
+                                   want_dx=self.needs_input_grad, residual_sub=rsub, dy_bn=dyb1)
 
     def flops(self, s):
         G, N, H, W, _ = s

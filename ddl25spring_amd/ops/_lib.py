@@ -78,7 +78,7 @@ class ConvF32Args(ctypes.Structure):  # conv_f32.hip
                 ("G", i32), ("N", i32), ("H", i32), ("W", i32), ("C", i32), ("K", i32), ("R", i32), ("S", i32),
                 ("P", i32), ("Q", i32), ("stride", i32), ("pad", i32), ("relu", i32), ("accumulate", i32),
                 ("split_k", i32), ("res_sub", i32), ("in_relu", i32), ("slots", i32), ("gscale", f32),
-                ("wsplit", vp), ("ws_gs", i64)]
+                ("wsplit", vp), ("ws_gs", i64), ("dyb_x", vp), ("dyb_coef", vp), ("dyb_out", vp)]
 
 
 class BNFBwdArgs(ctypes.Structure):  # bn_f32.hip
@@ -192,6 +192,7 @@ _SIGS.update({
     "ddl_headf_train": [ctypes.POINTER(HeadFArgs), vp],
     "ddl_bnf_channel_sum": [vp, vp, i64, vp, i64, i32, i32, vp],
     "ddl_bnf_fold_ws": [i32, i32, i32],
+    "ddl_bnf_coef_apply": [vp, vp, vp, vp, i64, i32, i32, vp],
 })
 _RESTYPES = {"ddl_convf32_slots": ctypes.c_longlong, "ddl_convf32_workspace": ctypes.c_longlong,
              "ddl_x6h_workspace": ctypes.c_longlong, "ddl_bnf_fold_ws": ctypes.c_longlong,

@@ -203,6 +203,7 @@ def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out=None, 
 
 
 def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0, bn=None, split_k=0,
+               dy_bn=None, dy_bn_out=None,
                mask_bn=None, residual_sub=1, _tune=True):
     """dx[G,N,H,W,C] = conv_transpose(dy, w) (+residual) * (mask > 0).
 
@@ -217,7 +218,8 @@ def conv_dgrad(dy, w, geom: ConvGeom, residual=None, mask=None, out=None, cfg=0,
         assert bn is not None and mask is None, "mask_bn recomputes the mask from bn's x"
     if F32.is_f32(dy):
         return F32.conv_dgrad(dy, w, geom, residual=residual, mask=mask, out=out, bn=bn, mask_bn=mask_bn,
-                              residual_sub=residual_sub, split_k=split_k)
+                              residual_sub=residual_sub, split_k=split_k, dy_bn=dy_bn, dy_bn_out=dy_bn_out)
+    assert dy_bn is None, "dy_bn: fp32 device activations only"
     if not dy.is_cuda:
         if mask_bn is not None:
             sc, sh = mask_bn
@@ -408,15 +410,27 @@ def conv_pair(dy, w, x, geom: ConvGeom, dw, dcfg: int, dsplit: int, wcfg: int, w
 
 
 def conv_dgrad_wgrad(dy, w, x, geom: ConvGeom, dw, residual=None, mask=None, bn=None, mask_bn=None,
-                     want_dx: bool = True, residual_sub: int = 1, dgeom: ConvGeom | None = None, in_bn=None):
+                     want_dx: bool = True, residual_sub: int = 1, dgeom: ConvGeom | None = None, in_bn=None,
+                     dy_bn=None):
     """``conv_wgrad(dy, x, geom, dw)`` and (if want_dx) ``conv_dgrad(dy, w, dgeom or geom, residual,
     mask, bn=bn, mask_bn=mask_bn, residual_sub=...)`` — both read dy and are independent, so on
     the GPU they may run as ONE paired launch (whichever of paired / back-to-back the tuner
     measured faster for this shape). ``dgeom``: the DGRAD's own geometry (a stride-2 1x1
     shortcut's input gradient on the compact grid). Returns what conv_dgrad returns (None
-    without want_dx). in_bn: the WGRAD's operand-side BN of x (as conv_fwd)."""
+    without want_dx). in_bn: the WGRAD's operand-side BN of x (as conv_fwd). dy_bn = (x_bn, coef)
+    (fp32): dY is the following BN's backward A * dy + B * x_bn + C, applied inside the DGRAD as it
+    stages dY (which also writes it out for the WGRAD) instead of by a separate apply pass."""
     dg = dgeom or geom
     dkw = dict(residual=residual, mask=mask, bn=bn, mask_bn=mask_bn, residual_sub=residual_sub)
+    if dy_bn is not None:
+        assert F32.is_f32(dy) and dgeom is None
+        if want_dx:
+            dc = torch.empty_like(dy)
+            dx = conv_dgrad(dy, w, dg, dy_bn=dy_bn, dy_bn_out=dc, **dkw)
+        else:
+            dc, dx = F32.coef_apply(dy, dy_bn[0], dy_bn[1]), None
+        conv_wgrad(dc, x, geom, dw, in_bn=in_bn)
+        return dx
     if F32.is_f32(dy) or in_bn is not None:
         # DGRAD first: in fp32 ``w`` IS the master weight that a direct-SGD WGRAD steps in place
         dx = conv_dgrad(dy, w, dg, **dkw) if want_dx else None

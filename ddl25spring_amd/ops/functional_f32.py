@@ -329,10 +329,20 @@ def conv_fwd(x, w, geom, bias=None, relu=False, stats=None, out=None, residual=N
 
 
 def conv_dgrad(dy, w, geom, residual=None, mask=None, out=None, bn=None, mask_bn=None, residual_sub=1,
-               split_k=0):
+               split_k=0, dy_bn=None, dy_bn_out=None):
+    """dy_bn = (x_bn, coef): the dY operand is the following BN's backward A * dy + B * x_bn + C
+    (bn_backward_coef), applied inside the halo kernel as dY is staged (written to ``dy_bn_out``
+    too, for the layer's WGRAD); launches off the halo kernel materialise it first."""
     dx = out if out is not None else torch.empty(geom.G, geom.N, geom.H, geom.W, geom.C, dtype=torch.float32,
                                                  device=dy.device)
     kw = {}
+    if dy_bn is not None:
+        xb, coef = dy_bn
+        assert xb.is_contiguous() and coef.is_contiguous() and xb.shape == dy.shape and dy.is_contiguous()
+        if uses_halo(F_DGRAD, geom) and split_k == 0:
+            kw.update(dyb_x=ptr(xb), dyb_coef=ptr(coef), dyb_out=ptr(dy_bn_out))
+        else:
+            dy = coef_apply(dy, xb, coef, out=dy_bn_out)
     if residual is not None:
         if residual_sub == 2:
             want = (geom.G, geom.N, (geom.H + 1) // 2, (geom.W + 1) // 2, geom.C)
@@ -436,11 +446,13 @@ def bn_stats(x):
     return st
 
 
-def _bwd_args(x, mean, rstd, gamma, dgamma, dbeta, part, dx, fold_slots: int = 0):
-    """fold_slots: size the two-level fold's workspace for this many slots (0: part's own)."""
+def _bwd_args(x, mean, rstd, gamma, dgamma, dbeta, part, dx, fold_slots: int = 0, coef=None):
+    """fold_slots: size the two-level fold's workspace for this many slots (0: part's own).
+    coef: where the folded (A | B | C) coefficients go (default: launch-local scratch)."""
     G, C = x.shape[0], x.shape[-1]
     t = _lib.BNFBwdArgs()
-    coef = ws.scratch((G, 3, C), x.device)
+    if coef is None:
+        coef = ws.scratch((G, 3, C), x.device)
     gs = _gs(gamma) if gamma is not None else 0
     if dgamma is not None or dbeta is not None:
         gd = _gs(dgamma) if dgamma is not None else _gs(dbeta)
@@ -475,6 +487,42 @@ def bn_backward(dy, ymask, x, mean, rstd, gamma, dgamma=None, dbeta=None, emit_d
     check(_lib.kernels().ddl_bnf_backward(ptr(dy), ptr(ymask), ctypes.byref(a), None, ptr(dym), M, C, G,
                                           int(do_reduce), stream()), "bn_backward_f32")
     return (dx, dym) if emit_dym else dx
+
+
+# BN backward folded into the consuming DGRAD (DDL_F32_BNFOLD=0: separate apply pass)
+BNFOLD = [os.environ.get("DDL_F32_BNFOLD", "1") != "0"]
+
+
+def bn_backward_coef(dy, x, mean, rstd, gamma, dgamma=None, dbeta=None, part=None):
+    """The BN backward WITHOUT its apply pass: d(gamma), d(beta) accumulated and the per-channel
+    coefficients coef [G, 3, C] = (A | B | C) of dx = A * dy + B * x + C returned, for a consumer
+    that applies them on the fly (conv_dgrad(dy_bn=(x, coef)))."""
+    G, C = x.shape[0], x.shape[-1]
+    M = x[0].numel() // C
+    assert dy.is_contiguous() and x.is_contiguous()
+    do_reduce = part is None
+    if do_reduce:
+        part = torch.empty(G, reduce_slots(M, C, G), 2, C, dtype=torch.float32, device=x.device)
+    coef = torch.empty(G, 3, C, dtype=torch.float32, device=x.device)
+    a = _bwd_args(x, mean, rstd, gamma, dgamma, dbeta, part, None, coef=coef)
+    check(_lib.kernels().ddl_bnf_backward(ptr(dy), None, ctypes.byref(a), None, None, M, C, G, int(do_reduce),
+                                          stream()), "bn_backward_coef_f32")
+    return coef
+
+
+def coef_apply(dy, x, coef, out=None):
+    """out = A * dy + B * x + C (coef from bn_backward_coef): the apply pass, for consumers that
+    cannot fuse it."""
+    G, C = x.shape[0], x.shape[-1]
+    out = out if out is not None else torch.empty_like(x)
+    check(_lib.kernels().ddl_bnf_coef_apply(ptr(dy), ptr(x), ptr(coef), ptr(out), x[0].numel() // C, C, G, stream()),
+          "bnf_coef_apply")
+    return out
+
+
+def uses_halo(mode: int, geom) -> bool:
+    cfg, _ = plan(mode, geom)
+    return bool(_cfg(cfg) & HALO_BIT) and halo_ok(mode, geom)
 
 
 def bn_backward2(dy, bn_a, bn_b):

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--layer", default="c64", choices=list(LAYERS))
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--halo", type=int, default=1, help="0: never the halo kernel (conv_x6h.hip)")
+    ap.add_argument("--dybn", type=int, default=0, help="dgrad: dY operand = BN backward (dy_bn), 2: + write-out")
     a = ap.parse_args()
     F32.set_math(a.math)
     F32.set_halo(bool(a.halo))
@@ -37,8 +38,11 @@ def main():
     w = torch.randn(g.G, g.K, g.R, g.S, g.C, device=dev) * 0.05
     dy = torch.randn(g.G, g.N, g.P, g.Q, g.K, device=dev)
     dw = torch.zeros_like(w)
+    xb, coef = torch.randn_like(dy), torch.randn(g.G, 3, g.K, device=dev)
+    dc = torch.empty_like(dy) if a.dybn == 2 else None
+    dyb = dict(dy_bn=(xb, coef), dy_bn_out=dc) if a.dybn else {}
     run = {"fwd": lambda: F32.conv_fwd(x, w, g, stats=F32.SlotStats()),
-           "dgrad": lambda: F32.conv_dgrad(dy, w, g),
+           "dgrad": lambda: F32.conv_dgrad(dy, w, g, **dyb),
            "wgrad": lambda: F32.conv_wgrad(dy, x, g, dw)}[a.mode]
     for _ in range(3):
         run()
@@ -52,7 +56,7 @@ def main():
     ms = e0.elapsed_time(e1) / a.reps
     fl = 2 * g.G * g.N * g.P * g.Q * g.K * g.R * g.S * g.C
     mode = {"fwd": F32.F_FWD, "dgrad": F32.F_DGRAD, "wgrad": F32.F_WGRAD}[a.mode]
-    print(f"{a.math} halo={a.halo} {a.mode} G={a.G} {a.layer}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF/s "
+    print(f"{a.math} halo={a.halo} dybn={a.dybn} {a.mode} G={a.G} {a.layer}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF/s "
           f"plan={F32.plan(mode, g)}")
 
 

@@ -55,7 +55,11 @@ def _worker_r18(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DDL_F32_TARGET_WG="1",
                       DDL_F32_TUNED="0")
+    from ddl25spring_amd.ops import functional_f32 as F32
     from ddl25spring_amd.runtime import dist as rdist
+    # the module is already imported (the test module's imports): set the plan knobs directly
+    F32.TARGET_WG, F32._TUNED = 1, {}
+    F32._PLANS.clear()
     ctx = rdist.init(backend="gloo", device="cuda")
     fa = _r18_fedavg(ctx)
     fa.round()

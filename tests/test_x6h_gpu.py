@@ -115,6 +115,38 @@ def test_x6h_dgrad(cuda, geom, split):
         F32.clear_plan(F32.F_DGRAD, geom)
 
 
+@pytest.mark.parametrize("split", [1, 2])
+@pytest.mark.parametrize("geom", GEOMS, ids=IDS)
+def test_x6h_dgrad_bn_backward_operand(cuda, geom, split):
+    """dy_bn: the DGRAD's dY operand is the following BN's backward A * dy + B * x_bn + C, applied
+    as the halo is staged, and written out exactly once per element (the layer's WGRAD operand);
+    the same call on a non-halo plan materialises it first (fallback)."""
+    if geom.K % 16:
+        pytest.skip("halo DGRAD needs K % 16 == 0")
+    torch.manual_seed(2)
+    dy = torch.randn(geom.G, geom.N, geom.P, geom.Q, geom.K, device=cuda)
+    xb = torch.randn_like(dy)
+    coef = torch.randn(geom.G, 3, geom.K, device=cuda)
+    w = _weights(geom, cuda)
+    c = coef.cpu().double()
+    dc_ref = c[:, 0, None, None, None] * dy.cpu().double() + c[:, 1, None, None, None] * xb.cpu().double() \
+        + c[:, 2, None, None, None]
+    dxr = ref_dgrad(dc_ref, w.cpu(), geom)
+    outs = []
+    for engine in ("x6h", "x6"):
+        Pd = geom.C
+        F32.set_plan(F32.F_DGRAD, geom, 128 if Pd > 64 else 64, 128 if engine == "x6h" else 64, split, engine)
+        try:
+            assert F32.uses_halo(F32.F_DGRAD, geom) == (engine == "x6h")
+            dc = torch.full_like(dy, float("nan"))
+            dx = Fn.conv_dgrad(dy, w, geom, dy_bn=(xb, coef), dy_bn_out=dc)
+            _close(dc, dc_ref, rel=1e-6)
+            _close(dx, dxr)
+            outs.append(dc)
+        finally:
+            F32.clear_plan(F32.F_DGRAD, geom)
+
+
 def test_x6h_split_weights(cuda):
     """The pre-split weight image reconstructs the fp32 weights exactly (h + m + l == w): per
     16-channel chunk three bf16 planes [h0..h15 | m0..m15 | l0..l15]."""
