@@ -1239,10 +1239,11 @@ def adam_step(p, g, m, v, shadow, lr, beta1, beta2, eps, wd, step, decoupled, gr
     a.p, a.g, a.m, a.v, a.shadow = ptr(p), ptr(g), ptr(m), ptr(v), ptr(shadow)
     a.n = p.numel()
     a.lr, a.beta1, a.beta2, a.eps, a.wd, a.grad_scale = lr, beta1, beta2, eps, wd, grad_scale
-    a.bc1, a.bc2 = 1 - beta1 ** step, 1 - beta2 ** step
-    if row_len > 0:
+    if row_len > 0:  # per-row device step counters: the kernel computes the corrections
         a.bc1 = a.bc2 = 1.0
         assert step_dev is not None and step_dev.numel() * row_len == p.numel()
+    else:
+        a.bc1, a.bc2 = 1 - beta1 ** step, 1 - beta2 ** step
     a.decoupled = int(decoupled)
     a.step_dev = ptr(step_dev)
     a.row_len = int(row_len)
