@@ -45,6 +45,10 @@ struct ConvF32Args {
   const float* dyb_x;
   const float* dyb_coef;
   float* dyb_out;
+  // WGRAD split-K (conv_f32.hip): one arrival counter per (group, tile), zero between launches;
+  // the last slice's workgroup folds the slices in slice order (no reduce launch). Null: reduce pass
+  int* tickets;
+  long long tickets_cap;
 };
 
 enum { F_FWD = 0, F_DGRAD = 1, F_WGRAD = 2 };

@@ -98,7 +98,8 @@ __global__ __launch_bounds__(256, (X6 && BP * BQ <= 64 * 128) ? 3 : 2) void conv
   const FGeo o = fgeo<MODE, BP, BQ>(a, bx, by, g, gy);
   const bool split_store = a.split_k > 1;
   if (o.q0 >= o.Qd || o.p0 >= o.Pd) {
-    if (!split_store) fzero_slot<MODE, BP>(a, o);
+    // an empty tile's statistics slot is zeroed once (by the epilogue launch without tickets)
+    if (!split_store || (a.tickets && o.split == 0)) fzero_slot<MODE, BP>(a, o);
     return;
   }
   const int nk = (o.Kr + FBK - 1) / FBK;
@@ -482,6 +483,64 @@ __global__ __launch_bounds__(256, (X6 && BP * BQ <= 64 * 128) ? 3 : 2) void conv
                                                                 acc[ti][tj][2], acc[ti][tj][3]);
         }
       }
+    if (a.tickets) {
+      // the last slice to arrive at this (group, phase, tile) folds all slices, in slice order, and
+      // runs the epilogue (no reduce / epilogue launch): the partial stores are released
+      // device-wide before the arrival counts, and acquired (L1 / L2 invalidated) by the folding
+      // workgroup after it sees the count complete
+      __threadfence();
+      __syncthreads();
+      int* const last = (int*)smem;
+      int* const ticket = a.tickets + ((long long)g * o.nph + o.phase) * gx + bx;
+      if (tid == 0) *last = atomicAdd(ticket, 1) == o.nsplit - 1;
+      __syncthreads();
+      if (!*last) return;
+      __threadfence();
+      if constexpr (MODE != F_WGRAD) {
+        // the split-K epilogue kernel's fold (convf32_splitk_epilogue), in this tile's registers
+        const long long qmax = (long long)a.slots / o.nph * BQ;
+        const long long slice = (long long)a.G * o.nph * qmax * o.Pd;
+        const float* base = a.partial + ((long long)g * o.nph + o.phase) * qmax * o.Pd;
+#pragma unroll
+        for (int ti = 0; ti < TP; ++ti)
+#pragma unroll
+          for (int tj = 0; tj < TQ; ++tj) {
+            const int q = o.q0 + wq * WQ + tj * 16 + (lane & 15);
+            const int p = o.p0 + wp * WP + ti * 16 + 4 * (lane >> 4);
+            f4v sm = (f4v){0.f, 0.f, 0.f, 0.f};
+            if (q < o.Qd && p < o.Pd) {
+              const float* src = base + (long long)q * o.Pd + p;
+              for (int k = 0; k < o.nsplit; ++k) {
+                const float4 v = *(const float4*)(src + k * slice);
+                sm[0] += v.x; sm[1] += v.y; sm[2] += v.z; sm[3] += v.w;
+              }
+            }
+            acc[ti][tj] = sm;
+          }
+        __syncthreads();  // the flag word in smem is epilogue scratch from here on
+        if (tid == 0) *ticket = 0;
+        fepi<MODE, BP, BQ, Lay16<BP, BQ>>(a, o, acc, smem);
+        return;
+      } else {
+        const long long per = (long long)o.Pd * o.Qd;
+        const float* src = a.partial + (long long)g * per;
+        float* dst = a.out + (long long)g * a.out_gs;
+        for (int e = tid; e < BP * (BQ / 4); e += 256) {
+          const int p = o.p0 + e / (BQ / 4), q = o.q0 + 4 * (e % (BQ / 4));
+          if (p >= o.Pd || q >= o.Qd) continue;
+          const long long off = (long long)p * o.Qd + q;
+          float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+          for (int k = 0; k < o.nsplit; ++k) {
+            const float4 v = *(const float4*)(src + (long long)k * a.G * per + off);
+            sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+          }
+          float4 b = a.accumulate ? *(const float4*)(dst + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+          b.x += a.gscale * sum.x; b.y += a.gscale * sum.y; b.z += a.gscale * sum.z; b.w += a.gscale * sum.w;
+          *(float4*)(dst + off) = b;
+        }
+        if (tid == 0) *ticket = 0;  // ready for the next launch (and graph replay)
+      }
+    }
     return;
   }
   fepi<MODE, BP, BQ, Lay16<BP, BQ>>(a, o, acc, smem);
@@ -557,9 +616,10 @@ static int launch_tile(ConvF32Args a, hipStream_t s) {
     if (!a.partial || need > a.partial_cap) return (int)hipErrorInvalidValue;
   }
   const dim3 grid((unsigned)(ntp * ntq), (unsigned)(nph * split), (unsigned)a.G);
+  if (split == 1 || (long long)a.G * nph * ntp * ntq > a.tickets_cap) a.tickets = nullptr;
   hipLaunchKernelGGL((convf32_kernel<MODE, BP, BQ, X6>), grid, dim3(256), 0, s, a);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess || split == 1) return (int)e;
+  if (e != hipSuccess || split == 1 || a.tickets) return (int)e;
   if (MODE == F_WGRAD) {
     const long long n4 = Pd * Qd / 4;
     hipLaunchKernelGGL(convf32_wgrad_reduce, dim3(grid_for((long long)a.G * n4, 256)), dim3(256), 0, s,

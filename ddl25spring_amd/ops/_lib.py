@@ -78,7 +78,8 @@ class ConvF32Args(ctypes.Structure):  # conv_f32.hip
                 ("G", i32), ("N", i32), ("H", i32), ("W", i32), ("C", i32), ("K", i32), ("R", i32), ("S", i32),
                 ("P", i32), ("Q", i32), ("stride", i32), ("pad", i32), ("relu", i32), ("accumulate", i32),
                 ("split_k", i32), ("res_sub", i32), ("in_relu", i32), ("slots", i32), ("gscale", f32),
-                ("wsplit", vp), ("ws_gs", i64), ("dyb_x", vp), ("dyb_coef", vp), ("dyb_out", vp)]
+                ("wsplit", vp), ("ws_gs", i64), ("dyb_x", vp), ("dyb_coef", vp), ("dyb_out", vp),
+                ("tickets", vp), ("tickets_cap", i64)]
 
 
 class BNFBwdArgs(ctypes.Structure):  # bn_f32.hip

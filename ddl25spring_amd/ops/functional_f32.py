@@ -68,6 +68,18 @@ def ensure_workspace(device) -> None:
         key = f"{device}:{role}"
         if key not in _WS:
             _WS[key] = torch.empty(WS_CAP, dtype=torch.float32, device=device)
+            # WGRAD split-K arrival counters (zero between launches: the folding workgroup resets
+            # its own), one set per role since the two streams' WGRADs may run concurrently
+            _WS[key + ":tickets"] = torch.zeros(TICKETS_CAP, dtype=torch.int32, device=device)
+
+
+# per-(group, phase, tile) counters of the in-kernel split-K fold (the last-arriving slice's
+# workgroup sums the slices and runs the epilogue). OFF by default (DDL_F32_WG_FOLD=1 enables it):
+# measured 28.5k vs 36.3k samples/s headline and 9.5k vs 21.0k at 1 client — every workgroup's
+# device-scope release fence writes back its XCD's L2, and one workgroup folding up to 64 slices
+# serially is slower than the parallel reduce launch (profiles/bench_wgfold_r4g.jsonl)
+TICKETS_CAP = 1 << 18
+WG_FOLD = [os.environ.get("DDL_F32_WG_FOLD", "0") == "1"]
 
 
 def _dims(mode, g):
@@ -275,6 +287,9 @@ def _launch(a, mode: int, geom, device, split_k: int = 0, ws_role: str = "main")
             a.split_k = split = 1  # plan-determined (same choice eager and captured)
         else:
             a.partial, a.partial_cap = buf.data_ptr(), buf.numel()
+            if WG_FOLD[0] and not (cfg & HALO_BIT):  # the halo kernel keeps its epilogue launch
+                t = _WS[f"{device}:{ws_role}:tickets"]
+                a.tickets, a.tickets_cap = t.data_ptr(), t.numel()
     name = ("conv_fwd", "conv_dgrad", "conv_wgrad")[mode] + "_f32"
     if cfg & HALO_BIT:
         ws_buf = split_weights(a, mode, geom, device)
