@@ -33,9 +33,15 @@ y = torch.randint(0, 10, (a.batch,))
 net.store.zero_grad()
 xin = net.prepare_input(x.to(cuda))
 loss, _ = net.train_step(torch.cat([xin] * G), torch.stack([y] * G).to(cuda, torch.int32))
+import copy  # noqa: E402
+t32 = copy.deepcopy(tm).float().to(cuda)  # stock torch fp32 (MIOpen) on the same GPU, for scale
+F.cross_entropy(t32(x.to(cuda)), y.to(cuda)).backward()
 t64 = tm.double()
 lt = F.cross_entropy(t64(x.double()), y)
 lt.backward()
+g32 = {n: p.grad for n, p in t32.named_parameters()}
+w32 = max(_err(g32[n], p.grad) for n, p in t64.named_parameters())
+print(f"stock torch fp32: worst relative gradient error {w32:.2e}")
 print(f"G={G} B={a.batch} twg={a.target_wg} halo={a.halo} math={a.math} loss {loss[0].item():.8f} "
       f"ref {lt.item():.8f}")
 for grp in range(G):
