@@ -32,6 +32,7 @@ from __future__ import annotations
 import math
 import time
 import warnings
+import weakref
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -295,7 +296,10 @@ class FederatedGAN:
             self._bz[G].copy_(z, non_blocking=False)
             if self.use_graph:
                 if G not in self._bgraphs:
-                    self._bgraphs[G] = CapturedStep(lambda G=G: self._batched_local(G), warmup=1)
+                    # a weak self: no engine <-> graph cycle, so the graph dies with the engine
+                    # (refcount), not in a later cyclic GC pass
+                    me = weakref.proxy(self)
+                    self._bgraphs[G] = CapturedStep(lambda G=G: me._batched_local(G), warmup=1)
                 ld, lg = self._bgraphs[G]()
             else:
                 ld, lg = self._batched_local(G)
@@ -353,7 +357,8 @@ class FederatedGAN:
                 self._z[int(c)].copy_(z)
                 if self.use_graph:
                     if int(c) not in self._graphs:
-                        self._graphs[int(c)] = CapturedStep(lambda c=int(c): self._local_steps(c), warmup=1)
+                        me = weakref.proxy(self)
+                        self._graphs[int(c)] = CapturedStep(lambda c=int(c): me._local_steps(c), warmup=1)
                     ld, lg = self._graphs[int(c)]()
                 else:
                     ld, lg = self._local_steps(int(c))

@@ -21,9 +21,17 @@ def pytest_configure(config):
 
 @pytest.fixture
 def cuda():
+    import gc
+
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from ddl25spring_amd.ops import _lib
     _lib.kernels()  # must load: no silent fallback on a GPU box
-    return torch.device("cuda")
+    yield torch.device("cuda")
+    # collect the test's HIP graphs / streams / pools HERE, with the device idle, rather than at
+    # whatever point a later test's allocation triggers the cyclic GC (inside its own graph
+    # warm-up, where destroying another graph once aborted the process)
+    torch.cuda.synchronize()
+    gc.collect()
+    torch.cuda.synchronize()

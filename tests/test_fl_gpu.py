@@ -172,7 +172,11 @@ def test_unsynchronised_rounds_match_on_device(cuda):
         ws.append(fa.w_global.clone())
     step = (ws[0] - w0).norm()
     noise = ((ws[0] - ws[2]).norm() / step).item()
-    assert ((ws[0] - ws[1]).norm() / step).item() < 2 * noise + 1e-2
+    # bf16 split-K WGRAD accumulates with fp32 atomics, so two runs can also land a few % of a
+    # round's update apart (1.7 % seen once after the DCGAN tests had tuned other plans while the
+    # two synchronised runs agreed to 1e-6); the bit-exact unsynchronised == synchronised check is
+    # the fp32 one (test_fp32_gpu.py::test_fp32_unsynchronised_rounds_equal_exactly)
+    assert ((ws[0] - ws[1]).norm() / step).item() < 2 * noise + 5e-2
 
 
 class _BothAttacks:
