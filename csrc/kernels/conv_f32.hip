@@ -566,6 +566,15 @@ __global__ __launch_bounds__(256) void convf32_wgrad_reduce(const float* __restr
   }
 }
 
+// the same fold for other WGRAD producers of [split][G][Pd][Qd] slices (conv_x6hw.hip)
+DDL_API int ddl_convf32_wgrad_reduce(const float* part, float* out, long long out_gs, int G, long long n, int splits,
+                                     int accumulate, float gscale, hipStream_t s) {
+  if (n % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(convf32_wgrad_reduce, dim3(grid_for((long long)G * (n / 4), 256)), dim3(256), 0, s, part, out,
+                     out_gs, G, n / 4, splits, accumulate, gscale);
+  return (int)hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------ launchers
 static void fdims(const ConvF32Args& a, int mode, long long& Pd, long long& Qd, long long& Qmax, long long& Kr,
                   int& nph) {

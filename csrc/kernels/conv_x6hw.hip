@@ -1,0 +1,334 @@
+// Halo-staged X6 WGRAD of stride-1 "same" 3x3 / 1x1 convolutions (fp32 operands on the bf16 MFMA).
+//
+// dW[k][r][s][c] = sum over output pixels q of dY[q][k] * X[q + (r - pd, s - pd)][c]. conv_f32.hip
+// runs this as an implicit GEMM whose X operand rows are (tap, channel): every X value is loaded,
+// split into its three bf16 pieces and transposed into LDS once PER TAP (9x), which makes that loop
+// VALU-bound (~6 VALU per MFMA, MFMA busy 30-37 %, profiles/pmc_wgrad_r4.txt). Here a workgroup
+// owns dW[k0:k0+64][all taps][c0:c0+32] and sweeps a slice of the pixel tiles; per tile of 128
+// output pixels it stages
+//   dY  [64 k][128 pixels]                        (planar h | m | l bf16, pixel-contiguous rows)
+//   X   [32 c][tile rows + halo][tile cols + halo] (planar, one image row per LDS row)
+// each ONCE (register transpose: a thread loads 8 pixels x 4 channels and writes each channel's 8
+// pixels as one 16-byte LDS store per plane), and the 9 taps read shifted windows of the X image.
+// MFMA v_mfma_f32_32x32x16_bf16 with the REDUCTION over pixels: lane l holds 8 consecutive pixels
+// (l >> 5 selects which 8 of the step's 16) of row / column l & 31; a tap's window starts s
+// elements into an LDS row, so its 16-byte reads are 2-byte aligned (gfx950 LDS serves them).
+// Per 16-pixel step and (k block, tap): six piece products chained from zero, then ONE IEEE add
+// into the fp32 accumulator (the halo FWD / DGRAD kernel's rounding discipline).
+// 4 waves: wave w computes k block (w >> 1) (32 rows) for taps 0..4 (w even) or 5..8 (w odd).
+// Split-K over pixel tiles writes [split][G][K][R*S*C] partial slices for convf32_wgrad_reduce;
+// unsplit launches apply out = (accumulate ? out : 0) + gscale * dW directly (direct SGD).
+#include "ddl_common.h"
+#include "conv_f32_core.h"
+
+namespace {
+
+typedef float f16v __attribute__((ext_vector_type(16)));  // 32x32 MFMA accumulator
+
+constexpr int HW_BK = 64, HW_BC = 32, HW_TP = 128;  // k rows, channels, pixels per tile
+constexpr int HW_KS = 136;                           // dY LDS row stride (elements): 272 B = 16 mod 256
+constexpr unsigned HW_OOB = 0x80000000u;
+
+struct HWGeo {
+  int lgW;      // log2 output width (8..64)
+  int SR;       // rows per image segment of a tile (min(128 / OW, OH))
+  int NSEG;     // image segments per tile
+  int HR, HCp;  // halo rows per segment (SR + R - 1), padded halo row length (elements, % 8 == 0)
+  int CS;       // X LDS channel stride (elements)
+  int ntile;    // pixel tiles per group
+  int NUX;      // X staging units per thread
+};
+
+__device__ __forceinline__ float4 hw_load(const __amdgpu_buffer_rsrc_t& rs, unsigned off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+}
+
+// 8 values -> the three bf16 planes of one 16-byte LDS row segment each
+__device__ __forceinline__ void split8(const float (&v)[8], s8v& h, s8v& m, s8v& l) {
+  s4v h0, m0, l0, h1, m1, l1;
+  split3(make_float4(v[0], v[1], v[2], v[3]), h0, m0, l0);
+  split3(make_float4(v[4], v[5], v[6], v[7]), h1, m1, l1);
+  h = cat44(h0, h1);
+  m = cat44(m0, m1);
+  l = cat44(l0, l1);
+}
+
+template <int RS, int NUX>
+__global__ __launch_bounds__(256, 1) void convx6hw_kernel(ConvF32Args a, HWGeo hg) {
+  constexpr int T = RS * RS, PD = (RS - 1) / 2;
+  constexpr int TAPS0 = (T + 1) / 2;  // taps of the even waves (5 of 9; 1 of 1)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* const dyl = (bf16_t*)smem;                        // [3][64][HW_KS]
+  bf16_t* const xl = dyl + 3 * HW_BK * HW_KS;               // [3][32][CS]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int OW = 1 << hg.lgW, TR = HW_TP >> hg.lgW;
+  const int nct = a.C / HW_BC;
+  const int k0 = (blockIdx.x / nct) * HW_BK, c0 = (blockIdx.x % nct) * HW_BC;
+  const int split = blockIdx.y, nsplit = gridDim.y, g = blockIdx.z;
+  const int per = (hg.ntile + nsplit - 1) / nsplit;
+  const int t0 = split * per, t1 = min(hg.ntile, t0 + per);
+  const int K = a.K, C = a.C, H = a.H, W = a.W;
+  const long long npix = (long long)a.N * H * W;
+
+  const __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.dy + (long long)g * a.dy_gs), 0, (int)(npix * K * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.x + (long long)g * a.x_gs), 0, (int)(npix * C * 4), 0x00020000);
+
+  // ---- dY unit: channels k0 + 4 * (tid & 15) .. + 3, tile pixels 8 * (tid >> 4) .. + 7
+  const int dkc = tid & 15, dpg = tid >> 4;
+  // ---- X units: channels c0 + 4 * cg, halo row xr (over segments), halo columns 8 * xc .. + 7
+  const int ncol8 = hg.HCp >> 3;
+  const int nxu = 8 * hg.NSEG * hg.HR * ncol8;
+  // operand-side BN of X (relu(x * scale + shift) on real pixels)
+  const bool xf = a.in_scale != nullptr;
+  float4 xsc[NUX], xsh[NUX];
+#pragma unroll
+  for (int u = 0; u < NUX; ++u) {
+    xsc[u] = make_float4(1.f, 1.f, 1.f, 1.f);
+    xsh[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int uu = tid + 256 * u;
+    if (xf && uu < nxu) {
+      const long long cc = (long long)g * C + c0 + 4 * (uu & 7);
+      xsc[u] = *(const float4*)(a.in_scale + cc);
+      xsh[u] = *(const float4*)(a.in_shift + cc);
+    }
+  }
+
+  float4 rd[8], rx[NUX][8];
+  unsigned xok[NUX];  // bit j: halo pixel j of the unit is a real input pixel
+  auto load_tile = [&](int tile) {
+    const long long p0 = (long long)tile * HW_TP;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const long long p = p0 + dpg * 8 + j;
+      rd[j] = hw_load(rD, p < npix ? (unsigned)((p * K + k0 + 4 * dkc) * 4) : HW_OOB);
+    }
+    // first output row of the tile over (n, oh): tile rows are whole image rows
+    const long long row0 = p0 >> hg.lgW;
+#pragma unroll
+    for (int u = 0; u < NUX; ++u) {
+      const int uu = tid + 256 * u;
+      xok[u] = 0;
+      const int cg = uu & 7, rest = uu >> 3;
+      const int xc = rest % ncol8, xrr = rest / ncol8;  // halo row over segments
+      const int seg = xrr / hg.HR, hr = xrr - seg * hg.HR;
+      const long long orow = row0 + (long long)seg * hg.SR;  // first output row of the segment
+      const long long n = orow / a.P;
+      const int ih = (int)(orow - n * a.P) + hr - PD;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int iw = 8 * xc + j - PD;
+        const bool ok = uu < nxu && n < a.N && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        xok[u] |= (ok ? 1u : 0u) << j;
+        rx[u][j] = hw_load(rX, ok ? (unsigned)((((n * H + ih) * W + iw) * C + c0 + 4 * cg) * 4) : HW_OOB);
+      }
+    }
+  };
+  auto store_tile = [&]() {
+    // dY: channel ch of the unit -> row k = 4 dkc + ch, pixels 8 dpg .. + 7
+#pragma unroll
+    for (int ch = 0; ch < 4; ++ch) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = ch == 0 ? rd[j].x : ch == 1 ? rd[j].y : ch == 2 ? rd[j].z : rd[j].w;
+      s8v h, m, l;
+      split8(v, h, m, l);
+      bf16_t* d = dyl + (4 * dkc + ch) * HW_KS + 8 * dpg;
+      *(s8v*)d = h;
+      *(s8v*)(d + HW_BK * HW_KS) = m;
+      *(s8v*)(d + 2 * HW_BK * HW_KS) = l;
+    }
+#pragma unroll
+    for (int u = 0; u < NUX; ++u) {
+      const int uu = tid + 256 * u;
+      if (uu >= nxu) continue;
+      const int cg = uu & 7, rest = uu >> 3;
+      const int xc = rest % ncol8, xrr = rest / ncol8;
+#pragma unroll
+      for (int ch = 0; ch < 4; ++ch) {
+        const float sc = ch == 0 ? xsc[u].x : ch == 1 ? xsc[u].y : ch == 2 ? xsc[u].z : xsc[u].w;
+        const float sh = ch == 0 ? xsh[u].x : ch == 1 ? xsh[u].y : ch == 2 ? xsh[u].z : xsh[u].w;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float e = ch == 0 ? rx[u][j].x : ch == 1 ? rx[u][j].y : ch == 2 ? rx[u][j].z : rx[u][j].w;
+          if (xf && ((xok[u] >> j) & 1u)) {
+            e = e * sc + sh;
+            if (a.in_relu) e = fmaxf(e, 0.f);
+          }
+          v[j] = e;
+        }
+        s8v h, m, l;
+        split8(v, h, m, l);
+        bf16_t* d = xl + (4 * cg + ch) * hg.CS + xrr * hg.HCp + 8 * xc;
+        *(s8v*)d = h;
+        *(s8v*)(d + HW_BC * hg.CS) = m;
+        *(s8v*)(d + 2 * HW_BC * hg.CS) = l;
+      }
+    }
+  };
+
+  // ---- fragments: wave (kb, tap half); lane l: row / column l & 31, pixels 8 (l >> 5) .. + 7
+  const int kb = wid >> 1, th = wid & 1;
+  const int tap0 = th ? TAPS0 : 0, ntap = th ? T - TAPS0 : TAPS0;
+  const int arow = (kb * 32 + (lane & 31)) * HW_KS;
+  int xbase[8];  // per step: halo element offset of the lane's first pixel (tap (0, 0))
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    const int p = 16 * ks + 8 * (lane >> 5);
+    const int prow = p >> hg.lgW, pcol = p & (OW - 1);
+    const int seg = prow / hg.SR, i = prow - seg * hg.SR;
+    xbase[ks] = (lane & 31) * hg.CS + (seg * hg.HR + i) * hg.HCp + pcol;
+  }
+  f16v acc[TAPS0];
+#pragma unroll
+  for (int t = 0; t < TAPS0; ++t)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[t][v] = 0.f;
+
+  if (t0 < t1) {
+    load_tile(t0);
+    for (int tile = t0; tile < t1; ++tile) {
+      __syncthreads();  // previous tile's fragment reads are done
+      store_tile();
+      if (tile + 1 < t1) load_tile(tile + 1);  // in flight during this tile's MFMAs
+      __syncthreads();
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const bf16_t* ap = dyl + arow + 16 * ks + 8 * (lane >> 5);
+        const s8v ah = *(const s8v*)ap, am = *(const s8v*)(ap + HW_BK * HW_KS),
+                  al = *(const s8v*)(ap + 2 * HW_BK * HW_KS);
+        s8v bh[TAPS0], bm[TAPS0], bl[TAPS0];
+#pragma unroll
+        for (int tt = 0; tt < TAPS0; ++tt) {
+          const int t = min(tap0 + tt, T - 1), r = t / RS, s = t - r * RS;
+          const bf16_t* bp = xl + xbase[ks] + r * hg.HCp + s;
+          bh[tt] = *(const s8v*)bp;
+          bm[tt] = *(const s8v*)(bp + HW_BC * hg.CS);
+          bl[tt] = *(const s8v*)(bp + 2 * HW_BC * hg.CS);
+        }
+        // the taps' six-product chains interleaved stage by stage: TAPS0 independent MFMAs
+        // between two dependent ones (one wave per SIMD: nothing else hides the MFMA latency)
+        f16v c[TAPS0];
+#pragma unroll
+        for (int tt = 0; tt < TAPS0; ++tt) c[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[tt], (f16v){}, 0, 0, 0);
+#pragma unroll
+        for (int tt = 0; tt < TAPS0; ++tt) c[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[tt], c[tt], 0, 0, 0);
+#pragma unroll
+        for (int tt = 0; tt < TAPS0; ++tt) c[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm[tt], c[tt], 0, 0, 0);
+#pragma unroll
+        for (int tt = 0; tt < TAPS0; ++tt) c[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm[tt], c[tt], 0, 0, 0);
+#pragma unroll
+        for (int tt = 0; tt < TAPS0; ++tt) c[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh[tt], c[tt], 0, 0, 0);
+#pragma unroll
+        for (int tt = 0; tt < TAPS0; ++tt) c[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[tt], c[tt], 0, 0, 0);
+#pragma unroll
+        for (int tt = 0; tt < TAPS0; ++tt) {
+#pragma unroll
+          for (int v = 0; v < 16; ++v) acc[tt][v] = acc[tt][v] + c[tt][v];
+          asm volatile("" : "+v"(acc[tt]));
+        }
+      }
+    }
+  }
+
+  // ---- epilogue: 32x32 block (kb, tap): col = lane & 31 (channel), row = 8 (v >> 2) + 4 (lane >> 5) + (v & 3)
+  const long long qd = (long long)T * C;  // dW row length (taps x channels)
+  const bool split_store = nsplit > 1;
+  float* dst = split_store ? a.partial + ((long long)split * a.G + g) * K * qd : a.out + (long long)g * a.out_gs;
+#pragma unroll
+  for (int tt = 0; tt < TAPS0; ++tt) {
+    if (tt >= ntap) break;
+    const int t = tap0 + tt;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int k = k0 + kb * 32 + 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
+      const long long off = (long long)k * qd + (long long)t * C + c0 + (lane & 31);
+      if (split_store) dst[off] = acc[tt][v];
+      else dst[off] = (a.accumulate ? dst[off] : 0.f) + a.gscale * acc[tt][v];
+    }
+  }
+}
+
+}  // namespace
+
+static bool hw_geo(const ConvF32Args& a, HWGeo& h, int& rs) {
+  if (a.stride != 1 || a.R != a.S || (a.R != 1 && a.R != 3) || a.pad != (a.R - 1) / 2) return false;
+  if (a.P != a.H || a.Q != a.W || a.K % HW_BK || a.C % HW_BC) return false;
+  const int OW = a.Q, OH = a.P;
+  if (OW < 8 || OW > HW_TP || (OW & (OW - 1))) return false;
+  rs = a.R;
+  int lg = 0;
+  while ((1 << lg) < OW) ++lg;
+  const int TR = HW_TP / OW;
+  int SR;
+  if (TR <= OH) {
+    if (OH % TR) return false;
+    SR = TR;
+  } else {
+    if (TR % OH) return false;
+    SR = OH;
+  }
+  h.lgW = lg;
+  h.SR = SR;
+  h.NSEG = TR / SR;
+  h.HR = SR + a.R - 1;
+  h.HCp = (OW + a.S - 1 + 7) / 8 * 8;
+  const int img = h.NSEG * h.HR * h.HCp;
+  h.CS = (img - 8 + 127) / 128 * 128 + 8;  // >= img, == 8 (mod 128): 16 B apart mod 256 B per channel
+  const long long npix = (long long)a.N * a.P * a.Q;
+  h.ntile = (int)((npix + HW_TP - 1) / HW_TP);
+  const int nxu = 8 * h.NSEG * h.HR * (h.HCp / 8);
+  h.NUX = (nxu + 255) / 256;
+  if (h.NUX > 2) return false;
+  const long long lim = (1LL << 31) - 64;
+  if (npix * a.C * 4 > lim || npix * a.K * 4 > lim) return false;
+  return true;
+}
+
+static size_t hw_lds(const HWGeo& h) { return (size_t)3 * (HW_BK * HW_KS + HW_BC * h.CS) * 2; }
+
+extern "C" __attribute__((visibility("default"))) int ddl_x6hw_ok(const ConvF32Args* ap) {
+  HWGeo h;
+  int rs;
+  return hw_geo(*ap, h, rs) && hw_lds(h) <= 160 * 1024 ? 1 : 0;
+}
+
+// pixel tiles per group (the split-K planner's unit)
+extern "C" __attribute__((visibility("default"))) int ddl_x6hw_tiles(const ConvF32Args* ap) {
+  HWGeo h;
+  int rs;
+  return hw_geo(*ap, h, rs) ? h.ntile : 0;
+}
+
+template <int RS, int NUX>
+static int launch_hw(const ConvF32Args& a, const HWGeo& h, hipStream_t s) {
+  const int split = a.split_k < 1 ? 1 : a.split_k;
+  const size_t lds = hw_lds(h);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)convx6hw_kernel<RS, NUX>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+    attr_set = true;
+  }
+  const dim3 grid((unsigned)((a.K / HW_BK) * (a.C / HW_BC)), (unsigned)split, (unsigned)a.G);
+  hipLaunchKernelGGL((convx6hw_kernel<RS, NUX>), grid, dim3(256), lds, s, a, h);
+  return (int)hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("default"))) int ddl_x6hw(const ConvF32Args* ap, hipStream_t s) {
+  const ConvF32Args& a = *ap;
+  HWGeo h;
+  int rs;
+  if (a.G < 1 || a.N < 1 || !hw_geo(a, h, rs) || hw_lds(h) > 160 * 1024) return (int)hipErrorInvalidValue;
+  const int split = a.split_k < 1 ? 1 : a.split_k;
+  if (split > 1) {
+    const long long need = (long long)split * a.G * a.K * a.R * a.S * a.C;
+    if (!a.partial || need > a.partial_cap) return (int)hipErrorInvalidValue;
+  }
+  int e;
+  if (rs == 3) e = h.NUX == 1 ? launch_hw<3, 1>(a, h, s) : launch_hw<3, 2>(a, h, s);
+  else e = h.NUX == 1 ? launch_hw<1, 1>(a, h, s) : launch_hw<1, 2>(a, h, s);
+  return e;
+}

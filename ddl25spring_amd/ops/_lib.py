@@ -180,6 +180,10 @@ _SIGS.update({
     # conv_x6h.hip
     "ddl_x6h": [ctypes.POINTER(ConvF32Args), i32, i32, vp],
     "ddl_x6h_ok": [ctypes.POINTER(ConvF32Args), i32, i32],
+    "ddl_x6hw": [ctypes.POINTER(ConvF32Args), vp],
+    "ddl_x6hw_ok": [ctypes.POINTER(ConvF32Args)],
+    "ddl_x6hw_tiles": [ctypes.POINTER(ConvF32Args)],
+    "ddl_convf32_wgrad_reduce": [vp, vp, i64, i32, i64, i32, i32, f32, vp],
     "ddl_x6h_workspace": [ctypes.POINTER(ConvF32Args), i32, i32],
     "ddl_x6_split_weights": [vp, vp, i32, i32, i32, i32, i32, i64, i64, i32, vp],
     # bn_f32.hip

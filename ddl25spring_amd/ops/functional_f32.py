@@ -386,11 +386,49 @@ def conv_dgrad(dy, w, geom, residual=None, mask=None, out=None, bn=None, mask_bn
     return dx if bn is None else (dx, part)
 
 
+# conv_x6hw.hip: the halo-staged X6 WGRAD (stride-1 "same" convs, K % 64, C % 32, OW a power of
+# two >= 8). Correct (tests/test_x6h_gpu.py::test_x6hw_wgrad) but not yet faster than conv_f32.hip
+# (c64 / c128 / c256 at 8 clients: 0.73 / 0.71 / 0.82 ms vs 0.64 / 0.51 / 0.49 ms; MFMA busy 21 %
+# with one LDS-bound workgroup per CU, profiles/x6hw_wgrad_r4.txt), so OFF by default:
+# DDL_F32_HALO_WGRAD=1 enables it.
+HALO_WGRAD = [os.environ.get("DDL_F32_HALO_WGRAD", "0") == "1"]
+HW_TARGET_WG = int(os.environ.get("DDL_F32_HW_TARGET_WG", "256"))  # one workgroup per CU (LDS-bound)
+
+
+def _halo_wgrad(a, geom, device, split_k: int, ws_role: str) -> bool:
+    """Launch the halo WGRAD when it takes this geometry: split-K over pixel tiles until ~one
+    workgroup per CU (each slice keeping >= 4 tiles), slices folded in slice order."""
+    if not (HALO_WGRAD[0] and _MATH[0] != "mfma32") or not _lib.kernels().ddl_x6hw_ok(ctypes.byref(a)):
+        return False
+    lib = _lib.kernels()
+    ntile = int(lib.ddl_x6hw_tiles(ctypes.byref(a)))
+    base = (geom.K // 64) * (geom.C // 32) * geom.G
+    split = split_k or 1
+    if not split_k:
+        while base * split < HW_TARGET_WG and ntile >= split * 2 * 4 and split < 64:
+            split *= 2
+    n = geom.K * geom.R * geom.S * geom.C
+    if split > 1:
+        buf = workspace(device, ws_role)
+        if split * geom.G * n > buf.numel():
+            split = 1
+        else:
+            a.partial, a.partial_cap = buf.data_ptr(), buf.numel()
+    a.split_k = split
+    check(lib.ddl_x6hw(ctypes.byref(a), stream()), "conv_wgrad_f32_halo")
+    if split > 1:
+        check(lib.ddl_convf32_wgrad_reduce(a.partial, a.out, a.out_gs, geom.G, n, split, a.accumulate, a.gscale,
+                                           stream()), "conv_wgrad_f32_halo_reduce")
+    return True
+
+
 def conv_wgrad(dy, x, geom, dw, accumulate=True, gscale=1.0, in_bn=None, split_k=0, ws_role="main"):
     if not accumulate and gscale != 1.0:
         raise ValueError("a scaled WGRAD must accumulate (it adds into the master weights)")
     a = _args(geom, x=ptr(x), dy=ptr(dy), out=ptr(dw), x_gs=_gs(x), dy_gs=_gs(dy), out_gs=_gs(dw),
               accumulate=int(bool(accumulate)), gscale=float(gscale), **_xform(in_bn))
+    if (F_WGRAD, geom) not in _OVERRIDE and _halo_wgrad(a, geom, dy.device, split_k, ws_role):
+        return dw
     _launch(a, F_WGRAD, geom, dy.device, split_k, ws_role)
     return dw
 

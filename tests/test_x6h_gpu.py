@@ -147,6 +147,57 @@ def test_x6h_dgrad_bn_backward_operand(cuda, geom, split):
             F32.clear_plan(F32.F_DGRAD, geom)
 
 
+WGEOMS = [
+    ConvGeom(G=2, N=5, H=32, W=32, C=64, K=64, R=3, S=3, stride=1, pad=1),    # 4 rows per tile
+    ConvGeom(G=1, N=3, H=16, W=16, C=128, K=128, R=3, S=3, stride=1, pad=1),  # 8 rows
+    ConvGeom(G=2, N=5, H=8, W=8, C=256, K=64, R=3, S=3, stride=1, pad=1),     # 2 images per tile, partial
+    ConvGeom(G=2, N=3, H=32, W=32, C=32, K=64, R=1, S=1, stride=1, pad=0),    # 1x1
+]
+
+
+@pytest.mark.parametrize("split", [0, 1])
+@pytest.mark.parametrize("geom", WGEOMS, ids=[f"{g.C}x{g.K}_{g.H}x{g.W}_{g.R}n{g.N}" for g in WGEOMS])
+def test_x6hw_wgrad(cuda, geom, split):
+    """conv_x6hw.hip: halo-staged WGRAD (pixel-reduction MFMAs over a once-split X halo image) vs
+    float64, plain and with the operand-side BN + ReLU of X, accumulating with a gscale (direct SGD),
+    split over pixel tiles (0 = planner) or not; and bitwise repeatable."""
+    from test_fp32_gpu import ref_wgrad
+    old = F32.HALO_WGRAD[0]
+    F32.HALO_WGRAD[0] = True  # the kernel is opt-in by default (not yet faster than conv_f32.hip)
+    try:
+        _x6hw_case(cuda, geom, split, ref_wgrad)
+    finally:
+        F32.HALO_WGRAD[0] = old
+
+
+def _x6hw_case(cuda, geom, split, ref_wgrad):
+    a = F32._args(geom)
+    assert _lib_ok(a), "geometry must take the halo WGRAD"
+    torch.manual_seed(3)
+    x = torch.randn(geom.G, geom.N, geom.H, geom.W, geom.C, device=cuda)
+    dy = torch.randn(geom.G, geom.N, geom.P, geom.Q, geom.K, device=cuda)
+    dw = torch.zeros(geom.G, geom.K, geom.R, geom.S, geom.C, device=cuda)
+    F32.conv_wgrad(dy, x, geom, dw, accumulate=False, split_k=split)
+    ref = ref_wgrad(dy.cpu(), x.cpu(), geom)
+    _close(dw, ref)
+    dw2 = torch.zeros_like(dw)
+    F32.conv_wgrad(dy, x, geom, dw2, accumulate=False, split_k=split)
+    assert torch.equal(dw, dw2)
+    sc = torch.rand(geom.G, geom.C, device=cuda) + 0.5
+    sh = torch.randn(geom.G, geom.C, device=cuda) * 0.3
+    xa = torch.relu(x.cpu().double() * sc.cpu().double()[:, None, None, None] + sh.cpu().double()[:, None, None, None])
+    w0 = torch.randn_like(dw)
+    w = w0.clone()
+    F32.conv_wgrad(dy, x, geom, w, accumulate=True, gscale=-0.5, in_bn=(sc, sh), split_k=split)
+    _close(w, w0.cpu().double() - 0.5 * ref_wgrad(dy.cpu(), xa, geom))
+
+
+def _lib_ok(a):
+    import ctypes
+    from ddl25spring_amd.ops import _lib
+    return bool(_lib.kernels().ddl_x6hw_ok(ctypes.byref(a)))
+
+
 def test_x6h_split_weights(cuda):
     """The pre-split weight image reconstructs the fp32 weights exactly (h + m + l == w): per
     16-channel chunk three bf16 planes [h0..h15 | m0..m15 | l0..l15]."""
