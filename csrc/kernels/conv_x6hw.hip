@@ -15,9 +15,12 @@
 // elements into an LDS row, so its 16-byte reads are 2-byte aligned (gfx950 LDS serves them).
 // Per 16-pixel step and (k block, tap): six piece products chained from zero, then ONE IEEE add
 // into the fp32 accumulator (the halo FWD / DGRAD kernel's rounding discipline).
-// 4 waves: wave w computes k block (w >> 1) (32 rows) for taps 0..4 (w even) or 5..8 (w odd).
+// 4 waves: wave w computes k block (w >> 1) (32 rows), all taps, over the even (w even) or odd
+// pixel steps of every tile; the two halves are summed once at the end.
 // Split-K over pixel tiles writes [split][G][K][R*S*C] partial slices for convf32_wgrad_reduce;
 // unsplit launches apply out = (accumulate ? out : 0) + gscale * dW directly (direct SGD).
+#include <cstdlib>
+
 #include "ddl_common.h"
 #include "conv_f32_core.h"
 
@@ -37,6 +40,7 @@ struct HWGeo {
   int CS;       // X LDS channel stride (elements)
   int ntile;    // pixel tiles per group
   int NUX;      // X staging units per thread
+  int probe;    // timing probes (DDL_HW_PROBE, wrong results): 1 skip LDS staging, 2 skip MFMAs, 4 skip loads
 };
 
 __device__ __forceinline__ float4 hw_load(const __amdgpu_buffer_rsrc_t& rs, unsigned off) {
@@ -56,7 +60,6 @@ __device__ __forceinline__ void split8(const float (&v)[8], s8v& h, s8v& m, s8v&
 template <int RS, int NUX>
 __global__ __launch_bounds__(256, 1) void convx6hw_kernel(ConvF32Args a, HWGeo hg) {
   constexpr int T = RS * RS, PD = (RS - 1) / 2;
-  constexpr int TAPS0 = (T + 1) / 2;  // taps of the even waves (5 of 9; 1 of 1)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* const dyl = (bf16_t*)smem;                        // [3][64][HW_KS]
   bf16_t* const xl = dyl + 3 * HW_BK * HW_KS;               // [3][32][CS]
@@ -95,56 +98,69 @@ __global__ __launch_bounds__(256, 1) void convx6hw_kernel(ConvF32Args a, HWGeo h
     }
   }
 
+  // per X unit: halo segment, halo row within it, 8-column group (fixed for the kernel)
+  int useg[NUX], uhr[NUX], uxc[NUX], uoff[NUX];  // uoff: LDS element offset of the unit's first channel
+  bool uvalid[NUX];
+#pragma unroll
+  for (int u = 0; u < NUX; ++u) {
+    const int uu = tid + 256 * u, rest = uu >> 3;
+    const int xc = rest % ncol8, xrr = rest / ncol8;  // halo row over segments
+    useg[u] = xrr / hg.HR;
+    uhr[u] = xrr - useg[u] * hg.HR;
+    uxc[u] = xc;
+    uoff[u] = 4 * (uu & 7) * hg.CS + xrr * hg.HCp + 8 * xc;
+    uvalid[u] = uu < nxu;
+  }
   float4 rd[8], rx[NUX][8];
   unsigned xok[NUX];  // bit j: halo pixel j of the unit is a real input pixel
   auto load_tile = [&](int tile) {
-    const long long p0 = (long long)tile * HW_TP;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const long long p = p0 + dpg * 8 + j;
+      const int p = tile * HW_TP + dpg * 8 + j;
       rd[j] = hw_load(rD, p < npix ? (unsigned)((p * K + k0 + 4 * dkc) * 4) : HW_OOB);
     }
-    // first output row of the tile over (n, oh): tile rows are whole image rows
-    const long long row0 = p0 >> hg.lgW;
+    // first output row of the tile over (n, oh): tile rows are whole image rows, one (uniform)
+    // division per tile; a segment past the first is a whole image (seg * SR == seg * P)
+    const int row0 = tile * TR;
+    const int n0 = row0 / a.P, oh0 = row0 - n0 * a.P;
 #pragma unroll
     for (int u = 0; u < NUX; ++u) {
-      const int uu = tid + 256 * u;
       xok[u] = 0;
-      const int cg = uu & 7, rest = uu >> 3;
-      const int xc = rest % ncol8, xrr = rest / ncol8;  // halo row over segments
-      const int seg = xrr / hg.HR, hr = xrr - seg * hg.HR;
-      const long long orow = row0 + (long long)seg * hg.SR;  // first output row of the segment
-      const long long n = orow / a.P;
-      const int ih = (int)(orow - n * a.P) + hr - PD;
+      const int n = n0 + useg[u];
+      const int ih = oh0 + uhr[u] - PD;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int iw = 8 * xc + j - PD;
-        const bool ok = uu < nxu && n < a.N && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        const int iw = 8 * uxc[u] + j - PD;
+        const bool ok = uvalid[u] && n < a.N && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
         xok[u] |= (ok ? 1u : 0u) << j;
-        rx[u][j] = hw_load(rX, ok ? (unsigned)((((n * H + ih) * W + iw) * C + c0 + 4 * cg) * 4) : HW_OOB);
+        rx[u][j] = hw_load(rX, ok ? (unsigned)((((n * H + ih) * W + iw) * C + c0 + 4 * (tid & 7)) * 4) : HW_OOB);
       }
     }
   };
-  auto store_tile = [&]() {
+  // split the loaded dY tile into its bf16 planes (splitting the next tile between the two compute
+  // halves of the current one, to overlap that VALU work with MFMAs, was measured slower: the
+  // extra live registers push the accumulators through AGPR moves)...
+  s8v sd[4][3], sx[NUX][4][3];  // sx: split at write time (registers)
+  auto split_tile = [&]() {
     // dY: channel ch of the unit -> row k = 4 dkc + ch, pixels 8 dpg .. + 7
 #pragma unroll
     for (int ch = 0; ch < 4; ++ch) {
       float v[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = ch == 0 ? rd[j].x : ch == 1 ? rd[j].y : ch == 2 ? rd[j].z : rd[j].w;
-      s8v h, m, l;
-      split8(v, h, m, l);
+      split8(v, sd[ch][0], sd[ch][1], sd[ch][2]);
+    }
+  };
+  // ... and write it to LDS once the previous tile's fragment reads are done
+  auto write_tile = [&]() {
+#pragma unroll
+    for (int ch = 0; ch < 4; ++ch) {
       bf16_t* d = dyl + (4 * dkc + ch) * HW_KS + 8 * dpg;
-      *(s8v*)d = h;
-      *(s8v*)(d + HW_BK * HW_KS) = m;
-      *(s8v*)(d + 2 * HW_BK * HW_KS) = l;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) *(s8v*)(d + pl * HW_BK * HW_KS) = sd[ch][pl];
     }
 #pragma unroll
     for (int u = 0; u < NUX; ++u) {
-      const int uu = tid + 256 * u;
-      if (uu >= nxu) continue;
-      const int cg = uu & 7, rest = uu >> 3;
-      const int xc = rest % ncol8, xrr = rest / ncol8;
 #pragma unroll
       for (int ch = 0; ch < 4; ++ch) {
         const float sc = ch == 0 ? xsc[u].x : ch == 1 ? xsc[u].y : ch == 2 ? xsc[u].z : xsc[u].w;
@@ -159,94 +175,141 @@ __global__ __launch_bounds__(256, 1) void convx6hw_kernel(ConvF32Args a, HWGeo h
           }
           v[j] = e;
         }
-        s8v h, m, l;
-        split8(v, h, m, l);
-        bf16_t* d = xl + (4 * cg + ch) * hg.CS + xrr * hg.HCp + 8 * xc;
-        *(s8v*)d = h;
-        *(s8v*)(d + HW_BC * hg.CS) = m;
-        *(s8v*)(d + 2 * HW_BC * hg.CS) = l;
+        split8(v, sx[u][ch][0], sx[u][ch][1], sx[u][ch][2]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NUX; ++u) {
+      if (!uvalid[u]) continue;
+#pragma unroll
+      for (int ch = 0; ch < 4; ++ch) {
+        bf16_t* d = xl + uoff[u] + ch * hg.CS;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) *(s8v*)(d + pl * HW_BC * hg.CS) = sx[u][ch][pl];
       }
     }
   };
 
-  // ---- fragments: wave (kb, tap half); lane l: row / column l & 31, pixels 8 (l >> 5) .. + 7
-  const int kb = wid >> 1, th = wid & 1;
-  const int tap0 = th ? TAPS0 : 0, ntap = th ? T - TAPS0 : TAPS0;
+  // ---- fragments: wave (kb, kh): k block kb (32 rows), the steps ks = kh, kh + 2, .. of each tile,
+  // ALL taps. lane l: row / column l & 31, pixels 8 (l >> 5) .. + 7. A tap row r is read as two
+  // 16-byte-ALIGNED chunks per plane (halo columns pcol .. pcol + 15); the s = 1, 2 windows are
+  // shifted out of those registers (misaligned ds_read_b128 run at a fraction of the LDS rate:
+  // timing probes DDL_HW_PROBE, profiles/x6hw_wgrad_r4.txt)
+  const int kb = wid >> 1, kh = wid & 1;
   const int arow = (kb * 32 + (lane & 31)) * HW_KS;
-  int xbase[8];  // per step: halo element offset of the lane's first pixel (tap (0, 0))
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
+  // halo element offset of the lane's first pixel (tap (0, 0)) in step ks
+  auto xbase = [&](int ks) {
     const int p = 16 * ks + 8 * (lane >> 5);
     const int prow = p >> hg.lgW, pcol = p & (OW - 1);
-    const int seg = prow / hg.SR, i = prow - seg * hg.SR;
-    xbase[ks] = (lane & 31) * hg.CS + (seg * hg.HR + i) * hg.HCp + pcol;
-  }
-  f16v acc[TAPS0];
+    const int seg = prow / hg.SR, r = prow - seg * hg.SR;
+    return (lane & 31) * hg.CS + (seg * hg.HR + r) * hg.HCp + pcol;
+  };
+  f16v acc[T];
 #pragma unroll
-  for (int t = 0; t < TAPS0; ++t)
+  for (int t = 0; t < T; ++t)
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[t][v] = 0.f;
 
   if (t0 < t1) {
-    load_tile(t0);
+    if (!(hg.probe & 4)) load_tile(t0);
     for (int tile = t0; tile < t1; ++tile) {
       __syncthreads();  // previous tile's fragment reads are done
-      store_tile();
-      if (tile + 1 < t1) load_tile(tile + 1);  // in flight during this tile's MFMAs
+      if (!(hg.probe & 1)) {
+        split_tile();
+        write_tile();
+      }
+      if (tile + 1 < t1 && !(hg.probe & 4)) load_tile(tile + 1);  // in flight during this tile's MFMAs
       __syncthreads();
+      if (hg.probe & 2) continue;
+#pragma unroll 1
+      for (int ip = 0; ip < 2; ++ip) {
+        // two own steps (ks = 4 ip + kh, 4 ip + 2 + kh) per chain: twelve piece products from
+        // zero, then one IEEE add per tap (half the VALU adds of per-step chains)
+        s8v ah[2], am[2], al[2];
+        int xb[2];
 #pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        const bf16_t* ap = dyl + arow + 16 * ks + 8 * (lane >> 5);
-        const s8v ah = *(const s8v*)ap, am = *(const s8v*)(ap + HW_BK * HW_KS),
-                  al = *(const s8v*)(ap + 2 * HW_BK * HW_KS);
-        s8v bh[TAPS0], bm[TAPS0], bl[TAPS0];
-#pragma unroll
-        for (int tt = 0; tt < TAPS0; ++tt) {
-          const int t = min(tap0 + tt, T - 1), r = t / RS, s = t - r * RS;
-          const bf16_t* bp = xl + xbase[ks] + r * hg.HCp + s;
-          bh[tt] = *(const s8v*)bp;
-          bm[tt] = *(const s8v*)(bp + HW_BC * hg.CS);
-          bl[tt] = *(const s8v*)(bp + 2 * HW_BC * hg.CS);
+        for (int j = 0; j < 2; ++j) {
+          const int ks = 4 * ip + 2 * j + kh;
+          xb[j] = xbase(ks);
+          const bf16_t* ap = dyl + arow + 16 * ks + 8 * (lane >> 5);
+          ah[j] = *(const s8v*)ap;
+          am[j] = *(const s8v*)(ap + HW_BK * HW_KS);
+          al[j] = *(const s8v*)(ap + 2 * HW_BK * HW_KS);
         }
-        // the taps' six-product chains interleaved stage by stage: TAPS0 independent MFMAs
-        // between two dependent ones (one wave per SIMD: nothing else hides the MFMA latency)
-        f16v c[TAPS0];
 #pragma unroll
-        for (int tt = 0; tt < TAPS0; ++tt) c[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[tt], (f16v){}, 0, 0, 0);
+        for (int r = 0; r < RS; ++r) {
+          f16v c[RS];
 #pragma unroll
-        for (int tt = 0; tt < TAPS0; ++tt) c[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[tt], c[tt], 0, 0, 0);
+          for (int j = 0; j < 2; ++j) {
+            const bf16_t* bp = xl + xb[j] + r * hg.HCp;
+            s8v bh[RS], bm[RS], bl[RS];
+            const s8v h0 = *(const s8v*)bp, m0 = *(const s8v*)(bp + HW_BC * hg.CS),
+                      l0 = *(const s8v*)(bp + 2 * HW_BC * hg.CS);
+            bh[0] = h0; bm[0] = m0; bl[0] = l0;
+            if constexpr (RS == 3) {
+              const s8v h1 = *(const s8v*)(bp + 8), m1 = *(const s8v*)(bp + 8 + HW_BC * hg.CS),
+                        l1 = *(const s8v*)(bp + 8 + 2 * HW_BC * hg.CS);
+              bh[1] = __builtin_shufflevector(h0, h1, 1, 2, 3, 4, 5, 6, 7, 8);
+              bm[1] = __builtin_shufflevector(m0, m1, 1, 2, 3, 4, 5, 6, 7, 8);
+              bl[1] = __builtin_shufflevector(l0, l1, 1, 2, 3, 4, 5, 6, 7, 8);
+              bh[2] = __builtin_shufflevector(h0, h1, 2, 3, 4, 5, 6, 7, 8, 9);
+              bm[2] = __builtin_shufflevector(m0, m1, 2, 3, 4, 5, 6, 7, 8, 9);
+              bl[2] = __builtin_shufflevector(l0, l1, 2, 3, 4, 5, 6, 7, 8, 9);
+            }
+            // the row's RS chains interleaved stage by stage
 #pragma unroll
-        for (int tt = 0; tt < TAPS0; ++tt) c[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm[tt], c[tt], 0, 0, 0);
+            for (int s2 = 0; s2 < RS; ++s2)
+              c[s2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[j], bh[s2], j ? c[s2] : (f16v){}, 0, 0, 0);
 #pragma unroll
-        for (int tt = 0; tt < TAPS0; ++tt) c[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm[tt], c[tt], 0, 0, 0);
+            for (int s2 = 0; s2 < RS; ++s2) c[s2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[j], bl[s2], c[s2], 0, 0, 0);
 #pragma unroll
-        for (int tt = 0; tt < TAPS0; ++tt) c[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh[tt], c[tt], 0, 0, 0);
+            for (int s2 = 0; s2 < RS; ++s2) c[s2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[j], bm[s2], c[s2], 0, 0, 0);
 #pragma unroll
-        for (int tt = 0; tt < TAPS0; ++tt) c[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[tt], c[tt], 0, 0, 0);
+            for (int s2 = 0; s2 < RS; ++s2) c[s2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[j], bm[s2], c[s2], 0, 0, 0);
 #pragma unroll
-        for (int tt = 0; tt < TAPS0; ++tt) {
+            for (int s2 = 0; s2 < RS; ++s2) c[s2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[j], bh[s2], c[s2], 0, 0, 0);
 #pragma unroll
-          for (int v = 0; v < 16; ++v) acc[tt][v] = acc[tt][v] + c[tt][v];
-          asm volatile("" : "+v"(acc[tt]));
+            for (int s2 = 0; s2 < RS; ++s2) c[s2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[j], bh[s2], c[s2], 0, 0, 0);
+          }
+#pragma unroll
+          for (int s2 = 0; s2 < RS; ++s2) {
+#pragma unroll
+            for (int v = 0; v < 16; ++v) acc[r * RS + s2][v] = acc[r * RS + s2][v] + c[s2][v];
+          }
         }
       }
     }
   }
+
+  // ---- the two step-parity halves of each k block: kh = 1 hands its sums to kh = 0 through LDS
+  // (fixed order: deterministic), which adds and writes
+  __syncthreads();
+  float* const red = (float*)smem;  // [2 kb][T][16][64]
+  if (kh == 1) {
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) red[((kb * T + t) * 16 + v) * 64 + lane] = acc[t][v];
+  }
+  __syncthreads();
+  if (kh == 1) return;
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[t][v] = acc[t][v] + red[((kb * T + t) * 16 + v) * 64 + lane];
 
   // ---- epilogue: 32x32 block (kb, tap): col = lane & 31 (channel), row = 8 (v >> 2) + 4 (lane >> 5) + (v & 3)
   const long long qd = (long long)T * C;  // dW row length (taps x channels)
   const bool split_store = nsplit > 1;
   float* dst = split_store ? a.partial + ((long long)split * a.G + g) * K * qd : a.out + (long long)g * a.out_gs;
 #pragma unroll
-  for (int tt = 0; tt < TAPS0; ++tt) {
-    if (tt >= ntap) break;
-    const int t = tap0 + tt;
+  for (int t = 0; t < T; ++t) {
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
       const int k = k0 + kb * 32 + 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
       const long long off = (long long)k * qd + (long long)t * C + c0 + (lane & 31);
-      if (split_store) dst[off] = acc[tt][v];
-      else dst[off] = (a.accumulate ? dst[off] : 0.f) + a.gscale * acc[tt][v];
+      if (split_store) dst[off] = acc[t][v];
+      else dst[off] = (a.accumulate ? dst[off] : 0.f) + a.gscale * acc[t][v];
     }
   }
 }
@@ -282,17 +345,23 @@ static bool hw_geo(const ConvF32Args& a, HWGeo& h, int& rs) {
   const int nxu = 8 * h.NSEG * h.HR * (h.HCp / 8);
   h.NUX = (nxu + 255) / 256;
   if (h.NUX > 2) return false;
+  static const int probe = getenv("DDL_HW_PROBE") ? atoi(getenv("DDL_HW_PROBE")) : 0;
+  h.probe = probe;
   const long long lim = (1LL << 31) - 64;
   if (npix * a.C * 4 > lim || npix * a.K * 4 > lim) return false;
   return true;
 }
 
-static size_t hw_lds(const HWGeo& h) { return (size_t)3 * (HW_BK * HW_KS + HW_BC * h.CS) * 2; }
+static size_t hw_lds(const HWGeo& h, int T) {
+  const size_t stage = (size_t)3 * (HW_BK * HW_KS + HW_BC * h.CS) * 2;
+  const size_t red = (size_t)2 * T * 16 * 64 * 4;  // the epilogue's cross-wave sums
+  return stage > red ? stage : red;
+}
 
 extern "C" __attribute__((visibility("default"))) int ddl_x6hw_ok(const ConvF32Args* ap) {
   HWGeo h;
   int rs;
-  return hw_geo(*ap, h, rs) && hw_lds(h) <= 160 * 1024 ? 1 : 0;
+  return hw_geo(*ap, h, rs) && hw_lds(h, rs * rs) <= 160 * 1024 ? 1 : 0;
 }
 
 // pixel tiles per group (the split-K planner's unit)
@@ -305,7 +374,7 @@ extern "C" __attribute__((visibility("default"))) int ddl_x6hw_tiles(const ConvF
 template <int RS, int NUX>
 static int launch_hw(const ConvF32Args& a, const HWGeo& h, hipStream_t s) {
   const int split = a.split_k < 1 ? 1 : a.split_k;
-  const size_t lds = hw_lds(h);
+  const size_t lds = hw_lds(h, RS * RS);
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)convx6hw_kernel<RS, NUX>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -321,7 +390,7 @@ extern "C" __attribute__((visibility("default"))) int ddl_x6hw(const ConvF32Args
   const ConvF32Args& a = *ap;
   HWGeo h;
   int rs;
-  if (a.G < 1 || a.N < 1 || !hw_geo(a, h, rs) || hw_lds(h) > 160 * 1024) return (int)hipErrorInvalidValue;
+  if (a.G < 1 || a.N < 1 || !hw_geo(a, h, rs) || hw_lds(h, rs * rs) > 160 * 1024) return (int)hipErrorInvalidValue;
   const int split = a.split_k < 1 ? 1 : a.split_k;
   if (split > 1) {
     const long long need = (long long)split * a.G * a.K * a.R * a.S * a.C;

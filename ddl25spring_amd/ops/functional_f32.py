@@ -387,18 +387,19 @@ def conv_dgrad(dy, w, geom, residual=None, mask=None, out=None, bn=None, mask_bn
 
 
 # conv_x6hw.hip: the halo-staged X6 WGRAD (stride-1 "same" convs, K % 64, C % 32, OW a power of
-# two >= 8). Correct (tests/test_x6h_gpu.py::test_x6hw_wgrad) but not yet faster than conv_f32.hip
-# (c64 / c128 / c256 at 8 clients: 0.73 / 0.71 / 0.82 ms vs 0.64 / 0.51 / 0.49 ms; MFMA busy 21 %
-# with one LDS-bound workgroup per CU, profiles/x6hw_wgrad_r4.txt), so OFF by default:
-# DDL_F32_HALO_WGRAD=1 enables it.
-HALO_WGRAD = [os.environ.get("DDL_F32_HALO_WGRAD", "0") == "1"]
+# two >= 8). It beats conv_f32.hip on images >= 16 wide (8 clients, c64 / c128: 0.49 / 0.46 ms vs
+# 0.65 / 0.50 ms) and loses on 8x8 (c256: 0.55 vs 0.50 ms: the halo is 60 % padding there),
+# profiles/x6hw_wgrad_r4.txt. DDL_F32_HALO_WGRAD=0 disables it; HW_MIN_W is the width rule.
+HALO_WGRAD = [os.environ.get("DDL_F32_HALO_WGRAD", "1") != "0"]
+HW_MIN_W = int(os.environ.get("DDL_F32_HW_MIN_W", "16"))
 HW_TARGET_WG = int(os.environ.get("DDL_F32_HW_TARGET_WG", "256"))  # one workgroup per CU (LDS-bound)
 
 
 def _halo_wgrad(a, geom, device, split_k: int, ws_role: str) -> bool:
     """Launch the halo WGRAD when it takes this geometry: split-K over pixel tiles until ~one
     workgroup per CU (each slice keeping >= 4 tiles), slices folded in slice order."""
-    if not (HALO_WGRAD[0] and _MATH[0] != "mfma32") or not _lib.kernels().ddl_x6hw_ok(ctypes.byref(a)):
+    if not (HALO_WGRAD[0] and _MATH[0] != "mfma32") or geom.W < HW_MIN_W \
+            or not _lib.kernels().ddl_x6hw_ok(ctypes.byref(a)):
         return False
     lib = _lib.kernels()
     ntile = int(lib.ddl_x6hw_tiles(ctypes.byref(a)))

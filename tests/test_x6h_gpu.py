@@ -162,12 +162,12 @@ def test_x6hw_wgrad(cuda, geom, split):
     float64, plain and with the operand-side BN + ReLU of X, accumulating with a gscale (direct SGD),
     split over pixel tiles (0 = planner) or not; and bitwise repeatable."""
     from test_fp32_gpu import ref_wgrad
-    old = F32.HALO_WGRAD[0]
-    F32.HALO_WGRAD[0] = True  # the kernel is opt-in by default (not yet faster than conv_f32.hip)
+    old = F32.HALO_WGRAD[0], F32.HW_MIN_W
+    F32.HALO_WGRAD[0], F32.HW_MIN_W = True, 0  # every geometry the kernel takes (8x8 included)
     try:
         _x6hw_case(cuda, geom, split, ref_wgrad)
     finally:
-        F32.HALO_WGRAD[0] = old
+        F32.HALO_WGRAD[0], F32.HW_MIN_W = old
 
 
 def _x6hw_case(cuda, geom, split, ref_wgrad):
