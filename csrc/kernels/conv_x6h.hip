@@ -88,6 +88,10 @@ __device__ __forceinline__ float4 bload4(const __amdgpu_buffer_rsrc_t& rs, unsig
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, soff, 0));
 }
 
+#ifndef X6H_CHAIN
+#define X6H_CHAIN 3
+#endif
+
 template <int MODE, int BP, int RS, int HB>
 __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo hg) {
   constexpr int T = RS * RS;                 // taps
@@ -271,7 +275,9 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
   for (int dr = 0; dr < RS; ++dr)
 #pragma unroll
     for (int tj = 0; tj < TJ; ++tj) bdr[dr][tj] = boff[tj] + dr * hg.ROWB;
-  auto compute = [&](int buf, int t) {
+  // X6H_CHAIN (1 or 2): steps per chain before the IEEE add (unrolled-tap path only)
+  f16v cch[TI][TJ];
+  auto compute = [&](int buf, int t, bool first = true, bool last = true) {
     const char* P = pimg + buf * PIMG;
     const int dr = t / RS, ds = t - dr * RS;
     // one 16-channel step: A (weights) and B (activations) as three piece vectors each; the six
@@ -295,17 +301,21 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
     for (int ti = 0; ti < TI; ++ti)
 #pragma unroll
       for (int tj = 0; tj < TJ; ++tj) {
-        f16v c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ti], bh[tj], (f16v){}, 0, 0, 0);
+        f16v c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ti], bh[tj], first ? (f16v){} : cch[ti][tj], 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ti], bl[tj], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[ti], bm[tj], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ti], bm[tj], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[ti], bh[tj], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ti], bh[tj], c, 0, 0, 0);
+        if (last) {
 #pragma unroll
-        for (int v = 0; v < 16; ++v) acc[ti][tj][v] = acc[ti][tj][v] + c[v];
-        // pin the adds to this step: otherwise they sink past the unrolled taps' barriers and
-        // every step's chain result lives (in scratch) until the end of the chunk
-        asm volatile("" : "+v"(acc[ti][tj]));
+          for (int v = 0; v < 16; ++v) acc[ti][tj][v] = acc[ti][tj][v] + c[v];
+          // pin the adds to this step: otherwise they sink past the unrolled taps' barriers and
+          // every step's chain result lives (in scratch) until the end of the chunk
+          asm volatile("" : "+v"(acc[ti][tj]));
+        } else {
+          cch[ti][tj] = c;
+        }
       }
   };
 
@@ -336,7 +346,9 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
           if (t + 2 < T) wload((t + 2) % 3, cc, t + 2);
           else if (more) wload((t + 2) % 3, cc + 1, t + 2 - T);
           if (t == HT && more) halo_load(cc + 1);
-          compute(t % 3, t);
+          if constexpr (X6H_CHAIN == 3) compute(t % 3, t, t % 3 == 0, t % 3 == 2);
+          else if constexpr (X6H_CHAIN == 2) compute(t % 3, t, t % 2 == 0, t % 2 == 1 || t == T - 1);
+          else compute(t % 3, t);
           // keep each step's MFMAs and adds inside the step: moved across the barrier into the next
           // step they pile up two steps' operands and chains and spill
           __builtin_amdgcn_sched_barrier(0);
