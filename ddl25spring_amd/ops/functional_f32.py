@@ -138,6 +138,9 @@ def set_halo(on: bool) -> None:
         _PLANS.clear()
 
 
+HALO_MIN_W = int(os.environ.get("DDL_F32_HALO_MIN_W", "8"))  # narrowest image the halo FWD / DGRAD takes by default
+
+
 def halo_ok(mode: int, g, auto: bool = False) -> bool:
     """Mirror of conv_x6h.hip x6h_geo: can the halo kernel run this (mode, geometry)? ``auto``: is it
     also the default choice there (explicit plans may pin it where it is not)?"""
@@ -148,7 +151,7 @@ def halo_ok(mode: int, g, auto: bool = False) -> bool:
     OH, OW = g.P, g.Q
     if OW < 4 or OW > 128 or OW & (OW - 1):
         return False
-    if auto and OW < 8:  # 8 images per tile: measured slower than conv_f32.hip (profiles/x6h_layers_r4.txt)
+    if auto and OW < HALO_MIN_W:  # 4x4: measured slower than conv_f32.hip (profiles/x6h_layers_r4.txt)
         return False
     TR = 128 // OW
     if TR <= OH:
@@ -397,7 +400,7 @@ HW_TARGET_WG = int(os.environ.get("DDL_F32_HW_TARGET_WG", "256"))  # one workgro
 
 def _halo_wgrad(a, geom, device, split_k: int, ws_role: str) -> bool:
     """Launch the halo WGRAD when it takes this geometry: split-K over pixel tiles until ~one
-    workgroup per CU (each slice keeping >= 4 tiles), slices folded in slice order."""
+    workgroup per CU (each slice keeping >= 3 tiles), slices folded in slice order."""
     if not (HALO_WGRAD[0] and _MATH[0] != "mfma32") or geom.W < HW_MIN_W \
             or not _lib.kernels().ddl_x6hw_ok(ctypes.byref(a)):
         return False
@@ -406,14 +409,14 @@ def _halo_wgrad(a, geom, device, split_k: int, ws_role: str) -> bool:
     base = (geom.K // 64) * (geom.C // 32) * geom.G
     split = split_k or 1
     if not split_k:
-        while base * split < HW_TARGET_WG and ntile >= split * 2 * 4 and split < 64:
+        while base * split < HW_TARGET_WG and ntile >= split * 2 * 3 and split < 128:
             split *= 2
     n = geom.K * geom.R * geom.S * geom.C
     if split > 1:
         buf = workspace(device, ws_role)
-        if split * geom.G * n > buf.numel():
-            split = 1
-        else:
+        while split > 1 and split * geom.G * n > buf.numel():
+            split //= 2  # the largest split the workspace holds (plan-determined: eager == captured)
+        if split > 1:
             a.partial, a.partial_cap = buf.data_ptr(), buf.numel()
     a.split_k = split
     check(lib.ddl_x6hw(ctypes.byref(a), stream()), "conv_wgrad_f32_halo")
