@@ -409,7 +409,8 @@ def _halo_wgrad(a, geom, device, split_k: int, ws_role: str) -> bool:
     base = (geom.K // 64) * (geom.C // 32) * geom.G
     split = split_k or 1
     if not split_k:
-        while base * split < HW_TARGET_WG and ntile >= split * 2 * 3 and split < 128:
+        target = min(HW_TARGET_WG, TARGET_WG)  # TARGET_WG = 1 pins split-K off for every conv
+        while base * split < target and ntile >= split * 2 * 3 and split < 128:
             split *= 2
     n = geom.K * geom.R * geom.S * geom.C
     if split > 1:

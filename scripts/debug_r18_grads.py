@@ -40,18 +40,21 @@ t64 = tm.double()
 lt = F.cross_entropy(t64(x.double()), y)
 lt.backward()
 g32 = {n: p.grad for n, p in t32.named_parameters()}
-w32 = max(_err(g32[n], p.grad) for n, p in t64.named_parameters())
-print(f"stock torch fp32: worst relative gradient error {w32:.2e}")
+e32 = sorted(_err(g32[n], p.grad) for n, p in t64.named_parameters())
+w32 = e32[-1]
+print(f"stock torch fp32: worst relative gradient error {w32:.2e}, median {e32[len(e32) // 2]:.2e}")
 print(f"G={G} B={a.batch} twg={a.target_wg} halo={a.halo} math={a.math} loss {loss[0].item():.8f} "
       f"ref {lt.item():.8f}")
 for grp in range(G):
     g = convert.export_torch(net, t64, mapping, group=grp, grads=True)
-    worst, bad = 0.0, []
+    worst, bad, errs = 0.0, [], []
     for name, p in t64.named_parameters():
         e = _err(g[name], p.grad)
+        errs.append(e)
         worst = max(worst, e)
         if e > 1e-4:
             bad.append(f"{name}:{e:.1e}")
         if not a.quiet:
             print(f"  {name:40s} {e:.2e} {'BAD' if e > 1e-4 else ''}")
-    print(f"  group {grp}: worst {worst:.2e}; {len(bad)} bad: {' '.join(bad[:12])}")
+    errs.sort()
+    print(f"  group {grp}: worst {worst:.2e}, median {errs[len(errs) // 2]:.2e}; {len(bad)} bad: {' '.join(bad[:12])}")
