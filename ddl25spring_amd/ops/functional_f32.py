@@ -167,6 +167,28 @@ def halo_ok(mode: int, g, auto: bool = False) -> bool:
     return HP <= HALO_HPMAX and SC % 16 == 0 and Pd % 4 == 0
 
 
+# A stride-1 1x1 conv is a GEMM over pixels: its image shape does not matter. FLAT1X1 re-shapes
+# such a launch as rows of 128 pixels (N = 1, W = 128) whenever N*H*W % 128 == 0 and the image width
+# is not already a power of two (ResNet-50's 56 / 28 / 14 / 7), so the halo kernels
+# (conv_x6h.hip FWD / DGRAD, conv_x6hw.hip WGRAD) take it; memory layout, strides, BN statistics
+# and residual / mask layouts are unchanged. OFF by default: ResNet-50 fp32 ran 2.86k vs 3.58k
+# images/s with every mode flattened (the image geometry keeps its tuned conv_f32 plans);
+# DDL_F32_FLAT1X1=1 (all modes) or a subset of "fdw" enables it.
+_FLAT_ENV = os.environ.get("DDL_F32_FLAT1X1", "0")
+FLAT1X1 = [_FLAT_ENV != "0", "fdw" if _FLAT_ENV == "1" else _FLAT_ENV]  # on, modes ("f", "d", "w")
+
+
+def _launch_geom(geom, mode: str = "f"):
+    if not FLAT1X1[0] or mode not in FLAT1X1[1] or geom.R != 1 or geom.S != 1 or geom.stride != 1 or geom.pad != 0:
+        return geom
+    if geom.W & (geom.W - 1) == 0 and geom.W <= 128:
+        return geom
+    npix = geom.N * geom.H * geom.W
+    if npix % 128:
+        return geom
+    return type(geom)(geom.G, 1, npix // 128, 128, geom.C, geom.K, 1, 1, 1, 0)
+
+
 def _cfg(cfg: int) -> int:
     """Launch cfg with the engine bit: forced by a fixed engine; under "auto" the plan's own."""
     if _MATH[0] == "x6":
@@ -332,6 +354,7 @@ def conv_fwd(x, w, geom, bias=None, relu=False, stats=None, out=None, residual=N
                                                 device=x.device)
     if residual is not None and (residual.stride(0) != y.stride(0) or not residual.is_contiguous()):
         residual = residual.contiguous()
+    geom = _launch_geom(geom, "f")
     a = _args(geom, x=ptr(x), w=ptr(w), out=ptr(y), bias=ptr(bias), residual=ptr(residual),
               x_gs=_gs(x), w_gs=_gs(w), out_gs=_gs(y), bias_gs=_gs(bias), relu=int(bool(relu)), **_xform(in_bn))
     if stats is not None:
@@ -353,6 +376,8 @@ def conv_dgrad(dy, w, geom, residual=None, mask=None, out=None, bn=None, mask_bn
     too, for the layer's WGRAD); launches off the halo kernel materialise it first."""
     dx = out if out is not None else torch.empty(geom.G, geom.N, geom.H, geom.W, geom.C, dtype=torch.float32,
                                                  device=dy.device)
+    if residual_sub == 1:
+        geom = _launch_geom(geom, "d")
     kw = {}
     if dy_bn is not None:
         xb, coef = dy_bn
@@ -430,6 +455,7 @@ def _halo_wgrad(a, geom, device, split_k: int, ws_role: str) -> bool:
 def conv_wgrad(dy, x, geom, dw, accumulate=True, gscale=1.0, in_bn=None, split_k=0, ws_role="main"):
     if not accumulate and gscale != 1.0:
         raise ValueError("a scaled WGRAD must accumulate (it adds into the master weights)")
+    geom = _launch_geom(geom, "w")
     a = _args(geom, x=ptr(x), dy=ptr(dy), out=ptr(dw), x_gs=_gs(x), dy_gs=_gs(dy), out_gs=_gs(dw),
               accumulate=int(bool(accumulate)), gscale=float(gscale), **_xform(in_bn))
     if (F_WGRAD, geom) not in _OVERRIDE and _halo_wgrad(a, geom, dy.device, split_k, ws_role):

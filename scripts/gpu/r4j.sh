@@ -11,6 +11,9 @@ step() {  # name timeout cmd...
   echo "[$name] rc=$rc :: $(tail -1 gpurun_out/${T}_${name}.log | cut -c1-260)"
   case $rc in 0) ;; *) echo "[$name] failed: stopping"; exit 1;; esac
 }
+for M in fwd dgrad; do for W in 8 4; do
+  DDL_F32_HALO_MIN_W=$W timeout -k 10 60 python scripts/conv_f32_bench.py --math auto --mode $M --layer c512 --reps 20 2>&1 | tail -1 | sed "s/^/minw=$W /" || exit 1
+done; done
 step bench 300 python -u bench.py --steps 5 --warmup 2
 for C in 1 2 4; do
   step clients$C 300 python -u bench.py --steps 5 --warmup 2 --clients $C --train-size $((6250 * C))
