@@ -91,3 +91,23 @@ def test_fp32_plans_engine_choice():
         F32.set_math(old_math)
         F32.set_halo(True)
         F32._PLANS.clear()
+
+
+def test_flat1x1_launch_geometry(monkeypatch):
+    """Stride-1 1x1 convs re-shaped as rows of 128 pixels (opt-in DDL_F32_FLAT1X1): only eligible
+    geometries change, the pixel count is preserved, and per-mode selection is honoured."""
+    from ddl25spring_amd.ops import functional_f32 as F32
+    monkeypatch.setattr(F32, "FLAT1X1", [True, "fdw"])
+    g = ConvGeom(G=2, N=4, H=56, W=56, C=64, K=256, R=1, S=1, stride=1, pad=0)
+    f = F32._launch_geom(g, "w")
+    assert (f.G, f.N, f.W, f.C, f.K, f.R, f.stride, f.pad) == (2, 1, 128, 64, 256, 1, 1, 0)
+    assert f.H * f.W == g.N * g.H * g.W and (f.P, f.Q) == (f.H, f.W)
+    for keep in (ConvGeom(2, 4, 56, 56, 64, 256, 3, 3, 1, 1),   # 3x3
+                 ConvGeom(2, 4, 56, 56, 64, 256, 1, 1, 2, 0),   # stride 2
+                 ConvGeom(2, 4, 32, 32, 64, 256, 1, 1, 1, 0),   # power-of-two width: halo takes it as is
+                 ConvGeom(2, 3, 7, 7, 64, 256, 1, 1, 1, 0)):    # 147 pixels: not a multiple of 128
+        assert F32._launch_geom(keep, "f") is keep
+    monkeypatch.setattr(F32, "FLAT1X1", [True, "d"])
+    assert F32._launch_geom(g, "w") is g and F32._launch_geom(g, "d") != g
+    monkeypatch.setattr(F32, "FLAT1X1", [False, "fdw"])
+    assert F32._launch_geom(g, "d") is g
