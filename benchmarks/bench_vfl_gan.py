@@ -5,7 +5,8 @@ with the D6 balanced feature split, batch 64, AdamW. world 2: rank 0 = active pa
 feature block 0), rank 1 = passive party (block 1), cut-layer tensors over RCCL P2P; world 1: both
 parties in one process. Metric: samples/s of split-NN training.
 DCGAN: CIFAR-10-shaped 32x32x3, 2 clients (one per rank at world 2), FedAvg of G and D every
-``--local-steps`` Adam steps. Metric: GAN images/s (real + fake images through D per step).
+``--local-steps`` Adam steps. Metric: GAN images/s (real + fake images through D per step), fp32
+(the reference's precision, on the main line) and bf16 (a second, labelled line).
 """
 from __future__ import annotations
 
@@ -25,6 +26,8 @@ def main():
     ap.add_argument("--local-steps", type=int, default=20)
     ap.add_argument("--gan-batch", type=int, default=128)
     ap.add_argument("--vfl-batch", type=int, default=64)
+    ap.add_argument("--gan-precisions", default="fp32,bf16",
+                    help="DCGAN precisions, the first is the headline line (fp32 = the reference's)")
     args = ap.parse_args()
     from ddl25spring_amd.apps.gan import GANConfig, client_images
     from ddl25spring_amd.data import heart as H
@@ -75,22 +78,37 @@ def main():
             pty.fit(xs[1], 1, args.vfl_batch)
     dt_v = timed(ctx, epoch, args.steps, args.warmup)
     vfl_sps = len(y) * args.steps / dt_v
-    # ---------------- federated DCGAN (2 clients)
+    # ---------------- federated DCGAN (2 clients): fp32 (the reference's precision) first, then bf16
     gcfg = GANConfig(clients=2, local_steps=args.local_steps, batch_size=args.gan_batch,
                      train_size=10000)
     data = client_images(gcfg, dev)
-    fg = FederatedGAN(data, ctx=ctx, local_steps=args.local_steps,
-                      batch_size=args.gan_batch, device=dev)
-    dt_g = timed(ctx, lambda: fg.run(1), args.steps, args.warmup)
+    gan = {}
+    for prec in args.gan_precisions.split(","):
+        fg = FederatedGAN(data, ctx=ctx, local_steps=args.local_steps,
+                          batch_size=args.gan_batch, device=dev, precision=prec)
+        fg.run(args.warmup)
+        # timed rounds enqueue without host syncs (device-made inputs, native aggregation); the
+        # losses are read once when run() returns
+        fg.sync_rounds = False
+        dt = timed(ctx, lambda: fg.run(args.steps), 1, 0)
+        gan[prec] = dt
     imgs = 2 * 2 * args.local_steps * args.gan_batch * args.steps  # 2 clients x (real + fake)
+    precs = list(gan)
     emit(ctx, metric="VFL split-NN samples/s + federated DCGAN images/s", value=round(vfl_sps, 1),
          unit="samples/s", n_gpus=ctx.world, steps=args.steps, warmup=args.warmup,
          ms_per_step=round(1e3 * dt_v / args.steps, 3), higher_is_better=True, scaling="strong",
-         vs_baseline=None, dtype="fp32 (split-NN) / bf16 (DCGAN)",
+         vs_baseline=None, dtype=f"fp32 (split-NN) / {precs[0]} (DCGAN)",
          data="heart.csv" if real else "synthetic",
-         gan_images_per_s=round(imgs / dt_g, 1), gan_ms_per_round=round(1e3 * dt_g / args.steps, 3),
+         gan_images_per_s=round(imgs / gan[precs[0]], 1), gan_ms_per_round=round(1e3 * gan[precs[0]] / args.steps, 3),
          config={"model": "splitnn-heart-2party + dcgan-cifar32", "global_batch": args.vfl_batch,
                  "seq_len": None, "parallelism": f"vfl2party-fedgan2-w{ctx.world}"})
+    for prec in precs[1:]:  # labelled extra lines (the faster non-reference precision)
+        emit(ctx, metric="federated DCGAN images/s", value=round(imgs / gan[prec], 1), unit="images/s",
+             n_gpus=ctx.world, steps=args.steps, warmup=args.warmup,
+             ms_per_step=round(1e3 * gan[prec] / args.steps, 3), higher_is_better=True, scaling="strong",
+             vs_baseline=None, dtype=prec, data="synthetic",
+             config={"model": "dcgan-cifar32", "global_batch": 2 * args.gan_batch, "seq_len": None,
+                     "parallelism": f"fedgan2-w{ctx.world}"})
     rdist.shutdown()
 
 

@@ -54,11 +54,18 @@ __device__ __forceinline__ void slot_fold(const float* __restrict__ base, int S,
   double a0 = 0.0, a1 = 0.0;
   if (valid) {
     int k = sg;
-    for (; k + NSG < S; k += 2 * NSG) {  // 2 slots' loads in flight per thread
-      const float x0 = base[(long long)k * 2 * C + c], y0 = base[(long long)k * 2 * C + C + c];
-      const float x1 = base[(long long)(k + NSG) * 2 * C + c], y1 = base[(long long)(k + NSG) * 2 * C + C + c];
-      a0 += x0; a0 += x1;
-      a1 += y0; a1 += y1;
+    for (; k + 7 * NSG < S; k += 8 * NSG) {  // 8 slots' loads in flight per thread, added in slot order
+      float xs[8], ys[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        xs[j] = base[(long long)(k + j * NSG) * 2 * C + c];
+        ys[j] = base[(long long)(k + j * NSG) * 2 * C + C + c];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        a0 += xs[j];
+        a1 += ys[j];
+      }
     }
     for (; k < S; k += NSG) {
       a0 += base[(long long)k * 2 * C + c];
@@ -92,13 +99,22 @@ __device__ __forceinline__ void slot_fold_chan(const float* __restrict__ base, i
   __syncthreads();
   double a = 0.0;
   if (valid) {
-    for (int k = sg; k < S; k += NSG) {
+    auto term = [&](int k, float s0) {
       const long long rem = M - (long long)k * rows;
       const double n = (double)(rem < rows ? rem : rows);
-      if (n <= 0.0) continue;
-      const double d = (double)base[(long long)k * 2 * C + c] - n * mu;
+      if (n <= 0.0) return;
+      const double d = (double)s0 - n * mu;
       a += d * d / n;
+    };
+    int k = sg;
+    for (; k + 7 * NSG < S; k += 8 * NSG) {  // loads ahead, terms in slot order
+      float xs[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xs[j] = base[(long long)(k + j * NSG) * 2 * C + c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) term(k + j * NSG, xs[j]);
     }
+    for (; k < S; k += NSG) term(k, base[(long long)k * 2 * C + c]);
   }
   red[sg * 64 + cl] = a;
   __syncthreads();

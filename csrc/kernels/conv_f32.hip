@@ -547,31 +547,53 @@ __global__ __launch_bounds__(256, (X6 && BP * BQ <= 64 * 128) ? 3 : 2) void conv
 }
 
 // WGRAD split-K: out = (accumulate ? out : 0) + gscale * sum_k partial[k] (slice order).
+// V floats per thread (4: float4 lanes for big outputs; 1: small outputs, e.g. a 64-channel 3x3
+// dW at one client, 36,864 floats over 128 slices, which as float4 threads filled only 36
+// workgroups and ran 30-70 us latency-bound). The slice loads are issued 8 at a time ahead of the
+// adds, which still run in slice order: the sum is bitwise the sequential one.
+template <int V>
 __global__ __launch_bounds__(256) void convf32_wgrad_reduce(const float* __restrict__ part, float* out,
-                                                            long long out_gs, int G, long long n4,
+                                                            long long out_gs, int G, long long nv,
                                                             int splits, int accumulate, float gscale) {
-  const long long per = n4 * 4;
-  GSTRIDE_LOOP(t, (long long)G * n4) {
-    const long long g = t / n4, i = (t - g * n4) * 4;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  typedef float vec __attribute__((ext_vector_type(V)));
+  const long long per = nv * V;
+  GSTRIDE_LOOP(t, (long long)G * nv) {
+    const long long g = t / nv, i = (t - g * nv) * V;
+    vec s = (vec)(0.f);
     const float* src = part + g * per + i;
-    for (int k = 0; k < splits; ++k) {
-      const float4 v = *(const float4*)(src + (long long)k * G * per);
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    const long long sstride = (long long)G * per;
+    int k = 0;
+    for (; k + 8 <= splits; k += 8) {
+      vec v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = *(const vec*)(src + (long long)(k + j) * sstride);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
     }
+    for (; k < splits; ++k) s += *(const vec*)(src + (long long)k * sstride);
     float* d = out + g * out_gs + i;
-    float4 b = accumulate ? *(const float4*)d : make_float4(0.f, 0.f, 0.f, 0.f);
-    b.x += gscale * s.x; b.y += gscale * s.y; b.z += gscale * s.z; b.w += gscale * s.w;
-    *(float4*)d = b;
+    vec b = accumulate ? *(const vec*)d : (vec)(0.f);
+    b += gscale * s;
+    *(vec*)d = b;
   }
+}
+
+static void launch_wgrad_reduce(const float* part, float* out, long long out_gs, int G, long long n, int splits,
+                                int accumulate, float gscale, hipStream_t s) {
+  // float4 lanes once that still gives >= 2 workgroups per CU, scalar lanes below
+  if ((long long)G * (n / 4) >= 512LL * 256)
+    hipLaunchKernelGGL(convf32_wgrad_reduce<4>, dim3(grid_for((long long)G * (n / 4), 256)), dim3(256), 0, s, part,
+                       out, out_gs, G, n / 4, splits, accumulate, gscale);
+  else
+    hipLaunchKernelGGL(convf32_wgrad_reduce<1>, dim3(grid_for((long long)G * n, 256)), dim3(256), 0, s, part, out,
+                       out_gs, G, n, splits, accumulate, gscale);
 }
 
 // the same fold for other WGRAD producers of [split][G][Pd][Qd] slices (conv_x6hw.hip)
 DDL_API int ddl_convf32_wgrad_reduce(const float* part, float* out, long long out_gs, int G, long long n, int splits,
                                      int accumulate, float gscale, hipStream_t s) {
   if (n % 4) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(convf32_wgrad_reduce, dim3(grid_for((long long)G * (n / 4), 256)), dim3(256), 0, s, part, out,
-                     out_gs, G, n / 4, splits, accumulate, gscale);
+  launch_wgrad_reduce(part, out, out_gs, G, n, splits, accumulate, gscale, s);
   return (int)hipGetLastError();
 }
 
@@ -630,9 +652,7 @@ static int launch_tile(ConvF32Args a, hipStream_t s) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || split == 1 || a.tickets) return (int)e;
   if (MODE == F_WGRAD) {
-    const long long n4 = Pd * Qd / 4;
-    hipLaunchKernelGGL(convf32_wgrad_reduce, dim3(grid_for((long long)a.G * n4, 256)), dim3(256), 0, s,
-                       (const float*)a.partial, a.out, a.out_gs, a.G, n4, split, a.accumulate, a.gscale);
+    launch_wgrad_reduce((const float*)a.partial, a.out, a.out_gs, a.G, Pd * Qd, split, a.accumulate, a.gscale, s);
   } else {
     hipLaunchKernelGGL((convf32_splitk_epilogue<MODE, BP, BQ>), dim3((unsigned)(ntp * ntq), nph, a.G),
                        dim3(256), 0, s, a);

@@ -467,6 +467,69 @@ __global__ __launch_bounds__(256) void x6_split_weights_kernel(const float* __re
   }
 }
 
+// Many weights' split images in ONE launch (a training step's pre-split: every halo layer's FWD and
+// DGRAD images of the step's weights, functional_f32.PresplitScope) instead of one launch per conv.
+// Entry e owns blocks [blk0, blk0 + nblk); its blocks grid-stride over its 16-element chunks.
+struct SplitDesc {
+  const float* w;
+  char* out;
+  long long w_gs, o_gs;
+  int G, K, T, C, layout, blk0, nblk, pad_;
+};
+
+__device__ __forceinline__ void split_chunk(const float* __restrict__ wg, char* d, long long e, int K, int T, int C,
+                                            int layout) {
+  float v[16];
+  if (layout == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4 f = *(const float4*)(wg + e * 16 + 4 * i);
+      v[4 * i] = f.x; v[4 * i + 1] = f.y; v[4 * i + 2] = f.z; v[4 * i + 3] = f.w;
+    }
+  } else {
+    const int K16 = K / 16;
+    const long long ct = e / K16;
+    const int k = (int)(e - ct * K16) * 16;
+    const int c = (int)(ct / T), tap = (int)(ct - (long long)c * T);
+    const float* s = wg + ((long long)k * T + tap) * C + c;
+    const long long ks = (long long)T * C;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = s[i * ks];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    s4v h, m, l;
+    split3(make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]), h, m, l);
+    *(s4v*)(d + 8 * q) = h;
+    *(s4v*)(d + 32 + 8 * q) = m;
+    *(s4v*)(d + 64 + 8 * q) = l;
+  }
+}
+
+__global__ __launch_bounds__(256) void x6_split_weights_multi_kernel(const SplitDesc* __restrict__ descs, int n) {
+  int lo = 0, hi = n - 1;  // the entry owning this block: last e with blk0 <= blockIdx.x
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (descs[mid].blk0 <= (int)blockIdx.x) lo = mid; else hi = mid - 1;
+  }
+  const SplitDesc d = descs[lo];
+  const long long per = (long long)d.K * d.T * d.C / 16;
+  const long long total = (long long)d.G * per;
+  for (long long t = (long long)(blockIdx.x - d.blk0) * 256 + threadIdx.x; t < total; t += (long long)d.nblk * 256) {
+    const long long g = t / per, e = t - g * per;
+    split_chunk(d.w + g * d.w_gs, d.out + g * d.o_gs + e * 96, e, d.K, d.T, d.C, d.layout);
+  }
+}
+
+DDL_API int ddl_x6_split_desc_size() { return (int)sizeof(SplitDesc); }
+
+// descs: device array of n SplitDesc (blk0 / nblk filled by the host), nblocks = total blocks
+DDL_API int ddl_x6_split_weights_multi(const void* descs, int n, int nblocks, hipStream_t s) {
+  if (n < 1 || nblocks < n) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(x6_split_weights_multi_kernel, dim3(nblocks), dim3(256), 0, s, (const SplitDesc*)descs, n);
+  return (int)hipGetLastError();
+}
+
 // Halo row / segment strides (in 16-B quads): the fewest bank conflicts of the fragment reads
 // (the 4 ds_read_b128 lane groups of a 32x32x16 B operand: lane l reads tile pixel l & 31, chunk
 // half l >> 5), then the fewest bytes; within HBSMALL when any candidate fits.
@@ -546,7 +609,9 @@ static bool x6h_geo(const ConvF32Args& a, int mode, int bp, HaloGeo& h, int& rs)
   const long long lim = (1LL << 31) - 64;
   if ((long long)a.N * a.H * a.W * h.SC * 4 > lim || (long long)h.Pd * a.R * a.S * h.SC * 6 > lim) return false;
   halo_layout(h);
-  if (h.HBYTES > HBLARGE || (h.HBYTES > HBSMALL && h.HP > 288) || (h.HBYTES <= HBSMALL && h.HP > 208)) return false;
+  // the instance is chosen by x6h_large(): a halo of more than 208 pixels (e.g. 64-wide images: two
+  // rows of 66) runs on the large instance even when its bytes would fit the small one
+  if (h.HBYTES > HBLARGE || h.HP > 288) return false;
   return true;
 }
 
@@ -575,10 +640,10 @@ static int dispatch_hb(const ConvF32Args& a, int bp, int rs, const HaloGeo& h, h
   if (rs == 3) return bp == 128 ? launch_x6h<MODE, 128, 3, HB>(a, h, s) : launch_x6h<MODE, 64, 3, HB>(a, h, s);
   return bp == 128 ? launch_x6h<MODE, 128, 1, HB>(a, h, s) : launch_x6h<MODE, 64, 1, HB>(a, h, s);
 }
+static bool x6h_large(const HaloGeo& h) { return h.HBYTES > HBSMALL || h.HP > 208; }
 template <int MODE>
 static int dispatch_x6h(const ConvF32Args& a, int bp, int rs, const HaloGeo& h, hipStream_t s) {
-  return h.HBYTES <= HBSMALL ? dispatch_hb<MODE, HBSMALL>(a, bp, rs, h, s)
-                             : dispatch_hb<MODE, HBLARGE>(a, bp, rs, h, s);
+  return x6h_large(h) ? dispatch_hb<MODE, HBLARGE>(a, bp, rs, h, s) : dispatch_hb<MODE, HBSMALL>(a, bp, rs, h, s);
 }
 
 // Can the halo kernel run this (mode, geometry) with BP = (cfg & 0xff) * 16?

@@ -427,6 +427,37 @@ DDL_API int ddl_bce_logits(const void* logits, int ld, const float* targets, flo
   return (int)hipGetLastError();
 }
 
+// fp32 logits (the reference-precision DCGAN): one workgroup, the per-thread partial sums meet in a
+// fixed-order LDS tree, so the loss is bitwise reproducible (no float atomics); R = clients x batch
+// rows is small. The loss is written, not accumulated.
+__global__ __launch_bounds__(256) void bce_logits_f32_kernel(const float* __restrict__ logits, int ld,
+                                                             const float* __restrict__ targets, float tval, int R,
+                                                             float gs, float* __restrict__ loss,
+                                                             float* __restrict__ dlogits) {
+  __shared__ float red[256];
+  float acc = 0.f;
+  for (int r = threadIdx.x; r < R; r += 256) {
+    const float l = logits[(long long)r * ld];
+    const float t = targets ? targets[r] : tval;
+    acc += fmaxf(l, 0.f) - l * t + log1pf(expf(-fabsf(l)));
+    if (dlogits) dlogits[(long long)r * ld] = (1.f / (1.f + expf(-l)) - t) * gs;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *loss = red[0];
+}
+
+DDL_API int ddl_bce_logits_f32(const float* logits, int ld, const float* targets, float tval, int R, float gs,
+                               float* loss, float* dlogits, hipStream_t s) {
+  if (R < 1 || ld < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bce_logits_f32_kernel, dim3(1), dim3(256), 0, s, logits, ld, targets, tval, R, gs, loss, dlogits);
+  return (int)hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------------------------
 // Fused classifier head of a training step: global average pool -> Linear (+bias) -> softmax CE
 // with hard labels -> the Linear's weight / bias gradients -> the pool's input gradient, masked by

@@ -869,3 +869,47 @@ NN_EXPORT(maxpool_fwd, (const void* x, void* y, void* am, int NB, int H, int W, 
 NN_EXPORT(maxpool_bwd, (const void* x, const void* dy, const void* am, void* dx, int NB, int H, int W, int C, int k,
                         int st, int pd, hipStream_t s),
           (x, dy, am, dx, NB, H, W, C, k, st, pd, s))
+
+// ---------------------------------------------------------------------------------------------
+// Federated-DCGAN round inputs generated on the device (fl/gan.py): for slot g (a client of the
+// round, desc[g] = {seed, n, off}) and local step i, the batch indices
+//   idx[i][g*B + b] = off + floor(u32 * n / 2^32),  u32 = Philox(seed, i*B + b, tag A).x
+// and the generator noise z[i][g][b][k] ~ N(0, 1) by Box-Muller on Philox(seed, (i*B+b)*nz + k, tag B).
+// Both are pure functions of the client's (round, client) seed, so a client's batches and noise do
+// not depend on its slot or on how many ranks share the clients; ops/reference.gan_inputs is the
+// numpy twin (the CPU engines).
+__global__ __launch_bounds__(256) void gan_inputs_kernel(const long long* __restrict__ desc, int G, int steps, int B,
+                                                         int nz, long long* __restrict__ idx, float* __restrict__ z) {
+  const long long ni = (long long)steps * G * B, nzt = ni * nz;
+  for (long long t = blockIdx.x * 256LL + threadIdx.x; t < ni + nzt; t += (long long)gridDim.x * 256) {
+    if (t < ni) {  // idx [steps][G*B]
+      const int i = (int)(t / ((long long)G * B));
+      const int gb = (int)(t - (long long)i * G * B), g = gb / B, b = gb - g * B;
+      const unsigned long long seed = (unsigned long long)desc[3 * g];
+      const unsigned long long e = (unsigned long long)i * B + b;
+      const uint4 r = philox4x32(make_uint4((uint32_t)e, (uint32_t)(e >> 32), 0x1d872b41u, 0u),
+                                 make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+      idx[t] = desc[3 * g + 2] + (long long)(((unsigned long long)r.x * (unsigned long long)desc[3 * g + 1]) >> 32);
+    } else {  // z [steps][G][B][nz]
+      const long long u = t - ni;
+      const long long row = u / nz;
+      const int k = (int)(u - row * nz);
+      const int i = (int)(row / ((long long)G * B));
+      const int gb = (int)(row - (long long)i * G * B), g = gb / B, b = gb - g * B;
+      const unsigned long long seed = (unsigned long long)desc[3 * g];
+      const unsigned long long e = ((unsigned long long)i * B + b) * nz + k;
+      const uint4 r = philox4x32(make_uint4((uint32_t)e, (uint32_t)(e >> 32), 0x6a09e667u, 0u),
+                                 make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+      const float u1 = fmaxf(u32_to_unit(r.x), 1e-12f), u2 = u32_to_unit(r.y);
+      z[u] = sqrtf(-2.f * logf(u1)) * cosf(6.28318530717958648f * u2);
+    }
+  }
+}
+
+DDL_API int ddl_gan_inputs(const long long* desc, int G, int steps, int B, int nz, long long* idx, float* z,
+                           hipStream_t s) {
+  if (G < 1 || steps < 1 || B < 1 || nz < 1) return (int)hipErrorInvalidValue;
+  const long long work = (long long)steps * G * B * (nz + 1);
+  hipLaunchKernelGGL(gan_inputs_kernel, dim3(grid_for(work, 256)), dim3(256), 0, s, desc, G, steps, B, nz, idx, z);
+  return (int)hipGetLastError();
+}

@@ -10,6 +10,8 @@ No torch.utils.cpp_extension / hipify step is involved: the kernels are plain HI
 from __future__ import annotations
 
 import argparse
+import hashlib
+import json
 import os
 import shutil
 import subprocess
@@ -76,16 +78,22 @@ def build_kernels(force: bool = False, verbose: bool = False) -> Path:
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", f"-I{CSRC / 'include'}",
              "-Wno-unused-result", "-Wno-unused-value", "-munsafe-fp-atomics"]
 
+    status: dict[str, str] = {}
+
     def compile_one(src: Path) -> Path:
         obj = OBJDIR / (src.stem + ".o")
         if force or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, hdr_time):
             if verbose:
                 print(f"[build] hipcc {src.name}", flush=True)
             _run([hipcc, *flags, *PER_FILE_FLAGS.get(src.name, []), "-c", str(src), "-o", str(obj)])
+            status[src.name] = "compiled"
+        else:
+            status[src.name] = "reused"
         return obj
 
     with ThreadPoolExecutor(_jobs()) as ex:
         objs = list(ex.map(compile_one, srcs))
+    linked = False
     if force or not KERNEL_LIB.exists() or KERNEL_LIB.stat().st_mtime < _newest(objs):
         if verbose:
             print(f"[build] link {KERNEL_LIB.name}", flush=True)
@@ -93,7 +101,44 @@ def build_kernels(force: bool = False, verbose: bool = False) -> Path:
         _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)])
         _check_undefined(tmp)
         os.replace(tmp, KERNEL_LIB)
+        linked = True
+    write_manifest(srcs + headers, status, linked)
+    if verbose:
+        n_c = sum(v == "compiled" for v in status.values())
+        print(f"[build] kernels: {n_c} compiled, {len(status) - n_c} reused (object newer than source), "
+              f"library {'linked' if linked else 'up to date'}; manifest {MANIFEST.name}", flush=True)
     return KERNEL_LIB
+
+
+MANIFEST = LIBDIR / "build_manifest.json"
+
+
+def _sha(p: Path) -> str:
+    return hashlib.sha256(p.read_bytes()).hexdigest()
+
+
+def write_manifest(sources, status: dict, linked: bool) -> None:
+    """Provenance of the kernel library: sha256 of every source / header it was built from and of
+    the library itself, and which objects this build compiled or reused. ``verify_manifest`` (run
+    by smoke() on the GPU box) re-hashes the tree's sources and the loaded library against it."""
+    man = {"arch": ARCH, "library": KERNEL_LIB.name, "library_sha256": _sha(KERNEL_LIB),
+           "sources": {str(p.relative_to(ROOT)): _sha(p) for p in sorted(sources)},
+           "objects": status, "linked_this_build": linked}
+    MANIFEST.write_text(json.dumps(man, indent=1, sort_keys=True))
+
+
+def verify_manifest() -> dict:
+    """-> {"ok": bool, "stale_sources": [...], "library_matches": bool}: does the library on disk
+    come from this tree's sources (as recorded when it was built)?"""
+    if not MANIFEST.exists() or not KERNEL_LIB.exists():
+        return {"ok": False, "error": "no manifest / library"}
+    man = json.loads(MANIFEST.read_text())
+    stale = [k for k, h in man["sources"].items() if not (ROOT / k).exists() or _sha(ROOT / k) != h]
+    srcs = sorted(str(p.relative_to(ROOT)) for p in [*(CSRC / "kernels").glob("*.hip"), *(CSRC / "include").glob("*.h")])
+    missing = [k for k in srcs if k not in man["sources"]]
+    lib_ok = _sha(KERNEL_LIB) == man["library_sha256"]
+    return {"ok": not stale and not missing and lib_ok, "stale_sources": stale + missing, "library_matches": lib_ok,
+            "library_sha256": man["library_sha256"][:16]}
 
 
 def build_runtime(force: bool = False, verbose: bool = False) -> Path:

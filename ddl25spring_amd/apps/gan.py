@@ -23,6 +23,7 @@ class GANConfig:
     save: str = ""  # rank 0 writes the final flat global (G | D | BN) weights here (torch.save)
     ckpt_dir: str = ""  # per-rank sharded checkpoint (runtime/checkpoint.py); resumes if committed
     ckpt_every: int = 0  # commit every N rounds (0: only at the end)
+    precision: str = "fp32"  # fp32 (the reference's generative lab) | bf16
 
 
 def client_images(cfg: GANConfig, device):
@@ -40,11 +41,13 @@ def run_gan(cfg: GANConfig, ctx, log=print):
     data = client_images(cfg, ctx.device)
     fg = FederatedGAN(data, ctx=ctx, ngf=cfg.ngf, ndf=cfg.ndf, lr=cfg.lr,
                       local_steps=cfg.local_steps, batch_size=cfg.batch_size,
-                      client_fraction=cfg.client_fraction, seed=cfg.seed, device=ctx.device)
+                      client_fraction=cfg.client_fraction, seed=cfg.seed, device=ctx.device,
+                      precision=cfg.precision)
     ckpt = None
     if cfg.ckpt_dir:
         from ..runtime.checkpoint import ShardedCheckpoint
-        tag = f"gan,clients={cfg.clients},C={cfg.client_fraction},bs={cfg.batch_size},ls={cfg.local_steps},seed={cfg.seed}"
+        tag = (f"gan,clients={cfg.clients},C={cfg.client_fraction},bs={cfg.batch_size},ls={cfg.local_steps},"
+               f"seed={cfg.seed},prec={cfg.precision}")
         ckpt = ShardedCheckpoint(cfg.ckpt_dir, ctx, tag=tag)
         got = ckpt.load()
         if got is not None:

@@ -6,9 +6,15 @@ of both networks (and of the BN running statistics), exactly as FedAvgServer doe
 (reference hfl_complete.py:336-390 is the aggregation template). One rank per GPU; client c
 lives on rank c % world for the whole run (its Adam state stays there, like a real device); the
 weighted sums of all ranks meet in ONE all-reduce per round over a flat fp32 buffer
-(G params | D params | BN buffers). Batch indices AND generator noise of a client's round are
-drawn from that client's own seeded generator, so the result does not depend on how many ranks
-share the clients: W ranks reproduce the single-process run.
+(G params | D params | BN buffers).
+
+Precision (``precision``): "fp32" by default — the reference's generative lab trains in fp32
+(lab/tutorial_2a/generative-modeling.py:13-130) — every layer on the fp32 kernels; "bf16" runs
+bf16 MFMA operands / activations with fp32 master weights.
+
+Batch indices AND generator noise of a client's round are a pure function of that client's
+(round, client) seed (Philox, ``Fn.gan_inputs``: generated on the device by one kernel, by its
+numpy twin on the CPU), so a client trains on the same data whatever slot or rank it lands on.
 
 Each client keeps its own Adam moments and step count across rounds, as a real client device
 would.
@@ -17,11 +23,13 @@ Client-batched engine (``batched``, the default on the GPU): all of a rank's cli
 train TOGETHER — G and D hold S client slots ([S, ...] slot tensors, models.dcgan.Grouped*), every
 layer of every client is ONE grouped launch (ops/grouped.py), one SlotAdam launch steps all slots
 with per-client step counters, and the round's ``local_steps`` steps of all slots replay from ONE
-HIP graph per slot count. Batch indices / noise are drawn per client from the same seeded
-generators as the sequential engine (so both engines train the same clients on the same data),
-uploaded once per round; download, weighted aggregation and the all-reduce stay on the device over
-the flat (G | D | BN) buffers, with one host sync per round (wall time and the loss log). Adam state
-stays in its slot while the slot keeps its client (client_fraction 1: never copied).
+HIP graph per slot count. The round's inputs are made on the device from a [G, 3] (seed, n,
+offset) descriptor (one small asynchronous upload); the n_k-weighted aggregation is the native
+``weighted_sum`` (products rounded, added in slot order) over the flat (G | D | BN) rows; then the
+all-reduce. With ``sync_rounds = False`` a round enqueues all of that without any host sync (the
+losses stay on the device until ``run`` returns). Adam state stays in its slot while the slot keeps
+its client (client_fraction 1: never copied). W ranks reproduce the single-process run up to the
+all-reduce's summation order (tests/test_gan_multirank_cpu.py).
 
 Sequential engine (``batched=False``; the CPU default): one client after another through a single
 (G, D) pair, its Adam state swapped in and out of the fused FlatAdam buffers; on the GPU each
@@ -40,6 +48,7 @@ import torch
 
 from ..models.dcgan import (Discriminator, GANTrainer, Generator, GroupedDiscriminator, GroupedGANTrainer,
                             GroupedGenerator)
+from ..ops import functional as Fn
 from ..runtime.graphs import CapturedStep
 
 # the slot tensors' gradients are strided rows of SlotAdam's [S, P] buffer (CPU autograd path)
@@ -80,14 +89,15 @@ class FederatedGAN:
     def __init__(self, client_data: list[torch.Tensor], ctx=None, nz: int = 100, ngf: int = 64,
                  ndf: int = 64, lr: float = 2e-4, betas=(0.5, 0.999), local_steps: int = 10,
                  batch_size: int = 64, client_fraction: float = 1.0, seed: int = 0, device=None,
-                 use_graph: bool = True, batched: bool | None = None):
+                 use_graph: bool = True, batched: bool | None = None, precision: str = "fp32"):
         self.ctx = ctx
         self.rank = ctx.rank if ctx else 0
         self.world = ctx.world if ctx else 1
         self.device = torch.device(device) if device is not None else client_data[0].device
         torch.manual_seed(seed)
-        self.G = Generator(nz, ngf).to(self.device)
-        self.D = Discriminator(ndf).to(self.device)
+        self.precision = precision
+        self.G = Generator(nz, ngf, precision=precision).to(self.device)
+        self.D = Discriminator(ndf, precision=precision).to(self.device)
         self.trainer = GANTrainer(self.G, self.D, lr, betas)
         self.optG, self.optD = self.trainer.optG, self.trainer.optD
         if ctx and self.world > 1:
@@ -104,6 +114,9 @@ class FederatedGAN:
         self._z: dict = {}      # client -> static [local_steps, batch, nz] generator noise buffer
         self._graphs: dict = {}  # client -> CapturedStep over its local steps
         self.round_idx = 0       # rounds done (seeds the per-round client generators)
+        # False: rounds run without host syncs (no per-round wall time / loss read; run() reads the
+        # losses once at the end), as FedAvg's unsynchronised rounds (fl/algorithms.py)
+        self.sync_rounds = True
         self.batched = (self.device.type == "cuda") if batched is None else bool(batched)
         if self.batched:
             self._init_batched(lr, betas)
@@ -155,6 +168,10 @@ class FederatedGAN:
             tdev = [None if o.t_dev is None else o.t_dev.clone() for o in (self.optG, self.optD)]
             self._state[c] = (self.optG.m.clone(), self.optG.v.clone(), self.optG.t,
                               self.optD.m.clone(), self.optD.v.clone(), self.optD.t, *tdev)
+
+    def _client_seed(self, c: int, r: int) -> int:
+        # round stride = all clients (not K): no two (round, client) pairs share a stream
+        return self.seed + int(c) + 1 + r * len(self.data)
 
     def _local_steps(self, c):
         data, idx, z = self.data[c], self._idx[c], self._z[c]
@@ -280,20 +297,12 @@ class FederatedGAN:
             oD.sync_shadow()
             mine = self._assign_slots(mine)
             B, nz = self.batch_size, self.G.nz
-            idx = torch.empty(self.local_steps, G * B, dtype=torch.int64)
-            z = torch.empty(self.local_steps, G, B, nz)
-            for i, c in enumerate(mine):
-                # the sequential engine's per-(round, client) stream: same batches, same noise
-                g = torch.Generator(device="cpu").manual_seed(self.seed + c + 1 + r * len(self.data))
-                n_c = len(self.data[c])
-                idx[:, i * B:(i + 1) * B] = torch.stack([torch.randint(0, n_c, (B,), generator=g)
-                                                         for _ in range(self.local_steps)]) + self._off[c]
-                z[:, i] = torch.randn(self.local_steps, B, nz, generator=g)
             if G not in self._bidx:
-                self._bidx[G] = torch.empty_like(idx, device=self.device)
-                self._bz[G] = torch.empty_like(z, device=self.device)
-            self._bidx[G].copy_(idx, non_blocking=False)
-            self._bz[G].copy_(z, non_blocking=False)
+                self._bidx[G] = torch.empty(self.local_steps, G * B, dtype=torch.int64, device=self.device)
+                self._bz[G] = torch.empty(self.local_steps, G, B, nz, device=self.device)
+            # the sequential engine's per-(round, client) streams: same batches, same noise
+            desc = [(self._client_seed(c, r), len(self.data[c]), self._off[c]) for c in mine]
+            Fn.gan_inputs(desc, self.local_steps, B, nz, self._bidx[G], self._bz[G])
             if self.use_graph:
                 if G not in self._bgraphs:
                     # a weak self: no engine <-> graph cycle, so the graph dies with the engine
@@ -304,24 +313,59 @@ class FederatedGAN:
             else:
                 ld, lg = self._batched_local(G)
             res.samples += self.batch_size * self.local_steps * G
-            coef = torch.tensor(self.n[mine] / wsum, dtype=torch.float32, device=self.device).view(G, 1)
-            with torch.no_grad():
-                parts = [self._row_global((coef * oG.data[:G]).sum(0), self.G, oG),
-                         self._row_global((coef * oD.data[:G]).sum(0), self.D, oD)]
-                parts += [(coef.view(G, *([1] * (gb.dim() - 1))) * gb[:G]).sum(0).reshape(-1) for gb in self._gbufs]
-                acc = torch.cat(parts)
+            acc = self._aggregate_slots(mine, G, wsum)
         else:
             acc = torch.zeros_like(self._flat())
             ld = lg = None
         if self.ctx and self.world > 1:
             self.ctx.all_reduce(acc)
         self._load_flat(acc)
-        if self.device.type == "cuda":
-            torch.cuda.synchronize()
-        res.wall_time.append(time.perf_counter() - t0)
-        # the grouped losses are sums over the slots' own mean losses: / G = the clients' mean
-        res.loss_d.append(float(ld) / G if G else 0.0)
-        res.loss_g.append(float(lg) / G if G else 0.0)
+        self._finish_round(res, t0, ld, lg, G)
+
+    def _aggregate_slots(self, mine, G, wsum):
+        """The rank's n_k-weighted partial FedAvg of its G slots in ``_flat``'s layout: on the device
+        the native weighted sum (aggregate.hip: products rounded, added in slot order) of the slot
+        rows of (G | D | BN buffers); the CPU path the same with torch ops."""
+        oG, oD = self.gtr.optG, self.gtr.optD
+        cvals = [float(self.n[c] / wsum) for c in mine]
+        with torch.no_grad():
+            if self.device.type == "cuda" and hasattr(self.optG, "data"):
+                coef = torch.tensor(cvals, dtype=torch.float32).pin_memory().to(self.device, non_blocking=True)
+                acc = torch.empty(self._flat_numel(), dtype=torch.float32, device=self.device)
+                off = 0
+                for rows in [oG.data[:G], oD.data[:G]] + [gb[:G].reshape(G, -1) for gb in self._gbufs]:
+                    n = rows.shape[1]
+                    Fn.weighted_sum(rows, coef, acc[off:off + n])
+                    off += n
+                return acc
+            coef = torch.tensor(cvals, dtype=torch.float32, device=self.device).view(G, 1)
+            parts = [self._row_global((coef * oG.data[:G]).sum(0), self.G, oG),
+                     self._row_global((coef * oD.data[:G]).sum(0), self.D, oD)]
+            parts += [(coef.view(G, *([1] * (gb.dim() - 1))) * gb[:G]).sum(0).reshape(-1) for gb in self._gbufs]
+            return torch.cat(parts)
+
+    def _flat_numel(self) -> int:
+        """Length of the flat (G | D | BN) buffer of ``_flat``."""
+        if not hasattr(self, "_flat_len"):
+            self._flat_len = sum(t.numel() for t in self._global_tensors())
+        return self._flat_len
+
+    def _finish_round(self, res, t0, ld, lg, nloc):
+        """Round bookkeeping. Synchronised rounds: device sync, peer-read barrier check, wall time
+        and the losses as floats. Unsynchronised: the losses stay device tensors (``run`` reads them
+        once at the end) and the round leaves no host sync behind."""
+        div = max(1, nloc)
+        if self.sync_rounds or self.device.type != "cuda":
+            if self.device.type == "cuda":
+                torch.cuda.synchronize()
+            if self.ctx is not None:
+                self.ctx.check_comm()  # a peer-read all-reduce timeout must not load a corrupt aggregate silently
+            res.wall_time.append(time.perf_counter() - t0)
+            res.loss_d.append(float(ld) / div if ld is not None else 0.0)
+            res.loss_g.append(float(lg) / div if lg is not None else 0.0)
+        else:
+            res.loss_d.append(ld.detach().clone() / div if ld is not None else 0.0)
+            res.loss_g.append(lg.detach().clone() / div if lg is not None else 0.0)
         res.rounds += 1
         self.round_idx += 1
 
@@ -331,7 +375,7 @@ class FederatedGAN:
         if self.batched:
             for _ in range(rounds):
                 self._round_batched(res)
-            return res
+            return self._settle(res)
         for _ in range(rounds):
             r = self.round_idx
             t0 = time.perf_counter()
@@ -344,17 +388,13 @@ class FederatedGAN:
             for c in mine:
                 self._load_flat(glob)
                 self._swap_in(int(c))
-                # round stride = all clients (not K): no two (round, client) pairs share a stream
-                g = torch.Generator(device="cpu").manual_seed(self.seed + int(c) + 1 + r * len(self.data))
                 data = self.data[int(c)]
-                idx = torch.stack([torch.randint(0, len(data), (self.batch_size,), generator=g)
-                                   for _ in range(self.local_steps)])
-                z = torch.randn(self.local_steps, self.batch_size, self.G.nz, generator=g)
                 if int(c) not in self._idx:
-                    self._idx[int(c)] = torch.empty_like(idx, device=data.device)
-                    self._z[int(c)] = torch.empty_like(z, device=data.device)
-                self._idx[int(c)].copy_(idx)
-                self._z[int(c)].copy_(z)
+                    self._idx[int(c)] = torch.empty(self.local_steps, self.batch_size, dtype=torch.int64,
+                                                    device=data.device)
+                    self._z[int(c)] = torch.empty(self.local_steps, self.batch_size, self.G.nz, device=data.device)
+                Fn.gan_inputs([(self._client_seed(c, r), len(data), 0)], self.local_steps, self.batch_size,
+                              self.G.nz, self._idx[int(c)], self._z[int(c)])
                 if self.use_graph:
                     if int(c) not in self._graphs:
                         me = weakref.proxy(self)
@@ -363,19 +403,25 @@ class FederatedGAN:
                 else:
                     ld, lg = self._local_steps(int(c))
                 res.samples += self.batch_size * self.local_steps
-                ld_sum += float(ld); lg_sum += float(lg)
+                ld_sum = ld_sum + ld.detach()
+                lg_sum = lg_sum + lg.detach()
                 self._swap_out(int(c))
                 acc.add_(self._flat(), alpha=float(self.n[c] / wsum))
             if self.ctx and self.world > 1:
                 self.ctx.all_reduce(acc)
             self._load_flat(acc)
+            self._finish_round(res, t0, ld_sum if len(mine) else None, lg_sum if len(mine) else None, len(mine))
+        return self._settle(res)
+
+    def _settle(self, res):
+        """Unsynchronised rounds: one device sync, the comm check and the loss reads, at the end."""
+        if any(torch.is_tensor(v) for v in res.loss_d + res.loss_g):
             if self.device.type == "cuda":
                 torch.cuda.synchronize()
-            res.wall_time.append(time.perf_counter() - t0)
-            res.loss_d.append(ld_sum / max(1, len(mine)))
-            res.loss_g.append(lg_sum / max(1, len(mine)))
-            res.rounds += 1
-            self.round_idx += 1
+            if self.ctx is not None:
+                self.ctx.check_comm()
+            res.loss_d = [float(v) for v in res.loss_d]
+            res.loss_g = [float(v) for v in res.loss_g]
         return res
 
     # --------------------------------------------------------------------------- checkpointing

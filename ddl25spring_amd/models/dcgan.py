@@ -4,11 +4,16 @@ The reference has no GAN (SURVEY M9 / BASELINE config "federated DCGAN"); this f
 standard DCGAN recipe at CIFAR-10 shape (32x32x3): transposed-conv generator with BN+ReLU and a
 tanh head, strided-conv discriminator with BN+LeakyReLU(0.2), N(0, 0.02) init, Adam(2e-4, 0.5).
 
-MI355X mapping: activations NHWC bf16; every conv / transposed conv is the implicit-GEMM MFMA
-kernel (a stride-2 transposed conv IS the phase-decomposed dgrad kernel), BN statistics come from
-the conv epilogue (discriminator) or one streaming pass (generator), BN+activation is one fused
-pass, BCE-with-logits is one kernel. RGB is carried as 32 channels whose extra weights are zero
-(they provably stay zero: their gradients are exactly zero), the 100-d latent as 128.
+MI355X mapping: activations NHWC; every conv / transposed conv is the implicit-GEMM MFMA kernel (a
+stride-2 transposed conv IS the phase-decomposed dgrad kernel), BN statistics come from the conv
+epilogue (discriminator) or one streaming pass (generator), BN+activation is one fused pass,
+BCE-with-logits is one kernel. RGB is carried as 32 channels whose extra weights are zero (they
+provably stay zero: their gradients are exactly zero), the 100-d latent as 128.
+
+Precision (``precision=``): "fp32" (default: the reference's generative lab trains in fp32,
+lab/tutorial_2a/generative-modeling.py:13-130) runs fp32 activations, weights and gradients on
+the fp32 kernels (conv_f32.hip X6 / exact-fp32 MFMA, bn_f32.hip, a deterministic fp32 BCE);
+"bf16" runs bf16 MFMA operands and activations with fp32 master weights.
 """
 from __future__ import annotations
 
@@ -20,6 +25,15 @@ from ..ops import autograd_ops as A
 
 def _pad32(c: int) -> int:
     return (c + 31) // 32 * 32
+
+
+PRECISIONS = ("fp32", "bf16")
+
+
+def _act_dtype(precision: str):
+    if precision not in PRECISIONS:
+        raise ValueError(f"DCGAN precision must be one of {PRECISIONS}, got {precision!r}")
+    return torch.float32 if precision == "fp32" else torch.bfloat16
 
 
 class _BN(nn.Module):
@@ -38,9 +52,10 @@ class _BN(nn.Module):
 class Generator(nn.Module):
     """z [N, nz] -> image NHWC [N, 32, 32, nc_pad] in [-1, 1] (channels >= nc are zero)."""
 
-    def __init__(self, nz: int = 100, ngf: int = 64, nc: int = 3):
+    def __init__(self, nz: int = 100, ngf: int = 64, nc: int = 3, precision: str = "fp32"):
         super().__init__()
         self.nz, self.nz_pad, self.nc, self.nc_pad, self.ngf = nz, _pad32(nz), nc, _pad32(nc), ngf
+        self.precision, self.act_dtype = precision, _act_dtype(precision)
         c0 = 4 * ngf
         # ConvTranspose2d(nz, 4ngf, 4, 1, 0) on a 1x1 input == a linear to [4, 4, 4ngf] (NHWC)
         w0 = torch.zeros(16 * c0, self.nz_pad)
@@ -60,7 +75,7 @@ class Generator(nn.Module):
         if z.shape[1] != self.nz_pad:
             z = torch.cat([z, z.new_zeros(N, self.nz_pad - z.shape[1])], 1)
         if z.is_cuda:
-            z = z.to(torch.bfloat16)  # bf16 device path (fp32 activations would select the fp32 linear)
+            z = z.to(self.act_dtype)  # the activation dtype selects the kernels' precision
         h = A.linear(z, self.proj).view(N, 4, 4, 4 * self.ngf)
         h = self.bn0(h, "relu")
         h = self.bn1(A.conv_transpose2d(h, self.up1, 2, 1), "relu")      # 8x8
@@ -75,9 +90,10 @@ class Generator(nn.Module):
 class Discriminator(nn.Module):
     """image NHWC [N, 32, 32, nc_pad] -> logits [N, 32] (column 0 is the real/fake logit)."""
 
-    def __init__(self, ndf: int = 64, nc: int = 3):
+    def __init__(self, ndf: int = 64, nc: int = 3, precision: str = "fp32"):
         super().__init__()
         self.nc, self.nc_pad, self.ndf = nc, _pad32(nc), ndf
+        self.precision, self.act_dtype = precision, _act_dtype(precision)
         w0 = torch.zeros(ndf, 4, 4, self.nc_pad)
         w0[..., :nc].normal_(0.0, 0.02)
         self.c0 = nn.Parameter(w0)
@@ -92,6 +108,8 @@ class Discriminator(nn.Module):
 
     def forward(self, x):
         N = x.shape[0]
+        if x.is_cuda:
+            x = x.to(self.act_dtype)
         h = A.activation(A.conv2d(x, self.c0, 2, 1), "leaky_relu")   # 16x16
         y, st = A.conv2d(h, self.c1, 2, 1, with_stats=True)            # 8x8
         h = self.bn1(y, "leaky_relu", st)
@@ -164,6 +182,7 @@ class GroupedGenerator(nn.Module):
     def __init__(self, gen: Generator, S: int):
         super().__init__()
         self.nz, self.nz_pad, self.nc, self.nc_pad, self.ngf = gen.nz, gen.nz_pad, gen.nc, gen.nc_pad, gen.ngf
+        self.precision, self.act_dtype = gen.precision, gen.act_dtype
         self.proj = nn.Parameter(_slots(gen.proj, S))
         self.bn0 = _GBN(gen.bn0, S)
         self.up1 = nn.Parameter(_slots(gen.up1, S))
@@ -177,6 +196,8 @@ class GroupedGenerator(nn.Module):
         G, N = z.shape[:2]
         if z.shape[2] != self.nz_pad:
             z = torch.cat([z, z.new_zeros(G, N, self.nz_pad - z.shape[2])], 2)
+        if z.is_cuda:
+            z = z.to(self.act_dtype)
         h = Gp.linear(z, self.proj).view(G, N, 4, 4, 4 * self.ngf)
         h = self.bn0(h, "relu")
         h = self.bn1(Gp.conv_transpose2d(h, self.up1, 2, 1), "relu")
@@ -190,6 +211,7 @@ class GroupedDiscriminator(nn.Module):
     def __init__(self, disc: Discriminator, S: int):
         super().__init__()
         self.nc, self.nc_pad, self.ndf = disc.nc, disc.nc_pad, disc.ndf
+        self.precision, self.act_dtype = disc.precision, disc.act_dtype
         self.c0 = nn.Parameter(_slots(disc.c0, S))
         self.c1 = nn.Parameter(_slots(disc.c1, S))
         self.bn1 = _GBN(disc.bn1, S)
@@ -200,6 +222,8 @@ class GroupedDiscriminator(nn.Module):
     def forward(self, x):
         from ..ops import grouped as Gp
         G, N = x.shape[:2]
+        if x.is_cuda:
+            x = x.to(self.act_dtype)
         h = A.activation(Gp.conv2d(x, self.c0, 2, 1), "leaky_relu")
         y, st = Gp.conv2d(h, self.c1, 2, 1, with_stats=True)
         h = self.bn1(y, "leaky_relu", st)
@@ -217,9 +241,9 @@ class GroupedGANTrainer:
                  betas=(0.5, 0.999)):
         from ..optim import SlotAdam
         self.G, self.D = gen, disc
-        cuda = gen.proj.is_cuda
-        self.optG = SlotAdam(gen.parameters(), S, lr=lr, betas=betas, bf16_shadow=cuda)
-        self.optD = SlotAdam(disc.parameters(), S, lr=lr, betas=betas, bf16_shadow=cuda)
+        shadow = gen.proj.is_cuda and gen.precision == "bf16"  # fp32 kernels read the fp32 rows
+        self.optG = SlotAdam(gen.parameters(), S, lr=lr, betas=betas, bf16_shadow=shadow)
+        self.optD = SlotAdam(disc.parameters(), S, lr=lr, betas=betas, bf16_shadow=shadow)
 
     def step(self, real, z):
         """real [G, N, 32, 32, nc_pad], z [G, N, nz] -> (sum of the clients' D losses, of G losses)."""

@@ -169,10 +169,17 @@ class Net:
         self._ws.begin(self.device)
         self.store.ensure_shadow()  # the fused-head path runs layer.forward itself
         try:
-            with self._cpu_storage():
+            with self._cpu_storage(), self._presplit(x):
                 return self._train_step(x, labels, ncls, scale, targets, with_correct)
         finally:
             self._ws.end()
+
+    def _presplit(self, x):
+        """fp32 on the GPU: every X6 weight image of the step in one launch at step start
+        (functional_f32.PresplitScope); the weights stay fixed until the step's own updates."""
+        if x.is_cuda and self.precision == "fp32":
+            return Fn.F32.presplit_scope(self)
+        return contextlib.nullcontext()
 
     def _train_step(self, x, labels, ncls, scale, targets, with_correct):
         head = self._fused_head(x, targets, ncls)

@@ -186,6 +186,10 @@ _SIGS.update({
     "ddl_convf32_wgrad_reduce": [vp, vp, i64, i32, i64, i32, i32, f32, vp],
     "ddl_x6h_workspace": [ctypes.POINTER(ConvF32Args), i32, i32],
     "ddl_x6_split_weights": [vp, vp, i32, i32, i32, i32, i32, i64, i64, i32, vp],
+    "ddl_x6_split_weights_multi": [vp, i32, i32, vp],
+    "ddl_bce_logits_f32": [vp, i32, vp, f32, i32, f32, vp, vp, vp],
+    "ddl_gan_inputs": [vp, i32, i32, i32, i32, vp, vp, vp],
+    "ddl_x6_split_desc_size": [],
     # bn_f32.hip
     "ddl_bnf_finalize": [ctypes.POINTER(BNFArgs), ctypes.POINTER(BNFArgs), vp],
     "ddl_bnf_apply": [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, vp],

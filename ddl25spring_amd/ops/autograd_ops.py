@@ -456,9 +456,20 @@ def cross_entropy_vocab(logits, targets, ignore_index=-100, scale: float = 1.0):
 # Activations are NHWC [N, H, W, C]; conv weights are fp32 parameters in the kernels' layout
 # [K, R, S, C] (conv) / [Cin, R, S, Cout] (transposed conv). Channel counts must be multiples of
 # 32 on the device (pad small ones, e.g. RGB 3 -> 32, with zero weights: they stay exactly zero).
+# Precision follows the activation dtype: fp32 device activations (the DCGAN's default, the
+# reference's precision) run the fp32 kernels (conv_f32.hip / bn_f32.hip / fp32 BCE) with the fp32
+# parameters themselves as operands; anything else runs bf16 on the bf16 weight shadow.
 def _geom(x_shape, C, K, R, S, stride, pad):
     N, H, W = x_shape[0], x_shape[1], x_shape[2]
     return Fn.ConvGeom(1, N, H, W, C, K, R, S, stride, pad)
+
+
+def _img_act(x):
+    return x if x.dtype in (torch.float32, torch.bfloat16) else x.to(torch.bfloat16)
+
+
+def _img_weight(w, dtype):
+    return w.detach().contiguous() if dtype == torch.float32 else _bf16_weight(w)
 
 
 class _Conv2d(torch.autograd.Function):
@@ -466,12 +477,13 @@ class _Conv2d(torch.autograd.Function):
     def forward(ctx, x, w, stride, pad, want_stats):
         Kc, R, S, C = w.shape
         g = _geom(x.shape, C, Kc, R, S, stride, pad)
-        wb = _bf16_weight(w).view(1, Kc, R, S, C)
-        stats = Fn.stats_buffer(1, Kc, x.device) if want_stats else None
-        y = Fn.conv_fwd(x.contiguous().view(1, *x.shape), wb, g, stats=stats)
+        wb = _img_weight(w, x.dtype).view(1, Kc, R, S, C)
+        x = x.contiguous()
+        stats = Fn.stats_buffer(1, Kc, x.device, like=x) if want_stats else None
+        y = Fn.conv_fwd(x.view(1, *x.shape), wb, g, stats=stats)
         ctx.save_for_backward(x, wb)
         ctx.g = g
-        if want_stats:
+        if want_stats and torch.is_tensor(stats):
             ctx.mark_non_differentiable(stats)
         return y.view(g.N, g.P, g.Q, Kc), stats
 
@@ -479,7 +491,7 @@ class _Conv2d(torch.autograd.Function):
     def backward(ctx, dy, _dstats):
         x, wb = ctx.saved_tensors
         g = ctx.g
-        dy5 = dy.to(torch.bfloat16).contiguous().view(1, g.N, g.P, g.Q, g.K)
+        dy5 = dy.to(x.dtype).contiguous().view(1, g.N, g.P, g.Q, g.K)
         dx = dw = None
         if ctx.needs_input_grad[1]:
             dw = torch.zeros(1, g.K, g.R, g.S, g.C, dtype=torch.float32, device=dy.device)
@@ -499,9 +511,7 @@ def conv2d(x, w, stride=1, pad=0, with_stats=False):
         y = F.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), stride=stride, padding=pad)
         y = y.permute(0, 2, 3, 1)
         return (y, None) if with_stats else y
-    if x.dtype != torch.bfloat16:
-        x = x.to(torch.bfloat16)
-    y, st = _Conv2d.apply(x, w, stride, pad, with_stats)
+    y, st = _Conv2d.apply(_img_act(x), w, stride, pad, with_stats)
     return (y, st) if with_stats else y
 
 
@@ -513,7 +523,7 @@ class _ConvT2d(torch.autograd.Function):
         Ho, Wo = (Hi - 1) * stride - 2 * pad + R, (Wi - 1) * stride - 2 * pad + S
         g = Fn.ConvGeom(1, N, Ho, Wo, Cout, Cin, R, S, stride, pad)  # the conv this one transposes
         assert (g.P, g.Q) == (Hi, Wi), "transposed conv geometry must invert exactly"
-        wb = _bf16_weight(w).view(1, Cin, R, S, Cout)
+        wb = _img_weight(w, x.dtype).view(1, Cin, R, S, Cout)
         y = Fn.conv_dgrad(x.contiguous().view(1, N, Hi, Wi, Cin), wb, g)
         ctx.save_for_backward(x, wb)
         ctx.g = g
@@ -523,7 +533,7 @@ class _ConvT2d(torch.autograd.Function):
     def backward(ctx, dy):
         x, wb = ctx.saved_tensors
         g = ctx.g
-        dy5 = dy.to(torch.bfloat16).contiguous().view(1, g.N, g.H, g.W, g.C)
+        dy5 = dy.to(x.dtype).contiguous().view(1, g.N, g.H, g.W, g.C)
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = Fn.conv_fwd(dy5, wb, g).view(x.shape)
@@ -540,9 +550,7 @@ def conv_transpose2d(x, w, stride=1, pad=0):
     if not x.is_cuda:
         y = F.conv_transpose2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), stride=stride, padding=pad)
         return y.permute(0, 2, 3, 1)
-    if x.dtype != torch.bfloat16:
-        x = x.to(torch.bfloat16)
-    return _ConvT2d.apply(x, w, stride, pad)
+    return _ConvT2d.apply(_img_act(x), w, stride, pad)
 
 
 _BN_ACT = {"none": 0, "relu": 1, "leaky_relu": 3}  # bn_apply codes (3 = leaky 0.2)
@@ -571,7 +579,7 @@ class _BatchNormAct(torch.autograd.Function):
     def backward(ctx, dy):
         xg, y, mean, rstd, ga = ctx.saved_tensors
         C = xg.shape[-1]
-        d = dy.to(torch.bfloat16).contiguous().view_as(xg)
+        d = dy.to(xg.dtype).contiguous().view_as(xg)
         ymask = None
         if ctx.act == "relu":
             ymask = y
@@ -592,9 +600,7 @@ def batch_norm_act(x, gamma, beta, running_mean=None, running_var=None, training
         y = F.batch_norm(x.reshape(-1, C), running_mean, running_var, gamma, beta, training,
                          momentum, eps).view(x.shape)
         return {"none": y, "relu": F.relu(y), "leaky_relu": F.leaky_relu(y, 0.2)}[act]
-    if x.dtype != torch.bfloat16:
-        x = x.to(torch.bfloat16)
-    return _BatchNormAct.apply(x, gamma, beta, running_mean, running_var, stats, training, momentum,
+    return _BatchNormAct.apply(_img_act(x), gamma, beta, running_mean, running_var, stats, training, momentum,
                                eps, act)
 
 
@@ -613,7 +619,7 @@ class _Act(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         (y,) = ctx.saved_tensors
-        return Fn.act_bwd(y, dy.to(torch.bfloat16).contiguous(), ctx.code, ctx.slope), None
+        return Fn.act_bwd(y, dy.to(y.dtype).contiguous(), ctx.code, ctx.slope), None
 
 
 def activation(x, kind):
@@ -621,9 +627,7 @@ def activation(x, kind):
     if not x.is_cuda:
         return {"relu": F.relu, "leaky_relu": lambda t: F.leaky_relu(t, 0.2),
                 "tanh": torch.tanh, "sigmoid": torch.sigmoid}[kind](x)
-    if x.dtype != torch.bfloat16:
-        x = x.to(torch.bfloat16)
-    return _Act.apply(x, kind)
+    return _Act.apply(_img_act(x), kind)
 
 
 class _BCE(torch.autograd.Function):
@@ -646,6 +650,4 @@ def bce_with_logits(logits, target):
     if not logits.is_cuda:
         t = target if torch.is_tensor(target) else torch.full((logits.shape[0],), float(target))
         return F.binary_cross_entropy_with_logits(logits[:, 0].float(), t.float())
-    if logits.dtype != torch.bfloat16:
-        logits = logits.to(torch.bfloat16)
-    return _BCE.apply(logits, target)
+    return _BCE.apply(_img_act(logits), target)

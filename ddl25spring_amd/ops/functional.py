@@ -1251,8 +1251,8 @@ def adam_step(p, g, m, v, shadow, lr, beta1, beta2, eps, wd, step, decoupled, gr
 
 
 def bce_logits(logits, target, scale=1.0, want_grad=True):
-    """Binary CE on column 0 of logits [R, ld] (bf16). target: float or fp32 [R] tensor.
-    -> (loss_sum fp32 [1], dlogits [R, ld] bf16 with (sigmoid(l)-t)*scale in column 0, or None)."""
+    """Binary CE on column 0 of logits [R, ld] (bf16 or fp32). target: float or fp32 [R] tensor.
+    -> (loss_sum fp32 [1], dlogits [R, ld] (logits' dtype) with (sigmoid(l)-t)*scale in column 0, or None)."""
     R, ld = logits.shape
     if not logits.is_cuda:
         t = target if torch.is_tensor(target) else torch.full((R,), float(target))
@@ -1262,6 +1262,14 @@ def bce_logits(logits, target, scale=1.0, want_grad=True):
             dl = torch.zeros_like(logits)
             dl[:, 0] = (d * scale).to(logits.dtype)
         return loss.reshape(1), dl
+    if logits.dtype == torch.float32:  # deterministic fp32 kernel (one workgroup, fixed-order sum)
+        assert logits.is_contiguous()
+        loss = torch.empty(1, dtype=torch.float32, device=logits.device)
+        dl = torch.zeros_like(logits) if want_grad else None
+        tt = target.float().contiguous() if torch.is_tensor(target) else None
+        check(_lib.kernels().ddl_bce_logits_f32(ptr(logits), ld, ptr(tt), 0.0 if tt is not None else float(target), R,
+                                                float(scale), ptr(loss), ptr(dl), stream()), "bce_logits_f32")
+        return loss, dl
     assert logits.is_contiguous() and logits.dtype == torch.bfloat16
     loss = torch.zeros(1, dtype=torch.float32, device=logits.device)
     dl = torch.zeros_like(logits) if want_grad else None
@@ -1270,6 +1278,26 @@ def bce_logits(logits, target, scale=1.0, want_grad=True):
     check(_lib.kernels().ddl_bce_logits(ptr(logits), ld, ptr(tt), tv, R, float(scale), ptr(loss), ptr(dl),
                                         stream()), "bce_logits")
     return loss, dl
+
+
+def gan_inputs(desc, steps: int, B: int, nz: int, idx_out, z_out):
+    """Federated-GAN round inputs (batch indices + generator noise) for G slots, each a pure
+    function of its client's seed: ``desc`` [(seed, n, off), ...] (host list) or a device int64
+    [G, 3] tensor; writes idx_out [steps, G*B] int64 and z_out [steps, G, B, nz] fp32 (nn_ops.hip
+    gan_inputs_kernel; on CPU tensors the numpy twin ``reference.gan_inputs``)."""
+    if not idx_out.is_cuda:
+        idx, z = ref.gan_inputs(desc, steps, B, nz)
+        idx_out.copy_(idx.view_as(idx_out))
+        z_out.copy_(z.view_as(z_out))
+        return idx_out, z_out
+    if not torch.is_tensor(desc):
+        desc = torch.tensor(desc, dtype=torch.int64).pin_memory().to(idx_out.device, non_blocking=True)
+    G = desc.shape[0]
+    assert idx_out.is_contiguous() and z_out.is_contiguous() and idx_out.dtype == torch.int64
+    assert idx_out.numel() == steps * G * B and z_out.numel() == steps * G * B * nz
+    check(_lib.kernels().ddl_gan_inputs(ptr(desc), G, steps, B, nz, ptr(idx_out), ptr(z_out), stream()),
+          "gan_inputs")
+    return idx_out, z_out
 
 
 # ------------------------------------------------------------------------------- aggregation

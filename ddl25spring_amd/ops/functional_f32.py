@@ -164,7 +164,29 @@ def halo_ok(mode: int, g, auto: bool = False) -> bool:
         SR = OH
     HP = (TR // SR) * (SR + g.R - 1) * (OW + g.S - 1)
     SC, Pd = (g.C, g.K) if mode == F_FWD else (g.K, g.C)
-    return HP <= HALO_HPMAX and SC % 16 == 0 and Pd % 4 == 0
+    if not (HP <= HALO_HPMAX and SC % 16 == 0 and Pd % 4 == 0):
+        return False
+    return _x6h_native_ok(mode, g)
+
+
+_X6H_OK: dict = {}
+
+
+def _x6h_native_ok(mode: int, g) -> bool:
+    """The kernel library's own geometry check (x6h_geo: halo layout search, LDS budget) where the
+    library is loadable; the Python mirror above only pre-filters, so plan() never picks a halo
+    launch that ddl_x6h would refuse."""
+    key = (mode, g)
+    r = _X6H_OK.get(key)
+    if r is None:
+        try:
+            lib = _lib.kernels()
+        except Exception:  # noqa: BLE001 - no library (CPU-only checkout): the mirror decides
+            return True
+        a = _args(g)
+        r = bool(lib.ddl_x6h_ok(ctypes.byref(a), mode, cfg_of(64, 128)))
+        _X6H_OK[key] = r
+    return r
 
 
 # A stride-1 1x1 conv is a GEMM over pixels: its image shape does not matter. FLAT1X1 re-shapes
@@ -326,14 +348,114 @@ def _launch(a, mode: int, geom, device, split_k: int = 0, ws_role: str = "main")
 
 def split_weights(a, mode: int, geom, device) -> torch.Tensor:
     """The X6 operand image of the launch's weights (6 bytes per element: three bf16 planes per 16
-    channels): FWD layout [G][K][R][S][C], DGRAD layout [G][C][R][S][K]. Rebuilt from the fp32
-    weights for every launch (the fused-SGD WGRAD updates them in place), into a stream-ordered
-    temporary."""
+    channels): FWD layout [G][K][R][S][C], DGRAD layout [G][C][R][S][K]. Inside an open
+    :class:`PresplitScope` (a training step) the image the scope built at step start; otherwise
+    rebuilt from the fp32 weights for this launch (the fused-SGD WGRAD updates them in place), into
+    a stream-ordered temporary."""
     T = geom.R * geom.S
+    layout = 0 if mode == F_FWD else 1
+    scope = _PRESPLIT[0]
+    if scope is not None:
+        key = (int(a.w), layout, geom.G, geom.K, T, geom.C, int(a.w_gs))
+        buf = scope.lookup(key)
+        if buf is not None:
+            return buf
     out = torch.empty(geom.G, geom.K * T * geom.C * 6, dtype=torch.uint8, device=device)
     check(_lib.kernels().ddl_x6_split_weights(a.w, out.data_ptr(), geom.G, geom.K, T, geom.C, 0 if mode == F_FWD else 1,
                                               a.w_gs, out.stride(0), 0, stream()), "x6_split_weights")
     return out
+
+
+class _SplitDesc(ctypes.Structure):  # conv_x6h.hip SplitDesc
+    _fields_ = [("w", ctypes.c_void_p), ("out", ctypes.c_void_p), ("w_gs", ctypes.c_longlong),
+                ("o_gs", ctypes.c_longlong), ("G", ctypes.c_int), ("K", ctypes.c_int), ("T", ctypes.c_int),
+                ("C", ctypes.c_int), ("layout", ctypes.c_int), ("blk0", ctypes.c_int), ("nblk", ctypes.c_int),
+                ("pad_", ctypes.c_int)]
+
+
+_PRESPLIT: list = [None]  # the open PresplitScope (one training step), or None
+PRESPLIT = [os.environ.get("DDL_F32_PRESPLIT", "1") != "0"]
+
+
+class PresplitScope:
+    """Every X6 weight image a training step needs, built by ONE launch at step start.
+
+    The halo kernels read the weights as pre-split bf16 piece images (``split_weights``); per conv
+    that was one small launch before each FWD and each DGRAD (23 per ResNet-18 step, ~5-14 us each
+    at one client per GPU, on the critical path). A step's weights do not change between its
+    forward and the DGRADs that read them (a direct-SGD WGRAD steps a layer's weights only after
+    that layer's DGRAD), so all images can be made up front. The first step through a scope
+    records the (weights, layout) pairs its halo launches ask for and splits them per launch as
+    before; from then on the scope owns one persistent image per pair, refreshed by
+    ``ddl_x6_split_weights_multi`` when the scope opens (a captured step replays that one launch).
+    A request the recording did not see falls back to the per-launch split. Use it only around
+    code whose weights stay fixed while it runs (``Net.train_step``), never around e.g. a GAN step
+    that updates D between two forwards."""
+
+    def __init__(self):
+        self.keys: list = []
+        self._seen: set = set()
+        self.bufs: dict = {}
+        self.desc = None
+        self.nblocks = 0
+        self.state = "record"  # -> "ready" once the images and the descriptor table exist
+        self._prev = None
+
+    def lookup(self, key):
+        if self.state == "ready":
+            return self.bufs.get(key)
+        if key not in self._seen:
+            self._seen.add(key)
+            self.keys.append(key)
+        return None
+
+    def __enter__(self):
+        self._prev = _PRESPLIT[0]
+        if not PRESPLIT[0]:
+            return self
+        if self.state == "ready":
+            check(_lib.kernels().ddl_x6_split_weights_multi(ptr(self.desc), len(self.keys), self.nblocks, stream()),
+                  "x6_split_weights_multi")
+        _PRESPLIT[0] = self
+        return self
+
+    def __exit__(self, *exc):
+        _PRESPLIT[0] = self._prev
+        if self.state == "record" and self.keys and not torch.cuda.is_current_stream_capturing() \
+                and exc[0] is None:
+            self._build()
+        return False
+
+    def _build(self):
+        lib = _lib.kernels()
+        if lib.ddl_x6_split_desc_size() != ctypes.sizeof(_SplitDesc):
+            raise RuntimeError("ABI mismatch for SplitDesc")
+        descs = (_SplitDesc * len(self.keys))()
+        dev = torch.device("cuda", torch.cuda.current_device())
+        blk = 0
+        for i, key in enumerate(self.keys):
+            w, layout, G, K, T, C, w_gs = key
+            buf = torch.empty(G, K * T * C * 6, dtype=torch.uint8, device=dev)
+            self.bufs[key] = buf
+            nblk = max(1, min(1024, -(-G * K * T * C // 16 // 256)))
+            d = descs[i]
+            d.w, d.out, d.w_gs, d.o_gs = w, buf.data_ptr(), w_gs, buf.stride(0)
+            d.G, d.K, d.T, d.C, d.layout, d.blk0, d.nblk = G, K, T, C, layout, blk, nblk
+            blk += nblk
+        self.nblocks = blk
+        raw = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8)
+        self.desc = raw.to(dev)
+        self.state = "ready"
+
+
+def presplit_scope(owner) -> "PresplitScope | contextlib.nullcontext":
+    """The owner's (a Net's) PresplitScope for one training step (a no-op context off the fp32
+    device path or with DDL_F32_PRESPLIT=0)."""
+    sc = getattr(owner, "_f32_presplit", None)
+    if sc is None:
+        sc = PresplitScope()
+        owner._f32_presplit = sc
+    return sc
 
 
 def _slots(a, mode: int, geom) -> int:

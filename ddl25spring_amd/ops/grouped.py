@@ -7,8 +7,13 @@ BN kernels are client-batched through their group dim); weight gradients accumul
 the slot rows of the parameter's gradient (``_ddl_fuse_grad``) or come back as a full [S, ...]
 gradient. On the CPU each op loops over the groups with plain PyTorch (the numerics reference).
 
+Precision follows the activations: fp32 inputs (the default, the reference's precision) run every
+op on the fp32 kernels (conv_f32.hip, bn_f32.hip, the deterministic fp32 BCE) with the fp32 slot
+rows of the parameters as operands; bf16 inputs run the bf16 MFMA kernels on the bf16 shadow rows.
+
 Used by the client-batched federated DCGAN (fl/gan.py; reference aggregation template
-lab/tutorial_1a/hfl_complete.py:336-390).
+lab/tutorial_1a/hfl_complete.py:336-390; the generative lab trains fp32,
+lab/tutorial_2a/generative-modeling.py:13-130).
 """
 from __future__ import annotations
 
@@ -33,15 +38,25 @@ def _full(p, G, rows):
     return out
 
 
-def _wb(w, G):
+def _wb(w, G, dtype=torch.bfloat16):
+    """The first G slot rows of a weight as the kernel operand: the fp32 master rows themselves
+    (strided rows of SlotAdam's buffer; the fp32 kernels take a group stride) or the bf16 shadow."""
+    if dtype == torch.float32:
+        return w.detach()[:G]
     sh = getattr(w, "_ddl_bf16", None)
     if sh is not None:
         return sh[:G]
     return Fn.to_bf16(w.detach()[:G].contiguous())
 
 
-def _bf(t):
-    return t.to(torch.bfloat16).contiguous()
+def _act(t, dtype=None):
+    """An activation in the op's precision: ``dtype`` if given, else its own (fp32 or bf16)."""
+    if dtype is None:
+        dtype = t.dtype if t.dtype in (torch.float32, torch.bfloat16) else torch.bfloat16
+    return t.to(dtype).contiguous()
+
+
+_bf = _act
 
 
 # ----------------------------------------------------------------------------------- conv
@@ -51,12 +66,12 @@ class _GConv2d(torch.autograd.Function):
         G, N, H, W, C = x.shape
         _, Kc, R, S, _ = w.shape
         g = Fn.ConvGeom(G, N, H, W, C, Kc, R, S, stride, pad)
-        wb = _wb(w, G)
-        stats = Fn.stats_buffer(G, Kc, x.device) if want_stats else None
+        wb = _wb(w, G, x.dtype)
+        stats = Fn.stats_buffer(G, Kc, x.device, like=x) if want_stats else None
         y = Fn.conv_fwd(x, wb, g, stats=stats)
         ctx.save_for_backward(x, wb)
         ctx.g, ctx.w = g, w
-        if want_stats:
+        if want_stats and torch.is_tensor(stats):
             ctx.mark_non_differentiable(stats)
         return y.view(G, N, g.P, g.Q, Kc), stats
 
@@ -64,7 +79,7 @@ class _GConv2d(torch.autograd.Function):
     def backward(ctx, dy, _dstats):
         x, wb = ctx.saved_tensors
         g = ctx.g
-        dy5 = _bf(dy).view(g.G, g.N, g.P, g.Q, g.K)
+        dy5 = _act(dy, x.dtype).view(g.G, g.N, g.P, g.Q, g.K)
         dx = dw = None
         if ctx.needs_input_grad[1]:
             sink = _sink(ctx.w, g.G)
@@ -85,7 +100,7 @@ def conv2d(x, w, stride=1, pad=0, with_stats=False):
               .permute(0, 2, 3, 1) for g in range(G)]
         y = torch.stack(ys)
         return (y, None) if with_stats else y
-    y, st = _GConv2d.apply(_bf(x), w, stride, pad, with_stats)
+    y, st = _GConv2d.apply(_act(x), w, stride, pad, with_stats)
     return (y, st) if with_stats else y
 
 
@@ -97,7 +112,7 @@ class _GConvT2d(torch.autograd.Function):
         Ho, Wo = (Hi - 1) * stride - 2 * pad + R, (Wi - 1) * stride - 2 * pad + S
         g = Fn.ConvGeom(G, N, Ho, Wo, Cout, Cin, R, S, stride, pad)  # the conv this one transposes
         assert (g.P, g.Q) == (Hi, Wi), "transposed conv geometry must invert exactly"
-        wb = _wb(w, G)
+        wb = _wb(w, G, x.dtype)
         y = Fn.conv_dgrad(x, wb, g)
         ctx.save_for_backward(x, wb)
         ctx.g, ctx.w = g, w
@@ -107,7 +122,7 @@ class _GConvT2d(torch.autograd.Function):
     def backward(ctx, dy):
         x, wb = ctx.saved_tensors
         g = ctx.g
-        dy5 = _bf(dy).view(g.G, g.N, g.H, g.W, g.C)
+        dy5 = _act(dy, x.dtype).view(g.G, g.N, g.H, g.W, g.C)
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = Fn.conv_fwd(dy5, wb, g).view(x.shape)
@@ -126,7 +141,7 @@ def conv_transpose2d(x, w, stride=1, pad=0):
     if not x.is_cuda:
         return torch.stack([F.conv_transpose2d(x[g].permute(0, 3, 1, 2), w[g].permute(0, 3, 1, 2), stride=stride,
                                                padding=pad).permute(0, 2, 3, 1) for g in range(G)])
-    return _GConvT2d.apply(_bf(x), w, stride, pad)
+    return _GConvT2d.apply(_act(x), w, stride, pad)
 
 
 # --------------------------------------------------------------------------------- linear
@@ -136,7 +151,7 @@ class _GLinear(torch.autograd.Function):
         G, N, C = x.shape
         Kout = w.shape[1]
         g = Fn.ConvGeom(G, N, 1, 1, C, Kout, 1, 1, 1, 0)
-        wb = _wb(w, G).view(G, Kout, 1, 1, C)
+        wb = _wb(w, G, x.dtype).view(G, Kout, 1, 1, C)
         y = Fn.conv_fwd(x.view(G, N, 1, 1, C), wb, g)
         ctx.save_for_backward(x, wb)
         ctx.g, ctx.w = g, w
@@ -146,7 +161,7 @@ class _GLinear(torch.autograd.Function):
     def backward(ctx, dy):
         x, wb = ctx.saved_tensors
         g = ctx.g
-        dy5 = _bf(dy).view(g.G, g.N, 1, 1, g.K)
+        dy5 = _act(dy, x.dtype).view(g.G, g.N, 1, 1, g.K)
         dx = dw = None
         if ctx.needs_input_grad[1]:
             sink = _sink(ctx.w, g.G)
@@ -167,7 +182,7 @@ def linear(x, w):
     G = x.shape[0]
     if not x.is_cuda:
         return torch.stack([x[g] @ w[g].t() for g in range(G)])
-    return _GLinear.apply(_bf(x), w)
+    return _GLinear.apply(_act(x), w)
 
 
 # ------------------------------------------------------------------------------ batchnorm
@@ -193,7 +208,7 @@ class _GBatchNormAct(torch.autograd.Function):
     def backward(ctx, dy):
         xg, y, mean, rstd, ga = ctx.saved_tensors
         G, C = xg.shape[0], xg.shape[-1]
-        d = _bf(dy).view_as(xg)
+        d = _act(dy, xg.dtype).view_as(xg)
         ymask = None
         if ctx.act == "relu":
             ymask = y
@@ -225,7 +240,7 @@ def batch_norm_act(x, gamma, beta, running_mean, running_var, training=True, mom
                              momentum, eps).view(x.shape[1:])
             ys.append({"none": y, "relu": F.relu(y), "leaky_relu": F.leaky_relu(y, 0.2)}[act])
         return torch.stack(ys)
-    return _GBatchNormAct.apply(_bf(x), gamma, beta, running_mean, running_var, stats, training, momentum, eps,
+    return _GBatchNormAct.apply(_act(x), gamma, beta, running_mean, running_var, stats, training, momentum, eps,
                                 act)
 
 
@@ -253,4 +268,4 @@ def bce_with_logits(logits, target):
         return sum(F.binary_cross_entropy_with_logits(logits[g, :, 0].float(),
                                                       torch.full((logits.shape[1],), float(target)))
                    for g in range(G))
-    return _GBCE.apply(_bf(logits), target)
+    return _GBCE.apply(_act(logits), target)

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import contextlib
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -383,3 +384,52 @@ def mse_kl(xr, x, mu, lv, kl_w=1.0):
     mse = ((xr - x) ** 2).sum()
     kl = -0.5 * (1 + lv - mu * mu - lv.exp()).sum()
     return mse + kl_w * kl
+
+
+# ------------------------------------------------------------------------- Philox (numpy twin)
+_M0, _M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+_W0, _W1 = np.uint32(0x9E3779B9), np.uint32(0xBB67AE85)
+
+
+def philox4x32(c0, c1, c2, c3, k0, k1):
+    """Philox-4x32-10 on uint32 arrays (csrc/include/ddl_common.h philox4x32)."""
+    c0, c1, c2, c3 = (np.asarray(v, dtype=np.uint32) for v in (c0, c1, c2, c3))
+    k0, k1 = np.uint32(k0), np.uint32(k1)
+    for _ in range(10):
+        p0 = _M0 * c0.astype(np.uint64)
+        p1 = _M1 * c2.astype(np.uint64)
+        hi0, lo0 = (p0 >> np.uint64(32)).astype(np.uint32), p0.astype(np.uint32)
+        hi1, lo1 = (p1 >> np.uint64(32)).astype(np.uint32), p1.astype(np.uint32)
+        c0, c1, c2, c3 = hi1 ^ c1 ^ k0, lo1, hi0 ^ c3 ^ k1, lo0
+        k0 = np.uint32((int(k0) + int(_W0)) & 0xFFFFFFFF)
+        k1 = np.uint32((int(k1) + int(_W1)) & 0xFFFFFFFF)
+    return c0, c1, c2, c3
+
+
+def _unit(x):  # (0, 1], u32_to_unit
+    return ((x >> np.uint32(8)).astype(np.float32) + np.float32(1.0)) * np.float32(1.0 / 16777216.0)
+
+
+def gan_inputs(desc, steps: int, B: int, nz: int):
+    """nn_ops.hip gan_inputs_kernel on the host: desc [(seed, n, off), ...] per slot ->
+    (idx int64 [steps, G*B], z fp32 [steps, G, B, nz])."""
+    G = len(desc)
+    idx = np.empty((steps, G * B), dtype=np.int64)
+    z = np.empty((steps, G, B, nz), dtype=np.float32)
+    for g, (seed, n, off) in enumerate(desc):
+        k0, k1 = int(seed) & 0xFFFFFFFF, (int(seed) >> 32) & 0xFFFFFFFF
+        e = np.arange(steps * B, dtype=np.uint64)
+        zeros = np.zeros_like(e, dtype=np.uint32)
+        r = philox4x32(e.astype(np.uint32), (e >> np.uint64(32)).astype(np.uint32), zeros + np.uint32(0x1d872b41),
+                       zeros, k0, k1)
+        u = (r[0].astype(np.uint64) * np.uint64(n)) >> np.uint64(32)
+        idx[:, g * B:(g + 1) * B] = (u.astype(np.int64) + int(off)).reshape(steps, B)
+        e = np.arange(steps * B * nz, dtype=np.uint64)
+        zeros = np.zeros_like(e, dtype=np.uint32)
+        r = philox4x32(e.astype(np.uint32), (e >> np.uint64(32)).astype(np.uint32), zeros + np.uint32(0x6a09e667),
+                       zeros, k0, k1)
+        u1 = np.maximum(_unit(r[0]), np.float32(1e-12))
+        u2 = _unit(r[1])
+        zz = np.sqrt(np.float32(-2.0) * np.log(u1)) * np.cos(np.float32(6.28318530717958648) * u2)
+        z[:, g] = zz.astype(np.float32).reshape(steps, B, nz)
+    return torch.from_numpy(idx), torch.from_numpy(z)

@@ -17,9 +17,10 @@ buffer, the IPC handles are exchanged over the process group, every rank maps ev
 bytes and reduces it in place (SUM). A barrier wait that exceeds ``timeout_s`` (a peer that never
 arrives) sets an error word instead of hanging the GPU; ``check()`` raises on it.
 
-The path is used by :class:`ddl25spring_amd.runtime.dist.DistContext` for messages up to
-``DDL_IPC_MAX_BYTES`` when ``DDL_IPC_ALLREDUCE=1`` (default off until it is measured against RCCL
-on a multi-GPU node, ``benchmarks/bench_comm.py``).
+The path is used by :class:`ddl25spring_amd.runtime.dist.DistContext` by default
+(``DDL_IPC_ALLREDUCE=auto``): at init every rank times it against RCCL at a ladder of sizes and the
+peer-read kernel keeps the messages below the measured crossover (``dist.probe_ipc_threshold``);
+``DDL_IPC_ALLREDUCE=1`` forces it up to ``DDL_IPC_MAX_BYTES``, ``0`` turns it off.
 """
 from __future__ import annotations
 
@@ -73,28 +74,54 @@ class IpcAllReduce:
         self.two_shot_bytes = two_shot_bytes
         self.nblocks = max(1, min(nblocks, self.lib.ddl_ipc_max_blocks()))
         self.timeout_ticks = int(timeout_s * 1e8)  # s_memrealtime: 100 MHz
+        # Setup is failure-agreeing: a rank whose allocation, export or peer mapping fails still
+        # takes part in every collective below, and all ranks agree (MAX of a failure flag) before
+        # anyone uses the buffers, so either every rank holds the peer-read path or none does
+        # (a one-sided failure would otherwise leave ranks on different all-reduce paths).
+        self._mine = None
+        self.bases: list[_vp] = []
+        self._opened: list[_vp] = []
+        err = None
         with torch.cuda.device(self.device):
-            mine = _vp()
-            check(self.lib.ddl_ipc_malloc(self.cap, ctypes.byref(mine)), "ipc_malloc")
-            self._mine = mine
             hsz = self.lib.ddl_ipc_handle_size()
-            buf = ctypes.create_string_buffer(64)
-            check(self.lib.ddl_ipc_get_handle(mine, buf), "ipc_get_handle")
-            handles = [None] * world
+            handle = None
+            try:
+                mine = _vp()
+                check(self.lib.ddl_ipc_malloc(self.cap, ctypes.byref(mine)), "ipc_malloc")
+                self._mine = mine
+                buf = ctypes.create_string_buffer(64)
+                check(self.lib.ddl_ipc_get_handle(mine, buf), "ipc_get_handle")
+                handle = buf.raw[:hsz]
+            except Exception as e:  # noqa: BLE001 - reported through the agreement below
+                err = e
+            handles = [handle] * world
             if world > 1:
-                dist.all_gather_object(handles, buf.raw[:hsz], group=group)
-            self.bases: list[_vp] = []
-            self._opened: list[_vp] = []
-            for r in range(world):
-                if r == rank:
-                    self.bases.append(mine)
-                    continue
-                p = _vp()
-                check(self.lib.ddl_ipc_open(ctypes.create_string_buffer(handles[r], 64), ctypes.byref(p)),
-                      f"ipc_open(rank {r})")
-                self.bases.append(p)
-                self._opened.append(p)
+                dist.all_gather_object(handles, handle, group=group)
+            if err is None and any(h is None for h in handles):
+                err = RuntimeError("a peer failed to export its IPC buffer")
+            if err is None:
+                try:
+                    for r in range(world):
+                        if r == rank:
+                            self.bases.append(self._mine)
+                            continue
+                        p = _vp()
+                        check(self.lib.ddl_ipc_open(ctypes.create_string_buffer(handles[r], 64), ctypes.byref(p)),
+                              f"ipc_open(rank {r})")
+                        self.bases.append(p)
+                        self._opened.append(p)
+                except Exception as e:  # noqa: BLE001
+                    err = e
             self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+            if world > 1:
+                fdev = "cpu" if dist.get_backend(group) == "gloo" else self.device
+                flag = torch.tensor([0 if err is None else 1], dtype=torch.int32, device=fdev)
+                dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+                if err is None and int(flag.item()):
+                    err = RuntimeError("a peer failed to map the IPC buffers")
+        if err is not None:
+            self._release()
+            raise RuntimeError(f"ipc all-reduce setup failed on some rank: {err}") from err
         if world > 1:
             dist.barrier(group=group)  # every peer has mapped every buffer before first use
         self.calls = 0
@@ -132,6 +159,9 @@ class IpcAllReduce:
         torch.cuda.synchronize(self.device)
         if self.world > 1 and dist.is_initialized():
             dist.barrier(group=group)
+        self._release()
+
+    def _release(self):
         for p in self._opened:
             self.lib.ddl_ipc_close(p)
         self._opened = []

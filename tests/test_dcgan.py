@@ -178,3 +178,71 @@ def test_batched_gan_engine_matches_sequential_gpu(cuda):
         flats.append(fg._flat().clone())
     upd = (flats[0] - w0).norm()
     assert ((flats[1] - flats[0]).norm() / upd).item() < 5e-2
+
+
+def _bce64(logits, t):
+    import torch.nn.functional as F
+    return sum(F.binary_cross_entropy_with_logits(logits[g, :, 0], torch.full_like(logits[g, :, 0], t))
+               for g in range(logits.shape[0]))
+
+
+@pytest.mark.gpu
+def test_grouped_dcgan_fp32_step_matches_float64(cuda):
+    """The reference-precision (fp32) client-batched DCGAN: one D step and one G step of G = 2
+    client slots (every layer one grouped launch on the fp32 kernels) against the same step in
+    float64 torch (the grouped ops' per-client CPU path): losses and every parameter gradient of
+    both networks <= 1e-4 relative."""
+    import copy
+    from ddl25spring_amd.models.dcgan import GroupedDiscriminator, GroupedGenerator
+    torch.manual_seed(0)
+    gen, disc = Generator(ngf=32, precision="fp32"), Discriminator(ndf=32, precision="fp32")
+    S = 2
+    gG, gD = GroupedGenerator(gen, S), GroupedDiscriminator(disc, S)
+    with torch.no_grad():  # distinct clients
+        for p in list(gG.parameters()) + list(gD.parameters()):
+            p[1].add_(0.01 * torch.randn_like(p[1]) * (p[1] != 0))
+    real = torch.zeros(S, 16, 32, 32, 32)
+    real[..., :3] = torch.rand(S, 16, 32, 32, 3) * 2 - 1
+    z = torch.randn(S, 16, 100)
+    mods = {"gpu": (copy.deepcopy(gG).to(cuda), copy.deepcopy(gD).to(cuda)),
+            "ref": (copy.deepcopy(gG).double(), copy.deepcopy(gD).double())}
+    out = {}
+    from ddl25spring_amd.ops import grouped as Gp
+    for name, (mg, md) in mods.items():
+        dev = cuda if name == "gpu" else "cpu"
+        dt = torch.float32 if name == "gpu" else torch.float64
+        r, zz = real.to(dev, dt), z.to(dev, dt)
+        bce = Gp.bce_with_logits if name == "gpu" else _bce64
+        fake = mg(zz)
+        lossD = bce(md(r), 1.0) + bce(md(fake.detach()), 0.0)
+        lossD.backward()
+        gd = [p.grad.detach().double().cpu().clone() for p in md.parameters()]
+        for p in md.parameters():
+            p.grad = None
+        lossG = bce(md(fake), 1.0)
+        lossG.backward()
+        gg = [p.grad.detach().double().cpu().clone() for p in mg.parameters()]
+        out[name] = (float(lossD), float(lossG), gd, gg)
+    a, b = out["gpu"], out["ref"]
+    assert abs(a[0] - b[0]) <= 1e-4 * abs(b[0]) and abs(a[1] - b[1]) <= 1e-4 * abs(b[1])
+    for ga, gb in zip(a[2] + a[3], b[2] + b[3]):
+        assert _rel(ga, gb) <= 1e-4, (_rel(ga, gb), tuple(gb.shape))
+
+
+@pytest.mark.gpu
+def test_batched_gan_fp32_unsynced_rounds_equal_synced(cuda):
+    """The fp32 client-batched federated GAN is deterministic: rounds enqueued without host syncs
+    (device-generated inputs, native weighted-sum aggregation, losses read once at the end) end in
+    bitwise the same global model and losses as host-synchronised rounds."""
+    from ddl25spring_amd.fl.gan import FederatedGAN
+    torch.manual_seed(0)
+    data = [to_nhwc_padded(torch.rand(64, 3, 32, 32) * 2 - 1).to(cuda) for _ in range(3)]
+    outs = []
+    for sync in (True, False):
+        fg = FederatedGAN(data, ngf=32, ndf=32, local_steps=2, batch_size=16, seed=1, device=cuda, batched=True)
+        assert fg.precision == "fp32" and fg.batched
+        fg.sync_rounds = sync
+        res = fg.run(3)
+        outs.append((fg._flat().clone(), res.loss_d, res.loss_g))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert outs[0][1] == outs[1][1] and outs[0][2] == outs[1][2]

@@ -23,6 +23,8 @@ GEOMS = [
     ConvGeom(G=1, N=11, H=4, W=4, C=512, K=192, R=3, S=3, stride=1, pad=1),   # 8 images (explicit plan)
     ConvGeom(G=2, N=3, H=32, W=32, C=32, K=64, R=1, S=1, stride=1, pad=0),    # 1x1 (the im2col stem)
     ConvGeom(G=1, N=2, H=8, W=8, C=48, K=36, R=3, S=3, stride=1, pad=1),      # odd channel counts
+    ConvGeom(G=1, N=2, H=64, W=64, C=32, K=32, R=3, S=3, stride=1, pad=1),    # 64 wide: 264-pixel halo
+    ConvGeom(G=2, N=3, H=8, W=4, C=64, K=64, R=3, S=3, stride=1, pad=1),      # 4 wide, 8 tall
 ]
 IDS = [f"{g.C}x{g.K}_{g.H}x{g.W}_{g.R}n{g.N}" for g in GEOMS]
 
@@ -302,3 +304,44 @@ def test_x6h_network_shapes_auto_plan(cuda, geom):
     d2, part2 = Fn.conv_dgrad(dy, w, geom, bn=(bx, mean, rstd), mask_bn=(sc2, sh2))
     keep = (bx.cpu().double() * b(sc2) + b(sh2)) > 0
     _close(d2, dxr * keep)
+
+
+def test_presplit_scope_matches_per_launch(cuda):
+    """PresplitScope (Net.train_step): the first pass records the halo launches' weight images,
+    later passes read the images ONE multi-tensor launch made at scope entry — bitwise the
+    per-launch split's results, refreshed when the weights change between steps."""
+    geoms = [ConvGeom(G=2, N=3, H=16, W=16, C=64, K=128, R=3, S=3, stride=1, pad=1),
+             ConvGeom(G=2, N=3, H=16, W=16, C=128, K=128, R=1, S=1, stride=1, pad=0)]
+    torch.manual_seed(7)
+    xs = [torch.randn(g.G, g.N, g.H, g.W, g.C, device=cuda) for g in geoms]
+    dys = [torch.randn(g.G, g.N, g.P, g.Q, g.K, device=cuda) for g in geoms]
+    ws = [_weights(g, cuda) for g in geoms]
+    for g in geoms:
+        _pin(F32.F_FWD, g, 1)
+        _pin(F32.F_DGRAD, g, 1)
+
+    def run():
+        return [t for g, x, dy, w in zip(geoms, xs, dys, ws)
+                for t in (Fn.conv_fwd(x, w, g), Fn.conv_dgrad(dy, w, g))]
+
+    try:
+        plain = run()
+        scope = F32.PresplitScope()
+        with scope:
+            rec = run()
+        assert scope.state == "ready" and len(scope.keys) == 4
+        with scope:
+            pre = run()
+        for a, b, c in zip(plain, rec, pre):
+            assert torch.equal(a, b) and torch.equal(a, c)
+        for w in ws:
+            w.mul_(1.01)
+        plain2 = run()
+        with scope:
+            pre2 = run()
+        for a, b in zip(plain2, pre2):
+            assert torch.equal(a, b)
+    finally:
+        for g in geoms:
+            F32.clear_plan(F32.F_FWD, g)
+            F32.clear_plan(F32.F_DGRAD, g)
