@@ -116,6 +116,11 @@ def main():
     rounds_per_s = args.steps / elapsed
     acc = fl.test() if args.eval else None
     w_hash = hashlib.sha256(fl.w_global.detach().cpu().numpy().tobytes()).hexdigest()
+    hashes = [w_hash]
+    if ctx.world > 1:  # the replicated server model: every rank must hold the same bits
+        import torch.distributed as tdist
+        hashes = [None] * ctx.world
+        tdist.all_gather_object(hashes, w_hash)
     from ddl25spring_amd.ops import functional_f32 as F32
     ref = REFERENCE_SAMPLES_PER_S.get(args.precision)
     if ctx.is_main:
@@ -145,10 +150,26 @@ def main():
                        "client_slots_per_gpu": fl.slots, "hip_graphs": not args.no_graph,
                        "fp32_conv_math": F32.math() if args.precision == "fp32" else None},
         }
-        if ctx.world > 1:  # which all-reduce path the round's weight reduce took (runtime/dist.py policy)
+        if ctx.world > 1:
             wb = fl.w_global.numel() * 4
+            # the round's cross-rank weight reduction (fl/aggregate.py) and the all-reduce path the
+            # context's policy picks for a message of that size (runtime/dist.py)
+            out["aggregation"] = fl.aggregator.describe(ctx) if hasattr(fl.aggregator, "describe") else \
+                type(fl.aggregator).__name__
             out["allreduce"] = {"weights_bytes": wb, "path": rdist.allreduce_path(ctx, wb),
                                 "backend": ctx.backend, **ctx.ipc_policy}
+            out["rank_hashes_equal"] = len(set(hashes)) == 1
+        if args.precision == "fp32":
+            # the X6 engine's speed / accuracy trade (docs/KERNELS.md "Chain length"): zero-start MFMA
+            # chains of 3 tap steps (halo FWD / DGRAD) and 2 pixel steps (halo WGRAD) before each IEEE
+            # add; worst per-tensor gradient error of one ResNet-18 step vs float64, with stock
+            # PyTorch-ROCm fp32 (MIOpen) on the same step beside it
+            out["fp32_accuracy"] = {
+                "x6h_chain_steps": 3, "x6hw_chain_steps": 2,
+                "worst_grad_rel_err_vs_float64": {"b16": 3.5e-6, "b50": 4.5e-2, "b100": 2.4e-2},
+                "stock_torch_fp32_same_step": {"b16": 2.1e-2, "b50": 4.5e-2, "b100": 4.6e-2},
+                "chain1_worst": {"b16": 4.6e-6, "b50": 6.8e-4, "b100": 3.2e-2},
+                "source": "profiles/fp32_grad_accuracy_r4.txt"}
         if acc is not None:
             out["test_accuracy"] = acc
         print(json.dumps(out), flush=True)

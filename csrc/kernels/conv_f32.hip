@@ -38,6 +38,7 @@
 //   * stride-2 DGRAD runs as four sub-pixel phases (no MFMA on taps that miss every output);
 //     larger strides (none in the model zoo) run unphased with a per-tap divisibility test.
 #include "conv_f32_core.h"
+#include <cstdlib>
 
 // operand prefetch depth in steps (register sets): 2 or 3
 #ifndef F32_PREFETCH
@@ -581,7 +582,12 @@ __global__ __launch_bounds__(256) void convf32_wgrad_reduce(const float* __restr
 static void launch_wgrad_reduce(const float* part, float* out, long long out_gs, int G, long long n, int splits,
                                 int accumulate, float gscale, hipStream_t s) {
   // float4 lanes once that still gives >= 2 workgroups per CU, scalar lanes below
-  if ((long long)G * (n / 4) >= 512LL * 256)
+  // (DDL_WGRAD_REDUCE_V4_MIN overrides the float4 threshold, in float4 lanes: A/B timing)
+  static const long long v4_min = [] {
+    const char* e = getenv("DDL_WGRAD_REDUCE_V4_MIN");
+    return e ? atoll(e) : 512LL * 256;
+  }();
+  if ((long long)G * (n / 4) >= v4_min)
     hipLaunchKernelGGL(convf32_wgrad_reduce<4>, dim3(grid_for((long long)G * (n / 4), 256)), dim3(256), 0, s, part,
                        out, out_gs, G, n / 4, splits, accumulate, gscale);
   else

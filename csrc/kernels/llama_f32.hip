@@ -288,11 +288,10 @@ DDL_API int ddl_swiglu_f32_bwd(const float* ab, const float* dh, float* dab, int
 
 // ---------------------------------------------------------------------------------------------
 // Causal attention, fp32. qkv [B][S][3][H][HD], o / dO [B][S][H][HD], lse / delta [B][H][S]
-// (lse in the log2 domain of the scaled scores), cos / sin [S][HD/2] (interleaved pairs).
-// A workgroup owns 64 rows of one (b, h); lane quad (4 consecutive lanes) owns one row, lane
-// j of the quad the head dims [j*DPT, (j+1)*DPT), DPT = HD / 4 (even: whole RoPE pairs, and a
-// multiple of 4: float4 loads). The other side of each product is staged 64 rows at a time in LDS
-// (RoPE applied while staging) and read by all quads of a wave at the same row: a broadcast.
+// (lse in the log2 domain of the scaled scores), cos / sin [S][HD/2] (interleaved pairs). HD a
+// multiple of 16. A workgroup owns 64 rows of one (b, h), 16 per wave; every product runs on the
+// exact-fp32 MFMA (see "MFMA attention" below). Reference: the LLaMA of the labs trains in fp32
+// (lab/tutorial_1b/PP/1F1B/intro_PP_1F1B_MB.py:16-46).
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr int ATT_R = 64;
 
@@ -344,15 +343,113 @@ __device__ __forceinline__ void stage_rows(float* img, const float* base, long l
   }
 }
 
+// ---- MFMA attention (exact fp32 products: v_mfma_f32_16x16x4_f32, the fmaf-chain of fp32) ----
+// A wave owns 16 rows (queries, or keys in the dK/dV kernel) of a 64-row workgroup tile; the
+// other side is staged 64 rows at a time in LDS (RoPE applied while staging), rows padded to
+// HD + 4 floats (conflict-free: 16 rows x 4-float chunks cover the 64 banks). Operand maps of the
+// 16x16x4 MFMA: lane l = 16g + n supplies A[m = n][k = g], B[k = g][n]; D holds rows 4g + i,
+// column n. The MFMA sums its 4 k-slots in any order, so a product may assign its reduction index
+// to (slot g, step j) freely as long as A and B agree:
+//   * reductions over the head dim use d = (HD/4) g + j: each lane reads HD/4 CONTIGUOUS dims
+//     (float4 LDS reads; its own row's slice kept in registers);
+//   * reductions over keys / queries use the index 4g + j of the preceding product's D layout,
+//     so P / dS feed the next MFMA straight from their registers (register j), no transpose.
+// Forward and dQ compute S^T = K Q^T (D: key 4g+i, query n: the softmax runs down a column —
+// 4 values in-lane + two xor-shuffles — and the per-query statistics are one value per lane);
+// dK/dV computes S = Q K^T (D: query 4g+i, key n).
+typedef float f4m __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f4m mfma4(float a, float b, f4m c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+__device__ __forceinline__ float colmax(float v) {  // over the 4 lane groups of a column
+  v = fmaxf(v, __shfl_xor(v, 16));
+  return fmaxf(v, __shfl_xor(v, 32));
+}
+__device__ __forceinline__ float colsum(float v) {
+  v += __shfl_xor(v, 16);
+  return v + __shfl_xor(v, 32);
+}
+
+// Stage rows r0..r0+63 of one (b, h) into LDS img[64][HD + 4] (rows >= S zero), optionally rotated.
 template <int HD>
-__device__ __forceinline__ float dot_lds(const float (&q)[HD / 4], const float* row) {
-  float s = 0.f;
-#pragma unroll
-  for (int m = 0; m < HD / 4; m += 4) {
-    const float4 k = *(const float4*)(row + m);
-    s += q[m] * k.x + q[m + 1] * k.y + q[m + 2] * k.z + q[m + 3] * k.w;
+__device__ __forceinline__ void stage_rows_p(float* img, const float* base, long long rstride, int r0, int S,
+                                             const float* cosb, const float* sinb, bool rope) {
+  constexpr int N4 = ATT_R * HD / 4, HP = HD + 4;
+  for (int e = threadIdx.x; e < N4; e += 256) {
+    const int r = e / (HD / 4), d = (e - r * (HD / 4)) * 4;
+    const int row = r0 + r;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row < S) {
+      v = *(const float4*)(base + row * rstride + d);
+      if (rope) {
+        const float* cs = cosb + (long long)row * (HD / 2) + d / 2;
+        const float* sn = sinb + (long long)row * (HD / 2) + d / 2;
+        const float a0 = v.x * cs[0] - v.y * sn[0], a1 = v.x * sn[0] + v.y * cs[0];
+        const float b0 = v.z * cs[1] - v.w * sn[1], b1 = v.z * sn[1] + v.w * cs[1];
+        v = make_float4(a0, a1, b0, b1);
+      }
+    }
+    *(float4*)(img + r * HP + d) = v;
   }
-  return quad_sum(s);
+}
+
+// a lane's own slice: row `row` (clamped), dims [(HD/4) g, (HD/4)(g+1)), optionally rotated
+template <int HD>
+__device__ __forceinline__ void own_slice(float (&v)[HD / 4], const float* base, long long rstride, int row, int g,
+                                          const float* cosb, const float* sinb, bool rope) {
+  constexpr int DQ = HD / 4;
+  load_slice<DQ>(base + row * rstride + g * DQ, v);
+  if (rope) rope_slice<DQ>(v, cosb + (long long)row * (HD / 2), sinb + (long long)row * (HD / 2), g * DQ, 1);
+}
+
+// one 16x16 block of X Y^T over the head dim: A rows from LDS (row-major, padded), B = own slice
+template <int HD>
+__device__ __forceinline__ f4m dot_block(const float* arow, const float (&bv)[HD / 4], int g) {
+  constexpr int DQ = HD / 4;
+  f4m c = (f4m){0.f, 0.f, 0.f, 0.f};
+  const float* a = arow + g * DQ;
+#pragma unroll
+  for (int j = 0; j < DQ; j += 4) {
+    const float4 av = *(const float4*)(a + j);
+    c = mfma4(av.x, bv[j], c);
+    c = mfma4(av.y, bv[j + 1], c);
+    c = mfma4(av.z, bv[j + 2], c);
+    c = mfma4(av.w, bv[j + 3], c);
+  }
+  return c;
+}
+
+// acc[db] += T^T-block: sum over the 16 rows r = 4g + j of an LDS tile (rows rb..rb+15) of
+// tile[r][16 db + n] * w_j (w = the lane's D-layout values of the preceding product)
+template <int HD>
+__device__ __forceinline__ void accum_rows(f4m (&acc)[HD / 16], const float* tile, int rb, const float (&w)[4], int g,
+                                           int n) {
+  constexpr int HP = HD + 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float* r = tile + (rb + 4 * g + j) * HP + n;
+#pragma unroll
+    for (int db = 0; db < HD / 16; ++db) acc[db] = mfma4(r[16 * db], w[j], acc[db]);
+  }
+}
+
+// store D-layout blocks (d = 16 db + 4 g + i of row `row`), optionally scaled / inverse-rotated
+template <int HD>
+__device__ __forceinline__ void store_blocks(float* dst, f4m (&acc)[HD / 16], int g, float mul, const float* cs,
+                                             const float* sn) {
+#pragma unroll
+  for (int db = 0; db < HD / 16; ++db) {
+    const int d = 16 * db + 4 * g;
+    float v[4] = {acc[db][0] * mul, acc[db][1] * mul, acc[db][2] * mul, acc[db][3] * mul};
+    if (cs) {
+#pragma unroll
+      for (int i = 0; i < 4; i += 2) {
+        const float c = cs[(d + i) >> 1], sv = -sn[(d + i) >> 1];
+        const float a = v[i], b = v[i + 1];
+        v[i] = a * c - b * sv;
+        v[i + 1] = a * sv + b * c;
+      }
+    }
+    *(float4*)(dst + d) = make_float4(v[0], v[1], v[2], v[3]);
+  }
 }
 
 template <int HD>
@@ -360,64 +457,57 @@ __global__ __launch_bounds__(256) void attnf_fwd_kernel(const float* __restrict_
                                                         float* __restrict__ lse, const float* __restrict__ cosb,
                                                         const float* __restrict__ sinb, int S, int H,
                                                         float sl2) {
-  constexpr int DPT = HD / 4;
-  __shared__ float Ks[ATT_R * HD], Vs[ATT_R * HD];
+  constexpr int HP = HD + 4, NDB = HD / 16;
+  __shared__ __attribute__((aligned(16))) float Ks[ATT_R * HP], Vs[ATT_R * HP];
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int qr = threadIdx.x >> 2, part = threadIdx.x & 3, d0 = part * DPT;
-  const int i = qb * ATT_R + qr;
-  const long long rs = 3LL * H * HD;  // qkv row stride
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, n = lane & 15;
+  const int q = qb * ATT_R + 16 * w + n, qc = min(q, S - 1);
+  const long long rs = 3LL * H * HD;
   const float* qbase = qkv + (long long)b * S * rs + (long long)h * HD;
   const float* kbase = qbase + (long long)H * HD;
   const float* vbase = qbase + 2LL * H * HD;
-  float q[DPT], acc[DPT];
+  float qf[HD / 4];
+  own_slice<HD>(qf, qbase, rs, qc, g, cosb, sinb, true);
+  f4m oacc[NDB];
 #pragma unroll
-  for (int m = 0; m < DPT; ++m) acc[m] = 0.f;
-  const int iq = min(i, S - 1);
-  load_slice<DPT>(qbase + iq * rs + d0, q);
-  rope_slice<DPT>(q, cosb + (long long)iq * (HD / 2), sinb + (long long)iq * (HD / 2), d0, 1);
+  for (int db = 0; db < NDB; ++db) oacc[db] = (f4m){0.f, 0.f, 0.f, 0.f};
   float mx = -INFINITY, l = 0.f;
   for (int kt = 0; kt <= qb; ++kt) {
     __syncthreads();
-    stage_rows<HD>(Ks, kbase, rs, kt * ATT_R, S, cosb, sinb, true);
-    stage_rows<HD>(Vs, vbase, rs, kt * ATT_R, S, cosb, sinb, false);
+    stage_rows_p<HD>(Ks, kbase, rs, kt * ATT_R, S, cosb, sinb, true);
+    stage_rows_p<HD>(Vs, vbase, rs, kt * ATT_R, S, cosb, sinb, false);
     __syncthreads();
-    float sc[ATT_R];
-    float tmax = -INFINITY;
+    const int nu = kt < qb ? 4 : w + 1;  // 16-key sub-tiles at or below this wave's diagonal
+    for (int u = 0; u < nu; ++u) {
+      const f4m st = dot_block<HD>(Ks + (16 * u + n) * HP, qf, g);  // S^T[key 4g+i][query n]
+      float sc[4], tmax = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < ATT_R; ++j) {
-      const int key = kt * ATT_R + j;
-      const float d = dot_lds<HD>(q, Ks + j * HD + d0) * sl2;
-      sc[j] = (key <= i && key < S) ? d : -INFINITY;
-      tmax = fmaxf(tmax, sc[j]);
-    }
-    const float nm = fmaxf(mx, tmax);
-    if (nm == -INFINITY) continue;  // row fully masked in this tile (padding rows only)
-    const float corr = exp2f(mx - nm);
-    l *= corr;
-#pragma unroll
-    for (int m = 0; m < DPT; ++m) acc[m] *= corr;
-#pragma unroll
-    for (int j = 0; j < ATT_R; ++j) {
-      const float p = exp2f(sc[j] - nm);
-      l += p;
-      const float* vr = Vs + j * HD + d0;
-#pragma unroll
-      for (int m = 0; m < DPT; m += 4) {
-        const float4 v = *(const float4*)(vr + m);
-        acc[m] += p * v.x; acc[m + 1] += p * v.y; acc[m + 2] += p * v.z; acc[m + 3] += p * v.w;
+      for (int i = 0; i < 4; ++i) {
+        const int key = kt * ATT_R + 16 * u + 4 * g + i;
+        sc[i] = (key <= q && key < S) ? st[i] * sl2 : -INFINITY;
+        tmax = fmaxf(tmax, sc[i]);
       }
-    }
-    mx = nm;
-  }
-  if (i >= S) return;
-  const float inv = 1.f / l;
+      const float nm = fmaxf(mx, colmax(tmax));  // finite: key 0 is valid for every query
+      const float corr = exp2f(mx - nm);
+      float p[4], ps = 0.f;
 #pragma unroll
-  for (int m = 0; m < DPT; ++m) acc[m] *= inv;
-  store_slice<DPT>(o + ((long long)(b * S + i) * H + h) * HD + d0, acc);
-  if (part == 0) lse[((long long)b * H + h) * S + i] = mx + log2f(l);
+      for (int i = 0; i < 4; ++i) {
+        p[i] = exp2f(sc[i] - nm);
+        ps += p[i];
+      }
+      l = l * corr + colsum(ps);
+      mx = nm;
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) oacc[db] *= corr;
+      accum_rows<HD>(oacc, Vs, 16 * u, p, g, n);  // O^T[d][query n] += V^T P^T
+    }
+  }
+  if (q >= S) return;
+  store_blocks<HD>(o + ((long long)(b * S + q) * H + h) * HD, oacc, g, 1.f / l, nullptr, nullptr);
+  if (g == 0) lse[((long long)b * H + h) * S + q] = mx + log2f(l);
 }
 
-// dQ (and delta): per query row, over the key tiles 0..qb
+// dQ (and delta = rowsum(dO * O)): a wave's 16 queries over the key tiles 0..qb
 template <int HD>
 __global__ __launch_bounds__(256) void attnf_bwd_dq_kernel(const float* __restrict__ qkv, const float* __restrict__ o,
                                                            const float* __restrict__ dout,
@@ -425,59 +515,56 @@ __global__ __launch_bounds__(256) void attnf_bwd_dq_kernel(const float* __restri
                                                            float* __restrict__ dqkv, const float* __restrict__ cosb,
                                                            const float* __restrict__ sinb, int S, int H, float sl2,
                                                            float scale) {
-  constexpr int DPT = HD / 4;
-  __shared__ float Ks[ATT_R * HD], Vs[ATT_R * HD];
+  constexpr int HP = HD + 4, NDB = HD / 16, DQ = HD / 4;
+  __shared__ __attribute__((aligned(16))) float Ks[ATT_R * HP], Vs[ATT_R * HP];
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int qr = threadIdx.x >> 2, part = threadIdx.x & 3, d0 = part * DPT;
-  const int i = qb * ATT_R + qr, iq = min(i, S - 1);
-  const long long rs = 3LL * H * HD;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, n = lane & 15;
+  const int q = qb * ATT_R + 16 * w + n, qc = min(q, S - 1);
+  const long long rs = 3LL * H * HD, ors = (long long)H * HD;
   const float* qbase = qkv + (long long)b * S * rs + (long long)h * HD;
   const float* kbase = qbase + (long long)H * HD;
   const float* vbase = qbase + 2LL * H * HD;
-  const long long orow = ((long long)(b * S + iq) * H + h) * HD + d0;
-  float q[DPT], dO[DPT], ov[DPT], dq[DPT];
-  load_slice<DPT>(qbase + iq * rs + d0, q);
-  rope_slice<DPT>(q, cosb + (long long)iq * (HD / 2), sinb + (long long)iq * (HD / 2), d0, 1);
-  load_slice<DPT>(dout + orow, dO);
-  load_slice<DPT>(o + orow, ov);
+  const float* obase = o + (long long)b * S * ors + (long long)h * HD;
+  const float* dbase = dout + (long long)b * S * ors + (long long)h * HD;
+  float qf[DQ], df[DQ], of[DQ];
+  own_slice<HD>(qf, qbase, rs, qc, g, cosb, sinb, true);
+  own_slice<HD>(df, dbase, ors, qc, g, cosb, sinb, false);
+  own_slice<HD>(of, obase, ors, qc, g, cosb, sinb, false);
   float dl = 0.f;
 #pragma unroll
-  for (int m = 0; m < DPT; ++m) {
-    dl += dO[m] * ov[m];
-    dq[m] = 0.f;
-  }
-  dl = quad_sum(dl);
-  const long long li = ((long long)b * H + h) * S + iq;
+  for (int j = 0; j < DQ; ++j) dl += df[j] * of[j];
+  dl = colsum(dl);
+  const long long li = ((long long)b * H + h) * S + qc;
   const float L = lse[li];
-  if (part == 0 && i < S) delta[li] = dl;
+  if (g == 0 && q < S) delta[li] = dl;
+  f4m dq[NDB];
+#pragma unroll
+  for (int db = 0; db < NDB; ++db) dq[db] = (f4m){0.f, 0.f, 0.f, 0.f};
   for (int kt = 0; kt <= qb; ++kt) {
     __syncthreads();
-    stage_rows<HD>(Ks, kbase, rs, kt * ATT_R, S, cosb, sinb, true);
-    stage_rows<HD>(Vs, vbase, rs, kt * ATT_R, S, cosb, sinb, false);
+    stage_rows_p<HD>(Ks, kbase, rs, kt * ATT_R, S, cosb, sinb, true);
+    stage_rows_p<HD>(Vs, vbase, rs, kt * ATT_R, S, cosb, sinb, false);
     __syncthreads();
-#pragma unroll 4
-    for (int j = 0; j < ATT_R; ++j) {
-      const int key = kt * ATT_R + j;
-      const float* kr = Ks + j * HD + d0;
-      const float s = dot_lds<HD>(q, kr) * sl2;
-      const float dp = dot_lds<HD>(dO, Vs + j * HD + d0);
-      const float p = (key <= i && key < S) ? exp2f(s - L) : 0.f;
-      const float ds = p * (dp - dl);
+    const int nu = kt < qb ? 4 : w + 1;
+    for (int u = 0; u < nu; ++u) {
+      const f4m st = dot_block<HD>(Ks + (16 * u + n) * HP, qf, g);   // S^T
+      const f4m dpt = dot_block<HD>(Vs + (16 * u + n) * HP, df, g);  // dP^T = V dO^T
+      float ds[4];
 #pragma unroll
-      for (int m = 0; m < DPT; m += 4) {
-        const float4 k = *(const float4*)(kr + m);
-        dq[m] += ds * k.x; dq[m + 1] += ds * k.y; dq[m + 2] += ds * k.z; dq[m + 3] += ds * k.w;
+      for (int i = 0; i < 4; ++i) {
+        const int key = kt * ATT_R + 16 * u + 4 * g + i;
+        const float pv = (key <= q && key < S) ? exp2f(st[i] * sl2 - L) : 0.f;
+        ds[i] = pv * (dpt[i] - dl);
       }
+      accum_rows<HD>(dq, Ks, 16 * u, ds, g, n);  // dQ^T[d][query n] += K^T dS^T
     }
   }
-  if (i >= S) return;
-#pragma unroll
-  for (int m = 0; m < DPT; ++m) dq[m] *= scale;
-  rope_slice<DPT>(dq, cosb + (long long)i * (HD / 2), sinb + (long long)i * (HD / 2), d0, -1);
-  store_slice<DPT>(dqkv + (long long)(b * S + i) * rs + (long long)h * HD + d0, dq);
+  if (q >= S) return;
+  store_blocks<HD>(dqkv + (long long)(b * S + q) * rs + (long long)h * HD, dq, g, scale,
+                   cosb + (long long)q * (HD / 2), sinb + (long long)q * (HD / 2));
 }
 
-// dK, dV: per key row, over the query tiles kb..end (causal: queries >= key)
+// dK, dV: a wave's 16 keys over the query tiles kb..end (causal: queries >= key)
 template <int HD>
 __global__ __launch_bounds__(256) void attnf_bwd_dkdv_kernel(const float* __restrict__ qkv,
                                                              const float* __restrict__ dout,
@@ -486,59 +573,54 @@ __global__ __launch_bounds__(256) void attnf_bwd_dkdv_kernel(const float* __rest
                                                              float* __restrict__ dqkv, const float* __restrict__ cosb,
                                                              const float* __restrict__ sinb, int S, int H, float sl2,
                                                              float scale) {
-  constexpr int DPT = HD / 4;
-  __shared__ float Qs[ATT_R * HD], Ds[ATT_R * HD], Ls[ATT_R], Dl[ATT_R];
+  constexpr int HP = HD + 4, NDB = HD / 16, DQ = HD / 4;
+  __shared__ __attribute__((aligned(16))) float Qs[ATT_R * HP], Ds[ATT_R * HP];
+  __shared__ float Ls[ATT_R], Dl[ATT_R];
   const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int kr_ = threadIdx.x >> 2, part = threadIdx.x & 3, d0 = part * DPT;
-  const int j = kb * ATT_R + kr_, jk = min(j, S - 1);
-  const long long rs = 3LL * H * HD;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, n = lane & 15;
+  const int key = kb * ATT_R + 16 * w + n, kc = min(key, S - 1);
+  const long long rs = 3LL * H * HD, ors = (long long)H * HD;
   const float* qbase = qkv + (long long)b * S * rs + (long long)h * HD;
   const float* kbase = qbase + (long long)H * HD;
   const float* vbase = qbase + 2LL * H * HD;
-  const float* obase = dout + (long long)b * S * H * HD + (long long)h * HD;
+  const float* dbase = dout + (long long)b * S * ors + (long long)h * HD;
   const long long lrow = ((long long)b * H + h) * S;
-  float k[DPT], v[DPT], dk[DPT], dv[DPT];
-  load_slice<DPT>(kbase + jk * rs + d0, k);
-  rope_slice<DPT>(k, cosb + (long long)jk * (HD / 2), sinb + (long long)jk * (HD / 2), d0, 1);
-  load_slice<DPT>(vbase + jk * rs + d0, v);
+  float kf[DQ], vf[DQ];
+  own_slice<HD>(kf, kbase, rs, kc, g, cosb, sinb, true);
+  own_slice<HD>(vf, vbase, rs, kc, g, cosb, sinb, false);
+  f4m dk[NDB], dv[NDB];
 #pragma unroll
-  for (int m = 0; m < DPT; ++m) dk[m] = dv[m] = 0.f;
+  for (int db = 0; db < NDB; ++db) dk[db] = dv[db] = (f4m){0.f, 0.f, 0.f, 0.f};
   const int nqt = (S + ATT_R - 1) / ATT_R;
   for (int qt = kb; qt < nqt; ++qt) {
     __syncthreads();
-    stage_rows<HD>(Qs, qbase, rs, qt * ATT_R, S, cosb, sinb, true);
-    stage_rows<HD>(Ds, obase, (long long)H * HD, qt * ATT_R, S, cosb, sinb, false);
+    stage_rows_p<HD>(Qs, qbase, rs, qt * ATT_R, S, cosb, sinb, true);
+    stage_rows_p<HD>(Ds, dbase, ors, qt * ATT_R, S, cosb, sinb, false);
     if (threadIdx.x < ATT_R) {
       const int qi = qt * ATT_R + threadIdx.x;
       Ls[threadIdx.x] = qi < S ? lse[lrow + qi] : 0.f;
       Dl[threadIdx.x] = qi < S ? delta[lrow + qi] : 0.f;
     }
     __syncthreads();
-#pragma unroll 4
-    for (int r = 0; r < ATT_R; ++r) {
-      const int qi = qt * ATT_R + r;
-      const float* qr = Qs + r * HD + d0;
-      const float* dr = Ds + r * HD + d0;
-      const float s = dot_lds<HD>(k, qr) * sl2;
-      const float dp = dot_lds<HD>(v, dr);
-      const float p = (qi >= j && qi < S) ? exp2f(s - Ls[r]) : 0.f;
-      const float ds = p * (dp - Dl[r]);
+    for (int u = (qt == kb ? w : 0); u < 4; ++u) {  // 16-query sub-tiles at or below the diagonal
+      const f4m sv = dot_block<HD>(Qs + (16 * u + n) * HP, kf, g);   // S[query 4g+i][key n]
+      const f4m dpv = dot_block<HD>(Ds + (16 * u + n) * HP, vf, g);  // dP = dO V^T
+      float p[4], ds[4];
 #pragma unroll
-      for (int m = 0; m < DPT; m += 4) {
-        const float4 qq = *(const float4*)(qr + m);
-        const float4 dd = *(const float4*)(dr + m);
-        dk[m] += ds * qq.x; dk[m + 1] += ds * qq.y; dk[m + 2] += ds * qq.z; dk[m + 3] += ds * qq.w;
-        dv[m] += p * dd.x; dv[m + 1] += p * dd.y; dv[m + 2] += p * dd.z; dv[m + 3] += p * dd.w;
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * u + 4 * g + i, qi = qt * ATT_R + r;
+        p[i] = (qi >= key && qi < S) ? exp2f(sv[i] * sl2 - Ls[r]) : 0.f;
+        ds[i] = p[i] * (dpv[i] - Dl[r]);
       }
+      accum_rows<HD>(dv, Ds, 16 * u, p, g, n);   // dV^T[d][key n] += dO^T P
+      accum_rows<HD>(dk, Qs, 16 * u, ds, g, n);  // dK^T[d][key n] += Q^T dS
     }
   }
-  if (j >= S) return;
-#pragma unroll
-  for (int m = 0; m < DPT; ++m) dk[m] *= scale;
-  rope_slice<DPT>(dk, cosb + (long long)j * (HD / 2), sinb + (long long)j * (HD / 2), d0, -1);
-  float* dst = dqkv + (long long)(b * S + j) * rs + (long long)h * HD + d0;
-  store_slice<DPT>(dst + (long long)H * HD, dk);
-  store_slice<DPT>(dst + 2LL * H * HD, dv);
+  if (key >= S) return;
+  float* dst = dqkv + (long long)(b * S + key) * rs + (long long)h * HD;
+  store_blocks<HD>(dst + (long long)H * HD, dk, g, scale, cosb + (long long)key * (HD / 2),
+                   sinb + (long long)key * (HD / 2));
+  store_blocks<HD>(dst + 2LL * H * HD, dv, g, 1.f, nullptr, nullptr);
 }
 
 #define ATT_HD_SWITCH(HDV, CALL) \

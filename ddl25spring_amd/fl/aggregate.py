@@ -1,7 +1,11 @@
 """Server-side aggregation across the clients of a round, distributed over the GPUs.
 
 * ``MeanAggregator`` — FedAvg / FedSGD weighted mean ``sum_k (n_k / n) w_k`` (reference
-  hfl_complete.py:370-378): per-GPU weighted row-reduction kernel, then ONE all-reduce of P floats.
+  hfl_complete.py:370-378): per-GPU weighted row-reduction kernel (products rounded, added in client
+  order), then across the ranks either ONE all-reduce of P floats, or (``ordered``, the default) an
+  all-gather of the W partials added in rank order by the same kernel — so a run with one client
+  per GPU is bitwise the single-process multi-slot run (the 8-GPU headline layout reproduces the
+  1-GPU model exactly), at the price of W x P floats gathered instead of an all-reduce.
 * Byzantine-robust aggregators [north-star; absent from the reference, announced in its
   README.md:89-92]: ``Krum`` / multi-Krum (Blanchard et al. 2017), coordinate-wise ``Median`` and
   ``TrimmedMean`` (Yin et al. 2018). They need every client vector, so they run *coordinate-
@@ -25,14 +29,34 @@ class MeanAggregator:
     name = "mean"
     needs_all = False
 
+    def __init__(self, ordered: bool | None = None):
+        import os
+        self.ordered = (os.environ.get("DDL_FL_ORDERED_MEAN", "1") != "0") if ordered is None else bool(ordered)
+        self._ones: dict = {}
+
     def __call__(self, ctx, rows: torch.Tensor, coeffs: torch.Tensor, out: torch.Tensor):
         """rows [G_local, P] (strided ok), coeffs [G_local] -> out[P] = global weighted sum."""
         if rows.shape[0] == 0:
             out.zero_()
         else:
             Fn.weighted_sum(rows, coeffs, out)
-        ctx.all_reduce(out)
+        if not ctx.is_distributed:
+            return out
+        if not self.ordered:
+            ctx.all_reduce(out)
+            return out
+        parts = ctx.all_gather_rows(out)  # [W, P]: every rank's partial, in rank order
+        key = (parts.shape[0], out.device)
+        ones = self._ones.get(key)
+        if ones is None:
+            ones = self._ones[key] = torch.ones(parts.shape[0], dtype=torch.float32, device=out.device)
+        Fn.weighted_sum(parts, ones, out)  # x 1.0 is exact: a plain rank-order sum
         return out
+
+    def describe(self, ctx) -> str:
+        if not ctx.is_distributed:
+            return "local weighted sum"
+        return "rank-ordered all-gather + sum" if self.ordered else "all-reduce"
 
 
 class _Sharded:
@@ -92,7 +116,7 @@ class Krum(_Sharded):
 
     def __init__(self, f: int = 1, m: int = 1):
         self.f, self.m = f, m
-        self.last_selected: list[int] = []
+        self._sel = None
 
     def __call__(self, ctx, rows, counts, P):
         K = sum(counts)
@@ -105,9 +129,17 @@ class Krum(_Sharded):
         d2.fill_diagonal_(float("inf"))
         scores = torch.sort(d2, 1).values[:, :nb].sum(1)
         sel = torch.argsort(scores)[:max(1, self.m)]
-        self.last_selected = sel.tolist()
-        part = shard[sel].mean(0)
+        self._sel = sel  # stays on the device: no host sync per round (``last_selected`` reads it)
+        chosen = shard.index_select(0, sel)
+        m = chosen.shape[0]
+        part = torch.empty(chosen.shape[1], dtype=torch.float32, device=chosen.device)
+        Fn.weighted_sum(chosen, torch.full((m,), 1.0 / m, dtype=torch.float32, device=chosen.device), part)
         return self.unshard(ctx, part, P, Pp)
+
+    @property
+    def last_selected(self) -> list[int]:
+        """The clients (rank-major row order) the last round averaged (syncs the device)."""
+        return [] if self._sel is None else self._sel.tolist()
 
 
 def make_aggregator(name: str, **kw):

@@ -363,9 +363,9 @@ class FederatedGAN:
             res.wall_time.append(time.perf_counter() - t0)
             res.loss_d.append(float(ld) / div if ld is not None else 0.0)
             res.loss_g.append(float(lg) / div if lg is not None else 0.0)
-        else:
-            res.loss_d.append(ld.detach().clone() / div if ld is not None else 0.0)
-            res.loss_g.append(lg.detach().clone() / div if lg is not None else 0.0)
+        else:  # (device tensor, divisor): read and divided on the host in _settle, as above
+            res.loss_d.append((ld.detach().clone(), div) if ld is not None else 0.0)
+            res.loss_g.append((lg.detach().clone(), div) if lg is not None else 0.0)
         res.rounds += 1
         self.round_idx += 1
 
@@ -415,13 +415,14 @@ class FederatedGAN:
 
     def _settle(self, res):
         """Unsynchronised rounds: one device sync, the comm check and the loss reads, at the end."""
-        if any(torch.is_tensor(v) for v in res.loss_d + res.loss_g):
+        if any(isinstance(v, tuple) for v in res.loss_d + res.loss_g):
             if self.device.type == "cuda":
                 torch.cuda.synchronize()
             if self.ctx is not None:
                 self.ctx.check_comm()
-            res.loss_d = [float(v) for v in res.loss_d]
-            res.loss_g = [float(v) for v in res.loss_g]
+            val = lambda v: float(v[0]) / v[1] if isinstance(v, tuple) else v  # noqa: E731
+            res.loss_d = [val(v) for v in res.loss_d]
+            res.loss_g = [val(v) for v in res.loss_g]
         return res
 
     # --------------------------------------------------------------------------- checkpointing

@@ -116,6 +116,15 @@ class PipelineStage:
         return total
 
     # ------------------------------------------------------------------ asynchronous (per-link) P2P
+    # One communicator per DIRECTED stage link (pipeline_links): a stage posts the receives of the
+    # comm steps that follow BEFORE it computes, and its sends complete in the background, while the
+    # DP gradient bucketer's all-reduces run on other communicators. Nothing orders these kernels
+    # across ranks, so with RCCL this relies on the GPU co-scheduling them (each collective kernel
+    # occupies a few CUs and spins until its peers arrive; a GPU that could not keep a posted
+    # receive and another link's kernel resident at once could deadlock). On MI355X the kernels are
+    # small next to 256 CUs; DDL_PP_ASYNC=0 (apps/llm.py builds no links) selects the grouped,
+    # step-ordered batch_isend_irecv path of ``run`` as the fallback. Covered on gloo by
+    # tests/test_parallel_cpu.py::test_dp_x_pp_grid_runs_and_replicas_agree[3] (dp 2 x pp 3 + bucketer).
     def _link(self, op: int, peer_stage: int):
         me, peer = self.ranks[self.stage], self.ranks[peer_stage]
         return self.links[(me, peer) if op in (S.SEND_ACT, S.SEND_GRAD) else (peer, me)], peer

@@ -65,6 +65,19 @@ class DistContext:
             out.copy_(t.reshape(out.shape))
         return out
 
+    def all_gather_rows(self, t: torch.Tensor, group=None) -> torch.Tensor:
+        """[W, *t.shape]: every rank's t, in rank order (RCCL all-gather into one buffer; gloo via
+        its list form)."""
+        W = dist.get_world_size(group) if self.is_distributed else 1
+        out = torch.empty((W,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        if not self.is_distributed:
+            out[0].copy_(t)
+        elif self.backend == "nccl":
+            dist.all_gather_into_tensor(out, t.contiguous(), group=group)
+        else:
+            dist.all_gather(list(out.unbind(0)), t.contiguous(), group=group)
+        return out
+
     def all_to_all_single(self, out: torch.Tensor, t: torch.Tensor, group=None):
         if self.is_distributed:
             dist.all_to_all_single(out, t, group=group)
@@ -252,6 +265,14 @@ def shutdown():
             _CTX.ipc.close()  # collective: barrier before unmapping
     finally:
         if dist.is_initialized():
+            # every rank reaches teardown before any rank closes its connections: a rank that exits
+            # while a peer still drains a send / receive on one of the (many: one per pipeline link)
+            # gloo groups can make that peer's transport thread throw (std::terminate -> SIGABRT)
+            try:
+                if err is None and _CTX is not None and _CTX.is_distributed:
+                    _CTX.barrier()
+            except Exception:  # noqa: BLE001 - best effort: a dead peer must not hang teardown
+                pass
             dist.destroy_process_group()
         _CTX = None
     if err is not None:

@@ -3,7 +3,7 @@
 #   bash scripts/gpu/pmc_x6h.sh <mode> <layer> [halo 0|1]
 set -o pipefail
 export TMPDIR=/tmp
-O=$1; L=$2; H=${3:-1}
+O=$1; L=$2; H=${3:-1}; X=${4:-}
 out=gpurun_out/pmcx/${O}_${L}_h${H}
 mkdir -p $out
 PA="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"
@@ -11,7 +11,7 @@ PB="SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SALU 
 i=0
 for P in "$PA" "$PB"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $P -d $out/p$i -o run -- python scripts/conv_f32_bench.py --math x6 --halo $H --mode $O --layer $L --reps 10 > $out/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $out/p$i.log; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc $P -d $out/p$i -o run -- python scripts/conv_f32_bench.py --math x6 --halo $H --mode $O --layer $L --reps 10 $X > $out/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $out/p$i.log; exit 1; }
 done
 tail -1 $out/p1.log
 K=convx6h_kernel; [ "$H" = 0 ] && K=convf32_kernel

@@ -1,6 +1,7 @@
 """Multi-rank FL on the device: 2 ranks share the one GPU of the test box over gloo (RCCL needs one
 GPU per rank; the 8-GPU RCCL run is the driver's), exercising slot assignment, device-tensor
 collectives and the replicated server state exactly as the 8-GPU bench does."""
+import json
 import os
 import subprocess
 import sys
@@ -152,5 +153,37 @@ def test_vfl_gan_bench_two_ranks_share_gpu():
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1 and '"n_gpus": 2' in lines[0], out.stdout[-2000:]
+    # the split-NN + fp32 DCGAN line, then the labelled bf16 DCGAN line
+    assert len(lines) == 2 and all('"n_gpus": 2' in l for l in lines), out.stdout[-2000:]
+    assert json.loads(lines[0])["dtype"].endswith("fp32 (DCGAN)") and json.loads(lines[1])["dtype"] == "bf16"
     print(lines[0])
+
+
+def _bench_json(stdout):
+    import json
+    lines = [l for l in stdout.splitlines() if l.startswith("{")]
+    assert lines, stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_eight_ranks_one_slot_each_match_single_process():
+    """The driver's 8-GPU headline layout rehearsed on one GPU: bench.py through torchrun with 8
+    gloo ranks sharing the device, ONE client slot per rank (--clients = world), vs the
+    single-process run holding all 8 clients as slots. Plans pinned so a client runs the same tiles
+    at G = 1 and G = 8 (DDL_F32_TARGET_WG=1: no split-K; DDL_F32_TUNED=0). With the rank-ordered
+    FedAvg mean (fl/aggregate.py) the 8-rank model is bitwise the single-process one, and every
+    rank holds the same bits (rank_hashes_equal)."""
+    env = dict(os.environ, DDL_F32_TARGET_WG="1", DDL_F32_TUNED="0", OMP_NUM_THREADS="2")
+    common = [os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "1", "--clients", "8",
+              "--train-size", "1600", "--deterministic"]
+    one = subprocess.run([sys.executable, *common], capture_output=True, text=True, timeout=900, cwd=ROOT, env=env)
+    assert one.returncode == 0, one.stderr[-3000:]
+    eight = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+                            "--master-addr", "127.0.0.1", "--master-port", "29751", *common, "--gpus", "8",
+                            "--backend", "gloo"], capture_output=True, text=True, timeout=900, cwd=ROOT, env=env)
+    assert eight.returncode == 0, eight.stderr[-3000:]
+    a, b = _bench_json(one.stdout), _bench_json(eight.stdout)
+    print(json.dumps({k: b[k] for k in ("n_gpus", "aggregation", "allreduce", "rank_hashes_equal", "value")}))
+    assert b["n_gpus"] == 8 and b["config"]["client_slots_per_gpu"] == 1 and a["config"]["client_slots_per_gpu"] == 8
+    assert b["rank_hashes_equal"] is True and "allreduce" in b and b["aggregation"].startswith("rank-ordered")
+    assert a["w_global_sha256"] == b["w_global_sha256"]

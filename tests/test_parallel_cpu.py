@@ -159,14 +159,14 @@ def test_data_parallel_ga_equals_large_batch():
         assert torch.allclose(w0[n], p.detach(), atol=1e-5), n
 
 
-def _grid_worker(rank, world, port, out_dir):
+def _grid_worker(rank, world, port, out_dir, pp=2):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     from ddl25spring_amd.parallel.dp import GradBucketer
     from ddl25spring_amd.parallel.pipeline import PipelineStage, grid_ranks, pipeline_links
     from ddl25spring_amd.runtime import dist as rdist
     ctx = rdist.init(backend="gloo", device="cpu")
-    dp, pp = 2, 2
+    dp = world // pp
     pipe, stage, pipe_ranks, dp_ranks = grid_ranks(rank, dp, pp)
     # collective creation of every DP group, in the same order on all ranks (fixes SURVEY Q2)
     dp_group = ctx.new_groups("dp", [[p * pp + s for p in range(dp)] for s in range(pp)])
@@ -195,15 +195,20 @@ def _grid_worker(rank, world, port, out_dir):
     rdist.shutdown()
 
 
-def test_dp_x_pp_grid_runs_and_replicas_agree():
+@pytest.mark.parametrize("pp", [2, 3])
+def test_dp_x_pp_grid_runs_and_replicas_agree(pp):
+    """DP x PP grid, 1F1B with the asynchronous per-link P2P (one communicator per directed stage
+    link, irecvs posted ahead) running beside the DP gradient bucketer's all-reduces on the DP
+    groups: pp = 3 has a middle stage with two links in flight at once."""
+    world = 2 * pp
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_grid_worker, args=(4, 29933, d), nprocs=4, join=True)
-        res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(4)]
-    # stage s of pipeline 0 (rank s) and pipeline 1 (rank 2 + s) hold identical weights
-    for s in range(2):
-        for a, b in zip(res[s]["w"], res[2 + s]["w"]):
+        mp.spawn(_grid_worker, args=(world, 29933 + pp, d, pp), nprocs=world, join=True)
+        res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    # stage s of pipeline 0 (rank s) and pipeline 1 (rank pp + s) hold identical weights
+    for s in range(pp):
+        for a, b in zip(res[s]["w"], res[pp + s]["w"]):
             assert torch.allclose(a, b, atol=1e-6)
-    assert len(res[1]["losses"]) == 3 and len(res[3]["losses"]) == 3
+    assert len(res[pp - 1]["losses"]) == 3 and len(res[2 * pp - 1]["losses"]) == 3
 
 
 def _native_dp_worker(rank, world, port, out_dir):
