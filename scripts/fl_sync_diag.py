@@ -48,19 +48,23 @@ def run(mode: str, cuda):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--modes", default="sync,unsync,jitter")
     a = ap.parse_args()
     cuda = torch.device("cuda")
-    ref = None
+    ref = prev = None
     for rep in range(a.reps):
-        for mode in ("sync", "unsync", "jitter"):
+        for mode in a.modes.split(","):
             w0, w, ntune = run(mode, cuda)
             if ref is None:
                 ref, step = w, (w - w0).norm()
                 print(f"rep {rep} {mode:6s}: reference (update norm {step.item():.4e}), tuner keys {ntune}")
+                prev = w
                 continue
             rel = ((w - ref).norm() / step).item()
-            print(f"rep {rep} {mode:6s}: rel to first sync run {rel:.3e}  bitwise {torch.equal(w, ref)}  "
-                  f"tuner keys {ntune}", flush=True)
+            same_prev = prev is not None and torch.equal(w, prev)
+            print(f"rep {rep} {mode:6s}: rel to first run {rel:.3e}  bitwise {torch.equal(w, ref)}  "
+                  f"equal to previous run {same_prev}  tuner keys {ntune}", flush=True)
+            prev = w
 
 
 if __name__ == "__main__":

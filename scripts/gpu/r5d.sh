@@ -24,3 +24,7 @@ bash scripts/gpu/pmc_x6h.sh fwd c128 1 > gpurun_out/${T}_pmc_fwd_c128.txt 2>&1 |
 cat gpurun_out/${T}_pmc_fwd_c128.txt | tail -22
 bash scripts/gpu/pmc_x6h.sh dgrad c64 1 "--dybn 2" > gpurun_out/${T}_pmc_dgrad_c64.txt 2>&1 || exit 1
 cat gpurun_out/${T}_pmc_dgrad_c64.txt | tail -22
+step diag_sync4 300 python -u scripts/fl_sync_diag.py --reps 4 --modes sync
+step diag_notune 300 env DDL_CONV_AUTOTUNE=0 python -u scripts/fl_sync_diag.py --reps 2 --modes sync,unsync,sync
+step llm_flat 300 env DDL_F32_FLAT1X1=1 python -u benchmarks/bench_llm.py --precision fp32 --steps 10 --warmup 3
+step llm_base 300 python -u benchmarks/bench_llm.py --precision fp32 --steps 10 --warmup 3
