@@ -27,6 +27,7 @@
 // Deterministic: fixed reduction order, per-step IEEE accumulation of the three-MFMA chains (the
 // bf16 MFMA's own accumulation is not round-to-nearest, see conv_f32.hip), plain stores only.
 #include "conv_f32_core.h"
+#include <cstdlib>
 
 constexpr int BQH = 128;    // output pixels per tile
 // Operand images are PLANAR per 16-channel chunk: [h0..h15 | m0..m15 | l0..l15] (3 x 32 B), one
@@ -62,6 +63,7 @@ struct HaloGeo {
   int SH, SW, SC;  // source (X for FWD, dY for DGRAD) height, width, channels
   int Pd;       // output channels (K for FWD, C for DGRAD)
   int ROWB, SEGB, HBYTES;  // halo row / segment strides, image bytes
+  int probe;    // timing probes (DDL_X6H_PROBE, WRONG results): 1 no weight DMA, 2 no halo loads, 4 no MFMAs
 };
 
 typedef float f16v __attribute__((ext_vector_type(16)));
@@ -174,6 +176,7 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
   float4 hreg[NUH];
   float4 hxb[DYB_OK ? NUH : 1];
   auto halo_load = [&](int cc) {
+    if (hg.probe & 2) return;
 #pragma unroll
     for (int i = 0; i < NUH; ++i) hreg[i] = bload4(rS, hoff[i], (unsigned)cc * 64u);
     if constexpr (DYB_OK) {
@@ -241,6 +244,7 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
     woff[i] = (row < BP && gr < 6 && p < Pd) ? (unsigned)((long long)p * T * SC * 6 + gr * 16) : OOB;
   }
   auto wload = [&](int buf, int cc, int t) {
+    if (hg.probe & 1) return;
     const int wtap = MODE == F_FWD ? t : T - 1 - t;  // DGRAD: the flipped kernel
     const unsigned add = (unsigned)(wtap * SC * 6 + cc * 96);  // wave-uniform: the scalar offset
 #pragma unroll
@@ -278,6 +282,7 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
   // X6H_CHAIN (1 or 2): steps per chain before the IEEE add (unrolled-tap path only)
   f16v cch[TI][TJ];
   auto compute = [&](int buf, int t, bool first = true, bool last = true) {
+    if (hg.probe & 4) return;
     const char* P = pimg + buf * PIMG;
     const int dr = t / RS, ds = t - dr * RS;
     // one 16-channel step: A (weights) and B (activations) as three piece vectors each; the six
@@ -609,6 +614,11 @@ static bool x6h_geo(const ConvF32Args& a, int mode, int bp, HaloGeo& h, int& rs)
   const long long lim = (1LL << 31) - 64;
   if ((long long)a.N * a.H * a.W * h.SC * 4 > lim || (long long)h.Pd * a.R * a.S * h.SC * 6 > lim) return false;
   halo_layout(h);
+  static const int probe = [] {
+    const char* e = getenv("DDL_X6H_PROBE");
+    return e ? atoi(e) : 0;
+  }();
+  h.probe = probe;
   // the instance is chosen by x6h_large(): a halo of more than 208 pixels (e.g. 64-wide images: two
   // rows of 66) runs on the large instance even when its bytes would fit the small one
   if (h.HBYTES > HBLARGE || h.HP > 288) return false;

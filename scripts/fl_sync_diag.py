@@ -10,7 +10,11 @@ synchronised runs do, the spread is timing-dependent fp32-atomic order (split-K 
 bf16 rounding — not an ordering / plan / buffer-reuse bug in the unsynchronised path (which the
 fp32 path checks bit for bit: test_fp32_gpu.py::test_fp32_unsynchronised_rounds_equal_exactly).
 
-    python scripts/fl_sync_diag.py [--reps 3]
+    python scripts/fl_sync_diag.py [--reps 3] [--modes sync,unsync,unsync_s,jitter]
+
+"unsync_s" runs the unsynchronised code path with a device sync after every round: if it matches
+the synchronised runs while "unsync" does not, the difference is a cross-stream race exposed by the
+host running ahead, not a code-path difference.
 """
 from __future__ import annotations
 
@@ -36,11 +40,13 @@ def run(mode: str, cuda):
                 client_fraction=1.0, seed=3, ctx=DistContext(device=cuda), eval_every=0)
     w0 = fa.w_global.clone()
     fa.round()
-    fa.sync_rounds = mode != "unsync"
+    fa.sync_rounds = not mode.startswith("unsync")
     for i in range(3):
         if mode == "jitter":
             torch.cuda._sleep(int(2e5 * (1 + i)))  # perturb launch timing only
         fa.round()
+        if mode == "unsync_s":  # unsynchronised code path, but the host never runs ahead
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     return w0, fa.w_global.clone(), len(autotune.cache())
 
