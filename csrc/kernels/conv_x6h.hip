@@ -63,7 +63,9 @@ struct HaloGeo {
   int SH, SW, SC;  // source (X for FWD, dY for DGRAD) height, width, channels
   int Pd;       // output channels (K for FWD, C for DGRAD)
   int ROWB, SEGB, HBYTES;  // halo row / segment strides, image bytes
-  int probe;    // timing probes (DDL_X6H_PROBE, WRONG results): 1 no weight DMA, 2 no halo loads, 4 no MFMAs
+  int probe;    // timing probes (DDL_X6H_PROBE, WRONG results): 1 no weight DMA, 2 no halo loads, 4 no
+                // fragment reads / MFMAs, 8 no epilogue, 16 no main-loop barriers, 32 no halo split / LDS stores, 64 return at
+                // once, 128 no main loop
 };
 
 typedef float f16v __attribute__((ext_vector_type(16)));
@@ -93,6 +95,152 @@ __device__ __forceinline__ float4 bload4(const __amdgpu_buffer_rsrc_t& rs, unsig
 #ifndef X6H_CHAIN
 #define X6H_CHAIN 3
 #endif
+// X6H_TRANSPOSE 1: activations are the MFMA A operand (D[q][p], fepi_t); 0: weights are (D[p][q],
+// the quads-of-channels epilogue fepi of conv_f32_core.h) — kept for A/B runs
+#ifndef X6H_TRANSPOSE
+#define X6H_TRANSPOSE 1
+#endif
+
+// Epilogue on the transposed accumulators (activations were the MFMA A operand): lane l of wave
+// (wp, wq) holds channel p = wp * BP/2 + ti * 32 + (l & 31) of the pixels
+// q = wq * 64 + tj * 32 + 8 * (r >> 2) + 4 * (l >> 5) + (r & 3), r = 0..15 (acc[ti][tj][r]).
+// Every store / residual / mask load is one dword per lane with 32 consecutive channels per
+// half-wave (full 128-B lines; the quads-of-channels layout of fepi wrote 32-B pieces of 32 lines
+// per instruction), addressed as buffer ops: the lane's (q, p) byte offset in a VGPR and the
+// element's uniform row offset (tj * 32 + 8 * (r >> 2) + (r & 3)) * Pd * 4 in the SCALAR offset, so
+// an element costs one memory instruction and no address VALU; rows past Qd fall outside the
+// descriptor's range (loads read 0, stores drop) and lanes past Pd carry the OOB offset. The BN
+// statistics reduce over a lane's own 32 pixels before a single cross-half shuffle (fepi: a 5-step
+// shuffle tree per channel quad). Same outputs and slot layout as fepi (conv_f32_core.h): FWD y =
+// [relu](acc + bias + residual) with per-tile (sum, M2 about the tile mean); stride-1 DGRAD
+// dx = mask(acc + residual) with the BN-backward sums.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const float* p, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float bld1(const __amdgpu_buffer_rsrc_t& rs, unsigned off, unsigned soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, soff, 0));
+}
+__device__ __forceinline__ void bst1(float v, const __amdgpu_buffer_rsrc_t& rs, unsigned off, unsigned soff) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rs, off, soff, 0);
+}
+
+template <int MODE, int BP>
+__device__ __forceinline__ void fepi_t(const ConvF32Args& a, const FGeo& o, f16v (&acc)[BP / 64][2], float* red) {
+  constexpr int WP = BP / 2, TI = WP / 32, TJ = 2;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wp = wid >> 1, wq = wid & 1;
+  const int g = o.g, Pd = o.Pd;
+  const bool want_stats = a.stats != nullptr;
+  const bool dg_stats = MODE == F_DGRAD && want_stats && a.bn_x;
+  const long long gofs = (long long)g * a.out_gs;
+  const long long nbytes = (long long)o.Qd * Pd * 4;  // one group's output (host: < 2^31)
+  const __amdgpu_buffer_rsrc_t rO = rsrc_of(a.out + gofs, nbytes);
+  const bool res_full = a.residual && (MODE == F_FWD || a.res_sub != 2);
+  const __amdgpu_buffer_rsrc_t rR = rsrc_of(res_full ? a.residual + gofs : a.out, nbytes);
+  const __amdgpu_buffer_rsrc_t rM = rsrc_of(a.mask ? a.mask + gofs : a.out, nbytes);
+  const __amdgpu_buffer_rsrc_t rX = rsrc_of(a.bn_x ? a.bn_x + gofs : a.out, nbytes);
+  const int qb = o.q0 + wq * 64 + 4 * (lane >> 5);
+  const bool full = o.q0 + BQH <= o.Qd;
+  const unsigned rowb = (unsigned)Pd * 4u;
+  // compact-grid residual (res_sub 2, the stride-2 shortcut's dX on even pixels): rare, plain loads
+  const FDiv dH = mk_fdiv((uint32_t)a.H);
+  int lgw = 0;
+  while ((1 << lgw) < a.W) ++lgw;
+#pragma unroll
+  for (int ti = 0; ti < TI; ++ti) {
+    const int pl = wp * WP + ti * 32 + (lane & 31);
+    const int p = o.p0 + pl;
+    const bool pv = p < Pd;
+    const unsigned vo = pv ? ((unsigned)qb * (unsigned)Pd + (unsigned)p) * 4u : OOB;
+    float bia = 0.f, bm = 0.f, br = 0.f, ms = 0.f, mh = 0.f;
+    if (MODE == F_FWD && a.bias && pv) bia = a.bias[(long long)g * a.bias_gs + p];
+    if (MODE == F_DGRAD && a.bn_x && pv) {
+      bm = a.bn_mean[(long long)g * Pd + p];
+      br = a.bn_rstd[(long long)g * Pd + p];
+    }
+    if (MODE == F_DGRAD && a.mask_scale && pv) {
+      ms = a.mask_scale[(long long)g * Pd + p];
+      mh = a.mask_shift[(long long)g * Pd + p];
+    }
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int tj = 0; tj < TJ; ++tj)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int dq = tj * 32 + 8 * (r >> 2) + (r & 3);
+        const unsigned so = (unsigned)dq * rowb;
+        const bool ok = pv && (full || qb + dq < o.Qd);
+        float v = acc[ti][tj][r];
+        if (MODE == F_FWD) {
+          v += bia;
+          if (res_full) v += bld1(rR, vo, so);
+          if (a.relu) v = fmaxf(v, 0.f);
+          if (want_stats) {
+            s0 += ok ? v : 0.f;
+            acc[ti][tj][r] = v;  // kept for the centred second pass
+          }
+        } else {
+          if (a.residual && !res_full && ok) {
+            const int q = qb + dq, t = q >> lgw, ww = q & (a.W - 1);
+            const int nn = fdv(t, dH), hh = t - nn * a.H;
+            if (((hh | ww) & 1) == 0) {
+              const int Hc = (a.H + 1) >> 1, Wc = (a.W + 1) >> 1;
+              v += a.residual[(long long)g * a.res_gs + (((long long)nn * Hc + (hh >> 1)) * Wc + (ww >> 1)) * Pd + p];
+            }
+          } else if (res_full) {
+            v += bld1(rR, vo, so);
+          }
+          if (a.mask && !(bld1(rM, vo, so) > 0.f)) v = 0.f;
+          if (a.bn_x) {
+            const float xs = bld1(rX, vo, so);
+            if (a.mask_scale && !(xs * ms + mh > 0.f)) v = 0.f;
+            if (want_stats && ok) {
+              s0 += v;
+              s1 += v * ((xs - bm) * br);
+            }
+          }
+        }
+        bst1(v, rO, vo, so);
+      }
+    if ((MODE == F_FWD && want_stats) || dg_stats) {
+      s0 += __shfl_xor(s0, 32, 64);
+      if (MODE == F_DGRAD) s1 += __shfl_xor(s1, 32, 64);
+      if (lane < 32) {
+        red[(wq * BP + pl) * 2] = s0;
+        if (MODE == F_DGRAD) red[(wq * BP + pl) * 2 + 1] = s1;
+      }
+    }
+  }
+  if (!want_stats || (MODE == F_DGRAD && !a.bn_x)) return;
+  if constexpr (MODE == F_FWD) {
+    // (sum, M2 about the tile mean), merged across tiles with Chan's formula in bnf_finalize
+    const int nq = min(BQH, o.Qd - o.q0);
+    __syncthreads();
+#pragma unroll
+    for (int ti = 0; ti < TI; ++ti) {
+      const int pl = wp * WP + ti * 32 + (lane & 31);
+      const bool pv = o.p0 + pl < Pd;
+      const float mu = (red[pl * 2] + red[(BP + pl) * 2]) / (float)nq;
+      float m2 = 0.f;
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int dq = tj * 32 + 8 * (r >> 2) + (r & 3);
+          const float d = acc[ti][tj][r] - mu;
+          m2 += (pv && (full || qb + dq < o.Qd)) ? d * d : 0.f;
+        }
+      m2 += __shfl_xor(m2, 32, 64);
+      if (lane < 32) red[(wq * BP + pl) * 2 + 1] = m2;
+    }
+  }
+  __syncthreads();
+  if (tid < BP && o.p0 + tid < Pd) {
+    const int slot = o.phase * (a.slots / o.nph) + o.tq;
+    float* st = a.stats + ((long long)g * a.slots + slot) * 2 * Pd + o.p0 + tid;
+    st[0] = red[tid * 2] + red[(BP + tid) * 2];
+    st[Pd] = red[tid * 2 + 1] + red[(BP + tid) * 2 + 1];
+  }
+}
 
 template <int MODE, int BP, int RS, int HB>
 __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo hg) {
@@ -114,6 +262,7 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
   const int lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
   const int u = xcd_remap(lin, gx * gy * gz);
   const int bx = u % gx, by = (u / gx) % gy, g = u / (gx * gy);
+  if (hg.probe & 64) return;  // launch / dispatch cost only
   const FGeo o = fgeo<MODE, BP, BQH>(a, bx, by, g, gy);
   const bool split_store = a.split_k > 1;
   if (o.q0 >= o.Qd || o.p0 >= o.Pd) {
@@ -198,6 +347,7 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
     }
   };
   auto halo_store = [&](int cc) {
+    if (hg.probe & 32) return;
 #pragma unroll
     for (int i = 0; i < NUH; ++i) {
       if (hlds[i] < 0) continue;
@@ -306,12 +456,20 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
     for (int ti = 0; ti < TI; ++ti)
 #pragma unroll
       for (int tj = 0; tj < TJ; ++tj) {
-        f16v c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ti], bh[tj], first ? (f16v){} : cch[ti][tj], 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ti], bl[tj], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[ti], bm[tj], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ti], bm[tj], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[ti], bh[tj], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ti], bh[tj], c, 0, 0, 0);
+        // activations as the A operand: D[q][p], so a lane ends up holding ONE channel of 16 pixels
+        // (fepi_t: coalesced stores, per-lane BN sums)
+#if X6H_TRANSPOSE
+#define X6MF(A, B, C) __builtin_amdgcn_mfma_f32_32x32x16_bf16(B, A, C, 0, 0, 0)
+#else
+#define X6MF(A, B, C) __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, B, C, 0, 0, 0)
+#endif
+        f16v c = X6MF(al[ti], bh[tj], first ? (f16v){} : cch[ti][tj]);
+        c = X6MF(ah[ti], bl[tj], c);
+        c = X6MF(am[ti], bm[tj], c);
+        c = X6MF(ah[ti], bm[tj], c);
+        c = X6MF(am[ti], bh[tj], c);
+        c = X6MF(ah[ti], bh[tj], c);
+#undef X6MF
         if (last) {
 #pragma unroll
           for (int v = 0; v < 16; ++v) acc[ti][tj][v] = acc[ti][tj][v] + c[v];
@@ -324,7 +482,7 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
       }
   };
 
-  if (k0 < k1) {
+  if (k0 < k1 && !(hg.probe & 128)) {
     // Weight images: a ring of NWB = 3; the DMA of step k + 2 is issued at step k into slot
     // (k + 2) % 3, whose last reader (step k - 1) is past the barrier. vmcnt counts in issue order
     // (DMA pieces and the halo register loads together): at the end of step k, step k + 1's pieces
@@ -365,7 +523,7 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
             else if (xf) wait_vm<UP + NUH + 2>();
             else wait_vm<UP + NUH>();
           } else wait_vm<UP>();
-          cta_barrier();
+          if (!(hg.probe & 16)) cta_barrier();
           if (t == T - 1 && more) {  // chunk boundary: every wave is done with this chunk's halo
             halo_store(cc + 1);
             wait_lds();
@@ -406,6 +564,16 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
   }
 
   // ---------------------------------------------------------------- epilogue
+  if (hg.probe & 8) {  // keep the accumulators live without storing them
+    float sink = 0.f;
+#pragma unroll
+    for (int ti = 0; ti < TI; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj) sink += acc[ti][tj][0] + acc[ti][tj][15];
+    if (sink == 1.2345f) a.out[tid] = sink;
+    return;
+  }
+#if !X6H_TRANSPOSE
   f4v quad[Lay32<BP, BQH>::NPQ][Lay32<BP, BQH>::NQ];
 #pragma unroll
   for (int ti = 0; ti < TI; ++ti)
@@ -416,7 +584,6 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
         quad[ti * 4 + gg][tj] = (f4v){acc[ti][tj][4 * gg], acc[ti][tj][4 * gg + 1], acc[ti][tj][4 * gg + 2],
                                       acc[ti][tj][4 * gg + 3]};
   if (split_store) {
-    // raw partial sums of this slice: [split][G][1][qmax][Pd] (the layout of conv_f32.hip)
     const long long qmax = (long long)a.slots * BQH;
     float* d = a.partial + ((long long)o.split * a.G + g) * qmax * Pd;
 #pragma unroll
@@ -431,6 +598,27 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
     return;
   }
   fepi<MODE, BP, BQH, Lay32<BP, BQH>>(a, o, quad, (float*)smem);
+#else
+  if (split_store) {
+    // raw partial sums of this slice: [split][G][1][qmax][Pd] (the layout of conv_f32.hip)
+    const long long qmax = (long long)a.slots * BQH;
+    float* d = a.partial + ((long long)o.split * a.G + g) * qmax * Pd;
+#pragma unroll
+    for (int ti = 0; ti < TI; ++ti) {
+      const int p = o.p0 + wp * WP + ti * 32 + (lane & 31);
+      if (p >= Pd) continue;
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int q = o.q0 + wq * 64 + tj * 32 + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
+          if (q < o.Qd) d[(long long)q * Pd + p] = acc[ti][tj][r];
+        }
+    }
+    return;
+  }
+  fepi_t<MODE, BP>(a, o, acc, (float*)smem);
+#endif
 }
 
 // Pre-split weights: FWD layout [G][K][T][C] (16-channel chunks of the input channels), DGRAD
@@ -613,6 +801,7 @@ static bool x6h_geo(const ConvF32Args& a, int mode, int bp, HaloGeo& h, int& rs)
   if (mode == F_DGRAD && a.in_scale) return false;
   const long long lim = (1LL << 31) - 64;
   if ((long long)a.N * a.H * a.W * h.SC * 4 > lim || (long long)h.Pd * a.R * a.S * h.SC * 6 > lim) return false;
+  if ((long long)a.N * a.P * a.Q * h.Pd * 4 > lim) return false;  // fepi_t: buffer-addressed output
   halo_layout(h);
   static const int probe = [] {
     const char* e = getenv("DDL_X6H_PROBE");

@@ -98,6 +98,12 @@ def test_x6h_dgrad(cuda, geom, split):
         mask = torch.randn(geom.G, geom.N, geom.H, geom.W, geom.C, device=cuda)
         d2 = Fn.conv_dgrad(dy, w, geom, residual=res, mask=mask)
         _close(d2, (dxr + res.cpu().double()) * (mask.cpu() > 0))
+        # compact-grid residual (a stride-2 shortcut's dX, added on even pixels only)
+        rc = torch.randn(geom.G, geom.N, (geom.H + 1) // 2, (geom.W + 1) // 2, geom.C, device=cuda)
+        d2c = Fn.conv_dgrad(dy, w, geom, residual=rc, residual_sub=2)
+        up = torch.zeros(geom.G, geom.N, geom.H, geom.W, geom.C, dtype=torch.float64)
+        up[:, :, ::2, ::2] = rc.cpu().double()
+        _close(d2c, dxr + up)
         bx = torch.randn(geom.G, geom.N, geom.H, geom.W, geom.C, device=cuda)
         mean = torch.randn(geom.G, geom.C, device=cuda) * 0.1
         rstd = torch.rand(geom.G, geom.C, device=cuda) + 0.5
