@@ -92,6 +92,9 @@ __device__ __forceinline__ float4 bload4(const __amdgpu_buffer_rsrc_t& rs, unsig
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, soff, 0));
 }
 
+#ifndef X6H_DGRAD128_CHAIN
+#define X6H_DGRAD128_CHAIN 3
+#endif
 #ifndef X6H_CHAIN
 #define X6H_CHAIN 3
 #endif
@@ -141,8 +144,9 @@ __device__ __forceinline__ void fepi_t(const ConvF32Args& a, const FGeo& o, f16v
   const int qb = o.q0 + wq * 64 + 4 * (lane >> 5);
   const bool full = o.q0 + BQH <= o.Qd;
   const unsigned rowb = (unsigned)Pd * 4u;
-  // compact-grid residual (res_sub 2, the stride-2 shortcut's dX on even pixels): rare, plain loads
-  const FDiv dH = mk_fdiv((uint32_t)a.H);
+  // compact-grid residual (res_sub 2, the stride-2 shortcut's dX on even pixels)
+  const __amdgpu_buffer_rsrc_t rC = rsrc_of(a.residual && !res_full ? a.residual + (long long)g * a.res_gs : a.out,
+                                            nbytes / 4);
   int lgw = 0;
   while ((1 << lgw) < a.W) ++lgw;
 #pragma unroll
@@ -161,37 +165,58 @@ __device__ __forceinline__ void fepi_t(const ConvF32Args& a, const FGeo& o, f16v
       ms = a.mask_scale[(long long)g * Pd + p];
       mh = a.mask_shift[(long long)g * Pd + p];
     }
+    // every operand load of a 16-element group is issued before any is used (a load behind a use,
+    // or behind a branch, waits out the previous one's full latency: the residual + mask + BN
+    // DGRAD epilogue ran ~4x the time of its bytes that way)
     float s0 = 0.f, s1 = 0.f;
+    // EB elements per load batch (BP 128 DGRAD sits at the 256-VGPR edge: 8)
+    constexpr int EB = (MODE == F_DGRAD && BP == 128) ? 8 : 16;
 #pragma unroll
-    for (int tj = 0; tj < TJ; ++tj)
+    for (int b0 = 0; b0 < TJ * 16; b0 += EB) {
+      float rv[EB], mv[EB], xv[EB];
+      auto soff = [&](int e) { return (unsigned)((e >> 4) * 32 + 8 * ((e & 15) >> 2) + (e & 3)) * rowb; };
+      if (res_full) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
+        for (int i = 0; i < EB; ++i) rv[i] = bld1(rR, vo, soff(b0 + i));
+      } else if (MODE == F_DGRAD && a.residual) {
+        // compact grid (res_sub 2, H and W even: host-checked): pixel (t = n*H + h, w) reads compact
+        // element ((t >> 1) * W/2 + (w >> 1)) when t and w are both even, else nothing (OOB)
+#pragma unroll
+        for (int i = 0; i < EB; ++i) {
+          const int e = b0 + i, q = qb + (e >> 4) * 32 + 8 * ((e & 15) >> 2) + (e & 3);
+          const int t = q >> lgw, w = q & (a.W - 1);
+          const unsigned ci = (unsigned)(((t >> 1) << (lgw - 1)) + (w >> 1));
+          rv[i] = bld1(rC, (((t | w) & 1) == 0 && pv) ? (ci * (unsigned)Pd + (unsigned)p) * 4u : OOB, 0u);
+        }
+      }
+      if (MODE == F_DGRAD && a.mask) {
+#pragma unroll
+        for (int i = 0; i < EB; ++i) mv[i] = bld1(rM, vo, soff(b0 + i));
+      }
+      if (MODE == F_DGRAD && a.bn_x) {
+#pragma unroll
+        for (int i = 0; i < EB; ++i) xv[i] = bld1(rX, vo, soff(b0 + i));
+      }
+#pragma unroll
+      for (int i = 0; i < EB; ++i) {
+        const int e = b0 + i, tj = e >> 4, r = e & 15;
         const int dq = tj * 32 + 8 * (r >> 2) + (r & 3);
         const unsigned so = (unsigned)dq * rowb;
         const bool ok = pv && (full || qb + dq < o.Qd);
         float v = acc[ti][tj][r];
         if (MODE == F_FWD) {
           v += bia;
-          if (res_full) v += bld1(rR, vo, so);
+          if (res_full) v += rv[i];
           if (a.relu) v = fmaxf(v, 0.f);
           if (want_stats) {
             s0 += ok ? v : 0.f;
             acc[ti][tj][r] = v;  // kept for the centred second pass
           }
         } else {
-          if (a.residual && !res_full && ok) {
-            const int q = qb + dq, t = q >> lgw, ww = q & (a.W - 1);
-            const int nn = fdv(t, dH), hh = t - nn * a.H;
-            if (((hh | ww) & 1) == 0) {
-              const int Hc = (a.H + 1) >> 1, Wc = (a.W + 1) >> 1;
-              v += a.residual[(long long)g * a.res_gs + (((long long)nn * Hc + (hh >> 1)) * Wc + (ww >> 1)) * Pd + p];
-            }
-          } else if (res_full) {
-            v += bld1(rR, vo, so);
-          }
-          if (a.mask && !(bld1(rM, vo, so) > 0.f)) v = 0.f;
+          if (a.residual) v += rv[i];
+          if (a.mask && !(mv[i] > 0.f)) v = 0.f;
           if (a.bn_x) {
-            const float xs = bld1(rX, vo, so);
+            const float xs = xv[i];
             if (a.mask_scale && !(xs * ms + mh > 0.f)) v = 0.f;
             if (want_stats && ok) {
               s0 += v;
@@ -201,6 +226,7 @@ __device__ __forceinline__ void fepi_t(const ConvF32Args& a, const FGeo& o, f16v
         }
         bst1(v, rO, vo, so);
       }
+    }
     if ((MODE == F_FWD && want_stats) || dg_stats) {
       s0 += __shfl_xor(s0, 32, 64);
       if (MODE == F_DGRAD) s1 += __shfl_xor(s1, 32, 64);
@@ -429,7 +455,10 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
   for (int dr = 0; dr < RS; ++dr)
 #pragma unroll
     for (int tj = 0; tj < TJ; ++tj) bdr[dr][tj] = boff[tj] + dr * hg.ROWB;
-  // X6H_CHAIN (1 or 2): steps per chain before the IEEE add (unrolled-tap path only)
+  // X6H_CHAIN (1 or 2): steps per chain before the IEEE add (unrolled-tap path only); the BP 128
+  // DGRAD (dY BN-backward operand: twice the halo registers) keeps per-step chains, whose carried
+  // chain registers would otherwise spill
+  constexpr int CHAIN = (MODE == F_DGRAD && BP == 128 && HB == HBSMALL) ? X6H_DGRAD128_CHAIN : X6H_CHAIN;
   f16v cch[TI][TJ];
   auto compute = [&](int buf, int t, bool first = true, bool last = true) {
     if (hg.probe & 4) return;
@@ -509,8 +538,8 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
           if (t + 2 < T) wload((t + 2) % 3, cc, t + 2);
           else if (more) wload((t + 2) % 3, cc + 1, t + 2 - T);
           if (t == HT && more) halo_load(cc + 1);
-          if constexpr (X6H_CHAIN == 3) compute(t % 3, t, t % 3 == 0, t % 3 == 2);
-          else if constexpr (X6H_CHAIN == 2) compute(t % 3, t, t % 2 == 0, t % 2 == 1 || t == T - 1);
+          if constexpr (CHAIN == 3) compute(t % 3, t, t % 3 == 0, t % 3 == 2);
+          else if constexpr (CHAIN == 2) compute(t % 3, t, t % 2 == 0, t % 2 == 1 || t == T - 1);
           else compute(t % 3, t);
           // keep each step's MFMAs and adds inside the step: moved across the barrier into the next
           // step they pile up two steps' operands and chains and spill
@@ -802,6 +831,8 @@ static bool x6h_geo(const ConvF32Args& a, int mode, int bp, HaloGeo& h, int& rs)
   const long long lim = (1LL << 31) - 64;
   if ((long long)a.N * a.H * a.W * h.SC * 4 > lim || (long long)h.Pd * a.R * a.S * h.SC * 6 > lim) return false;
   if ((long long)a.N * a.P * a.Q * h.Pd * 4 > lim) return false;  // fepi_t: buffer-addressed output
+  // fepi_t reads a compact-grid residual on even-sized images only (split-K runs the generic epilogue)
+  if (mode == F_DGRAD && a.residual && a.res_sub == 2 && ((a.H | a.W) & 1) && a.split_k <= 1) return false;
   halo_layout(h);
   static const int probe = [] {
     const char* e = getenv("DDL_X6H_PROBE");

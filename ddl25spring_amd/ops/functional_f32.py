@@ -508,6 +508,12 @@ def conv_dgrad(dy, w, geom, residual=None, mask=None, out=None, bn=None, mask_bn
             kw.update(dyb_x=ptr(xb), dyb_coef=ptr(coef), dyb_out=ptr(dy_bn_out))
         else:
             dy = coef_apply(dy, xb, coef, out=dy_bn_out)
+    if residual is not None and residual_sub == 2 and (geom.H | geom.W) & 1 and uses_halo(F_DGRAD, geom) \
+            and (split_k or plan(F_DGRAD, geom)[1]) <= 1:
+        # the halo epilogue reads the compact grid on even-sized images only (conv_x6h.hip fepi_t)
+        full = torch.zeros_like(dx)
+        full[:, :, ::2, ::2] = residual
+        residual, residual_sub = full, 1
     if residual is not None:
         if residual_sub == 2:
             want = (geom.G, geom.N, (geom.H + 1) // 2, (geom.W + 1) // 2, geom.C)

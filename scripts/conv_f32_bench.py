@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--halo", type=int, default=1, help="0: never the halo kernel (conv_x6h.hip)")
     ap.add_argument("--dybn", type=int, default=0, help="dgrad: dY operand = BN backward (dy_bn), 2: + write-out")
+    ap.add_argument("--epi", default="", choices=["", "mbn", "rmb"],
+                    help="dgrad epilogue of the network: mbn = producer BN reduce + recomputed ReLU mask "
+                         "(a block's conv2), rmb = residual + mask tensor + BN reduce (a block's conv1)")
     a = ap.parse_args()
     F32.set_math(a.math)
     F32.set_halo(bool(a.halo))
@@ -41,6 +44,15 @@ def main():
     xb, coef = torch.randn_like(dy), torch.randn(g.G, 3, g.K, device=dev)
     dc = torch.empty_like(dy) if a.dybn == 2 else None
     dyb = dict(dy_bn=(xb, coef), dy_bn_out=dc) if a.dybn else {}
+    if a.epi:
+        bx = torch.randn(g.G, g.N, g.H, g.W, g.C, device=dev)
+        mean, rstd = torch.randn(g.G, g.C, device=dev) * 0.1, torch.rand(g.G, g.C, device=dev) + 0.5
+        dyb["bn"] = (bx, mean, rstd)
+        if a.epi == "mbn":
+            dyb["mask_bn"] = (torch.rand(g.G, g.C, device=dev) + 0.5, torch.randn(g.G, g.C, device=dev))
+        else:
+            dyb["residual"] = torch.randn(g.G, g.N, g.H, g.W, g.C, device=dev)
+            dyb["mask"] = torch.randn(g.G, g.N, g.H, g.W, g.C, device=dev)
     run = {"fwd": lambda: F32.conv_fwd(x, w, g, stats=F32.SlotStats()),
            "dgrad": lambda: F32.conv_dgrad(dy, w, g, **dyb),
            "wgrad": lambda: F32.conv_wgrad(dy, x, g, dw)}[a.mode]
@@ -56,7 +68,7 @@ def main():
     ms = e0.elapsed_time(e1) / a.reps
     fl = 2 * g.G * g.N * g.P * g.Q * g.K * g.R * g.S * g.C
     mode = {"fwd": F32.F_FWD, "dgrad": F32.F_DGRAD, "wgrad": F32.F_WGRAD}[a.mode]
-    print(f"{a.math} halo={a.halo} dybn={a.dybn} {a.mode} G={a.G} {a.layer}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF/s "
+    print(f"{a.math} halo={a.halo} dybn={a.dybn} epi={a.epi or '-'} {a.mode} G={a.G} {a.layer}: {ms:.4f} ms {fl / ms / 1e9:.1f} TF/s "
           f"plan={F32.plan(mode, g)}")
 
 
