@@ -202,17 +202,46 @@ __device__ __forceinline__ void fepi(const ConvF32Args& a, const FGeo& o, f4v (&
       mh[v] = (MODE == F_DGRAD && a.mask_scale && pv) ? a.mask_shift[(long long)g * Pd + p + v] : 0.f;
     }
     float s0[4] = {0.f, 0.f, 0.f, 0.f}, s1[4] = {0.f, 0.f, 0.f, 0.f};
+    // every operand load of the row is issued before any is used (a load behind a use or a
+    // branch waits out the previous one's latency: conv_x6h.hip's DGRAD epilogue ran ~4x its bytes'
+    // time that way). Lanes without an element read element 0 of the group and drop the value.
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 rr[NQ], mm[NQ], xx[NQ];
+    long long ee[NQ];
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) ee[j] = (qv[j] && pv) ? pix[j] * Pd + p : 0;
+    const long long gofs = (long long)g * a.out_gs;
+    if (a.residual && (MODE == F_FWD || a.res_sub != 2)) {
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) rr[j] = *(const float4*)(a.residual + gofs + ee[j]);
+    } else if (MODE == F_DGRAD && a.residual) {  // compact grid: even (h, w) only
+      const int Hc = (a.H + 1) >> 1, Wc = (a.W + 1) >> 1;
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) {
+        const bool on = qv[j] && pv && ((hq[j] | wqq[j]) & 1) == 0;
+        const long long re = on ? (((long long)nq_[j] * Hc + (hq[j] >> 1)) * Wc + (wqq[j] >> 1)) * Pd + p : 0;
+        rr[j] = *(const float4*)(a.residual + (long long)g * a.res_gs + re);
+        if (!on) rr[j] = z4;
+      }
+    }
+    if (MODE == F_DGRAD && a.mask) {
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) mm[j] = *(const float4*)(a.mask + gofs + ee[j]);
+    }
+    if (MODE == F_DGRAD && a.bn_x) {
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) xx[j] = *(const float4*)(a.bn_x + gofs + ee[j]);
+    }
 #pragma unroll
     for (int j = 0; j < NQ; ++j) {
       if (!qv[j] || !pv) continue;
-      const long long e = pix[j] * Pd + p;
+      const long long e = ee[j];
       float v4[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if (MODE == F_FWD) {
 #pragma unroll
         for (int v = 0; v < 4; ++v) v4[v] += bia[v];
         if (a.residual) {
-          const float4 r = *(const float4*)(a.residual + (long long)g * a.out_gs + e);
-          v4[0] += r.x; v4[1] += r.y; v4[2] += r.z; v4[3] += r.w;
+          v4[0] += rr[j].x; v4[1] += rr[j].y; v4[2] += rr[j].z; v4[3] += rr[j].w;
         }
         if (a.relu) {
 #pragma unroll
@@ -227,28 +256,17 @@ __device__ __forceinline__ void fepi(const ConvF32Args& a, const FGeo& o, f4v (&
         }
       } else {  // DGRAD
         if (a.residual) {
-          if (a.res_sub == 2) {
-            if (((hq[j] | wqq[j]) & 1) == 0) {
-              const int Hc = (a.H + 1) >> 1, Wc = (a.W + 1) >> 1;
-              const long long re = (((long long)nq_[j] * Hc + (hq[j] >> 1)) * Wc + (wqq[j] >> 1)) * Pd + p;
-              const float4 r = *(const float4*)(a.residual + (long long)g * a.res_gs + re);
-              v4[0] += r.x; v4[1] += r.y; v4[2] += r.z; v4[3] += r.w;
-            }
-          } else {
-            const float4 r = *(const float4*)(a.residual + (long long)g * a.out_gs + e);
-            v4[0] += r.x; v4[1] += r.y; v4[2] += r.z; v4[3] += r.w;
-          }
+          v4[0] += rr[j].x; v4[1] += rr[j].y; v4[2] += rr[j].z; v4[3] += rr[j].w;
         }
         if (a.mask) {
-          const float4 m = *(const float4*)(a.mask + (long long)g * a.out_gs + e);
+          const float4 m = mm[j];
           if (!(m.x > 0.f)) v4[0] = 0.f;
           if (!(m.y > 0.f)) v4[1] = 0.f;
           if (!(m.z > 0.f)) v4[2] = 0.f;
           if (!(m.w > 0.f)) v4[3] = 0.f;
         }
         if (a.bn_x) {
-          const float4 xb = *(const float4*)(a.bn_x + (long long)g * a.out_gs + e);
-          const float xs[4] = {xb.x, xb.y, xb.z, xb.w};
+          const float xs[4] = {xx[j].x, xx[j].y, xx[j].z, xx[j].w};
           if (a.mask_scale) {
 #pragma unroll
             for (int v = 0; v < 4; ++v)

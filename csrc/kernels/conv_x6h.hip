@@ -650,45 +650,6 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
 #endif
 }
 
-// Pre-split weights: FWD layout [G][K][T][C] (16-channel chunks of the input channels), DGRAD
-// layout [G][C][T][K] (16-channel chunks of the output channels), 6 bytes per element: per chunk
-// the three bf16 planes [h0..h15 | m0..m15 | l0..l15] (the LDS operand image row of conv_x6h).
-__global__ __launch_bounds__(256) void x6_split_weights_kernel(const float* __restrict__ w, char* out, int G, int K,
-                                                               int T, int C, int layout, long long w_gs,
-                                                               long long o_gs) {
-  const long long per = (long long)K * T * C / 16;  // 16-chunks per group
-  GSTRIDE_LOOP(t, (long long)G * per) {
-    const long long g = t / per, e = t - g * per;
-    const float* wg = w + g * w_gs;
-    float v[16];
-    if (layout == 0) {  // chunk (k, tap, c..c+15): contiguous in w
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float4 f = *(const float4*)(wg + e * 16 + 4 * i);
-        v[4 * i] = f.x; v[4 * i + 1] = f.y; v[4 * i + 2] = f.z; v[4 * i + 3] = f.w;
-      }
-    } else {  // chunk (c, tap, k..k+15): w[k + i][tap][c]
-      const int K16 = K / 16;
-      const long long ct = e / K16;
-      const int k = (int)(e - ct * K16) * 16;
-      const int c = (int)(ct / T), tap = (int)(ct - (long long)c * T);
-      const float* s = wg + ((long long)k * T + tap) * C + c;
-      const long long ks = (long long)T * C;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = s[i * ks];
-    }
-    char* d = out + g * o_gs + e * 96;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      s4v h, m, l;
-      split3(make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]), h, m, l);
-      *(s4v*)(d + 8 * q) = h;
-      *(s4v*)(d + 32 + 8 * q) = m;
-      *(s4v*)(d + 64 + 8 * q) = l;
-    }
-  }
-}
-
 // Many weights' split images in ONE launch (a training step's pre-split: every halo layer's FWD and
 // DGRAD images of the step's weights, functional_f32.PresplitScope) instead of one launch per conv.
 // Entry e owns blocks [blk0, blk0 + nblk); its blocks grid-stride over its 16-element chunks.
@@ -699,32 +660,61 @@ struct SplitDesc {
   int G, K, T, C, layout, blk0, nblk, pad_;
 };
 
-__device__ __forceinline__ void split_chunk(const float* __restrict__ wg, char* d, long long e, int K, int T, int C,
+// Work item u of one group -> the 16-element chunk it splits. Layout 0: chunk u (16 consecutive c
+// of one (k, tap): contiguous reads). Layout 1: items run c fastest, u = ((k16 * T) + tap) * C + c,
+// so the 16 strided reads w[k16*16 + i][tap][c] of consecutive items are coalesced; the item's
+// output chunk is e = (c * T + tap) * K/16 + k16. Every chunk is written as six 16-byte stores.
+__device__ __forceinline__ void split_chunk(const float* __restrict__ wg, char* og, long long u, int K, int T, int C,
                                             int layout) {
   float v[16];
+  long long e;
   if (layout == 0) {
+    e = u;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float4 f = *(const float4*)(wg + e * 16 + 4 * i);
+      const float4 f = *(const float4*)(wg + u * 16 + 4 * i);
       v[4 * i] = f.x; v[4 * i + 1] = f.y; v[4 * i + 2] = f.z; v[4 * i + 3] = f.w;
     }
   } else {
     const int K16 = K / 16;
-    const long long ct = e / K16;
-    const int k = (int)(e - ct * K16) * 16;
-    const int c = (int)(ct / T), tap = (int)(ct - (long long)c * T);
-    const float* s = wg + ((long long)k * T + tap) * C + c;
+    const int c = (int)(u % C);
+    const long long kt = u / C;
+    const int tap = (int)(kt % T), k16 = (int)(kt / T);
+    const float* src = wg + ((long long)k16 * 16 * T + tap) * C + c;
     const long long ks = (long long)T * C;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = s[i * ks];
+    for (int i = 0; i < 16; ++i) v[i] = src[i * ks];
+    e = ((long long)c * T + tap) * K16 + k16;
   }
+  s8v h[2], m[2], l[2];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    s4v h, m, l;
-    split3(make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]), h, m, l);
-    *(s4v*)(d + 8 * q) = h;
-    *(s4v*)(d + 32 + 8 * q) = m;
-    *(s4v*)(d + 64 + 8 * q) = l;
+  for (int q = 0; q < 2; ++q) {
+    s4v h0, m0, l0, h1, m1, l1;
+    split3(make_float4(v[8 * q], v[8 * q + 1], v[8 * q + 2], v[8 * q + 3]), h0, m0, l0);
+    split3(make_float4(v[8 * q + 4], v[8 * q + 5], v[8 * q + 6], v[8 * q + 7]), h1, m1, l1);
+    h[q] = cat44(h0, h1);
+    m[q] = cat44(m0, m1);
+    l[q] = cat44(l0, l1);
+  }
+  char* d = og + e * 96;
+  *(s8v*)(d) = h[0];
+  *(s8v*)(d + 16) = h[1];
+  *(s8v*)(d + 32) = m[0];
+  *(s8v*)(d + 48) = m[1];
+  *(s8v*)(d + 64) = l[0];
+  *(s8v*)(d + 80) = l[1];
+}
+
+// Pre-split weights: FWD layout [G][K][T][C] (16-channel chunks of the input channels), DGRAD
+// layout [G][C][T][K] (16-channel chunks of the output channels), 6 bytes per element: per chunk
+// the three bf16 planes [h0..h15 | m0..m15 | l0..l15] (the LDS operand image row of conv_x6h).
+__global__ __launch_bounds__(256) void x6_split_weights_kernel(const float* __restrict__ w, char* out, int G, int K,
+                                                               int T, int C, int layout, long long w_gs,
+                                                               long long o_gs) {
+  const long long per = (long long)K * T * C / 16;  // 16-chunks per group
+  GSTRIDE_LOOP(t, (long long)G * per) {
+    const long long g = t / per, u = t - g * per;
+    split_chunk(w + g * w_gs, out + g * o_gs, u, K, T, C, layout);
   }
 }
 
@@ -738,8 +728,8 @@ __global__ __launch_bounds__(256) void x6_split_weights_multi_kernel(const Split
   const long long per = (long long)d.K * d.T * d.C / 16;
   const long long total = (long long)d.G * per;
   for (long long t = (long long)(blockIdx.x - d.blk0) * 256 + threadIdx.x; t < total; t += (long long)d.nblk * 256) {
-    const long long g = t / per, e = t - g * per;
-    split_chunk(d.w + g * d.w_gs, d.out + g * d.o_gs + e * 96, e, d.K, d.T, d.C, d.layout);
+    const long long g = t / per, u = t - g * per;
+    split_chunk(d.w + g * d.w_gs, d.out + g * d.o_gs, u, d.K, d.T, d.C, d.layout);
   }
 }
 

@@ -43,8 +43,23 @@ struct HWGeo {
   int probe;    // timing probes (DDL_HW_PROBE, wrong results): 1 skip LDS staging, 2 skip MFMAs, 4 skip loads
 };
 
-__device__ __forceinline__ float4 hw_load(const __amdgpu_buffer_rsrc_t& rs, unsigned off) {
-  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+// Prefetch loads straight into AGPRs (inline asm: the compiler neither sees nor waits on them).
+// With compiler-visible loads the next tile's staging registers were copied into AGPRs right
+// after issue to free VGPRs for the MFMA loop — a vmcnt wait that exposed the whole load latency
+// at every tile (the DDL_HW_PROBE "no loads" probe ran 25 % faster). hw_wait() at the next tile's
+// staging is the one wait, and pins every prefetch register behind it.
+typedef int hw_rsrc __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ hw_rsrc hw_make_rsrc(const void* p, long long bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  hw_rsrc r;
+  r.x = (int)(unsigned)(a & 0xffffffffull);
+  r.y = (int)(unsigned)((a >> 32) & 0xffffull);
+  r.z = (int)bytes;
+  r.w = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ void hw_load(f4v& d, const hw_rsrc& rs, unsigned off) {
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=a"(d) : "v"(off), "s"(rs) : "memory");
 }
 
 // 8 values -> the three bf16 planes of one 16-byte LDS row segment each
@@ -73,10 +88,8 @@ __global__ __launch_bounds__(256, 1) void convx6hw_kernel(ConvF32Args a, HWGeo h
   const int K = a.K, C = a.C, H = a.H, W = a.W;
   const long long npix = (long long)a.N * H * W;
 
-  const __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.dy + (long long)g * a.dy_gs), 0, (int)(npix * K * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.x + (long long)g * a.x_gs), 0, (int)(npix * C * 4), 0x00020000);
+  const hw_rsrc rD = hw_make_rsrc(a.dy + (long long)g * a.dy_gs, npix * K * 4);
+  const hw_rsrc rX = hw_make_rsrc(a.x + (long long)g * a.x_gs, npix * C * 4);
 
   // ---- dY unit: channels k0 + 4 * (tid & 15) .. + 3, tile pixels 8 * (tid >> 4) .. + 7
   const int dkc = tid & 15, dpg = tid >> 4;
@@ -111,13 +124,13 @@ __global__ __launch_bounds__(256, 1) void convx6hw_kernel(ConvF32Args a, HWGeo h
     uoff[u] = 4 * (uu & 7) * hg.CS + xrr * hg.HCp + 8 * xc;
     uvalid[u] = uu < nxu;
   }
-  float4 rd[8], rx[NUX][8];
+  f4v rd[8], rx[NUX][8];
   unsigned xok[NUX];  // bit j: halo pixel j of the unit is a real input pixel
   auto load_tile = [&](int tile) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int p = tile * HW_TP + dpg * 8 + j;
-      rd[j] = hw_load(rD, p < npix ? (unsigned)((p * K + k0 + 4 * dkc) * 4) : HW_OOB);
+      hw_load(rd[j], rD, p < npix ? (unsigned)((p * K + k0 + 4 * dkc) * 4) : HW_OOB);
     }
     // first output row of the tile over (n, oh): tile rows are whole image rows, one (uniform)
     // division per tile; a segment past the first is a whole image (seg * SR == seg * P)
@@ -133,7 +146,7 @@ __global__ __launch_bounds__(256, 1) void convx6hw_kernel(ConvF32Args a, HWGeo h
         const int iw = 8 * uxc[u] + j - PD;
         const bool ok = uvalid[u] && n < a.N && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
         xok[u] |= (ok ? 1u : 0u) << j;
-        rx[u][j] = hw_load(rX, ok ? (unsigned)((((n * H + ih) * W + iw) * C + c0 + 4 * (tid & 7)) * 4) : HW_OOB);
+        hw_load(rx[u][j], rX, ok ? (unsigned)((((n * H + ih) * W + iw) * C + c0 + 4 * (tid & 7)) * 4) : HW_OOB);
       }
     }
   };
@@ -141,6 +154,15 @@ __global__ __launch_bounds__(256, 1) void convx6hw_kernel(ConvF32Args a, HWGeo h
   // halves of the current one, to overlap that VALU work with MFMAs, was measured slower: the
   // extra live registers push the accumulators through AGPR moves)...
   s8v sd[4][3], sx[NUX][4][3];  // sx: split at write time (registers)
+  auto hw_wait = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(rd[j]));
+#pragma unroll
+    for (int u = 0; u < NUX; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(rx[u][j]));
+  };
   auto split_tile = [&]() {
     // dY: channel ch of the unit -> row k = 4 dkc + ch, pixels 8 dpg .. + 7
 #pragma unroll
@@ -214,6 +236,7 @@ __global__ __launch_bounds__(256, 1) void convx6hw_kernel(ConvF32Args a, HWGeo h
     if (!(hg.probe & 4)) load_tile(t0);
     for (int tile = t0; tile < t1; ++tile) {
       __syncthreads();  // previous tile's fragment reads are done
+      hw_wait();
       if (!(hg.probe & 1)) {
         split_tile();
         write_tile();
@@ -304,12 +327,20 @@ __global__ __launch_bounds__(256, 1) void convx6hw_kernel(ConvF32Args a, HWGeo h
   float* dst = split_store ? a.partial + ((long long)split * a.G + g) * K * qd : a.out + (long long)g * a.out_gs;
 #pragma unroll
   for (int t = 0; t < T; ++t) {
+    // the read-modify-write's 16 loads are all issued before the first use (one at a time, each
+    // waited out, they serialised the unsplit epilogue)
+    float old[16];
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
       const int k = k0 + kb * 32 + 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
       const long long off = (long long)k * qd + (long long)t * C + c0 + (lane & 31);
-      if (split_store) dst[off] = acc[t][v];
-      else dst[off] = (a.accumulate ? dst[off] : 0.f) + a.gscale * acc[t][v];
+      old[v] = (!split_store && a.accumulate) ? dst[off] : 0.f;
+    }
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int k = k0 + kb * 32 + 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
+      const long long off = (long long)k * qd + (long long)t * C + c0 + (lane & 31);
+      dst[off] = split_store ? acc[t][v] : old[v] + a.gscale * acc[t][v];
     }
   }
 }

@@ -31,12 +31,17 @@ def main():
     ap.add_argument("--epi", default="", choices=["", "mbn", "rmb"],
                     help="dgrad epilogue of the network: mbn = producer BN reduce + recomputed ReLU mask "
                          "(a block's conv2), rmb = residual + mask tensor + BN reduce (a block's conv1)")
+    ap.add_argument("--pin", default="", help="pin a plan: 'bp/bq/split[/x6h]' (x6h = the halo kernel)")
     a = ap.parse_args()
     F32.set_math(a.math)
     F32.set_halo(bool(a.halo))
     H, C, K, R, st = LAYERS[a.layer]
     g = ConvGeom(a.G, a.N, H, H, C, K, R, R, st, (R - 1) // 2)
     dev = torch.device("cuda")
+    if a.pin:
+        f = a.pin.replace(",", "/").split("/")
+        mode_id = {"fwd": F32.F_FWD, "dgrad": F32.F_DGRAD, "wgrad": F32.F_WGRAD}[a.mode]
+        F32.set_plan(mode_id, g, int(f[0]), int(f[1]), int(f[2]), *(f[3:4]))
     x = torch.randn(g.G, g.N, g.H, g.W, g.C, device=dev)
     w = torch.randn(g.G, g.K, g.R, g.S, g.C, device=dev) * 0.05
     dy = torch.randn(g.G, g.N, g.P, g.Q, g.K, device=dev)
