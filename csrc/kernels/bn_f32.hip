@@ -393,6 +393,7 @@ struct BNFBwdArgs {  // same layout as BNBwdArgs (batchnorm.hip) + the slot coun
   int slots;
   int pad0_;
   double* fold_ws;  // two-level fold: per-slot-block partials [S / FB_SB][2][C] (null: one-level fold)
+  int* tickets;     // two-level fold in ONE launch: zeroed arrival counters [2][G][C/32] (null: two launches)
 };
 
 __device__ __forceinline__ void bnf_fold_body(const BNFBwdArgs& t, long long M, int C, double* red) {
@@ -492,6 +493,87 @@ __global__ __launch_bounds__(256) void bnf_fold_fin_kernel(BNFBwdArgs a, BNFBwdA
   t.coef[(long long)g * 3 * C + 2 * C + c] = (float)(-A * s0 * invM - B * mu);
 }
 
+// The two levels in ONE launch: every level-1 block publishes its double partials write-through
+// (relaxed agent-scope atomic stores: sc1, no release fence), drains them, and arrives on its
+// (BN, group, channel group) counter; the last block to arrive acquires and folds the partials in
+// block order — the sums and coefficients of bnf_fold_fin, bit for bit — then returns the counter
+// to zero for the next launch. One launch and one kernel boundary fewer per BN backward.
+__global__ __launch_bounds__(256) void bnf_fold_one_kernel(BNFBwdArgs a, BNFBwdArgs b, long long M, int C, int nb) {
+  const BNFBwdArgs& t = blockIdx.z ? b : a;
+  __shared__ double red[FB_SG * 64];
+  __shared__ int is_last;
+  const int g = blockIdx.y, cg = blockIdx.x / nb, sb = blockIdx.x - cg * nb;
+  const int sg = threadIdx.x >> 5, cl = threadIdx.x & 31, c = cg * 32 + cl;
+  const int S = t.slots;
+  const float* base = t.part + (long long)g * S * 2 * C;
+  constexpr int PER = FB_SB / FB_SG;
+  float x0[PER], x1[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int k = sb * FB_SB + sg + j * FB_SG;
+    const bool ok = c < C && k < S;
+    x0[j] = ok ? base[(long long)k * 2 * C + c] : 0.f;
+    x1[j] = ok ? base[(long long)k * 2 * C + C + c] : 0.f;
+  }
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    a0 += x0[j];
+    a1 += x1[j];
+  }
+  red[sg * 64 + cl] = a0;
+  red[sg * 64 + 32 + cl] = a1;
+  __syncthreads();
+  double* const wsb = t.fold_ws + (long long)g * nb * 2 * C;
+  if (sg == 0 && c < C) {
+    double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < FB_SG; ++k) {
+      t0 += red[k * 64 + cl];
+      t1 += red[k * 64 + 32 + cl];
+    }
+    double* w = wsb + (long long)sb * 2 * C;
+    __hip_atomic_store((unsigned long long*)(w + c), __double_as_longlong(t0), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((unsigned long long*)(w + C + c), __double_as_longlong(t1), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the arrival
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int* ctr = t.tickets + ((long long)blockIdx.z * gridDim.y + g) * ((C + 31) / 32) + cg;
+    const int prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = prev == nb - 1;
+    if (is_last) {
+      __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (!is_last || sg != 0 || c >= C) return;
+  double s0 = 0.0, s1 = 0.0;
+  for (int k = 0; k < nb; ++k) {
+    s0 += wsb[(long long)k * 2 * C + c];
+    s1 += wsb[(long long)k * 2 * C + C + c];
+  }
+  const int i = g * C + c;
+  const long long po = (long long)g * t.gs_param + c;
+  const float mu = t.mean[i], rs = t.rstd[i];
+  const float ga = t.gamma ? t.gamma[po] : 1.f;
+  if (t.dbeta) t.dbeta[po] = t.dbeta[po] + (float)s0;
+  if (t.dgamma) t.dgamma[po] = t.dgamma[po] + (float)s1;
+  const double invM = 1.0 / (double)M;
+  const double A = (double)ga * rs;
+  const double B = -A * rs * s1 * invM;
+  t.coef[(long long)g * 3 * C + c] = (float)A;
+  t.coef[(long long)g * 3 * C + C + c] = (float)B;
+  t.coef[(long long)g * 3 * C + 2 * C + c] = (float)(-A * s0 * invM - B * mu);
+}
+
+// ints of arrival counters a one-launch fold of up to two BNs with C channels and G groups uses
+DDL_API long long ddl_bnf_fold_tickets(int C, int G) { return 2LL * G * ((C + 31) / 32); }
+
 // doubles of fold workspace a BN backward with S slots needs (two-level fold)
 DDL_API long long ddl_bnf_fold_ws(int S, int C, int G) {
   const int nb = (S + FB_SB - 1) / FB_SB;
@@ -575,8 +657,12 @@ DDL_API int ddl_bnf_backward(const float* dy, const float* ymask, const BNFBwdAr
     // one grid for both BNs: nb of the larger; blocks past a BN's own slots add exact zeros
     const int sm = two && b.slots > a.slots ? b.slots : a.slots;
     const int nb = (sm + FB_SB - 1) / FB_SB;
-    hipLaunchKernelGGL(bnf_fold_part_kernel, dim3((C + 31) / 32 * nb, G, 1 + two), dim3(256), 0, s, a, b, C, nb);
-    hipLaunchKernelGGL(bnf_fold_fin_kernel, dim3((C + 255) / 256, G, 1 + two), dim3(256), 0, s, a, b, M, C, nb);
+    if (a.tickets) {
+      hipLaunchKernelGGL(bnf_fold_one_kernel, dim3((C + 31) / 32 * nb, G, 1 + two), dim3(256), 0, s, a, b, M, C, nb);
+    } else {
+      hipLaunchKernelGGL(bnf_fold_part_kernel, dim3((C + 31) / 32 * nb, G, 1 + two), dim3(256), 0, s, a, b, C, nb);
+      hipLaunchKernelGGL(bnf_fold_fin_kernel, dim3((C + 255) / 256, G, 1 + two), dim3(256), 0, s, a, b, M, C, nb);
+    }
   } else {
     hipLaunchKernelGGL(bnf_fold_kernel, dim3((C + 31) / 32, G, 1 + two), dim3(FOLD_T), 0, s, a, b, M, C);
   }

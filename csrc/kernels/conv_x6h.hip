@@ -63,6 +63,8 @@ struct HaloGeo {
   int SH, SW, SC;  // source (X for FWD, dY for DGRAD) height, width, channels
   int Pd;       // output channels (K for FWD, C for DGRAD)
   int ROWB, SEGB, HBYTES;  // halo row / segment strides, image bytes
+  int OWr;      // real output width (< 1 << lgW: rows padded to the power of two, PADW instances)
+  int Qv;       // virtual output pixels N * OH * (1 << lgW) (the tiles run over these)
   int probe;    // timing probes (DDL_X6H_PROBE, WRONG results): 1 no weight DMA, 2 no halo loads, 4 no
                 // fragment reads / MFMAs, 8 no epilogue, 16 no main-loop barriers, 32 no halo split / LDS stores, 64 return at
                 // once, 128 no main loop
@@ -127,15 +129,20 @@ __device__ __forceinline__ void bst1(float v, const __amdgpu_buffer_rsrc_t& rs, 
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rs, off, soff, 0);
 }
 
-template <int MODE, int BP>
-__device__ __forceinline__ void fepi_t(const ConvF32Args& a, const FGeo& o, f16v (&acc)[BP / 64][2], float* red) {
+// PADW: the image rows are padded to 1 << lgW pixels (OWr real): o.Qd counts VIRTUAL pixels, a
+// pixel q is real when (q & (2^lgW - 1)) < OWr and sits at (q >> lgW) * OWr + that column; element
+// offsets are per lane (no scalar row offset) and padding pixels are neither stored nor counted.
+template <int MODE, int BP, bool PADW>
+__device__ __forceinline__ void fepi_t(const ConvF32Args& a, const FGeo& o, f16v (&acc)[BP / 64][2], float* red,
+                                       int lgW, int OWr) {
   constexpr int WP = BP / 2, TI = WP / 32, TJ = 2;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wp = wid >> 1, wq = wid & 1;
   const int g = o.g, Pd = o.Pd;
   const bool want_stats = a.stats != nullptr;
   const bool dg_stats = MODE == F_DGRAD && want_stats && a.bn_x;
   const long long gofs = (long long)g * a.out_gs;
-  const long long nbytes = (long long)o.Qd * Pd * 4;  // one group's output (host: < 2^31)
+  const long long nreal = PADW ? (long long)(o.Qd >> lgW) * OWr : (long long)o.Qd;
+  const long long nbytes = nreal * Pd * 4;  // one group's output (host: < 2^31)
   const __amdgpu_buffer_rsrc_t rO = rsrc_of(a.out + gofs, nbytes);
   const bool res_full = a.residual && (MODE == F_FWD || a.res_sub != 2);
   const __amdgpu_buffer_rsrc_t rR = rsrc_of(res_full ? a.residual + gofs : a.out, nbytes);
@@ -147,14 +154,23 @@ __device__ __forceinline__ void fepi_t(const ConvF32Args& a, const FGeo& o, f16v
   // compact-grid residual (res_sub 2, the stride-2 shortcut's dX on even pixels)
   const __amdgpu_buffer_rsrc_t rC = rsrc_of(a.residual && !res_full ? a.residual + (long long)g * a.res_gs : a.out,
                                             nbytes / 4);
-  int lgw = 0;
-  while ((1 << lgw) < a.W) ++lgw;
+  const int Wc = (a.W + 1) >> 1;  // compact grid width
+  const int wmask = (1 << lgW) - 1;
+  // per element (e = 16 tj + r): virtual pixel qb + dq(e), its real index (PADW) and validity
+  auto dq_of = [](int e) { return (e >> 4) * 32 + 8 * ((e & 15) >> 2) + (e & 3); };
+  auto real_of = [&](int q) { return PADW ? (q >> lgW) * OWr + (q & wmask) : q; };
+  auto valid_q = [&](int q) { return (full || q < o.Qd) && (!PADW || (q & wmask) < OWr); };
 #pragma unroll
   for (int ti = 0; ti < TI; ++ti) {
     const int pl = wp * WP + ti * 32 + (lane & 31);
     const int p = o.p0 + pl;
     const bool pv = p < Pd;
     const unsigned vo = pv ? ((unsigned)qb * (unsigned)Pd + (unsigned)p) * 4u : OOB;
+    // PADW: element e's byte offset (vector), padding pixels out of range
+    auto voff = [&](int e) -> unsigned {
+      const int q = qb + dq_of(e);
+      return (pv && valid_q(q)) ? ((unsigned)real_of(q) * (unsigned)Pd + (unsigned)p) * 4u : OOB;
+    };
     float bia = 0.f, bm = 0.f, br = 0.f, ms = 0.f, mh = 0.f;
     if (MODE == F_FWD && a.bias && pv) bia = a.bias[(long long)g * a.bias_gs + p];
     if (MODE == F_DGRAD && a.bn_x && pv) {
@@ -174,35 +190,43 @@ __device__ __forceinline__ void fepi_t(const ConvF32Args& a, const FGeo& o, f16v
 #pragma unroll
     for (int b0 = 0; b0 < TJ * 16; b0 += EB) {
       float rv[EB], mv[EB], xv[EB];
-      auto soff = [&](int e) { return (unsigned)((e >> 4) * 32 + 8 * ((e & 15) >> 2) + (e & 3)) * rowb; };
+      unsigned ve[PADW ? EB : 1];
+      if constexpr (PADW) {
+#pragma unroll
+        for (int i = 0; i < EB; ++i) ve[i] = voff(b0 + i);
+      }
+      // element i's (vector, scalar) offsets: scalar row offset on the dense layout, per-lane on PADW
+      auto ld = [&](const __amdgpu_buffer_rsrc_t& rs, int i) {
+        if constexpr (PADW) return bld1(rs, ve[i], 0u);
+        else return bld1(rs, vo, (unsigned)dq_of(b0 + i) * rowb);
+      };
       if (res_full) {
 #pragma unroll
-        for (int i = 0; i < EB; ++i) rv[i] = bld1(rR, vo, soff(b0 + i));
+        for (int i = 0; i < EB; ++i) rv[i] = ld(rR, i);
       } else if (MODE == F_DGRAD && a.residual) {
-        // compact grid (res_sub 2, H and W even: host-checked): pixel (t = n*H + h, w) reads compact
-        // element ((t >> 1) * W/2 + (w >> 1)) when t and w are both even, else nothing (OOB)
+        // compact grid (res_sub 2, H even: host-checked): pixel (t = n*H + h, w) reads compact element
+        // ((t >> 1) * ceil(W/2) + (w >> 1)) when t and w are both even, else nothing (OOB)
 #pragma unroll
         for (int i = 0; i < EB; ++i) {
-          const int e = b0 + i, q = qb + (e >> 4) * 32 + 8 * ((e & 15) >> 2) + (e & 3);
-          const int t = q >> lgw, w = q & (a.W - 1);
-          const unsigned ci = (unsigned)(((t >> 1) << (lgw - 1)) + (w >> 1));
-          rv[i] = bld1(rC, (((t | w) & 1) == 0 && pv) ? (ci * (unsigned)Pd + (unsigned)p) * 4u : OOB, 0u);
+          const int q = qb + dq_of(b0 + i);
+          const int t = q >> lgW, w = q & wmask;
+          const unsigned ci = (unsigned)((t >> 1) * Wc + (w >> 1));
+          rv[i] = bld1(rC, (((t | w) & 1) == 0 && pv && valid_q(q)) ? (ci * (unsigned)Pd + (unsigned)p) * 4u : OOB, 0u);
         }
       }
       if (MODE == F_DGRAD && a.mask) {
 #pragma unroll
-        for (int i = 0; i < EB; ++i) mv[i] = bld1(rM, vo, soff(b0 + i));
+        for (int i = 0; i < EB; ++i) mv[i] = ld(rM, i);
       }
       if (MODE == F_DGRAD && a.bn_x) {
 #pragma unroll
-        for (int i = 0; i < EB; ++i) xv[i] = bld1(rX, vo, soff(b0 + i));
+        for (int i = 0; i < EB; ++i) xv[i] = ld(rX, i);
       }
 #pragma unroll
       for (int i = 0; i < EB; ++i) {
         const int e = b0 + i, tj = e >> 4, r = e & 15;
-        const int dq = tj * 32 + 8 * (r >> 2) + (r & 3);
-        const unsigned so = (unsigned)dq * rowb;
-        const bool ok = pv && (full || qb + dq < o.Qd);
+        const int dq = dq_of(e);
+        const bool ok = pv && valid_q(qb + dq);
         float v = acc[ti][tj][r];
         if (MODE == F_FWD) {
           v += bia;
@@ -224,7 +248,8 @@ __device__ __forceinline__ void fepi_t(const ConvF32Args& a, const FGeo& o, f16v
             }
           }
         }
-        bst1(v, rO, vo, so);
+        if constexpr (PADW) bst1(v, rO, ve[i], 0u);
+        else bst1(v, rO, vo, (unsigned)dq * rowb);
       }
     }
     if ((MODE == F_FWD && want_stats) || dg_stats) {
@@ -239,7 +264,7 @@ __device__ __forceinline__ void fepi_t(const ConvF32Args& a, const FGeo& o, f16v
   if (!want_stats || (MODE == F_DGRAD && !a.bn_x)) return;
   if constexpr (MODE == F_FWD) {
     // (sum, M2 about the tile mean), merged across tiles with Chan's formula in bnf_finalize
-    const int nq = min(BQH, o.Qd - o.q0);
+    const int nq = PADW ? (min(BQH, o.Qd - o.q0) >> lgW) * OWr : min(BQH, o.Qd - o.q0);  // valid pixels
     __syncthreads();
 #pragma unroll
     for (int ti = 0; ti < TI; ++ti) {
@@ -251,9 +276,8 @@ __device__ __forceinline__ void fepi_t(const ConvF32Args& a, const FGeo& o, f16v
       for (int tj = 0; tj < TJ; ++tj)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int dq = tj * 32 + 8 * (r >> 2) + (r & 3);
           const float d = acc[ti][tj][r] - mu;
-          m2 += (pv && (full || qb + dq < o.Qd)) ? d * d : 0.f;
+          m2 += (pv && valid_q(qb + dq_of(tj * 16 + r))) ? d * d : 0.f;
         }
       m2 += __shfl_xor(m2, 32, 64);
       if (lane < 32) red[(wq * BP + pl) * 2 + 1] = m2;
@@ -268,7 +292,7 @@ __device__ __forceinline__ void fepi_t(const ConvF32Args& a, const FGeo& o, f16v
   }
 }
 
-template <int MODE, int BP, int RS, int HB>
+template <int MODE, int BP, int RS, int HB, bool PADW>
 __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo hg) {
   constexpr int T = RS * RS;                 // taps
   constexpr int PD = (RS - 1) / 2;           // pad
@@ -289,7 +313,8 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
   const int u = xcd_remap(lin, gx * gy * gz);
   const int bx = u % gx, by = (u / gx) % gy, g = u / (gx * gy);
   if (hg.probe & 64) return;  // launch / dispatch cost only
-  const FGeo o = fgeo<MODE, BP, BQH>(a, bx, by, g, gy);
+  FGeo o = fgeo<MODE, BP, BQH>(a, bx, by, g, gy);
+  o.Qd = hg.Qv;  // tiles run over the virtual (row-padded) pixels; == N*P*Q unless PADW
   const bool split_store = a.split_k > 1;
   if (o.q0 >= o.Qd || o.p0 >= o.Pd) {
     if (!split_store) fzero_slot<MODE, BP>(a, o);
@@ -344,7 +369,7 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
       const int sr = r0 + hi - PD, sc = hj - PD;
       if (n < a.N && (unsigned)sr < (unsigned)hg.SH && (unsigned)sc < (unsigned)hg.SW)
         hoff[i] = (unsigned)((((long long)n * hg.SH + sr) * hg.SW + sc) * SC + ch * 4) * 4u;
-      if (hoff[i] != OOB && hi >= PD && hi < PD + hg.SR && hj >= PD && hj < PD + (1 << hg.lgW)) own |= 1u << i;
+      if (hoff[i] != OOB && hi >= PD && hi < PD + hg.SR && hj >= PD && hj < PD + hg.OWr) own |= 1u << i;
       hlds[i] = seg * hg.SEGB + hi * hg.ROWB + hj * HSTR + ch * 8;
     }
   }
@@ -603,6 +628,7 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
     return;
   }
 #if !X6H_TRANSPOSE
+  static_assert(!PADW, "row-padded halo tiles need the transposed epilogue");
   f4v quad[Lay32<BP, BQH>::NPQ][Lay32<BP, BQH>::NQ];
 #pragma unroll
   for (int ti = 0; ti < TI; ++ti)
@@ -646,7 +672,7 @@ __global__ __launch_bounds__(256, 2) void convx6h_kernel(ConvF32Args a, HaloGeo 
     }
     return;
   }
-  fepi_t<MODE, BP>(a, o, acc, (float*)smem);
+  fepi_t<MODE, BP, PADW>(a, o, acc, (float*)smem, hg.lgW, hg.OWr);
 #endif
 }
 
@@ -793,10 +819,13 @@ static bool x6h_geo(const ConvF32Args& a, int mode, int bp, HaloGeo& h, int& rs)
   if (a.stride != 1 || a.R != a.S || (a.R != 1 && a.R != 3) || a.pad != (a.R - 1) / 2) return false;
   if (a.P != a.H || a.Q != a.W) return false;
   rs = a.R;
-  const int OH = a.P, OW = a.Q;
-  if (OW < 4 || OW > BQH || (OW & (OW - 1))) return false;
+  const int OH = a.P, OWr = a.Q;
+  if (OWr < 4 || OWr > BQH) return false;
   int lg = 0;
-  while ((1 << lg) < OW) ++lg;
+  while ((1 << lg) < OWr) ++lg;
+  const int OW = 1 << lg;  // rows padded to the power of two (PADW instances when OW != OWr)
+  // a padded row's tile cannot be split over K: the split-K epilogue tiles the REAL pixels
+  if (OW != OWr && a.split_k > 1) return false;
   const int TR = BQH / OW;
   int SR;
   if (TR <= OH) {
@@ -807,6 +836,8 @@ static bool x6h_geo(const ConvF32Args& a, int mode, int bp, HaloGeo& h, int& rs)
     SR = OH;
   }
   h.lgW = lg;
+  h.OWr = OWr;
+  h.Qv = a.N * OH * OW;
   h.SR = SR;
   h.HR = SR + a.R - 1;
   h.HC = OW + a.S - 1;
@@ -821,8 +852,8 @@ static bool x6h_geo(const ConvF32Args& a, int mode, int bp, HaloGeo& h, int& rs)
   const long long lim = (1LL << 31) - 64;
   if ((long long)a.N * a.H * a.W * h.SC * 4 > lim || (long long)h.Pd * a.R * a.S * h.SC * 6 > lim) return false;
   if ((long long)a.N * a.P * a.Q * h.Pd * 4 > lim) return false;  // fepi_t: buffer-addressed output
-  // fepi_t reads a compact-grid residual on even-sized images only (split-K runs the generic epilogue)
-  if (mode == F_DGRAD && a.residual && a.res_sub == 2 && ((a.H | a.W) & 1) && a.split_k <= 1) return false;
+  // fepi_t reads a compact-grid residual on even-height images only (split-K: the generic epilogue)
+  if (mode == F_DGRAD && a.residual && a.res_sub == 2 && (a.H & 1) && a.split_k <= 1) return false;
   halo_layout(h);
   static const int probe = [] {
     const char* e = getenv("DDL_X6H_PROBE");
@@ -835,9 +866,9 @@ static bool x6h_geo(const ConvF32Args& a, int mode, int bp, HaloGeo& h, int& rs)
   return true;
 }
 
-template <int MODE, int BP, int RS, int HB>
+template <int MODE, int BP, int RS, int HB, bool PADW>
 static int launch_x6h(ConvF32Args a, const HaloGeo& h, hipStream_t s) {
-  const long long Pd = h.Pd, Qd = (long long)a.N * a.P * a.Q;
+  const long long Pd = h.Pd, Qd = h.Qv;
   const long long ntp = (Pd + BP - 1) / BP, ntq = (Qd + BQH - 1) / BQH;
   a.slots = (int)ntq;
   const int split = a.split_k < 1 ? 1 : a.split_k;
@@ -847,7 +878,7 @@ static int launch_x6h(ConvF32Args a, const HaloGeo& h, hipStream_t s) {
     if (!a.partial || need > a.partial_cap) return (int)hipErrorInvalidValue;
   }
   const dim3 grid((unsigned)(ntp * ntq), (unsigned)split, (unsigned)a.G);
-  hipLaunchKernelGGL((convx6h_kernel<MODE, BP, RS, HB>), grid, dim3(256), 0, s, a, h);
+  hipLaunchKernelGGL((convx6h_kernel<MODE, BP, RS, HB, PADW>), grid, dim3(256), 0, s, a, h);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || split == 1) return (int)e;
   hipLaunchKernelGGL((convf32_splitk_epilogue<MODE, BP, BQH>), dim3((unsigned)(ntp * ntq), 1, a.G), dim3(256), 0,
@@ -855,15 +886,29 @@ static int launch_x6h(ConvF32Args a, const HaloGeo& h, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+template <int MODE, int HB, bool PADW>
+static int dispatch_rs(const ConvF32Args& a, int bp, int rs, const HaloGeo& h, hipStream_t s) {
+  if (rs == 3)
+    return bp == 128 ? launch_x6h<MODE, 128, 3, HB, PADW>(a, h, s) : launch_x6h<MODE, 64, 3, HB, PADW>(a, h, s);
+  return bp == 128 ? launch_x6h<MODE, 128, 1, HB, PADW>(a, h, s) : launch_x6h<MODE, 64, 1, HB, PADW>(a, h, s);
+}
 template <int MODE, int HB>
 static int dispatch_hb(const ConvF32Args& a, int bp, int rs, const HaloGeo& h, hipStream_t s) {
-  if (rs == 3) return bp == 128 ? launch_x6h<MODE, 128, 3, HB>(a, h, s) : launch_x6h<MODE, 64, 3, HB>(a, h, s);
-  return bp == 128 ? launch_x6h<MODE, 128, 1, HB>(a, h, s) : launch_x6h<MODE, 64, 1, HB>(a, h, s);
+  return h.OWr != (1 << h.lgW) ? dispatch_rs<MODE, HB, true>(a, bp, rs, h, s) : dispatch_rs<MODE, HB, false>(a, bp, rs, h, s);
 }
 static bool x6h_large(const HaloGeo& h) { return h.HBYTES > HBSMALL || h.HP > 208; }
 template <int MODE>
 static int dispatch_x6h(const ConvF32Args& a, int bp, int rs, const HaloGeo& h, hipStream_t s) {
   return x6h_large(h) ? dispatch_hb<MODE, HBLARGE>(a, bp, rs, h, s) : dispatch_hb<MODE, HBSMALL>(a, bp, rs, h, s);
+}
+
+// Statistics / BN-reduce slots of a halo launch (= its 128-pixel tiles per group: over the
+// row-padded pixels when the width is not a power of two), -1 when the kernel declines it
+DDL_API long long ddl_x6h_slots(const ConvF32Args* ap, int mode) {
+  HaloGeo h;
+  int rs;
+  if (!x6h_geo(*ap, mode, 64, h, rs)) return -1;
+  return ((long long)h.Qv + BQH - 1) / BQH;
 }
 
 // Can the halo kernel run this (mode, geometry) with BP = (cfg & 0xff) * 16?

@@ -85,7 +85,7 @@ class ConvF32Args(ctypes.Structure):  # conv_f32.hip
 class BNFBwdArgs(ctypes.Structure):  # bn_f32.hip
     _fields_ = [("x", vp), ("mean", vp), ("rstd", vp), ("gamma", vp), ("dgamma", vp), ("dbeta", vp),
                 ("part", vp), ("coef", vp), ("dx", vp), ("gs_param", i64), ("slots", i32), ("pad0_", i32),
-                ("fold_ws", vp)]
+                ("fold_ws", vp), ("tickets", vp)]
 
 
 class HeadFArgs(ctypes.Structure):  # bn_f32.hip
@@ -180,6 +180,7 @@ _SIGS.update({
     # conv_x6h.hip
     "ddl_x6h": [ctypes.POINTER(ConvF32Args), i32, i32, vp],
     "ddl_x6h_ok": [ctypes.POINTER(ConvF32Args), i32, i32],
+    "ddl_x6h_slots": [ctypes.POINTER(ConvF32Args), i32],
     "ddl_x6hw": [ctypes.POINTER(ConvF32Args), vp],
     "ddl_x6hw_ok": [ctypes.POINTER(ConvF32Args)],
     "ddl_x6hw_tiles": [ctypes.POINTER(ConvF32Args)],
@@ -201,10 +202,11 @@ _SIGS.update({
     "ddl_headf_train": [ctypes.POINTER(HeadFArgs), vp],
     "ddl_bnf_channel_sum": [vp, vp, i64, vp, i64, i32, i32, vp],
     "ddl_bnf_fold_ws": [i32, i32, i32],
+    "ddl_bnf_fold_tickets": [i32, i32],
     "ddl_bnf_coef_apply": [vp, vp, vp, vp, i64, i32, i32, vp],
 })
 _RESTYPES = {"ddl_convf32_slots": ctypes.c_longlong, "ddl_convf32_workspace": ctypes.c_longlong,
-             "ddl_x6h_workspace": ctypes.c_longlong, "ddl_bnf_fold_ws": ctypes.c_longlong,
+             "ddl_x6h_workspace": ctypes.c_longlong, "ddl_x6h_slots": ctypes.c_longlong, "ddl_bnf_fold_ws": ctypes.c_longlong, "ddl_bnf_fold_tickets": ctypes.c_longlong,
              "ddl_gram_f32_workspace": ctypes.c_longlong}
 
 _OPTIONAL_SIGS: dict[str, list] = {}

@@ -71,6 +71,8 @@ def ensure_workspace(device) -> None:
             # WGRAD split-K arrival counters (zero between launches: the folding workgroup resets
             # its own), one set per role since the two streams' WGRADs may run concurrently
             _WS[key + ":tickets"] = torch.zeros(TICKETS_CAP, dtype=torch.int32, device=device)
+    if torch.device(device).type == "cuda" and _dev_key(device) not in _TICKETS:
+        _TICKETS[_dev_key(device)] = torch.zeros(TICKETS_N, dtype=torch.int32, device=device)
 
 
 # per-(group, phase, tile) counters of the in-kernel split-K fold (the last-arriving slice's
@@ -138,7 +140,13 @@ def set_halo(on: bool) -> None:
         _PLANS.clear()
 
 
-HALO_MIN_W = int(os.environ.get("DDL_F32_HALO_MIN_W", "8"))  # narrowest image the halo FWD / DGRAD takes by default
+# narrowest image the halo FWD / DGRAD takes by default: 4x4 lost to conv_f32.hip in round 4
+# (profiles/x6h_layers_r4.txt) and wins since the round-5 epilogue (c512 at 8 clients, BP 64:
+# FWD 406 vs 436 us, DGRAD 417 vs 489, profiles/x6h_l4_r5.txt)
+HALO_MIN_W = int(os.environ.get("DDL_F32_HALO_MIN_W", "4"))
+# widths that are not a power of two (ResNet-50's 56 / 28) run with rows padded to one
+# (DDL_F32_HALO_PADW=0: conv_f32.hip); their tiles are never split over K
+HALO_PADW = [os.environ.get("DDL_F32_HALO_PADW", "1") != "0"]
 
 
 def halo_ok(mode: int, g, auto: bool = False) -> bool:
@@ -148,10 +156,15 @@ def halo_ok(mode: int, g, auto: bool = False) -> bool:
         return False
     if g.P != g.H or g.Q != g.W:
         return False
-    OH, OW = g.P, g.Q
-    if OW < 4 or OW > 128 or OW & (OW - 1):
+    OH, OWr = g.P, g.Q
+    if OWr < 4 or OWr > 128:
         return False
-    if auto and OW < HALO_MIN_W:  # 4x4: measured slower than conv_f32.hip (profiles/x6h_layers_r4.txt)
+    if auto and OWr < HALO_MIN_W:
+        return False
+    OW = 1 << (OWr - 1).bit_length()  # rows padded to a power of two (conv_x6h.hip PADW)
+    if OW != OWr and (not HALO_PADW[0] or (auto and g.R == 1)):
+        # padded 1x1 convs stay on conv_f32.hip's tuned plans by default: a 1x1 conv has no taps
+        # to reuse the staged tile (the FLAT1X1 finding, profiles/r50_flat1x1_r4m.txt)
         return False
     TR = 128 // OW
     if TR <= OH:
@@ -299,7 +312,8 @@ def _halo_plan(mode: int, geom) -> tuple[int, int]:
     tiles = -(-Pd // bp) * -(-Qd // 128) * geom.G
     nch = SC // 16
     split = 1
-    while tiles * split < TARGET_WG and nch >= split * 2 * 4 and split < 32:
+    padded = geom.Q & (geom.Q - 1) != 0
+    while not padded and tiles * split < TARGET_WG and nch >= split * 2 * 4 and split < 32:
         split *= 2
     return cfg_of(bp, 128) | X6_BIT | HALO_BIT, split
 
@@ -460,7 +474,19 @@ def presplit_scope(owner) -> "PresplitScope | contextlib.nullcontext":
 
 def _slots(a, mode: int, geom) -> int:
     cfg, _ = plan(mode, geom)
+    if uses_halo(mode, geom):  # the halo kernel's own tiles (row-padded widths included)
+        return int(_lib.kernels().ddl_x6h_slots(ctypes.byref(a), mode))
     return int(_lib.kernels().ddl_convf32_slots(ctypes.byref(a), mode, _cfg(cfg)))
+
+
+def slot_rows(mode: int, geom) -> int:
+    """Output pixels per statistics slot of a launch: the tile's BQ, or on the halo kernel with a
+    row-padded width its real pixels, (128 / padded width) rows of W."""
+    cfg, _ = plan(mode, geom)
+    bq = ((_cfg(cfg) >> 8) & 0xFF) * 16
+    if uses_halo(mode, geom) and geom.Q & (geom.Q - 1):
+        return bq // (1 << (geom.Q - 1).bit_length()) * geom.Q
+    return bq
 
 
 def _xform(in_bn):
@@ -484,7 +510,7 @@ def conv_fwd(x, w, geom, bias=None, relu=False, stats=None, out=None, residual=N
         a.stats = ptr(st)
         if isinstance(stats, SlotStats):
             stats.t = st
-            stats.rows = ((_cfg(plan(F_FWD, geom)[0]) >> 8) & 0xFF) * 16  # the tile's BQ
+            stats.rows = slot_rows(F_FWD, geom)
         else:
             raise TypeError("fp32 conv statistics go to a SlotStats (Fn.stats_buffer(..., like=x))")
     _launch(a, F_FWD, geom, x.device, split_k)
@@ -508,9 +534,9 @@ def conv_dgrad(dy, w, geom, residual=None, mask=None, out=None, bn=None, mask_bn
             kw.update(dyb_x=ptr(xb), dyb_coef=ptr(coef), dyb_out=ptr(dy_bn_out))
         else:
             dy = coef_apply(dy, xb, coef, out=dy_bn_out)
-    if residual is not None and residual_sub == 2 and (geom.H | geom.W) & 1 and uses_halo(F_DGRAD, geom) \
+    if residual is not None and residual_sub == 2 and geom.H & 1 and uses_halo(F_DGRAD, geom) \
             and (split_k or plan(F_DGRAD, geom)[1]) <= 1:
-        # the halo epilogue reads the compact grid on even-sized images only (conv_x6h.hip fepi_t)
+        # the halo epilogue reads the compact grid on even-height images only (conv_x6h.hip fepi_t)
         full = torch.zeros_like(dx)
         full[:, :, ::2, ::2] = residual
         residual, residual_sub = full, 1
@@ -678,12 +704,42 @@ def _bwd_args(x, mean, rstd, gamma, dgamma, dbeta, part, dx, fold_slots: int = 0
     if FOLD2[0] and S > 0:
         fws = torch.empty(int(_lib.kernels().ddl_bnf_fold_ws(S, C, G)), dtype=torch.float64, device=x.device)
         t.fold_ws = fws.data_ptr()
+        if FOLD1L[0] and x.is_cuda:
+            t.tickets = _fold_tickets(x.device, int(_lib.kernels().ddl_bnf_fold_tickets(C, G)))
     t._keep = (coef, fws)  # scratch that must outlive the launch (its memory would be reused otherwise)
     return t
 
 
-# BN-backward coefficient fold: two small-block levels (DDL_F32_FOLD2=0: the one-level fold)
+# BN-backward coefficient fold: two small-block levels (DDL_F32_FOLD2=0: the one-level fold), in
+# ONE launch whose last-arriving block folds the level-1 partials (DDL_F32_FOLD1L=0: two launches)
 FOLD2 = [os.environ.get("DDL_F32_FOLD2", "1") != "0"]
+FOLD1L = [os.environ.get("DDL_F32_FOLD1L", "1") != "0"]
+_TICKETS: dict = {}
+
+
+TICKETS_N = 1 << 16  # >= 2 * G * C / 32 of any BN (G = 64 clients at C = 512: 2048)
+
+
+def _dev_key(device) -> str:
+    d = torch.device(device)
+    return f"cuda:{d.index if d.index is not None else torch.cuda.current_device()}"
+
+
+def _fold_tickets(device, n: int) -> int:
+    """Zeroed arrival counters of the one-launch fold, one buffer per device: every fold returns
+    its counters to zero, so the BN backwards (all on the step's main stream) share them.
+    Allocated eagerly with the split-K workspace (a first use inside a graph capture raises)."""
+    key = _dev_key(device)
+    buf = _TICKETS.get(key)
+    if buf is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("fp32 BN fold counters first requested inside a graph capture: run one eager "
+                               "step (or functional_f32.ensure_workspace) before capturing")
+        buf = torch.zeros(TICKETS_N, dtype=torch.int32, device=device)
+        _TICKETS[key] = buf
+    if n > buf.numel():
+        raise ValueError(f"BN fold needs {n} counters (> {buf.numel()})")
+    return buf.data_ptr()
 
 
 def bn_backward(dy, ymask, x, mean, rstd, gamma, dgamma=None, dbeta=None, emit_dym=False, part=None):

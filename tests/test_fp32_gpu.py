@@ -270,6 +270,43 @@ def test_bn_f32_backward2_and_reduce_part(cuda):
     _close(dxb, refs[1], rel=2e-5)
 
 
+@pytest.mark.parametrize("G,M,C", [(3, 300, 128), (8, 102400, 64), (1, 1600, 512)])
+def test_bn_f32_one_launch_fold_equals_two_launch(cuda, monkeypatch, G, M, C):
+    """bnf_fold_one_kernel (last-arriving block folds the level-1 partials) is bit for bit the two-launch
+    fold (bnf_fold_part + bnf_fold_fin), for one BN and for two sharing dy; its arrival counters are
+    back at zero after every launch (the next call would otherwise mis-detect its last block)."""
+    from ddl25spring_amd.ops import functional_f32 as F32
+    torch.manual_seed(9)
+    dy = torch.randn(G, M, C, device=cuda)
+    bns = []
+    for _ in range(2):
+        c = torch.randn(G, M, C, device=cuda)
+        mean, var = c.mean(1), c.var(1, unbiased=False)
+        part = Fn.bn_bwd_reduce_part(dy, None, c, mean, 1 / torch.sqrt(var + 1e-5))
+        bns.append((c, mean, 1 / torch.sqrt(var + 1e-5), torch.rand(G, C, device=cuda) + 0.5, part))
+
+    def run():
+        outs = []
+        for c, mean, rstd, gamma, part in bns:  # one BN
+            dg, db = torch.zeros(G, C, device=cuda), torch.zeros(G, C, device=cuda)
+            coef = F32.bn_backward_coef(dy, c, mean, rstd, gamma, dg, db, part=part)
+            outs += [coef, dg, db]
+        two = [(c, mean, rstd, gamma, torch.zeros(G, C, device=cuda), torch.zeros(G, C, device=cuda), part)
+               for c, mean, rstd, gamma, part in bns]
+        outs += list(Fn.bn_backward2(dy, two[0], two[1])) + [t[4] for t in two] + [t[5] for t in two]
+        torch.cuda.synchronize()
+        return outs
+
+    monkeypatch.setattr(F32, "FOLD1L", [True])
+    one = run()
+    F32.ensure_workspace(cuda)
+    assert int(F32._TICKETS[F32._dev_key(cuda)].abs().sum()) == 0
+    monkeypatch.setattr(F32, "FOLD1L", [False])
+    two = run()
+    for a, b in zip(one, two):
+        assert torch.equal(a, b)
+
+
 def test_head_f32_matches_torch(cuda):
     """pool -> FC -> softmax CE -> FC grads -> pool backward masked by the block's ReLU + BN reduce."""
     torch.manual_seed(6)
