@@ -5,13 +5,15 @@ time, span and union-busy time (the wall time at least one kernel ran).
 
     python scripts/step_trace_db.py run_results.db
 """
+import os
 import sqlite3
 import sys
 
 c = sqlite3.connect(sys.argv[1])
 rows = c.execute("select name,start,end,grid_x*grid_y*grid_z/(workgroup_x*workgroup_y*workgroup_z) from kernels "
                  "order by start").fetchall()
-idx = [i for i, r in enumerate(rows) if r[0].startswith("sgd_")]
+mark = os.environ.get("STEP_MARK", "sgd_")  # the kernel that ends a step (LLaMA: adam_)
+idx = [i for i, r in enumerate(rows) if r[0].startswith(mark)]
 a, b = idx[-3], idx[-2]
 tot = 0.0
 busy = 0.0
