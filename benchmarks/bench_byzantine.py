@@ -92,6 +92,9 @@ def main():
         fa = make("mean", False)
         clean_rps, _ = timed(fa)
         del fa
+        if ctx.rank == 0:
+            import sys
+            print(f"[bench_byzantine] clean mean: {clean_rps:.4f} rounds/s", file=sys.stderr, flush=True)
     for agg in args.aggregators.split(","):
         fa = make(agg, True)
         rps, agg_ms = timed(fa)
@@ -109,6 +112,9 @@ def main():
             res["test_accuracy_clean"] = round(clean.test(), 4)
             del clean
         results[agg] = res
+        if ctx.rank == 0:  # progress (a full sweep runs for minutes)
+            import sys
+            print(f"[bench_byzantine] {agg}: {res}", file=sys.stderr, flush=True)
         del fa
     emit(ctx, metric="Byzantine-robust FedAvg rounds/s (8 clients, 2 label-flip + 2 sign-flip)",
          value=results.get("krum", next(iter(results.values())))["rounds_per_s"], unit="rounds/s",
