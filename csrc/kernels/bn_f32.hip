@@ -475,7 +475,21 @@ __global__ __launch_bounds__(256) void bnf_fold_fin_kernel(BNFBwdArgs a, BNFBwdA
   if (c >= C) return;
   double s0 = 0.0, s1 = 0.0;
   const double* w = t.fold_ws + (long long)g * nb * 2 * C;
-  for (int k = 0; k < nb; ++k) {
+  int k = 0;
+  for (; k + 8 <= nb; k += 8) {  // loads ahead, added in block order (as bnf_fold_one_kernel)
+    double y0[8], y1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      y0[j] = w[(long long)(k + j) * 2 * C + c];
+      y1[j] = w[(long long)(k + j) * 2 * C + C + c];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s0 += y0[j];
+      s1 += y1[j];
+    }
+  }
+  for (; k < nb; ++k) {
     s0 += w[(long long)k * 2 * C + c];
     s1 += w[(long long)k * 2 * C + C + c];
   }
@@ -553,7 +567,21 @@ __global__ __launch_bounds__(256) void bnf_fold_one_kernel(BNFBwdArgs a, BNFBwdA
   __syncthreads();
   if (!is_last || sg != 0 || c >= C) return;
   double s0 = 0.0, s1 = 0.0;
-  for (int k = 0; k < nb; ++k) {
+  int k = 0;
+  for (; k + 8 <= nb; k += 8) {  // 16 loads in flight, added in block order (one at a time they
+    double y0[8], y1[8];          // made the last block's fold a chain of load latencies)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      y0[j] = wsb[(long long)(k + j) * 2 * C + c];
+      y1[j] = wsb[(long long)(k + j) * 2 * C + C + c];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s0 += y0[j];
+      s1 += y1[j];
+    }
+  }
+  for (; k < nb; ++k) {
     s0 += wsb[(long long)k * 2 * C + c];
     s1 += wsb[(long long)k * 2 * C + C + c];
   }

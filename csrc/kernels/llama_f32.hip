@@ -678,7 +678,7 @@ DDL_API int ddl_attnf_bwd(const float* qkv, const float* o, const float* dout, c
 
 // ---------------------------------------------------------------------------------------------
 // Vocabulary cross-entropy, fp32 logits [R][V] (row stride ld), int32 labels. One block per row:
-// pass 1 online max / sum-exp, pass 2 d = (softmax - onehot) * (*inv); rowloss[r] = lse - z[label]
+// pass 1 max / sum-exp, pass 2 d = (softmax - onehot) * (*inv); rowloss[r] = lse - z[label]
 // (0 for ignored rows, whose gradient row is zero).
 __device__ __forceinline__ void block_maxsum(float& m, float& s, float* sm) {
   // merge (m, s) pairs: wave level, then the 4 waves in a fixed order
@@ -742,6 +742,57 @@ __global__ __launch_bounds__(256) void cevf_rows_kernel(const float* __restrict_
   }
 }
 
+// Rows of up to 1024 * NV4 logits held in registers: one HBM read of z instead of two (the
+// streaming kernel above re-reads a 128 KB row after its sum pass, from HBM at 32k vocab).
+template <int NV4>
+__global__ __launch_bounds__(256) void cevf_rows_reg_kernel(const float* __restrict__ z,
+                                                            const int* __restrict__ labels, int V, long long ld,
+                                                            const float* __restrict__ inv, int ignore_index,
+                                                            float* __restrict__ rowloss, float* __restrict__ dz,
+                                                            long long ldd) {
+  __shared__ float sm[8];
+  const int row = blockIdx.x;
+  const float* zr = z + row * ld;
+  const int lab = labels[row];
+  const int n4 = V >> 2;
+  float4 v[NV4];
+#pragma unroll
+  for (int j = 0; j < NV4; ++j) {
+    const int c = threadIdx.x + j * 256;
+    v[j] = c < n4 ? ((const float4*)zr)[c] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < NV4; ++j) mx = fmaxf(mx, fmaxf(fmaxf(v[j].x, v[j].y), fmaxf(v[j].z, v[j].w)));
+  float m = mx * LOG2E, s = 0.f;
+  if (mx != -INFINITY) {
+#pragma unroll
+    for (int j = 0; j < NV4; ++j)
+      s += (exp2f(v[j].x * LOG2E - m) + exp2f(v[j].y * LOG2E - m)) +
+           (exp2f(v[j].z * LOG2E - m) + exp2f(v[j].w * LOG2E - m));
+  }
+  block_maxsum(m, s, sm);
+  const float lse2 = m + log2f(s);
+  const bool valid = lab != ignore_index && lab >= 0 && lab < V;
+  if (threadIdx.x == 0) rowloss[row] = valid ? (lse2 / LOG2E - zr[lab]) : 0.f;
+  if (!dz) return;
+  const float k = valid ? *inv : 0.f;
+  float4* dr = (float4*)(dz + row * ldd);
+#pragma unroll
+  for (int j = 0; j < NV4; ++j) {
+    const int c = threadIdx.x + j * 256;
+    if (c < n4) {
+      const int b = 4 * c;
+      float4 p;
+      p.x = (exp2f(v[j].x * LOG2E - lse2) - (b == lab ? 1.f : 0.f)) * k;
+      p.y = (exp2f(v[j].y * LOG2E - lse2) - (b + 1 == lab ? 1.f : 0.f)) * k;
+      p.z = (exp2f(v[j].z * LOG2E - lse2) - (b + 2 == lab ? 1.f : 0.f)) * k;
+      p.w = (exp2f(v[j].w * LOG2E - lse2) - (b + 3 == lab ? 1.f : 0.f)) * k;
+      dr[c] = p;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void cevf_fold_kernel(const float* __restrict__ rowloss, int R,
                                                         const float* __restrict__ inv, float* __restrict__ loss) {
   __shared__ float sm[4];
@@ -756,8 +807,21 @@ __global__ __launch_bounds__(256) void cevf_fold_kernel(const float* __restrict_
 DDL_API int ddl_cevf(const float* z, const int* labels, int R, int V, long long ld, const float* inv,
                      int ignore_index, float* rowloss, float* loss, float* dz, long long ldd, hipStream_t s) {
   if (R < 1 || V < 1) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(cevf_rows_kernel, dim3(R), dim3(256), 0, s, z, labels, V, ld, inv, ignore_index, rowloss, dz,
-                     ldd);
+  const bool vec = V % 4 == 0 && ld % 4 == 0 && (!dz || ldd % 4 == 0) && ((uintptr_t)z & 15) == 0 &&
+                   ((uintptr_t)dz & 15) == 0;
+  const int n4 = V / 4;
+  if (vec && n4 <= 256 * 8)
+    hipLaunchKernelGGL(cevf_rows_reg_kernel<8>, dim3(R), dim3(256), 0, s, z, labels, V, ld, inv, ignore_index,
+                       rowloss, dz, ldd);
+  else if (vec && n4 <= 256 * 16)
+    hipLaunchKernelGGL(cevf_rows_reg_kernel<16>, dim3(R), dim3(256), 0, s, z, labels, V, ld, inv, ignore_index,
+                       rowloss, dz, ldd);
+  else if (vec && n4 <= 256 * 32)
+    hipLaunchKernelGGL(cevf_rows_reg_kernel<32>, dim3(R), dim3(256), 0, s, z, labels, V, ld, inv, ignore_index,
+                       rowloss, dz, ldd);
+  else
+    hipLaunchKernelGGL(cevf_rows_kernel, dim3(R), dim3(256), 0, s, z, labels, V, ld, inv, ignore_index, rowloss,
+                       dz, ldd);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(cevf_fold_kernel, dim3(1), dim3(256), 0, s, rowloss, R, inv, loss);

@@ -32,6 +32,9 @@ DIRECT_SGD = os.environ.get("DDL_DIRECT_SGD", "1") != "0"
 # the GPU idle ~1 ms at every round boundary even with the host rounds ahead (sync_rounds off);
 # with two instances (DDL_ROUND_GRAPHS=2) the host can submit round r+1 while round r runs.
 ROUND_GRAPHS = max(1, int(os.environ.get("DDL_ROUND_GRAPHS", "1")))
+# Longest step sequence in one captured graph. A whole 50,000-sample single-client epoch (500 steps,
+# ~80k kernel nodes) segfaulted inside hipGraphLaunch; longer rounds replay a graph per chunk.
+GRAPH_MAX_STEPS = max(1, int(os.environ.get("DDL_GRAPH_MAX_STEPS", "128")))
 
 
 class LocalTrainer:
@@ -83,6 +86,15 @@ class LocalTrainer:
         static plan buffer), so a round costs one plan copy and one graph launch. Without the tail
         in the graph, the short step (6,250 samples per client at B=100: 62 steps + 50 samples)
         ran eagerly every round, ~130 host-side launches."""
+        if hasattr(self.label_transform, "refresh"):  # this round's device-side transform state
+            self.label_transform.refresh(plan_dev.device)
+        k0 = 0
+        while nsteps - k0 > GRAPH_MAX_STEPS:  # full chunks share one graph (plan rows copied in)
+            self._replay(plan_dev[k0:k0 + GRAPH_MAX_STEPS], GRAPH_MAX_STEPS, G, None)
+            k0 += GRAPH_MAX_STEPS
+        self._replay(plan_dev[k0:nsteps], nsteps - k0, G, tail)
+
+    def _replay(self, plan_dev: torch.Tensor, nsteps: int, G: int, tail):
         key = (G, self.B, nsteps, None if tail is None else tail.shape[-1],
                getattr(self.label_transform, "graph_key", None))
         ents = self._graphs.get(key)
@@ -96,8 +108,6 @@ class LocalTrainer:
         ent["plan"].copy_(plan_dev[:nsteps])
         if tail is not None:
             ent["tail"].copy_(tail)
-        if hasattr(self.label_transform, "refresh"):  # this round's device-side transform state
-            self.label_transform.refresh(plan_dev.device)
         ent["graph"].replay()
         self.last_loss = ent["loss"]
 

@@ -45,6 +45,30 @@ def test_graph_replay_equals_eager(cuda, batch, flip):
     assert ((ws[0] - ws[1]).norm() / step).item() < 1e-2
 
 
+@pytest.mark.parametrize("flip", [False, True])
+def test_chunked_round_graph_equals_whole(cuda, monkeypatch, flip):
+    """A round longer than GRAPH_MAX_STEPS replays one graph per chunk of steps (a 500-step
+    single-client round in one graph segfaulted in hipGraphLaunch). Chunks of 2 steps, the last
+    chunk with the short step: same weights as the whole round in one graph."""
+    import ddl25spring_amd.fl.local as L
+    arr = synthetic_images("mnist", 800, seed=0)
+    parts = split(4, True, 3, labels=arr.labels)
+    ws = []
+    for chunk in (1000, 2):
+        monkeypatch.setattr(L, "GRAPH_MAX_STEPS", chunk)
+        data = DeviceImageDataset(arr, cuda)
+        fa = FedAvg(mnist_cnn, data, parts, lr=0.05, batch_size=60, client_fraction=1.0,
+                    seed=3, ctx=_ctx(cuda), use_graph=True, eval_every=0,
+                    attack=LabelFlip([1]) if flip else None)
+        w0 = fa.w_global.clone()
+        fa.round()
+        fa.round()
+        ws.append(fa.w_global.clone())
+    step = (ws[1] - w0).norm()
+    assert step > 0
+    assert ((ws[0] - ws[1]).norm() / step).item() < 1e-2
+
+
 def test_fedavg_mnist_cnn_learns_on_device(cuda):
     arr = synthetic_images("mnist", 3000, seed=0)
     tarr = synthetic_images("mnist", 1000, seed=1)
