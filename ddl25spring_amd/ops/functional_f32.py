@@ -262,6 +262,20 @@ def _tuned(mode: int, g):
     return None if p is None else (cfg_of(p[0], p[1]), int(p[2]))
 
 
+# Plain-GEMM callers (the fp32 LLaMA linears) may run a product on the vendor fp32 GEMM (torch.mm ->
+# hipBLASLt, true fp32 MFMA) where the tuner measured it faster than both native engines: "blas:"
+# entries of f32_plans.json (scripts/conv_f32_tune.py --model llama288). DDL_F32_BLAS: auto (the
+# table), 0 (never), 1 (always).
+BLAS = [os.environ.get("DDL_F32_BLAS", "auto")]
+
+
+def vendor_gemm(mode: int, g) -> bool:
+    if BLAS[0] in ("0", "1"):
+        return BLAS[0] == "1"
+    _tuned(mode, g)  # loads the table
+    return f"blas:{_MODE_NAMES[mode]}:{g.G},{g.N},{g.H},{g.W},{g.C},{g.K},{g.R},{g.S},{g.stride},{g.pad}" in _TUNED
+
+
 def set_plan(mode: int, geom, bp: int, bq: int, split: int, engine: str | None = None) -> None:
     """Pin a launch plan (tile BP x BQ, split-K slices[, engine under "auto": "x6", "mfma32", or
     "x6h" = the halo kernel, BQ 128]) for one (mode, geometry) — the tuner and the tests."""

@@ -23,6 +23,7 @@ import torch
 
 from . import _lib
 from . import functional as Fn
+from . import functional_f32 as F32
 from ._lib import check, ptr, stream
 
 vp, i32, i64, f32 = _lib.vp, _lib.i32, _lib.i64, _lib.f32
@@ -74,12 +75,17 @@ class LinearF32(torch.autograd.Function):
         T = x2.shape[0]
         wc = w.detach().contiguous()
         ctx.conv = conv_linear_ok(C, Kout)
-        if ctx.conv:
-            geom = Fn.ConvGeom(1, T, 1, 1, C, Kout, 1, 1, 1, 0)
+        geom = Fn.ConvGeom(1, T, 1, 1, C, Kout, 1, 1, 1, 0)
+        ctx.geom = geom
+        if ctx.conv and F32.vendor_gemm(F32.F_FWD, geom):  # tuned: the vendor fp32 GEMM is faster here
+            y = torch.mm(x2, wc.t()) if residual is None else \
+                torch.addmm(residual.reshape(T, Kout).float(), x2, wc.t())
+            if b is not None:
+                y.add_(b.detach().view(1, Kout))
+        elif ctx.conv:
             res = residual.reshape(1, T, 1, 1, Kout).contiguous() if residual is not None else None
             y = Fn.conv_fwd(x2.view(1, T, 1, 1, C), wc.view(1, Kout, 1, 1, C), geom,
                             bias=None if b is None else b.detach().contiguous().view(1, Kout), residual=res)
-            ctx.geom = geom
         else:
             from .tabular_ops import gemm_f32
             y = torch.empty(T, Kout, dtype=torch.float32, device=x.device)
@@ -103,14 +109,25 @@ class LinearF32(torch.autograd.Function):
         if ctx.conv:
             g = ctx.geom
             dy5 = d2.view(1, T, 1, 1, Kout)
+            vd = want_dx and F32.vendor_gemm(F32.F_DGRAD, g)  # tuned per mode (functional_f32.vendor_gemm)
+            vw = want_dw and F32.vendor_gemm(F32.F_WGRAD, g)
+            if vd:
+                dx = torch.mm(d2, wc)
             if want_dw:
                 dwt = sink.view(1, Kout, 1, 1, C) if sink is not None else \
                     torch.zeros(1, Kout, 1, 1, C, dtype=torch.float32, device=dy.device)
-                dx = Fn.conv_dgrad_wgrad(dy5, wc.view(1, Kout, 1, 1, C), x2.view(1, T, 1, 1, C), g, dwt,
-                                         want_dx=want_dx)
+                if vw:
+                    dwt.view(Kout, C).addmm_(d2.t(), x2)
+                    if want_dx and not vd:
+                        dx = Fn.conv_dgrad(dy5, wc.view(1, Kout, 1, 1, C), g)
+                else:
+                    d = Fn.conv_dgrad_wgrad(dy5, wc.view(1, Kout, 1, 1, C), x2.view(1, T, 1, 1, C), g, dwt,
+                                            want_dx=want_dx and not vd)
+                    if not vd:
+                        dx = d
                 if sink is None:
                     dw = dwt.view(Kout, C)
-            elif want_dx:
+            elif want_dx and not vd:
                 dx = Fn.conv_dgrad(dy5, wc.view(1, Kout, 1, 1, C), g)
         else:
             from .tabular_ops import gemm_f32

@@ -64,6 +64,24 @@ def resnet50_geoms(G: int, N: int):
     return list(dict.fromkeys(gs))
 
 
+LLM_SHAPES = ((288, 864), (288, 288), (288, 1536), (768, 288), (288, 32000))  # qkv, wo, w13, w2, LM head
+
+
+def llama288_geoms(tokens=(8192, 2048)):
+    """The LLaMA-288d linears as 1x1 convs over T token pixels (ops/llama_f32.LinearF32): T = 8192
+    at pp=1 (batch 32 x 256), 2048 per micro-batch with a pipeline."""
+    return [ConvGeom(1, T, 1, 1, C, K, 1, 1, 1, 0) for T in tokens for C, K in LLM_SHAPES]
+
+
+def vendor_run(mode, g, x, w, dy, dw):
+    """The same product on the vendor fp32 GEMM (torch.mm -> hipBLASLt), as LinearF32 runs it."""
+    T = g.N * g.H * g.W
+    x2, w2, d2, dw2 = x.view(T, g.C), w.view(g.K, g.C), dy.view(T, g.K), dw.view(g.K, g.C)
+    return {F32.F_FWD: lambda: torch.mm(x2, w2.t()),
+            F32.F_DGRAD: lambda: torch.mm(d2, w2),
+            F32.F_WGRAD: lambda: dw2.addmm_(d2.t(), x2)}[mode]
+
+
 def timed(fn, reps):
     for _ in range(2):
         fn()
@@ -84,7 +102,7 @@ def main():
     ap.add_argument("--batch", type=int, default=100)
     ap.add_argument("--budget-s", type=float, default=240.0)
     ap.add_argument("--math", default="mfma32", choices=list(F32.MATHS))
-    ap.add_argument("--model", default="resnet18", choices=("resnet18", "resnet50"))
+    ap.add_argument("--model", default="resnet18", choices=("resnet18", "resnet50", "llama288"))
     a = ap.parse_args()
     F32.set_math(a.math)
     prefix = "" if a.math == "mfma32" else f"{a.math}:"
@@ -92,8 +110,10 @@ def main():
     dev = torch.device("cuda")
     t_start = time.time()
     plans, report = {}, []
-    for G in a.groups:
-        for g in (resnet50_geoms if a.model == "resnet50" else resnet18_geoms)(G, a.batch):
+    geoms = {"resnet50": resnet50_geoms, "resnet18": resnet18_geoms,
+             "llama288": lambda G, N: llama288_geoms()}[a.model]
+    for G in (a.groups if a.model != "llama288" else [1]):
+        for g in geoms(G, a.batch):
             x = torch.randn(g.G, g.N, g.H, g.W, g.C, device=dev)
             w = torch.randn(g.G, g.K, g.R, g.S, g.C, device=dev) * 0.05
             dy = torch.randn(g.G, g.N, g.P, g.Q, g.K, device=dev)
@@ -143,6 +163,11 @@ def main():
                            tflops=round(flops / ms / 1e9, 1),
                            pct_peak=round(100 * flops / ms / 1e9 / PEAK_TF, 1),
                            heuristic_ms=None if hms is None else round(hms, 4))
+                if a.model == "llama288":  # plain GEMMs: the vendor fp32 GEMM is a candidate too
+                    bms = timed(vendor_run(mode, g, x, w, dy, dw), 10)
+                    row["vendor_ms"] = round(bms, 4)
+                    if bms < 0.97 * ms:
+                        plans["blas:" + key[len(prefix):]] = [round(bms, 4), round(ms, 4)]
                 report.append(row)
                 print(json.dumps(row), flush=True)
                 if time.time() - t_start > a.budget_s:
