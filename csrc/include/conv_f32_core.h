@@ -383,23 +383,34 @@ __global__ __launch_bounds__(256) void convf32_splitk_epilogue(ConvF32Args a) {
   const long long qmax = (long long)a.slots / nph * BQ;
   const long long slice = (long long)a.G * nph * qmax * o.Pd;
   const float* base = a.partial + ((long long)o.g * nph + o.phase) * qmax * o.Pd;
+  // slice-outer: each slice's TP x TQ fragment loads are in flight together (fragment-outer, every
+  // load of a fragment's slice chain waited on the previous add); per fragment the adds still run
+  // in slice order, so the sum is bitwise the same
   f4v acc[TP][TQ];
+  bool ok[TP][TQ];
+  const float* src[TP][TQ];
 #pragma unroll
   for (int ti = 0; ti < TP; ++ti)
 #pragma unroll
     for (int tj = 0; tj < TQ; ++tj) {
       const int q = o.q0 + wq * WQ + tj * 16 + (lane & 15);
       const int p = o.p0 + wp * WP + ti * 16 + 4 * (lane >> 4);
-      f4v s = (f4v){0.f, 0.f, 0.f, 0.f};
-      if (q < o.Qd && p < o.Pd) {
-        const float* src = base + (long long)q * o.Pd + p;
-        for (int k = 0; k < a.split_k; ++k) {
-          const float4 v = *(const float4*)(src + k * slice);
-          s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
-        }
-      }
-      acc[ti][tj] = s;
+      ok[ti][tj] = q < o.Qd && p < o.Pd;
+      src[ti][tj] = base + (ok[ti][tj] ? (long long)q * o.Pd + p : 0);
+      acc[ti][tj] = (f4v){0.f, 0.f, 0.f, 0.f};
     }
+  for (int k = 0; k < a.split_k; ++k) {
+    f4v v[TP][TQ];
+#pragma unroll
+    for (int ti = 0; ti < TP; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < TQ; ++tj)
+        v[ti][tj] = ok[ti][tj] ? *(const f4v*)(src[ti][tj] + k * slice) : (f4v){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ti = 0; ti < TP; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < TQ; ++tj) acc[ti][tj] += v[ti][tj];
+  }
   fepi<MODE, BP, BQ, Lay16<BP, BQ>>(a, o, acc, red);
 }
 

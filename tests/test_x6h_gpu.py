@@ -327,10 +327,13 @@ def test_x6h_network_shapes_auto_plan(cuda, geom):
     _close(d2, dxr * keep)
 
 
-def test_presplit_scope_matches_per_launch(cuda):
+@pytest.mark.parametrize("side", [False, True])
+def test_presplit_scope_matches_per_launch(cuda, monkeypatch, side):
     """PresplitScope (Net.train_step): the first pass records the halo launches' weight images,
-    later passes read the images ONE multi-tensor launch made at scope entry — bitwise the
-    per-launch split's results, refreshed when the weights change between steps."""
+    later passes read the images ONE multi-tensor launch made at scope entry (side: the first
+    image up front, the rest on a side stream the step's stream joins at their first use) —
+    bitwise the per-launch split's results, refreshed when the weights change between steps."""
+    monkeypatch.setattr(F32, "PRESPLIT_SIDE", [side])
     geoms = [ConvGeom(G=2, N=3, H=16, W=16, C=64, K=128, R=3, S=3, stride=1, pad=1),
              ConvGeom(G=2, N=3, H=16, W=16, C=128, K=128, R=1, S=1, stride=1, pad=0)]
     torch.manual_seed(7)
@@ -351,6 +354,7 @@ def test_presplit_scope_matches_per_launch(cuda):
         with scope:
             rec = run()
         assert scope.state == "ready" and len(scope.keys) == 4
+        assert len(scope.tables) == (2 if side else 1) and len(scope.tail) == (3 if side else 0)
         with scope:
             pre = run()
         for a, b, c in zip(plain, rec, pre):
