@@ -316,8 +316,16 @@ def plan(mode: int, geom) -> tuple[int, int]:
 
 
 def _halo_plan(mode: int, geom) -> tuple[int, int]:
-    """Halo kernel: BP 128 where the output channels allow, 128-pixel tiles, split-K over the
-    16-channel chunks until ~TARGET_WG workgroups (each slice keeping >= 4 chunks)."""
+    """Halo kernel: a measured plan ('x6h:' entries of f32_plans.json, scripts/halo_plan_probe.py:
+    e.g. BP 64 without split-K for the 16x16 layer at one client, 59 vs 78 us); otherwise BP 128
+    where the output channels allow, 128-pixel tiles, split-K over the 16-channel chunks until
+    ~TARGET_WG workgroups (each slice keeping >= 4 chunks)."""
+    _tuned(mode, geom)  # loads the table
+    if TARGET_WG != 1:  # TARGET_WG = 1 pins split-K off (the multi-rank rehearsal's plans)
+        p = _TUNED.get(f"x6h:{_MODE_NAMES[mode]}:{geom.G},{geom.N},{geom.H},{geom.W},{geom.C},{geom.K},"
+                       f"{geom.R},{geom.S},{geom.stride},{geom.pad}")
+        if p is not None:
+            return cfg_of(int(p[0]), int(p[1])) | X6_BIT | HALO_BIT, int(p[2])
     Pd, Qd, _, _ = _dims(mode, geom)
     SC = geom.C if mode == F_FWD else geom.K
     # BP 128 where the channels allow, except 4x4 images: their 8-image halo (43 KiB) with a BP 128

@@ -1,0 +1,92 @@
+"""Halo-kernel plan sweep (BP x split-K) per ResNet-18 stride-1 3x3 layer and client count, in
+one process: device time of FWD (with BN statistics) and DGRAD per pinned plan, against the
+default plan (functional_f32._halo_plan).
+
+    python scripts/halo_plan_probe.py [--G 1 2 4 8] [--reps 20] [--out gpurun_out/x6h_plans.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+from ddl25spring_amd.ops import functional_f32 as F32  # noqa: E402
+from ddl25spring_amd.ops.functional import ConvGeom  # noqa: E402
+
+def timed(fn, reps):
+    """Device time per call: reps calls captured in one graph (the eager calls are host-bound at
+    one or two clients), replayed after a warm-up."""
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+LAYERS = {"c64": (32, 64), "c128": (16, 128), "c256": (8, 256), "c512": (4, 512)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--G", type=int, nargs="*", default=[1])
+    ap.add_argument("--N", type=int, default=100)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--out", default="", help="write the best plans as 'x6h:' table entries (scripts/merge_plans.py)")
+    a = ap.parse_args()
+    plans, report = {}, []
+    dev = torch.device("cuda")
+    F32.ensure_workspace(dev)
+    for G in a.G:
+        for name, (H, C) in LAYERS.items():
+            g = ConvGeom(G, a.N, H, H, C, C, 3, 3, 1, 1)
+            x = torch.randn(g.G, g.N, g.H, g.W, g.C, device=dev)
+            w = torch.randn(g.G, g.K, 3, 3, g.C, device=dev) * 0.05
+            dy = torch.randn(g.G, g.N, g.P, g.Q, g.K, device=dev)
+            for mode, mname in ((F32.F_FWD, "fwd"), (F32.F_DGRAD, "dgrad")):
+                run = (lambda: F32.conv_fwd(x, w, g, stats=F32.SlotStats())) if mode == F32.F_FWD else \
+                    (lambda: F32.conv_dgrad(dy, w, g))
+                F32.clear_plan(mode, g)
+                dflt = F32.plan(mode, g)
+                t0 = timed(run, a.reps)
+                res = []
+                for bp in (64, 128):
+                    for split in (1, 2, 4, 8):
+                        if C // 16 < split * 4:
+                            continue
+                        F32.set_plan(mode, g, bp, 128, split, "x6h")
+                        try:
+                            res.append((timed(run, a.reps), bp, split))
+                        except Exception as e:  # noqa: BLE001
+                            print("skip", name, mname, bp, split, e, flush=True)
+                F32.clear_plan(mode, g)
+                res.sort()
+                best = res[0]
+                key = f"x6h:{mname}:{g.G},{g.N},{g.H},{g.W},{g.C},{g.K},{g.R},{g.S},{g.stride},{g.pad}"
+                plans[key] = [best[1], 128, best[2]]
+                report.append(dict(G=G, layer=name, mode=mname, default=list(dflt), default_us=round(t0 * 1e3, 1),
+                                   best=plans[key], best_us=round(best[0] * 1e3, 1)))
+                print(f"G={G} {name} {mname}: default {dflt} {t0 * 1e3:6.1f} us | best bp={best[1]} split={best[2]} "
+                      f"{best[0] * 1e3:6.1f} us | " + " ".join(f"{b}/{s}:{t * 1e3:.1f}" for t, b, s in res), flush=True)
+            del x, w, dy
+    if a.out:
+        Path(a.out).parent.mkdir(parents=True, exist_ok=True)
+        Path(a.out).write_text(json.dumps({"plans": plans, "report": report}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
