@@ -639,9 +639,17 @@ HW_MIN_W = int(os.environ.get("DDL_F32_HW_MIN_W", "16"))
 HW_TARGET_WG = int(os.environ.get("DDL_F32_HW_TARGET_WG", "256"))  # one workgroup per CU (LDS-bound)
 
 
+def uses_halo_wgrad(geom) -> bool:
+    """Does conv_wgrad take the halo WGRAD (conv_x6hw.hip) for this geometry?"""
+    a = _args(geom)
+    return HALO_WGRAD[0] and _MATH[0] != "mfma32" and geom.W >= HW_MIN_W \
+        and bool(_lib.kernels().ddl_x6hw_ok(ctypes.byref(a)))
+
+
 def _halo_wgrad(a, geom, device, split_k: int, ws_role: str) -> bool:
-    """Launch the halo WGRAD when it takes this geometry: split-K over pixel tiles until ~one
-    workgroup per CU (each slice keeping >= 3 tiles), slices folded in slice order."""
+    """Launch the halo WGRAD when it takes this geometry: a measured slice count ('x6hw:' entries of
+    f32_plans.json, scripts/halo_plan_probe.py), else split-K over pixel tiles until ~one
+    workgroup per CU (each slice keeping >= 3 tiles); slices folded in slice order."""
     if not (HALO_WGRAD[0] and _MATH[0] != "mfma32") or geom.W < HW_MIN_W \
             or not _lib.kernels().ddl_x6hw_ok(ctypes.byref(a)):
         return False
@@ -649,6 +657,12 @@ def _halo_wgrad(a, geom, device, split_k: int, ws_role: str) -> bool:
     ntile = int(lib.ddl_x6hw_tiles(ctypes.byref(a)))
     base = (geom.K // 64) * (geom.C // 32) * geom.G
     split = split_k or 1
+    if not split_k and TARGET_WG != 1:
+        _tuned(F_WGRAD, geom)  # loads the table
+        p = _TUNED.get(f"x6hw:wgrad:{geom.G},{geom.N},{geom.H},{geom.W},{geom.C},{geom.K},{geom.R},{geom.S},"
+                       f"{geom.stride},{geom.pad}")
+        if p is not None:
+            split_k = split = int(p[0])
     if not split_k:
         target = min(HW_TARGET_WG, TARGET_WG)  # TARGET_WG = 1 pins split-K off for every conv
         while base * split < target and ntile >= split * 2 * 3 and split < 128:

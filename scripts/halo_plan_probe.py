@@ -82,6 +82,23 @@ def main():
                                    best=plans[key], best_us=round(best[0] * 1e3, 1)))
                 print(f"G={G} {name} {mname}: default {dflt} {t0 * 1e3:6.1f} us | best bp={best[1]} split={best[2]} "
                       f"{best[0] * 1e3:6.1f} us | " + " ".join(f"{b}/{s}:{t * 1e3:.1f}" for t, b, s in res), flush=True)
+            if F32.uses_halo_wgrad(g):  # halo WGRAD: slice count sweep
+                dw = torch.zeros_like(w)
+                base = (g.K // 64) * (g.C // 32) * G
+                t0 = timed(lambda: F32.conv_wgrad(dy, x, g, dw), a.reps)
+                res = []
+                for split in (1, 2, 4, 8, 16, 32, 64, 128):
+                    if base * split > 2048:
+                        break
+                    res.append((timed(lambda: F32.conv_wgrad(dy, x, g, dw, split_k=split), a.reps), split))
+                res.sort()
+                key = f"x6hw:wgrad:{g.G},{g.N},{g.H},{g.W},{g.C},{g.K},{g.R},{g.S},{g.stride},{g.pad}"
+                plans[key] = [res[0][1]]
+                report.append(dict(G=G, layer=name, mode="wgrad", default_us=round(t0 * 1e3, 1),
+                                   best=plans[key], best_us=round(res[0][0] * 1e3, 1)))
+                print(f"G={G} {name} wgrad(x6hw): default {t0 * 1e3:6.1f} us | best split={res[0][1]} "
+                      f"{res[0][0] * 1e3:6.1f} us | " + " ".join(f"{s_}:{t * 1e3:.1f}" for t, s_ in res), flush=True)
+                del dw
             del x, w, dy
     if a.out:
         Path(a.out).parent.mkdir(parents=True, exist_ok=True)
