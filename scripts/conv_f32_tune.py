@@ -88,8 +88,9 @@ EAGER = [False]
 def timed(fn, reps):
     """Device time per call: ``reps`` calls captured in one graph and replayed (timing eager calls
     measured the host at one or two clients, where a launch's Python outlasts its kernels). With
-    --eager-timing: eager calls — for models whose step runs eagerly (the LLaMA linears: tuned
-    eagerly 726k -> 868k tok/s, graph-timed 855k)."""
+    --eager-timing: eager calls, as the LLaMA linears' table was tuned (its whole graph-replayed
+    step: eager-tuned 872k tok/s, graph-tuned 855k — per-launch differences within isolated-timing
+    noise decided the choices, and the eager set won end to end)."""
     if EAGER[0]:
         for _ in range(2):
             fn()
