@@ -46,14 +46,20 @@ def main():
     ap.add_argument("--G", type=int, nargs="*", default=[1])
     ap.add_argument("--N", type=int, default=100)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--model", default="resnet18", choices=("resnet18", "resnet50"))
     ap.add_argument("--out", default="", help="write the best plans as 'x6h:' table entries (scripts/merge_plans.py)")
     a = ap.parse_args()
     plans, report = {}, []
     dev = torch.device("cuda")
     F32.ensure_workspace(dev)
     for G in a.G:
-        for name, (H, C) in LAYERS.items():
-            g = ConvGeom(G, a.N, H, H, C, C, 3, 3, 1, 1)
+        if a.model == "resnet50":  # the bottleneck 3x3 stride-1 convs (rows padded to a power of two)
+            from conv_f32_tune import resnet50_geoms
+            layers = [(f"r50_{g.H}x{g.C}", g) for g in resnet50_geoms(G, a.N) if g.R == 3 and g.stride == 1]
+        else:
+            layers = [(name, ConvGeom(G, a.N, H, H, C, C, 3, 3, 1, 1)) for name, (H, C) in LAYERS.items()]
+        for name, g in layers:
+            C = g.C
             x = torch.randn(g.G, g.N, g.H, g.W, g.C, device=dev)
             w = torch.randn(g.G, g.K, 3, 3, g.C, device=dev) * 0.05
             dy = torch.randn(g.G, g.N, g.P, g.Q, g.K, device=dev)

@@ -111,3 +111,32 @@ def test_flat1x1_launch_geometry(monkeypatch):
     assert F32._launch_geom(g, "w") is g and F32._launch_geom(g, "d") != g
     monkeypatch.setattr(F32, "FLAT1X1", [False, "fdw"])
     assert F32._launch_geom(g, "d") is g
+
+
+def test_fp32_measured_halo_and_vendor_entries(monkeypatch):
+    """'x6h:' table entries set the halo plan (unless TARGET_WG = 1 pins split-K off), and 'blas:'
+    entries route one product of a plain-GEMM linear to the vendor fp32 GEMM (DDL_F32_BLAS 0 / 1
+    override the table)."""
+    from ddl25spring_amd.ops import functional_f32 as F32
+    from ddl25spring_amd.ops.functional import ConvGeom
+    g = ConvGeom(3, 7, 8, 8, 16, 16, 3, 3, 1, 1)
+    lin = ConvGeom(1, 64, 1, 1, 32, 48, 1, 1, 1, 0)
+    old_math, old_tuned = F32.math(), F32._TUNED
+    try:
+        F32._TUNED = {"x6h:fwd:3,7,8,8,16,16,3,3,1,1": [64, 128, 2],
+                      "blas:dgrad:1,64,1,1,32,48,1,1,1,0": [0.01, 0.02]}
+        F32.set_math("auto")
+        F32._PLANS.clear()
+        assert F32.plan(F32.F_FWD, g) == (F32.cfg_of(64, 128) | F32.X6_BIT | F32.HALO_BIT, 2)
+        monkeypatch.setattr(F32, "TARGET_WG", 1)
+        F32._PLANS.clear()
+        assert F32.plan(F32.F_FWD, g)[1] == 1
+        assert F32.vendor_gemm(F32.F_DGRAD, lin) and not F32.vendor_gemm(F32.F_FWD, lin)
+        monkeypatch.setattr(F32, "BLAS", ["0"])
+        assert not F32.vendor_gemm(F32.F_DGRAD, lin)
+        monkeypatch.setattr(F32, "BLAS", ["1"])
+        assert F32.vendor_gemm(F32.F_FWD, lin)
+    finally:
+        F32._TUNED = old_tuned
+        F32.set_math(old_math)
+        F32._PLANS.clear()
