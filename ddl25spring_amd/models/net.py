@@ -119,7 +119,9 @@ class Net:
     # Weight grads on a side stream (Fn.wgrad_overlap). DDL_WGRAD_OVERLAP=1 / 0 forces it; by default
     # it is on for fp32 activations, where it was measured faster on the graph-replayed ResNet-18
     # FedAvg step (1 client 17.97k -> 19.11k, 8 clients 33.9k -> 35.0k samples/s), and off for
-    # bf16, where it was measured slower (1 client: 138 -> 152 ms per round).
+    # bf16, where it was measured slower (1 client: 138 -> 152 ms per round). Round 5 (tuned
+    # per-client-count plans, scripts/gpu/r5ov.sh): on at 1 / 4 / 8 slots (+0.7 / +0.8 / +1.6 %),
+    # off at 2 slots, where it costs 1.4 % (31.4k vs 31.9k samples/s).
     _OVERLAP_ENV = os.environ.get("DDL_WGRAD_OVERLAP", "auto")
 
     @property
@@ -129,7 +131,7 @@ class Net:
             return forced
         if self._OVERLAP_ENV in ("0", "1"):
             return self._OVERLAP_ENV == "1"
-        return self.act_dtype == torch.float32
+        return self.act_dtype == torch.float32 and self.G != 2
 
     @overlap_wgrad.setter
     def overlap_wgrad(self, on: bool) -> None:
