@@ -289,6 +289,24 @@ def clear_plan(mode: int, geom) -> None:
     _PLANS.pop((mode, geom), None)
 
 
+# DDL_F32_RECORD=<path>: every (mode, geometry) a process plans is written there as JSON at exit,
+# for scripts/conv_f32_tune.py --geoms-file (tune exactly the launches a workload makes)
+_RECORD_PATH = os.environ.get("DDL_F32_RECORD", "")
+_RECORDED: set = set()
+
+
+def _write_record():
+    import json
+    rows = sorted({(m, (g.G, g.N, g.H, g.W, g.C, g.K, g.R, g.S, g.stride, g.pad)) for m, g in _RECORDED})
+    with open(_RECORD_PATH, "w") as f:
+        json.dump([{"mode": _MODE_NAMES[m], "geom": list(g)} for m, g in rows], f)
+
+
+if _RECORD_PATH:
+    import atexit
+    atexit.register(_write_record)
+
+
 def plan(mode: int, geom) -> tuple[int, int]:
     """(cfg, split) heuristic: 128-wide tiles where the dimension allows, then split-K until the
     grid has ~TARGET_WG workgroups (each slice keeping >= 8 reduction steps)."""
@@ -296,6 +314,8 @@ def plan(mode: int, geom) -> tuple[int, int]:
     p = _PLANS.get(key)
     if p is not None:
         return p
+    if _RECORD_PATH:
+        _RECORDED.add(key)
     p = _OVERRIDE.get(key)
     if p is None and _HALO[0] and _MATH[0] != "mfma32" and halo_ok(mode, geom, auto=True):
         p = _halo_plan(mode, geom)

@@ -127,6 +127,8 @@ def main():
     ap.add_argument("--batch", type=int, default=100)
     ap.add_argument("--budget-s", type=float, default=240.0)
     ap.add_argument("--eager-timing", action="store_true", help="time eager calls (see timed)")
+    ap.add_argument("--geoms-file", default="",
+                    help="tune the (mode, geometry) launches a workload recorded (DDL_F32_RECORD=<file>)")
     ap.add_argument("--skip-halo", action="store_true",
                     help="skip launches the halo kernels take (FWD / DGRAD halo plans, halo WGRAD)")
     ap.add_argument("--math", default="mfma32", choices=list(F32.MATHS))
@@ -142,7 +144,14 @@ def main():
     plans, report = {}, []
     geoms = {"resnet50": resnet50_geoms, "resnet18": resnet18_geoms,
              "llama288": lambda G, N: llama288_geoms()}[a.model]
-    for G in (a.groups if a.model != "llama288" else [1]):
+    only = None
+    if a.geoms_file:  # recorded launches: their geometries, and per geometry only the recorded modes
+        rec = json.loads(Path(a.geoms_file).read_text())
+        only = {}
+        for r in rec:
+            only.setdefault(ConvGeom(*r["geom"]), set()).add(r["mode"])
+        geoms = lambda G, N: list(only)  # noqa: E731
+    for G in (a.groups if a.model != "llama288" and only is None else [1]):
         for g in geoms(G, a.batch):
             x = torch.randn(g.G, g.N, g.H, g.W, g.C, device=dev)
             w = torch.randn(g.G, g.K, g.R, g.S, g.C, device=dev) * 0.05
@@ -150,7 +159,9 @@ def main():
             dw = torch.zeros_like(w)
             flops = 2 * g.G * g.N * g.P * g.Q * g.K * g.R * g.S * g.C
             for mode, name in ((F32.F_FWD, "fwd"), (F32.F_DGRAD, "dgrad"), (F32.F_WGRAD, "wgrad")):
-                if mode == F32.F_DGRAD and g.C in (32, 160) and g.R == 1:
+                if only is not None and name not in only[g]:
+                    continue
+                if only is None and mode == F32.F_DGRAD and g.C in (32, 160) and g.R == 1:
                     continue  # the (im2col'd) stem needs no input gradient
                 if a.skip_halo and (F32.uses_halo(mode, g) or (mode == F32.F_WGRAD and F32.uses_halo_wgrad(g))):
                     continue

@@ -140,3 +140,23 @@ def test_fp32_measured_halo_and_vendor_entries(monkeypatch):
         F32._TUNED = old_tuned
         F32.set_math(old_math)
         F32._PLANS.clear()
+
+
+def test_fp32_launch_record(tmp_path):
+    """DDL_F32_RECORD=<file>: the (mode, geometry) pairs a process planned are written at exit, in
+    the form scripts/conv_f32_tune.py --geoms-file reads."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    out = tmp_path / "rec.json"
+    code = ("from ddl25spring_amd.ops import functional_f32 as F32\n"
+            "from ddl25spring_amd.ops.functional import ConvGeom\n"
+            "g = ConvGeom(2, 4, 8, 8, 32, 64, 3, 3, 2, 1)\n"
+            "F32.plan(F32.F_FWD, g); F32.plan(F32.F_WGRAD, g); F32.plan(F32.F_FWD, g)\n")
+    subprocess.run([sys.executable, "-c", code], env=dict(os.environ, DDL_F32_RECORD=str(out)), check=True,
+                   cwd=str(Path(__file__).resolve().parent.parent), timeout=120)
+    rec = json.loads(out.read_text())
+    assert rec == [{"mode": "fwd", "geom": [2, 4, 8, 8, 32, 64, 3, 3, 2, 1]},
+                   {"mode": "wgrad", "geom": [2, 4, 8, 8, 32, 64, 3, 3, 2, 1]}]
