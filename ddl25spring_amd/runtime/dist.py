@@ -202,6 +202,14 @@ def probe_ipc_threshold(ctx: DistContext, sizes=PROBE_SIZES, iters: int = 5) -> 
     times = torch.zeros(2, len(sizes), dtype=torch.float64, device=dev)
     try:
         for j, nb in enumerate(sizes):
+            # correctness first: a peer path that reads stale or unmapped memory must lose the probe
+            # (rank + 1 summed over ranks: small integers, exact in fp32)
+            y = torch.full((nb // 4,), float(ctx.rank + 1), dtype=torch.float32, device=dev)
+            ctx.ipc.all_reduce(y)
+            torch.cuda.synchronize(dev)
+            want = float(ctx.world * (ctx.world + 1) // 2)
+            if not bool((y == want).all()):
+                raise RuntimeError(f"peer-read all-reduce of {nb} B returned wrong sums")
             x = torch.ones(nb // 4, dtype=torch.float32, device=dev)
             for path in (0, 1):
                 run = (lambda: ctx.ipc.all_reduce(x)) if path == 0 else (lambda: dist.all_reduce(x))
