@@ -497,6 +497,47 @@ __device__ __forceinline__ void stage_rows_p(float* img, const float* base, long
   }
 }
 
+// Stage rows r0..r0+63 of one (b, h) TRANSPOSED into LDS imgT[HD][ATT_R + 4] (rows >= S zero), so
+// a lane reads 4 consecutive rows of one dim as one float4 (accum_rows_t).
+template <int HD>
+__device__ __forceinline__ void stage_rows_t(float* imgT, const float* base, long long rstride, int r0, int S,
+                                             const float* cosb = nullptr, const float* sinb = nullptr,
+                                             bool rope = false) {
+  constexpr int N4 = ATT_R * HD / 4, KP = ATT_R + 4;
+  for (int e = threadIdx.x; e < N4; e += 256) {
+    const int r = e % ATT_R, d = (e / ATT_R) * 4;  // consecutive threads: consecutive rows
+    const int row = r0 + r;
+    float4 v = row < S ? *(const float4*)(base + row * rstride + d) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (rope && row < S) {
+      const float* cs = cosb + (long long)row * (HD / 2) + d / 2;
+      const float* sn = sinb + (long long)row * (HD / 2) + d / 2;
+      const float a0 = v.x * cs[0] - v.y * sn[0], a1 = v.x * sn[0] + v.y * cs[0];
+      const float b0 = v.z * cs[1] - v.w * sn[1], b1 = v.z * sn[1] + v.w * cs[1];
+      v = make_float4(a0, a1, b0, b1);
+    }
+    imgT[(d + 0) * KP + r] = v.x;
+    imgT[(d + 1) * KP + r] = v.y;
+    imgT[(d + 2) * KP + r] = v.z;
+    imgT[(d + 3) * KP + r] = v.w;
+  }
+}
+
+// accum_rows over a transposed tile: acc[db] += sum_j tileT[16 db + n][rb + 4g + j] * w_j, the four
+// rows of a lane in one float4 read (accum_rows: one scalar LDS read per MFMA)
+template <int HD>
+__device__ __forceinline__ void accum_rows_t(f4m (&acc)[HD / 16], const float* tileT, int rb, const float (&w)[4],
+                                             int g, int n) {
+  constexpr int KP = ATT_R + 4;
+#pragma unroll
+  for (int db = 0; db < HD / 16; ++db) {
+    const float4 t = *(const float4*)(tileT + (16 * db + n) * KP + rb + 4 * g);
+    acc[db] = mfma4(t.x, w[0], acc[db]);
+    acc[db] = mfma4(t.y, w[1], acc[db]);
+    acc[db] = mfma4(t.z, w[2], acc[db]);
+    acc[db] = mfma4(t.w, w[3], acc[db]);
+  }
+}
+
 // a lane's own slice: row `row` (clamped), dims [(HD/4) g, (HD/4)(g+1)), optionally rotated
 template <int HD>
 __device__ __forceinline__ void own_slice(float (&v)[HD / 4], const float* base, long long rstride, int row, int g,
@@ -563,8 +604,8 @@ __global__ __launch_bounds__(256) void attnf_fwd_kernel(const float* __restrict_
                                                         float* __restrict__ lse, const float* __restrict__ cosb,
                                                         const float* __restrict__ sinb, int S, int H,
                                                         float sl2) {
-  constexpr int HP = HD + 4, NDB = HD / 16;
-  __shared__ __attribute__((aligned(16))) float Ks[ATT_R * HP], Vs[ATT_R * HP];
+  constexpr int HP = HD + 4, NDB = HD / 16, KP = ATT_R + 4;
+  __shared__ __attribute__((aligned(16))) float Ks[ATT_R * HP], Vt[HD * KP];
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, n = lane & 15;
   const int q = qb * ATT_R + 16 * w + n, qc = min(q, S - 1);
@@ -581,32 +622,44 @@ __global__ __launch_bounds__(256) void attnf_fwd_kernel(const float* __restrict_
   for (int kt = 0; kt <= qb; ++kt) {
     __syncthreads();
     stage_rows_p<HD>(Ks, kbase, rs, kt * ATT_R, S, cosb, sinb, true);
-    stage_rows_p<HD>(Vs, vbase, rs, kt * ATT_R, S, cosb, sinb, false);
+    stage_rows_t<HD>(Vt, vbase, rs, kt * ATT_R, S);
     __syncthreads();
-    const int nu = kt < qb ? 4 : w + 1;  // 16-key sub-tiles at or below this wave's diagonal
-    for (int u = 0; u < nu; ++u) {
-      const f4m st = dot_block<HD>(Ks + (16 * u + n) * HP, qf, g);  // S^T[key 4g+i][query n]
-      float sc[4], tmax = -INFINITY;
+    // the tile's 16-key sub-tiles at or below this wave's diagonal: all scores first, then one
+    // max / sum exchange per 64-key tile (per 16-key sub-tile: four cross-lane shuffles each)
+    const int nu = kt < qb ? 4 : w + 1;
+    float sc[4][4], tmax = -INFINITY;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = kt * ATT_R + 16 * u + 4 * g + i;
-        sc[i] = (key <= q && key < S) ? st[i] * sl2 : -INFINITY;
-        tmax = fmaxf(tmax, sc[i]);
+    for (int u = 0; u < 4; ++u) {
+      if (u < nu) {
+        const f4m st = dot_block<HD>(Ks + (16 * u + n) * HP, qf, g);  // S^T[key 4g+i][query n]
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = kt * ATT_R + 16 * u + 4 * g + i;
+          sc[u][i] = (key <= q && key < S) ? st[i] * sl2 : -INFINITY;
+          tmax = fmaxf(tmax, sc[u][i]);
+        }
       }
-      const float nm = fmaxf(mx, colmax(tmax));  // finite: key 0 is valid for every query
-      const float corr = exp2f(mx - nm);
-      float p[4], ps = 0.f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        p[i] = exp2f(sc[i] - nm);
-        ps += p[i];
-      }
-      l = l * corr + colsum(ps);
-      mx = nm;
-#pragma unroll
-      for (int db = 0; db < NDB; ++db) oacc[db] *= corr;
-      accum_rows<HD>(oacc, Vs, 16 * u, p, g, n);  // O^T[d][query n] += V^T P^T
     }
+    const float nm = fmaxf(mx, colmax(tmax));  // finite: key 0 is valid for every query
+    const float corr = exp2f(mx - nm);
+    float p[4][4], ps = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (u < nu) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          p[u][i] = exp2f(sc[u][i] - nm);
+          ps += p[u][i];
+        }
+      }
+    }
+    l = l * corr + colsum(ps);
+    mx = nm;
+#pragma unroll
+    for (int db = 0; db < NDB; ++db) oacc[db] *= corr;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (u < nu) accum_rows_t<HD>(oacc, Vt, 16 * u, p[u], g, n);  // O^T[d][query n] += V^T P^T
   }
   if (q >= S) return;
   store_blocks<HD>(o + ((long long)(b * S + q) * H + h) * HD, oacc, g, 1.f / l, nullptr, nullptr);
