@@ -85,45 +85,51 @@ __device__ __forceinline__ void slot_fold(const float* __restrict__ base, int S,
   }
 }
 
-// Chan's parallel merge of per-tile (sum, M2) slots, fixed order, in double: mean = sum S0 / M,
-// M2 = sum M2_i + sum (S0_i - n_i mean)^2 / n_i, n_i = min(rows, M - i * rows). Two slot passes.
+// Chan's parallel merge of per-tile (sum, M2) slots, fixed order, in double, ONE slot pass:
+// mean = sum S0 / M, M2 = sum M2_i + (sum S0_i^2 / n_i - (sum S0)^2 / M), n_i = min(rows, M - i * rows)
+// (the between-tile term sum n_i (mean_i - mean)^2 expanded: in double its cancellation costs
+// ~1e-16 * mean^2 / var relative, where the two-pass form waited out a second round of slot loads).
+// red: NSG * 96 doubles.
 __device__ __forceinline__ void slot_fold_chan(const float* __restrict__ base, int S, int C, int c, bool valid,
                                                double* red, long long M, int rows, double& mean, double& m2) {
-  double t0, t1;
-  slot_fold(base, S, C, c, valid, red, t0, t1);  // t0 = sum S0, t1 = sum M2 (on sg == 0)
   const int sg = threadIdx.x >> 5, cl = threadIdx.x & 31;
-  __syncthreads();
-  if (sg == 0) red[cl] = t0 / (double)M;
-  __syncthreads();
-  const double mu = red[cl];
-  __syncthreads();
-  double a = 0.0;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
   if (valid) {
-    auto term = [&](int k, float s0) {
+    auto term = [&](int k, float s0, float q) {
+      a0 += s0;
+      a1 += q;
       const long long rem = M - (long long)k * rows;
       const double n = (double)(rem < rows ? rem : rows);
-      if (n <= 0.0) return;
-      const double d = (double)s0 - n * mu;
-      a += d * d / n;
+      if (n > 0.0) a2 += (double)s0 * (double)s0 / n;
     };
     int k = sg;
-    for (; k + 7 * NSG < S; k += 8 * NSG) {  // loads ahead, terms in slot order
-      float xs[8];
+    for (; k + 7 * NSG < S; k += 8 * NSG) {  // 8 slots' loads in flight per thread, added in slot order
+      float xs[8], ys[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) xs[j] = base[(long long)(k + j * NSG) * 2 * C + c];
+      for (int j = 0; j < 8; ++j) {
+        xs[j] = base[(long long)(k + j * NSG) * 2 * C + c];
+        ys[j] = base[(long long)(k + j * NSG) * 2 * C + C + c];
+      }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) term(k + j * NSG, xs[j]);
+      for (int j = 0; j < 8; ++j) term(k + j * NSG, xs[j], ys[j]);
     }
-    for (; k < S; k += NSG) term(k, base[(long long)k * 2 * C + c]);
+    for (; k < S; k += NSG) term(k, base[(long long)k * 2 * C + c], base[(long long)k * 2 * C + C + c]);
   }
-  red[sg * 64 + cl] = a;
+  red[sg * 96 + cl] = a0;
+  red[sg * 96 + 32 + cl] = a1;
+  red[sg * 96 + 64 + cl] = a2;
   __syncthreads();
-  double b = 0.0;
+  mean = m2 = 0.0;
   if (sg == 0) {
-    for (int k = 0; k < NSG; ++k) b += red[k * 64 + cl];
+    double t0 = 0.0, t1 = 0.0, t2 = 0.0;
+    for (int j = 0; j < NSG; ++j) {
+      t0 += red[j * 96 + cl];
+      t1 += red[j * 96 + 32 + cl];
+      t2 += red[j * 96 + 64 + cl];
+    }
+    mean = t0 / (double)M;
+    m2 = t1 + (t2 - t0 * t0 / (double)M);
   }
-  mean = mu;
-  m2 = t1 + b;
 }
 
 __device__ __forceinline__ void bnf_finalize_body(const BNFArgs& a, double* red) {
@@ -173,7 +179,7 @@ __device__ __forceinline__ void bnf_finalize_body(const BNFArgs& a, double* red)
 }
 
 __global__ __launch_bounds__(FOLD_T) void bnf_finalize_kernel(BNFArgs a, BNFArgs b) {
-  __shared__ double red[NSG * 64];
+  __shared__ double red[NSG * 96];  // slot_fold_chan's three partials (slot_fold uses the first 64)
   bnf_finalize_body(blockIdx.z ? b : a, red);
 }
 
