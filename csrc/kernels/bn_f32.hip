@@ -435,7 +435,10 @@ __global__ __launch_bounds__(FOLD_T) void bnf_fold_kernel(BNFBwdArgs a, BNFBwdAr
 // block order and derives the coefficients. Both levels are small blocks that fit beside the
 // side-stream WGRAD's resident workgroups (the one-level fold's 1024-thread blocks waited for a
 // whole CU to drain: ~100 us per fold inside the overlapped backward).
-constexpr int FB_SG = 8, FB_SB = 64;
+#ifndef BNF_FB_SB
+#define BNF_FB_SB 64
+#endif
+constexpr int FB_SG = 8, FB_SB = BNF_FB_SB;
 
 __global__ __launch_bounds__(256) void bnf_fold_part_kernel(BNFBwdArgs a, BNFBwdArgs b, int C, int nb) {
   const BNFBwdArgs& t = blockIdx.z ? b : a;
