@@ -17,10 +17,13 @@
 __global__ void weighted_sum_kernel(const float* __restrict__ src, long long ld,
                                     const float* __restrict__ coeff, int G, long long n,
                                     float* __restrict__ out, int accumulate) {
+  // float4 path only when every row start and the output are 16-B aligned (a sub-slice of a
+  // flat buffer passed as `out` / `src` need not be)
+  const bool vec = (ld % 4) == 0 && (((uintptr_t)out | (uintptr_t)src) & 15) == 0;
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t * 4 < n;
        t += (long long)gridDim.x * blockDim.x) {
     const long long e = t * 4;
-    if (e + 4 <= n && (ld % 4) == 0) {
+    if (e + 4 <= n && vec) {
       float4 acc = accumulate ? *(const float4*)(out + e) : make_float4(0, 0, 0, 0);
       // products rounded, then added in client order (no fused multiply-add): the same bits as
       // clients spread over ranks (each rank's product, then the all-reduce add) for 2 ranks, and

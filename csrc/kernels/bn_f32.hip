@@ -561,6 +561,11 @@ __global__ __launch_bounds__(256) void bnf_fold_one_kernel(BNFBwdArgs a, BNFBwdA
     __hip_atomic_store((unsigned long long*)(w + C + c), __double_as_longlong(t1), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   }
+  // Hand-off (cdna_hip_programming.md 'Projection GEMM at M = 256' item 2, the sc1 form): the
+  // partials above are agent-scope atomic stores (write-through, no release fence needed), every
+  // storing wave drains them before the workgroup's one relaxed agent-scope arrival, and the last
+  // arriver acquires (agent fence) before its plain loads. Counters are per device and shared by
+  // all folds, so every fold must run on one stream (functional_f32._fold_tickets).
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the arrival
   __syncthreads();
   if (threadIdx.x == 0) {

@@ -544,13 +544,28 @@ class PresplitScope:
         self.state = "ready"
 
 
+def _store_identity(owner):
+    """(data_ptr, numel, storage id) of the owner's weight store: the scope's image keys are raw
+    weight pointers, valid only while the store they point into is the same allocation."""
+    store = getattr(owner, "store", None)
+    data = getattr(store, "data", None)
+    if data is None:
+        return None
+    return data.data_ptr(), data.numel(), id(data.untyped_storage())
+
+
 def presplit_scope(owner) -> "PresplitScope | contextlib.nullcontext":
     """The owner's (a Net's) PresplitScope for one training step (a no-op context off the fp32
-    device path or with DDL_F32_PRESPLIT=0)."""
+    device path or with DDL_F32_PRESPLIT=0). A scope is rebuilt (re-recorded) whenever the owner's
+    weight store was re-materialised since it recorded: its persistent images and descriptor table
+    are keyed on the old weight pointers, which a reallocation would turn into reads of freed
+    memory (or, worse, of a new tensor the allocator placed at the same address)."""
+    sig = _store_identity(owner)
     sc = getattr(owner, "_f32_presplit", None)
-    if sc is None:
+    if sc is None or getattr(owner, "_f32_presplit_sig", None) != sig:
         sc = PresplitScope()
         owner._f32_presplit = sc
+        owner._f32_presplit_sig = sig
     return sc
 
 
@@ -823,7 +838,9 @@ def _dev_key(device) -> str:
 
 def _fold_tickets(device, n: int) -> int:
     """Zeroed arrival counters of the one-launch fold, one buffer per device: every fold returns
-    its counters to zero, so the BN backwards (all on the step's main stream) share them.
+    its counters to zero, so the BN backwards share them — which requires every fold of a device
+    to run on ONE stream (they do: the step's main stream, eager or captured; the side stream only
+    carries conv WGRADs). ``fold_tickets_clean`` checks the invariant after a step (tests).
     Allocated eagerly with the split-K workspace (a first use inside a graph capture raises)."""
     key = _dev_key(device)
     buf = _TICKETS.get(key)
@@ -836,6 +853,13 @@ def _fold_tickets(device, n: int) -> int:
     if n > buf.numel():
         raise ValueError(f"BN fold needs {n} counters (> {buf.numel()})")
     return buf.data_ptr()
+
+
+def fold_tickets_clean() -> bool:
+    """Debug check: every BN-fold arrival counter is back to zero (a fold that was aborted, or two
+    folds racing on one counter set, would leave counts behind and corrupt later coefficients)."""
+    torch.cuda.synchronize()
+    return all(int(b.abs().sum().item()) == 0 for b in _TICKETS.values())
 
 
 def bn_backward(dy, ymask, x, mean, rstd, gamma, dgamma=None, dbeta=None, emit_dym=False, part=None):

@@ -8,22 +8,24 @@ device tensors of dtype float32 here; the bf16 ops stay the opt-in fast path. Ev
 deterministic (no float atomics: slot / block partials folded in a fixed order), so an fp32 LLaMA
 step gives the same bits run to run.
 
-  linear      y = x W^T (+ b) (+ residual): a 1x1 fp32 convolution over T = tokens "pixels"
-              (FWD on conv_f32, dX = DGRAD, dW = WGRAD accumulated straight into a fused grad sink);
-              shapes the conv engine does not take (in % 16, out % 16) run on the exact-fp32
-              tabular GEMM (tabular.hip gemm_f32)
+  linear      y = x W^T (+ b) (+ residual): FWD, DGRAD and WGRAD on the X6 planes GEMM
+              (gemm_x6.hip; x, W, dY split once), dW accumulated straight into a fused grad sink;
+              per (mode, shape) the tuner may pin the X6 / exact-fp32 conv engine instead (a 1x1
+              conv over T "pixels"); shapes neither takes run on the exact-fp32 tabular GEMM
   rmsnorm     fork variant sums the residual branch's gradient in the backward kernel
   swiglu, embedding, causal RoPE attention, vocabulary cross-entropy
 """
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
 from . import _lib
 from . import functional as Fn
 from . import functional_f32 as F32
+from . import gemm_x6 as X6G
 from ._lib import check, ptr, stream
 
 vp, i32, i64, f32 = _lib.vp, _lib.i32, _lib.i64, _lib.f32
@@ -66,7 +68,41 @@ def conv_linear_ok(C: int, Kout: int) -> bool:
     return C % 16 == 0 and Kout % 16 == 0
 
 
+def x6g_ok(T: int, C: int, Kout: int) -> bool:
+    """Can the planes GEMM (ops/gemm_x6.py) run a linear T x C -> Kout (every extent % 8)?"""
+    return T % 8 == 0 and C % 8 == 0 and Kout % 8 == 0
+
+
+# Engine of each linear product (FWD / DGRAD / WGRAD), all native unless asked otherwise:
+#   "x6g"  the X6 GEMM on pre-split planes (gemm_x6.hip): x, W and dY are split ONCE per step and
+#          serve all three products (default);
+#   "conv" the X6 / exact-fp32 conv engine (conv_f32.hip) as a 1x1 conv over T "pixels", where the
+#          tuner measured it faster for a (mode, shape) ('lin:' entries of f32_plans.json, value
+#          "conv");
+#   "blas" the vendor fp32 GEMM (torch.mm -> hipBLASLt): opt-in A/B only (DDL_F32_LINEAR=blas, or
+#          the older DDL_F32_BLAS=1), never chosen by default.
+LINEAR = [os.environ.get("DDL_F32_LINEAR", "auto")]
+_MODES = ("fwd", "dgrad", "wgrad")
+
+
+def linear_engine(mode: int, T: int, C: int, Kout: int) -> str:
+    if LINEAR[0] in ("x6g", "conv", "blas"):
+        eng = LINEAR[0]
+    elif F32.BLAS[0] == "1":
+        eng = "blas"
+    else:
+        F32._tuned(mode, Fn.ConvGeom(1, T, 1, 1, C, Kout, 1, 1, 1, 0))  # loads the table
+        eng = F32._TUNED.get(f"lin:{_MODES[mode]}:{T},{C},{Kout}", "x6g")
+    if eng == "x6g" and not x6g_ok(T, C, Kout):
+        eng = "conv"
+    if eng == "conv" and not conv_linear_ok(C, Kout):
+        eng = "tab"
+    return eng
+
+
 class LinearF32(torch.autograd.Function):
+    """y = x W^T (+ b) (+ residual) at fp32, every product on a native kernel (see LINEAR)."""
+
     @staticmethod
     def forward(ctx, x, w, b, residual):
         C = x.shape[-1]
@@ -74,26 +110,34 @@ class LinearF32(torch.autograd.Function):
         x2 = x.reshape(-1, C).contiguous()
         T = x2.shape[0]
         wc = w.detach().contiguous()
-        ctx.conv = conv_linear_ok(C, Kout)
+        eng = [linear_engine(m, T, C, Kout) for m in range(3)]
+        ctx.eng = eng
         geom = Fn.ConvGeom(1, T, 1, 1, C, Kout, 1, 1, 1, 0)
         ctx.geom = geom
-        if ctx.conv and F32.vendor_gemm(F32.F_FWD, geom):  # tuned: the vendor fp32 GEMM is faster here
-            y = torch.mm(x2, wc.t()) if residual is None else \
-                torch.addmm(residual.reshape(T, Kout).float(), x2, wc.t())
-            if b is not None:
-                y.add_(b.detach().view(1, Kout))
-        elif ctx.conv:
-            res = residual.reshape(1, T, 1, 1, Kout).contiguous() if residual is not None else None
+        # planes: x for FWD / WGRAD, W for FWD / DGRAD (split once, kept for the backward)
+        px = X6G.split(x2) if "x6g" in (eng[0], eng[2]) else None
+        pw = X6G.split(wc) if "x6g" in (eng[0], eng[1]) else None
+        res2 = residual.reshape(T, Kout).float().contiguous() if residual is not None else None
+        bias = b.detach().contiguous() if b is not None else None
+        if eng[0] == "x6g":
+            y = torch.empty(T, Kout, dtype=torch.float32, device=x.device)
+            X6G.gemm(pw, False, px, False, y, residual=res2, bias=bias)
+        elif eng[0] == "blas":
+            y = torch.mm(x2, wc.t()) if res2 is None else torch.addmm(res2, x2, wc.t())
+            if bias is not None:
+                y.add_(bias.view(1, Kout))
+        elif eng[0] == "conv":
+            res = res2.view(1, T, 1, 1, Kout) if res2 is not None else None
             y = Fn.conv_fwd(x2.view(1, T, 1, 1, C), wc.view(1, Kout, 1, 1, C), geom,
-                            bias=None if b is None else b.detach().contiguous().view(1, Kout), residual=res)
+                            bias=None if bias is None else bias.view(1, Kout), residual=res)
         else:
             from .tabular_ops import gemm_f32
             y = torch.empty(T, Kout, dtype=torch.float32, device=x.device)
-            if residual is not None:
-                y.copy_(residual.reshape(T, Kout))
-            gemm_f32(x2, wc, y, T, Kout, C, C, 1, 1, C, bias=None if b is None else b.detach().contiguous(),
-                     accumulate=residual is not None)
+            if res2 is not None:
+                y.copy_(res2)
+            gemm_f32(x2, wc, y, T, Kout, C, C, 1, 1, C, bias=bias, accumulate=res2 is not None)
         ctx.save_for_backward(x2, wc)
+        ctx.px, ctx.pw = px, pw
         ctx.has_b, ctx.has_res, ctx.xshape, ctx.w = b is not None, residual is not None, x.shape, w
         return y.view(*x.shape[:-1], Kout)
 
@@ -106,41 +150,45 @@ class LinearF32(torch.autograd.Function):
         dx = dw = db = None
         want_dx, want_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         sink = _sink(ctx.w) if want_dw else None
-        if ctx.conv:
-            g = ctx.geom
-            dy5 = d2.view(1, T, 1, 1, Kout)
-            vd = want_dx and F32.vendor_gemm(F32.F_DGRAD, g)  # tuned per mode (functional_f32.vendor_gemm)
-            vw = want_dw and F32.vendor_gemm(F32.F_WGRAD, g)
-            if vd:
-                dx = torch.mm(d2, wc)
-            if want_dw:
-                dwt = sink.view(1, Kout, 1, 1, C) if sink is not None else \
-                    torch.zeros(1, Kout, 1, 1, C, dtype=torch.float32, device=dy.device)
-                if vw:
-                    dwt.view(Kout, C).addmm_(d2.t(), x2)
-                    if want_dx and not vd:
-                        dx = Fn.conv_dgrad(dy5, wc.view(1, Kout, 1, 1, C), g)
-                else:
-                    d = Fn.conv_dgrad_wgrad(dy5, wc.view(1, Kout, 1, 1, C), x2.view(1, T, 1, 1, C), g, dwt,
-                                            want_dx=want_dx and not vd)
-                    if not vd:
-                        dx = d
-                if sink is None:
-                    dw = dwt.view(Kout, C)
-            elif want_dx and not vd:
-                dx = Fn.conv_dgrad(dy5, wc.view(1, Kout, 1, 1, C), g)
-        else:
+        eng, g = ctx.eng, ctx.geom
+        ed, ew = eng[1] if want_dx else None, eng[2] if want_dw else None
+        pd = X6G.split(d2) if "x6g" in (ed, ew) else None
+        dy5 = d2.view(1, T, 1, 1, Kout)
+        if want_dw:
+            dwt = sink.view(Kout, C) if sink is not None else \
+                torch.zeros(Kout, C, dtype=torch.float32, device=dy.device)
+        # DGRAD and WGRAD sharing the conv engine run as one fused conv_dgrad_wgrad call
+        if ed == "conv" and ew == "conv":
+            dx = Fn.conv_dgrad_wgrad(dy5, wc.view(1, Kout, 1, 1, C), x2.view(1, T, 1, 1, C), g,
+                                     dwt.view(1, Kout, 1, 1, C), want_dx=True)
+            ed = ew = None
+        if ed == "x6g":
+            dx = torch.empty(T, C, dtype=torch.float32, device=dy.device)
+            X6G.gemm(ctx.pw, True, pd, False, dx)
+        elif ed == "blas":
+            dx = torch.mm(d2, wc)
+        elif ed == "conv":
+            dx = Fn.conv_dgrad(dy5, wc.view(1, Kout, 1, 1, C), g)
+        elif ed == "tab":
             from .tabular_ops import gemm_f32
-            if want_dx:
-                dx = torch.empty(T, C, dtype=torch.float32, device=dy.device)
-                gemm_f32(d2, wc, dx, T, C, Kout, Kout, 1, C, 1)
-            if want_dw:
-                tgt = sink if sink is not None else torch.zeros(Kout, C, dtype=torch.float32, device=dy.device)
-                gemm_f32(d2, x2, tgt, Kout, C, T, 1, Kout, C, 1, accumulate=True)
-                if sink is None:
-                    dw = tgt
-        if want_dw and sink is not None:
-            _ready(ctx.w)
+            dx = torch.empty(T, C, dtype=torch.float32, device=dy.device)
+            gemm_f32(d2, wc, dx, T, C, Kout, Kout, 1, C, 1)
+        if ew == "x6g":
+            X6G.gemm(ctx.px, True, pd, True, dwt, accumulate=True)
+        elif ew == "blas":
+            dwt.addmm_(d2.t(), x2)
+        elif ew == "conv":
+            Fn.conv_dgrad_wgrad(dy5, wc.view(1, Kout, 1, 1, C), x2.view(1, T, 1, 1, C), g,
+                                dwt.view(1, Kout, 1, 1, C), want_dx=False)
+        elif ew == "tab":
+            from .tabular_ops import gemm_f32
+            gemm_f32(d2, x2, dwt, Kout, C, T, 1, Kout, C, 1, accumulate=True)
+        ctx.px = ctx.pw = None
+        if want_dw:
+            if sink is not None:
+                _ready(ctx.w)
+            else:
+                dw = dwt
         if dx is not None:
             dx = dx.reshape(ctx.xshape)
         if ctx.has_b and ctx.needs_input_grad[2]:

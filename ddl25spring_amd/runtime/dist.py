@@ -191,48 +191,84 @@ def init(backend: str | None = None, device: str | None = None, rank: int | None
 PROBE_SIZES = (16 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20, 8 << 20)
 
 
+def _sync(dev) -> None:
+    if torch.device(dev).type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def _timed(run, iters: int, dev) -> float:
+    """Mean ms per call of ``run`` (device events on a GPU, wall clock on the CPU)."""
+    for _ in range(2):
+        run()
+    _sync(dev)
+    if torch.device(dev).type == "cuda":
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            run()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / iters
+    import time
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        run()
+    return (time.perf_counter() - t0) * 1e3 / iters
+
+
+def _agree_bad(bad: bool, dev) -> bool:
+    """Collective: True on EVERY rank when any rank reports a failure."""
+    flag = torch.tensor([1.0 if bad else 0.0], dtype=torch.float64, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    return flag.item() != 0.0
+
+
 def probe_ipc_threshold(ctx: DistContext, sizes=PROBE_SIZES, iters: int = 5) -> int:
     """Time the peer-read all-reduce against the process group's all-reduce (RCCL) at each size on
     every rank, take the slowest rank per (path, size) and keep the peer-read path up to the largest
     size below which it always won. Sets ctx.ipc_max_bytes / ctx.ipc_policy (identical on every
     rank: the decision is made on all-reduced timings) and releases the peer buffers when the
-    crossover is 0. Returns the threshold in bytes."""
+    crossover is 0. Returns the threshold in bytes.
+
+    Every rank issues the SAME sequence of process-group collectives whatever happens on the peer
+    path: per size, (1) a peer-path correctness check and (2) its timing each end in an agreed
+    failure flag (MAX over ranks) before anything else runs, so a rank that sees wrong sums or a
+    peer timeout leaves the loop at the same point as every other rank and the group falls back
+    to RCCL for every size (no mismatched collectives)."""
     sizes = [s for s in sizes if s <= ctx.ipc.cap]
     dev = ctx.device
     times = torch.zeros(2, len(sizes), dtype=torch.float64, device=dev)
-    try:
-        for j, nb in enumerate(sizes):
-            # correctness first: a peer path that reads stale or unmapped memory must lose the probe
-            # (rank + 1 summed over ranks: small integers, exact in fp32)
+    failed, err = False, ""
+    for j, nb in enumerate(sizes):
+        # correctness first: a peer path that reads stale or unmapped memory must lose the probe
+        # (rank + 1 summed over ranks: small integers, exact in fp32)
+        bad = False
+        try:
             y = torch.full((nb // 4,), float(ctx.rank + 1), dtype=torch.float32, device=dev)
             ctx.ipc.all_reduce(y)
-            torch.cuda.synchronize(dev)
+            _sync(dev)
             want = float(ctx.world * (ctx.world + 1) // 2)
             if not bool((y == want).all()):
-                raise RuntimeError(f"peer-read all-reduce of {nb} B returned wrong sums")
-            x = torch.ones(nb // 4, dtype=torch.float32, device=dev)
-            for path in (0, 1):
-                run = (lambda: ctx.ipc.all_reduce(x)) if path == 0 else (lambda: dist.all_reduce(x))
-                for _ in range(2):
-                    run()
-                torch.cuda.synchronize(dev)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(iters):
-                    run()
-                e1.record()
-                e1.synchronize()
-                times[path, j] = e0.elapsed_time(e1) / iters
-        ctx.ipc.check()
-        ok = True
-    except Exception as e:  # a peer timed out / the kernel refused: RCCL for everything
-        ok = False
-        err = str(e)[:200]
-    flag = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=dev)
-    dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+                bad, err = True, f"peer-read all-reduce of {nb} B returned wrong sums"
+        except Exception as e:  # a peer timed out / the kernel refused
+            bad, err = True, str(e)[:200]
+        if _agree_bad(bad, dev):
+            failed = True
+            break
+        x = torch.ones(nb // 4, dtype=torch.float32, device=dev)
+        try:
+            times[0, j] = _timed(lambda: ctx.ipc.all_reduce(x), iters, dev)
+            if j == len(sizes) - 1:
+                ctx.ipc.check()
+        except Exception as e:
+            bad, err = True, str(e)[:200]
+        if _agree_bad(bad, dev):
+            failed = True
+            break
+        times[1, j] = _timed(lambda: dist.all_reduce(x), iters, dev)
     dist.all_reduce(times, op=dist.ReduceOp.MAX)
     thr = 0
-    if flag.item() == 0.0:
+    if not failed:
         for j, nb in enumerate(sizes):
             if times[0, j] < times[1, j]:
                 thr = nb
@@ -242,8 +278,8 @@ def probe_ipc_threshold(ctx: DistContext, sizes=PROBE_SIZES, iters: int = 5) -> 
     ctx.ipc_policy = {"mode": "auto", "ipc_threshold_bytes": thr,
                       "probe_ms": {str(nb): {"ipc": round(float(times[0, j]), 4), "rccl": round(float(times[1, j]), 4)}
                                    for j, nb in enumerate(sizes)}}
-    if flag.item() != 0.0:
-        ctx.ipc_policy["error"] = err if not ok else "a peer failed the probe"
+    if failed:
+        ctx.ipc_policy["error"] = err or "a peer failed the probe"
     if thr == 0:
         ctx.ipc.close()
         ctx.ipc = None
@@ -259,6 +295,25 @@ def allreduce_path(ctx: DistContext, nbytes: int) -> str:
 
 def context() -> DistContext:
     return _CTX if _CTX is not None else init()
+
+
+_BARRIER_GEN = [0]
+
+
+def _store_barrier(world: int, tag: str, timeout_s: float) -> None:
+    """A barrier through the rendezvous store with a deadline. Unlike a process-group barrier it
+    cannot hang when a peer died without raising here (an NCCL barrier would block until the
+    watchdog's timeout, or forever with async error handling off): it raises TimeoutError."""
+    import time
+    store = dist.distributed_c10d._get_default_store()
+    _BARRIER_GEN[0] += 1
+    key = f"ddl_barrier/{tag}/{_BARRIER_GEN[0]}"
+    store.add(key, 1)
+    deadline = time.monotonic() + timeout_s
+    while int(store.add(key, 0)) < world:
+        if time.monotonic() > deadline:
+            raise TimeoutError(f"store barrier {key}: peers missing after {timeout_s:.0f} s")
+        time.sleep(0.005)
 
 
 def shutdown():
@@ -278,7 +333,7 @@ def shutdown():
             # gloo groups can make that peer's transport thread throw (std::terminate -> SIGABRT)
             try:
                 if err is None and _CTX is not None and _CTX.is_distributed:
-                    _CTX.barrier()
+                    _store_barrier(_CTX.world, "teardown", float(os.environ.get("DDL_TEARDOWN_TIMEOUT", "60")))
             except Exception:  # noqa: BLE001 - best effort: a dead peer must not hang teardown
                 pass
             dist.destroy_process_group()
