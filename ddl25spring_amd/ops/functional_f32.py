@@ -262,11 +262,11 @@ def _tuned(mode: int, g):
     return None if p is None else (cfg_of(p[0], p[1]), int(p[2]))
 
 
-# Plain-GEMM callers (the fp32 LLaMA linears) may run a product on the vendor fp32 GEMM (torch.mm ->
-# hipBLASLt, true fp32 MFMA) where the tuner measured it faster than both native engines: "blas:"
-# entries of f32_plans.json (scripts/conv_f32_tune.py --model llama288). DDL_F32_BLAS: auto (the
-# table), 0 (never), 1 (always).
-BLAS = [os.environ.get("DDL_F32_BLAS", "auto")]
+# The vendor fp32 GEMM (torch.mm -> hipBLASLt) for plain-GEMM callers is an opt-in A/B only:
+# DDL_F32_BLAS=1 (always) or "auto" (where a "blas:" entry of the plan table says so; the shipped
+# table has none since round 6: every fp32 LLaMA linear product runs a native engine, see
+# ops/llama_f32.py LINEAR). Default 0: never.
+BLAS = [os.environ.get("DDL_F32_BLAS", "0")]
 
 
 def vendor_gemm(mode: int, g) -> bool:

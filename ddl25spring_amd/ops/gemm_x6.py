@@ -100,6 +100,8 @@ def plan(M: int, N: int, K: int) -> tuple[int, int, int, int]:
     if _FORCE:
         tp, tq, ns, sp = (int(v) for v in _FORCE.split(","))
         p = (tp, tq, ns, sp)
+    elif _tuned_plan(M, N, K) is not None:
+        p = _tuned_plan(M, N, K)
     else:
         tp = 3 if (M % 96 == 0 and M <= 384) else 4
         tq = 4
@@ -111,6 +113,21 @@ def plan(M: int, N: int, K: int) -> tuple[int, int, int, int]:
         p = (tp, tq, _NS or (3 if tq == 4 else 4), sp)
     _PLANS[key] = p
     return p
+
+
+def _tuned_plan(M: int, N: int, K: int):
+    """A measured plan ('x6g:M,N,K' entries of f32_plans.json, scripts/llm_linear_tune_x6g.py)."""
+    from . import functional_f32 as F32
+    F32._tuned(F32.F_FWD, _GEOM_PROBE)  # loads the table
+    v = F32._TUNED.get(f"x6g:{M},{N},{K}")
+    return None if v is None else tuple(int(t) for t in v)
+
+
+class _GeomProbe:  # any geometry: _tuned() only needs one to load the table
+    G = N = H = W = C = K = R = S = P = Q = stride = pad = 1
+
+
+_GEOM_PROBE = _GeomProbe()
 
 
 def _extent(pl: Planes, mn: bool) -> tuple[int, int]:

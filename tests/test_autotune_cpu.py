@@ -115,8 +115,8 @@ def test_flat1x1_launch_geometry(monkeypatch):
 
 def test_fp32_measured_halo_and_vendor_entries(monkeypatch):
     """'x6h:' table entries set the halo plan (unless TARGET_WG = 1 pins split-K off), and 'blas:'
-    entries route one product of a plain-GEMM linear to the vendor fp32 GEMM (DDL_F32_BLAS 0 / 1
-    override the table)."""
+    entries route one product of a plain-GEMM linear to the vendor fp32 GEMM only as an opt-in
+    (DDL_F32_BLAS=auto; the default 0 never does, 1 always)."""
     from ddl25spring_amd.ops import functional_f32 as F32
     from ddl25spring_amd.ops.functional import ConvGeom
     g = ConvGeom(3, 7, 8, 8, 16, 16, 3, 3, 1, 1)
@@ -131,6 +131,8 @@ def test_fp32_measured_halo_and_vendor_entries(monkeypatch):
         monkeypatch.setattr(F32, "TARGET_WG", 1)
         F32._PLANS.clear()
         assert F32.plan(F32.F_FWD, g)[1] == 1
+        assert not F32.vendor_gemm(F32.F_DGRAD, lin)  # default DDL_F32_BLAS=0: never the vendor GEMM
+        monkeypatch.setattr(F32, "BLAS", ["auto"])
         assert F32.vendor_gemm(F32.F_DGRAD, lin) and not F32.vendor_gemm(F32.F_FWD, lin)
         monkeypatch.setattr(F32, "BLAS", ["0"])
         assert not F32.vendor_gemm(F32.F_DGRAD, lin)
