@@ -17,6 +17,10 @@
 __global__ void weighted_sum_kernel(const float* __restrict__ src, long long ld,
                                     const float* __restrict__ coeff, int G, long long n,
                                     float* __restrict__ out, int accumulate) {
+  // every product rounded on its own, then added: hipcc contracts a * b + c into an fma by default
+  // (also through __fmul_rn / __fadd_rn, whose header bodies carry the contract flag), which made the
+  // G-row single-process sum differ from per-rank partials summed across ranks
+#pragma clang fp contract(off)
   // float4 path only when every row start and the output are 16-B aligned (a sub-slice of a
   // flat buffer passed as `out` / `src` need not be)
   const bool vec = (ld % 4) == 0 && (((uintptr_t)out | (uintptr_t)src) & 15) == 0;
@@ -31,14 +35,14 @@ __global__ void weighted_sum_kernel(const float* __restrict__ src, long long ld,
       for (int g = 0; g < G; ++g) {
         const float c = coeff[g];
         const float4 v = *(const float4*)(src + g * ld + e);
-        acc.x = __fadd_rn(acc.x, __fmul_rn(c, v.x)); acc.y = __fadd_rn(acc.y, __fmul_rn(c, v.y));
-        acc.z = __fadd_rn(acc.z, __fmul_rn(c, v.z)); acc.w = __fadd_rn(acc.w, __fmul_rn(c, v.w));
+        acc.x = acc.x + c * v.x; acc.y = acc.y + c * v.y;  // no contraction: see the pragma
+        acc.z = acc.z + c * v.z; acc.w = acc.w + c * v.w;
       }
       *(float4*)(out + e) = acc;
     } else {
       for (long long k = e; k < min(n, e + 4); ++k) {
         float acc = accumulate ? out[k] : 0.f;
-        for (int g = 0; g < G; ++g) acc = __fadd_rn(acc, __fmul_rn(coeff[g], src[g * ld + k]));
+        for (int g = 0; g < G; ++g) acc = acc + coeff[g] * src[g * ld + k];
         out[k] = acc;
       }
     }

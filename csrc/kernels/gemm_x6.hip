@@ -5,7 +5,8 @@
 // lab/tutorial_1b/DP/gradient_aggr/intro_DP_GA.py:27-28,47-51) run here instead of a vendor GEMM.
 //
 // Operands are PRE-SPLIT "planes": an fp32 matrix X[R][C] becomes three bf16 matrices h, m, l of the
-// same shape (x = h + m + l exactly; x6_planes_kernel below), stored plane after plane. A GEMM
+// same shape (x = h + m + l exactly; x6_planes_kernel below), stored plane after plane, each
+// zero-padded to whole 32-row / 32-column multiples (a partial last reduction stage reads zeros). A GEMM
 // operand reads them in whichever orientation the product needs, without a transpose pass:
 //   * K-major (the reduction index is the contiguous one: X[p][k]) -> LDS image [plane][rows][16 k],
 //     fragments by ds_read_b64;
@@ -17,8 +18,9 @@
 // Per 16-deep reduction step and 16x16 tile, three v_mfma_f32_16x16x32_bf16 (lane group g = the
 // four k values 4g..4g+3, fragment halves assembled in registers from the plane reads):
 //   A (l | h) . B (h | m) = lh + hm      A (h | m) . B (l | h) = hl + mh      A (h | m) . B (h | m) = hh + mm
-// chained from zero (smallest products first), then ONE IEEE add into the fp32 accumulator (the
-// rounding discipline of conv_f32.hip: the MFMA's internal sum is not an RNE fp32 chain).
+// chained from zero (smallest products first) over four steps (64 reduction values), then ONE IEEE
+// add into the fp32 accumulator (the rounding discipline of conv_f32.hip / conv_x6h.hip: the
+// MFMA's internal sum is not an RNE fp32 chain, so chains stay short).
 //
 // Staging: LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB per wave-instruction, lane-linear destination,
 // 16-B chunk XOR swizzles applied by permuting each lane's SOURCE chunk) into an NS-deep ring, one
@@ -75,6 +77,13 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+}
+
+// One LDS-DMA piece (16 B per lane to lds + 16 * lane; byte offset off + soff). Kept out of the
+// kernel body: inline in a __global__ template (address-space cast, runtime scalar offset) the host
+// pass silently drops the kernel's launch stub (conv_x6h.hip dma16).
+__device__ __forceinline__ void dma16(const __amdgpu_buffer_rsrc_t& rs, char* lds, unsigned off, unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds, 16, off, soff, 0, 0);
 }
 
 // LDS byte address of a __shared__ object (kept out of the kernel templates: with the address-space
@@ -183,28 +192,30 @@ __global__ __launch_bounds__(256, 1) void gemm_x6_kernel(GemmX6Args a) {
   for (int i = 0; i < OA::PW; ++i) sa[i] = src_base(OA{}, wsc + 4 * i, p0, a.M, a.lda, a.a_ps, ka[i]);
 #pragma unroll
   for (int i = 0; i < OB::PW; ++i) sb[i] = src_base(OB{}, wsc + 4 * i, q0, a.N, a.ldb, a.b_ps, kb[i]);
+  // 32-bit per-lane byte offsets at stage 0 (invalid rows / columns: OOBV) and the stage advance in
+  // the SCALAR offset: a piece costs no VALU. The planes are zero-padded to whole 32-deep stages
+  // along the reduction (ops/gemm_x6.py split), so a partial last stage needs no per-lane k test.
+  // Stages past the slice take the scalar offset OOBS: every wave issues the same, constant number
+  // of pieces per stage (constant vmcnt waits, no branch). Images are < 2^30 B (host-checked), so
+  // OOBV + any advance and any valid offset + OOBS both stay in [2^30, 2^31): past the range.
+  constexpr unsigned OOBV = 0x40000000u, OOBS = 0x40000000u;
+  unsigned va[OA::PW], vb[OB::PW];
+#pragma unroll
+  for (int i = 0; i < OA::PW; ++i) va[i] = sa[i] >= 0 ? (unsigned)(sa[i] * 2) : OOBV;
+#pragma unroll
+  for (int i = 0; i < OB::PW; ++i) vb[i] = sb[i] >= 0 ? (unsigned)(sb[i] * 2) : OOBV;
+  const unsigned a_adv = AMN ? (unsigned)(XBK * a.lda * 2) : (unsigned)(XBK * 2);  // bytes per stage
+  const unsigned b_adv = BMN ? (unsigned)(XBK * a.ldb * 2) : (unsigned)(XBK * 2);
 
-  // DMA piece d (0 .. OPS-1: this wave's A pieces, then its B pieces) of stage kt into `slot`.
-  // Stages past the slice read out of range (zeros): every wave issues the same, constant number
-  // of pieces per stage, so the vmcnt waits are constants and the issue needs no branch.
+  // DMA piece d (0 .. OPS-1: this wave's A pieces, then its B pieces) of stage kt into `slot`
   auto dma_piece = [&](int d, int kt, int slot) {
     char* base = smem + slot * STAGE;
-    const int k0 = kt * XBK;
     const bool kin = kt < kt1;
     if (d < OA::PW) {
-      long long e;
-      if constexpr (AMN) e = (kin && sa[d] >= 0 && k0 + ka[d] < a.K) ? sa[d] + (long long)k0 * a.lda : -1;
-      else e = (kin && sa[d] >= 0 && k0 + ka[d] < a.K) ? sa[d] + k0 : -1;
-      const unsigned off = e >= 0 ? (unsigned)(e * 2) : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(base + (wsc + 4 * d) * 1024), 16, off, 0, 0, 0);
+      dma16(rA, base + (wsc + 4 * d) * 1024, va[d], kin ? (unsigned)kt * a_adv : OOBS);
     } else {
       const int i = d - OA::PW;
-      long long e;
-      if constexpr (BMN) e = (kin && sb[i] >= 0 && k0 + kb[i] < a.K) ? sb[i] + (long long)k0 * a.ldb : -1;
-      else e = (kin && sb[i] >= 0 && k0 + kb[i] < a.K) ? sb[i] + k0 : -1;
-      const unsigned off = e >= 0 ? (unsigned)(e * 2) : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(base + OA::BYTES + (wsc + 4 * i) * 1024), 16, off,
-                                               0, 0, 0);
+      dma16(rB, base + OA::BYTES + (wsc + 4 * i) * 1024, vb[i], kin ? (unsigned)kt * b_adv : OOBS);
     }
   };
 
@@ -325,15 +336,23 @@ __global__ __launch_bounds__(256, 1) void gemm_x6_kernel(GemmX6Args a) {
     raw_barrier();
 #pragma unroll
     for (int c = 0; c < NC; ++c) read_frag(c, 0, 0, fa0, fb0);
-    for (int i = 0; i < nk; ++i) {
+    // one stage: its two 16-deep steps; the MFMA chain runs over TWO stages (four steps, 12 piece
+    // products per tile) before its IEEE add
+    auto iter = [&](int i, bool first, bool last) {
       const int slot = i % NS, nslot = (i + 1) % NS;
       lgkm_wait();  // step 0's fragments
-      step(fa0, fb0, true, false, slot, 1, fa1, fb1, false, 0, 0);
+      step(fa0, fb0, first, false, slot, 1, fa1, fb1, false, 0, 0);
       wait_vm<(NS - 2) * OPS>();
       lgkm_wait();  // step 1's fragments (before the barrier: the slot's last reads)
       raw_barrier();
-      step(fa1, fb1, false, true, nslot, 0, fa0, fb0, true, kt0 + i + NS, slot);
+      step(fa1, fb1, false, last, nslot, 0, fa0, fb0, true, kt0 + i + NS, slot);
+    };
+    int i = 0;
+    for (; i + 1 < nk; i += 2) {
+      iter(i, true, false);
+      iter(i + 1, false, true);
     }
+    if (i < nk) iter(i, true, true);
     wait_vm<0>();  // the ring's trailing (zero-fill) pieces land before the LDS is reused
   }
 
@@ -426,13 +445,14 @@ __device__ __forceinline__ void split1(float x, uint16_t& h, uint16_t& m, uint16
 }
 
 __global__ __launch_bounds__(256) void x6_planes_kernel(const float* __restrict__ x, long long ld, bf16_t* out,
-                                                        long long ldp, long long ps, int R, int C) {
-  const int c8 = C / 8;
-  GSTRIDE_LOOP(t, (long long)R * c8) {
+                                                        long long ldp, long long ps, int R, int C, int Rp, int Cp) {
+  const int c8 = Cp / 8;
+  GSTRIDE_LOOP(t, (long long)Rp * c8) {
     const long long r = t / c8;
     const int c = (int)(t - r * c8) * 8;
-    const float4 v0 = *(const float4*)(x + r * ld + c);
-    const float4 v1 = *(const float4*)(x + r * ld + c + 4);
+    const bool in = r < R && c < C;  // the zero padding (to whole 32-deep GEMM stages) is written too
+    const float4 v0 = in ? *(const float4*)(x + r * ld + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 v1 = in ? *(const float4*)(x + r * ld + c + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
     const float e[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
     uint16_t h[8], m[8], l[8];
 #pragma unroll
@@ -486,7 +506,7 @@ DDL_API int ddl_gemm_x6(const GemmX6Args* ap, int cfg, hipStream_t s) {
   // chunk granularity: K-major operands need K % 8, MN-major ones their output extent % 8; float4 epilogue
   if (a.M % 8 || a.N % 8 || a.K % 8 || a.ldo % 4 || a.lda % 8 || a.ldb % 8 || a.a_ps % 8 || a.b_ps % 8)
     return (int)hipErrorInvalidValue;
-  if (a.a_ps * 6 >= (1LL << 31) || a.b_ps * 6 >= (1LL << 31)) return (int)hipErrorInvalidValue;
+  if (a.a_ps * 6 >= (1LL << 30) || a.b_ps * 6 >= (1LL << 30)) return (int)hipErrorInvalidValue;
   if (a.split_k < 1) a.split_k = 1;
   if (a.split_k > 1) {
     if (!a.partial || (long long)a.split_k * a.M * a.N > a.partial_cap) return (int)hipErrorInvalidValue;
@@ -502,11 +522,13 @@ DDL_API int ddl_gemm_x6(const GemmX6Args* ap, int cfg, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// planes of x [R][C] (pitch ld) as [3][Rp][Cp] (pitch ldp >= Cp, plane stride ps), zero-padded
 DDL_API int ddl_x6_planes(const float* x, long long ld, void* out, long long ldp, long long ps, int R, int C,
-                          hipStream_t s) {
-  if (R < 1 || C < 1 || C % 8 || ld % 4 || ldp % 8 || ps % 8) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(x6_planes_kernel, dim3(grid_for((long long)R * (C / 8), 256)), dim3(256), 0, s, x, ld,
-                     (bf16_t*)out, ldp, ps, R, C);
+                          int Rp, int Cp, hipStream_t s) {
+  if (R < 1 || C < 1 || C % 8 || Cp % 8 || Cp < C || Rp < R || ld % 4 || ldp % 8 || ldp < Cp || ps % 8)
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(x6_planes_kernel, dim3(grid_for((long long)Rp * (Cp / 8), 256)), dim3(256), 0, s, x, ld,
+                     (bf16_t*)out, ldp, ps, R, C, Rp, Cp);
   return (int)hipGetLastError();
 }
 

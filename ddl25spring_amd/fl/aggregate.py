@@ -2,10 +2,12 @@
 
 * ``MeanAggregator`` — FedAvg / FedSGD weighted mean ``sum_k (n_k / n) w_k`` (reference
   hfl_complete.py:370-378): per-GPU weighted row-reduction kernel (products rounded, added in client
-  order), then across the ranks either ONE all-reduce of P floats, or (``ordered``, the default) an
-  all-gather of the W partials added in rank order by the same kernel — so a run with one client
-  per GPU is bitwise the single-process multi-slot run (the 8-GPU headline layout reproduces the
-  1-GPU model exactly), at the price of W x P floats gathered instead of an all-reduce.
+  order), then across the ranks either ONE all-reduce of P floats, or (``ordered``, the default) a
+  rank-ORDER sum of the W partials — so a run with one client per GPU is bitwise the single-process
+  multi-slot run (the 8-GPU headline layout reproduces the 1-GPU model exactly). On one node the
+  ordered sum runs on the peer-read kernel over xGMI (runtime/ipc.py, slot-sized chunks, every
+  rank adds p0 + p1 + ... itself); without peer mappings (or on gloo) an all-gather of the W
+  partials added in rank order by the weighted-sum kernel.
 * Byzantine-robust aggregators [north-star; absent from the reference, announced in its
   README.md:89-92]: ``Krum`` / multi-Krum (Blanchard et al. 2017), coordinate-wise ``Median`` and
   ``TrimmedMean`` (Yin et al. 2018). They need every client vector, so they run *coordinate-
@@ -45,6 +47,12 @@ class MeanAggregator:
         if not self.ordered:
             ctx.all_reduce(out)
             return out
+        ipc = getattr(ctx, "ipc", None)
+        if ipc is not None and out.is_cuda and out.is_contiguous() and out.data_ptr() % 16 == 0:
+            # rank-order sum by peer reads over xGMI, in slot-sized chunks: the same bits as the
+            # all-gather + ordered add below, moving ~2P floats per GPU instead of W x P
+            ipc.all_reduce_ordered(out)
+            return out
         parts = ctx.all_gather_rows(out)  # [W, P]: every rank's partial, in rank order
         key = (parts.shape[0], out.device)
         ones = self._ones.get(key)
@@ -56,7 +64,11 @@ class MeanAggregator:
     def describe(self, ctx) -> str:
         if not ctx.is_distributed:
             return "local weighted sum"
-        return "rank-ordered all-gather + sum" if self.ordered else "all-reduce"
+        if not self.ordered:
+            return "all-reduce"
+        if getattr(ctx, "ipc", None) is not None:
+            return "ipc peer-read rank-ordered sum"
+        return "rank-ordered all-gather + sum"
 
 
 class _Sharded:

@@ -38,14 +38,22 @@ class GemmX6Args(ctypes.Structure):  # csrc/kernels/gemm_x6.hip GemmX6Args
 
 _lib.register_signatures({
     "ddl_gemm_x6": [vp, i32, vp],
-    "ddl_x6_planes": [vp, i64, vp, i64, i64, i32, i32, vp],
+    "ddl_x6_planes": [vp, i64, vp, i64, i64, i32, i32, i32, i32, vp],
     "ddl_gemm_x6_args_size": [],
 })
 
 
+PAD = 32  # planes are zero-padded to whole 32-deep GEMM stages in both dimensions
+MAX_PLANE_BYTES = 1 << 30  # 3 planes of one matrix (gemm_x6.hip's 32-bit offsets with out-of-range margins)
+
+
+def _pad(n: int) -> int:
+    return -(-n // PAD) * PAD
+
+
 class Planes:
-    """X6 planes of an fp32 matrix [R][C]: ``data`` int16 [3, R, C] (bf16 bit patterns h | m | l);
-    on CPU ``data`` is the fp32 matrix itself."""
+    """X6 planes of an fp32 matrix [R][C]: ``data`` int16 [3, Rp, Cp] (bf16 bit patterns h | m | l,
+    zero-padded to multiples of 32); on CPU ``data`` is the fp32 matrix itself."""
     __slots__ = ("data", "R", "C")
 
     def __init__(self, data: torch.Tensor, R: int, C: int):
@@ -55,13 +63,26 @@ class Planes:
     def is_cuda(self) -> bool:
         return self.data.is_cuda
 
+    @property
+    def ld(self) -> int:
+        return self.data.shape[-1]
+
+    @property
+    def plane_stride(self) -> int:
+        return self.data.shape[-1] * self.data.shape[-2]
+
     def dense(self) -> torch.Tensor:
         """The fp32 matrix back (h + m + l; exact)."""
         if not self.data.is_cuda:
             return self.data
         u = self.data.view(torch.int16).to(torch.int32) & 0xFFFF
         f = (u << 16).view(torch.float32)
-        return (f[2] + f[1]) + f[0]
+        return ((f[2] + f[1]) + f[0])[:self.R, :self.C]
+
+
+def fits(R: int, C: int) -> bool:
+    """Can an [R][C] matrix be a planes-GEMM operand (C % 8, padded planes < MAX_PLANE_BYTES)?"""
+    return C % 8 == 0 and 6 * _pad(R) * _pad(C) < MAX_PLANE_BYTES
 
 
 def split(x: torch.Tensor, out: torch.Tensor | None = None) -> Planes:
@@ -74,9 +95,11 @@ def split(x: torch.Tensor, out: torch.Tensor | None = None) -> Planes:
         raise TypeError("X6 planes split fp32 matrices")
     if x.stride(1) != 1:
         x = x.contiguous()
+    Rp, Cp = _pad(R), _pad(C)
     if out is None:
-        out = torch.empty(3, R, C, dtype=torch.int16, device=x.device)
-    check(_lib.kernels().ddl_x6_planes(ptr(x), x.stride(0), ptr(out), C, R * C, R, C, stream()), "x6_planes")
+        out = torch.empty(3, Rp, Cp, dtype=torch.int16, device=x.device)
+    check(_lib.kernels().ddl_x6_planes(ptr(x), x.stride(0), ptr(out), Cp, Rp * Cp, R, C, Rp, Cp, stream()),
+          "x6_planes")
     return Planes(out, R, C)
 
 
@@ -165,8 +188,8 @@ def gemm(a: Planes, a_mn: bool, b: Planes, b_mn: bool, out: torch.Tensor, *, res
     if residual is not None:
         assert residual.stride() == out.stride()
     ar.bias = ptr(bias)
-    ar.a_ps, ar.b_ps = a.R * a.C, b.R * b.C
-    ar.lda, ar.ldb, ar.ldo = a.C, b.C, out.stride(0)
+    ar.a_ps, ar.b_ps = a.plane_stride, b.plane_stride
+    ar.lda, ar.ldb, ar.ldo = a.ld, b.ld, out.stride(0)
     ar.M, ar.N, ar.K = M, N, K
     ar.accumulate, ar.alpha = int(bool(accumulate)), float(alpha)
     if sp > 1:

@@ -69,8 +69,10 @@ def conv_linear_ok(C: int, Kout: int) -> bool:
 
 
 def x6g_ok(T: int, C: int, Kout: int) -> bool:
-    """Can the planes GEMM (ops/gemm_x6.py) run a linear T x C -> Kout (every extent % 8)?"""
-    return T % 8 == 0 and C % 8 == 0 and Kout % 8 == 0
+    """Can the planes GEMM (ops/gemm_x6.py) run a linear T x C -> Kout (every extent % 8, each
+    operand's planes within the GEMM's addressing limit)?"""
+    return (T % 8 == 0 and C % 8 == 0 and Kout % 8 == 0 and X6G.fits(T, C) and X6G.fits(Kout, C)
+            and X6G.fits(T, Kout))
 
 
 # Engine of each linear product (FWD / DGRAD / WGRAD), all native unless asked otherwise:

@@ -174,7 +174,7 @@ def init(backend: str | None = None, device: str | None = None, rank: int | None
     mode = os.environ.get("DDL_IPC_ALLREDUCE", "auto")
     if (world > 1 and backend == "nccl" and mode != "0"
             and int(os.environ.get("LOCAL_WORLD_SIZE", world)) == world and world <= 8):
-        cap = int(os.environ.get("DDL_IPC_MAX_BYTES", str(8 << 20)))
+        cap = int(os.environ.get("DDL_IPC_MAX_BYTES", str(16 << 20)))
         try:
             from .ipc import IpcAllReduce
             _CTX.ipc = IpcAllReduce(rank, world, dev, capacity=cap)
@@ -228,7 +228,8 @@ def probe_ipc_threshold(ctx: DistContext, sizes=PROBE_SIZES, iters: int = 5) -> 
     every rank, take the slowest rank per (path, size) and keep the peer-read path up to the largest
     size below which it always won. Sets ctx.ipc_max_bytes / ctx.ipc_policy (identical on every
     rank: the decision is made on all-reduced timings) and releases the peer buffers when the
-    crossover is 0. Returns the threshold in bytes.
+    probe fails (a working peer path stays mapped for rank-ordered reductions even at crossover 0).
+    Returns the threshold in bytes.
 
     Every rank issues the SAME sequence of process-group collectives whatever happens on the peer
     path: per size, (1) a peer-path correctness check and (2) its timing each end in an agreed
@@ -280,9 +281,10 @@ def probe_ipc_threshold(ctx: DistContext, sizes=PROBE_SIZES, iters: int = 5) -> 
                                    for j, nb in enumerate(sizes)}}
     if failed:
         ctx.ipc_policy["error"] = err or "a peer failed the probe"
-    if thr == 0:
         ctx.ipc.close()
         ctx.ipc = None
+    # a working peer path stays mapped even when RCCL wins every all-reduce size: the ordered FedAvg
+    # mean (fl/aggregate.py) uses it instead of an all-gather of W full partials
     return thr
 
 

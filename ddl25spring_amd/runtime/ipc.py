@@ -148,6 +148,17 @@ class IpcAllReduce:
         self.calls += 1
         return t
 
+    def all_reduce_ordered(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place rank-ORDER sum of an fp32 contiguous device tensor of any size: slot-sized
+        chunks, each one peer-read kernel (one- or two-shot, both add the ranks' values in rank
+        order: p0 + p1 + ... bitwise on every rank). What the ordered FedAvg mean needs
+        (fl/aggregate.py) without all-gathering W full copies."""
+        step = self.cap // 4
+        flat = t.view(-1)
+        for off in range(0, flat.numel(), step):
+            self.all_reduce(flat[off:off + step])
+        return t
+
     def check(self):
         """Raise if any barrier of the calls so far timed out (synchronises the device)."""
         if int(self.err.item()):

@@ -23,7 +23,8 @@ def test_planes_exact(cuda):
     x = torch.randn(37, 56, device=cuda) * torch.logspace(-20, 20, 56, device=cuda)
     x[0, :8] = torch.tensor([0.0, -0.0, 1e-30, -1e-32, 3.4e38, -3.4e38, 1.0, -2.5])
     p = G.split(x)
-    assert p.data.shape == (3, 37, 56)
+    assert p.data.shape == (3, 64, 64)  # zero-padded to whole 32-deep stages
+    assert p.data[:, 37:].abs().sum() == 0 and p.data[:, :, 56:].abs().sum() == 0
     assert torch.equal(p.dense(), x)
 
 

@@ -118,3 +118,60 @@ def test_ipc_threshold_probe_agrees_across_ranks(cuda):
     for r in res:
         assert torch.equal(r["x"], torch.full((50000,), 3.0))
         assert r["path"] == ("ipc" if r["thr"] >= 200000 else "gloo")
+
+
+def _fedavg_worker(rank, world, port, out_path, P):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from ddl25spring_amd.fl.aggregate import MeanAggregator
+    from ddl25spring_amd.runtime import dist as rdist
+    from ddl25spring_amd.runtime.ipc import IpcAllReduce
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    ctx = rdist.DistContext(rank, world, rank, dev, "gloo")
+    ctx.ipc = IpcAllReduce(rank, world, dev, capacity=16 << 20, nblocks=16, timeout_s=20.0)
+    g = torch.Generator().manual_seed(11)
+    rows = torch.randn(world, P, generator=g)
+    coef = torch.rand(world, generator=g)
+    coef /= coef.sum()
+    agg = MeanAggregator(ordered=True)
+    out = torch.empty(P, device=dev)
+    agg(ctx, rows[rank:rank + 1].to(dev), coef[rank:rank + 1].to(dev), out)  # this rank's one client
+    desc = agg.describe(ctx)
+    ipc, ctx.ipc = ctx.ipc, None  # the all-gather fallback of the same reduction, for comparison
+    out_g = torch.empty(P, device=dev)
+    agg(ctx, rows[rank:rank + 1].to(dev), coef[rank:rank + 1].to(dev), out_g)
+    ctx.ipc = ipc
+    torch.save({"out": out.cpu(), "gather": out_g.cpu(), "desc": desc}, os.path.join(out_path, f"f{rank}.pt"))
+    dist.barrier()
+    ctx.ipc.check()
+    ctx.ipc.close()
+    dist.destroy_process_group()
+
+
+def test_ipc_ordered_fedavg_mean_bitwise_single_process(cuda):
+    """The 8-GPU headline's ordered FedAvg reduction (fl/aggregate.MeanAggregator) on the peer-read
+    kernel: 4 ranks with one client each (sharing the GPU) give bitwise the single-process 4-slot
+    weighted sum, on a vector of 5M floats (two-shot path, three slot-sized chunks)."""
+    from ddl25spring_amd.ops import functional as Fn
+    from ddl25spring_amd.runtime.launch import free_port
+    world, P = 4, 5_000_003
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_fedavg_worker, args=(world, free_port(), d, P), nprocs=world, join=True,
+                           start_method="spawn")
+        res = [torch.load(os.path.join(d, f"f{r}.pt"), weights_only=True) for r in range(world)]
+    g = torch.Generator().manual_seed(11)
+    rows = torch.randn(world, P, generator=g)
+    coef = torch.rand(world, generator=g)
+    coef /= coef.sum()
+    ref = torch.empty(P, device=cuda)
+    Fn.weighted_sum(rows.to(cuda), coef.to(cuda), ref)
+    ref = ref.cpu()
+    for r in res:
+        assert r["desc"] == "ipc peer-read rank-ordered sum"
+        bad = (r["out"] != ref).nonzero().flatten()
+        badg = (r["gather"] != ref).nonzero().flatten()
+        assert bad.numel() == 0 and badg.numel() == 0, (bad.numel(), bad[:8].tolist(), badg.numel(),
+                                                        (r["out"] - ref).abs().max().item())
