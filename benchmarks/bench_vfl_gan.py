@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--local-steps", type=int, default=20)
     ap.add_argument("--gan-batch", type=int, default=128)
     ap.add_argument("--vfl-batch", type=int, default=64)
+    ap.add_argument("--vfl-engine", choices=("fused", "graph"), default="fused",
+                    help="world 1: one-launch epoch kernel, or the module path replayed from a HIP graph")
     ap.add_argument("--gan-precisions", default="fp32,bf16",
                     help="DCGAN precisions, the first is the headline line (fp32 = the reference's)")
     args = ap.parse_args()
@@ -45,7 +47,7 @@ def main():
     parts = H.partition_balanced(list(X.columns), 2)
     Xtr, _ = H.row_split(X)
     Ytr, _ = H.row_split(Y)
-    xs = [torch.tensor(Xtr[p].values.astype(np.float32), device=dev) for p in parts]
+    xs = [torch.tensor(Xtr[p].values.astype(np.float32), device=dev).contiguous() for p in parts]
     y = torch.tensor(Ytr.values.astype(np.float32), device=dev)
     torch.manual_seed(0)
     bottoms = [T.BottomModel(len(p), 2 * len(p)).to(dev) for p in parts]
@@ -65,7 +67,16 @@ def main():
                 crit(net([x[b:b + args.vfl_batch] for x in xs]), y[b:b + args.vfl_batch]).backward()
                 net.optimizer.step()
 
-        epoch = CapturedStep(one_epoch, warmup=1, enabled=dev.type == "cuda")
+        eng = net.fused_epoch_engine(args.vfl_batch) if args.vfl_engine == "fused" else None
+        if eng is not None:
+            # the whole epoch (13 mini-batches: forward, CE, backward, AdamW) in one launch,
+            # csrc/kernels/mlp_epoch.hip
+            stats = torch.zeros(2, device=dev)
+
+            def epoch():
+                eng.run(xs, y, stats)
+        else:
+            epoch = CapturedStep(one_epoch, warmup=1, enabled=dev.type == "cuda")
     elif ctx.rank == 0:
         srv = SplitNNServer(top, [1], [2 * len(parts[1])], local_bottom=bottoms[0])
 
@@ -99,6 +110,8 @@ def main():
          ms_per_step=round(1e3 * dt_v / args.steps, 3), higher_is_better=True, scaling="strong",
          vs_baseline=None, dtype=f"fp32 (split-NN) / {precs[0]} (DCGAN)",
          data="heart.csv" if real else "synthetic",
+         vfl_engine="fused-epoch-kernel" if ctx.world == 1 and args.vfl_engine == "fused" and dev.type == "cuda"
+         else ("hip-graph" if ctx.world == 1 else "rccl-p2p"),
          gan_images_per_s=round(imgs / gan[precs[0]], 1), gan_ms_per_round=round(1e3 * gan[precs[0]] / args.steps, 3),
          config={"model": "splitnn-heart-2party + dcgan-cifar32", "global_batch": args.vfl_batch,
                  "seq_len": None, "parallelism": f"vfl2party-fedgan2-w{ctx.world}"})

@@ -261,7 +261,27 @@ class VFLNetwork(nn.Module):
         xs = [torch.tensor(x[f].values.astype(np.float32)) for f in cli_features]
         yt = torch.tensor(y.values.astype(np.float32))
         dev = next(self.parameters()).device
-        return [t.to(dev) for t in xs], yt.to(dev)
+        return [t.to(dev).contiguous() for t in xs], yt.to(dev).contiguous()
+
+    def fused_epoch_engine(self, batch_sz):
+        """The one-launch epoch engine (ops/mlp_epoch.py, csrc/kernels/mlp_epoch.hip) when this net
+        and its optimizer fit it: on the GPU, FlatAdamW over exactly the bottoms + top, gradients
+        zeroed per mini-batch, bottoms registered; else None (the module path runs)."""
+        from ..ops import mlp_epoch as ME
+        from ..optim import FlatAdam
+        opt = self.optimizer
+        if not (ME.ENABLED[0] and self.zero_grad_per_batch and self.register_bottoms
+                and isinstance(opt, FlatAdam) and opt.data.is_cuda):
+            return None
+        key = (batch_sz, id(opt))
+        eng = getattr(self, "_fused", None)
+        if eng is None or eng[0] != key:
+            try:
+                eng = (key, ME.MlpEpoch(ME.splitnn_graph(list(self.bottom_models), self.top_model), opt, batch_sz))
+            except (TypeError, ValueError):
+                eng = (key, None)
+            self._fused = eng
+        return eng[1]
 
     def train_with_settings(self, epochs, batch_sz, n_cli, cli_features, x, y, log_loss=None,
                             verbose=False):
@@ -270,7 +290,18 @@ class VFLNetwork(nn.Module):
         n = len(yt)
         nb = (n + batch_sz - 1) // batch_sz
         hist = []
+        eng = self.fused_epoch_engine(batch_sz)
         for epoch in range(epochs):
+            if eng is not None:  # the whole epoch in one launch; loss / correct stay on the device
+                stats = torch.zeros(2, device=yt.device)
+                eng.run(xs, yt, stats)
+                hist.append(stats / torch.tensor([float(nb), float(n)], device=yt.device))
+                if log_loss is not None:
+                    log_loss(float(hist[-1][0]))
+                if verbose:
+                    l, a = hist[-1].tolist()
+                    print(f"Epoch: {epoch} Train accuracy: {100 * a:.2f}% Loss: {l:.3f}")
+                continue
             self.train()
             for m in self.bottom_models:
                 m.train()
