@@ -113,3 +113,32 @@ def test_vfl_network_routes_to_fused_epoch(cuda):
     assert len(hist) == 8 and hist[-1][0] < hist[0][0]
     assert 0.0 <= hist[-1][1] <= 1.0
     assert int(net.optimizer.t_dev.item()) == 8 * 5
+
+
+def test_fused_epoch_golden_party_scaling(cuda):
+    """Device golden run on the one-launch epoch engine: lab/homework-2.ipynb:306 (cell 4) setup --
+    4 parties on the balanced split of the 30 encoded heart columns, 300 epochs, B=64, seed 42 --
+    with the reference's quirks fixed (bottoms optimised, zero_grad per mini-batch: the
+    configuration the fused engine serves). Published 84.31 % (quirks on); the fixed net must land
+    within 5 pp of it or above. Data: tests/data/heart_vfl.npz (the reference heart.csv after the
+    D3 recipe; the reference tree is not on the GPU box)."""
+    import numpy as np
+    import pandas as pd
+    from pathlib import Path
+    from ddl25spring_amd.data import heart as H
+    z = np.load(Path(__file__).parent / "data" / "heart_vfl.npz", allow_pickle=False)
+    X = pd.DataFrame(z["x"], columns=[str(c) for c in z["x_cols"]])
+    Y = pd.DataFrame(z["y"], columns=[str(c) for c in z["y_cols"]])
+    parts = H.partition_balanced(list(X.columns), 4)
+    Xtr, Xte = H.row_split(X)
+    Ytr, Yte = H.row_split(Y)
+    torch.manual_seed(42)
+    bottoms = [T.BottomModel(len(p), 2 * len(p)).to(cuda) for p in parts]
+    net = T.VFLNetwork(bottoms, 2).to(cuda)
+    net.optimizer = FlatAdamW(net.parameters())
+    assert net.fused_epoch_engine(64) is not None
+    hist = net.train_with_settings(300, 64, 4, parts, Xtr, Ytr)
+    assert int(net.optimizer.t_dev.item()) == 300 * -(-len(Ytr) // 64)  # every step ran in the kernel
+    acc = float(net.test(Xte, Yte)[0])
+    assert hist[-1][0] < hist[0][0]
+    assert acc >= 0.8431 - 0.05, acc
