@@ -154,14 +154,23 @@ def main():
             wb = fl.w_global.numel() * 4
             # the round's cross-rank weight reduction (fl/aggregate.py) and the all-reduce path the
             # context's policy picks for a message of that size (runtime/dist.py)
-            out["aggregation"] = fl.aggregator.describe(ctx) if hasattr(fl.aggregator, "describe") else \
+            agg = fl.aggregator.describe(ctx) if hasattr(fl.aggregator, "describe") else \
                 type(fl.aggregator).__name__
-            out["allreduce"] = {"weights_bytes": wb, "path": rdist.allreduce_path(ctx, wb),
-                                "backend": ctx.backend, **ctx.ipc_policy}
+            out["aggregation"] = agg
+            # the transport of the round's weight reduction: the IPC peer-read kernel (rank-ordered
+            # sum), an all-gather, or -- only for the unordered mean -- the all-reduce path the
+            # context's size policy picks for a message of that size
+            comm = {"weights_bytes": wb, "backend": ctx.backend, **ctx.ipc_policy}
+            if agg == "all-reduce":
+                comm["allreduce_path"] = rdist.allreduce_path(ctx, wb)
+            else:
+                comm["transport"] = "ipc" if agg.startswith("ipc") else "all_gather"
+            out["comm"] = comm
             out["rank_hashes_equal"] = len(set(hashes)) == 1
         if args.precision == "fp32":
             # the X6 engine's chain lengths (zero-start MFMA chains before each IEEE add, docs/KERNELS.md
             # "Chain length"); the measured gradient error of this tree: profiles/fp32_grad_accuracy_r6.txt
+            # (scripts/debug_r18_grads.py); no accuracy figure is hard-coded here
             out["fp32_chains"] = {"x6h_tap_steps": 3, "x6hw_pixel_steps": 2}
         if acc is not None:
             out["test_accuracy"] = acc
