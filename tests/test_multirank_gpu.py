@@ -183,7 +183,28 @@ def test_bench_eight_ranks_one_slot_each_match_single_process():
                             "--backend", "gloo"], capture_output=True, text=True, timeout=900, cwd=ROOT, env=env)
     assert eight.returncode == 0, eight.stderr[-3000:]
     a, b = _bench_json(one.stdout), _bench_json(eight.stdout)
-    print(json.dumps({k: b[k] for k in ("n_gpus", "aggregation", "allreduce", "rank_hashes_equal", "value")}))
+    print(json.dumps({k: b[k] for k in ("n_gpus", "aggregation", "comm", "rank_hashes_equal", "value")}))
     assert b["n_gpus"] == 8 and b["config"]["client_slots_per_gpu"] == 1 and a["config"]["client_slots_per_gpu"] == 8
-    assert b["rank_hashes_equal"] is True and "allreduce" in b and b["aggregation"].startswith("rank-ordered")
+    assert b["rank_hashes_equal"] is True and b["aggregation"].startswith("rank-ordered")
+    assert b["comm"]["transport"] == "all_gather"  # gloo: no IPC peer-read path
     assert a["w_global_sha256"] == b["w_global_sha256"]
+
+
+def test_bench_eight_ranks_tuned_plans_rank_hashes_equal():
+    """The same 8-rank rehearsal with the plans an 8-GPU run actually uses: the tuned plan table ON
+    and split-K free (no DDL_F32_TUNED / DDL_F32_TARGET_WG pins), i.e. the G = 1 tuned entries. The
+    model is then not bitwise the G = 8 single-process one (different tiles), but every rank must
+    still hold the same bits after the rank-ordered FedAvg (rank_hashes_equal)."""
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    env.pop("DDL_F32_TUNED", None)
+    env.pop("DDL_F32_TARGET_WG", None)
+    common = [os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "1", "--clients", "8",
+              "--train-size", "1600", "--deterministic"]
+    eight = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+                            "--master-addr", "127.0.0.1", "--master-port", "29753", *common, "--gpus", "8",
+                            "--backend", "gloo"], capture_output=True, text=True, timeout=900, cwd=ROOT, env=env)
+    assert eight.returncode == 0, eight.stderr[-3000:]
+    b = _bench_json(eight.stdout)
+    print(json.dumps({k: b[k] for k in ("n_gpus", "aggregation", "comm", "rank_hashes_equal", "value")}))
+    assert b["n_gpus"] == 8 and b["config"]["client_slots_per_gpu"] == 1
+    assert b["rank_hashes_equal"] is True
