@@ -86,7 +86,11 @@ DDL_API int ddl_broadcast_rows(const float* src, float* dst, long long ld, int G
 // gram_reduce_kernel sums the slices in block order: the K x K result is bit-reproducible (no
 // float atomics), which Krum's argsort of scores needs to pick the same clients on every run.
 // Staging: LDS tile [KP][CHUNK] fp32 with a +1 float pad per row (conflict-free column reads).
-constexpr int GRAM_CHUNK = 64;
+// Chunks of the coordinate axis: 256 columns for KP <= 32 (a small Gram has little MFMA work per
+// chunk, so each barrier round should move more bytes), 64 above. The next chunk's elements are
+// loaded into registers while the current chunk's MFMAs run (one chunk of prefetch).
+constexpr int GRAM_CHUNK = 64;  // the workspace sizing granule (gram_blocks)
+template <int KP> constexpr int gram_chunk() { return KP <= 32 ? 256 : 64; }
 
 __host__ __device__ inline int gram_blocks_cap(int KP) { return KP <= 64 ? 1024 : 512; }
 
@@ -94,10 +98,12 @@ template <int KP>
 __global__ __launch_bounds__(256) void gram_f32_kernel(const float* __restrict__ X, long long ld,
                                                        const float* __restrict__ center, int K,
                                                        long long n, float* __restrict__ part) {
-  constexpr int LDW = GRAM_CHUNK + 1;
+  constexpr int CH = gram_chunk<KP>();
+  constexpr int LDW = CH + 1;
   constexpr int NT = KP / 16;
   constexpr int TILES = NT * (NT + 1) / 2;
   constexpr int TPW = (TILES + 3) / 4;  // tiles per wave
+  constexpr int PER = KP * CH / 256;    // staged elements per thread
   __shared__ float tile[KP * LDW];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   int ti_[TPW], tj_[TPW];
@@ -111,23 +117,36 @@ __global__ __launch_bounds__(256) void gram_f32_kernel(const float* __restrict__
   f4v acc[TPW];
 #pragma unroll
   for (int i = 0; i < TPW; ++i) acc[i] = (f4v){0.f, 0.f, 0.f, 0.f};
-  for (long long c0 = (long long)blockIdx.x * GRAM_CHUNK; c0 < n; c0 += (long long)gridDim.x * GRAM_CHUNK) {
-    __syncthreads();
-    for (int e = tid; e < KP * GRAM_CHUNK; e += 256) {
-      const int r = e / GRAM_CHUNK, c = e - r * GRAM_CHUNK;
+  float nxt[PER];
+  auto fetch = [&](long long c0) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = tid + i * 256, r = e / CH, c = e - r * CH;
       const long long col = c0 + c;
       float v = 0.f;
       if (r < K && col < n) v = X[r * ld + col] - (center ? center[col] : 0.f);
-      tile[r * LDW + c] = v;
+      nxt[i] = v;
+    }
+  };
+  const long long stride = (long long)gridDim.x * CH;
+  long long c0 = (long long)blockIdx.x * CH;
+  if (c0 < n) fetch(c0);
+  for (; c0 < n; c0 += stride) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = tid + i * 256, r = e / CH, c = e - r * CH;
+      tile[r * LDW + c] = nxt[i];
     }
     __syncthreads();
+    if (c0 + stride < n) fetch(c0 + stride);  // in flight during this chunk's MFMAs
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
       if (ti_[t] < NT) {
         const float* ra = tile + (ti_[t] * 16 + (lane & 15)) * LDW + (lane >> 4);
         const float* rb = tile + (tj_[t] * 16 + (lane & 15)) * LDW + (lane >> 4);
 #pragma unroll
-        for (int k = 0; k < GRAM_CHUNK; k += 4)
+        for (int k = 0; k < CH; k += 4)
           // A[i][k] lane: i = lane&15, k = lane>>4 ; B[k][j] lane: j = lane&15, k = lane>>4
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[k], rb[k], acc[t], 0, 0, 0);
       }
@@ -299,4 +318,100 @@ DDL_API int ddl_coord_select(const float* X, long long ld, int K, long long n, i
   SEL_CASE(8) SEL_CASE(16) SEL_CASE(32) SEL_CASE(64) SEL_CASE(128)
 #undef SEL_CASE
   return (int)hipErrorInvalidValue;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Robust aggregation glue (round 6): the coordinate-sharded rules' all-to-all send buffer in one
+// pass, and Krum's scoring / selection / winners' mean on the device without torch sort glue.
+//
+// send[w][g][s] = rows[g][w * S + s] for g < G and w * S + s < P, else 0 (g < gmax): client rows
+// [G][P] (row stride ld) cut into W coordinate shards of S, zero-padded to gmax rows per rank.
+__global__ void pack_shards_kernel(const float* __restrict__ rows, long long ld, int G, long long P,
+                                   int W, long long S, int gmax, float* __restrict__ send) {
+  const long long n = (long long)W * gmax * S;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long s = e % S, wg = e / S;
+    const int g = (int)(wg % gmax), w = (int)(wg / gmax);
+    const long long c = (long long)w * S + s;
+    send[e] = (g < G && c < P) ? rows[g * ld + c] : 0.f;
+  }
+}
+
+DDL_API int ddl_pack_shards(const float* rows, long long ld, int G, long long P, int W, long long S,
+                            int gmax, float* send, hipStream_t st) {
+  if (W < 1 || S < 1 || gmax < 1 || G > gmax || (long long)W * S < P) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_shards_kernel, dim3(grid_for((long long)W * gmax * S, 256)), dim3(256), 0, st,
+                     rows, ld, G, P, W, S, gmax, send);
+  return (int)hipGetLastError();
+}
+
+// Krum (Blanchard et al. 2017) from the K x K Gram of the client updates: d2[i][j] = g_ii + g_jj -
+// 2 g_ij (clamped at 0), score_i = sum of the nb smallest d2[i][j], j != i (ascending order, as a
+// sort would add them), sel = the m clients of least score (ties by index). One block, a thread per
+// client: its row sorted in registers by the bitonic network above.
+template <int KP>
+__global__ __launch_bounds__(128) void krum_select_kernel(const float* __restrict__ gram, int K, int nb,
+                                                          int m, float* __restrict__ scores,
+                                                          int* __restrict__ sel) {
+#pragma clang fp contract(off)
+  __shared__ float sc[128];
+  const int i = threadIdx.x;
+  if (i < K) {
+    float v[KP];
+    const float gii = gram[i * K + i];
+#pragma unroll
+    for (int j = 0; j < KP; ++j) {
+      float d = INFINITY;
+      if (j < K && j != i) d = fmaxf(gii + gram[j * K + j] - 2.f * gram[i * K + j], 0.f);
+      v[j] = d;
+    }
+    sort_values<KP>(v);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < KP; ++j)
+      if (j < nb) s += v[j];
+    sc[i] = s;
+    if (scores) scores[i] = s;
+  }
+  __syncthreads();
+  if (i < K) {
+    const float s = sc[i];
+    int rank = 0;
+    for (int j = 0; j < K; ++j) rank += (sc[j] < s || (sc[j] == s && j < i)) ? 1 : 0;
+    if (rank < m) sel[rank] = i;
+  }
+}
+
+DDL_API int ddl_krum_select(const float* gram, int K, int nb, int m, float* scores, int* sel, hipStream_t st) {
+  if (K < 1 || K > 128 || nb < 1 || nb > K - 1 + (K == 1) || m < 1 || m > K) return (int)hipErrorInvalidValue;
+#define KRUM_CASE(KP_) \
+  if (K <= KP_) { \
+    hipLaunchKernelGGL(krum_select_kernel<KP_>, dim3(1), dim3(128), 0, st, gram, K, nb, m, scores, sel); \
+    return (int)hipGetLastError(); \
+  }
+  KRUM_CASE(8) KRUM_CASE(16) KRUM_CASE(32) KRUM_CASE(64) KRUM_CASE(128)
+#undef KRUM_CASE
+  return (int)hipErrorInvalidValue;
+}
+
+// out[e] = sum_t (1/m) * X[sel[t]][e], t = 0 .. m-1 in selection order (products rounded, then
+// added: the same bits as weighted_sum over the gathered rows)
+__global__ void mean_rows_idx_kernel(const float* __restrict__ X, long long ld, const int* __restrict__ sel,
+                                     int m, long long n, float* __restrict__ out) {
+#pragma clang fp contract(off)
+  const float c = 1.f / (float)m;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n;
+       e += (long long)gridDim.x * blockDim.x) {
+    float acc = 0.f;
+    for (int t = 0; t < m; ++t) acc = acc + c * X[(long long)sel[t] * ld + e];
+    out[e] = acc;
+  }
+}
+
+DDL_API int ddl_mean_rows_idx(const float* X, long long ld, const int* sel, int m, long long n, float* out,
+                              hipStream_t st) {
+  if (m < 1 || n < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(mean_rows_idx_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, X, ld, sel, m, n, out);
+  return (int)hipGetLastError();
 }

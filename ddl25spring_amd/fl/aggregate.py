@@ -14,7 +14,9 @@
   sharded*: one all-to-all gives each GPU 1/W of the coordinates of all K clients; median /
   trimmed-mean are local per-coordinate selection kernels followed by an all-gather; Krum computes
   a partial K x K Gram on its shard with the exact-fp32 MFMA, all-reduces the tiny K x K matrix,
-  scores redundantly on every GPU and averages the winners' shards.
+  scores and selects redundantly on every GPU in one small kernel (krum_select) and averages the
+  winners' shards by index (mean_rows_idx). One GPU skips the sharding: the rules read the client
+  rows in place; several GPUs build the all-to-all send buffer with one pack kernel.
 Robust rules operate on client *updates* (w_k - w_global) — distances between raw weights would
 cancel catastrophically in fp32.
 """
@@ -76,25 +78,31 @@ class _Sharded:
     needs_all = True
 
     def shard(self, ctx, rows: torch.Tensor, counts: list[int]):
+        """-> (X [K, S] client rows over this rank's S coordinates, rank-major; S; padded P).
+        One GPU: the rows themselves (no copy). Several: ONE pack kernel builds the all-to-all send
+        buffer (shards cut, zero-padded to the largest per-rank client count), and when every rank
+        holds the same number of clients the receive buffer is used as is."""
         W = ctx.world
         K = sum(counts)
         P = rows.shape[1]
+        if W == 1:
+            return (rows if rows.stride(1) == 1 else rows.contiguous())[:K], P, P
         Pp = math.ceil(P / W) * W
         S = Pp // W
         gmax = max(counts)
-        G = rows.shape[0]
-        dev = rows.device
-        send = torch.zeros(W, gmax, S, dtype=torch.float32, device=dev)
-        if G:
-            padded = torch.zeros(G, Pp, dtype=torch.float32, device=dev)
-            padded[:, :P] = rows
-            send[:, :G] = padded.reshape(G, W, S).transpose(0, 1)
+        if rows.shape[0] and rows.stride(1) != 1:
+            rows = rows.contiguous()
+        send = Fn.pack_shards(rows, W, S, gmax)
         recv = torch.empty_like(send)
         ctx.all_to_all_single(recv, send)
+        if all(c == gmax for c in counts):
+            return recv.view(W * gmax, S), S, Pp
         valid = torch.cat([recv[i, :counts[i]] for i in range(W)], 0) if K else recv[:0, 0]
         return valid.contiguous(), S, Pp  # [K, S] rows ordered rank-major
 
     def unshard(self, ctx, part: torch.Tensor, P: int, Pp: int):
+        if ctx.world == 1:
+            return part[:P]
         full = torch.empty(Pp, dtype=torch.float32, device=part.device)
         ctx.all_gather_into(full, part.contiguous())
         return full[:P]
@@ -134,16 +142,23 @@ class Krum(_Sharded):
         K = sum(counts)
         shard, S, Pp = self.shard(ctx, rows, counts)
         gram = Fn.gram(shard)
-        ctx.all_reduce(gram)
+        if ctx.is_distributed:
+            ctx.all_reduce(gram)
+        nb = max(1, K - self.f - 2)
+        m = max(1, self.m)
+        if K <= Fn.MAX_ROBUST_CLIENTS:
+            # scores, selection and the winners' mean on the device: krum_select + mean_rows_idx
+            # (aggregate.hip), no torch sort / argsort / index_select glue
+            _, sel = Fn.krum_select(gram.contiguous(), nb, m)
+            self._sel = sel  # stays on the device: no host sync per round (``last_selected`` reads it)
+            return self.unshard(ctx, Fn.mean_rows_idx(shard, sel), P, Pp)
         sq = torch.diagonal(gram)
         d2 = (sq[:, None] + sq[None, :] - 2 * gram).clamp_min(0)
-        nb = max(1, K - self.f - 2)
         d2.fill_diagonal_(float("inf"))
         scores = torch.sort(d2, 1).values[:, :nb].sum(1)
-        sel = torch.argsort(scores)[:max(1, self.m)]
-        self._sel = sel  # stays on the device: no host sync per round (``last_selected`` reads it)
+        sel = torch.argsort(scores)[:m]
+        self._sel = sel
         chosen = shard.index_select(0, sel)
-        m = chosen.shape[0]
         part = torch.empty(chosen.shape[1], dtype=torch.float32, device=chosen.device)
         Fn.weighted_sum(chosen, torch.full((m,), 1.0 / m, dtype=torch.float32, device=chosen.device), part)
         return self.unshard(ctx, part, P, Pp)

@@ -1374,6 +1374,61 @@ def _gram_blocked(X, center=None):
     return out
 
 
+def pack_shards(rows, W: int, S: int, gmax: int, out=None):
+    """The coordinate-sharded aggregators' all-to-all send buffer in one pass: out[w][g][s] =
+    rows[g][w*S + s] (zero past P and for g >= G). rows [G, P] with unit column stride."""
+    G, P = rows.shape
+    if out is None:
+        out = torch.empty(W, gmax, S, dtype=torch.float32, device=rows.device)
+    if not rows.is_cuda:
+        out.zero_()
+        if G:
+            pad = torch.zeros(G, W * S, dtype=torch.float32)
+            pad[:, :P] = rows
+            out[:, :G] = pad.reshape(G, W, S).transpose(0, 1)
+        return out
+    assert rows.dtype == torch.float32 and (G == 0 or rows.stride(1) == 1) and out.is_contiguous()
+    check(_lib.kernels().ddl_pack_shards(ptr(rows) if G else ptr(out), rows.stride(0) if G else 0, G, P, W, S,
+                                         gmax, ptr(out), stream()), "pack_shards")
+    return out
+
+
+def krum_select(gram, nb: int, m: int):
+    """Krum scores (sum of the nb smallest squared distances to the other clients) from a K x K Gram,
+    and the m clients of least score (ties by index) -> (scores [K] fp32, sel [m] int32)."""
+    K = gram.shape[0]
+    if not gram.is_cuda:
+        sq = torch.diagonal(gram)
+        d2 = (sq[:, None] + sq[None, :] - 2 * gram).clamp_min(0)
+        d2.fill_diagonal_(float("inf"))
+        scores = torch.sort(d2, 1).values[:, :nb].sum(1)
+        order = sorted(range(K), key=lambda i: (float(scores[i]), i))
+        return scores, torch.tensor(order[:m], dtype=torch.int32)
+    assert gram.dtype == torch.float32 and gram.is_contiguous() and K <= MAX_ROBUST_CLIENTS
+    scores = torch.empty(K, dtype=torch.float32, device=gram.device)
+    sel = torch.empty(m, dtype=torch.int32, device=gram.device)
+    check(_lib.kernels().ddl_krum_select(ptr(gram), K, nb, m, ptr(scores), ptr(sel), stream()), "krum_select")
+    return scores, sel
+
+
+def mean_rows_idx(X, sel, out=None):
+    """out = (1/m) sum over the rows X[sel[t]] in selection order (products rounded, then added)."""
+    n = X.shape[1]
+    m = sel.numel()
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=X.device)
+    if not X.is_cuda:
+        rows = X.index_select(0, sel.long())
+        out.zero_()
+        for t in range(m):
+            out.add_(rows[t] * (1.0 / m))
+        return out
+    assert X.dtype == torch.float32 and X.stride(1) == 1 and sel.dtype == torch.int32
+    check(_lib.kernels().ddl_mean_rows_idx(ptr(X), X.stride(0), ptr(sel), m, n, ptr(out), stream()),
+          "mean_rows_idx")
+    return out
+
+
 def coord_select(X, mode: str, trim: int = 0):
     """Coordinate-wise median ('median') or trimmed mean ('trimmed') over K rows of X [K, n]."""
     m = 0 if mode == "median" else 1

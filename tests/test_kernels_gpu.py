@@ -683,3 +683,32 @@ def test_head_train(cuda, case):
         _close(dx, dx_r, rel=1e-2)
         if bn:
             _close(part.sum(1), part_r.sum(1), rel=5e-3)
+
+
+@pytest.mark.parametrize("G,P,W,gmax", [(3, 1001, 4, 3), (2, 64, 2, 4), (0, 10, 3, 1), (5, 333, 1, 5)])
+def test_pack_shards(cuda, G, P, W, gmax):
+    """The all-to-all send buffer of the coordinate-sharded aggregators in one pass (aggregate.hip
+    pack_shards) == the torch zero / pad / transpose composition."""
+    S = -(-P // W)
+    rows = torch.randn(G, P + 7)[:, :P]  # a row stride larger than P
+    got = Fn.pack_shards(rows.to(cuda), W, S, gmax).cpu()
+    want = Fn.pack_shards(rows.contiguous(), W, S, gmax)
+    assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("K,f,m", [(5, 1, 1), (8, 2, 1), (33, 4, 3), (100, 20, 2), (128, 10, 1)])
+def test_krum_select_and_indexed_mean(cuda, K, f, m):
+    """Krum scores / selection on the device (aggregate.hip krum_select, a register bitonic sort per
+    client) and the winners' mean by index (mean_rows_idx) vs the torch reference."""
+    torch.manual_seed(K)
+    X = torch.randn(K, 3000)
+    X[: f] *= 5.0  # f far-away clients
+    g = (X.double() @ X.double().t()).float()
+    nb = max(1, K - f - 2)
+    sc, sel = Fn.krum_select(g.to(cuda), nb, m)
+    sc_ref, sel_ref = Fn.krum_select(g, nb, m)
+    assert torch.allclose(sc.cpu(), sc_ref, rtol=1e-5)
+    assert sel.cpu().tolist() == sel_ref.tolist()
+    out = Fn.mean_rows_idx(X.to(cuda), sel)
+    want = Fn.mean_rows_idx(X, sel.cpu())
+    assert torch.equal(out.cpu(), want)
