@@ -163,17 +163,26 @@ __global__ __launch_bounds__(256) void gram_f32_kernel(const float* __restrict__
   }
 }
 
-// out[i][j] = sum over blocks (in block order) of the stored tile holding (i, j) or (j, i)
-__global__ void gram_reduce_kernel(const float* __restrict__ part, int blocks, int K, int KP,
-                                   float* __restrict__ out) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= K * K) return;
+// out[i][j] = sum over the blocks' partials of the stored tile holding (i, j) or (j, i): one
+// block per output element, thread t adding blocks t, t + 256, ... in order, then a fixed LDS tree
+// -- a fixed summation order, so the result is bit-reproducible (no float atomics)
+__global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restrict__ part, int blocks, int K,
+                                                          int KP, float* __restrict__ out) {
+  __shared__ float red[256];
+  const int e = blockIdx.x;
   int i = e / K, j = e - (e / K) * K;
   if ((i >> 4) > (j >> 4)) { const int t = i; i = j; j = t; }
   const float* p = part + i * KP + j;
   float s = 0.f;
-  for (int b = 0; b < blocks; ++b) s += p[(long long)b * KP * KP];
-  out[e] = s;
+  for (int b = threadIdx.x; b < blocks; b += 256) s += p[(long long)b * KP * KP];
+  red[threadIdx.x] = s;
+  __syncthreads();
+#pragma unroll
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[e] = red[0];
 }
 
 static int gram_kp(int K) { return K <= 16 ? 16 : K <= 32 ? 32 : K <= 48 ? 48 : K <= 64 ? 64 : K <= 96 ? 96 : 128; }
@@ -200,8 +209,7 @@ DDL_API int ddl_gram_f32(const float* X, long long ld, const float* center, int 
 #undef GRAM_CASE
     default: return (int)hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL(gram_reduce_kernel, dim3((K * K + 255) / 256), dim3(256), 0, s, part, blocks, K,
-                     gram_kp(K), out);
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3(K * K), dim3(256), 0, s, part, blocks, K, gram_kp(K), out);
   return (int)hipGetLastError();
 }
 
@@ -348,12 +356,13 @@ DDL_API int ddl_pack_shards(const float* rows, long long ld, int G, long long P,
 
 // Krum (Blanchard et al. 2017) from the K x K Gram of the client updates: d2[i][j] = g_ii + g_jj -
 // 2 g_ij (clamped at 0), score_i = sum of the nb smallest d2[i][j], j != i (ascending order, as a
-// sort would add them), sel = the m clients of least score (ties by index). One block, a thread per
+// sort would add them), sel = the m clients of least score (exact ties to the smaller key: the
+// client's global order, so the choice does not depend on the rank layout; default the index). One block, a thread per
 // client: its row sorted in registers by the bitonic network above.
 template <int KP>
 __global__ __launch_bounds__(128) void krum_select_kernel(const float* __restrict__ gram, int K, int nb,
-                                                          int m, float* __restrict__ scores,
-                                                          int* __restrict__ sel) {
+                                                          int m, const int* __restrict__ keys,
+                                                          float* __restrict__ scores, int* __restrict__ sel) {
 #pragma clang fp contract(off)
   __shared__ float sc[128];
   const int i = threadIdx.x;
@@ -378,16 +387,18 @@ __global__ __launch_bounds__(128) void krum_select_kernel(const float* __restric
   if (i < K) {
     const float s = sc[i];
     int rank = 0;
-    for (int j = 0; j < K; ++j) rank += (sc[j] < s || (sc[j] == s && j < i)) ? 1 : 0;
+    const int ki = keys ? keys[i] : i;
+    for (int j = 0; j < K; ++j) rank += (sc[j] < s || (sc[j] == s && (keys ? keys[j] : j) < ki)) ? 1 : 0;
     if (rank < m) sel[rank] = i;
   }
 }
 
-DDL_API int ddl_krum_select(const float* gram, int K, int nb, int m, float* scores, int* sel, hipStream_t st) {
+DDL_API int ddl_krum_select(const float* gram, int K, int nb, int m, const int* keys, float* scores, int* sel,
+                            hipStream_t st) {
   if (K < 1 || K > 128 || nb < 1 || nb > K - 1 + (K == 1) || m < 1 || m > K) return (int)hipErrorInvalidValue;
 #define KRUM_CASE(KP_) \
   if (K <= KP_) { \
-    hipLaunchKernelGGL(krum_select_kernel<KP_>, dim3(1), dim3(128), 0, st, gram, K, nb, m, scores, sel); \
+    hipLaunchKernelGGL(krum_select_kernel<KP_>, dim3(1), dim3(128), 0, st, gram, K, nb, m, keys, scores, sel); \
     return (int)hipGetLastError(); \
   }
   KRUM_CASE(8) KRUM_CASE(16) KRUM_CASE(32) KRUM_CASE(64) KRUM_CASE(128)

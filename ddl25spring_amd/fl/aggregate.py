@@ -111,7 +111,7 @@ class _Sharded:
 class Median(_Sharded):
     name = "median"
 
-    def __call__(self, ctx, rows, counts, P):
+    def __call__(self, ctx, rows, counts, P, keys=None):
         shard, S, Pp = self.shard(ctx, rows, counts)
         return self.unshard(ctx, Fn.coord_select(shard, "median"), P, Pp)
 
@@ -122,7 +122,7 @@ class TrimmedMean(_Sharded):
     def __init__(self, trim: int | float = 0.1):
         self.trim = trim
 
-    def __call__(self, ctx, rows, counts, P):
+    def __call__(self, ctx, rows, counts, P, keys=None):
         K = sum(counts)
         b = int(self.trim * K) if isinstance(self.trim, float) and self.trim < 1 else int(self.trim)
         b = min(b, (K - 1) // 2)
@@ -138,7 +138,10 @@ class Krum(_Sharded):
         self.f, self.m = f, m
         self._sel = None
 
-    def __call__(self, ctx, rows, counts, P):
+    def __call__(self, ctx, rows, counts, P, keys=None):
+        """keys: each (rank-major) row's global client order; exact score ties (a mutual-nearest
+        pair always ties when nb = 1) go to the smaller key, so the choice does not depend on how
+        the clients are spread over ranks. Default: the row index."""
         K = sum(counts)
         shard, S, Pp = self.shard(ctx, rows, counts)
         gram = Fn.gram(shard)
@@ -149,14 +152,16 @@ class Krum(_Sharded):
         if K <= Fn.MAX_ROBUST_CLIENTS:
             # scores, selection and the winners' mean on the device: krum_select + mean_rows_idx
             # (aggregate.hip), no torch sort / argsort / index_select glue
-            _, sel = Fn.krum_select(gram.contiguous(), nb, m)
+            _, sel = Fn.krum_select(gram.contiguous(), nb, m, keys)
             self._sel = sel  # stays on the device: no host sync per round (``last_selected`` reads it)
             return self.unshard(ctx, Fn.mean_rows_idx(shard, sel), P, Pp)
         sq = torch.diagonal(gram)
         d2 = (sq[:, None] + sq[None, :] - 2 * gram).clamp_min(0)
         d2.fill_diagonal_(float("inf"))
         scores = torch.sort(d2, 1).values[:, :nb].sum(1)
-        sel = torch.argsort(scores)[:m]
+        kk = torch.arange(K, device=scores.device) if keys is None else torch.tensor(keys, device=scores.device)
+        order = sorted(range(K), key=lambda i: (float(scores[i]), int(kk[i])))  # K > 128 only
+        sel = torch.tensor(order[:m], dtype=torch.long, device=scores.device)
         self._sel = sel
         chosen = shard.index_select(0, sel)
         part = torch.empty(chosen.shape[1], dtype=torch.float32, device=chosen.device)

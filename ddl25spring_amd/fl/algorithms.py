@@ -162,6 +162,12 @@ class FederatedBase:
         counts = [len(chosen[i::self.W]) for i in range(self.W)]
         return mine, counts
 
+    def _row_keys(self, counts):
+        """Each rank-major client row's position in the round's `chosen` order (round-robin
+        assignment above): the robust rules break exact ties by it, so a run gives the same
+        aggregate on one GPU and on W."""
+        return [l * self.W + w for w in range(self.W) for l in range(counts[w])]
+
     def _download(self, G):
         st = self.net.store
         if G:
@@ -293,7 +299,7 @@ class FedAvg(FederatedBase):
             self.aggregator(self.ctx, rows, coeffs, self.w_global)
         else:
             upd = rows - self.w_global  # robust rules act on updates
-            agg = self.aggregator(self.ctx, upd, counts, self.w_global.numel())
+            agg = self.aggregator(self.ctx, upd, counts, self.w_global.numel(), keys=self._row_keys(counts))
             self.w_global.add_(agg)
 
 
@@ -347,7 +353,8 @@ class FedSGD(FederatedBase):
         if not getattr(self.aggregator, "needs_all", False):
             self.aggregator(self.ctx, st.grad[:G], coeffs, self.g_global)
         else:
-            self.g_global.copy_(self.aggregator(self.ctx, st.grad[:G], counts, self.w_global.numel()))
+            self.g_global.copy_(self.aggregator(self.ctx, st.grad[:G], counts, self.w_global.numel(),
+                                                keys=self._row_keys(counts)))
         # server SGD step (no momentum, as the reference's SGD(lr))
         self.w_global.add_(self.g_global, alpha=-self.lr)
         if G:  # BN running stats from this round's forward passes

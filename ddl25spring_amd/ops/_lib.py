@@ -166,7 +166,7 @@ _SIGS = {
     "ddl_gemm_nt_bf16": [vp, vp, vp, i32, i32, i32, i64, vp],
     "ddl_coord_select": [vp, i64, i32, i64, i32, i32, vp, vp],
     "ddl_pack_shards": [vp, i64, i32, i64, i32, i64, i32, vp, vp],
-    "ddl_krum_select": [vp, i32, i32, i32, vp, vp, vp],
+    "ddl_krum_select": [vp, i32, i32, i32, vp, vp, vp, vp],
     "ddl_mean_rows_idx": [vp, i64, vp, i32, i64, vp, vp],
 }
 

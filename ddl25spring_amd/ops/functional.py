@@ -1393,21 +1393,27 @@ def pack_shards(rows, W: int, S: int, gmax: int, out=None):
     return out
 
 
-def krum_select(gram, nb: int, m: int):
+def krum_select(gram, nb: int, m: int, keys=None):
     """Krum scores (sum of the nb smallest squared distances to the other clients) from a K x K Gram,
-    and the m clients of least score (ties by index) -> (scores [K] fp32, sel [m] int32)."""
+    and the m clients of least score -> (scores [K] fp32, sel [m] int32 row indices). Exact ties go
+    to the smaller key (``keys``: a per-row int list, default the row index)."""
     K = gram.shape[0]
+    if keys is None:
+        keys = list(range(K))
     if not gram.is_cuda:
         sq = torch.diagonal(gram)
         d2 = (sq[:, None] + sq[None, :] - 2 * gram).clamp_min(0)
         d2.fill_diagonal_(float("inf"))
         scores = torch.sort(d2, 1).values[:, :nb].sum(1)
-        order = sorted(range(K), key=lambda i: (float(scores[i]), i))
+        order = sorted(range(K), key=lambda i: (float(scores[i]), keys[i]))
         return scores, torch.tensor(order[:m], dtype=torch.int32)
     assert gram.dtype == torch.float32 and gram.is_contiguous() and K <= MAX_ROBUST_CLIENTS
     scores = torch.empty(K, dtype=torch.float32, device=gram.device)
     sel = torch.empty(m, dtype=torch.int32, device=gram.device)
-    check(_lib.kernels().ddl_krum_select(ptr(gram), K, nb, m, ptr(scores), ptr(sel), stream()), "krum_select")
+    kt = torch.tensor(keys, dtype=torch.int32).to(gram.device, non_blocking=True)
+    check(_lib.kernels().ddl_krum_select(ptr(gram), K, nb, m, ptr(kt), ptr(scores), ptr(sel), stream()),
+          "krum_select")
+    scores._keep = kt
     return scores, sel
 
 

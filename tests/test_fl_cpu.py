@@ -144,8 +144,10 @@ def _dist_worker(rank, world, port, out_dir, agg):
     rdist.shutdown()
 
 
-@pytest.mark.parametrize("agg", ["mean", "median"])
+@pytest.mark.parametrize("agg", ["mean", "median", "trimmed_mean", "krum"])
 def test_distributed_fedavg_matches_single_process(fp32, agg):
+    """2 gloo ranks x 2 clients vs one process holding the 4: the coordinate-sharded rules go through
+    pack_shards + all-to-all + all-gather at world 2 and read the rows in place at world 1."""
     arr, data = _data(400)
     parts = split(4, True, 7, labels=arr.labels)
     single = FedAvg(mnist_mlp, data, parts, lr=0.1, batch_size=50, client_fraction=1.0, seed=7,
@@ -153,7 +155,7 @@ def test_distributed_fedavg_matches_single_process(fp32, agg):
     single.round()
     single.round()
     with tempfile.TemporaryDirectory() as d:
-        port = 29600 + (os.getpid() % 200) + (0 if agg == "mean" else 1)
+        port = 29600 + (os.getpid() % 200) + 10 * ["mean", "median", "trimmed_mean", "krum"].index(agg)
         mp.spawn(_dist_worker, args=(2, port, d, agg), nprocs=2, join=True)
         w0 = torch.load(os.path.join(d, "w0.pt"), weights_only=True)
         w1 = torch.load(os.path.join(d, "w1.pt"), weights_only=True)
