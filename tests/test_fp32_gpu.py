@@ -536,3 +536,17 @@ def test_resnet50_fp32_step_as_accurate_as_torch_fp32(cuda):
     med = sorted(e for _, e in ours)[len(ours) // 2]
     med32 = sorted(ref32)[len(ref32) // 2]
     assert med <= 2 * med32 + 1e-4, (med, med32)
+
+
+def test_fp32_resnet18_128_step_chunk_graph_equals_eager(cuda):
+    """The round-graph chunk size actually shipped (fl/local.py GRAPH_MAX_STEPS = 128): one client,
+    ResNet-18, 16-sample batches over 2,072 samples = 129 full steps + a short one, so a round is a
+    128-step chunk graph, then a 1-step chunk with the tail -- bit for bit the eager round."""
+    import ddl25spring_amd.fl.local as L
+    assert L.GRAPH_MAX_STEPS == 128
+    ws = []
+    for graph in (True, False):
+        fa = _fedavg(cuda, "resnet18", "cifar10", 2072, 1, 16, use_graph=graph)
+        fa.round()
+        ws.append(fa.w_global.clone())
+    assert torch.equal(ws[0], ws[1]), (ws[0] - ws[1]).abs().max().item()
