@@ -32,9 +32,14 @@ DIRECT_SGD = os.environ.get("DDL_DIRECT_SGD", "1") != "0"
 # the GPU idle ~1 ms at every round boundary even with the host rounds ahead (sync_rounds off);
 # with two instances (DDL_ROUND_GRAPHS=2) the host can submit round r+1 while round r runs.
 ROUND_GRAPHS = max(1, int(os.environ.get("DDL_ROUND_GRAPHS", "1")))
-# Longest step sequence in one captured graph. A whole 50,000-sample single-client epoch (500 steps,
-# ~80k kernel nodes) segfaulted inside hipGraphLaunch; longer rounds replay a graph per chunk.
+# Longest step sequence in one captured graph. hipGraphLaunch segfaults once a graph holds between
+# 76,145 and 76,930 kernel nodes (measured: 485 ResNet-18 steps of 157 nodes run, 490 crash;
+# profiles/graph_node_limit_r6.txt); longer rounds replay a graph per chunk. 128 steps = 20,096
+# nodes, a 3.8x margin, and larger chunks gain nothing (26.1-26.3k samples/s from 256 to 485).
 GRAPH_MAX_STEPS = max(1, int(os.environ.get("DDL_GRAPH_MAX_STEPS", "128")))
+# keep the captured hipGraph_t (torch keep_graph=True) so diagnostics can count its nodes
+# (scripts/graph_nodes.py); off by default: the instantiated executable is all a replay needs
+KEEP_GRAPH = os.environ.get("DDL_GRAPH_KEEP", "0") == "1"
 
 
 class LocalTrainer:
@@ -130,7 +135,7 @@ class LocalTrainer:
         # zero-initialised momentum == torch's "buffer = first grad" when dampening == 0, so the
         # frozen first_step=False inside the graph is exact for every step of a round
         assert opt.dampening == 0.0
-        graph = torch.cuda.CUDAGraph()
+        graph = torch.cuda.CUDAGraph(keep_graph=KEEP_GRAPH)
         # DDL_GRAPH_PRIO=1: capture on a high-priority stream, so the step's critical path (the
         # main stream) outranks the side-stream weight gradients (Fn.wgrad_overlap) it overlaps
         cap = torch.cuda.Stream(priority=-1) if os.environ.get("DDL_GRAPH_PRIO", "0") == "1" else None
