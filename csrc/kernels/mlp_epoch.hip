@@ -58,7 +58,7 @@ struct MlpEpochArgs {
   long long nparam, lds_floats;        // flat length, LDS arena size (floats; host-checked)
   unsigned long long seed;
   float lr, beta1, beta2, eps, wd;
-  int n, B, ncls, nlayers, nbufs, nlev, logits_buf, probe;  // timing bits: 1 no GEMM loads, 2 no MFMA, 4 no epilogue, 8 no tiles, 16 no AdamW
+  int n, B, ncls, nlayers, nbufs, nlev, logits_buf, probe;  // timing bits: 1 no GEMM loads, 2 no MFMA, 4 no epilogue, 8 no tiles, 16 no AdamW, 32 no DGRAD, 64 no WGRAD, 128 DGRAD reads W as if transposed
   MlpBuf bufs[MAXB];
   MlpLayer layers[MAXL];
 };
@@ -296,8 +296,8 @@ __device__ __forceinline__ int slot64(int n) { return (n + 63) & ~63; }  // Flat
 __device__ __forceinline__ int job_tiles(const Ctx& c, const MlpLayer& L, int kind) {
   switch (kind) {
     case J_FWD: return ((c.M + 31) >> 5) * ((L.N + 31) >> 5);
-    case J_DGRAD: return L.need_dx ? ((c.M + 31) >> 5) * ((L.K + 31) >> 5) : 0;
-    case J_WGRAD: return ((L.N + 31) >> 5) * ((L.K + 31) >> 5);
+    case J_DGRAD: return (L.need_dx && !(c.a->probe & 32)) ? ((c.M + 31) >> 5) * ((L.K + 31) >> 5) : 0;
+    case J_WGRAD: return (c.a->probe & 64) ? 0 : ((L.N + 31) >> 5) * ((L.K + 31) >> 5);
     case J_BIAS: return (L.N + 63) >> 6;
     default:  // AdamW over the layer's W and b slots
       return (c.a->probe & 16) ? 0 : (slot64(L.N * L.K) + ADAM_TILE - 1) / ADAM_TILE + (slot64(L.N) + ADAM_TILE - 1) / ADAM_TILE;
@@ -426,7 +426,10 @@ __device__ __forceinline__ void run_tile(const Ctx& c, const MlpLayer& L, int t)
     if (xin) mma_tile<O_GK, O_GK>(gop(xb, a.x_ld[xp], c.M), gop(W, L.K, Q), p0, q0, ni, nj, L.K, acc, a.probe);
     else mma_tile<O_LK, O_GK>(lop(ib.off + L.in_col, ib.ld), gop(W, L.K, Q), p0, q0, ni, nj, L.K, acc, a.probe);
   } else if (kind == J_DGRAD) {  // d[m][k]: A = dp (m, n), B = W^T (k, n)
-    mma_tile<O_LK, O_GMN>(lop(dpo, ob.ld), gop(W, L.K, Q), p0, q0, ni, nj, L.N, acc, a.probe);
+    if (a.probe & 128)  // timing probe: W^T read with the float4 pattern of a transposed copy
+      mma_tile<O_LK, O_GK>(lop(dpo, ob.ld), gop(W, L.N, Q), p0, q0, ni, nj, L.N, acc, a.probe);
+    else
+      mma_tile<O_LK, O_GMN>(lop(dpo, ob.ld), gop(W, L.K, Q), p0, q0, ni, nj, L.N, acc, a.probe);
   } else {                    // g[n][k]: A = dp^T (n, m), B = in^T (k, m)
     if (xin) mma_tile<O_LMN, O_GMN>(lop(dpo, ob.ld), gop(xb, a.x_ld[xp], Q), p0, q0, ni, nj, c.M, acc, a.probe);
     else mma_tile<O_LMN, O_LMN>(lop(dpo, ob.ld), lop(ib.off + L.in_col, ib.ld), p0, q0, ni, nj, c.M, acc, a.probe);
