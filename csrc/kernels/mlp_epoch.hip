@@ -5,7 +5,7 @@
 //
 // Why one workgroup: the nets are ~44 K parameters on 64-row mini-batches. Unfused, a mini-batch
 // is ~40 launches of 1-6 us kernels that each fill a few CUs, i.e. launch / tail bound. Here one
-// workgroup of 8 waves walks every mini-batch of the epoch: forward levels, the CE, backward
+// workgroup of 16 waves walks every mini-batch of the epoch: forward levels, the CE, backward
 // levels, the AdamW update, with a workgroup barrier between phases. Activations / gradients live
 // in a few hundred KB of scratch that stays in the CU's L1 / the XCD's L2; nothing returns to the
 // host until the epoch ends (loss / accuracy accumulate on the device).
@@ -26,7 +26,8 @@
 namespace {
 
 #ifndef MLP_NT
-#define MLP_NT 512  // 8 waves: the phase code needs > 128 VGPRs (2x2 tiles + operand prefetch)
+#define MLP_NT 1024  // 16 waves, 4 per SIMD: more latency hiding than 8 despite ~40 VGPR spills outside the
+                     // MFMA loops (120.7 vs 125 us per mini-batch; 512 threads need no spills)
 #endif
 #ifndef MLP_RING
 #define MLP_RING 1  // chunks of a global operand in flight (scripts/mlp_epoch_variants.sh A/B)
