@@ -114,6 +114,27 @@ __device__ __forceinline__ float u32_to_unit(uint32_t x) {  // (0,1]
 
 // Bijective XCD-aware remap of a 1-D block id (8 XCDs, round-robin dispatch): consecutive
 // logical tiles land on the same XCD (shared L2) — see cdna_hip_programming.md T1.
+// 3-D grid (tiles t fastest, then y, z) -> (t, y, z) such that every XCD gets the same MIX of t.
+// Workgroups are dealt round-robin over the 8 XCDs in grid order, so with a small tile extent
+// (causal attention: 4 query tiles at S = 256, work 1:2:3:4) XCD k would only ever receive tile
+// k mod 4. Bijective when the grid divides into 8 x tiles; the identity otherwise.
+__device__ __forceinline__ void xcd_spread_block(int& t, int& y, int& z) {
+  const int nt = gridDim.x, ny = gridDim.y, nz = gridDim.z;
+  const int lin = blockIdx.x + nt * (blockIdx.y + ny * blockIdx.z);
+  if ((nt * ny * nz) % (8 * nt) == 0) {
+    const int xcd = lin & 7, j = lin >> 3;
+    // an XCD's 32 CUs take its workgroups in turn: rotating by the round (j / 32) also gives each
+    // CU's co-resident workgroups different tiles (groups of nt consecutive j never straddle a
+    // round when nt divides 32, so the map stays bijective)
+    t = (32 % nt == 0) ? (j + (j >> 5)) % nt : j % nt;
+    const int rest = (j / nt) * 8 + xcd;
+    y = rest % ny;
+    z = rest / ny;
+  } else {
+    t = blockIdx.x; y = blockIdx.y; z = blockIdx.z;
+  }
+}
+
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int nx = 8;
   if (nwg < nx * 2) return bid;

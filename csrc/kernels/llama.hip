@@ -458,7 +458,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
   constexpr int NT = L::NT, KP = L::KP, VP = L::VP;
   __shared__ __attribute__((aligned(16))) bf16_t Ks[AT * KP];
   __shared__ __attribute__((aligned(16))) bf16_t Vt[HD * VP];
-  const int b = blockIdx.z, h = blockIdx.y, qt = blockIdx.x;
+  int qt, h, b;
+  xcd_spread_block(qt, h, b);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, lq = lane & 15, lg = lane >> 4;
   const long long rs = 3LL * H * HD, ro = (long long)H * HD;
   const bf16_t* base = qkv + (long long)b * S * rs + h * HD;
@@ -532,7 +533,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(
   __shared__ __attribute__((aligned(16))) bf16_t Ks[AT * KP];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[AT * KP];
   __shared__ __attribute__((aligned(16))) bf16_t Kt[HD * VP];
-  const int b = blockIdx.z, h = blockIdx.y, qt = blockIdx.x;
+  int qt, h, b;
+  xcd_spread_block(qt, h, b);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, lq = lane & 15, lg = lane >> 4;
   const long long rs = 3LL * H * HD, ro = (long long)H * HD;
   const bf16_t* base = qkv + (long long)b * S * rs + h * HD;
@@ -611,7 +613,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(
   __shared__ __attribute__((aligned(16))) bf16_t Qt[HD * VP];
   __shared__ __attribute__((aligned(16))) bf16_t Dt[HD * VP];
   __shared__ float Ls[AT], Dl[AT];
-  const int b = blockIdx.z, h = blockIdx.y, kt = blockIdx.x;
+  int kt, h, b;
+  xcd_spread_block(kt, h, b);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, lq = lane & 15, lg = lane >> 4;
   const long long rs = 3LL * H * HD, ro = (long long)H * HD;
   const bf16_t* base = qkv + (long long)b * S * rs + h * HD;

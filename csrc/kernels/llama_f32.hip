@@ -606,7 +606,8 @@ __global__ __launch_bounds__(256) void attnf_fwd_kernel(const float* __restrict_
                                                         float sl2) {
   constexpr int HP = HD + 4, NDB = HD / 16, KP = ATT_R + 4;
   __shared__ __attribute__((aligned(16))) float Ks[ATT_R * HP], Vt[HD * KP];
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  int qb, h, b;
+  xcd_spread_block(qb, h, b);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, n = lane & 15;
   const int q = qb * ATT_R + 16 * w + n, qc = min(q, S - 1);
   const long long rs = 3LL * H * HD;
@@ -676,7 +677,8 @@ __global__ __launch_bounds__(256) void attnf_bwd_dq_kernel(const float* __restri
                                                            float scale) {
   constexpr int HP = HD + 4, NDB = HD / 16, DQ = HD / 4;
   __shared__ __attribute__((aligned(16))) float Ks[ATT_R * HP], Vs[ATT_R * HP];
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  int qb, h, b;
+  xcd_spread_block(qb, h, b);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, n = lane & 15;
   const int q = qb * ATT_R + 16 * w + n, qc = min(q, S - 1);
   const long long rs = 3LL * H * HD, ors = (long long)H * HD;
@@ -735,7 +737,8 @@ __global__ __launch_bounds__(256) void attnf_bwd_dkdv_kernel(const float* __rest
   constexpr int HP = HD + 4, NDB = HD / 16, DQ = HD / 4;
   __shared__ __attribute__((aligned(16))) float Qs[ATT_R * HP], Ds[ATT_R * HP];
   __shared__ float Ls[ATT_R], Dl[ATT_R];
-  const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  int kb, h, b;
+  xcd_spread_block(kb, h, b);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, n = lane & 15;
   const int key = kb * ATT_R + 16 * w + n, kc = min(key, S - 1);
   const long long rs = 3LL * H * HD, ors = (long long)H * HD;

@@ -87,7 +87,7 @@ def test_swiglu_embedding_f32(cuda):
 
 
 @pytest.mark.parametrize("B,S,H,hd", [(3, 256, 6, 48), (1, 100, 2, 64), (2, 64, 4, 32), (1, 77, 2, 128),
-                                      (2, 130, 3, 16)])
+                                      (2, 130, 3, 16), (4, 256, 2, 48), (8, 130, 2, 16)])
 def test_attention_f32(cuda, B, S, H, hd):
     torch.manual_seed(3)
     qkv = torch.randn(B, S, 3 * H * hd)

@@ -107,7 +107,8 @@ def test_linear_rmsnorm_swiglu_embedding(cuda):
     assert _rel(ec.grad, eh.grad) < 1e-2 and ec.grad[0].abs().max() == 0
 
 
-@pytest.mark.parametrize("B,S,H,hd", [(2, 256, 6, 48), (1, 100, 2, 64), (3, 64, 4, 32), (1, 77, 2, 128)])
+@pytest.mark.parametrize("B,S,H,hd", [(2, 256, 6, 48), (1, 100, 2, 64), (3, 64, 4, 32), (1, 77, 2, 128),
+                                      (4, 256, 2, 48), (8, 130, 2, 32)])
 def test_fused_rope_attention(cuda, B, S, H, hd):
     torch.manual_seed(1)
     qkv = torch.randn(B, S, 3 * H * hd)
