@@ -242,59 +242,77 @@ __global__ __launch_bounds__(256) void rmsf_fwd_kernel(const float* __restrict__
 }
 
 // dx = r*g*dy - x * r^3 * sum(g*dy*x) / D (+ dres);  part[block][d] = sum over the block's rows of
-// dy*x*r (fixed row order per wave, waves combined in a fixed order).
+// dy*x*r (fixed row order per wave, waves combined in a fixed order). KV float4 slots per lane
+// (D <= 256 * KV); a wave loads RG rows' x / dy before using any of them, so RG rows' loads are in
+// flight at once (one row at a time waited a full HBM round trip per row: 18.9 us at T = 8192).
+template <int KV, int RMS_RG = 8 / KV>
 __global__ __launch_bounds__(256) void rmsf_bwd_kernel(const float* __restrict__ x, const float* __restrict__ g,
                                                        const float* __restrict__ rstd,
                                                        const float* __restrict__ dy,
                                                        const float* __restrict__ dres, float* __restrict__ dx,
                                                        float* __restrict__ part, int T, int D, int rows_per_block) {
-  __shared__ float4 sdg[4][64 * RMS_MAXV];
+  __shared__ float4 sdg[4][64 * KV];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int D4 = D / 4;
   const float4* g4 = (const float4*)g;
-  float4 dg[RMS_MAXV], gg[RMS_MAXV];
+  float4 dg[KV], gg[KV];
 #pragma unroll
-  for (int k = 0; k < RMS_MAXV; ++k) {
+  for (int k = 0; k < KV; ++k) {
     const int c = lane + 64 * k;
     dg[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     gg[k] = c < D4 ? g4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   const int r0 = blockIdx.x * rows_per_block, r1 = min(T, r0 + rows_per_block);
-  for (int row = r0 + wv; row < r1; row += 4) {
-    const float4* xr = (const float4*)(x + (long long)row * D);
-    const float4* dr = (const float4*)(dy + (long long)row * D);
-    const float r = rstd[row];
-    float4 xv[RMS_MAXV], dv[RMS_MAXV];
-    float s = 0.f;
+  for (int rb = r0 + wv; rb < r1; rb += 4 * RMS_RG) {
+    float4 xv[RMS_RG][KV], dv[RMS_RG][KV];
+    float r[RMS_RG];
 #pragma unroll
-    for (int k = 0; k < RMS_MAXV; ++k) {
-      const int c = lane + 64 * k;
-      xv[k] = c < D4 ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-      dv[k] = c < D4 ? dr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-      s += gg[k].x * dv[k].x * xv[k].x + gg[k].y * dv[k].y * xv[k].y + gg[k].z * dv[k].z * xv[k].z +
-           gg[k].w * dv[k].w * xv[k].w;
-    }
-    s = wave_sum(s);
-    const float c3 = r * r * r * s / (float)D;
-    float4* out = (float4*)(dx + (long long)row * D);
-    const float4* rs = dres ? (const float4*)(dres + (long long)row * D) : nullptr;
+    for (int i = 0; i < RMS_RG; ++i) {
+      const int row = rb + 4 * i;
+      const bool rin = row < r1;
+      const float4* xr = (const float4*)(x + (long long)row * D);
+      const float4* dr = (const float4*)(dy + (long long)row * D);
+      r[i] = rin ? rstd[row] : 0.f;
 #pragma unroll
-    for (int k = 0; k < RMS_MAXV; ++k) {
-      const int c = lane + 64 * k;
-      if (c >= D4) continue;
-      float4 o = make_float4(r * gg[k].x * dv[k].x - xv[k].x * c3, r * gg[k].y * dv[k].y - xv[k].y * c3,
-                             r * gg[k].z * dv[k].z - xv[k].z * c3, r * gg[k].w * dv[k].w - xv[k].w * c3);
-      if (rs) {
-        const float4 q = rs[c];
-        o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+      for (int k = 0; k < KV; ++k) {
+        const int c = lane + 64 * k;
+        const bool in = rin && c < D4;
+        xv[i][k] = in ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        dv[i][k] = in ? dr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
       }
-      out[c] = o;
-      dg[k].x += dv[k].x * xv[k].x * r; dg[k].y += dv[k].y * xv[k].y * r;
-      dg[k].z += dv[k].z * xv[k].z * r; dg[k].w += dv[k].w * xv[k].w * r;
+    }
+#pragma unroll
+    for (int i = 0; i < RMS_RG; ++i) {
+      const int row = rb + 4 * i;
+      if (row >= r1) break;  // wave-uniform
+      float sm = 0.f;
+#pragma unroll
+      for (int k = 0; k < KV; ++k)
+        sm += gg[k].x * dv[i][k].x * xv[i][k].x + gg[k].y * dv[i][k].y * xv[i][k].y +
+              gg[k].z * dv[i][k].z * xv[i][k].z + gg[k].w * dv[i][k].w * xv[i][k].w;
+      sm = wave_sum(sm);
+      const float rr = r[i];
+      const float c3 = rr * rr * rr * sm / (float)D;
+      float4* out = (float4*)(dx + (long long)row * D);
+      const float4* rs = dres ? (const float4*)(dres + (long long)row * D) : nullptr;
+#pragma unroll
+      for (int k = 0; k < KV; ++k) {
+        const int c = lane + 64 * k;
+        if (c >= D4) continue;
+        float4 o = make_float4(rr * gg[k].x * dv[i][k].x - xv[i][k].x * c3, rr * gg[k].y * dv[i][k].y - xv[i][k].y * c3,
+                               rr * gg[k].z * dv[i][k].z - xv[i][k].z * c3, rr * gg[k].w * dv[i][k].w - xv[i][k].w * c3);
+        if (rs) {
+          const float4 q = rs[c];
+          o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+        }
+        out[c] = o;
+        dg[k].x += dv[i][k].x * xv[i][k].x * rr; dg[k].y += dv[i][k].y * xv[i][k].y * rr;
+        dg[k].z += dv[i][k].z * xv[i][k].z * rr; dg[k].w += dv[i][k].w * xv[i][k].w * rr;
+      }
     }
   }
 #pragma unroll
-  for (int k = 0; k < RMS_MAXV; ++k) sdg[wv][lane + 64 * k] = dg[k];
+  for (int k = 0; k < KV; ++k) sdg[wv][lane + 64 * k] = dg[k];
   __syncthreads();
   float4* p = (float4*)(part + (long long)blockIdx.x * D);
   for (int c = threadIdx.x; c < D4; c += 256) {
@@ -308,23 +326,36 @@ __global__ __launch_bounds__(256) void rmsf_bwd_kernel(const float* __restrict__
   }
 }
 
-__global__ void rmsf_fold_kernel(const float* __restrict__ part, float* __restrict__ dg, int nb, int D,
-                                 int accumulate) {
-  const int d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= D) return;
-  // 16 partials' loads in flight ahead of the adds, which keep block order (bitwise the serial
-  // sum): the serial loop waited one L2 round trip per block (256 blocks: ~60 us per fold)
+// d(gamma) fold: a block per 16 columns, 16 slices per column (slice s sums the partials of blocks
+// s, s + 16, ... in order, every load of a thread in flight at once), then the slices in a fixed
+// tree order: deterministic. One thread per column summing all partials serially ran on 2
+// workgroups at D = 288 (8.4 us).
+constexpr int RMSF_FOLD_COLS = 16, RMSF_FOLD_SLICES = 16;
+__global__ __launch_bounds__(256) void rmsf_fold_kernel(const float* __restrict__ part, float* __restrict__ dg, int nb,
+                                                        int D, int accumulate) {
+  __shared__ float red[RMSF_FOLD_SLICES][RMSF_FOLD_COLS];
+  const int cl = threadIdx.x % RMSF_FOLD_COLS, sl = threadIdx.x / RMSF_FOLD_COLS;
+  const int d = blockIdx.x * RMSF_FOLD_COLS + cl;
   float s = 0.f;
-  int b = 0;
-  for (; b + 16 <= nb; b += 16) {
-    float v[16];
+  if (d < D) {
+    int b = sl;
+    for (; b + 7 * RMSF_FOLD_SLICES < nb; b += 8 * RMSF_FOLD_SLICES) {
+      float v[8];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = part[(long long)(b + j) * D + d];
+      for (int j = 0; j < 8; ++j) v[j] = part[(long long)(b + j * RMSF_FOLD_SLICES) * D + d];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) s += v[j];
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; b < nb; b += RMSF_FOLD_SLICES) s += part[(long long)b * D + d];
   }
-  for (; b < nb; ++b) s += part[(long long)b * D + d];
-  dg[d] = accumulate ? dg[d] + s : s;
+  red[sl][cl] = s;
+  __syncthreads();
+#pragma unroll
+  for (int h = RMSF_FOLD_SLICES / 2; h > 0; h >>= 1) {
+    if (sl < h) red[sl][cl] += red[sl + h][cl];
+    __syncthreads();
+  }
+  if (sl == 0 && d < D) dg[d] = accumulate ? dg[d] + red[0][cl] : red[0][cl];
 }
 
 DDL_API int ddl_rmsf_fwd(const float* x, const float* g, float* y, float* rstd, int T, int D, float eps,
@@ -337,7 +368,8 @@ DDL_API int ddl_rmsf_fwd(const float* x, const float* g, float* y, float* rstd, 
 
 // blocks of the backward grid for T rows (the d(gamma) partial buffer holds nb x D floats)
 DDL_API int ddl_rmsf_blocks(int T) {
-  const int rpb = T <= 1024 ? 4 : ((T + 255) / 256 + 3) / 4 * 4;
+  // ~512 workgroups (two per CU) at large T: each wave then holds its rows' loads in flight at once
+  const int rpb = T <= 2048 ? 4 : ((T + 511) / 512 + 3) / 4 * 4;
   return (T + rpb - 1) / rpb;
 }
 
@@ -347,10 +379,18 @@ DDL_API int ddl_rmsf_bwd(const float* x, const float* g, const float* rstd, cons
   if (T < 1) return 0;
   const int nb = ddl_rmsf_blocks(T);
   const int rpb = (T + nb - 1) / nb;
-  hipLaunchKernelGGL(rmsf_bwd_kernel, dim3(nb), dim3(256), 0, s, x, g, rstd, dy, dres, dx, part, T, D, rpb);
+  const int kv = (D / 4 + 63) / 64;
+  if (kv <= 2)
+    hipLaunchKernelGGL(rmsf_bwd_kernel<2>, dim3(nb), dim3(256), 0, s, x, g, rstd, dy, dres, dx, part, T, D, rpb);
+  else if (kv <= 4)
+    hipLaunchKernelGGL(rmsf_bwd_kernel<4>, dim3(nb), dim3(256), 0, s, x, g, rstd, dy, dres, dx, part, T, D, rpb);
+  else
+    hipLaunchKernelGGL(rmsf_bwd_kernel<RMS_MAXV>, dim3(nb), dim3(256), 0, s, x, g, rstd, dy, dres, dx, part, T, D,
+                       rpb);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !dg) return (int)e;
-  hipLaunchKernelGGL(rmsf_fold_kernel, dim3((D + 255) / 256), dim3(256), 0, s, part, dg, nb, D, accumulate);
+  hipLaunchKernelGGL(rmsf_fold_kernel, dim3((D + RMSF_FOLD_COLS - 1) / RMSF_FOLD_COLS), dim3(256), 0, s, part, dg, nb,
+                     D, accumulate);
   return (int)hipGetLastError();
 }
 
