@@ -10,9 +10,11 @@ Here:
   * ``GradBucketer`` gives every parameter a ``.grad`` that is a VIEW into flat bucket buffers laid
     out in gradient-ready (reverse) order; a post-accumulate hook launches the bucket's RCCL
     all-reduce as soon as its last gradient lands, so communication overlaps the rest of backward
-    (no barrier, no host staging, no cat/split copies). Bucket boundaries come from the native
-    bucket planner; the default 64 MB cap suits xGMI rings (per-link bound ~150 GB/s: a bucket takes
-    ~0.5 ms, long enough to amortise RCCL launch latency, short enough to overlap);
+    (no barrier, no host staging, no cat/split copies); a bucket below the measured peer-read
+    crossover runs the one-kernel IPC all-reduce instead (``allreduce_bucket``). Bucket boundaries
+    come from the native bucket planner; the default 64 MB cap suits xGMI rings (per-link bound
+    ~150 GB/s: a bucket takes ~0.5 ms, long enough to amortise RCCL launch latency, short enough
+    to overlap);
   * ``NativeGradBucketer`` does the same for the flat-store native nets (ResNet): buckets are
     contiguous slices of ``store.grad`` fired from the per-layer backward hook;
   * ``average_weights`` is DP-WA done right (in-place write-back).
@@ -35,6 +37,34 @@ def broadcast_parameters(module, ctx, src: int = 0, group=None):
     with torch.no_grad():
         for t in list(module.parameters()) + list(module.buffers()):
             dist.broadcast(t.data, src, group=group)
+
+
+class _Enqueued:
+    """Handle of a peer-read bucket all-reduce: its kernel is on the stream that produced the
+    bucket's last gradient, so everything after it on that stream (the averaging, the optimizer)
+    is already ordered behind it; there is nothing to wait for on the host."""
+
+    @staticmethod
+    def wait():
+        return None
+
+
+def _spans_world(ctx, group) -> bool:
+    return group is None or dist.get_world_size(group) == ctx.world
+
+
+def allreduce_bucket(ctx, t: torch.Tensor, group=None):
+    """Start a bucket's SUM all-reduce and return a handle with ``wait()``. Below the crossover
+    that ``runtime.dist.probe_ipc_threshold`` measured at init (the context's ``ipc_max_bytes``), a
+    bucket over the whole world takes the one-kernel peer-read all-reduce over xGMI
+    (``runtime/ipc.py``); anything larger, or over a sub-group, is an async RCCL all-reduce."""
+    from ..runtime.dist import allreduce_path
+    if (getattr(ctx, "ipc", None) is not None and t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
+            and t.data_ptr() % 16 == 0 and allreduce_path(ctx, t.numel() * 4) == "ipc"
+            and _spans_world(ctx, group)):
+        ctx.ipc.all_reduce(t)
+        return _Enqueued
+    return dist.all_reduce(t, group=group, async_op=True)
 
 
 def bucket_plan(sizes: list[int], cap_bytes: int, elem_bytes: int = 4) -> list[int]:
@@ -96,7 +126,7 @@ class GradBucketer:
         b = self.buckets[self.owner[p]]
         b["pending"] -= 1
         if b["pending"] == 0 and b["handle"] is None:
-            b["handle"] = dist.all_reduce(b["flat"], group=self.group, async_op=True)
+            b["handle"] = allreduce_bucket(self.ctx, b["flat"], self.group)
 
     @contextlib.contextmanager
     def no_sync(self):
@@ -112,7 +142,7 @@ class GradBucketer:
         for b in self.buckets:
             if self.ctx.is_distributed:
                 if b["handle"] is None:
-                    b["handle"] = dist.all_reduce(b["flat"], group=self.group, async_op=True)
+                    b["handle"] = allreduce_bucket(self.ctx, b["flat"], self.group)
                 b["handle"].wait()
                 b["flat"].div_(self.world)
             b["handle"] = None
@@ -180,7 +210,7 @@ class NativeGradBucketer:
             if bi not in self._fired and sp[0] <= lo:
                 self._fired.add(bi)
                 view = self.net.store.grad[:, lo:hi]
-                self.handles.append((dist.all_reduce(view, group=self.group, async_op=True), view))
+                self.handles.append((allreduce_bucket(self.ctx, view, self.group), view))
 
     def finish(self):
         if self.ctx.is_distributed:
@@ -188,7 +218,7 @@ class NativeGradBucketer:
             for bi, (lo, hi) in enumerate(self.bounds):
                 if bi not in self._fired:
                     view = st.grad[:, lo:hi]
-                    self.handles.append((dist.all_reduce(view, group=self.group, async_op=True), view))
+                    self.handles.append((allreduce_bucket(self.ctx, view, self.group), view))
             for h, view in self.handles:
                 h.wait()
             st.grad.div_(self.world)
@@ -204,7 +234,7 @@ def average_weights(module, ctx, group=None):
     world = dist.get_world_size(group)
     params = [p for p in module.parameters()]
     flat = torch.cat([p.data.reshape(-1) for p in params])
-    dist.all_reduce(flat, group=group)
+    allreduce_bucket(ctx, flat, group).wait()
     flat.div_(world)
     off = 0
     for p in params:

@@ -175,3 +175,69 @@ def test_ipc_ordered_fedavg_mean_bitwise_single_process(cuda):
         badg = (r["gather"] != ref).nonzero().flatten()
         assert bad.numel() == 0 and badg.numel() == 0, (bad.numel(), bad[:8].tolist(), badg.numel(),
                                                         (r["out"] - ref).abs().max().item())
+
+
+def _bucket_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from ddl25spring_amd.parallel.dp import GradBucketer, average_weights
+    from ddl25spring_amd.runtime import dist as rdist
+    from ddl25spring_amd.runtime.ipc import IpcAllReduce
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    ctx = rdist.DistContext(rank, world, rank, dev, "gloo")
+    ctx.ipc = IpcAllReduce(rank, world, dev, capacity=1 << 20, nblocks=8, timeout_s=20.0)
+    ctx.ipc_max_bytes = 1 << 20
+    calls = []
+    inner = ctx.ipc.all_reduce
+    ctx.ipc.all_reduce = lambda t: (calls.append(t.numel()), inner(t))[1]
+    torch.manual_seed(5)
+    m = torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.ReLU(), torch.nn.Linear(128, 10)).to(dev)
+    g = torch.Generator().manual_seed(100 + rank)
+    x, y = torch.randn(32, 64, generator=g).to(dev), torch.randint(0, 10, (32,), generator=g).to(dev)
+    torch.nn.functional.cross_entropy(m(x), y).backward()
+    local = [p.grad.detach().cpu().clone() for p in m.parameters()]
+    for p in m.parameters():
+        p.grad = None
+    gb = GradBucketer(m, ctx, bucket_mb=0.02)  # several buckets, each below the 1 MiB crossover
+    gb.zero_grad()
+    torch.nn.functional.cross_entropy(m(x), y).backward()
+    gb.finish()
+    synced = [p.grad.detach().cpu().clone() for p in m.parameters()]
+    nb = len(gb.buckets)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(float(rank))
+    average_weights(m, ctx)
+    w = [p.detach().cpu().clone() for p in m.parameters()]
+    torch.cuda.synchronize()
+    ctx.ipc.check()
+    torch.save({"local": local, "synced": synced, "calls": calls, "buckets": nb, "w": w},
+               os.path.join(out_path, f"b{rank}.pt"))
+    dist.barrier()
+    ctx.ipc.close()
+    dist.destroy_process_group()
+
+
+def test_grad_bucketer_takes_peer_read_allreduce_below_crossover(cuda):
+    """DP gradient buckets (parallel/dp.GradBucketer) and DP-WA below the measured crossover run
+    the peer-read all-reduce (runtime/ipc.py) instead of RCCL: 2 ranks sharing the GPU, every
+    bucket and the weight average on the peer path, gradients = the mean of the ranks' local
+    gradients, bitwise equal on both ranks."""
+    from ddl25spring_amd.runtime.launch import free_port
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_bucket_worker, args=(world, free_port(), d), nprocs=world, join=True,
+                           start_method="spawn")
+        res = [torch.load(os.path.join(d, f"b{r}.pt"), weights_only=True) for r in range(world)]
+    nb = res[0]["buckets"]
+    assert nb >= 2
+    for r in res:
+        assert len(r["calls"]) == nb + 1, r["calls"]  # every bucket + the DP-WA flat vector
+    for i in range(len(res[0]["synced"])):
+        want = (res[0]["local"][i] + res[1]["local"][i]) / 2
+        assert torch.equal(res[0]["synced"][i], res[1]["synced"][i])
+        assert torch.allclose(res[0]["synced"][i], want, rtol=1e-5, atol=1e-6)
+        assert torch.equal(res[0]["w"][i], res[1]["w"][i])
