@@ -206,10 +206,12 @@ def _x6h_native_ok(mode: int, g) -> bool:
 # such a launch as rows of 128 pixels (N = 1, W = 128) whenever N*H*W % 128 == 0 and the image width
 # is not already a power of two (ResNet-50's 56 / 28 / 14 / 7), so the halo kernels
 # (conv_x6h.hip FWD / DGRAD, conv_x6hw.hip WGRAD) take it; memory layout, strides, BN statistics
-# and residual / mask layouts are unchanged. OFF by default: ResNet-50 fp32 ran 2.86k vs 3.58k
-# images/s with every mode flattened (the image geometry keeps its tuned conv_f32 plans);
-# DDL_F32_FLAT1X1=1 (all modes) or a subset of "fdw" enables it.
-_FLAT_ENV = os.environ.get("DDL_F32_FLAT1X1", "0")
+# and residual / mask layouts are unchanged. Round 4: ResNet-50 fp32 ran 2.86k vs 3.58k images/s
+# with every mode flattened (the image geometry keeps its tuned conv_f32 plans). Round 6, per mode
+# (scripts/gpu/r6_flat.sh, images/s): none 3744 / w 3158 / d 3764 / f 3798 / fd 3822 / dw 3240, so
+# FWD and DGRAD are flattened by default and WGRAD keeps the image geometry. DDL_F32_FLAT1X1=0 turns
+# it off, 1 flattens all modes, or a subset of "fdw".
+_FLAT_ENV = os.environ.get("DDL_F32_FLAT1X1", "fd")
 FLAT1X1 = [_FLAT_ENV != "0", "fdw" if _FLAT_ENV == "1" else _FLAT_ENV]  # on, modes ("f", "d", "w")
 
 
