@@ -46,7 +46,7 @@ def main():
     ap.add_argument("--G", type=int, nargs="*", default=[1])
     ap.add_argument("--N", type=int, default=100)
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--model", default="resnet18", choices=("resnet18", "resnet50"))
+    ap.add_argument("--model", default="resnet18", choices=("resnet18", "resnet50", "resnet50_flat1x1"))
     ap.add_argument("--out", default="", help="write the best plans as 'x6h:' table entries (scripts/merge_plans.py)")
     a = ap.parse_args()
     plans, report = {}, []
@@ -56,12 +56,16 @@ def main():
         if a.model == "resnet50":  # the bottleneck 3x3 stride-1 convs (rows padded to a power of two)
             from conv_f32_tune import resnet50_geoms
             layers = [(f"r50_{g.H}x{g.C}", g) for g in resnet50_geoms(G, a.N) if g.R == 3 and g.stride == 1]
+        elif a.model == "resnet50_flat1x1":  # stride-1 1x1 convs as rows of 128 pixels (FLAT1X1 FWD / DGRAD)
+            from conv_f32_tune import resnet50_geoms
+            flat = [F32._launch_geom(g, "f") for g in resnet50_geoms(G, a.N) if g.R == 1 and g.stride == 1]
+            layers = [(f"r50_1x1_{g.C}to{g.K}_{g.H}rows", g) for g in dict.fromkeys(flat) if g.W == 128]
         else:
             layers = [(name, ConvGeom(G, a.N, H, H, C, C, 3, 3, 1, 1)) for name, (H, C) in LAYERS.items()]
         for name, g in layers:
             C = g.C
             x = torch.randn(g.G, g.N, g.H, g.W, g.C, device=dev)
-            w = torch.randn(g.G, g.K, 3, 3, g.C, device=dev) * 0.05
+            w = torch.randn(g.G, g.K, g.R, g.S, g.C, device=dev) * 0.05
             dy = torch.randn(g.G, g.N, g.P, g.Q, g.K, device=dev)
             for mode, mname in ((F32.F_FWD, "fwd"), (F32.F_DGRAD, "dgrad")):
                 run = (lambda: F32.conv_fwd(x, w, g, stats=F32.SlotStats())) if mode == F32.F_FWD else \
@@ -80,6 +84,8 @@ def main():
                         except Exception as e:  # noqa: BLE001
                             print("skip", name, mname, bp, split, e, flush=True)
                 F32.clear_plan(mode, g)
+                if not res:
+                    continue
                 res.sort()
                 best = res[0]
                 key = f"x6h:{mname}:{g.G},{g.N},{g.H},{g.W},{g.C},{g.K},{g.R},{g.S},{g.stride},{g.pad}"
@@ -88,7 +94,7 @@ def main():
                                    best=plans[key], best_us=round(best[0] * 1e3, 1)))
                 print(f"G={G} {name} {mname}: default {dflt} {t0 * 1e3:6.1f} us | best bp={best[1]} split={best[2]} "
                       f"{best[0] * 1e3:6.1f} us | " + " ".join(f"{b}/{s}:{t * 1e3:.1f}" for t, b, s in res), flush=True)
-            if F32.uses_halo_wgrad(g):  # halo WGRAD: slice count sweep
+            if a.model != "resnet50_flat1x1" and F32.uses_halo_wgrad(g):  # halo WGRAD: slice count sweep
                 dw = torch.zeros_like(w)
                 base = (g.K // 64) * (g.C // 32) * G
                 t0 = timed(lambda: F32.conv_wgrad(dy, x, g, dw), a.reps)
