@@ -196,7 +196,11 @@ class _GBatchNormAct(torch.autograd.Function):
             stats = Fn.bn_stats(xg)
         if stats is None:
             stats = torch.zeros(G, 2, C, dtype=torch.float32, device=x.device)
-        ga, be = gamma.detach()[:G].contiguous(), beta.detach()[:G].contiguous()
+        ga, be = gamma.detach()[:G], beta.detach()[:G]
+        if not (Fn.F32.is_f32(xg) and ga.stride(-1) == 1 and be.stride(-1) == 1 and ga.stride(0) == be.stride(0)):
+            # the fp32 BN kernels take the slot rows in place (one group stride for gamma and beta:
+            # rows of SlotAdam's flat buffer); otherwise compact copies
+            ga, be = ga.contiguous(), be.contiguous()
         rm, rv = running_mean[:G], running_var[:G]
         scale, shift, mean, rstd = Fn.bn_finalize(stats, ga, be, rm, rv, M, eps, momentum, training)
         y = Fn.bn_apply(xg, scale, shift, act=_BN_ACT[act])
@@ -214,6 +218,15 @@ class _GBatchNormAct(torch.autograd.Function):
             ymask = y
         elif ctx.act == "leaky_relu":
             d = Fn.act_bwd(y, d, 2, 0.2)
+        sg, sb = (_sink(p, G) for p in ctx.params)
+        if sg is not None and sb is not None and sg.stride(0) == sb.stride(0) == ga.stride(0) \
+                and sg.stride(-1) == 1 and sb.stride(-1) == 1:
+            # the kernel accumulates d(gamma), d(beta) into the gradient's slot rows: bitwise the
+            # zero-filled temporaries plus add_ it replaces (0 + s is exact), four launches fewer
+            dx = Fn.bn_backward(d, ymask, xg, mean, rstd, ga, sg, sb)
+            return dx.view(ctx.shape), None, None, None, None, None, None, None, None, None
+        if ga.stride(0) != C:
+            ga = ga.contiguous()
         dgamma = torch.zeros(G, C, dtype=torch.float32, device=dy.device)
         dbeta = torch.zeros(G, C, dtype=torch.float32, device=dy.device)
         dx = Fn.bn_backward(d, ymask, xg, mean, rstd, ga, dgamma, dbeta)
