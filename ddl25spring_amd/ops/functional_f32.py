@@ -803,7 +803,7 @@ def _bwd_args(x, mean, rstd, gamma, dgamma, dbeta, part, dx, fold_slots: int = 0
     G, C = x.shape[0], x.shape[-1]
     t = _lib.BNFBwdArgs()
     if coef is None:
-        coef = ws.scratch((G, 3, C), x.device)
+        coef = ws.scratch_uninit((G, 3, C), x.device)  # the fold writes every coefficient
     gs = _gs(gamma) if gamma is not None else 0
     if dgamma is not None or dbeta is not None:
         gd = _gs(dgamma) if dgamma is not None else _gs(dbeta)

@@ -62,3 +62,12 @@ def zeros(shape, device) -> torch.Tensor:
 def scratch(shape, device) -> torch.Tensor:
     """Uninitialised-OK fp32 scratch (same arena; contents are zero but callers must not rely)."""
     return zeros(shape, device)
+
+
+def scratch_uninit(shape, device) -> torch.Tensor:
+    """Scratch that its kernel fully writes before reading: the step arena's slice when one is
+    active (graph capture never allocates), else ``torch.empty`` (no memset launch)."""
+    ws = _CURRENT
+    if ws is not None and ws.active:
+        return ws.take(tuple(shape), device)
+    return torch.empty(tuple(shape), dtype=torch.float32, device=device)
