@@ -440,7 +440,11 @@ __global__ __launch_bounds__(256) void bce_logits_f32_kernel(const float* __rest
     const float l = logits[(long long)r * ld];
     const float t = targets ? targets[r] : tval;
     acc += fmaxf(l, 0.f) - l * t + log1pf(expf(-fabsf(l)));
-    if (dlogits) dlogits[(long long)r * ld] = (1.f / (1.f + expf(-l)) - t) * gs;
+    if (dlogits) {
+      float* d = dlogits + (long long)r * ld;
+      d[0] = (1.f / (1.f + expf(-l)) - t) * gs;
+      for (int j = 1; j < ld; ++j) d[j] = 0.f;  // the padded columns: the caller needs no memset
+    }
   }
   red[threadIdx.x] = acc;
   __syncthreads();

@@ -1265,7 +1265,7 @@ def bce_logits(logits, target, scale=1.0, want_grad=True):
     if logits.dtype == torch.float32:  # deterministic fp32 kernel (one workgroup, fixed-order sum)
         assert logits.is_contiguous()
         loss = torch.empty(1, dtype=torch.float32, device=logits.device)
-        dl = torch.zeros_like(logits) if want_grad else None
+        dl = torch.empty_like(logits) if want_grad else None  # every element written by the kernel
         tt = target.float().contiguous() if torch.is_tensor(target) else None
         check(_lib.kernels().ddl_bce_logits_f32(ptr(logits), ld, ptr(tt), 0.0 if tt is not None else float(target), R,
                                                 float(scale), ptr(loss), ptr(dl), stream()), "bce_logits_f32")
